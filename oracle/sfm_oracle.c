@@ -1,0 +1,604 @@
+/*
+ * sfm_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C restatement of the reference's hot path
+ * (pvrohin/Structure-from-Motion-, "Phase 1/"), used as the parity checker by
+ * tests/, by __graft_entry__.smoke() and as bench.py's cpu_baseline leg.
+ * Nothing in the product (structure-from-motion-_amd/) links or calls this.
+ *
+ * Pinned against golden vectors produced by importing the reference itself
+ * (tests/golden/make_golden.py -> tests/golden/ fixtures; tests/test_oracle.py).
+ *
+ * Arithmetic is IEEE fp64 throughout; build with -ffp-contract=off and never
+ * with -ffast-math so every +,*,/,sqrt rounds like numpy's.
+ *
+ * Reference correspondence:
+ *   orc_f8            EstimateFundamentalMatrix.py:21-83   (SVD restated as
+ *                     one-sided Jacobi; F/F[2,2] removes the sign ambiguity)
+ *   orc_ransac_score  GetInliersRANSAC.py:64-81            (symmetric epipolar
+ *                     distance, strict '<' threshold)
+ *   orc_ransac        GetInliersRANSAC.py:53-106           (strict '>' best
+ *                     update: earliest iteration wins ties)
+ *   orc_triangulate   LinearTriangulation.py:44-92         (4x4 DLT, Vt[-1])
+ *   orc_ba_residuals  BundleAdjustment.py:43-110           (r = obs - proj,
+ *                     proj = K(RX+t)[:2] / (K(RX+t)[2] + 1e-8))
+ *   orc_ba_lm         converged least-squares on the same residual
+ *                     (SURVEY.md §8(c) "converged oracle"), as a Schur-
+ *                     complement Levenberg-Marquardt: the CPU-strong baseline.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ */
+/* one-sided (Hestenes) Jacobi SVD: A is m x n row-major, n <= 16.     */
+/* On return A's columns are U*S, V (n x n, row-major) the right        */
+/* singular vectors as columns, s the column norms.                    */
+/* ------------------------------------------------------------------ */
+static void jacobi_svd(double *A, int m, int n, double *V, double *s) {
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) V[i * n + j] = (i == j) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        double off = 0.0;
+        for (int p = 0; p < n - 1; ++p) {
+            for (int q = p + 1; q < n; ++q) {
+                double a = 0, b = 0, c = 0;
+                for (int k = 0; k < m; ++k) {
+                    double x = A[k * n + p], y = A[k * n + q];
+                    a += x * x; b += y * y; c += x * y;
+                }
+                if (c == 0.0) continue;
+                double r = fabs(c) / sqrt(a * b);
+                if (!(r > 1e-15)) continue;
+                if (r > off) off = r;
+                double zeta = (b - a) / (2.0 * c);
+                double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                double cs = 1.0 / sqrt(1.0 + t * t), sn = cs * t;
+                for (int k = 0; k < m; ++k) {
+                    double x = A[k * n + p], y = A[k * n + q];
+                    A[k * n + p] = cs * x - sn * y;
+                    A[k * n + q] = sn * x + cs * y;
+                }
+                for (int k = 0; k < n; ++k) {
+                    double x = V[k * n + p], y = V[k * n + q];
+                    V[k * n + p] = cs * x - sn * y;
+                    V[k * n + q] = sn * x + cs * y;
+                }
+            }
+        }
+        if (off < 1e-15) break;
+    }
+    for (int j = 0; j < n; ++j) {
+        double a = 0;
+        for (int k = 0; k < m; ++k) a += A[k * n + j] * A[k * n + j];
+        s[j] = sqrt(a);
+    }
+}
+
+/* index of the smallest singular value */
+static int argmin(const double *s, int n) {
+    int b = 0;
+    for (int j = 1; j < n; ++j) if (s[j] < s[b]) b = j;
+    return b;
+}
+
+/* EstimateFundamentalMatrix.py:21-83 for n >= 8 correspondences.     */
+/* Returns 0 on success, -1 if n < 8.                                  */
+int orc_f8(const double *p1, const double *p2, int64_t n, double *F_out) {
+    if (n < 8) return -1;
+    double m1x = 0, m1y = 0, m2x = 0, m2y = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        m1x += p1[2 * i]; m1y += p1[2 * i + 1];
+        m2x += p2[2 * i]; m2y += p2[2 * i + 1];
+    }
+    m1x /= (double)n; m1y /= (double)n; m2x /= (double)n; m2y /= (double)n;
+    double d1 = 0, d2 = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        double ax = p1[2 * i] - m1x, ay = p1[2 * i + 1] - m1y;
+        double bx = p2[2 * i] - m2x, by = p2[2 * i + 1] - m2y;
+        d1 += sqrt(ax * ax + ay * ay);
+        d2 += sqrt(bx * bx + by * by);
+    }
+    double s1 = sqrt(2.0) / (d1 / (double)n + 1e-8);
+    double s2 = sqrt(2.0) / (d2 / (double)n + 1e-8);
+    double o1x = -s1 * m1x, o1y = -s1 * m1y, o2x = -s2 * m2x, o2y = -s2 * m2y;
+    /* A: n x 9 (EstimateFundamentalMatrix.py:58-62) */
+    double *A = (double *)malloc(sizeof(double) * (size_t)n * 9);
+    for (int64_t i = 0; i < n; ++i) {
+        double x1 = s1 * p1[2 * i] + o1x, y1 = s1 * p1[2 * i + 1] + o1y;
+        double x2 = s2 * p2[2 * i] + o2x, y2 = s2 * p2[2 * i + 1] + o2y;
+        double *r = A + i * 9;
+        r[0] = x1 * x2; r[1] = x1 * y2; r[2] = x1;
+        r[3] = y1 * x2; r[4] = y1 * y2; r[5] = y1;
+        r[6] = x2; r[7] = y2; r[8] = 1.0;
+    }
+    double V[81], s[9];
+    if (n > 9) {
+        /* reduce to the 9x9 Gram-free triangular factor by Householder QR so
+         * the Jacobi sweeps work on 9 rows; singular vectors are unchanged. */
+        for (int k = 0; k < 9; ++k) {
+            double nrm = 0;
+            for (int64_t i = k; i < n; ++i) nrm += A[i * 9 + k] * A[i * 9 + k];
+            nrm = sqrt(nrm);
+            if (nrm == 0) continue;
+            double alpha = A[k * 9 + k] > 0 ? -nrm : nrm;
+            double v0 = A[k * 9 + k] - alpha;
+            /* v = [v0, A[k+1..n-1][k]] ; H = I - 2 vv^T / v^T v */
+            double vtv = v0 * v0;
+            for (int64_t i = k + 1; i < n; ++i) vtv += A[i * 9 + k] * A[i * 9 + k];
+            for (int j = k + 1; j < 9; ++j) {
+                double d = v0 * A[k * 9 + j];
+                for (int64_t i = k + 1; i < n; ++i) d += A[i * 9 + k] * A[i * 9 + j];
+                double f = 2.0 * d / vtv;
+                A[k * 9 + j] -= f * v0;
+                for (int64_t i = k + 1; i < n; ++i) A[i * 9 + j] -= f * A[i * 9 + k];
+            }
+            A[k * 9 + k] = alpha;
+            for (int64_t i = k + 1; i < n; ++i) A[i * 9 + k] = 0.0;
+        }
+        jacobi_svd(A, 9, 9, V, s);
+    } else {
+        jacobi_svd(A, (int)n, 9, V, s);
+    }
+    free(A);
+    int j = argmin(s, 9);
+    double f[9];
+    for (int k = 0; k < 9; ++k) f[k] = V[k * 9 + j];
+    /* rank-2 (EstimateFundamentalMatrix.py:70-72): F = sum over the two
+     * largest singular triplets = B V^T with the weakest column of B zeroed */
+    double B[9], W[9], sw[3];
+    memcpy(B, f, sizeof B);
+    jacobi_svd(B, 3, 3, W, sw);
+    int z = argmin(sw, 3);
+    double F2[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+            double acc = 0;
+            for (int k = 0; k < 3; ++k)
+                if (k != z) acc += B[r * 3 + k] * W[c * 3 + k];
+            F2[r * 3 + c] = acc;
+        }
+    /* F = T2^T F T1 (EstimateFundamentalMatrix.py:75, reproduced as shipped) */
+    double T1[9] = {s1, 0, o1x, 0, s1, o1y, 0, 0, 1};
+    double T2[9] = {s2, 0, o2x, 0, s2, o2y, 0, 0, 1};
+    double tmp[9], G[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+            double acc = 0;
+            for (int k = 0; k < 3; ++k) acc += T2[k * 3 + r] * F2[k * 3 + c];
+            tmp[r * 3 + c] = acc;
+        }
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+            double acc = 0;
+            for (int k = 0; k < 3; ++k) acc += tmp[r * 3 + k] * T1[k * 3 + c];
+            G[r * 3 + c] = acc;
+        }
+    double d = G[8];
+    for (int k = 0; k < 9; ++k) F_out[k] = G[k] / d;  /* :78 */
+    return 0;
+}
+
+/* GetInliersRANSAC.py:64-81: inlier test for one F over N points. */
+static inline int epi_inlier(const double *F, double x1, double y1, double x2, double y2, double thr) {
+    double a0 = F[0] * x1 + F[1] * y1 + F[2];
+    double a1 = F[3] * x1 + F[4] * y1 + F[5];
+    double a2 = F[6] * x1 + F[7] * y1 + F[8];
+    double b0 = F[0] * x2 + F[3] * y2 + F[6];
+    double b1 = F[1] * x2 + F[4] * y2 + F[7];
+    double e = x2 * a0 + y2 * a1 + a2;
+    double ae = fabs(e);
+    double d1 = ae / (sqrt(a0 * a0 + a1 * a1) + 1e-8);
+    double d2 = ae / (sqrt(b0 * b0 + b1 * b1) + 1e-8);
+    double err = (d1 + d2) / 2.0;
+    return err < thr;
+}
+
+/* counts[h] for every hypothesis; mask (nullable) for hypothesis h_mask */
+void orc_ransac_score(const double *x1, const double *x2, int64_t n, const double *F, int64_t H,
+                      double thr, int32_t *counts) {
+    for (int64_t h = 0; h < H; ++h) {
+        const double *f = F + 9 * h;
+        int32_t c = 0;
+        int finite = 1;
+        for (int k = 0; k < 9; ++k) finite &= isfinite(f[k]) ? 1 : 0;
+        if (finite)
+            for (int64_t i = 0; i < n; ++i)
+                c += epi_inlier(f, x1[2 * i], x1[2 * i + 1], x2[2 * i], x2[2 * i + 1], thr);
+        counts[h] = c;
+    }
+}
+
+void orc_ransac_mask(const double *x1, const double *x2, int64_t n, const double *F, double thr,
+                     uint8_t *mask) {
+    for (int64_t i = 0; i < n; ++i)
+        mask[i] = (uint8_t)epi_inlier(F, x1[2 * i], x1[2 * i + 1], x2[2 * i], x2[2 * i + 1], thr);
+}
+
+/* Full RANSAC loop (GetInliersRANSAC.py:53-106) over a host-drawn H x 8
+ * sample table.  Returns best iteration (-1 if no hypothesis had inliers). */
+int64_t orc_ransac(const double *x1, const double *x2, int64_t n, const int32_t *samples, int64_t H,
+                   int k, double thr, int32_t *counts, double *F_best, uint8_t *mask) {
+    int64_t best = -1;
+    int32_t best_c = 0;
+    double p1[2 * 64], p2[2 * 64], F[9];
+    for (int64_t h = 0; h < H; ++h) {
+        for (int j = 0; j < k; ++j) {
+            int32_t s = samples[h * k + j];
+            p1[2 * j] = x1[2 * s]; p1[2 * j + 1] = x1[2 * s + 1];
+            p2[2 * j] = x2[2 * s]; p2[2 * j + 1] = x2[2 * s + 1];
+        }
+        int32_t c = 0;
+        if (orc_f8(p1, p2, k, F) == 0) orc_ransac_score(x1, x2, n, F, 1, thr, &c);
+        if (counts) counts[h] = c;
+        if (c > best_c) {
+            best_c = c; best = h;
+            memcpy(F_best, F, sizeof F);
+        }
+    }
+    if (best >= 0 && mask) orc_ransac_mask(x1, x2, n, F_best, thr, mask);
+    return best;
+}
+
+/* LinearTriangulation.py:44-92.  P1, P2: 3x4 row-major. */
+void orc_triangulate(const double *P1, const double *P2, const double *x1, const double *x2,
+                     int64_t n, double *X) {
+    for (int64_t i = 0; i < n; ++i) {
+        double A[16], V[16], s[4];
+        double u1 = x1[2 * i], v1 = x1[2 * i + 1], u2 = x2[2 * i], v2 = x2[2 * i + 1];
+        for (int c = 0; c < 4; ++c) {
+            A[0 * 4 + c] = v1 * P1[8 + c] - P1[4 + c];
+            A[1 * 4 + c] = P1[0 + c] - u1 * P1[8 + c];
+            A[2 * 4 + c] = v2 * P2[8 + c] - P2[4 + c];
+            A[3 * 4 + c] = P2[0 + c] - u2 * P2[8 + c];
+        }
+        jacobi_svd(A, 4, 4, V, s);
+        int j = argmin(s, 4);
+        double h0 = V[0 * 4 + j], h1 = V[1 * 4 + j], h2 = V[2 * 4 + j], h3 = V[3 * 4 + j];
+        if (fabs(h3) > 1e-8) {
+            X[3 * i] = h0 / h3; X[3 * i + 1] = h1 / h3; X[3 * i + 2] = h2 / h3;
+        } else {
+            X[3 * i] = h0; X[3 * i + 1] = h1; X[3 * i + 2] = h2;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* Bundle adjustment                                                   */
+/* ------------------------------------------------------------------ */
+
+/* Rotation.from_rotvec(...).as_matrix() */
+void orc_rotvec_to_R(const double *w, double *R) {
+    double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    double th = sqrt(th2), a, b;
+    if (th < 1e-6) {
+        a = 1.0 - th2 / 6.0 + th2 * th2 / 120.0;
+        b = 0.5 - th2 / 24.0 + th2 * th2 / 720.0;
+    } else {
+        a = sin(th) / th;
+        b = (1.0 - cos(th)) / th2;
+    }
+    double x = w[0], y = w[1], z = w[2];
+    R[0] = 1.0 - b * (y * y + z * z); R[1] = -a * z + b * x * y;       R[2] = a * y + b * x * z;
+    R[3] = a * z + b * x * y;         R[4] = 1.0 - b * (x * x + z * z); R[5] = -a * x + b * y * z;
+    R[6] = -a * y + b * x * z;        R[7] = a * x + b * y * z;         R[8] = 1.0 - b * (x * x + y * y);
+}
+
+/* Rotation.from_matrix(R).as_rotvec() (via the quaternion, w >= 0) */
+void orc_R_to_rotvec(const double *R, double *w) {
+    double tr = R[0] + R[4] + R[8], q[4]; /* x y z w */
+    if (tr > R[0] && tr > R[4] && tr > R[8]) {
+        q[3] = 1.0 + tr;
+        q[0] = R[7] - R[5]; q[1] = R[2] - R[6]; q[2] = R[3] - R[1];
+    } else {
+        int i = (R[0] >= R[4] && R[0] >= R[8]) ? 0 : (R[4] >= R[8] ? 1 : 2);
+        int j = (i + 1) % 3, k = (j + 1) % 3;
+        q[i] = 1.0 - tr + 2.0 * R[i * 4];
+        q[j] = R[j * 3 + i] + R[i * 3 + j];
+        q[k] = R[k * 3 + i] + R[i * 3 + k];
+        q[3] = R[k * 3 + j] - R[j * 3 + k];
+    }
+    double nq = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    for (int i = 0; i < 4; ++i) q[i] /= nq;
+    if (q[3] < 0) for (int i = 0; i < 4; ++i) q[i] = -q[i];
+    double vn = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2]);
+    double ang = 2.0 * atan2(vn, q[3]);
+    double sc;
+    if (ang <= 1e-3) {
+        double a2 = ang * ang;
+        sc = 2.0 + a2 / 12.0 + 7.0 * a2 * a2 / 2880.0;
+    } else {
+        sc = ang / sin(ang / 2.0);
+    }
+    w[0] = sc * q[0]; w[1] = sc * q[1]; w[2] = sc * q[2];
+}
+
+/* BundleAdjustment.py:43-110 residuals r = obs - proj, interleaved. */
+void orc_ba_residuals(int32_t n_cams, int64_t n_obs, const int32_t *cam, const int32_t *pt,
+                      const double *obs, const double *K, const double *cams /* n x 6 */,
+                      const double *pts /* n x 3 */, double *r) {
+    double *R = (double *)malloc(sizeof(double) * 9 * (size_t)n_cams);
+    for (int c = 0; c < n_cams; ++c) orc_rotvec_to_R(cams + 6 * c, R + 9 * c);
+    for (int64_t o = 0; o < n_obs; ++o) {
+        const double *Rc = R + 9 * cam[o], *t = cams + 6 * cam[o] + 3, *X = pts + 3 * pt[o];
+        double xc[3], u[3];
+        for (int i = 0; i < 3; ++i) xc[i] = Rc[3 * i] * X[0] + Rc[3 * i + 1] * X[1] + Rc[3 * i + 2] * X[2] + t[i];
+        for (int i = 0; i < 3; ++i) u[i] = K[3 * i] * xc[0] + K[3 * i + 1] * xc[1] + K[3 * i + 2] * xc[2];
+        double w = u[2] + 1e-8;
+        r[2 * o] = obs[2 * o] - u[0] / w;
+        r[2 * o + 1] = obs[2 * o + 1] - u[1] / w;
+    }
+    free(R);
+}
+
+typedef struct {
+    int32_t max_iterations;
+    double function_tolerance; /* stop when |dcost|/cost < ftol on an accepted step */
+    double gradient_tolerance;
+    double parameter_tolerance;
+    double initial_lambda;
+} orc_ba_opts;
+
+typedef struct {
+    int32_t iterations;  /* LM iterations = damped solves + trial evaluations */
+    int32_t accepted;
+    int32_t status;      /* 1 ftol, 2 gtol, 3 xtol, 4 max_iter, 5 lambda overflow */
+    double cost0, cost;
+} orc_ba_report;
+
+/* one observation: residual + Jacobians wrt (dtheta, t) and X, with the
+ * rotation perturbed on the left: R <- exp([dtheta]x) R */
+static void linearize_obs(const double *Rc, const double *t, const double *X, const double *K,
+                          const double *ob, double *r, double *Jc /*2x6*/, double *Jp /*2x3*/) {
+    double p[3], xc[3], u[3];
+    for (int i = 0; i < 3; ++i) p[i] = Rc[3 * i] * X[0] + Rc[3 * i + 1] * X[1] + Rc[3 * i + 2] * X[2];
+    for (int i = 0; i < 3; ++i) xc[i] = p[i] + t[i];
+    for (int i = 0; i < 3; ++i) u[i] = K[3 * i] * xc[0] + K[3 * i + 1] * xc[1] + K[3 * i + 2] * xc[2];
+    double w = u[2] + 1e-8, iw = 1.0 / w;
+    double pu = u[0] * iw, pv = u[1] * iw;
+    r[0] = ob[0] - pu;
+    r[1] = ob[1] - pv;
+    /* dr/du = -[[iw,0,-pu*iw],[0,iw,-pv*iw]] ; A = dr/du K (2x3) */
+    double A[6];
+    for (int c = 0; c < 3; ++c) {
+        A[c] = -(iw * K[c] - pu * iw * K[6 + c]);
+        A[3 + c] = -(iw * K[3 + c] - pv * iw * K[6 + c]);
+    }
+    for (int a = 0; a < 2; ++a) {
+        const double *Aa = A + 3 * a;
+        /* d xc / d theta = -[p]x */
+        Jc[6 * a + 0] = Aa[1] * (-p[2]) + Aa[2] * p[1];
+        Jc[6 * a + 1] = Aa[0] * p[2] + Aa[2] * (-p[0]);
+        Jc[6 * a + 2] = Aa[0] * (-p[1]) + Aa[1] * p[0];
+        Jc[6 * a + 3] = Aa[0]; Jc[6 * a + 4] = Aa[1]; Jc[6 * a + 5] = Aa[2];
+        for (int c = 0; c < 3; ++c) Jp[3 * a + c] = Aa[0] * Rc[c] + Aa[1] * Rc[3 + c] + Aa[2] * Rc[6 + c];
+    }
+}
+
+static int cholesky_solve(double *S, int n, double *b) {
+    for (int j = 0; j < n; ++j) {
+        double d = S[j * n + j];
+        for (int k = 0; k < j; ++k) d -= S[j * n + k] * S[j * n + k];
+        if (!(d > 0)) return -1;
+        d = sqrt(d);
+        S[j * n + j] = d;
+        for (int i = j + 1; i < n; ++i) {
+            double v = S[i * n + j];
+            for (int k = 0; k < j; ++k) v -= S[i * n + k] * S[j * n + k];
+            S[i * n + j] = v / d;
+        }
+    }
+    for (int i = 0; i < n; ++i) {
+        double v = b[i];
+        for (int k = 0; k < i; ++k) v -= S[i * n + k] * b[k];
+        b[i] = v / S[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        double v = b[i];
+        for (int k = i + 1; k < n; ++k) v -= S[k * n + i] * b[k];
+        b[i] = v / S[i * n + i];
+    }
+    return 0;
+}
+
+static void inv3_sym(const double *M, double *I) {
+    double a = M[0], b = M[1], c = M[2], d = M[4], e = M[5], f = M[8];
+    double A = d * f - e * e, B = c * e - b * f, C = b * e - c * d;
+    double det = a * A + b * B + c * C;
+    double id = 1.0 / det;
+    I[0] = A * id; I[1] = B * id; I[2] = C * id;
+    I[3] = B * id; I[4] = (a * f - c * c) * id; I[5] = (b * c - a * e) * id;
+    I[6] = C * id; I[7] = (b * c - a * e) * id; I[8] = (a * d - b * b) * id;
+}
+
+static double clampd(double x) { return x < 1e-6 ? 1e-6 : (x > 1e32 ? 1e32 : x); }
+
+/* Schur-complement LM.  Observations must be point-major (sorted by pt),
+ * as the reference assembles them (BundleAdjustment.py:164-169).
+ * cams: n_cams x 6 [rotvec, t] in/out, pts: n_pts x 3 in/out. */
+int orc_ba_lm(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt,
+              const double *obs, const double *K, double *cams, double *pts,
+              const orc_ba_opts *opt, orc_ba_report *rep) {
+    const int ns = 6 * nc;
+    double *R = malloc(sizeof(double) * 9 * nc), *t = malloc(sizeof(double) * 3 * nc);
+    double *Rn = malloc(sizeof(double) * 9 * nc), *tn = malloc(sizeof(double) * 3 * nc);
+    double *Xn = malloc(sizeof(double) * 3 * np_);
+    double *J = malloc(sizeof(double) * 20 * no); /* r(2) Jc(12) Jp(6) */
+    double *U = malloc(sizeof(double) * 36 * nc), *gc = malloc(sizeof(double) * ns);
+    double *V = malloc(sizeof(double) * 9 * np_), *gp = malloc(sizeof(double) * 3 * np_);
+    double *Vi = malloc(sizeof(double) * 9 * np_);
+    double *S = malloc(sizeof(double) * ns * ns), *b = malloc(sizeof(double) * ns);
+    double *dp = malloc(sizeof(double) * 3 * np_);
+    int64_t *pstart = malloc(sizeof(int64_t) * (np_ + 1));
+    if (!R || !t || !Rn || !tn || !Xn || !J || !U || !gc || !V || !gp || !Vi || !S || !b || !dp || !pstart)
+        return -2;
+    /* CSR of observations by point */
+    for (int64_t p = 0; p <= np_; ++p) pstart[p] = 0;
+    for (int64_t o = 0; o < no; ++o) pstart[pt[o] + 1]++;
+    for (int64_t p = 0; p < np_; ++p) pstart[p + 1] += pstart[p];
+    for (int64_t o = 1; o < no; ++o) if (pt[o] < pt[o - 1]) return -3;
+    for (int c = 0; c < nc; ++c) {
+        orc_rotvec_to_R(cams + 6 * c, R + 9 * c);
+        memcpy(t + 3 * c, cams + 6 * c + 3, 3 * sizeof(double));
+    }
+    double lambda = opt->initial_lambda, nu = 2.0, cost = 0;
+    int need_lin = 1, status = 4, accepted = 0, it = 0;
+    double cost0 = -1;
+    for (it = 0; it < opt->max_iterations; ++it) {
+        if (need_lin) {
+            memset(U, 0, sizeof(double) * 36 * nc);
+            memset(gc, 0, sizeof(double) * ns);
+            cost = 0;
+            for (int64_t p = 0; p < np_; ++p) {
+                double *Vp = V + 9 * p, *g = gp + 3 * p;
+                memset(Vp, 0, 9 * sizeof(double)); memset(g, 0, 3 * sizeof(double));
+                for (int64_t o = pstart[p]; o < pstart[p + 1]; ++o) {
+                    int c = cam[o];
+                    double *e = J + 20 * o, *Jc = e + 2, *Jp = e + 14;
+                    linearize_obs(R + 9 * c, t + 3 * c, pts + 3 * p, K, obs + 2 * o, e, Jc, Jp);
+                    cost += 0.5 * (e[0] * e[0] + e[1] * e[1]);
+                    double *Uc = U + 36 * c;
+                    for (int i = 0; i < 6; ++i) {
+                        for (int j = 0; j < 6; ++j) Uc[6 * i + j] += Jc[i] * Jc[j] + Jc[6 + i] * Jc[6 + j];
+                        gc[6 * c + i] += Jc[i] * e[0] + Jc[6 + i] * e[1];
+                    }
+                    for (int i = 0; i < 3; ++i) {
+                        for (int j = 0; j < 3; ++j) Vp[3 * i + j] += Jp[i] * Jp[j] + Jp[3 + i] * Jp[3 + j];
+                        g[i] += Jp[i] * e[0] + Jp[3 + i] * e[1];
+                    }
+                }
+            }
+            if (cost0 < 0) cost0 = cost;
+            double gmax = 0;
+            for (int i = 0; i < ns; ++i) if (fabs(gc[i]) > gmax) gmax = fabs(gc[i]);
+            for (int64_t i = 0; i < 3 * np_; ++i) if (fabs(gp[i]) > gmax) gmax = fabs(gp[i]);
+            if (gmax < opt->gradient_tolerance) { status = 2; break; }
+            need_lin = 0;
+        }
+        /* damped Schur system */
+        memset(S, 0, sizeof(double) * ns * ns);
+        for (int c = 0; c < nc; ++c)
+            for (int i = 0; i < 6; ++i) {
+                for (int j = 0; j < 6; ++j) S[(6 * c + i) * ns + 6 * c + j] = U[36 * c + 6 * i + j];
+                S[(6 * c + i) * ns + 6 * c + i] += lambda * clampd(U[36 * c + 7 * i]);
+                b[6 * c + i] = -gc[6 * c + i];
+            }
+        for (int64_t p = 0; p < np_; ++p) {
+            double Vd[9];
+            memcpy(Vd, V + 9 * p, sizeof Vd);
+            for (int i = 0; i < 3; ++i) Vd[4 * i] += lambda * clampd(V[9 * p + 4 * i]);
+            double *Vinv = Vi + 9 * p;
+            inv3_sym(Vd, Vinv);
+            const double *g = gp + 3 * p;
+            double Vg[3];
+            for (int i = 0; i < 3; ++i) Vg[i] = Vinv[3 * i] * g[0] + Vinv[3 * i + 1] * g[1] + Vinv[3 * i + 2] * g[2];
+            for (int64_t oa = pstart[p]; oa < pstart[p + 1]; ++oa) {
+                const double *Ja = J + 20 * oa;
+                double Wa[18], Ya[18]; /* W = Jc^T Jp (6x3), Y = W Vinv */
+                for (int i = 0; i < 6; ++i)
+                    for (int j = 0; j < 3; ++j) Wa[3 * i + j] = Ja[2 + i] * Ja[14 + j] + Ja[8 + i] * Ja[17 + j];
+                for (int i = 0; i < 6; ++i)
+                    for (int j = 0; j < 3; ++j)
+                        Ya[3 * i + j] = Wa[3 * i] * Vinv[j] + Wa[3 * i + 1] * Vinv[3 + j] + Wa[3 * i + 2] * Vinv[6 + j];
+                int ca = cam[oa];
+                for (int i = 0; i < 6; ++i)
+                    b[6 * ca + i] += Wa[3 * i] * Vg[0] + Wa[3 * i + 1] * Vg[1] + Wa[3 * i + 2] * Vg[2];
+                for (int64_t ob = pstart[p]; ob < pstart[p + 1]; ++ob) {
+                    const double *Jb = J + 20 * ob;
+                    int cb = cam[ob];
+                    double Wb[18];
+                    for (int i = 0; i < 6; ++i)
+                        for (int j = 0; j < 3; ++j) Wb[3 * i + j] = Jb[2 + i] * Jb[14 + j] + Jb[8 + i] * Jb[17 + j];
+                    for (int i = 0; i < 6; ++i)
+                        for (int j = 0; j < 6; ++j)
+                            S[(6 * ca + i) * ns + 6 * cb + j] -=
+                                Ya[3 * i] * Wb[3 * j] + Ya[3 * i + 1] * Wb[3 * j + 1] + Ya[3 * i + 2] * Wb[3 * j + 2];
+                }
+            }
+        }
+        double *dc = b; /* solved in place */
+        int ok = cholesky_solve(S, ns, b) == 0;
+        double model = 0, cost_new = 0, dnorm = 0, xnorm = 0;
+        if (ok) {
+            /* back-substitution dp = Vinv (-gp - W^T dc) */
+            for (int64_t p = 0; p < np_; ++p) {
+                double rhs[3] = {-gp[3 * p], -gp[3 * p + 1], -gp[3 * p + 2]};
+                for (int64_t o = pstart[p]; o < pstart[p + 1]; ++o) {
+                    const double *Jo = J + 20 * o;
+                    const double *d = dc + 6 * cam[o];
+                    for (int j = 0; j < 3; ++j) {
+                        double w = 0;
+                        for (int i = 0; i < 6; ++i) w += (Jo[2 + i] * Jo[14 + j] + Jo[8 + i] * Jo[17 + j]) * d[i];
+                        rhs[j] -= w;
+                    }
+                }
+                const double *Vinv = Vi + 9 * p;
+                for (int i = 0; i < 3; ++i)
+                    dp[3 * p + i] = Vinv[3 * i] * rhs[0] + Vinv[3 * i + 1] * rhs[1] + Vinv[3 * i + 2] * rhs[2];
+            }
+            /* model decrease 0.5 * d^T (lambda D d - g) */
+            for (int c = 0; c < nc; ++c)
+                for (int i = 0; i < 6; ++i) {
+                    double d = dc[6 * c + i];
+                    model += d * (lambda * clampd(U[36 * c + 7 * i]) * d - gc[6 * c + i]);
+                    dnorm += d * d;
+                }
+            for (int64_t p = 0; p < np_; ++p)
+                for (int i = 0; i < 3; ++i) {
+                    double d = dp[3 * p + i];
+                    model += d * (lambda * clampd(V[9 * p + 4 * i]) * d - gp[3 * p + i]);
+                    dnorm += d * d;
+                    xnorm += pts[3 * p + i] * pts[3 * p + i];
+                }
+            model *= 0.5;
+            /* trial state */
+            for (int c = 0; c < nc; ++c) {
+                double dR[9], *Rnc = Rn + 9 * c;
+                orc_rotvec_to_R(dc + 6 * c, dR);
+                for (int i = 0; i < 3; ++i)
+                    for (int j = 0; j < 3; ++j)
+                        Rnc[3 * i + j] = dR[3 * i] * R[9 * c + j] + dR[3 * i + 1] * R[9 * c + 3 + j] + dR[3 * i + 2] * R[9 * c + 6 + j];
+                for (int i = 0; i < 3; ++i) { tn[3 * c + i] = t[3 * c + i] + dc[6 * c + 3 + i]; xnorm += t[3 * c + i] * t[3 * c + i]; }
+            }
+            for (int64_t i = 0; i < 3 * np_; ++i) Xn[i] = pts[i] + dp[i];
+            for (int64_t o = 0; o < no; ++o) {
+                double e[2], Jc[12], Jp[6];
+                int c = cam[o];
+                linearize_obs(Rn + 9 * c, tn + 3 * c, Xn + 3 * pt[o], K, obs + 2 * o, e, Jc, Jp);
+                cost_new += 0.5 * (e[0] * e[0] + e[1] * e[1]);
+            }
+        }
+        double rho = ok && model > 0 ? (cost - cost_new) / model : -1.0;
+        if (ok && rho > 1e-3 && isfinite(cost_new)) {
+            double dcost = cost - cost_new;
+            memcpy(R, Rn, sizeof(double) * 9 * nc);
+            memcpy(t, tn, sizeof(double) * 3 * nc);
+            memcpy(pts, Xn, sizeof(double) * 3 * np_);
+            accepted++;
+            double f = 2.0 * rho - 1.0;
+            f = 1.0 - f * f * f;
+            lambda *= f > 1.0 / 3.0 ? f : 1.0 / 3.0;
+            nu = 2.0;
+            cost = cost_new;
+            need_lin = 1;
+            if (dcost < opt->function_tolerance * cost) { status = 1; it++; break; }
+            if (sqrt(dnorm) < opt->parameter_tolerance * (sqrt(xnorm) + opt->parameter_tolerance)) { status = 3; it++; break; }
+        } else {
+            lambda *= nu;
+            nu *= 2.0;
+            if (lambda > 1e32) { status = 5; it++; break; }
+        }
+    }
+    for (int c = 0; c < nc; ++c) {
+        orc_R_to_rotvec(R + 9 * c, cams + 6 * c);
+        memcpy(cams + 6 * c + 3, t + 3 * c, 3 * sizeof(double));
+    }
+    if (rep) {
+        rep->iterations = it; rep->accepted = accepted; rep->status = status;
+        rep->cost0 = cost0; rep->cost = cost;
+    }
+    free(R); free(t); free(Rn); free(tn); free(Xn); free(J); free(U); free(gc); free(V); free(gp);
+    free(Vi); free(S); free(b); free(dp); free(pstart);
+    return 0;
+}
