@@ -1,0 +1,153 @@
+/*
+ * sfmcore.h -- C-ABI of libsfmcore.so, the MI355X (gfx950) numerical core
+ * that replaces the reference's hot path
+ *   EstimateFundamentalMatrix -> GetInliersRANSAC -> LinearTriangulation
+ *   -> BundleAdjustment       (pvrohin/Structure-from-Motion-, "Phase 1/").
+ *
+ * Plain C types only: caller-owned, row-major, C-contiguous host buffers,
+ * int return codes (0 = OK, < 0 = error; message via sfm_last_error()).
+ * No C++ exception crosses this line.  Every entry point is reentrant: each
+ * host thread gets its own HIP stream and scratch buffers per device.
+ *
+ * The Python drop-in modules in structure-from-motion-_amd/ bind these with
+ * ctypes (_sfmcore.py); INTEGRATION.md shows the binding.
+ */
+#ifndef SFMCORE_H
+#define SFMCORE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SFM_ABI_VERSION 1
+
+enum {
+    SFM_OK = 0,
+    SFM_ERR_ARG = -1,     /* bad argument (shape, null pointer, range)   */
+    SFM_ERR_HIP = -2,     /* HIP runtime error                           */
+    SFM_ERR_NOMEM = -3,   /* device allocation failed                    */
+    SFM_ERR_SOLVE = -4,   /* reduced camera system not positive definite */
+    SFM_ERR_COMM = -5     /* RCCL error                                  */
+};
+
+int sfm_version(void);
+/* last error message of the calling thread ("" if none) */
+const char *sfm_last_error(void);
+int sfm_device_count(void);
+/* per-call phase timings of the calling thread's last call (ms):
+ * [0] host->device upload, [1] kernels, [2] device->host download,
+ * [3] kernel-only time of the dominant kernel.  Returns the count written. */
+int sfm_last_timings(double *out, int n);
+
+/* ---------------------------------------------------------------------
+ * Python `random` replay (host code, no GPU).
+ * Replaces the n_max calls of random.sample(range(n), k) made by
+ * GetInliersRANSAC.py:55 on the *global* MT19937 instance.  `mt_state`
+ * is random.getstate()[1] (624 words + position) and is advanced in place
+ * exactly as CPython 3.10 would (random.py:_randbelow_with_getrandbits and
+ * sample()'s pool / set branches), so random.setstate() afterwards leaves
+ * the global stream where the reference leaves it.  out: H x k int32.
+ * ------------------------------------------------------------------- */
+int sfm_pyrandom_sample_table(uint32_t *mt_state /* 625 in/out */, int64_t n, int32_t k,
+                              int64_t H, int32_t *out);
+
+/* ---------------------------------------------------------------------
+ * EstimateFundamentalMatrix (EstimateFundamentalMatrix.py:3-83)
+ * ------------------------------------------------------------------- */
+/* H independent 8-point estimates: x1s, x2s are H x 8 x 2; F is H x 9. */
+int sfm_f8_batch(const double *x1s, const double *x2s, int64_t H, double *F, int device);
+/* one estimate from N >= 8 correspondences (least-squares null vector). */
+int sfm_f8_general(const double *x1, const double *x2, int64_t N, double *F, int device);
+
+/* ---------------------------------------------------------------------
+ * GetInliersRANSAC (GetInliersRANSAC.py:5-106)
+ * x1, x2: N x 2; samples: H x 8 indices (host-drawn, see above).
+ * counts_out (H, nullable): inliers per hypothesis.  *best_iter: first
+ * hypothesis with the strictly largest positive count, or -1 if every
+ * count is 0 (the reference's "F_best is None").  F_best (9) and
+ * best_mask (N, 1 = inlier) are written only when *best_iter >= 0.
+ * ------------------------------------------------------------------- */
+int sfm_ransac_f8(const double *x1, const double *x2, int64_t N, const int32_t *samples, int64_t H,
+                  double thr, int32_t *counts_out, int64_t *best_iter, double *F_best,
+                  uint8_t *best_mask, int device);
+
+/* ---------------------------------------------------------------------
+ * LinearTriangulation (LinearTriangulation.py:3-92)
+ * P1, P2: 3 x 4 projection matrices K[R | -RC]; x1, x2: N x 2; X: N x 3.
+ * ------------------------------------------------------------------- */
+int sfm_triangulate_dlt(const double *P1, const double *P2, const double *x1, const double *x2,
+                        int64_t N, double *X, int device);
+
+/* ---------------------------------------------------------------------
+ * BundleAdjustment (BundleAdjustment.py:8-242)
+ * Camera parameters are the reference's: [rotvec(3), t(3)] with
+ * x_cam = R(rotvec) X + t, proj = K x_cam [:2] / (K x_cam [2] + 1e-8),
+ * residual r = obs - proj (BundleAdjustment.py:73-110).
+ * ------------------------------------------------------------------- */
+/* project_points (BundleAdjustment.py:8-40) for one camera P = K[R|-RC]:
+ * P is 3 x 4, X is M x 3, out M x 2. */
+int sfm_project_points(const double *P, const double *X, int64_t M, double *out, int device);
+/* bundle_adjustment_residuals: r (2 * n_obs), interleaved [rx0, ry0, ...]. */
+int sfm_ba_residuals(int32_t n_cams, int64_t n_pts, int64_t n_obs, const int32_t *cam_idx,
+                     const int32_t *pt_idx, const double *obs, const double *K,
+                     const double *cam_params, const double *points, double *r, int device);
+
+typedef struct {
+    int32_t max_iterations;      /* LM iterations (damped solve + trial)        */
+    int32_t fixed_iterations;    /* 1: run exactly max_iterations (benchmark)   */
+    double function_tolerance;   /* stop: accepted step with dcost < ftol*cost  */
+    double gradient_tolerance;   /* stop: max |J^T r| < gtol                     */
+    double parameter_tolerance;  /* stop: |dx| < xtol (|x| + xtol)               */
+    double initial_lambda;       /* Marquardt damping on clamp(diag(J^T J))      */
+} sfm_ba_opts;
+
+typedef struct {
+    int32_t iterations;  /* LM iterations performed                             */
+    int32_t accepted;    /* accepted steps (re-linearisations)                  */
+    int32_t status;      /* 1 ftol, 2 gtol, 3 xtol, 4 max_iterations, 5 lambda */
+    int32_t n_ranks;
+    double cost0, cost;  /* 0.5 sum r^2 before / after                          */
+    double t_setup_ms;   /* host prep + uploads                                 */
+    double t_loop_ms;    /* LM loop wall time                                   */
+    double t_download_ms;
+    double lambda;
+} sfm_ba_report;
+
+/* Observations must be point-major (sorted by pt_idx, as the reference
+ * assembles them: BundleAdjustment.py:164-169).  cam_params (n_cams x 6)
+ * and points (n_pts x 3) are updated in place. */
+int sfm_ba_lm(int32_t n_cams, int64_t n_pts, int64_t n_obs, const int32_t *cam_idx,
+              const int32_t *pt_idx, const double *obs, const double *K, double *cam_params,
+              double *points, const sfm_ba_opts *opts, sfm_ba_report *report, int device);
+
+/* ---- device-resident BA session (bench / multi-GPU) -------------------
+ * A problem is uploaded once and iterated many times.  With a communicator
+ * each rank holds a disjoint subset of the points (and all of their
+ * observations) and every camera; one RCCL all-reduce (sum, fp64) of the
+ * partial reduced camera system per LM iteration + one of the trial cost. */
+typedef struct sfm_comm sfm_comm;
+typedef struct sfm_ba_problem sfm_ba_problem;
+
+int sfm_comm_unique_id(char out[128]);
+int sfm_comm_init(const char id[128], int nranks, int rank, int device, sfm_comm **out);
+int sfm_comm_destroy(sfm_comm *comm);
+
+int sfm_ba_create(int32_t n_cams, int64_t n_pts, int64_t n_obs, const int32_t *cam_idx,
+                  const int32_t *pt_idx, const double *obs, const double *K,
+                  const double *cam_params, const double *points, int device, sfm_comm *comm,
+                  sfm_ba_problem **out);
+int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *opts, sfm_ba_report *report);
+/* reset the device state to the initial parameters given at create time */
+int sfm_ba_reset(sfm_ba_problem *p);
+int sfm_ba_download(sfm_ba_problem *p, double *cam_params, double *points);
+/* average device time per LM iteration of each kernel family over the
+ * last solve (ms): names are written ';'-separated into `names`. */
+int sfm_ba_kernel_times(sfm_ba_problem *p, double *ms, int n, char *names, int names_len);
+int sfm_ba_destroy(sfm_ba_problem *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SFMCORE_H */

@@ -1,0 +1,154 @@
+"""Drop-in for the reference module ``BundleAdjustment``
+(Phase 1/BundleAdjustment.py:8-242).
+
+``perform_bundle_adjustment`` keeps the reference's signature, observation
+order (point-major, camera ascending, :164-169), parameterisation
+([rotvec, t] per camera then points, :183-197), printed lines (:202, :236,
+:241) and failure contract (any exception -> print + return the inputs
+unchanged, :240-242; scipy's m < n and non-finite-x0 errors reproduced).
+The solve itself is the MI355X sparse Schur-complement Levenberg-Marquardt
+of libsfmcore (csrc/ba.hip) run to convergence on the reference residual.
+The reference's scipy call stops at max_nfev=100 and, for any problem with
+6*n_cams + 3*n_pts >= 98 parameters, returns x0 unchanged;
+the drop-in's result is never worse than that and matches the converged
+least-squares solution (tests/test_gpu_parity.py).
+"""
+import numpy as np
+from scipy.spatial.transform import Rotation
+
+import _sfmcore as _core
+
+
+def project_points(K, C, R, X):
+    """
+    Project 3D points to 2D image coordinates.
+
+    Parameters
+    ----------
+    K : numpy.ndarray
+        Camera intrinsic matrix (3 x 3)
+    C : numpy.ndarray
+        Camera center (3,)
+    R : numpy.ndarray
+        Camera rotation matrix (3 x 3)
+    X : numpy.ndarray
+        3D points (N x 3)
+
+    Returns
+    -------
+    x_proj : numpy.ndarray
+        Projected 2D points (N x 2)
+    """
+    P = K @ np.hstack([R, -R @ C.reshape(3, 1)])  # :32
+    return _core.project(P, np.asarray(X).reshape(-1, 3))
+
+
+def bundle_adjustment_residuals(params, n_cameras, n_points, camera_indices, point_indices,
+                                points_2d, K, n_cam_params=6):
+    """
+    Compute residuals for bundle adjustment.
+
+    Returns
+    -------
+    residuals : numpy.ndarray
+        Reprojection errors (2*N,), interleaved [r0x, r0y, r1x, ...]
+    """
+    params = np.asarray(params, dtype=np.float64)
+    camera_params = params[:n_cameras * n_cam_params].reshape(n_cameras, n_cam_params)[:, :6]
+    points_3d = params[n_cameras * n_cam_params:].reshape(n_points, 3)
+    return _core.ba_residuals(camera_params, points_3d, camera_indices, point_indices,
+                              np.asarray(points_2d).reshape(-1, 2), K)
+
+
+def _observations(filtered_world_coords, feature_x, feature_y, filtered_feature_flags, n_cameras):
+    """Dense flags -> COO observations in the reference's order (:164-169)."""
+    valid_point_indices = np.where(np.asarray(filtered_world_coords).flatten() == 1)[0]
+    flags = np.asarray(filtered_feature_flags)[valid_point_indices][:, :n_cameras] == 1
+    point_indices, camera_indices = np.nonzero(flags)  # row-major = point-major, camera ascending
+    rows = valid_point_indices[point_indices]
+    points_2d = np.column_stack([np.asarray(feature_x)[rows, camera_indices],
+                                 np.asarray(feature_y)[rows, camera_indices]])
+    return valid_point_indices, camera_indices, point_indices, points_2d
+
+
+def perform_bundle_adjustment(all_world_coords, filtered_world_coords, feature_x, feature_y,
+                              filtered_feature_flags, R_set, C_set, K, cam_index, *,
+                              max_iterations=100, function_tolerance=1e-10, parameter_tolerance=1e-12,
+                              initial_lambda=1e-4):
+    """
+    Perform bundle adjustment to optimize camera poses and 3D points.
+
+    Parameters
+    ----------
+    all_world_coords : numpy.ndarray
+        All 3D points (n_features x 3)
+    filtered_world_coords : numpy.ndarray
+        Flag array indicating which points are valid (n_features x 1)
+    feature_x : numpy.ndarray
+        X coordinates of features (n_features x n_cameras)
+    feature_y : numpy.ndarray
+        Y coordinates of features (n_features x n_cameras)
+    filtered_feature_flags : numpy.ndarray
+        Flag matrix indicating which features are visible in which cameras (n_features x n_cameras)
+    R_set : list
+        List of rotation matrices for each camera
+    C_set : list
+        List of camera centers for each camera
+    K : numpy.ndarray
+        Camera intrinsic matrix (3 x 3)
+    cam_index : int
+        Current camera index (0-based); unused, as in the reference
+    max_iterations, function_tolerance, parameter_tolerance, initial_lambda :
+        keyword-only LM controls of the GPU solver (not in the reference)
+
+    Returns
+    -------
+    R_set_opt : list
+        Optimized rotation matrices
+    C_set_opt : list
+        Optimized camera centers
+    all_world_coords_opt : numpy.ndarray
+        Optimized 3D points
+    """
+    valid_point_indices = np.where(np.asarray(filtered_world_coords).flatten() == 1)[0]
+    if len(valid_point_indices) == 0:  # :152-153
+        return R_set, C_set, all_world_coords
+    n_cameras = len(R_set)
+    n_points = len(valid_point_indices)
+    valid_point_indices, camera_indices, point_indices, points_2d = _observations(
+        filtered_world_coords, feature_x, feature_y, filtered_feature_flags, n_cameras)
+    if len(camera_indices) == 0:  # :171-172
+        return R_set, C_set, all_world_coords
+    cams0 = np.zeros((n_cameras, 6))
+    for i in range(n_cameras):  # :183-193
+        R = np.array(R_set[i])
+        C = np.array(C_set[i])
+        cams0[i, :3] = Rotation.from_matrix(R).as_rotvec()
+        cams0[i, 3:] = -R @ C
+    pts0 = np.asarray(all_world_coords, dtype=np.float64)[valid_point_indices]
+    print(f"  Bundle adjustment: {n_cameras} cameras, {n_points} points, {len(camera_indices)} observations")
+    _core.require_device()  # a missing GPU is an error, never a silent "failed"
+    try:
+        if 2 * len(camera_indices) < 6 * n_cameras + 3 * n_points:  # scipy least_squares.py:850-852
+            raise ValueError("Method 'lm' doesn't work when the number of residuals is less than the "
+                             "number of variables.")
+        r0 = _core.ba_residuals(cams0, pts0, camera_indices, point_indices, points_2d, K)
+        if not np.all(np.isfinite(r0)):  # least_squares.py:843-845
+            raise ValueError("Residuals are not finite in the initial point.")
+        cams, pts, rep = _core.ba_lm(cams0, pts0, camera_indices, point_indices, points_2d, K,
+                                     max_iterations=max_iterations, function_tolerance=function_tolerance,
+                                     parameter_tolerance=parameter_tolerance, initial_lambda=initial_lambda)
+        R_set_opt = []
+        C_set_opt = []
+        for i in range(n_cameras):  # :220-228
+            R_opt = Rotation.from_rotvec(cams[i, :3]).as_matrix()
+            C_opt = -R_opt.T @ cams[i, 3:]
+            R_set_opt.append(R_opt)
+            C_set_opt.append(C_opt)
+        all_world_coords_opt = all_world_coords.copy()  # :231-234
+        all_world_coords_opt[valid_point_indices] = pts
+        print(f"  Bundle adjustment completed. Final cost: {rep['cost']:.6f}")
+        return R_set_opt, C_set_opt, all_world_coords_opt
+    except Exception as e:
+        print(f"  Bundle adjustment failed: {e}")
+        return R_set, C_set, all_world_coords

@@ -1,0 +1,77 @@
+"""Drop-in for the reference module ``GetInliersRANSAC``
+(Phase 1/GetInliersRANSAC.py:5-121).
+
+The reference loop (:53-92: sample 8, estimate F, score all N, strict '>'
+update) becomes one batched evaluation on the MI355X:
+
+1. the n_max samples are drawn from the GLOBAL ``random`` instance exactly as
+   the reference draws them (n_max calls of random.sample(range(N), 8) in
+   iteration order, replayed natively and written back with setstate), so
+   the stream seen by later callers (PnPRANSAC, the next image pair) is
+   unchanged;
+2. libsfmcore builds every hypothesis F (one thread each), scores every
+   (hypothesis, correspondence) pair (one wavefront per hypothesis, LDS
+   tiles, ballot popcount) and picks the first hypothesis with the strictly
+   largest count -- the reference's tie rule (:85-88).
+"""
+import numpy as np
+
+import _sfmcore as _core
+from EstimateFundamentalMatrix import EstimateFundamentalMatrix  # noqa: F401  (re-exported as in :3)
+
+
+def GetInliersRANSAC(points1, points2, index, threshold=0.06, n_max=1000):
+    """
+    Rejects the outliers from a set of feature matches and returns the inliner indices.
+
+    Parameters
+    ----------
+    points1 : numpy.ndarray
+        feature points for matching in first image
+    points2 : numpy.ndarray
+        feature points for matching in second image
+    index : numpy.ndarray
+        index of all feature matches
+    threshold : float
+        threshold for inlier detection (default: 0.06)
+    n_max : int
+        maximum number of RANSAC iterations (default: 1000)
+
+    Results
+    -------
+    inlier_index : numpy.ndarray
+        index of all inlier feature matches
+    outlier_index : numpy.ndarray
+        index of all outlier feature matches for visulaization
+    F_best : numpy.ndarray
+        the best fundamental matrix
+    """
+    points1 = np.array(points1)
+    points2 = np.array(points2)
+    index = np.array(index)
+    n_points = len(points1)
+    if n_points < 8:  # :38-40
+        return np.array([]), index, None
+    n_iter = max(int(n_max), 0)
+    samples = _core.sample_table(n_points, min(8, n_points), n_iter)
+    best, F_best, mask, _ = _core.ransac_f8(points1.reshape(n_points, 2), points2.reshape(n_points, 2),
+                                            samples, threshold)
+    if best < 0:  # :95-96 (no hypothesis with a positive count)
+        return np.array([]), index, None
+    inlier_index = np.where(mask)[0]
+    outlier_indices = index[~mask]
+    return inlier_index, outlier_indices, F_best
+
+
+def get_inliers_ransac(points1, points2, index, threshold=0.06, n_max=1000):
+    """
+    Alias for GetInliersRANSAC with lowercase name.
+    Returns (F_best, inlier_index) instead of (inlier_index, outlier_index, F_best)
+    for compatibility with wrapper code.
+    """
+    inlier_index, outlier_indices, F_best = GetInliersRANSAC(points1, points2, index, threshold, n_max)
+    if len(inlier_index) > 0:  # :113-121
+        inlier_idx = index[inlier_index]
+    else:
+        inlier_idx = np.array([])
+    return F_best, inlier_idx

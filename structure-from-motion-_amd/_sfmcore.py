@@ -1,0 +1,286 @@
+"""ctypes binding of libsfmcore.so (include/sfmcore.h) for the drop-in modules.
+
+This is the only route to compute: there is no CPU fallback.  Importing this
+module fails loudly if the HIP library has not been built, and every compute
+call raises ``SfmCoreError`` if no MI355X is visible.
+
+The device is ``$SFM_DEVICE`` (default 0).
+"""
+import ctypes
+import os
+import random
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsfmcore.so")
+
+
+class SfmCoreError(RuntimeError):
+    pass
+
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"libsfmcore.so not built at {LIB_PATH}: run `make -C {_HERE}` "
+                      "(or __graft_entry__.build()); there is no CPU fallback")
+
+_lib = ctypes.CDLL(LIB_PATH)
+
+_d = ctypes.POINTER(ctypes.c_double)
+_i32 = ctypes.POINTER(ctypes.c_int32)
+_u32 = ctypes.POINTER(ctypes.c_uint32)
+_i64 = ctypes.POINTER(ctypes.c_int64)
+_u8 = ctypes.POINTER(ctypes.c_uint8)
+_c = ctypes.c_int
+_i = ctypes.c_int64
+
+
+class BAOpts(ctypes.Structure):
+    _fields_ = [("max_iterations", ctypes.c_int32), ("fixed_iterations", ctypes.c_int32),
+                ("function_tolerance", ctypes.c_double), ("gradient_tolerance", ctypes.c_double),
+                ("parameter_tolerance", ctypes.c_double), ("initial_lambda", ctypes.c_double)]
+
+
+class BAReport(ctypes.Structure):
+    _fields_ = [("iterations", ctypes.c_int32), ("accepted", ctypes.c_int32), ("status", ctypes.c_int32),
+                ("n_ranks", ctypes.c_int32), ("cost0", ctypes.c_double), ("cost", ctypes.c_double),
+                ("t_setup_ms", ctypes.c_double), ("t_loop_ms", ctypes.c_double),
+                ("t_download_ms", ctypes.c_double), ("lambda_", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# (name, restype, argtypes) -- every symbol include/sfmcore.h declares
+SIGNATURES = [
+    ("sfm_version", _c, []),
+    ("sfm_last_error", ctypes.c_char_p, []),
+    ("sfm_device_count", _c, []),
+    ("sfm_last_timings", _c, [_d, _c]),
+    ("sfm_pyrandom_sample_table", _c, [_u32, _i, ctypes.c_int32, _i, _i32]),
+    ("sfm_f8_batch", _c, [_d, _d, _i, _d, _c]),
+    ("sfm_f8_general", _c, [_d, _d, _i, _d, _c]),
+    ("sfm_ransac_f8", _c, [_d, _d, _i, _i32, _i, ctypes.c_double, _i32, _i64, _d, _u8, _c]),
+    ("sfm_triangulate_dlt", _c, [_d, _d, _d, _d, _i, _d, _c]),
+    ("sfm_project_points", _c, [_d, _d, _i, _d, _c]),
+    ("sfm_ba_residuals", _c, [ctypes.c_int32, _i, _i, _i32, _i32, _d, _d, _d, _d, _d, _c]),
+    ("sfm_ba_lm", _c, [ctypes.c_int32, _i, _i, _i32, _i32, _d, _d, _d, _d, ctypes.POINTER(BAOpts),
+                       ctypes.POINTER(BAReport), _c]),
+    ("sfm_comm_unique_id", _c, [ctypes.c_char_p]),
+    ("sfm_comm_init", _c, [ctypes.c_char_p, _c, _c, _c, ctypes.POINTER(ctypes.c_void_p)]),
+    ("sfm_comm_destroy", _c, [ctypes.c_void_p]),
+    ("sfm_ba_create", _c, [ctypes.c_int32, _i, _i, _i32, _i32, _d, _d, _d, _d, _c, ctypes.c_void_p,
+                           ctypes.POINTER(ctypes.c_void_p)]),
+    ("sfm_ba_solve", _c, [ctypes.c_void_p, ctypes.POINTER(BAOpts), ctypes.POINTER(BAReport)]),
+    ("sfm_ba_reset", _c, [ctypes.c_void_p]),
+    ("sfm_ba_download", _c, [ctypes.c_void_p, _d, _d]),
+    ("sfm_ba_kernel_times", _c, [ctypes.c_void_p, _d, _c, ctypes.c_char_p, _c]),
+    ("sfm_ba_destroy", _c, [ctypes.c_void_p]),
+]
+for _name, _res, _args in SIGNATURES:
+    _f = getattr(_lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+DEVICE = int(os.environ.get("SFM_DEVICE", "0"))
+
+
+def version():
+    return _lib.sfm_version()
+
+
+def device_count():
+    return _lib.sfm_device_count()
+
+
+def require_device():
+    if _lib.sfm_device_count() <= 0:
+        raise SfmCoreError("libsfmcore: no HIP device visible (the MI355X path has no CPU fallback)")
+
+
+def _check(rc):
+    if rc != 0:
+        raise SfmCoreError(f"libsfmcore error {rc}: {_lib.sfm_last_error().decode(errors='replace')}")
+
+
+def _p(a, t=_d):
+    return a.ctypes.data_as(t)
+
+
+def _f64(a, shape=None):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    if shape is not None:
+        a = a.reshape(shape)
+    return a
+
+
+def last_timings():
+    out = np.zeros(8)
+    n = _lib.sfm_last_timings(_p(out), 8)
+    return out[:n]
+
+
+# ------------------------------------------------------------------ random
+def sample_table(n, k, H):
+    """H draws of random.sample(range(n), k) on the GLOBAL random instance,
+    replayed natively; the global state is advanced exactly as the
+    reference's loop (GetInliersRANSAC.py:53-55) would advance it."""
+    version_, internal, gauss = random.getstate()
+    st = np.array(internal, dtype=np.uint32)
+    out = np.empty((H, k), dtype=np.int32)
+    _check(_lib.sfm_pyrandom_sample_table(_p(st, _u32), int(n), int(k), int(H), _p(out, _i32)))
+    random.setstate((version_, tuple(int(v) for v in st), gauss))
+    return out
+
+
+# --------------------------------------------------------------- geometry
+def f8_batch(x1s, x2s):
+    """H independent 8-point F estimates; x1s, x2s: (H, 8, 2)."""
+    require_device()
+    x1s, x2s = _f64(x1s), _f64(x2s)
+    H = x1s.shape[0]
+    F = np.zeros((H, 9))
+    _check(_lib.sfm_f8_batch(_p(x1s), _p(x2s), H, _p(F), DEVICE))
+    return F.reshape(H, 3, 3)
+
+
+def f8_general(x1, x2):
+    require_device()
+    x1, x2 = _f64(x1), _f64(x2)
+    F = np.zeros(9)
+    _check(_lib.sfm_f8_general(_p(x1), _p(x2), len(x1), _p(F), DEVICE))
+    return F.reshape(3, 3)
+
+
+def ransac_f8(x1, x2, samples, thr, want_counts=False):
+    """Returns (best_iter or -1, F_best (3,3) or None, mask (N,) bool, counts or None)."""
+    require_device()
+    x1, x2 = _f64(x1), _f64(x2)
+    samples = np.ascontiguousarray(samples, dtype=np.int32)
+    N, H = len(x1), len(samples)
+    counts = np.zeros(H, dtype=np.int32) if want_counts else None
+    best = np.zeros(1, dtype=np.int64)
+    F = np.zeros(9)
+    mask = np.zeros(N, dtype=np.uint8)
+    _check(_lib.sfm_ransac_f8(_p(x1), _p(x2), N, _p(samples, _i32), H, float(thr),
+                              _p(counts, _i32) if want_counts else None, _p(best, _i64), _p(F),
+                              _p(mask, _u8), DEVICE))
+    b = int(best[0])
+    if b < 0:
+        return -1, None, np.zeros(N, dtype=bool), counts
+    return b, F.reshape(3, 3), mask.astype(bool), counts
+
+
+def triangulate(P1, P2, x1, x2):
+    require_device()
+    P1, P2, x1, x2 = _f64(P1), _f64(P2), _f64(x1), _f64(x2)
+    X = np.zeros((len(x1), 3))
+    _check(_lib.sfm_triangulate_dlt(_p(P1), _p(P2), _p(x1), _p(x2), len(x1), _p(X), DEVICE))
+    return X
+
+
+def project(P, X):
+    require_device()
+    P, X = _f64(P), _f64(X)
+    out = np.zeros((len(X), 2))
+    _check(_lib.sfm_project_points(_p(P), _p(X), len(X), _p(out), DEVICE))
+    return out
+
+
+def ba_residuals(cams, pts, cam_idx, pt_idx, obs, K):
+    require_device()
+    cams, pts, obs, K = _f64(cams), _f64(pts), _f64(obs), _f64(K)
+    ci = np.ascontiguousarray(cam_idx, dtype=np.int32)
+    pi = np.ascontiguousarray(pt_idx, dtype=np.int32)
+    r = np.zeros(2 * len(ci))
+    _check(_lib.sfm_ba_residuals(len(cams), len(pts), len(ci), _p(ci, _i32), _p(pi, _i32), _p(obs), _p(K),
+                                 _p(cams), _p(pts), _p(r), DEVICE))
+    return r
+
+
+def ba_opts(max_iterations=100, fixed_iterations=False, function_tolerance=1e-10, gradient_tolerance=0.0,
+            parameter_tolerance=1e-12, initial_lambda=1e-4):
+    return BAOpts(int(max_iterations), int(bool(fixed_iterations)), function_tolerance, gradient_tolerance,
+                  parameter_tolerance, initial_lambda)
+
+
+def ba_lm(cams, pts, cam_idx, pt_idx, obs, K, **opts):
+    """Schur-complement LM on the GPU. Returns (cams, pts, report dict)."""
+    require_device()
+    cams, pts = _f64(cams).copy(), _f64(pts).copy()
+    obs, K = _f64(obs), _f64(K)
+    ci = np.ascontiguousarray(cam_idx, dtype=np.int32)
+    pi = np.ascontiguousarray(pt_idx, dtype=np.int32)
+    o, rep = ba_opts(**opts), BAReport()
+    _check(_lib.sfm_ba_lm(len(cams), len(pts), len(ci), _p(ci, _i32), _p(pi, _i32), _p(obs), _p(K), _p(cams),
+                          _p(pts), ctypes.byref(o), ctypes.byref(rep), DEVICE))
+    return cams, pts, rep.as_dict()
+
+
+class Comm:
+    """RCCL communicator for the multi-GPU BA (one process per GPU)."""
+
+    @staticmethod
+    def unique_id():
+        buf = ctypes.create_string_buffer(128)
+        _check(_lib.sfm_comm_unique_id(buf))
+        return buf.raw
+
+    def __init__(self, uid, nranks, rank, device=None):
+        require_device()
+        self.h = ctypes.c_void_p()
+        dev = DEVICE if device is None else device
+        _check(_lib.sfm_comm_init(ctypes.c_char_p(bytes(uid)), nranks, rank, dev, ctypes.byref(self.h)))
+
+    def close(self):
+        if self.h:
+            _lib.sfm_comm_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+
+class BAProblem:
+    """Device-resident BA problem (uploaded once, iterated many times)."""
+
+    def __init__(self, cams, pts, cam_idx, pt_idx, obs, K, comm=None, device=None):
+        require_device()
+        self.n_cams, self.n_pts = len(cams), len(pts)
+        cams, pts, obs, K = _f64(cams), _f64(pts), _f64(obs), _f64(K)
+        ci = np.ascontiguousarray(cam_idx, dtype=np.int32)
+        pi = np.ascontiguousarray(pt_idx, dtype=np.int32)
+        self.n_obs = len(ci)
+        self.h = ctypes.c_void_p()
+        dev = DEVICE if device is None else device
+        _check(_lib.sfm_ba_create(self.n_cams, self.n_pts, self.n_obs, _p(ci, _i32), _p(pi, _i32), _p(obs),
+                                  _p(K), _p(cams), _p(pts), dev, comm.h if comm is not None else None,
+                                  ctypes.byref(self.h)))
+
+    def solve(self, **opts):
+        o, rep = ba_opts(**opts), BAReport()
+        _check(_lib.sfm_ba_solve(self.h, ctypes.byref(o), ctypes.byref(rep)))
+        return rep.as_dict()
+
+    def reset(self):
+        _check(_lib.sfm_ba_reset(self.h))
+
+    def download(self):
+        cams = np.zeros((self.n_cams, 6))
+        pts = np.zeros((self.n_pts, 3))
+        _check(_lib.sfm_ba_download(self.h, _p(cams), _p(pts)))
+        return cams, pts
+
+    def kernel_times(self):
+        ms = np.zeros(16)
+        names = ctypes.create_string_buffer(512)
+        n = _lib.sfm_ba_kernel_times(self.h, _p(ms), 16, names, 512)
+        return dict(zip(names.value.decode().split(";"), ms[:n].tolist()))
+
+    def close(self):
+        if self.h:
+            _lib.sfm_ba_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,1047 @@
+// Sparse Schur-complement Levenberg-Marquardt bundle adjustment for gfx950.
+//
+// Replaces perform_bundle_adjustment's scipy least_squares(method='lm')
+// (BundleAdjustment.py:113-242) on the reference residual
+// (BundleAdjustment.py:43-110): r = obs - proj, proj = K(RX+t)[:2]/(K(RX+t)[2]+1e-8).
+//
+// One LM iteration = one damped solve + one trial evaluation:
+//   k_linearize      (after an accepted step) thread per point: residual,
+//                    analytic 2x6 / 2x3 Jacobians per observation -> J cache;
+//                    point block V = sum Jp^T Jp, g_p = sum Jp^T r.
+//   k_point_prep     thread per point: Vd = V + lambda*clamp(diag V) = C C^T,
+//                    L = C^-T (so Vd^-1 = L L^T), q = L^T g_p,
+//                    Z_o = (Jc^T Jp)_o L per observation.
+//   k_schur_blocks   workgroup per co-visible camera pair (i <= j):
+//                    S_ij = U_i [i==j] - sum_p Z_pi Z_pj^T over the points
+//                    both cameras see (static pair list, fixed order ->
+//                    deterministic, no atomics); diagonal blocks also reduce
+//                    U_i, g_i and sum Z q.
+//   [RCCL all-reduce of the packed partial system across ranks]
+//   k_assemble       S += lambda*clamp(diag U), b = -g_c + sum Z q, padded.
+//   k_chol_panel / k_chol_update / k_chol_solve
+//                    blocked right-looking fp64 Cholesky of the reduced
+//                    camera system + triangular solves.
+//   k_camera_trial   R' = exp([dtheta]x) R, t' = t + dt; camera part of the
+//                    model decrease.
+//   k_backsub_trial  thread per point: dp = L L^T(-g_p - sum W^T dc),
+//                    X' = X + dp, trial cost of its observations.
+//   k_finalize       fixed-order reduction of per-block partials.
+// The host reads 8 scalars per iteration and applies Nielsen's damping
+// update; on a rejected step only k_point_prep onwards is repeated.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <vector>
+
+#include "sfm_common.hpp"
+#include "sfm_geom.hpp"
+
+struct sfm_comm {
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0, device = 0;
+};
+
+namespace sfm {
+
+constexpr int NB = 32;            // Cholesky tile
+constexpr int PT_THREADS = 128;   // per-point kernels
+constexpr int SCHUR_THREADS = 256;
+
+__device__ __forceinline__ double clampd(double x) { return fmin(fmax(x, 1e-6), 1e32); }
+
+// ----------------------------------------------------------- reductions
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// block of PT_THREADS threads: reduce NV values, thread 0 writes out[0..NV)
+template <int NV>
+__device__ __forceinline__ void block_sum_store(double (&v)[NV], double *out) {
+    __shared__ double red[PT_THREADS / 64][NV];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const double s = wave_sum(v[k]);
+        if (lane == 0) red[w][k] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            double s = 0;
+            for (int i = 0; i < PT_THREADS / 64; ++i) s += red[i][k];
+            out[k] = s;
+        }
+    }
+}
+
+// ------------------------------------------------------ observation model
+// residual + Jacobians wrt (dtheta (left perturbation), t) and X.
+struct ObsLin {
+    double r[2], Jc[2][6], Jp[2][3];
+};
+
+__device__ __forceinline__ void linearize_obs(const double *__restrict__ Rt, const double *X,
+                                              const double (&K)[9], double2 ob, ObsLin &L) {
+    const double *R = Rt;
+    double p[3], u[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) p[i] = R[3 * i] * X[0] + R[3 * i + 1] * X[1] + R[3 * i + 2] * X[2];
+    const double xc0 = p[0] + Rt[9], xc1 = p[1] + Rt[10], xc2 = p[2] + Rt[11];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) u[i] = K[3 * i] * xc0 + K[3 * i + 1] * xc1 + K[3 * i + 2] * xc2;
+    const double iw = 1.0 / (u[2] + 1e-8);
+    const double pu = u[0] * iw, pv = u[1] * iw;
+    L.r[0] = ob.x - pu;
+    L.r[1] = ob.y - pv;
+    double A[2][3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        A[0][c] = -(iw * K[c] - pu * iw * K[6 + c]);
+        A[1][c] = -(iw * K[3 + c] - pv * iw * K[6 + c]);
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        L.Jc[a][0] = A[a][1] * (-p[2]) + A[a][2] * p[1];
+        L.Jc[a][1] = A[a][0] * p[2] + A[a][2] * (-p[0]);
+        L.Jc[a][2] = A[a][0] * (-p[1]) + A[a][1] * p[0];
+        L.Jc[a][3] = A[a][0];
+        L.Jc[a][4] = A[a][1];
+        L.Jc[a][5] = A[a][2];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) L.Jp[a][c] = A[a][0] * R[c] + A[a][1] * R[3 + c] + A[a][2] * R[6 + c];
+    }
+}
+
+__device__ __forceinline__ double obs_cost(const double *__restrict__ Rt, const double *X, const double (&K)[9],
+                                           double2 ob) {
+    double xc[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) xc[i] = Rt[3 * i] * X[0] + Rt[3 * i + 1] * X[1] + Rt[3 * i + 2] * X[2] + Rt[9 + i];
+    double u[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) u[i] = K[3 * i] * xc[0] + K[3 * i + 1] * xc[1] + K[3 * i + 2] * xc[2];
+    const double iw = 1.0 / (u[2] + 1e-8);
+    const double r0 = ob.x - u[0] * iw, r1 = ob.y - u[1] * iw;
+    return 0.5 * (r0 * r0 + r1 * r1);
+}
+
+struct Kmat {
+    double k[9];
+};
+
+// J cache layout per observation (20 doubles): r0 r1 | Jc row0 (6) | Jc row1 (6) | Jp row0 (3) | Jp row1 (3)
+constexpr int JS = 20;
+
+__global__ void __launch_bounds__(PT_THREADS) k_linearize(int64_t np_, const int32_t *__restrict__ pstart,
+                                                          const int32_t *__restrict__ cam,
+                                                          const double2 *__restrict__ obs, Kmat Km,
+                                                          const double *__restrict__ Rt,
+                                                          const double *__restrict__ X, double *__restrict__ J,
+                                                          double *__restrict__ Vg, double *__restrict__ partial) {
+    const int64_t p = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x;
+    double K[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) K[i] = Km.k[i];
+    double acc[1] = {0.0};
+    if (p < np_) {
+        double x[3] = {X[3 * p], X[3 * p + 1], X[3 * p + 2]};
+        double V[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+        for (int32_t o = pstart[p]; o < pstart[p + 1]; ++o) {
+            ObsLin L;
+            linearize_obs(Rt + 12 * cam[o], x, K, obs[o], L);
+            double *j = J + (int64_t)JS * o;
+            j[0] = L.r[0]; j[1] = L.r[1];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) { j[2 + i] = L.Jc[0][i]; j[8 + i] = L.Jc[1][i]; }
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { j[14 + i] = L.Jp[0][i]; j[17 + i] = L.Jp[1][i]; }
+            acc[0] += 0.5 * (L.r[0] * L.r[0] + L.r[1] * L.r[1]);
+            V[0] += L.Jp[0][0] * L.Jp[0][0] + L.Jp[1][0] * L.Jp[1][0];
+            V[1] += L.Jp[0][0] * L.Jp[0][1] + L.Jp[1][0] * L.Jp[1][1];
+            V[2] += L.Jp[0][0] * L.Jp[0][2] + L.Jp[1][0] * L.Jp[1][2];
+            V[3] += L.Jp[0][1] * L.Jp[0][1] + L.Jp[1][1] * L.Jp[1][1];
+            V[4] += L.Jp[0][1] * L.Jp[0][2] + L.Jp[1][1] * L.Jp[1][2];
+            V[5] += L.Jp[0][2] * L.Jp[0][2] + L.Jp[1][2] * L.Jp[1][2];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) g[i] += L.Jp[0][i] * L.r[0] + L.Jp[1][i] * L.r[1];
+        }
+        double *vg = Vg + 9 * p;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) vg[i] = V[i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) vg[6 + i] = g[i];
+    }
+    block_sum_store<1>(acc, partial + blockIdx.x);
+}
+
+// Lq layout per point (9 doubles): L00 L01 L02 L11 L12 L22 | q0 q1 q2
+__global__ void __launch_bounds__(PT_THREADS) k_point_prep(int64_t np_, const int32_t *__restrict__ pstart,
+                                                           const double *__restrict__ J,
+                                                           const double *__restrict__ Vg, double lambda,
+                                                           double *__restrict__ Lq, double *__restrict__ Z) {
+    const int64_t p = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x;
+    if (p >= np_) return;
+    const double *vg = Vg + 9 * p;
+    const double v00 = vg[0] + lambda * clampd(vg[0]), v01 = vg[1], v02 = vg[2];
+    const double v11 = vg[3] + lambda * clampd(vg[3]), v12 = vg[4];
+    const double v22 = vg[5] + lambda * clampd(vg[5]);
+    const double c00 = sqrt(v00), c10 = v01 / c00, c20 = v02 / c00;
+    const double c11 = sqrt(v11 - c10 * c10), c21 = (v12 - c20 * c10) / c11;
+    const double c22 = sqrt(v22 - c20 * c20 - c21 * c21);
+    const double i00 = 1.0 / c00, i11 = 1.0 / c11, i22 = 1.0 / c22;
+    const double i10 = -c10 * i00 * i11;
+    const double i21 = -c21 * i11 * i22;
+    const double i20 = -(c20 * i00 + c21 * i10) * i22;
+    // L = Cinv^T (upper)
+    const double L00 = i00, L01 = i10, L02 = i20, L11 = i11, L12 = i21, L22 = i22;
+    const double g0 = vg[6], g1 = vg[7], g2 = vg[8];
+    double *lq = Lq + 9 * p;
+    lq[0] = L00; lq[1] = L01; lq[2] = L02; lq[3] = L11; lq[4] = L12; lq[5] = L22;
+    lq[6] = L00 * g0;
+    lq[7] = L01 * g0 + L11 * g1;
+    lq[8] = L02 * g0 + L12 * g1 + L22 * g2;
+    for (int32_t o = pstart[p]; o < pstart[p + 1]; ++o) {
+        const double *j = J + (int64_t)JS * o;
+        double *z = Z + (int64_t)18 * o;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const double a0 = j[2 + i], a1 = j[8 + i];
+            const double w0 = a0 * j[14] + a1 * j[17];
+            const double w1 = a0 * j[15] + a1 * j[18];
+            const double w2 = a0 * j[16] + a1 * j[19];
+            z[3 * i + 0] = w0 * L00;
+            z[3 * i + 1] = w0 * L01 + w1 * L11;
+            z[3 * i + 2] = w0 * L02 + w1 * L12 + w2 * L22;
+        }
+    }
+}
+
+// Payload layout (doubles): S[ns*ns] | diagU[ns] | gc[ns] | bZ[ns] | cost
+__global__ void __launch_bounds__(SCHUR_THREADS) k_schur_blocks(
+    int32_t ns, const int2 *__restrict__ blk_ij, const int32_t *__restrict__ bstart, const int2 *__restrict__ pairs,
+    const int32_t *__restrict__ pt, const double *__restrict__ J, const double *__restrict__ Z,
+    const double *__restrict__ Lq, double *__restrict__ payload) {
+    __shared__ double red[SCHUR_THREADS / 64][36 + 21 + 12];
+    const int b = blockIdx.x;
+    const int2 ij = blk_ij[b];
+    const bool diag = ij.x == ij.y;
+    const int32_t k0 = bstart[b], k1 = bstart[b + 1];
+    double acc[36];
+#pragma unroll
+    for (int k = 0; k < 36; ++k) acc[k] = 0.0;
+    double U[21], g[6], bz[6];
+#pragma unroll
+    for (int k = 0; k < 21; ++k) U[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { g[k] = 0.0; bz[k] = 0.0; }
+    for (int32_t k = k0 + threadIdx.x; k < k1; k += SCHUR_THREADS) {
+        const int2 pr = pairs[k];
+        const double *za = Z + (int64_t)18 * pr.x;
+        const double *zb = Z + (int64_t)18 * pr.y;
+        double a[18], c[18];
+#pragma unroll
+        for (int i = 0; i < 18; ++i) { a[i] = za[i]; c[i] = zb[i]; }
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int s = 0; s < 6; ++s)
+                acc[6 * r + s] += a[3 * r] * c[3 * s] + a[3 * r + 1] * c[3 * s + 1] + a[3 * r + 2] * c[3 * s + 2];
+        if (diag) {
+            const double *j = J + (int64_t)JS * pr.x;
+            const double *lq = Lq + 9 * (int64_t)pt[pr.x];
+            const double q0 = lq[6], q1 = lq[7], q2 = lq[8];
+            int u = 0;
+#pragma unroll
+            for (int r = 0; r < 6; ++r) {
+#pragma unroll
+                for (int s = r; s < 6; ++s) U[u++] += j[2 + r] * j[2 + s] + j[8 + r] * j[8 + s];
+                g[r] += j[2 + r] * j[0] + j[8 + r] * j[1];
+                bz[r] += a[3 * r] * q0 + a[3 * r + 1] * q1 + a[3 * r + 2] * q2;
+            }
+        }
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 36; ++k) {
+        const double s = wave_sum(acc[k]);
+        if (lane == 0) red[w][k] = s;
+    }
+    if (diag) {
+#pragma unroll
+        for (int k = 0; k < 21; ++k) {
+            const double s = wave_sum(U[k]);
+            if (lane == 0) red[w][36 + k] = s;
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const double s1 = wave_sum(g[k]), s2 = wave_sum(bz[k]);
+            if (lane == 0) { red[w][57 + k] = s1; red[w][63 + k] = s2; }
+        }
+    }
+    __syncthreads();
+    const int nv = diag ? 69 : 36;
+    for (int k = threadIdx.x; k < nv; k += SCHUR_THREADS) {
+        double s = 0;
+        for (int i = 0; i < SCHUR_THREADS / 64; ++i) s += red[i][k];
+        red[0][k] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < 36) {
+        const int r = threadIdx.x / 6, s = threadIdx.x % 6;
+        double v = -red[0][threadIdx.x];
+        if (diag) {
+            const int lo = r < s ? r : s, hi = r < s ? s : r;
+            const int ui = lo * 6 - lo * (lo - 1) / 2 + (hi - lo);
+            v += red[0][36 + ui];
+        }
+        const int64_t row = 6 * ij.x + r, col = 6 * ij.y + s;
+        payload[row * ns + col] = v;
+        if (!diag) payload[col * ns + row] = v;
+    }
+    if (diag && threadIdx.x < 6) {
+        const int r = threadIdx.x;
+        const int ui = r * 6 - r * (r - 1) / 2;
+        const int64_t base = (int64_t)ns * ns;
+        payload[base + 6 * ij.x + r] = red[0][36 + ui];
+        payload[base + ns + 6 * ij.x + r] = red[0][57 + r];
+        payload[base + 2 * ns + 6 * ij.x + r] = red[0][63 + r];
+    }
+}
+
+// A (nsp x nsp, padded with identity), bvec (nsp)
+__global__ void k_assemble(int32_t ns, int32_t nsp, const double *__restrict__ payload, double lambda,
+                           double *__restrict__ A, double *__restrict__ bvec) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)nsp * nsp) return;
+    const int r = (int)(idx / nsp), c = (int)(idx % nsp);
+    double v;
+    if (r < ns && c < ns) {
+        v = payload[(int64_t)r * ns + c];
+        if (r == c) v += lambda * clampd(payload[(int64_t)ns * ns + r]);
+    } else {
+        v = (r == c) ? 1.0 : 0.0;
+    }
+    A[idx] = v;
+    if (c == 0) {
+        const int64_t base = (int64_t)ns * ns;
+        bvec[r] = r < ns ? -payload[base + ns + r] + payload[base + 2 * ns + r] : 0.0;
+    }
+}
+
+// --------------------------------------------------------------- Cholesky
+// factor the NB x NB tile T (LDS, row-major) in place: lower triangle = L.
+__device__ void chol_tile(double (&T)[NB][NB + 1], int *bad) {
+    for (int k = 0; k < NB; ++k) {
+        if (threadIdx.x == 0) {
+            const double d = T[k][k];
+            if (!(d > 0.0)) *bad = 1;
+            T[k][k] = sqrt(d);
+        }
+        __syncthreads();
+        const double dk = T[k][k];
+        for (int i = k + 1 + threadIdx.x; i < NB; i += blockDim.x) T[i][k] /= dk;
+        __syncthreads();
+        for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+            const int i = e / NB, j = e % NB;
+            if (i > k && j > k && j <= i) T[i][j] -= T[i][k] * T[j][k];
+        }
+        __syncthreads();
+    }
+}
+
+// grid = nT - kt workgroups; workgroup w factors diag tile kt (redundantly)
+// and, for w > 0, solves tile row kt + w: L_rk = A_rk L_kk^-T.
+// A is read-only here (every workgroup re-factors A_kk); workgroup 0 puts
+// L_kk in the scratch tile D, which k_chol_update copies back into A.
+__global__ void __launch_bounds__(256) k_chol_panel(double *__restrict__ A, int32_t nsp, int kt,
+                                                    double *__restrict__ D, int *__restrict__ bad) {
+    __shared__ double T[NB][NB + 1];
+    __shared__ double B[NB][NB + 1];
+    const int k0 = kt * NB;
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+        const int i = e / NB, j = e % NB;
+        T[i][j] = A[(int64_t)(k0 + i) * nsp + k0 + j];
+    }
+    __syncthreads();
+    chol_tile(T, bad);
+    if (blockIdx.x == 0) {
+        for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+            const int i = e / NB, j = e % NB;
+            D[e] = j <= i ? T[i][j] : 0.0;
+        }
+        return;
+    }
+    const int r0 = (kt + blockIdx.x) * NB;
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+        const int i = e / NB, j = e % NB;
+        B[i][j] = A[(int64_t)(r0 + i) * nsp + k0 + j];
+    }
+    __syncthreads();
+    // row i of X solves X L^T = B  <=>  for j: X[i][j] = (B[i][j] - sum_{m<j} X[i][m] L[j][m]) / L[j][j]
+    if (threadIdx.x < NB) {
+        const int i = threadIdx.x;
+        for (int j = 0; j < NB; ++j) {
+            double v = B[i][j];
+            for (int m = 0; m < j; ++m) v -= B[i][m] * T[j][m];
+            B[i][j] = v / T[j][j];
+        }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+        const int i = e / NB, j = e % NB;
+        A[(int64_t)(r0 + i) * nsp + k0 + j] = B[i][j];
+    }
+}
+
+// block 0 stores L_kk from the scratch tile; blocks 1.. do the trailing
+// update of tile (r, c), kt < c <= r: A_rc -= L_rk L_ck^T
+__global__ void __launch_bounds__(256) k_chol_update(double *__restrict__ A, int32_t nsp, int kt,
+                                                     const double *__restrict__ D) {
+    __shared__ double Lr[NB][NB + 1];
+    __shared__ double Lc[NB][NB + 1];
+    if (blockIdx.x == 0) {
+        const int k0 = kt * NB;
+        for (int e = threadIdx.x; e < NB * NB; e += blockDim.x)
+            A[(int64_t)(k0 + e / NB) * nsp + k0 + e % NB] = D[e];
+        return;
+    }
+    // decode linear block index into (r, c) with c <= r, offsets from kt+1
+    int t = blockIdx.x - 1, r = 0;
+    while (t > r) { t -= r + 1; ++r; }
+    const int c = t;
+    const int rr = (kt + 1 + r) * NB, cc = (kt + 1 + c) * NB, k0 = kt * NB;
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+        const int i = e / NB, j = e % NB;
+        Lr[i][j] = A[(int64_t)(rr + i) * nsp + k0 + j];
+        Lc[i][j] = A[(int64_t)(cc + i) * nsp + k0 + j];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+        const int i = e / NB, j = e % NB;
+        double s = 0;
+#pragma unroll 8
+        for (int m = 0; m < NB; ++m) s += Lr[i][m] * Lc[j][m];
+        A[(int64_t)(rr + i) * nsp + cc + j] -= s;
+    }
+}
+
+// forward / backward substitution with the factor (lower triangle of A).
+__global__ void __launch_bounds__(256) k_chol_solve(const double *__restrict__ A, int32_t nsp,
+                                                    double *__restrict__ x) {
+    __shared__ double part[256];
+    const int nT = nsp / NB;
+    // forward: L y = b
+    for (int kt = 0; kt < nT; ++kt) {
+        const int k0 = kt * NB;
+        // subtract contributions of solved tiles: rows k0..k0+NB, cols 0..k0
+        {
+            const int row = threadIdx.x % NB, sl = threadIdx.x / NB;  // 8 slices
+            double s = 0;
+            for (int m = sl; m < k0; m += 256 / NB) s += A[(int64_t)(k0 + row) * nsp + m] * x[m];
+            part[threadIdx.x] = s;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int i = 0; i < NB; ++i) {
+                double v = x[k0 + i];
+                for (int sl = 0; sl < 256 / NB; ++sl) v -= part[sl * NB + i];
+                for (int m = 0; m < i; ++m) v -= A[(int64_t)(k0 + i) * nsp + k0 + m] * x[k0 + m];
+                x[k0 + i] = v / A[(int64_t)(k0 + i) * nsp + k0 + i];
+            }
+        }
+        __syncthreads();
+    }
+    // backward: L^T x = y
+    for (int kt = nT - 1; kt >= 0; --kt) {
+        const int k0 = kt * NB;
+        {
+            const int row = threadIdx.x % NB, sl = threadIdx.x / NB;
+            double s = 0;
+            for (int m = k0 + NB + sl; m < nsp; m += 256 / NB) s += A[(int64_t)m * nsp + k0 + row] * x[m];
+            part[threadIdx.x] = s;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int i = NB - 1; i >= 0; --i) {
+                double v = x[k0 + i];
+                for (int sl = 0; sl < 256 / NB; ++sl) v -= part[sl * NB + i];
+                for (int m = i + 1; m < NB; ++m) v -= A[(int64_t)(k0 + m) * nsp + k0 + i] * x[k0 + m];
+                x[k0 + i] = v / A[(int64_t)(k0 + i) * nsp + k0 + i];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// one workgroup: trial cameras + camera part of model decrease / norms.
+// cam_out[0..3) = {model_c, |dc|^2, |t|^2}
+__global__ void __launch_bounds__(256) k_camera_trial(int32_t nc, const double *__restrict__ dc,
+                                                      const double *__restrict__ payload, int32_t ns, double lambda,
+                                                      const double *__restrict__ Rt, double *__restrict__ Rt_new,
+                                                      double *__restrict__ cam_out) {
+    __shared__ double red[3][256];
+    double m = 0, dn = 0, xn = 0;
+    const double *diagU = payload + (int64_t)ns * ns, *gc = diagU + ns;
+    for (int c = threadIdx.x; c < nc; c += blockDim.x) {
+        const double *d = dc + 6 * c;
+        double dR[9];
+        rotvec_to_R(d[0], d[1], d[2], dR);
+        const double *R = Rt + 12 * c;
+        double *Rn = Rt_new + 12 * c;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) Rn[3 * i + j] = dR[3 * i] * R[j] + dR[3 * i + 1] * R[3 + j] + dR[3 * i + 2] * R[6 + j];
+        for (int i = 0; i < 3; ++i) {
+            Rn[9 + i] = R[9 + i] + d[3 + i];
+            xn += R[9 + i] * R[9 + i];
+        }
+        for (int i = 0; i < 6; ++i) {
+            m += d[i] * (lambda * clampd(diagU[6 * c + i]) * d[i] - gc[6 * c + i]);
+            dn += d[i] * d[i];
+        }
+    }
+    red[0][threadIdx.x] = m; red[1][threadIdx.x] = dn; red[2][threadIdx.x] = xn;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s)
+            for (int k = 0; k < 3; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x < 3) cam_out[threadIdx.x] = red[threadIdx.x][0];
+}
+
+// partial[block][4] = {trial cost, model_p, |dp|^2, |X|^2}
+__global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const int32_t *__restrict__ pstart,
+                                                              const int32_t *__restrict__ cam,
+                                                              const double2 *__restrict__ obs, Kmat Km,
+                                                              const double *__restrict__ J,
+                                                              const double *__restrict__ Vg,
+                                                              const double *__restrict__ Lq,
+                                                              const double *__restrict__ dc, double lambda,
+                                                              const double *__restrict__ Rt_new,
+                                                              const double *__restrict__ X,
+                                                              double *__restrict__ X_new, double *__restrict__ partial) {
+    const int64_t p = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x;
+    double K[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) K[i] = Km.k[i];
+    double acc[4] = {0, 0, 0, 0};
+    if (p < np_) {
+        const double *vg = Vg + 9 * p;
+        double rhs[3] = {-vg[6], -vg[7], -vg[8]};
+        const int32_t o0 = pstart[p], o1 = pstart[p + 1];
+        for (int32_t o = o0; o < o1; ++o) {
+            const double *j = J + (int64_t)JS * o;
+            const double *d = dc + 6 * cam[o];
+            double s0 = 0, s1 = 0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) { s0 += j[2 + i] * d[i]; s1 += j[8 + i] * d[i]; }
+#pragma unroll
+            for (int i = 0; i < 3; ++i) rhs[i] -= j[14 + i] * s0 + j[17 + i] * s1;
+        }
+        const double *l = Lq + 9 * p;  // L upper: 00 01 02 11 12 22
+        // y = L^T rhs ; dp = L y
+        const double y0 = l[0] * rhs[0];
+        const double y1 = l[1] * rhs[0] + l[3] * rhs[1];
+        const double y2 = l[2] * rhs[0] + l[4] * rhs[1] + l[5] * rhs[2];
+        const double dp[3] = {l[0] * y0 + l[1] * y1 + l[2] * y2, l[3] * y1 + l[4] * y2, l[5] * y2};
+        const double x[3] = {X[3 * p], X[3 * p + 1], X[3 * p + 2]};
+        double xn[3];
+        const double dg[3] = {vg[0], vg[3], vg[5]};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            xn[i] = x[i] + dp[i];
+            X_new[3 * p + i] = xn[i];
+            acc[1] += dp[i] * (lambda * clampd(dg[i]) * dp[i] - vg[6 + i]);
+            acc[2] += dp[i] * dp[i];
+            acc[3] += x[i] * x[i];
+        }
+        for (int32_t o = o0; o < o1; ++o) acc[0] += obs_cost(Rt_new + 12 * cam[o], xn, K, obs[o]);
+    }
+    block_sum_store<4>(acc, partial + 4 * (int64_t)blockIdx.x);
+}
+
+// fixed-order sum of nblk partials of width w into out[0..w)
+__global__ void __launch_bounds__(256) k_finalize(const double *__restrict__ partial, int nblk, int w,
+                                                  double *__restrict__ out) {
+    __shared__ double red[256];
+    for (int k = 0; k < w; ++k) {
+        double s = 0;
+        for (int b = threadIdx.x; b < nblk; b += 256) s += partial[(int64_t)b * w + k];
+        red[threadIdx.x] = s;
+        __syncthreads();
+        for (int st = 128; st > 0; st >>= 1) {
+            if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) out[k] = red[0];
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- host math
+static void h_rotvec_to_R(const double *w, double *R) {
+    double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    double th = std::sqrt(th2), a, b;
+    if (th < 1e-6) {
+        a = 1.0 - th2 / 6.0 + th2 * th2 / 120.0;
+        b = 0.5 - th2 / 24.0 + th2 * th2 / 720.0;
+    } else {
+        a = std::sin(th) / th;
+        b = (1.0 - std::cos(th)) / th2;
+    }
+    double x = w[0], y = w[1], z = w[2];
+    R[0] = 1.0 - b * (y * y + z * z); R[1] = -a * z + b * x * y;       R[2] = a * y + b * x * z;
+    R[3] = a * z + b * x * y;         R[4] = 1.0 - b * (x * x + z * z); R[5] = -a * x + b * y * z;
+    R[6] = -a * y + b * x * z;        R[7] = a * x + b * y * z;         R[8] = 1.0 - b * (x * x + y * y);
+}
+
+// scipy Rotation.from_matrix(R).as_rotvec() (quaternion route, w >= 0)
+static void h_R_to_rotvec(const double *R, double *w) {
+    double tr = R[0] + R[4] + R[8], q[4];
+    if (tr > R[0] && tr > R[4] && tr > R[8]) {
+        q[3] = 1.0 + tr;
+        q[0] = R[7] - R[5]; q[1] = R[2] - R[6]; q[2] = R[3] - R[1];
+    } else {
+        int i = (R[0] >= R[4] && R[0] >= R[8]) ? 0 : (R[4] >= R[8] ? 1 : 2);
+        int j = (i + 1) % 3, k = (j + 1) % 3;
+        q[i] = 1.0 - tr + 2.0 * R[i * 4];
+        q[j] = R[j * 3 + i] + R[i * 3 + j];
+        q[k] = R[k * 3 + i] + R[i * 3 + k];
+        q[3] = R[k * 3 + j] - R[j * 3 + k];
+    }
+    double nq = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    for (double &v : q) v /= nq;
+    if (q[3] < 0)
+        for (double &v : q) v = -v;
+    double vn = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2]);
+    double ang = 2.0 * std::atan2(vn, q[3]);
+    double sc = ang <= 1e-3 ? 2.0 + ang * ang / 12.0 + 7.0 * ang * ang * ang * ang / 2880.0 : ang / std::sin(ang / 2.0);
+    w[0] = sc * q[0]; w[1] = sc * q[1]; w[2] = sc * q[2];
+}
+
+}  // namespace sfm
+
+using namespace sfm;
+
+// ------------------------------------------------------------ problem
+enum { T_LIN, T_PREP, T_SCHUR, T_COMM, T_SOLVE, T_TRIAL, T_NT };
+static const char *kTimerNames = "linearize;point_prep;schur_blocks;allreduce;cholesky;backsub_trial";
+
+struct sfm_ba_problem {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    sfm_comm *comm = nullptr;
+    int32_t nc = 0, ns = 0, nsp = 0, nT = 0;
+    int64_t np = 0, no = 0, npairs = 0;
+    int32_t nblocks = 0;
+    Kmat K;
+    std::vector<double> cams0, pts0;
+    // device
+    int32_t *d_cam = nullptr, *d_pt = nullptr, *d_pstart = nullptr, *d_bstart = nullptr;
+    int2 *d_blk = nullptr, *d_pairs = nullptr;
+    double2 *d_obs = nullptr;
+    double *d_Rt = nullptr, *d_Rt2 = nullptr, *d_X = nullptr, *d_X2 = nullptr;
+    double *d_J = nullptr, *d_Vg = nullptr, *d_Lq = nullptr, *d_Z = nullptr;
+    double *d_payload = nullptr, *d_A = nullptr, *d_b = nullptr, *d_D = nullptr;
+    double *d_partial = nullptr, *d_scal = nullptr;
+    int *d_bad = nullptr;
+    double *h_scal = nullptr;  // pinned
+    int64_t payload_len = 0;
+    int pt_blocks = 0;
+    hipEvent_t ev[2 * T_NT] = {};
+    double t_acc[T_NT] = {};
+    int t_iters = 0;
+    std::vector<void *> allocs;
+    ~sfm_ba_problem() {
+        (void)hipSetDevice(device);
+        for (void *p : allocs) (void)hipFree(p);
+        if (h_scal) (void)hipHostFree(h_scal);
+        for (auto &e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+    template <class T> int alloc(T *&p, int64_t n) {
+        void *q = nullptr;
+        size_t bytes = (size_t)std::max<int64_t>(n, 1) * sizeof(T);
+        if (hipMalloc(&q, bytes) != hipSuccess) {
+            set_error("hipMalloc(%zu) failed", bytes);
+            return SFM_ERR_NOMEM;
+        }
+        allocs.push_back(q);
+        p = reinterpret_cast<T *>(q);
+        return 0;
+    }
+};
+
+static int upload_state(sfm_ba_problem *p) {
+    std::vector<double> Rt(12 * (size_t)p->nc);
+    for (int c = 0; c < p->nc; ++c) {
+        h_rotvec_to_R(&p->cams0[6 * c], &Rt[12 * c]);
+        for (int i = 0; i < 3; ++i) Rt[12 * c + 9 + i] = p->cams0[6 * c + 3 + i];
+    }
+    SFM_HIP(hipMemcpyAsync(p->d_Rt, Rt.data(), Rt.size() * 8, hipMemcpyHostToDevice, p->stream));
+    SFM_HIP(hipMemcpyAsync(p->d_X, p->pts0.data(), p->pts0.size() * 8, hipMemcpyHostToDevice, p->stream));
+    SFM_HIP(hipStreamSynchronize(p->stream));
+    return 0;
+}
+
+extern "C" int sfm_comm_unique_id(char out[128]) {
+    SFM_CHECK_ARG(out, "null pointer");
+    static_assert(sizeof(ncclUniqueId) <= 128, "unique id size");
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) {
+        set_error("ncclGetUniqueId failed");
+        return SFM_ERR_COMM;
+    }
+    std::memset(out, 0, 128);
+    std::memcpy(out, &id, sizeof id);
+    return 0;
+}
+
+extern "C" int sfm_comm_init(const char id[128], int nranks, int rank, int device, sfm_comm **out) {
+    SFM_CHECK_ARG(id && out && nranks >= 1 && rank >= 0 && rank < nranks, "bad communicator arguments");
+    SFM_HIP(hipSetDevice(device));
+    auto *c = new sfm_comm();
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof uid);
+    ncclResult_t r = ncclCommInitRank(&c->comm, nranks, uid, rank);
+    if (r != ncclSuccess) {
+        set_error("ncclCommInitRank: %s", ncclGetErrorString(r));
+        delete c;
+        return SFM_ERR_COMM;
+    }
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = device;
+    *out = c;
+    return 0;
+}
+
+extern "C" int sfm_comm_destroy(sfm_comm *c) {
+    if (!c) return 0;
+    if (c->comm) ncclCommDestroy(c->comm);
+    delete c;
+    return 0;
+}
+
+extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt,
+                             const double *obs, const double *K, const double *cams, const double *pts, int device,
+                             sfm_comm *comm, sfm_ba_problem **out) {
+    SFM_CHECK_ARG(out && K && cams && (pts || np_ == 0) && (no == 0 || (cam && pt && obs)), "null pointer");
+    SFM_CHECK_ARG(nc >= 1 && np_ >= 0 && no >= 0, "bad sizes");
+    SFM_CHECK_ARG(no < ((int64_t)1 << 31) && nc <= 8192, "problem too large for int32 indexing");
+    for (int64_t o = 0; o < no; ++o) {
+        SFM_CHECK_ARG(cam[o] >= 0 && cam[o] < nc && pt[o] >= 0 && pt[o] < np_, "observation index out of range");
+        SFM_CHECK_ARG(o == 0 || pt[o] >= pt[o - 1], "observations must be point-major (sorted by point)");
+    }
+    SFM_HIP(hipSetDevice(device));
+    auto p = std::make_unique<sfm_ba_problem>();
+    p->device = device;
+    p->comm = comm;
+    p->nc = nc;
+    p->np = np_;
+    p->no = no;
+    p->ns = 6 * nc;
+    p->nT = (p->ns + NB - 1) / NB;
+    p->nsp = p->nT * NB;
+    std::memcpy(p->K.k, K, sizeof p->K.k);
+    p->cams0.assign(cams, cams + 6 * (size_t)nc);
+    p->pts0.assign(pts, pts + 3 * (size_t)np_);
+    SFM_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+    for (auto &e : p->ev) SFM_HIP(hipEventCreate(&e));
+    // point CSR
+    std::vector<int32_t> pstart(np_ + 1, 0);
+    for (int64_t o = 0; o < no; ++o) pstart[pt[o] + 1]++;
+    for (int64_t i = 0; i < np_; ++i) pstart[i + 1] += pstart[i];
+    // camera-pair lists (static sparsity of the reduced camera system)
+    std::vector<int64_t> cnt((size_t)nc * nc, 0);
+    for (int64_t i = 0; i < np_; ++i)
+        for (int32_t a = pstart[i]; a < pstart[i + 1]; ++a)
+            for (int32_t b = a; b < pstart[i + 1]; ++b) {
+                int ci = cam[a], cj = cam[b];
+                if (ci > cj) std::swap(ci, cj);
+                SFM_CHECK_ARG(a == b || cam[a] != cam[b], "a point is observed twice by the same camera");
+                cnt[(size_t)ci * nc + cj]++;
+            }
+    std::vector<int2> blk;
+    std::vector<int32_t> bstart(1, 0);
+    std::vector<int64_t> boff((size_t)nc * nc, -1);
+    int64_t tot = 0;
+    for (int i = 0; i < nc; ++i)
+        for (int j = i; j < nc; ++j)
+            if (cnt[(size_t)i * nc + j] > 0) {
+                boff[(size_t)i * nc + j] = tot;
+                tot += cnt[(size_t)i * nc + j];
+                blk.push_back(make_int2(i, j));
+                bstart.push_back((int32_t)tot);
+            }
+    SFM_CHECK_ARG(tot < ((int64_t)1 << 31), "too many co-observation pairs");
+    std::vector<int2> pairs(tot);
+    for (int64_t i = 0; i < np_; ++i)
+        for (int32_t a = pstart[i]; a < pstart[i + 1]; ++a)
+            for (int32_t b = a; b < pstart[i + 1]; ++b) {
+                int32_t oa = a, ob = b;
+                if (cam[oa] > cam[ob]) std::swap(oa, ob);
+                pairs[boff[(size_t)cam[oa] * nc + cam[ob]]++] = make_int2(oa, ob);
+            }
+    p->npairs = tot;
+    p->nblocks = (int32_t)blk.size();
+    p->pt_blocks = std::max(1, ceil_div(np_, PT_THREADS));
+    p->payload_len = (int64_t)p->ns * p->ns + 3 * p->ns + 1;
+    int rc;
+    if ((rc = p->alloc(p->d_cam, no)) || (rc = p->alloc(p->d_pt, no)) || (rc = p->alloc(p->d_pstart, np_ + 1)) ||
+        (rc = p->alloc(p->d_obs, no)) || (rc = p->alloc(p->d_blk, p->nblocks)) ||
+        (rc = p->alloc(p->d_bstart, p->nblocks + 1)) || (rc = p->alloc(p->d_pairs, tot)) ||
+        (rc = p->alloc(p->d_Rt, 12 * (int64_t)nc)) || (rc = p->alloc(p->d_Rt2, 12 * (int64_t)nc)) ||
+        (rc = p->alloc(p->d_X, 3 * np_)) || (rc = p->alloc(p->d_X2, 3 * np_)) ||
+        (rc = p->alloc(p->d_J, JS * no)) || (rc = p->alloc(p->d_Vg, 9 * np_)) || (rc = p->alloc(p->d_Lq, 9 * np_)) ||
+        (rc = p->alloc(p->d_Z, 18 * no)) || (rc = p->alloc(p->d_payload, p->payload_len + 8)) ||
+        (rc = p->alloc(p->d_A, (int64_t)p->nsp * p->nsp)) || (rc = p->alloc(p->d_b, p->nsp)) ||
+        (rc = p->alloc(p->d_D, NB * NB)) ||
+        (rc = p->alloc(p->d_partial, 4 * (int64_t)p->pt_blocks)) || (rc = p->alloc(p->d_scal, 16)) ||
+        (rc = p->alloc(p->d_bad, 4)))
+        return rc;
+    SFM_HIP(hipHostMalloc((void **)&p->h_scal, 16 * sizeof(double)));
+    hipStream_t s = p->stream;
+    if (no) {
+        SFM_HIP(hipMemcpyAsync(p->d_cam, cam, no * 4, hipMemcpyHostToDevice, s));
+        SFM_HIP(hipMemcpyAsync(p->d_pt, pt, no * 4, hipMemcpyHostToDevice, s));
+        SFM_HIP(hipMemcpyAsync(p->d_obs, obs, no * 16, hipMemcpyHostToDevice, s));
+    }
+    SFM_HIP(hipMemcpyAsync(p->d_pstart, pstart.data(), pstart.size() * 4, hipMemcpyHostToDevice, s));
+    if (p->nblocks) {
+        SFM_HIP(hipMemcpyAsync(p->d_blk, blk.data(), blk.size() * sizeof(int2), hipMemcpyHostToDevice, s));
+        SFM_HIP(hipMemcpyAsync(p->d_bstart, bstart.data(), bstart.size() * 4, hipMemcpyHostToDevice, s));
+        SFM_HIP(hipMemcpyAsync(p->d_pairs, pairs.data(), pairs.size() * sizeof(int2), hipMemcpyHostToDevice, s));
+    }
+    if ((rc = upload_state(p.get()))) return rc;
+    *out = p.release();
+    return 0;
+}
+
+extern "C" int sfm_ba_reset(sfm_ba_problem *p) {
+    SFM_CHECK_ARG(p, "null problem");
+    SFM_HIP(hipSetDevice(p->device));
+    return upload_state(p);
+}
+
+extern "C" int sfm_ba_destroy(sfm_ba_problem *p) {
+    delete p;
+    return 0;
+}
+
+static int allreduce(sfm_ba_problem *p, double *buf, int64_t n) {
+    if (!p->comm || p->comm->nranks <= 1) return 0;
+    ncclResult_t r = ncclAllReduce(buf, buf, (size_t)n, ncclDouble, ncclSum, p->comm->comm, p->stream);
+    if (r != ncclSuccess) {
+        set_error("ncclAllReduce: %s", ncclGetErrorString(r));
+        return SFM_ERR_COMM;
+    }
+    return 0;
+}
+
+// launches one linearisation (J, V, g) and, into d_scal[8], the cost.
+static int run_linearize(sfm_ba_problem *p) {
+    hipStream_t s = p->stream;
+    hipLaunchKernelGGL(k_linearize, dim3(p->pt_blocks), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam, p->d_obs,
+                       p->K, p->d_Rt, p->d_X, p->d_J, p->d_Vg, p->d_partial);
+    SFM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, p->d_partial, p->pt_blocks, 1, p->d_scal + 8);
+    SFM_HIP(hipGetLastError());
+    return allreduce(p, p->d_scal + 8, 1);
+}
+
+// one damped solve + trial evaluation; on return h_scal holds
+// [cost_trial, model_p, dn_p, xn_p, model_c, dn_c, xn_c, bad]
+static int run_step(sfm_ba_problem *p, double lambda, bool timed) {
+    hipStream_t s = p->stream;
+    int rc;
+    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_PREP], s));
+    SFM_HIP(hipMemsetAsync(p->d_payload, 0, p->payload_len * sizeof(double), s));
+    SFM_HIP(hipMemsetAsync(p->d_bad, 0, sizeof(int), s));
+    hipLaunchKernelGGL(k_point_prep, dim3(p->pt_blocks), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_J, p->d_Vg,
+                       lambda, p->d_Lq, p->d_Z);
+    SFM_HIP(hipGetLastError());
+    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_PREP + 1], s));
+    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_SCHUR], s));
+    if (p->nblocks) {
+        hipLaunchKernelGGL(k_schur_blocks, dim3(p->nblocks), dim3(SCHUR_THREADS), 0, s, p->ns, p->d_blk, p->d_bstart,
+                           p->d_pairs, p->d_pt, p->d_J, p->d_Z, p->d_Lq, p->d_payload);
+        SFM_HIP(hipGetLastError());
+    }
+    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_SCHUR + 1], s));
+    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_COMM], s));
+    if ((rc = allreduce(p, p->d_payload, p->payload_len - 1))) return rc;
+    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_COMM + 1], s));
+    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_SOLVE], s));
+    const int64_t nA = (int64_t)p->nsp * p->nsp;
+    hipLaunchKernelGGL(k_assemble, dim3(ceil_div(nA, 256)), dim3(256), 0, s, p->ns, p->nsp, p->d_payload, lambda,
+                       p->d_A, p->d_b);
+    SFM_HIP(hipGetLastError());
+    for (int kt = 0; kt < p->nT; ++kt) {
+        hipLaunchKernelGGL(k_chol_panel, dim3(p->nT - kt), dim3(256), 0, s, p->d_A, p->nsp, kt, p->d_D, p->d_bad);
+        SFM_HIP(hipGetLastError());
+        const int T = p->nT - kt - 1;
+        hipLaunchKernelGGL(k_chol_update, dim3(T * (T + 1) / 2 + 1), dim3(256), 0, s, p->d_A, p->nsp, kt, p->d_D);
+        SFM_HIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(256), 0, s, p->d_A, p->nsp, p->d_b);
+    SFM_HIP(hipGetLastError());
+    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_SOLVE + 1], s));
+    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_TRIAL], s));
+    hipLaunchKernelGGL(k_camera_trial, dim3(1), dim3(256), 0, s, p->nc, p->d_b, p->d_payload, p->ns, lambda, p->d_Rt,
+                       p->d_Rt2, p->d_scal + 4);
+    SFM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_backsub_trial, dim3(p->pt_blocks), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam,
+                       p->d_obs, p->K, p->d_J, p->d_Vg, p->d_Lq, p->d_b, lambda, p->d_Rt2, p->d_X, p->d_X2,
+                       p->d_partial);
+    SFM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, p->d_partial, p->pt_blocks, 4, p->d_scal);
+    SFM_HIP(hipGetLastError());
+    if ((rc = allreduce(p, p->d_scal, 4))) return rc;
+    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_TRIAL + 1], s));
+    SFM_HIP(hipMemcpyAsync(p->h_scal, p->d_scal, 7 * sizeof(double), hipMemcpyDeviceToHost, s));
+    SFM_HIP(hipMemcpyAsync(p->h_scal + 7, p->d_bad, sizeof(int), hipMemcpyDeviceToHost, s));
+    SFM_HIP(hipStreamSynchronize(s));
+    if (timed) {
+        for (int k = T_PREP; k < T_NT; ++k) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, p->ev[2 * k], p->ev[2 * k + 1]);
+            p->t_acc[k] += ms;
+        }
+    }
+    return 0;
+}
+
+extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_report *rep) {
+    SFM_CHECK_ARG(p && o, "null pointer");
+    SFM_HIP(hipSetDevice(p->device));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (double &t : p->t_acc) t = 0;
+    p->t_iters = 0;
+    int rc;
+    double lambda = o->initial_lambda, nu = 2.0, cost = 0, cost0 = 0;
+    int status = 4, accepted = 0, it = 0;
+    bool need_lin = true, first = true;
+    for (it = 0; it < o->max_iterations; ++it) {
+        if (need_lin) {
+            SFM_HIP(hipEventRecord(p->ev[2 * T_LIN], p->stream));
+            if ((rc = run_linearize(p))) return rc;
+            SFM_HIP(hipEventRecord(p->ev[2 * T_LIN + 1], p->stream));
+            if (first) {
+                SFM_HIP(hipMemcpyAsync(p->h_scal + 8, p->d_scal + 8, sizeof(double), hipMemcpyDeviceToHost, p->stream));
+                SFM_HIP(hipStreamSynchronize(p->stream));
+                cost = cost0 = p->h_scal[8];
+                first = false;
+            }
+            need_lin = false;
+        }
+        if ((rc = run_step(p, lambda, true))) return rc;
+        {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, p->ev[2 * T_LIN], p->ev[2 * T_LIN + 1]) == hipSuccess) p->t_acc[T_LIN] += ms;
+        }
+        p->t_iters++;
+        const double *h = p->h_scal;
+        int bad = 0;
+        std::memcpy(&bad, h + 7, sizeof(int));
+        const double cost_new = h[0];
+        const double model = 0.5 * (h[1] + h[4]);
+        const double dnorm = std::sqrt(h[2] + h[5]), xnorm = std::sqrt(h[3] + h[6]);
+        const double rho = (!bad && model > 0) ? (cost - cost_new) / model : -1.0;
+        if (!bad && std::isfinite(cost_new) && rho > 1e-3) {
+            std::swap(p->d_Rt, p->d_Rt2);
+            std::swap(p->d_X, p->d_X2);
+            const double dcost = cost - cost_new;
+            cost = cost_new;
+            accepted++;
+            double f = 2.0 * rho - 1.0;
+            f = 1.0 - f * f * f;
+            lambda *= std::max(f, 1.0 / 3.0);
+            nu = 2.0;
+            need_lin = true;
+            if (!o->fixed_iterations) {
+                if (dcost < o->function_tolerance * cost) { status = 1; ++it; break; }
+                if (dnorm < o->parameter_tolerance * (xnorm + o->parameter_tolerance)) { status = 3; ++it; break; }
+            }
+        } else {
+            lambda *= nu;
+            nu *= 2.0;
+            if (lambda > 1e32) {
+                if (!o->fixed_iterations) { status = 5; ++it; break; }
+                lambda = o->initial_lambda;
+                nu = 2.0;
+            }
+        }
+        // the timing event for linearize is re-recorded only on the next accepted step
+        SFM_HIP(hipEventRecord(p->ev[2 * T_LIN], p->stream));
+        SFM_HIP(hipEventRecord(p->ev[2 * T_LIN + 1], p->stream));
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    if (rep) {
+        rep->iterations = it;
+        rep->accepted = accepted;
+        rep->status = status;
+        rep->n_ranks = p->comm ? p->comm->nranks : 1;
+        rep->cost0 = cost0;
+        rep->cost = cost;
+        rep->t_loop_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        rep->lambda = lambda;
+    }
+    return 0;
+}
+
+extern "C" int sfm_ba_download(sfm_ba_problem *p, double *cams, double *pts) {
+    SFM_CHECK_ARG(p, "null problem");
+    SFM_HIP(hipSetDevice(p->device));
+    std::vector<double> Rt(12 * (size_t)p->nc);
+    SFM_HIP(hipMemcpyAsync(Rt.data(), p->d_Rt, Rt.size() * 8, hipMemcpyDeviceToHost, p->stream));
+    if (pts && p->np) SFM_HIP(hipMemcpyAsync(pts, p->d_X, (size_t)p->np * 24, hipMemcpyDeviceToHost, p->stream));
+    SFM_HIP(hipStreamSynchronize(p->stream));
+    if (cams)
+        for (int c = 0; c < p->nc; ++c) {
+            h_R_to_rotvec(&Rt[12 * c], cams + 6 * c);
+            for (int i = 0; i < 3; ++i) cams[6 * c + 3 + i] = Rt[12 * c + 9 + i];
+        }
+    return 0;
+}
+
+extern "C" int sfm_ba_kernel_times(sfm_ba_problem *p, double *ms, int n, char *names, int names_len) {
+    SFM_CHECK_ARG(p, "null problem");
+    const int m = std::min(n, (int)T_NT);
+    for (int k = 0; k < m; ++k) ms[k] = p->t_iters ? p->t_acc[k] / p->t_iters : 0.0;
+    if (names && names_len > 0) {
+        std::strncpy(names, kTimerNames, names_len - 1);
+        names[names_len - 1] = 0;
+    }
+    return m;
+}
+
+extern "C" int sfm_ba_lm(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt,
+                         const double *obs, const double *K, double *cams, double *pts, const sfm_ba_opts *o,
+                         sfm_ba_report *rep, int device) {
+    SFM_CHECK_ARG(o && cams, "null pointer");
+    const auto t0 = std::chrono::steady_clock::now();
+    sfm_ba_problem *p = nullptr;
+    int rc = sfm_ba_create(nc, np_, no, cam, pt, obs, K, cams, pts, device, nullptr, &p);
+    if (rc) return rc;
+    const auto t1 = std::chrono::steady_clock::now();
+    rc = sfm_ba_solve(p, o, rep);
+    const auto t2 = std::chrono::steady_clock::now();
+    if (!rc) rc = sfm_ba_download(p, cams, pts);
+    const auto t3 = std::chrono::steady_clock::now();
+    if (rep) {
+        rep->t_setup_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        rep->t_download_ms = std::chrono::duration<double, std::milli>(t3 - t2).count();
+    }
+    sfm_ba_destroy(p);
+    return rc;
+}

@@ -1,0 +1,462 @@
+// libsfmcore: C-ABI plumbing + the small entry points
+// (EstimateFundamentalMatrix general-N, LinearTriangulation, project_points,
+// bundle_adjustment_residuals) and the host-side CPython random replay.
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <unordered_map>
+
+#include "sfm_common.hpp"
+#include "sfm_geom.hpp"
+
+namespace sfm {
+
+static thread_local std::string g_err;
+static thread_local double g_timings[8];
+static thread_local int g_ntimings = 0;
+
+void set_error(const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+void clear_error() { g_err.clear(); }
+void set_timings(const double *t, int n) {
+    g_ntimings = n < 8 ? n : 8;
+    for (int i = 0; i < g_ntimings; ++i) g_timings[i] = t[i];
+}
+
+ThreadCtx *thread_ctx(int device) {
+    static thread_local std::unordered_map<int, std::unique_ptr<ThreadCtx>> ctxs;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        set_error("no HIP device visible (hipGetDeviceCount=%d)", ndev);
+        return nullptr;
+    }
+    if (device < 0 || device >= ndev) {
+        set_error("device %d out of range (%d devices)", device, ndev);
+        return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        set_error("hipSetDevice(%d) failed", device);
+        return nullptr;
+    }
+    auto &slot = ctxs[device];
+    if (!slot) {
+        auto c = std::make_unique<ThreadCtx>();
+        c->device = device;
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+            set_error("hipStreamCreate failed on device %d", device);
+            return nullptr;
+        }
+        for (auto &e : c->ev)
+            if (hipEventCreate(&e) != hipSuccess) {
+                set_error("hipEventCreate failed");
+                return nullptr;
+            }
+        slot = std::move(c);
+    }
+    return slot.get();
+}
+
+// ---------------------------------------------------------------- kernels
+
+// EstimateFundamentalMatrix for N >= 8 (EstimateFundamentalMatrix.py:21-83):
+// one workgroup.  Hartley statistics by block reduction; the N x 9 design
+// matrix is reduced to a 9 x 9 triangular factor by per-thread Givens QR
+// plus a binary tree merge in LDS (same right singular vectors as A);
+// thread 0 then runs a 9-column one-sided Jacobi SVD for the null vector.
+constexpr int FG_THREADS = 128;
+
+__device__ __forceinline__ void givens_absorb(double (&R)[9][9], double (&a)[9]) {
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+        if (a[j] != 0.0) {
+            const double r = sqrt(R[j][j] * R[j][j] + a[j] * a[j]);
+            const double c = R[j][j] / r, s = a[j] / r;
+#pragma unroll
+            for (int k = j; k < 9; ++k) {
+                const double u = R[j][k], v = a[k];
+                R[j][k] = c * u + s * v;
+                a[k] = -s * u + c * v;
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(FG_THREADS) k_f8_general(const double2 *__restrict__ x1,
+                                                           const double2 *__restrict__ x2, int64_t N,
+                                                           double *__restrict__ F) {
+    __shared__ double red[4][FG_THREADS];
+    __shared__ double Rs[FG_THREADS][45];
+    const int t = threadIdx.x;
+    double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    for (int64_t i = t; i < N; i += FG_THREADS) {
+        const double2 p = x1[i], q = x2[i];
+        s0 += p.x; s1 += p.y; s2 += q.x; s3 += q.y;
+    }
+    red[0][t] = s0; red[1][t] = s1; red[2][t] = s2; red[3][t] = s3;
+    __syncthreads();
+    for (int w = FG_THREADS / 2; w > 0; w >>= 1) {
+        if (t < w)
+            for (int k = 0; k < 4; ++k) red[k][t] += red[k][t + w];
+        __syncthreads();
+    }
+    const double m1x = red[0][0] / (double)N, m1y = red[1][0] / (double)N;
+    const double m2x = red[2][0] / (double)N, m2y = red[3][0] / (double)N;
+    __syncthreads();
+    double d1 = 0, d2 = 0;
+    for (int64_t i = t; i < N; i += FG_THREADS) {
+        const double2 p = x1[i], q = x2[i];
+        const double ax = p.x - m1x, ay = p.y - m1y, bx = q.x - m2x, by = q.y - m2y;
+        d1 += sqrt(ax * ax + ay * ay);
+        d2 += sqrt(bx * bx + by * by);
+    }
+    red[0][t] = d1; red[1][t] = d2;
+    __syncthreads();
+    for (int w = FG_THREADS / 2; w > 0; w >>= 1) {
+        if (t < w) { red[0][t] += red[0][t + w]; red[1][t] += red[1][t + w]; }
+        __syncthreads();
+    }
+    Hartley h1, h2;
+    h1.s = 1.4142135623730951 / (red[0][0] / (double)N + 1e-8);
+    h2.s = 1.4142135623730951 / (red[1][0] / (double)N + 1e-8);
+    h1.ox = -h1.s * m1x; h1.oy = -h1.s * m1y; h2.ox = -h2.s * m2x; h2.oy = -h2.s * m2y;
+    double R[9][9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+#pragma unroll
+        for (int j = 0; j < 9; ++j) R[i][j] = 0.0;
+    for (int64_t i = t; i < N; i += FG_THREADS) {
+        const double2 p = x1[i], q = x2[i];
+        const double a = h1.s * p.x + h1.ox, b = h1.s * p.y + h1.oy;
+        const double c = h2.s * q.x + h2.ox, d = h2.s * q.y + h2.oy;
+        double row[9] = {a * c, a * d, a, b * c, b * d, b, c, d, 1.0};
+        givens_absorb(R, row);
+    }
+    for (int w = FG_THREADS / 2; w > 0; w >>= 1) {
+        if (t >= w && t < 2 * w) {
+            int k = 0;
+#pragma unroll
+            for (int i = 0; i < 9; ++i)
+#pragma unroll
+                for (int j = i; j < 9; ++j) Rs[t][k++] = R[i][j];
+        }
+        __syncthreads();
+        if (t < w) {
+#pragma unroll
+            for (int i = 0; i < 9; ++i) {
+                double row[9];
+#pragma unroll
+                for (int j = 0; j < 9; ++j) row[j] = 0.0;
+#pragma unroll
+                for (int j = i; j < 9; ++j) row[j] = Rs[t + w][i * 9 - i * (i - 1) / 2 + (j - i)];
+                givens_absorb(R, row);
+            }
+        }
+        __syncthreads();
+    }
+    if (t != 0) return;
+    double a[9][9], V[9][9];  // a[col][row]
+#pragma unroll
+    for (int c = 0; c < 9; ++c)
+#pragma unroll
+        for (int r = 0; r < 9; ++r) a[c][r] = R[r][c];
+    jacobi_onesided<9, 9, 40>(a, V);
+    const int j = weakest_column<9, 9>(a);
+    double f[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f[k] = V[k][j];
+    f8_finish(f, h1, h2, F);
+}
+
+// LinearTriangulation.py:54-90: one thread per point, 4x4 DLT system,
+// right singular vector of the smallest singular value by one-sided Jacobi.
+struct P2 {
+    double p[24];
+};
+
+__global__ void __launch_bounds__(256) k_triangulate(P2 P, const double2 *__restrict__ x1,
+                                                     const double2 *__restrict__ x2, int64_t N,
+                                                     double *__restrict__ X) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const double *P1 = P.p, *Q = P.p + 12;
+    const double2 u = x1[i], v = x2[i];
+    double a[4][4], V[4][4];  // a[col][row]
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        a[c][0] = u.y * P1[8 + c] - P1[4 + c];
+        a[c][1] = P1[c] - u.x * P1[8 + c];
+        a[c][2] = v.y * Q[8 + c] - Q[4 + c];
+        a[c][3] = Q[c] - v.x * Q[8 + c];
+    }
+    jacobi_onesided<4, 4, 40>(a, V);
+    const int j = weakest_column<4, 4>(a);
+    const double h0 = V[0][j], h1 = V[1][j], h2 = V[2][j], h3 = V[3][j];
+    if (fabs(h3) > 1e-8) {
+        X[3 * i] = h0 / h3; X[3 * i + 1] = h1 / h3; X[3 * i + 2] = h2 / h3;
+    } else {
+        X[3 * i] = h0; X[3 * i + 1] = h1; X[3 * i + 2] = h2;
+    }
+}
+
+// project_points (BundleAdjustment.py:29-38)
+struct P1s {
+    double p[12];
+};
+__global__ void __launch_bounds__(256) k_project(P1s P, const double *__restrict__ X, int64_t M,
+                                                 double *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M) return;
+    const double x = X[3 * i], y = X[3 * i + 1], z = X[3 * i + 2];
+    const double *p = P.p;
+    const double u = p[0] * x + p[1] * y + p[2] * z + p[3];
+    const double v = p[4] * x + p[5] * y + p[6] * z + p[7];
+    const double w = p[8] * x + p[9] * y + p[10] * z + p[11];
+    out[2 * i] = u / (w + 1e-8);
+    out[2 * i + 1] = v / (w + 1e-8);
+}
+
+// bundle_adjustment_residuals (BundleAdjustment.py:73-110): per camera
+// R = from_rotvec, C = -R^T t, P = K [R | -R C]; per observation obs - proj.
+__global__ void k_camera_P(int32_t nc, const double *__restrict__ cams, const double *__restrict__ Kd,
+                           double *__restrict__ P) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nc) return;
+    double R[9];
+    const double *w = cams + 6 * c;
+    rotvec_to_R(w[0], w[1], w[2], R);
+    double C[3], tt[3];
+    for (int i = 0; i < 3; ++i) C[i] = -(R[i] * w[3] + R[3 + i] * w[4] + R[6 + i] * w[5]);
+    for (int i = 0; i < 3; ++i) tt[i] = -(R[3 * i] * C[0] + R[3 * i + 1] * C[1] + R[3 * i + 2] * C[2]);
+    for (int r = 0; r < 3; ++r) {
+        for (int k = 0; k < 3; ++k)
+            P[12 * c + 4 * r + k] = Kd[3 * r] * R[k] + Kd[3 * r + 1] * R[3 + k] + Kd[3 * r + 2] * R[6 + k];
+        P[12 * c + 4 * r + 3] = Kd[3 * r] * tt[0] + Kd[3 * r + 1] * tt[1] + Kd[3 * r + 2] * tt[2];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_ba_residuals(int64_t n_obs, const int32_t *__restrict__ cam,
+                                                      const int32_t *__restrict__ pt,
+                                                      const double2 *__restrict__ obs,
+                                                      const double *__restrict__ P,
+                                                      const double *__restrict__ X, double2 *__restrict__ r) {
+    const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= n_obs) return;
+    const double *p = P + 12 * cam[o];
+    const double *x = X + 3 * (int64_t)pt[o];
+    const double u = p[0] * x[0] + p[1] * x[1] + p[2] * x[2] + p[3];
+    const double v = p[4] * x[0] + p[5] * x[1] + p[6] * x[2] + p[7];
+    const double w = p[8] * x[0] + p[9] * x[1] + p[10] * x[2] + p[11];
+    const double2 ob = obs[o];
+    r[o] = make_double2(ob.x - u / (w + 1e-8), ob.y - v / (w + 1e-8));
+}
+
+// ------------------------------------------------------ CPython random replay
+// MT19937 exactly as CPython's _randommodule.c genrand_uint32, plus
+// random.py (3.10) _randbelow_with_getrandbits and sample()'s branches.
+struct PyMT {
+    uint32_t mt[624];
+    int idx;
+    uint32_t next() {
+        static const uint32_t mag01[2] = {0x0U, 0x9908b0dfU};
+        if (idx >= 624) {
+            int kk;
+            uint32_t y;
+            for (kk = 0; kk < 624 - 397; kk++) {
+                y = (mt[kk] & 0x80000000U) | (mt[kk + 1] & 0x7fffffffU);
+                mt[kk] = mt[kk + 397] ^ (y >> 1) ^ mag01[y & 0x1U];
+            }
+            for (; kk < 623; kk++) {
+                y = (mt[kk] & 0x80000000U) | (mt[kk + 1] & 0x7fffffffU);
+                mt[kk] = mt[kk + (397 - 624)] ^ (y >> 1) ^ mag01[y & 0x1U];
+            }
+            y = (mt[623] & 0x80000000U) | (mt[0] & 0x7fffffffU);
+            mt[623] = mt[396] ^ (y >> 1) ^ mag01[y & 0x1U];
+            idx = 0;
+        }
+        uint32_t y = mt[idx++];
+        y ^= (y >> 11);
+        y ^= (y << 7) & 0x9d2c5680U;
+        y ^= (y << 15) & 0xefc60000U;
+        y ^= (y >> 18);
+        return y;
+    }
+    uint32_t getrandbits(int k) { return k == 0 ? 0u : next() >> (32 - k); }
+    int64_t randbelow(int64_t n) {
+        if (n == 0) return 0;
+        int k = 0;
+        for (uint64_t m = (uint64_t)n; m; m >>= 1) ++k;  // n.bit_length()
+        if (k > 32) return -1;  // not needed for N < 2^31
+        uint32_t r = getrandbits(k);
+        while ((int64_t)r >= n) r = getrandbits(k);
+        return r;
+    }
+};
+
+}  // namespace sfm
+
+using namespace sfm;
+
+extern "C" int sfm_version(void) { return SFM_ABI_VERSION; }
+extern "C" const char *sfm_last_error(void) { return g_err.c_str(); }
+extern "C" int sfm_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+extern "C" int sfm_last_timings(double *out, int n) {
+    const int m = n < g_ntimings ? n : g_ntimings;
+    for (int i = 0; i < m; ++i) out[i] = g_timings[i];
+    return m;
+}
+
+extern "C" int sfm_pyrandom_sample_table(uint32_t *st, int64_t n, int32_t k, int64_t H, int32_t *out) {
+    SFM_CHECK_ARG(st && (out || H == 0), "null pointer");
+    SFM_CHECK_ARG(k >= 0 && k <= n && n < (int64_t)1 << 31, "need 0 <= k <= n < 2^31");
+    SFM_CHECK_ARG(st[624] <= 624, "bad MT19937 position");
+    PyMT m;
+    std::memcpy(m.mt, st, sizeof m.mt);
+    m.idx = (int)st[624];
+    int64_t setsize = 21;
+    if (k > 5) setsize += (int64_t)std::pow(4.0, std::ceil(std::log((double)k * 3) / std::log(4.0)));
+    std::vector<int32_t> pool;
+    for (int64_t h = 0; h < H; ++h) {
+        int32_t *res = out + h * k;
+        if (n <= setsize) {
+            pool.resize(n);
+            for (int64_t i = 0; i < n; ++i) pool[i] = (int32_t)i;
+            for (int32_t i = 0; i < k; ++i) {
+                const int64_t j = m.randbelow(n - i);
+                res[i] = pool[j];
+                pool[j] = pool[n - i - 1];
+            }
+        } else {
+            for (int32_t i = 0; i < k; ++i) {
+                int64_t j;
+                for (;;) {
+                    j = m.randbelow(n);
+                    bool dup = false;
+                    for (int32_t q = 0; q < i; ++q) dup |= (res[q] == (int32_t)j);
+                    if (!dup) break;
+                }
+                res[i] = (int32_t)j;
+            }
+        }
+    }
+    std::memcpy(st, m.mt, sizeof m.mt);
+    st[624] = (uint32_t)m.idx;
+    return 0;
+}
+
+extern "C" int sfm_f8_general(const double *x1, const double *x2, int64_t N, double *F, int device) {
+    SFM_CHECK_ARG(N >= 1, "need N >= 1 correspondences");
+    SFM_CHECK_ARG(x1 && x2 && F, "null pointer");
+    ThreadCtx *c = thread_ctx(device);
+    if (!c) return SFM_ERR_HIP;
+    const size_t pb = (size_t)N * sizeof(double2);
+    int rc;
+    if ((rc = c->buf[0].reserve(pb)) || (rc = c->buf[1].reserve(pb)) || (rc = c->buf[2].reserve(9 * sizeof(double))))
+        return rc;
+    SFM_HIP(hipMemcpyAsync(c->buf[0].p, x1, pb, hipMemcpyHostToDevice, c->stream));
+    SFM_HIP(hipMemcpyAsync(c->buf[1].p, x2, pb, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_f8_general, dim3(1), dim3(FG_THREADS), 0, c->stream, c->buf[0].as<double2>(),
+                       c->buf[1].as<double2>(), N, c->buf[2].as<double>());
+    SFM_HIP(hipGetLastError());
+    SFM_HIP(hipMemcpyAsync(F, c->buf[2].p, 9 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    SFM_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" int sfm_triangulate_dlt(const double *P1, const double *P2_, const double *x1, const double *x2,
+                                   int64_t N, double *X, int device) {
+    SFM_CHECK_ARG(N >= 0, "N < 0");
+    if (N == 0) return 0;
+    SFM_CHECK_ARG(P1 && P2_ && x1 && x2 && X, "null pointer");
+    ThreadCtx *c = thread_ctx(device);
+    if (!c) return SFM_ERR_HIP;
+    const size_t pb = (size_t)N * sizeof(double2);
+    int rc;
+    if ((rc = c->buf[0].reserve(pb)) || (rc = c->buf[1].reserve(pb)) || (rc = c->buf[2].reserve((size_t)N * 24)))
+        return rc;
+    P2 P;
+    std::memcpy(P.p, P1, 12 * sizeof(double));
+    std::memcpy(P.p + 12, P2_, 12 * sizeof(double));
+    hipStream_t s = c->stream;
+    SFM_HIP(hipEventRecord(c->ev[0], s));
+    SFM_HIP(hipMemcpyAsync(c->buf[0].p, x1, pb, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipMemcpyAsync(c->buf[1].p, x2, pb, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipEventRecord(c->ev[1], s));
+    hipLaunchKernelGGL(k_triangulate, dim3(ceil_div(N, 256)), dim3(256), 0, s, P, c->buf[0].as<double2>(),
+                       c->buf[1].as<double2>(), N, c->buf[2].as<double>());
+    SFM_HIP(hipGetLastError());
+    SFM_HIP(hipEventRecord(c->ev[2], s));
+    SFM_HIP(hipMemcpyAsync(X, c->buf[2].p, (size_t)N * 24, hipMemcpyDeviceToHost, s));
+    SFM_HIP(hipEventRecord(c->ev[3], s));
+    SFM_HIP(hipStreamSynchronize(s));
+    float a = 0, b = 0, d = 0;
+    (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
+    (void)hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
+    (void)hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
+    const double t[4] = {a, b, d, b};
+    set_timings(t, 4);
+    return 0;
+}
+
+extern "C" int sfm_project_points(const double *P, const double *X, int64_t M, double *out, int device) {
+    SFM_CHECK_ARG(M >= 0, "M < 0");
+    if (M == 0) return 0;
+    SFM_CHECK_ARG(P && X && out, "null pointer");
+    ThreadCtx *c = thread_ctx(device);
+    if (!c) return SFM_ERR_HIP;
+    int rc;
+    if ((rc = c->buf[0].reserve((size_t)M * 24)) || (rc = c->buf[1].reserve((size_t)M * 16))) return rc;
+    P1s p;
+    std::memcpy(p.p, P, sizeof p.p);
+    SFM_HIP(hipMemcpyAsync(c->buf[0].p, X, (size_t)M * 24, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_project, dim3(ceil_div(M, 256)), dim3(256), 0, c->stream, p, c->buf[0].as<double>(), M,
+                       c->buf[1].as<double>());
+    SFM_HIP(hipGetLastError());
+    SFM_HIP(hipMemcpyAsync(out, c->buf[1].p, (size_t)M * 16, hipMemcpyDeviceToHost, c->stream));
+    SFM_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" int sfm_ba_residuals(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt,
+                                const double *obs, const double *K, const double *cams, const double *pts,
+                                double *r, int device) {
+    SFM_CHECK_ARG(nc >= 0 && np_ >= 0 && no >= 0, "negative size");
+    if (no == 0) return 0;
+    SFM_CHECK_ARG(cam && pt && obs && K && cams && pts && r, "null pointer");
+    for (int64_t o = 0; o < no; ++o)
+        SFM_CHECK_ARG(cam[o] >= 0 && cam[o] < nc && pt[o] >= 0 && pt[o] < np_, "index out of range");
+    ThreadCtx *c = thread_ctx(device);
+    if (!c) return SFM_ERR_HIP;
+    int rc;
+    if ((rc = c->buf[0].reserve((size_t)no * 8)) || (rc = c->buf[1].reserve((size_t)no * 16)) ||
+        (rc = c->buf[2].reserve((size_t)nc * 48 + 72)) || (rc = c->buf[3].reserve((size_t)np_ * 24)) ||
+        (rc = c->buf[4].reserve((size_t)nc * 96)) || (rc = c->buf[5].reserve((size_t)no * 16)))
+        return rc;
+    hipStream_t s = c->stream;
+    int32_t *dcam = c->buf[0].as<int32_t>(), *dpt = dcam + no;
+    double *dK = c->buf[2].as<double>(), *dcams = dK + 9;
+    SFM_HIP(hipMemcpyAsync(dcam, cam, (size_t)no * 4, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipMemcpyAsync(dpt, pt, (size_t)no * 4, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipMemcpyAsync(c->buf[1].p, obs, (size_t)no * 16, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipMemcpyAsync(dK, K, 72, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipMemcpyAsync(dcams, cams, (size_t)nc * 48, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipMemcpyAsync(c->buf[3].p, pts, (size_t)np_ * 24, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_camera_P, dim3(ceil_div(nc, 64)), dim3(64), 0, s, nc, dcams, dK, c->buf[4].as<double>());
+    SFM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_ba_residuals, dim3(ceil_div(no, 256)), dim3(256), 0, s, no, dcam, dpt,
+                       c->buf[1].as<double2>(), c->buf[4].as<double>(), c->buf[3].as<double>(),
+                       c->buf[5].as<double2>());
+    SFM_HIP(hipGetLastError());
+    SFM_HIP(hipMemcpyAsync(r, c->buf[5].p, (size_t)no * 16, hipMemcpyDeviceToHost, s));
+    SFM_HIP(hipStreamSynchronize(s));
+    return 0;
+}

@@ -1,0 +1,105 @@
+"""CPU checks of the boundary: libsfmcore.so loads, exports every symbol
+include/sfmcore.h declares, the drop-in modules keep the reference's public
+signatures, and the host-side random replay is exact.  No GPU needed."""
+import inspect
+import os
+import random
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+
+def header_symbols():
+    txt = open(os.path.join(REPO, "include", "sfmcore.h")).read()
+    return sorted(set(re.findall(r"\b(sfm_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    import _sfmcore
+    syms = header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(_sfmcore._lib, s), s
+    assert {n for n, _, _ in _sfmcore.SIGNATURES} == set(syms)
+    assert _sfmcore.version() == 1
+
+
+def test_compute_fails_loudly_without_gpu():
+    import _sfmcore
+    if _sfmcore.device_count() > 0:
+        pytest.skip("GPU present")
+    with pytest.raises(_sfmcore.SfmCoreError):
+        _sfmcore.f8_batch(np.zeros((1, 8, 2)), np.zeros((1, 8, 2)))
+    from BundleAdjustment import perform_bundle_adjustment
+    import sfm_synthetic as syn
+    p = syn.ba_problem(3, 30, 3, seed=1)
+    with pytest.raises(_sfmcore.SfmCoreError):
+        perform_bundle_adjustment(p["X0"], p["filtered_world_coords"], p["feature_x"], p["feature_y"], p["flags"],
+                                  list(p["R0"]), list(p["C0"]), syn.K_REF, 2)
+
+
+# reference public surface; Phase 1/*.py signatures
+REFERENCE_SIGNATURES = {
+    ("EstimateFundamentalMatrix", "EstimateFundamentalMatrix"): "(points1, points2)",
+    ("GetInliersRANSAC", "GetInliersRANSAC"): "(points1, points2, index, threshold=0.06, n_max=1000)",
+    ("GetInliersRANSAC", "get_inliers_ransac"): "(points1, points2, index, threshold=0.06, n_max=1000)",
+    ("GetInliersRANSAC", "EstimateFundamentalMatrix"): "(points1, points2)",
+    ("LinearTriangulation", "LinearTriangulation"): "(K, C1, R1, C2, R2, x1, x2)",
+    ("LinearTriangulation", "linear_triangulation"): "(K, C1, R1, C2, R2, x1, x2)",
+    ("BundleAdjustment", "project_points"): "(K, C, R, X)",
+    ("BundleAdjustment", "bundle_adjustment_residuals"):
+        "(params, n_cameras, n_points, camera_indices, point_indices, points_2d, K, n_cam_params=6)",
+}
+
+
+@pytest.mark.parametrize("mod,fn", sorted(REFERENCE_SIGNATURES))
+def test_dropin_signatures(mod, fn):
+    m = __import__(mod)
+    assert str(inspect.signature(getattr(m, fn))) == REFERENCE_SIGNATURES[(mod, fn)]
+
+
+def test_perform_bundle_adjustment_signature():
+    from BundleAdjustment import perform_bundle_adjustment
+    sig = inspect.signature(perform_bundle_adjustment)
+    pos = [p.name for p in sig.parameters.values() if p.kind == p.POSITIONAL_OR_KEYWORD]
+    assert pos == ["all_world_coords", "filtered_world_coords", "feature_x", "feature_y",
+                   "filtered_feature_flags", "R_set", "C_set", "K", "cam_index"]
+    assert all(p.default is not p.empty for p in sig.parameters.values() if p.kind == p.KEYWORD_ONLY)
+
+
+@pytest.mark.parametrize("n,k,H", [(5000, 8, 3000), (86, 8, 500), (85, 8, 500), (8, 8, 100), (558, 8, 1000),
+                                   (20, 4, 300), (3, 2, 50), (2 ** 20 + 3, 8, 200)])
+def test_sample_table_replays_python_random(n, k, H):
+    import _sfmcore
+    random.seed(n * 31 + k)
+    random.random()  # arbitrary position inside the MT block
+    st = random.getstate()
+    t = _sfmcore.sample_table(n, k, H)
+    after = random.getstate()
+    random.setstate(st)
+    ref = np.array([random.sample(range(n), k) for _ in range(H)], dtype=np.int32).reshape(H, k)
+    assert np.array_equal(t, ref)
+    assert after == random.getstate()
+
+
+def test_ba_observation_order_matches_reference_loop():
+    """Dense flags -> COO exactly as BundleAdjustment.py:164-169 assembles it."""
+    from BundleAdjustment import _observations
+    rng = np.random.default_rng(0)
+    F, C = 60, 5
+    flags = (rng.random((F, C + 2)) < 0.5).astype(np.int64)
+    fx, fy = rng.random((F, C + 2)), rng.random((F, C + 2))
+    valid = (rng.random((F, 1)) < 0.7).astype(np.int64)
+    vpi, cams, pts, p2d = _observations(valid, fx, fy, flags, C)
+    ref_c, ref_p, ref_2d = [], [], []
+    vp = np.where(valid.flatten() == 1)[0]
+    for pt_idx in vp:
+        for cam_idx in range(C):
+            if flags[pt_idx, cam_idx] == 1:
+                ref_c.append(cam_idx)
+                ref_p.append(np.where(vp == pt_idx)[0][0])
+                ref_2d.append([fx[pt_idx, cam_idx], fy[pt_idx, cam_idx]])
+    assert np.array_equal(cams, ref_c) and np.array_equal(pts, ref_p) and np.array_equal(p2d, ref_2d)

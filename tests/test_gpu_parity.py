@@ -1,0 +1,295 @@
+"""Parity of the HIP path (through the C-ABI and the drop-in modules) with the
+reference, on a real MI355X.  Expected values come from tests/golden/ (made
+by importing the reference, tests/golden/make_golden.py) and from the C
+oracle (oracle/sfm_oracle.c) on the same seeded inputs.
+
+Tolerances:
+  * RANSAC: identical per-hypothesis counts, best iteration, inlier set,
+    and the global random state afterwards; |F - F_ref| / |F_ref| <= 1e-9.
+  * 8-point F and DLT triangulation: relative error <= 1e-9.
+  * BA: reprojection RMSE within 1e-4 (relative) of the converged
+    least-squares solution of the reference residual, and never above the
+    as-shipped reference result.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import oracle as O
+import sfm_synthetic as syn
+
+pytestmark = pytest.mark.gpu
+K = syn.K_REF
+
+
+@pytest.fixture(scope="module")
+def core():
+    import _sfmcore
+    _sfmcore.require_device()
+    return _sfmcore
+
+
+def rel(a, b):
+    return np.abs(np.asarray(a) - np.asarray(b)).max() / np.abs(np.asarray(b)).max()
+
+
+def degenerate_samples(x1, x2, samples):
+    rows = np.concatenate([x1[samples], x2[samples]], axis=2)
+    return np.array([len(np.unique(r, axis=0)) < len(r) for r in rows])
+
+
+# ------------------------------------------------------------------ F / RANSAC
+def test_f8_batch_matches_reference(core, golden):
+    g = golden("f8.npz")
+    F = core.f8_batch(g["p1"], g["p2"])
+    r = np.abs(F - g["F"]).max(axis=(1, 2)) / np.abs(g["F"]).max(axis=(1, 2))
+    assert r.max() < 1e-9, r.max()
+
+
+@pytest.mark.parametrize("n", [9, 20, 100, 558])
+def test_estimate_fundamental_matrix_general_n(core, golden, n):
+    from EstimateFundamentalMatrix import EstimateFundamentalMatrix
+    g = golden("f8.npz")
+    F = EstimateFundamentalMatrix(g[f"genN{n}_p1"], g[f"genN{n}_p2"])
+    assert rel(F, g[f"genN{n}_F"]) < 1e-9
+
+
+def test_estimate_fundamental_matrix_8pt_dropin(core, golden):
+    from EstimateFundamentalMatrix import EstimateFundamentalMatrix
+    g = golden("f8.npz")
+    for i in range(0, 512, 97):
+        assert rel(EstimateFundamentalMatrix(g["p1"][i].tolist(), g["p2"][i]), g["F"][i]) < 1e-9
+    with pytest.raises(ValueError):
+        EstimateFundamentalMatrix(np.zeros((8, 3)), np.zeros((8, 3)))
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_ransac_cfg2_bit_exact(core, golden, seed):
+    """cfg2: N=5000, 40 % outliers, 16384 (seed 0) / 2000 hypotheses."""
+    from GetInliersRANSAC import GetInliersRANSAC
+    c = golden("ransac_cfg2.npz")
+    x1, x2, idx = c["x1"], c["x2"], c["index"]
+    H = int(c[f"s{seed}_n_max"])
+    random.seed(seed)
+    st = random.getstate()
+    samples = np.array([random.sample(range(len(x1)), 8) for _ in range(H)], dtype=np.int32)
+    best, F, mask, counts = core.ransac_f8(x1, x2, samples, 0.06, want_counts=True)
+    assert np.array_equal(counts, c[f"s{seed}_counts"].astype(np.int32))
+    assert best == int(c[f"s{seed}_best_iter"])
+    # through the drop-in, consuming the global random stream itself
+    random.setstate(st)
+    inl, outl, F2 = GetInliersRANSAC(x1, x2, idx, 0.06, H)
+    assert np.array_equal(inl, c[f"s{seed}_inlier_pos"])
+    assert np.array_equal(np.sort(np.concatenate([inl, outl])), idx)
+    assert rel(F2, c[f"s{seed}_F"]) < 1e-9
+    assert np.array_equal(np.array(random.getstate()[1], dtype=np.uint32), c[f"s{seed}_state_after"])
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_ransac_p3data_all_pairs(core, golden, seed):
+    """cfg1: the reference driver's 10 image pairs (Wrapper_dev.py:69-123)."""
+    from GetInliersRANSAC import get_inliers_ransac
+    p = golden("ransac_p3data.npz")
+    n_pairs = 0
+    for a in range(1, 6):
+        for b in range(a + 1, 6):
+            key = f"s{seed}_{a}_{b}"
+            if key + "_x1" not in p:
+                continue
+            random.setstate((3, tuple(int(v) for v in p[key + "_state_before"]), None))
+            F, f_idx = get_inliers_ransac(p[key + "_x1"], p[key + "_x2"], p[key + "_index"], threshold=0.06,
+                                          n_max=1000)
+            assert np.array_equal(np.asarray(f_idx, dtype=np.int64), p[key + "_inlier_idx"]), key
+            assert rel(F, p[key + "_F"]) < 1e-9, key
+            assert np.array_equal(np.array(random.getstate()[1], dtype=np.uint32), p[key + "_state_after"])
+            n_pairs += 1
+    assert n_pairs == 10
+
+
+def test_ransac_p3data_pair12_counts(core, golden):
+    p = golden("ransac_p3data.npz")
+    key = "s0_1_2"
+    x1, x2 = p[key + "_x1"], p[key + "_x2"]
+    random.setstate((3, tuple(int(v) for v in p[key + "_state_before"]), None))
+    samples = core.sample_table(len(x1), 8, 1000)
+    best, F, mask, counts = core.ransac_f8(x1, x2, samples, 0.06, want_counts=True)
+    degen = degenerate_samples(x1, x2, samples)
+    assert np.array_equal(counts[~degen], p[key + "_counts"][~degen])
+    assert best == int(np.argmax(p[key + "_counts"]))
+    assert np.array_equal(p[key + "_index"][mask], p[key + "_inlier_idx"])
+
+
+def test_ransac_matches_oracle_random_inputs(core):
+    rng = np.random.default_rng(7)
+    for N, H in ((8, 50), (64, 300), (1000, 700), (4097, 129)):
+        x1, x2, _, _ = syn.two_view(n=N, seed=int(rng.integers(1 << 30)))
+        samples = np.stack([rng.choice(N, 8, replace=False) for _ in range(H)]).astype(np.int32)
+        b, counts, F, mask = O.ransac(x1, x2, samples, 0.5)
+        b2, F2, mask2, counts2 = core.ransac_f8(x1, x2, samples, 0.5, want_counts=True)
+        assert np.array_equal(counts, counts2)
+        assert b == b2
+        if b >= 0:
+            assert np.array_equal(mask, mask2)
+            assert rel(F2, F) < 1e-9
+
+
+def test_ransac_edge_cases(core):
+    from GetInliersRANSAC import GetInliersRANSAC, get_inliers_ransac
+    x1, x2, idx, _ = syn.two_view(n=200, seed=3)
+    # N < 8: early exit, random untouched
+    random.seed(5)
+    st = random.getstate()
+    inl, outl, F = GetInliersRANSAC(x1[:7], x2[:7], idx[:7])
+    assert len(inl) == 0 and F is None and np.array_equal(outl, idx[:7]) and random.getstate() == st
+    # n_max = 0: no hypotheses
+    inl, outl, F = GetInliersRANSAC(x1, x2, idx, 0.06, 0)
+    assert F is None and len(inl) == 0
+    # threshold 0: every count is 0 -> None, but the stream still advanced n_max draws
+    random.seed(5)
+    Fb, fi = get_inliers_ransac(x1, x2, idx, threshold=0.0, n_max=37)
+    st_after = random.getstate()
+    random.seed(5)
+    for _ in range(37):
+        random.sample(range(200), 8)
+    assert Fb is None and fi.dtype == np.float64 and len(fi) == 0 and random.getstate() == st_after
+    # NaN correspondence: hypotheses that sample it score 0, others unaffected
+    y1 = x1.copy()
+    y1[3] = np.nan
+    rng = np.random.default_rng(1)
+    samples = np.stack([rng.choice(200, 8, replace=False) for _ in range(200)]).astype(np.int32)
+    b, counts, _, _ = O.ransac(y1, x2, samples, 0.5)
+    b2, _, _, counts2 = core.ransac_f8(y1, x2, samples, 0.5, want_counts=True)
+    assert np.array_equal(counts, counts2) and b == b2
+
+
+def test_ransac_full_size_properties(core):
+    """cfg2 at 4x the hypotheses: every reported inlier satisfies the test,
+    the winner's count equals its mask size and is the maximum."""
+    x1, x2, idx, _ = syn.two_view(n=5000, seed=9)
+    random.seed(11)
+    samples = core.sample_table(5000, 8, 65536)
+    best, F, mask, counts = core.ransac_f8(x1, x2, samples, 0.06, want_counts=True)
+    assert counts.max() == counts[best] == mask.sum()
+    assert np.argmax(counts) == best
+    assert np.array_equal(O.ransac_mask(x1, x2, F, 0.06), mask)
+
+
+# ------------------------------------------------------------- triangulation
+def test_triangulation_matches_reference(core, golden):
+    from LinearTriangulation import LinearTriangulation, linear_triangulation
+    t = golden("triangulation.npz")
+    for i in range(4):
+        X = linear_triangulation(K, np.zeros(3), np.eye(3), t["p3_Cset"][i], t["p3_Rset"][i], t["p3_x1"], t["p3_x2"])
+        assert rel(X, t[f"p3_X{i}"]) < 1e-9
+    X = LinearTriangulation(K, np.zeros(3), np.eye(3), t["syn_C2"], t["syn_R2"], t["syn_x1"], t["syn_x2"])
+    r = np.abs(X - t["syn_X"]).max(axis=1) / np.abs(t["syn_X"]).max(axis=1)
+    assert r.max() < 1e-9
+    assert LinearTriangulation(K, np.zeros(3), np.eye(3), t["syn_C2"], t["syn_R2"], [], []).shape == (0,)
+
+
+def test_triangulation_large_vs_oracle(core):
+    _, _, _, m = syn.two_view(n=200_000, seed=4)
+    rng = np.random.default_rng(2)
+    x1 = m["clean1"] + rng.normal(0, 0.5, m["clean1"].shape)
+    x2 = m["clean2"] + rng.normal(0, 0.5, m["clean2"].shape)
+    P1 = O.projection(K, np.zeros(3), np.eye(3))
+    P2 = O.projection(K, m["C2"], m["R2"])
+    X = core.triangulate(P1, P2, x1, x2)
+    Xo = O.triangulate(K, np.zeros(3), np.eye(3), m["C2"], m["R2"], x1[:20000], x2[:20000])
+    r = np.abs(X[:20000] - Xo).max(axis=1) / np.abs(Xo).max(axis=1)
+    assert r.max() < 1e-9
+    # size-independent property: the DLT point reprojects close to the data
+    err = np.abs(core.project(P2, X) - x2).max()
+    assert err < 5.0
+
+
+# ---------------------------------------------------------------------- BA
+def test_project_and_residuals_match_oracle(core):
+    from BundleAdjustment import bundle_adjustment_residuals, project_points
+    p = syn.ba_problem(5, 300, 3, seed=1)
+    cams = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
+    params = np.concatenate([cams.ravel(), p["X0"].ravel()])
+    r = bundle_adjustment_residuals(params, 5, 300, p["cam_idx"], p["pt_idx"], p["obs"], K)
+    ro = O.ba_residuals(cams, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K)
+    assert rel(r, ro) < 1e-9
+    x = project_points(K, p["C0"][2], p["R0"][2], p["X0"])
+    xo = (K @ (p["R0"][2] @ (p["X0"] - p["C0"][2]).T)).T
+    xo = xo[:, :2] / (xo[:, 2:3] + 1e-8)
+    assert rel(x, xo) < 1e-9
+
+
+def _rmse_of(R_set, C_set, Xw, prob, rows=None):
+    nc = len(R_set)
+    cams = np.concatenate([np.concatenate([O.R_to_rotvec(np.asarray(R_set[i])), -np.asarray(R_set[i]) @ C_set[i]])
+                           for i in range(nc)]).reshape(nc, 6)
+    r = O.ba_residuals(cams, Xw if rows is None else Xw[rows], prob["cam_idx"], prob["pt_idx"], prob["obs"], K)
+    return syn.rmse_from_cost(0.5 * r @ r, len(prob["cam_idx"]))
+
+
+@pytest.mark.parametrize("name,shape", [("tiny2", (2, 20, 2)), ("tiny", (3, 30, 3)),
+                                        ("small", (6, 200, 4)), ("cfg3", (6, 2000, 5))])
+def test_perform_bundle_adjustment_matches_converged_reference(core, golden, name, shape, capsys):
+    from BundleAdjustment import perform_bundle_adjustment
+    b = golden("ba.npz")
+    nc, npt, k = shape
+    p = syn.ba_problem(nc, npt, k, seed=3)
+    R0, C0 = [p["R0"][i] for i in range(nc)], [p["C0"][i] for i in range(nc)]
+    Xw = p["X0"].copy()
+    R1, C1, X1 = perform_bundle_adjustment(Xw, p["filtered_world_coords"], p["feature_x"], p["feature_y"],
+                                           p["flags"], R0, C0, K, nc - 1)
+    out = capsys.readouterr().out
+    assert f"  Bundle adjustment: {nc} cameras, {npt} points, {len(p['cam_idx'])} observations" in out
+    assert "  Bundle adjustment completed. Final cost: " in out
+    assert X1 is not Xw and np.array_equal(Xw, p["X0"])  # input untouched, copy returned
+    n = len(p["cam_idx"])
+    rm = _rmse_of(R1, C1, X1, p)
+    rc = syn.rmse_from_cost(float(b[f"{name}_cost_conv"]), n)
+    assert abs(rm - rc) <= 1e-4 * rc, (rm, rc)
+    if f"{name}_shipped_X" in b:
+        rs = _rmse_of(b[f"{name}_shipped_R"], b[f"{name}_shipped_C"], b[f"{name}_shipped_X"], p)
+        assert rm <= rs + 1e-9
+
+
+def test_ba_matches_oracle_midsize(core):
+    p = syn.ba_problem(12, 5000, 6, seed=5, dense=False)
+    cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
+    _, _, ro = O.ba_lm(cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K, max_iterations=100)
+    _, _, rg = core.ba_lm(cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K, max_iterations=100)
+    n = len(p["cam_idx"])
+    assert abs(rg["cost0"] - ro["cost0"]) <= 1e-9 * ro["cost0"]
+    ro_r, rg_r = syn.rmse_from_cost(ro["cost"], n), syn.rmse_from_cost(rg["cost"], n)
+    assert abs(ro_r - rg_r) <= 1e-4 * ro_r
+
+
+def test_ba_cfg4_full_size_properties(core):
+    """cfg4 (50 cams / 100k pts / 1M obs): converges to the noise floor,
+    deterministic run to run."""
+    p = syn.ba_problem_cfg("cfg4", dense=False)
+    cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
+    c1, x1, r1 = core.ba_lm(cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K, max_iterations=50)
+    c2, x2, r2 = core.ba_lm(cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K, max_iterations=50)
+    n = len(p["cam_idx"])
+    assert r1["cost"] < r1["cost0"]
+    assert syn.rmse_from_cost(r1["cost"], n) < 0.75  # pixel noise sigma 0.5 per axis
+    assert r1["cost"] == r2["cost"] and np.array_equal(x1, x2) and np.array_equal(c1, c2)
+    r = core.ba_residuals(c1, x1, p["cam_idx"], p["pt_idx"], p["obs"], K)
+    assert abs(0.5 * r @ r - r1["cost"]) <= 1e-8 * r1["cost"]
+
+
+def test_ba_failure_contract(core, capsys):
+    from BundleAdjustment import perform_bundle_adjustment
+    p = syn.ba_problem(3, 30, 2, seed=2)  # 2*60 residuals < 18 + 90 params? no: 120 >= 108
+    R0, C0 = [p["R0"][i] for i in range(3)], [p["C0"][i] for i in range(3)]
+    # too few observations -> scipy's m < n error, inputs returned as the same objects
+    flags = p["flags"].copy()
+    flags[:, 2] = 0
+    Xw = p["X0"].copy()
+    R1, C1, X1 = perform_bundle_adjustment(Xw, p["filtered_world_coords"], p["feature_x"], p["feature_y"],
+                                           flags, R0, C0, K, 2)
+    assert R1 is R0 and C1 is C0 and X1 is Xw
+    assert "Bundle adjustment failed: Method 'lm' doesn't work" in capsys.readouterr().out
+    # no valid points -> inputs, nothing printed
+    R1, C1, X1 = perform_bundle_adjustment(Xw, 0 * p["filtered_world_coords"], p["feature_x"], p["feature_y"],
+                                           p["flags"], R0, C0, K, 2)
+    assert X1 is Xw and capsys.readouterr().out == ""
