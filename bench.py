@@ -1,0 +1,246 @@
+"""Benchmark of the MI355X SfM hot path (BASELINE.json metric:
+"BA LM-iterations/sec + RANSAC hypotheses/sec at 1/2/4/8 MI355X; final
+reproj RMSE vs ref").
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg4|cfg5]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Workload (BASELINE config 4, the one the north-star target is quoted on):
+synthetic BA, 50 cameras / 100k points / 1M observations (sfm_synthetic).
+A step is one LM iteration (damped Schur solve + trial evaluation, plus the
+re-linearisation after an accepted step) of the sparse Schur-complement LM,
+with the problem resident in HBM.  N > 1: points are sharded across ranks
+(strong scaling of the same problem) with one RCCL all-reduce of the
+reduced camera system per iteration.  value = LM iterations / s of the job.
+
+Also reported: RANSAC hypotheses/s on config 2 (5000 correspondences, 40 %
+outliers, 16384 hypotheses) on rank 0's GPU; the converged RMSE vs the
+reference's least-squares oracle; the roofline of the dominant kernel
+(HIP-event time on the library's own stream); a CPU baseline (the C oracle,
+1 thread, rank 0 at N = 1).
+"""
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "structure-from-motion-_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (imported before libsfmcore: one HIP runtime per process)
+
+import _sfmcore as core  # noqa: E402
+import sfm_dist  # noqa: E402
+import sfm_synthetic as syn  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 vector
+
+
+def algorithmic_bytes(name, n_obs, n_pts, n_pairs, nblocks, ns):
+    """Compulsory bytes one launch of each kernel family moves."""
+    if name == "schur_blocks":
+        return 144 * n_obs + 112 * n_obs + 24 * n_pts + 8 * n_pairs + 12 * nblocks + 8 * (ns * ns + 3 * ns)
+    if name == "point_prep":
+        return 160 * n_obs + 144 * n_obs + 72 * n_pts + 72 * n_pts
+    if name == "linearize":
+        return (16 + 4 + 160) * n_obs + (24 + 72 + 4) * n_pts
+    if name == "backsub_trial":
+        return (160 + 16 + 4) * n_obs + (72 + 72 + 24 + 24 + 4) * n_pts
+    return None
+
+
+def n_pairs_of(pt_idx):
+    k = np.bincount(pt_idx)
+    return int((k * (k + 1) // 2).sum())
+
+
+def cpu_baseline_ba(prob, K):
+    import oracle as O  # test infrastructure: the CPU restatement, timed as the baseline
+    cams0 = np.column_stack([prob["rotvec0"], np.einsum("nij,nj->ni", -prob["R0"], prob["C0"])])
+    t = time.perf_counter()
+    _, _, rep = O.ba_lm(cams0, prob["X0"], prob["cam_idx"], prob["pt_idx"], prob["obs"], K, max_iterations=50)
+    dt = time.perf_counter() - t
+    return rep["iterations"] / dt, rep, dt
+
+
+def cpu_baseline_ransac(x1, x2, samples):
+    import oracle as O
+    t = time.perf_counter()
+    O.ransac(x1, x2, samples, 0.06)
+    dt = time.perf_counter() - t
+    return len(samples) / dt, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="cfg4", choices=["cfg3", "cfg4", "cfg5"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ransac-hyps", type=int, default=16384)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    assert torch.cuda.is_available(), "bench.py needs an MI355X"
+    torch.cuda.set_device(local_rank)
+    core.require_device()
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+
+    def allmax(v):
+        if world == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        return float(t.item())
+
+    # ---------------- BA workload (every rank generates the same problem)
+    K = syn.K_REF
+    prob = syn.ba_problem_cfg(args.workload, dense=False)
+    cams0 = np.column_stack([prob["rotvec0"], np.einsum("nij,nj->ni", -prob["R0"], prob["C0"])])
+    ci, pi, ob, X0, (lo, hi) = sfm_dist.shard_ba(prob["cam_idx"], prob["pt_idx"], prob["obs"], prob["X0"],
+                                                 world, rank)
+    comm = None
+    if world > 1:
+        uid = [core.Comm.unique_id() if rank == 0 else None]
+        torch.distributed.broadcast_object_list(uid, src=0)
+        comm = core.Comm(uid[0], world, rank, device=local_rank)
+    ba = core.BAProblem(cams0, X0, ci, pi, ob, K, comm=comm, device=local_rank)
+
+    # converged solve (RMSE vs the reference's least-squares solution)
+    conv = ba.solve(max_iterations=100)
+    n_obs_total = len(prob["cam_idx"])
+    rmse0 = syn.rmse_from_cost(conv["cost0"], n_obs_total)
+    rmse = syn.rmse_from_cost(conv["cost"], n_obs_total)
+
+    # warmup, then exactly K timed LM iterations from the initial state
+    ba.reset()
+    ba.solve(max_iterations=args.warmup, fixed_iterations=True)
+    ba.reset()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rep = ba.solve(max_iterations=args.steps, fixed_iterations=True)
+    torch.cuda.synchronize()
+    barrier()
+    dt = allmax(time.perf_counter() - t0)
+    ktimes = ba.kernel_times()
+    ba.close()
+    if comm is not None:
+        comm.close()
+
+    # ---------------- RANSAC (config 2) on this rank's GPU
+    x1, x2, idx, _ = syn.two_view(n=5000, seed=0)
+    random.seed(0)
+    samples = core.sample_table(5000, 8, args.ransac_hyps)
+    for _ in range(3):
+        core.ransac_f8(x1, x2, samples, 0.06, device=local_rank)
+    reps = 20
+    t = time.perf_counter()
+    for _ in range(reps):
+        random.seed(0)
+        s = core.sample_table(5000, 8, args.ransac_hyps)
+        best, F, mask, _ = core.ransac_f8(x1, x2, s, 0.06, device=local_rank)
+    t_e2e = (time.perf_counter() - t) / reps
+    kt = []
+    for _ in range(reps):
+        core.ransac_f8(x1, x2, samples, 0.06, device=local_rank)
+        tm = core.last_timings()
+        kt.append((tm[1], tm[3]))
+    k_all, k_score = np.median([a for a, _ in kt]), np.median([b for _, b in kt])
+
+    if rank != 0:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+
+    n_pairs = n_pairs_of(prob["pt_idx"][prob["pt_idx"] < hi] if world > 1 else prob["pt_idx"])
+    ns = 6 * prob["n_cams"]
+    nblocks = prob["n_cams"] * (prob["n_cams"] + 1) // 2
+    fam = {k: v for k, v in ktimes.items() if k != "allreduce"}
+    dom = max(fam, key=fam.get)
+    n_obs_local, n_pts_local = len(ci), len(X0)
+    alg = algorithmic_bytes(dom, n_obs_local, n_pts_local, n_pairs, nblocks, ns)
+    if alg is not None:
+        ach = alg / (ktimes[dom] * 1e-3) / 1e9
+        roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes": int(alg),
+                "avg_launch_ms": round(ktimes[dom], 4)}
+    else:  # cholesky: n^3/3 flops
+        nsp = ((ns + 31) // 32) * 32
+        fl = nsp ** 3 / 3.0
+        ach = fl / (ktimes[dom] * 1e-3) / 1e12
+        roof = {"kernel": dom, "bound": "fp64", "achieved": round(ach, 4), "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(ach / FP64_PEAK_TFLOPS, 5), "traffic": None,
+                "avg_launch_ms": round(ktimes[dom], 4)}
+    iter_bytes = 52 * n_obs_total + 240 * prob["n_pts"]  # SURVEY §8(d) compulsory bytes / LM iteration
+    ms_per_step = dt / args.steps * 1e3
+    out = {
+        "metric": "BA LM-iterations/sec (+ RANSAC hypotheses/sec, final reproj RMSE vs ref)",
+        "value": round(args.steps / dt, 3),
+        "unit": "LM-iterations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (sfm_synthetic.ba_problem, seed 3)",
+        "config": {"workload": f"{args.workload}: BA {prob['n_cams']} cams / {prob['n_pts']} pts / "
+                               f"{n_obs_total} obs, Schur-complement LM, points sharded over {world} rank(s)",
+                   "parallelism": f"point-shard x{world} + RCCL all-reduce of the reduced camera system"},
+        "roofline": roof,
+        "kernel_ms_per_iter": {k: round(v, 4) for k, v in ktimes.items()},
+        "iteration_roofline": {"compulsory_bytes": iter_bytes,
+                               "achieved_GBs": round(iter_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+                               "frac": round(iter_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)},
+        "rmse": {"initial": round(rmse0, 6), "converged": round(rmse, 6), "lm_iterations": conv["iterations"],
+                 "note": "cfg3 parity vs the reference least-squares oracle in tests/test_gpu_parity.py"},
+        "ransac": {"workload": "cfg2: 5000 corr, 40% outliers", "hypotheses": args.ransac_hyps,
+                   "hyps_per_s_end_to_end": round(args.ransac_hyps / t_e2e, 1),
+                   "hyps_per_s_kernels": round(args.ransac_hyps / (k_all * 1e-3), 1),
+                   "score_kernel_ms": round(float(k_score), 4), "best_iter": int(best), "inliers": int(mask.sum())},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        v, crep, cdt = cpu_baseline_ba(prob, K)
+        hs = samples[:1024]
+        rv, rdt = cpu_baseline_ransac(x1, x2, hs)
+        out["cpu_baseline"] = {"value": round(v, 4), "unit": "LM-iterations/s", "cores": 1, "kind": "port",
+                               "sample": f"C oracle Schur-LM (oracle/sfm_oracle.c), full {args.workload} problem, "
+                                         f"{crep['iterations']} LM iterations to convergence in {cdt:.1f}s, 1 thread",
+                               "speedup": round(out["value"] / v, 1),
+                               "ransac_hyps_per_s": round(rv, 1),
+                               "ransac_sample": f"C oracle, 1024 cfg2 hypotheses in {rdt:.2f}s, 1 thread",
+                               "cpu": _cpu_model(), "os_cpu_count": os.cpu_count()}
+    print(json.dumps(out))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+if __name__ == "__main__":
+    main()

@@ -152,7 +152,7 @@ def f8_general(x1, x2):
     return F.reshape(3, 3)
 
 
-def ransac_f8(x1, x2, samples, thr, want_counts=False):
+def ransac_f8(x1, x2, samples, thr, want_counts=False, device=None):
     """Returns (best_iter or -1, F_best (3,3) or None, mask (N,) bool, counts or None)."""
     require_device()
     x1, x2 = _f64(x1), _f64(x2)
@@ -164,7 +164,7 @@ def ransac_f8(x1, x2, samples, thr, want_counts=False):
     mask = np.zeros(N, dtype=np.uint8)
     _check(_lib.sfm_ransac_f8(_p(x1), _p(x2), N, _p(samples, _i32), H, float(thr),
                               _p(counts, _i32) if want_counts else None, _p(best, _i64), _p(F),
-                              _p(mask, _u8), DEVICE))
+                              _p(mask, _u8), DEVICE if device is None else device))
     b = int(best[0])
     if b < 0:
         return -1, None, np.zeros(N, dtype=bool), counts

@@ -11,11 +11,11 @@
 //   k_point_prep     thread per point: Vd = V + lambda*clamp(diag V) = C C^T,
 //                    L = C^-T (so Vd^-1 = L L^T), q = L^T g_p,
 //                    Z_o = (Jc^T Jp)_o L per observation.
-//   k_schur_blocks   workgroup per co-visible camera pair (i <= j):
-//                    S_ij = U_i [i==j] - sum_p Z_pi Z_pj^T over the points
-//                    both cameras see (static pair list, fixed order ->
-//                    deterministic, no atomics); diagonal blocks also reduce
-//                    U_i, g_i and sum Z q.
+//   k_camera_lin     (after linearize) workgroup per camera: U_c, g_c.
+//   k_schur_pairs    S_ij = U_i [i==j] - sum_p Z_pi Z_pj^T from static
+//                    co-observation pair lists, sliced into work items;
+//   k_schur_finish   fixed-order sum of the items of each camera block ->
+//                    deterministic, no atomics.
 //   [RCCL all-reduce of the packed partial system across ranks]
 //   k_assemble       S += lambda*clamp(diag U), b = -g_c + sum Z q, padded.
 //   k_chol_panel / k_chol_update / k_chol_solve
@@ -50,7 +50,6 @@ namespace sfm {
 
 constexpr int NB = 32;            // Cholesky tile
 constexpr int PT_THREADS = 128;   // per-point kernels
-constexpr int SCHUR_THREADS = 256;
 
 __device__ __forceinline__ double clampd(double x) { return fmin(fmax(x, 1e-6), 1e32); }
 
@@ -225,94 +224,162 @@ __global__ void __launch_bounds__(PT_THREADS) k_point_prep(int64_t np_, const in
 }
 
 // Payload layout (doubles): S[ns*ns] | diagU[ns] | gc[ns] | bZ[ns] | cost
-__global__ void __launch_bounds__(SCHUR_THREADS) k_schur_blocks(
-    int32_t ns, const int2 *__restrict__ blk_ij, const int32_t *__restrict__ bstart, const int2 *__restrict__ pairs,
-    const int32_t *__restrict__ pt, const double *__restrict__ J, const double *__restrict__ Z,
-    const double *__restrict__ Lq, double *__restrict__ payload) {
-    __shared__ double red[SCHUR_THREADS / 64][36 + 21 + 12];
-    const int b = blockIdx.x;
-    const int2 ij = blk_ij[b];
-    const bool diag = ij.x == ij.y;
-    const int32_t k0 = bstart[b], k1 = bstart[b + 1];
-    double acc[36];
+constexpr int CAMLIN = 27;  // U_c (21, upper) | g_c (6)
+
+// Reduced camera system S_ij = [i==j](U_i) - sum_{p seen by i and j} Z_pi Z_pj^T.
+// Static pair lists (a, b) grouped by camera block (i <= j); a work item
+// is a slice of <= PAIR_CHUNK pairs of one block, so the large diagonal
+// blocks do not form a tail.  Each item writes its partial 6x6 block (+ the
+// diagonal block's sum Z_a q_p) to a slab; k_schur_finish sums the items of
+// a block in item order: deterministic, no atomics.  Z is the only large
+// array read here (144 B / observation), so with the pair list it stays
+// resident in the 256 MiB Infinity Cache at the BASELINE sizes.
+constexpr int PAIR_CHUNK = 4096;
+constexpr int PAIR_THREADS = 256;
+constexpr int ITEM_W = 42;  // 36 block + 6 bZ
+
+struct PairItem {
+    int32_t blk, k0, k1, diag;
+};
+
+// Two lanes per pair: lane parity h computes rows 3h..3h+2 of the 6x6
+// block (18 accumulators) -- half the registers of one lane per pair, so
+// more waves hide the gather latency; the two lanes' Z_b loads coalesce.
+__global__ void __launch_bounds__(PAIR_THREADS) k_schur_pairs(const PairItem *__restrict__ items,
+                                                              const int2 *__restrict__ pairs,
+                                                              const int32_t *__restrict__ pt,
+                                                              const double *__restrict__ Z,
+                                                              const double *__restrict__ Lq,
+                                                              double *__restrict__ slab) {
+    __shared__ double red[PAIR_THREADS / 64][ITEM_W];
+    const PairItem it = items[blockIdx.x];
+    const int h = threadIdx.x & 1;
+    double acc[21];
 #pragma unroll
-    for (int k = 0; k < 36; ++k) acc[k] = 0.0;
-    double U[21], g[6], bz[6];
-#pragma unroll
-    for (int k = 0; k < 21; ++k) U[k] = 0.0;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) { g[k] = 0.0; bz[k] = 0.0; }
-    for (int32_t k = k0 + threadIdx.x; k < k1; k += SCHUR_THREADS) {
+    for (int k = 0; k < 21; ++k) acc[k] = 0.0;
+    for (int32_t k = it.k0 + (threadIdx.x >> 1); k < it.k1; k += PAIR_THREADS / 2) {
         const int2 pr = pairs[k];
-        const double *za = Z + (int64_t)18 * pr.x;
+        const double *za = Z + (int64_t)18 * pr.x + 9 * h;
         const double *zb = Z + (int64_t)18 * pr.y;
-        double a[18], c[18];
+        double a[9], c[18];
 #pragma unroll
-        for (int i = 0; i < 18; ++i) { a[i] = za[i]; c[i] = zb[i]; }
+        for (int i = 0; i < 9; ++i) a[i] = za[i];
 #pragma unroll
-        for (int r = 0; r < 6; ++r)
+        for (int i = 0; i < 18; ++i) c[i] = zb[i];
 #pragma unroll
-            for (int s = 0; s < 6; ++s)
-                acc[6 * r + s] += a[3 * r] * c[3 * s] + a[3 * r + 1] * c[3 * s + 1] + a[3 * r + 2] * c[3 * s + 2];
-        if (diag) {
-            const double *j = J + (int64_t)JS * pr.x;
-            const double *lq = Lq + 9 * (int64_t)pt[pr.x];
-            const double q0 = lq[6], q1 = lq[7], q2 = lq[8];
-            int u = 0;
+        for (int r = 0; r < 3; ++r)
 #pragma unroll
-            for (int r = 0; r < 6; ++r) {
+            for (int s2 = 0; s2 < 6; ++s2)
+                acc[6 * r + s2] += a[3 * r] * c[3 * s2] + a[3 * r + 1] * c[3 * s2 + 1] + a[3 * r + 2] * c[3 * s2 + 2];
+        if (it.diag) {
+            const double *q = Lq + 9 * (int64_t)pt[pr.x] + 6;
+            const double q0 = q[0], q1 = q[1], q2 = q[2];
 #pragma unroll
-                for (int s = r; s < 6; ++s) U[u++] += j[2 + r] * j[2 + s] + j[8 + r] * j[8 + s];
-                g[r] += j[2 + r] * j[0] + j[8 + r] * j[1];
-                bz[r] += a[3 * r] * q0 + a[3 * r + 1] * q1 + a[3 * r + 2] * q2;
-            }
+            for (int r = 0; r < 3; ++r) acc[18 + r] += a[3 * r] * q0 + a[3 * r + 1] * q1 + a[3 * r + 2] * q2;
+        }
+    }
+    // lanes of equal parity hold the same outputs: reduce over the other 32
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 21; ++k) {
+        double v = acc[k];
+#pragma unroll
+        for (int o = 32; o > 1; o >>= 1) v += __shfl_xor(v, o);
+        if (lane < 2) {
+            const int idx = k < 18 ? 18 * lane + k : 36 + 3 * lane + (k - 18);
+            red[w][idx] = v;
+        }
+    }
+    __syncthreads();
+    const int nv = it.diag ? ITEM_W : 36;
+    if ((int)threadIdx.x < nv) {
+        double v = 0;
+#pragma unroll
+        for (int i = 0; i < PAIR_THREADS / 64; ++i) v += red[i][threadIdx.x];
+        slab[(int64_t)ITEM_W * blockIdx.x + threadIdx.x] = v;
+    }
+}
+
+// Camera blocks of the normal equations, once per linearisation: the
+// diagonal pair items are exactly chunks of one camera's observations, so
+// each item sums U = sum Jc^T Jc (21) and g = sum Jc^T r (6) over its chunk
+// and k_camera_lin_finish adds a camera's items in order (deterministic).
+__global__ void __launch_bounds__(256) k_camera_lin(const PairItem *__restrict__ items,
+                                                    const int2 *__restrict__ pairs,
+                                                    const double *__restrict__ J, double *__restrict__ slab2) {
+    __shared__ double red[4][CAMLIN];
+    const PairItem it = items[blockIdx.x];
+    double acc[CAMLIN];
+#pragma unroll
+    for (int k = 0; k < CAMLIN; ++k) acc[k] = 0.0;
+    for (int32_t k = it.k0 + threadIdx.x; k < it.k1; k += 256) {
+        const double *j = J + (int64_t)JS * pairs[k].x;
+        const double r0 = j[0], r1 = j[1];
+        double a[6], b[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) { a[i] = j[2 + i]; b[i] = j[8 + i]; }
+        int u = 0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+#pragma unroll
+            for (int s2 = r; s2 < 6; ++s2) acc[u++] += a[r] * a[s2] + b[r] * b[s2];
+            acc[21 + r] += a[r] * r0 + b[r] * r1;
         }
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-    for (int k = 0; k < 36; ++k) {
-        const double s = wave_sum(acc[k]);
-        if (lane == 0) red[w][k] = s;
-    }
-    if (diag) {
-#pragma unroll
-        for (int k = 0; k < 21; ++k) {
-            const double s = wave_sum(U[k]);
-            if (lane == 0) red[w][36 + k] = s;
-        }
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            const double s1 = wave_sum(g[k]), s2 = wave_sum(bz[k]);
-            if (lane == 0) { red[w][57 + k] = s1; red[w][63 + k] = s2; }
-        }
+    for (int k = 0; k < CAMLIN; ++k) {
+        const double v = wave_sum(acc[k]);
+        if (lane == 0) red[w][k] = v;
     }
     __syncthreads();
-    const int nv = diag ? 69 : 36;
-    for (int k = threadIdx.x; k < nv; k += SCHUR_THREADS) {
-        double s = 0;
-        for (int i = 0; i < SCHUR_THREADS / 64; ++i) s += red[i][k];
-        red[0][k] = s;
-    }
-    __syncthreads();
-    if (threadIdx.x < 36) {
-        const int r = threadIdx.x / 6, s = threadIdx.x % 6;
-        double v = -red[0][threadIdx.x];
+    if (threadIdx.x < CAMLIN)
+        slab2[(int64_t)CAMLIN * blockIdx.x + threadIdx.x] =
+            red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+// one 64-thread workgroup per camera block: fixed-order sum of its items
+struct BlockInfo {
+    int32_t i, j, first_item, last_item;
+};
+
+__global__ void __launch_bounds__(64) k_camera_lin_finish(const BlockInfo *__restrict__ blocks,
+                                                          const double *__restrict__ slab2,
+                                                          double *__restrict__ camlin) {
+    const BlockInfo bi = blocks[blockIdx.x];  // diagonal blocks come first
+    if (threadIdx.x >= CAMLIN) return;
+    double v = 0;
+    for (int k = bi.first_item; k < bi.last_item; ++k) v += slab2[(int64_t)CAMLIN * k + threadIdx.x];
+    camlin[CAMLIN * bi.i + threadIdx.x] = v;
+}
+
+__global__ void __launch_bounds__(64) k_schur_finish(int32_t ns, const BlockInfo *__restrict__ blocks,
+                                                     const double *__restrict__ slab,
+                                                     const double *__restrict__ camlin,
+                                                     double *__restrict__ payload) {
+    const BlockInfo bi = blocks[blockIdx.x];
+    const int t = threadIdx.x;
+    const bool diag = bi.i == bi.j;
+    if (t >= (diag ? ITEM_W : 36)) return;
+    double v = 0;
+    for (int k = bi.first_item; k < bi.last_item; ++k) v += slab[(int64_t)ITEM_W * k + t];
+    const int64_t base = (int64_t)ns * ns;
+    if (t < 36) {
+        const int r = t / 6, c = t % 6;
+        const int64_t row = 6 * bi.i + r, col = 6 * bi.j + c;
         if (diag) {
-            const int lo = r < s ? r : s, hi = r < s ? s : r;
-            const int ui = lo * 6 - lo * (lo - 1) / 2 + (hi - lo);
-            v += red[0][36 + ui];
+            const int lo = r < c ? r : c, hi = r < c ? c : r;
+            const double u = camlin[CAMLIN * bi.i + lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];
+            payload[row * ns + col] = u - v;
+            if (r == c) payload[base + row] = u;  // diag(U)
+        } else {
+            payload[row * ns + col] = -v;
+            payload[col * ns + row] = -v;
         }
-        const int64_t row = 6 * ij.x + r, col = 6 * ij.y + s;
-        payload[row * ns + col] = v;
-        if (!diag) payload[col * ns + row] = v;
-    }
-    if (diag && threadIdx.x < 6) {
-        const int r = threadIdx.x;
-        const int ui = r * 6 - r * (r - 1) / 2;
-        const int64_t base = (int64_t)ns * ns;
-        payload[base + 6 * ij.x + r] = red[0][36 + ui];
-        payload[base + ns + 6 * ij.x + r] = red[0][57 + r];
-        payload[base + 2 * ns + 6 * ij.x + r] = red[0][63 + r];
+    } else {
+        const int r = t - 36;
+        payload[base + ns + 6 * bi.i + r] = camlin[CAMLIN * bi.i + 21 + r];  // g_c
+        payload[base + 2 * ns + 6 * bi.i + r] = v;                           // sum Z q
     }
 }
 
@@ -337,87 +404,112 @@ __global__ void k_assemble(int32_t ns, int32_t nsp, const double *__restrict__ p
 }
 
 // --------------------------------------------------------------- Cholesky
-// factor the NB x NB tile T (LDS, row-major) in place: lower triangle = L.
-__device__ void chol_tile(double (&T)[NB][NB + 1], int *bad) {
-    for (int k = 0; k < NB; ++k) {
-        if (threadIdx.x == 0) {
-            const double d = T[k][k];
-            if (!(d > 0.0)) *bad = 1;
-            T[k][k] = sqrt(d);
-        }
-        __syncthreads();
-        const double dk = T[k][k];
-        for (int i = k + 1 + threadIdx.x; i < NB; i += blockDim.x) T[i][k] /= dk;
-        __syncthreads();
-        for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-            const int i = e / NB, j = e % NB;
-            if (i > k && j > k && j <= i) T[i][j] -= T[i][k] * T[j][k];
-        }
-        __syncthreads();
-    }
+// Right-looking blocked Cholesky of the padded nsp x nsp reduced camera
+// system with the forward substitution folded in (b is carried as an extra
+// column).  Per tile column kt:
+//   k_chol_panel   one wave per tile row kt..nT-1: every wave factors the
+//                  diagonal tile in LDS (lane = row, column broadcast);
+//                  wave 0 also solves L_kk y_k = b_k, the others solve their
+//                  tile row L_rk = A_rk L_kk^-T and write it plus its mirror.
+//   k_chol_update  block 0 stores L_kk and updates b_r -= L_rk y_k; the
+//                  others apply the trailing update A_rc -= L_rk L_ck^T.
+// k_chol_backsolve then solves L^T x = y in one workgroup.
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// grid = nT - kt workgroups; workgroup w factors diag tile kt (redundantly)
-// and, for w > 0, solves tile row kt + w: L_rk = A_rk L_kk^-T.
-// A is read-only here (every workgroup re-factors A_kk); workgroup 0 puts
-// L_kk in the scratch tile D, which k_chol_update copies back into A.
-__global__ void __launch_bounds__(256) k_chol_panel(double *__restrict__ A, int32_t nsp, int kt,
-                                                    double *__restrict__ D, int *__restrict__ bad) {
-    __shared__ double T[NB][NB + 1];
-    __shared__ double B[NB][NB + 1];
+// broadcast lane l's double to the whole wave (two v_readlane_b32 -> SGPRs)
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const unsigned long long u = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+__global__ void __launch_bounds__(64) k_chol_panel(double *__restrict__ A, int32_t nsp, int kt,
+                                                   double *__restrict__ D, double *__restrict__ bvec,
+                                                   int *__restrict__ bad) {
+    __shared__ double Ls[NB][NB + 1];
+    const int lane = threadIdx.x;
     const int k0 = kt * NB;
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-        const int i = e / NB, j = e % NB;
-        T[i][j] = A[(int64_t)(k0 + i) * nsp + k0 + j];
+    const int li = lane < NB ? lane : NB - 1;
+    double r[NB];  // lane i: row i of the diagonal tile -> row i of L_kk
+#pragma unroll
+    for (int j = 0; j < NB; ++j) r[j] = A[(int64_t)(k0 + li) * nsp + k0 + j];
+    // updates hit every lane's whole row: above the diagonal they only touch
+    // the unused upper triangle, which saves the predication
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        const double d = readlane_f64(r[k], k);
+        if (lane == 0 && !(d > 0.0)) *bad = 1;
+        const double lkk = sqrt(d);
+        r[k] = (lane == k) ? lkk : r[k] / lkk;
+#pragma unroll
+        for (int j = k + 1; j < NB; ++j) r[j] -= r[k] * readlane_f64(r[k], j);
     }
-    __syncthreads();
-    chol_tile(T, bad);
     if (blockIdx.x == 0) {
-        for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-            const int i = e / NB, j = e % NB;
-            D[e] = j <= i ? T[i][j] : 0.0;
+        double y = bvec[k0 + li];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const double yj = readlane_f64(y, j) / readlane_f64(r[j], j);
+            if (lane == j) y = yj;
+            if (lane > j) y -= r[j] * yj;
+        }
+        if (lane < NB) {
+            bvec[k0 + lane] = y;
+#pragma unroll
+            for (int j = 0; j < NB; ++j) D[lane * NB + j] = j <= lane ? r[j] : 0.0;
         }
         return;
     }
     const int r0 = (kt + blockIdx.x) * NB;
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-        const int i = e / NB, j = e % NB;
-        B[i][j] = A[(int64_t)(r0 + i) * nsp + k0 + j];
+    double x[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) x[j] = A[(int64_t)(r0 + li) * nsp + k0 + j];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        double v = x[j];
+#pragma unroll
+        for (int m = 0; m < j; ++m) v -= x[m] * readlane_f64(r[m], j);
+        x[j] = v / readlane_f64(r[j], j);
     }
-    __syncthreads();
-    // row i of X solves X L^T = B  <=>  for j: X[i][j] = (B[i][j] - sum_{m<j} X[i][m] L[j][m]) / L[j][j]
-    if (threadIdx.x < NB) {
-        const int i = threadIdx.x;
-        for (int j = 0; j < NB; ++j) {
-            double v = B[i][j];
-            for (int m = 0; m < j; ++m) v -= B[i][m] * T[j][m];
-            B[i][j] = v / T[j][j];
-        }
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-        const int i = e / NB, j = e % NB;
-        A[(int64_t)(r0 + i) * nsp + k0 + j] = B[i][j];
-    }
+    if (lane < NB)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) Ls[lane][j] = x[j];
+    wave_sync_lds();
+    for (int e = lane; e < NB * NB; e += 64)
+        A[(int64_t)(r0 + e / NB) * nsp + k0 + e % NB] = Ls[e / NB][e % NB];
+    for (int e = lane; e < NB * NB; e += 64)  // mirror into the upper triangle
+        A[(int64_t)(k0 + e / NB) * nsp + r0 + e % NB] = Ls[e % NB][e / NB];
 }
 
-// block 0 stores L_kk from the scratch tile; blocks 1.. do the trailing
-// update of tile (r, c), kt < c <= r: A_rc -= L_rk L_ck^T
 __global__ void __launch_bounds__(256) k_chol_update(double *__restrict__ A, int32_t nsp, int kt,
-                                                     const double *__restrict__ D) {
+                                                     const double *__restrict__ D, double *__restrict__ bvec) {
     __shared__ double Lr[NB][NB + 1];
     __shared__ double Lc[NB][NB + 1];
+    const int k0 = kt * NB;
     if (blockIdx.x == 0) {
-        const int k0 = kt * NB;
-        for (int e = threadIdx.x; e < NB * NB; e += blockDim.x)
-            A[(int64_t)(k0 + e / NB) * nsp + k0 + e % NB] = D[e];
+        for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+            const int i = e / NB, j = e % NB;
+            A[(int64_t)(k0 + i) * nsp + k0 + j] = i >= j ? D[i * NB + j] : D[j * NB + i];
+        }
+        __shared__ double yk[NB];
+        if (threadIdx.x < NB) yk[threadIdx.x] = bvec[k0 + threadIdx.x];
+        __syncthreads();
+        for (int i = k0 + NB + threadIdx.x; i < nsp; i += blockDim.x) {
+            double s = 0;
+#pragma unroll 8
+            for (int m = 0; m < NB; ++m) s += A[(int64_t)(k0 + m) * nsp + i] * yk[m];  // L[i][k0+m] (mirror)
+            bvec[i] -= s;
+        }
         return;
     }
-    // decode linear block index into (r, c) with c <= r, offsets from kt+1
     int t = blockIdx.x - 1, r = 0;
     while (t > r) { t -= r + 1; ++r; }
     const int c = t;
-    const int rr = (kt + 1 + r) * NB, cc = (kt + 1 + c) * NB, k0 = kt * NB;
+    const int rr = (kt + 1 + r) * NB, cc = (kt + 1 + c) * NB;
     for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
         const int i = e / NB, j = e % NB;
         Lr[i][j] = A[(int64_t)(rr + i) * nsp + k0 + j];
@@ -433,52 +525,44 @@ __global__ void __launch_bounds__(256) k_chol_update(double *__restrict__ A, int
     }
 }
 
-// forward / backward substitution with the factor (lower triangle of A).
-__global__ void __launch_bounds__(256) k_chol_solve(const double *__restrict__ A, int32_t nsp,
-                                                    double *__restrict__ x) {
-    __shared__ double part[256];
+// L^T x = y (y already in xg from the folded forward substitution).
+constexpr int SOLVE_THREADS = 256;
+constexpr int SOLVE_MAX = 4096;
+
+__global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(const double *__restrict__ A, int32_t nsp,
+                                                                  double *__restrict__ xg) {
+    __shared__ double x[SOLVE_MAX];
+    __shared__ double yt[NB];
+    const int t = threadIdx.x, lane = t & 63;
     const int nT = nsp / NB;
-    // forward: L y = b
-    for (int kt = 0; kt < nT; ++kt) {
-        const int k0 = kt * NB;
-        // subtract contributions of solved tiles: rows k0..k0+NB, cols 0..k0
-        {
-            const int row = threadIdx.x % NB, sl = threadIdx.x / NB;  // 8 slices
-            double s = 0;
-            for (int m = sl; m < k0; m += 256 / NB) s += A[(int64_t)(k0 + row) * nsp + m] * x[m];
-            part[threadIdx.x] = s;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            for (int i = 0; i < NB; ++i) {
-                double v = x[k0 + i];
-                for (int sl = 0; sl < 256 / NB; ++sl) v -= part[sl * NB + i];
-                for (int m = 0; m < i; ++m) v -= A[(int64_t)(k0 + i) * nsp + k0 + m] * x[k0 + m];
-                x[k0 + i] = v / A[(int64_t)(k0 + i) * nsp + k0 + i];
-            }
-        }
-        __syncthreads();
-    }
-    // backward: L^T x = y
+    for (int i = t; i < nsp; i += SOLVE_THREADS) x[i] = xg[i];
+    __syncthreads();
     for (int kt = nT - 1; kt >= 0; --kt) {
         const int k0 = kt * NB;
-        {
-            const int row = threadIdx.x % NB, sl = threadIdx.x / NB;
-            double s = 0;
-            for (int m = k0 + NB + sl; m < nsp; m += 256 / NB) s += A[(int64_t)m * nsp + k0 + row] * x[m];
-            part[threadIdx.x] = s;
+        if (t < 64) {
+            const int li = lane < NB ? lane : NB - 1;
+            double cl[NB];  // cl[m] = L[k0+m][k0+li]
+#pragma unroll
+            for (int m = 0; m < NB; ++m) cl[m] = A[(int64_t)(k0 + m) * nsp + k0 + li];
+            double v = x[k0 + li];
+#pragma unroll
+            for (int j = NB - 1; j >= 0; --j) {
+                const double vj = readlane_f64(v, j) / readlane_f64(cl[j], j);
+                if (lane == j) v = vj;
+                if (lane < j) v -= cl[j] * vj;
+            }
+            if (lane < NB) { x[k0 + lane] = v; yt[lane] = v; }
         }
         __syncthreads();
-        if (threadIdx.x == 0) {
-            for (int i = NB - 1; i >= 0; --i) {
-                double v = x[k0 + i];
-                for (int sl = 0; sl < 256 / NB; ++sl) v -= part[sl * NB + i];
-                for (int m = i + 1; m < NB; ++m) v -= A[(int64_t)(k0 + m) * nsp + k0 + i] * x[k0 + m];
-                x[k0 + i] = v / A[(int64_t)(k0 + i) * nsp + k0 + i];
-            }
+        for (int i = t; i < k0; i += SOLVE_THREADS) {
+            double s = 0;
+#pragma unroll 8
+            for (int m = 0; m < NB; ++m) s += A[(int64_t)(k0 + m) * nsp + i] * yt[m];  // L[k0+m][i]
+            x[i] -= s;
         }
         __syncthreads();
     }
+    for (int i = t; i < nsp; i += SOLVE_THREADS) xg[i] = x[i];
 }
 
 // one workgroup: trial cameras + camera part of model decrease / norms.
@@ -641,12 +725,15 @@ struct sfm_ba_problem {
     sfm_comm *comm = nullptr;
     int32_t nc = 0, ns = 0, nsp = 0, nT = 0;
     int64_t np = 0, no = 0, npairs = 0;
-    int32_t nblocks = 0;
+    int32_t nitems = 0, nblocks = 0, ndiag_items = 0, ndiag_blocks = 0;
     Kmat K;
     std::vector<double> cams0, pts0;
     // device
-    int32_t *d_cam = nullptr, *d_pt = nullptr, *d_pstart = nullptr, *d_bstart = nullptr;
-    int2 *d_blk = nullptr, *d_pairs = nullptr;
+    int32_t *d_cam = nullptr, *d_pt = nullptr, *d_pstart = nullptr, *d_cam_obs = nullptr, *d_cstart = nullptr;
+    int2 *d_pairs = nullptr;
+    PairItem *d_items = nullptr;
+    BlockInfo *d_blocks = nullptr;
+    double *d_slab = nullptr, *d_slab2 = nullptr, *d_camlin = nullptr;
     double2 *d_obs = nullptr;
     double *d_Rt = nullptr, *d_Rt2 = nullptr, *d_X = nullptr, *d_X2 = nullptr;
     double *d_J = nullptr, *d_Vg = nullptr, *d_Lq = nullptr, *d_Z = nullptr;
@@ -737,12 +824,14 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
                              sfm_comm *comm, sfm_ba_problem **out) {
     SFM_CHECK_ARG(out && K && cams && (pts || np_ == 0) && (no == 0 || (cam && pt && obs)), "null pointer");
     SFM_CHECK_ARG(nc >= 1 && np_ >= 0 && no >= 0, "bad sizes");
-    SFM_CHECK_ARG(no < ((int64_t)1 << 31) && nc <= 8192, "problem too large for int32 indexing");
+    SFM_CHECK_ARG(no < ((int64_t)1 << 31), "problem too large for int32 indexing");
+    SFM_CHECK_ARG(6 * nc <= SOLVE_MAX, "at most 682 cameras (dense reduced camera system)");
     for (int64_t o = 0; o < no; ++o) {
         SFM_CHECK_ARG(cam[o] >= 0 && cam[o] < nc && pt[o] >= 0 && pt[o] < np_, "observation index out of range");
         SFM_CHECK_ARG(o == 0 || pt[o] >= pt[o - 1], "observations must be point-major (sorted by point)");
     }
     SFM_HIP(hipSetDevice(device));
+    (void)hipGetLastError();  // launches below are checked with hipGetLastError: start clean
     auto p = std::make_unique<sfm_ba_problem>();
     p->device = device;
     p->comm = comm;
@@ -761,6 +850,18 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     std::vector<int32_t> pstart(np_ + 1, 0);
     for (int64_t o = 0; o < no; ++o) pstart[pt[o] + 1]++;
     for (int64_t i = 0; i < np_; ++i) pstart[i + 1] += pstart[i];
+    // camera-major observation list (stable: point order within a camera)
+    std::vector<int32_t> cstart(nc + 1, 0), cam_obs(no);
+    for (int64_t o = 0; o < no; ++o) cstart[cam[o] + 1]++;
+    for (int c = 0; c < nc; ++c) cstart[c + 1] += cstart[c];
+    {
+        std::vector<int32_t> fill(cstart.begin(), cstart.end() - 1);
+        for (int64_t o = 0; o < no; ++o) cam_obs[fill[cam[o]]++] = (int32_t)o;
+    }
+    for (int64_t i = 0; i < np_; ++i)
+        for (int32_t a = pstart[i]; a < pstart[i + 1]; ++a)
+            for (int32_t b = a + 1; b < pstart[i + 1]; ++b)
+                SFM_CHECK_ARG(cam[a] != cam[b], "a point is observed twice by the same camera");
     // camera-pair lists (static sparsity of the reduced camera system)
     std::vector<int64_t> cnt((size_t)nc * nc, 0);
     for (int64_t i = 0; i < np_; ++i)
@@ -768,21 +869,39 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
             for (int32_t b = a; b < pstart[i + 1]; ++b) {
                 int ci = cam[a], cj = cam[b];
                 if (ci > cj) std::swap(ci, cj);
-                SFM_CHECK_ARG(a == b || cam[a] != cam[b], "a point is observed twice by the same camera");
                 cnt[(size_t)ci * nc + cj]++;
             }
-    std::vector<int2> blk;
-    std::vector<int32_t> bstart(1, 0);
+    std::vector<BlockInfo> blocks;
+    std::vector<PairItem> items;
     std::vector<int64_t> boff((size_t)nc * nc, -1);
     int64_t tot = 0;
-    for (int i = 0; i < nc; ++i)
-        for (int j = i; j < nc; ++j)
-            if (cnt[(size_t)i * nc + j] > 0) {
+    // diagonal blocks first: they are the largest
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int i = 0; i < nc; ++i)
+            for (int j = i; j < nc; ++j) {
+                if ((pass == 0) != (i == j)) continue;
+                const int64_t n = cnt[(size_t)i * nc + j];
+                if (n == 0) continue;
                 boff[(size_t)i * nc + j] = tot;
-                tot += cnt[(size_t)i * nc + j];
-                blk.push_back(make_int2(i, j));
-                bstart.push_back((int32_t)tot);
+                BlockInfo bi;
+                bi.i = i; bi.j = j; bi.first_item = (int32_t)items.size();
+                for (int64_t k = 0; k < n; k += PAIR_CHUNK) {
+                    PairItem it;
+                    it.blk = (int32_t)blocks.size();
+                    it.k0 = (int32_t)(tot + k);
+                    it.k1 = (int32_t)(tot + std::min<int64_t>(n, k + PAIR_CHUNK));
+                    it.diag = i == j;
+                    items.push_back(it);
+                }
+                bi.last_item = (int32_t)items.size();
+                blocks.push_back(bi);
+                tot += n;
             }
+        if (pass == 0) {
+            p->ndiag_items = (int32_t)items.size();
+            p->ndiag_blocks = (int32_t)blocks.size();
+        }
+    }
     SFM_CHECK_ARG(tot < ((int64_t)1 << 31), "too many co-observation pairs");
     std::vector<int2> pairs(tot);
     for (int64_t i = 0; i < np_; ++i)
@@ -793,13 +912,17 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
                 pairs[boff[(size_t)cam[oa] * nc + cam[ob]]++] = make_int2(oa, ob);
             }
     p->npairs = tot;
-    p->nblocks = (int32_t)blk.size();
+    p->nitems = (int32_t)items.size();
+    p->nblocks = (int32_t)blocks.size();
     p->pt_blocks = std::max(1, ceil_div(np_, PT_THREADS));
     p->payload_len = (int64_t)p->ns * p->ns + 3 * p->ns + 1;
     int rc;
     if ((rc = p->alloc(p->d_cam, no)) || (rc = p->alloc(p->d_pt, no)) || (rc = p->alloc(p->d_pstart, np_ + 1)) ||
-        (rc = p->alloc(p->d_obs, no)) || (rc = p->alloc(p->d_blk, p->nblocks)) ||
-        (rc = p->alloc(p->d_bstart, p->nblocks + 1)) || (rc = p->alloc(p->d_pairs, tot)) ||
+        (rc = p->alloc(p->d_obs, no)) || (rc = p->alloc(p->d_cam_obs, no)) || (rc = p->alloc(p->d_cstart, nc + 1)) ||
+        (rc = p->alloc(p->d_pairs, tot)) || (rc = p->alloc(p->d_items, p->nitems)) ||
+        (rc = p->alloc(p->d_blocks, p->nblocks)) || (rc = p->alloc(p->d_slab, (int64_t)ITEM_W * p->nitems)) ||
+        (rc = p->alloc(p->d_camlin, (int64_t)CAMLIN * nc)) ||
+        (rc = p->alloc(p->d_slab2, (int64_t)CAMLIN * std::max<int64_t>(1, p->ndiag_items))) ||
         (rc = p->alloc(p->d_Rt, 12 * (int64_t)nc)) || (rc = p->alloc(p->d_Rt2, 12 * (int64_t)nc)) ||
         (rc = p->alloc(p->d_X, 3 * np_)) || (rc = p->alloc(p->d_X2, 3 * np_)) ||
         (rc = p->alloc(p->d_J, JS * no)) || (rc = p->alloc(p->d_Vg, 9 * np_)) || (rc = p->alloc(p->d_Lq, 9 * np_)) ||
@@ -817,10 +940,13 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         SFM_HIP(hipMemcpyAsync(p->d_obs, obs, no * 16, hipMemcpyHostToDevice, s));
     }
     SFM_HIP(hipMemcpyAsync(p->d_pstart, pstart.data(), pstart.size() * 4, hipMemcpyHostToDevice, s));
-    if (p->nblocks) {
-        SFM_HIP(hipMemcpyAsync(p->d_blk, blk.data(), blk.size() * sizeof(int2), hipMemcpyHostToDevice, s));
-        SFM_HIP(hipMemcpyAsync(p->d_bstart, bstart.data(), bstart.size() * 4, hipMemcpyHostToDevice, s));
-        SFM_HIP(hipMemcpyAsync(p->d_pairs, pairs.data(), pairs.size() * sizeof(int2), hipMemcpyHostToDevice, s));
+    if (no) SFM_HIP(hipMemcpyAsync(p->d_cam_obs, cam_obs.data(), no * 4, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipMemcpyAsync(p->d_cstart, cstart.data(), cstart.size() * 4, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipMemsetAsync(p->d_camlin, 0, (size_t)CAMLIN * nc * sizeof(double), s));
+    if (tot) SFM_HIP(hipMemcpyAsync(p->d_pairs, pairs.data(), tot * sizeof(int2), hipMemcpyHostToDevice, s));
+    if (p->nitems) {
+        SFM_HIP(hipMemcpyAsync(p->d_items, items.data(), items.size() * sizeof(PairItem), hipMemcpyHostToDevice, s));
+        SFM_HIP(hipMemcpyAsync(p->d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), hipMemcpyHostToDevice, s));
     }
     if ((rc = upload_state(p.get()))) return rc;
     *out = p.release();
@@ -851,11 +977,20 @@ static int allreduce(sfm_ba_problem *p, double *buf, int64_t n) {
 // launches one linearisation (J, V, g) and, into d_scal[8], the cost.
 static int run_linearize(sfm_ba_problem *p) {
     hipStream_t s = p->stream;
+
     hipLaunchKernelGGL(k_linearize, dim3(p->pt_blocks), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam, p->d_obs,
                        p->K, p->d_Rt, p->d_X, p->d_J, p->d_Vg, p->d_partial);
     SFM_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, p->d_partial, p->pt_blocks, 1, p->d_scal + 8);
     SFM_HIP(hipGetLastError());
+    if (p->ndiag_items) {
+        hipLaunchKernelGGL(k_camera_lin, dim3(p->ndiag_items), dim3(256), 0, s, p->d_items, p->d_pairs, p->d_J,
+                           p->d_slab2);
+        SFM_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_camera_lin_finish, dim3(p->ndiag_blocks), dim3(64), 0, s, p->d_blocks, p->d_slab2,
+                           p->d_camlin);
+        SFM_HIP(hipGetLastError());
+    }
     return allreduce(p, p->d_scal + 8, 1);
 }
 
@@ -872,9 +1007,12 @@ static int run_step(sfm_ba_problem *p, double lambda, bool timed) {
     SFM_HIP(hipGetLastError());
     if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_PREP + 1], s));
     if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_SCHUR], s));
-    if (p->nblocks) {
-        hipLaunchKernelGGL(k_schur_blocks, dim3(p->nblocks), dim3(SCHUR_THREADS), 0, s, p->ns, p->d_blk, p->d_bstart,
-                           p->d_pairs, p->d_pt, p->d_J, p->d_Z, p->d_Lq, p->d_payload);
+    if (p->nitems) {
+        hipLaunchKernelGGL(k_schur_pairs, dim3(p->nitems), dim3(PAIR_THREADS), 0, s, p->d_items, p->d_pairs, p->d_pt,
+                           p->d_Z, p->d_Lq, p->d_slab);
+        SFM_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_schur_finish, dim3(p->nblocks), dim3(64), 0, s, p->ns, p->d_blocks, p->d_slab,
+                           p->d_camlin, p->d_payload);
         SFM_HIP(hipGetLastError());
     }
     if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_SCHUR + 1], s));
@@ -887,13 +1025,15 @@ static int run_step(sfm_ba_problem *p, double lambda, bool timed) {
                        p->d_A, p->d_b);
     SFM_HIP(hipGetLastError());
     for (int kt = 0; kt < p->nT; ++kt) {
-        hipLaunchKernelGGL(k_chol_panel, dim3(p->nT - kt), dim3(256), 0, s, p->d_A, p->nsp, kt, p->d_D, p->d_bad);
+        hipLaunchKernelGGL(k_chol_panel, dim3(p->nT - kt), dim3(64), 0, s, p->d_A, p->nsp, kt, p->d_D, p->d_b,
+                           p->d_bad);
         SFM_HIP(hipGetLastError());
         const int T = p->nT - kt - 1;
-        hipLaunchKernelGGL(k_chol_update, dim3(T * (T + 1) / 2 + 1), dim3(256), 0, s, p->d_A, p->nsp, kt, p->d_D);
+        hipLaunchKernelGGL(k_chol_update, dim3(T * (T + 1) / 2 + 1), dim3(256), 0, s, p->d_A, p->nsp, kt, p->d_D,
+                           p->d_b);
         SFM_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(256), 0, s, p->d_A, p->nsp, p->d_b);
+    hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(SOLVE_THREADS), 0, s, p->d_A, p->nsp, p->d_b);
     SFM_HIP(hipGetLastError());
     if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_SOLVE + 1], s));
     if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_TRIAL], s));
@@ -924,6 +1064,7 @@ static int run_step(sfm_ba_problem *p, double lambda, bool timed) {
 extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_report *rep) {
     SFM_CHECK_ARG(p && o, "null pointer");
     SFM_HIP(hipSetDevice(p->device));
+    (void)hipGetLastError();
     const auto t0 = std::chrono::steady_clock::now();
     for (double &t : p->t_acc) t = 0;
     p->t_iters = 0;

@@ -44,6 +44,7 @@ ThreadCtx *thread_ctx(int device) {
         set_error("hipSetDevice(%d) failed", device);
         return nullptr;
     }
+    (void)hipGetLastError();  // launches are checked with hipGetLastError: start clean
     auto &slot = ctxs[device];
     if (!slot) {
         auto c = std::make_unique<ThreadCtx>();
