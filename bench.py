@@ -53,6 +53,20 @@ def algorithmic_bytes(name, n_obs, n_pts, n_pairs, nblocks, ns):
     return None
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass
+    (tools/profile_round.sh + tools/pmc_summary.py), or None."""
+    names = {"schur_blocks": "k_schur_pairs", "point_prep": "k_point_prep", "linearize": "k_linearize",
+             "backsub_trial": "k_backsub_trial"}
+    path = os.path.join(REPO, "profiles", "round1", "pmc_traffic.json")
+    try:
+        d = json.load(open(path)).get(names.get(kernel, kernel), {})
+        v = d.get("hbm_bytes_per_launch")
+        return int(v) if v else None
+    except (OSError, ValueError):
+        return None
+
+
 def n_pairs_of(pt_idx):
     k = np.bincount(pt_idx)
     return int((k * (k + 1) // 2).sum())
@@ -176,8 +190,10 @@ def main():
     if alg is not None:
         ach = alg / (ktimes[dom] * 1e-3) / 1e9
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes": int(alg),
-                "avg_launch_ms": round(ktimes[dom], 4)}
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom), "algorithmic_bytes": int(alg),
+                "avg_launch_ms": round(ktimes[dom], 4),
+                "traffic_source": "profiles/round1/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE, "
+                                  "2*FETCH+WRITE KiB)"}
     else:  # cholesky: n^3/3 flops
         nsp = ((ns + 31) // 32) * 32
         fl = nsp ** 3 / 3.0

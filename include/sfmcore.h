@@ -132,6 +132,9 @@ typedef struct sfm_ba_problem sfm_ba_problem;
 
 int sfm_comm_unique_id(char out[128]);
 int sfm_comm_init(const char id[128], int nranks, int rank, int device, sfm_comm **out);
+/* in-process group of nranks communicators (one host thread per rank, any
+ * devices, the same device allowed): out receives nranks handles */
+int sfm_comm_init_local(int nranks, sfm_comm **out);
 int sfm_comm_destroy(sfm_comm *comm);
 
 int sfm_ba_create(int32_t n_cams, int64_t n_pts, int64_t n_obs, const int32_t *cam_idx,
@@ -146,6 +149,14 @@ int sfm_ba_download(sfm_ba_problem *p, double *cam_params, double *points);
  * last solve (ms): names are written ';'-separated into `names`. */
 int sfm_ba_kernel_times(sfm_ba_problem *p, double *ms, int n, char *names, int names_len);
 int sfm_ba_destroy(sfm_ba_problem *p);
+
+/* single-process multi-GPU BA: points split over `devices` (n_ranks
+ * entries; repeats allowed), one host thread per rank, reduced camera
+ * system summed every LM iteration.  Same arguments as sfm_ba_lm. */
+int sfm_ba_lm_multi(int32_t n_cams, int64_t n_pts, int64_t n_obs, const int32_t *cam_idx,
+                    const int32_t *pt_idx, const double *obs, const double *K, double *cam_params,
+                    double *points, const sfm_ba_opts *opts, sfm_ba_report *report, const int *devices,
+                    int n_ranks);
 
 #ifdef __cplusplus
 }

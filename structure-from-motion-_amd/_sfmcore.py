@@ -68,6 +68,7 @@ SIGNATURES = [
                        ctypes.POINTER(BAReport), _c]),
     ("sfm_comm_unique_id", _c, [ctypes.c_char_p]),
     ("sfm_comm_init", _c, [ctypes.c_char_p, _c, _c, _c, ctypes.POINTER(ctypes.c_void_p)]),
+    ("sfm_comm_init_local", _c, [_c, ctypes.POINTER(ctypes.c_void_p)]),
     ("sfm_comm_destroy", _c, [ctypes.c_void_p]),
     ("sfm_ba_create", _c, [ctypes.c_int32, _i, _i, _i32, _i32, _d, _d, _d, _d, _c, ctypes.c_void_p,
                            ctypes.POINTER(ctypes.c_void_p)]),
@@ -76,6 +77,8 @@ SIGNATURES = [
     ("sfm_ba_download", _c, [ctypes.c_void_p, _d, _d]),
     ("sfm_ba_kernel_times", _c, [ctypes.c_void_p, _d, _c, ctypes.c_char_p, _c]),
     ("sfm_ba_destroy", _c, [ctypes.c_void_p]),
+    ("sfm_ba_lm_multi", _c, [ctypes.c_int32, _i, _i, _i32, _i32, _d, _d, _d, _d, ctypes.POINTER(BAOpts),
+                             ctypes.POINTER(BAReport), ctypes.POINTER(ctypes.c_int), _c]),
 ]
 for _name, _res, _args in SIGNATURES:
     _f = getattr(_lib, _name)
@@ -214,6 +217,20 @@ def ba_lm(cams, pts, cam_idx, pt_idx, obs, K, **opts):
     o, rep = ba_opts(**opts), BAReport()
     _check(_lib.sfm_ba_lm(len(cams), len(pts), len(ci), _p(ci, _i32), _p(pi, _i32), _p(obs), _p(K), _p(cams),
                           _p(pts), ctypes.byref(o), ctypes.byref(rep), DEVICE))
+    return cams, pts, rep.as_dict()
+
+
+def ba_lm_multi(cams, pts, cam_idx, pt_idx, obs, K, devices, **opts):
+    """Single-process multi-GPU LM: points split over `devices` (repeats allowed)."""
+    require_device()
+    cams, pts = _f64(cams).copy(), _f64(pts).copy()
+    obs, K = _f64(obs), _f64(K)
+    ci = np.ascontiguousarray(cam_idx, dtype=np.int32)
+    pi = np.ascontiguousarray(pt_idx, dtype=np.int32)
+    dev = (ctypes.c_int * len(devices))(*devices)
+    o, rep = ba_opts(**opts), BAReport()
+    _check(_lib.sfm_ba_lm_multi(len(cams), len(pts), len(ci), _p(ci, _i32), _p(pi, _i32), _p(obs), _p(K), _p(cams),
+                                _p(pts), ctypes.byref(o), ctypes.byref(rep), dev, len(devices)))
     return cams, pts, rep.as_dict()
 
 

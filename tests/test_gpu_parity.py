@@ -293,3 +293,19 @@ def test_ba_failure_contract(core, capsys):
     R1, C1, X1 = perform_bundle_adjustment(Xw, 0 * p["filtered_world_coords"], p["feature_x"], p["feature_y"],
                                            p["flags"], R0, C0, K, 2)
     assert X1 is Xw and capsys.readouterr().out == ""
+
+
+@pytest.mark.parametrize("ranks", [2, 3])
+def test_ba_multi_rank_matches_single_rank(core, ranks):
+    """The point-sharded LM (one partial reduced camera system per rank,
+    summed every iteration) on several ranks sharing the one GPU gives the
+    single-rank result: same accept/reject sequence, RMSE equal to 1e-9."""
+    p = syn.ba_problem(20, 20000, 6, seed=6, dense=False)
+    cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
+    c1, x1, r1 = core.ba_lm(cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K, max_iterations=40)
+    cN, xN, rN = core.ba_lm_multi(cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K, [0] * ranks,
+                                  max_iterations=40)
+    assert rN["n_ranks"] == ranks
+    assert rN["iterations"] == r1["iterations"] and rN["accepted"] == r1["accepted"]
+    assert abs(rN["cost"] - r1["cost"]) <= 1e-9 * r1["cost"]
+    assert np.abs(xN - x1).max() < 1e-6 and np.abs(cN - c1).max() < 1e-8

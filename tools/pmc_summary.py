@@ -1,0 +1,56 @@
+"""Summarise rocprofv3 runs into profiles/<round>/ (committed evidence).
+
+  python tools/pmc_summary.py gpurun_out/<dir> profiles/round1
+
+<dir> holds: kernel_trace/ (rocprofv3 --kernel-trace --stats) and
+FETCH_SIZE/, WRITE_SIZE/, TCC_HIT_sum_TCC_MISS_sum/ (separate --pmc passes).
+Writes kernel_stats.csv (copy), kernel_stats.md and pmc_traffic.json with
+per-launch averages per kernel.  HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) *
+1024: FETCH_SIZE/WRITE_SIZE are KiB, and on gfx950 FETCH_SIZE reports half
+of a wide coalesced read (MI355X_MICROARCH.md, HBM section).
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+
+def short(name):
+    return name.split("(")[0].replace("sfm::", "")
+
+
+def main(src, dst):
+    os.makedirs(dst, exist_ok=True)
+    ks = os.path.join(src, "kernel_trace", "run_kernel_stats.csv")
+    out = {}
+    if os.path.exists(ks):
+        shutil.copy(ks, os.path.join(dst, "kernel_stats.csv"))
+        rows = list(csv.DictReader(open(ks)))
+        with open(os.path.join(dst, "kernel_stats.md"), "w") as f:
+            f.write("| kernel | calls | avg us | total ms | % |\n|---|---|---|---|---|\n")
+            for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
+                f.write(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | "
+                        f"{float(r['TotalDurationNs']) / 1e6:.3f} | {float(r['Percentage']):.1f} |\n")
+    for tag in ("FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum_TCC_MISS_sum"):
+        f = os.path.join(src, tag, "run_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        agg = collections.defaultdict(lambda: collections.defaultdict(list))
+        for r in csv.DictReader(open(f)):
+            agg[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for k, d in agg.items():
+            for c, v in d.items():
+                out.setdefault(k, {})[c] = sum(v) / len(v)
+    for k, d in out.items():
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            d["hbm_bytes_per_launch"] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
+        if "TCC_HIT_sum" in d:
+            d["l2_hit_rate"] = d["TCC_HIT_sum"] / max(1.0, d["TCC_HIT_sum"] + d.get("TCC_MISS_sum", 0))
+    json.dump(out, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1, sort_keys=True)
+    print(json.dumps({k: {c: round(v, 1) for c, v in d.items()} for k, d in out.items() if "k_" in k}, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
