@@ -41,15 +41,16 @@ FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 vector
 
 
 def algorithmic_bytes(name, n_obs, n_pts, n_pairs, nblocks, ns):
-    """Compulsory bytes one launch of each kernel family moves."""
-    if name == "schur_blocks":
-        return 144 * n_obs + 112 * n_obs + 24 * n_pts + 8 * n_pairs + 12 * nblocks + 8 * (ns * ns + 3 * ns)
-    if name == "point_prep":
-        return 160 * n_obs + 144 * n_obs + 72 * n_pts + 72 * n_pts
-    if name == "linearize":
-        return (16 + 4 + 160) * n_obs + (24 + 72 + 4) * n_pts
-    if name == "backsub_trial":
-        return (160 + 16 + 4) * n_obs + (72 + 72 + 24 + 24 + 4) * n_pts
+    """Compulsory bytes one launch of each single-kernel family moves
+    (DESIGN.md §4): every array the kernel must read or write, once."""
+    if name == "schur_blocks":  # k_schur_pairs: Schur records (p, G) 128 B/obs, pair list, q, slab
+        return 128 * n_obs + 8 * n_pairs + 24 * n_pts + 16 * nblocks + 8 * (ns * ns + 3 * ns)
+    if name == "point_prep":    # J 96 B + cam 4 B read, Schur record 128 B written per obs; V,g / L,q per pt
+        return (96 + 4 + 128) * n_obs + (72 + 72 + 4) * n_pts
+    if name == "linearize":     # obs, cam read, J 96 B written per obs; X, V,g per pt
+        return (16 + 4 + 96) * n_obs + (24 + 72 + 4) * n_pts
+    if name == "backsub_trial": # J, obs, cam per obs; V,g, L,q, X, X' per pt
+        return (96 + 16 + 4) * n_obs + (72 + 72 + 24 + 24 + 4) * n_pts
     return None
 
 
@@ -97,6 +98,7 @@ def main():
     ap.add_argument("--workload", default="cfg4", choices=["cfg3", "cfg4", "cfg5"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ransac-hyps", type=int, default=16384)
+    ap.add_argument("--force-comm", action="store_true", help="use the RCCL communicator even with one rank")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -127,9 +129,10 @@ def main():
     ci, pi, ob, X0, (lo, hi) = sfm_dist.shard_ba(prob["cam_idx"], prob["pt_idx"], prob["obs"], prob["X0"],
                                                  world, rank)
     comm = None
-    if world > 1:
+    if world > 1 or args.force_comm:
         uid = [core.Comm.unique_id() if rank == 0 else None]
-        torch.distributed.broadcast_object_list(uid, src=0)
+        if world > 1:
+            torch.distributed.broadcast_object_list(uid, src=0)
         comm = core.Comm(uid[0], world, rank, device=local_rank)
     ba = core.BAProblem(cams0, X0, ci, pi, ob, K, comm=comm, device=local_rank)
 
@@ -183,24 +186,18 @@ def main():
     n_pairs = n_pairs_of(prob["pt_idx"][prob["pt_idx"] < hi] if world > 1 else prob["pt_idx"])
     ns = 6 * prob["n_cams"]
     nblocks = prob["n_cams"] * (prob["n_cams"] + 1) // 2
-    fam = {k: v for k, v in ktimes.items() if k != "allreduce"}
+    # dominant single kernel (the Cholesky family is a chain of ~2 launches
+    # per 16-column panel, latency-bound; it is reported in kernel_ms_per_iter)
+    fam = {k: v for k, v in ktimes.items() if algorithmic_bytes(k, 1, 1, 1, 1, 1) is not None}
     dom = max(fam, key=fam.get)
     n_obs_local, n_pts_local = len(ci), len(X0)
     alg = algorithmic_bytes(dom, n_obs_local, n_pts_local, n_pairs, nblocks, ns)
-    if alg is not None:
-        ach = alg / (ktimes[dom] * 1e-3) / 1e9
-        roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom), "algorithmic_bytes": int(alg),
-                "avg_launch_ms": round(ktimes[dom], 4),
-                "traffic_source": "profiles/round1/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE, "
-                                  "2*FETCH+WRITE KiB)"}
-    else:  # cholesky: n^3/3 flops
-        nsp = ((ns + 31) // 32) * 32
-        fl = nsp ** 3 / 3.0
-        ach = fl / (ktimes[dom] * 1e-3) / 1e12
-        roof = {"kernel": dom, "bound": "fp64", "achieved": round(ach, 4), "peak": FP64_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(ach / FP64_PEAK_TFLOPS, 5), "traffic": None,
-                "avg_launch_ms": round(ktimes[dom], 4)}
+    ach = alg / (ktimes[dom] * 1e-3) / 1e9
+    roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom), "algorithmic_bytes": int(alg),
+            "avg_launch_ms": round(ktimes[dom], 4),
+            "traffic_source": "profiles/round1/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE, "
+                              "(2*FETCH+WRITE) KiB per launch)"}
     iter_bytes = 52 * n_obs_total + 240 * prob["n_pts"]  # SURVEY §8(d) compulsory bytes / LM iteration
     ms_per_step = dt / args.steps * 1e3
     out = {

@@ -1121,8 +1121,10 @@ static int local_allreduce(sfm_ba_problem *p, double *buf, int64_t n) {
 }
 
 static int allreduce(sfm_ba_problem *p, double *buf, int64_t n) {
-    if (!p->comm || p->comm->nranks <= 1) return 0;
-    if (p->comm->local) return local_allreduce(p, buf, n);
+    if (!p->comm) return 0;
+    if (p->comm->local) return p->comm->nranks > 1 ? local_allreduce(p, buf, n) : 0;
+    // RCCL: also with a single rank (an in-place no-op), so the transport
+    // is exercised by the one-GPU tests
     ncclResult_t r = ncclAllReduce(buf, buf, (size_t)n, ncclDouble, ncclSum, p->comm->comm, p->stream);
     if (r != ncclSuccess) {
         set_error("ncclAllReduce: %s", ncclGetErrorString(r));

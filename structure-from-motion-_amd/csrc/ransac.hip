@@ -68,6 +68,8 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES) k_ransac_score(const double2
         finite &= isfinite(f[k]) ? 1 : 0;
     }
     int cnt = 0;
+    const double thr_lo = thr >= 0 ? thr * (1.0 - 1e-4) : thr * (1.0 + 1e-4);
+    const double thr_hi = thr >= 0 ? thr * (1.0 + 1e-4) : thr * (1.0 - 1e-4);
     for (int64_t base = 0; base < N; base += SCORE_TILE) {
         const int n = (int)min<int64_t>(SCORE_TILE, N - base);
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
@@ -81,7 +83,7 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES) k_ransac_score(const double2
                 bool inl = false;
                 if (i < n) {
                     const double2 p = s1[i], q = s2[i];
-                    inl = epi_inlier(f, p.x, p.y, q.x, q.y, thr);
+                    inl = epi_inlier_fast(f, p.x, p.y, q.x, q.y, thr, thr_lo, thr_hi);
                 }
                 cnt += __popcll(__ballot(inl));
             }

@@ -23,6 +23,32 @@ __device__ __forceinline__ bool epi_inlier(const double *F, double x, double y, 
     return (d1 + d2) * 0.5 < thr;
 }
 
+// Same decision, cheaper: approximate sqrt / reciprocal (v_rsq_f64,
+// v_rcp_f64, ~1e-7 relative) decide every pair whose approximate error is
+// farther than 1e-4 relative from the threshold; the rest (and any
+// non-finite / tiny operand) take the exact expression above.  The
+// decision is therefore always the exact one.
+__device__ __forceinline__ bool epi_inlier_fast(const double *F, double x, double y, double u, double v,
+                                                double thr, double thr_lo, double thr_hi) {
+    const double a0 = F[0] * x + F[1] * y + F[2];
+    const double a1 = F[3] * x + F[4] * y + F[5];
+    const double a2 = F[6] * x + F[7] * y + F[8];
+    const double b0 = F[0] * u + F[3] * v + F[6];
+    const double b1 = F[1] * u + F[4] * v + F[7];
+    const double e = u * a0 + v * a1 + a2;
+    const double ae = fabs(e);
+    const double qa = a0 * a0 + a1 * a1, qb = b0 * b0 + b1 * b1;
+    const double sa = qa * __builtin_amdgcn_rsq(qa), sb = qb * __builtin_amdgcn_rsq(qb);
+    const double ap = (ae * __builtin_amdgcn_rcp(sa + 1e-8) + ae * __builtin_amdgcn_rcp(sb + 1e-8)) * 0.5;
+    const bool sure_in = ap < thr_lo && qa > 1e-280 && qb > 1e-280;
+    const bool sure_out = ap > thr_hi && qa > 1e-280 && qb > 1e-280 && qa < 1e280 && qb < 1e280;
+    if (sure_in) return true;
+    if (sure_out) return false;
+    const double d1 = ae / (sqrt(qa) + 1e-8);
+    const double d2 = ae / (sqrt(qb) + 1e-8);
+    return (d1 + d2) * 0.5 < thr;
+}
+
 // --------------------------------------------------------------------
 // One-sided (Hestenes) Jacobi on an M x N matrix held column-major in
 // registers: a[j][i] = column j, row i.  V (N x N) accumulates rotations,
