@@ -1,0 +1,103 @@
+// Dev probe: runs the reduced-camera Cholesky kernels of ba.hip on a random
+// SPD matrix and checks them against a host Cholesky.  Not part of the product.
+// Build: hipcc -c this file to an object, link it with structure-from-motion-_amd/build/{sfm_api,ransac}.o -lrccl
+#include "../structure-from-motion-_amd/csrc/ba.hip"
+#include <cstdio>
+#include <random>
+#include <vector>
+
+static int run(int ns, int reps) {
+    const int nT = (ns + NB - 1) / NB, nsp = nT * NB;
+    std::mt19937_64 g(ns);
+    std::normal_distribution<double> nd;
+    std::vector<double> M((size_t)nsp * (nsp + 8)), S((size_t)nsp * nsp, 0.0), b(nsp);
+    for (auto &v : M) v = nd(g);
+    for (int i = 0; i < nsp; ++i)
+        for (int j = 0; j <= i; ++j) {
+            double s = 0;
+            for (int k = 0; k < nsp + 8; ++k) s += M[(size_t)i * (nsp + 8) + k] * M[(size_t)j * (nsp + 8) + k];
+            S[(size_t)i * nsp + j] = S[(size_t)j * nsp + i] = s;
+        }
+    for (auto &v : b) v = nd(g);
+    // host Cholesky + forward + back solve
+    std::vector<double> L(S), x(b);
+    for (int k = 0; k < nsp; ++k) {
+        double d = L[(size_t)k * nsp + k];
+        for (int m = 0; m < k; ++m) d -= L[(size_t)k * nsp + m] * L[(size_t)k * nsp + m];
+        d = sqrt(d);
+        L[(size_t)k * nsp + k] = d;
+        for (int i = k + 1; i < nsp; ++i) {
+            double s = L[(size_t)i * nsp + k];
+            for (int m = 0; m < k; ++m) s -= L[(size_t)i * nsp + m] * L[(size_t)k * nsp + m];
+            L[(size_t)i * nsp + k] = s / d;
+        }
+    }
+    for (int i = 0; i < nsp; ++i) {
+        double s = x[i];
+        for (int m = 0; m < i; ++m) s -= L[(size_t)i * nsp + m] * x[m];
+        x[i] = s / L[(size_t)i * nsp + i];
+    }
+    for (int i = nsp - 1; i >= 0; --i) {
+        double s = x[i];
+        for (int m = i + 1; m < nsp; ++m) s -= L[(size_t)m * nsp + i] * x[m];
+        x[i] = s / L[(size_t)i * nsp + i];
+    }
+    double *dA, *dA0, *db, *db0;
+    int *dbad;
+    double *dD;
+    hipMalloc(&dD, NB * NB * 8);
+    hipMalloc(&dA, S.size() * 8); hipMalloc(&dA0, S.size() * 8);
+    hipMalloc(&db, nsp * 8); hipMalloc(&db0, nsp * 8);
+    hipMalloc(&dbad, 4); hipMemset(dbad, 0, 4);
+    hipMemcpy(dA0, S.data(), S.size() * 8, hipMemcpyHostToDevice);
+    hipMemcpy(db0, b.data(), nsp * 8, hipMemcpyHostToDevice);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0); hipEventCreate(&e1);
+    float best = 1e30f;
+    for (int r = 0; r < reps; ++r) {
+        hipMemcpy(dA, dA0, S.size() * 8, hipMemcpyDeviceToDevice);
+        hipMemcpy(db, db0, nsp * 8, hipMemcpyDeviceToDevice);
+        hipEventRecord(e0, 0);
+        {
+            for (int kt = 0; kt < nT; ++kt) {
+                hipLaunchKernelGGL(k_chol_panel, dim3(nT - kt), dim3(64), 0, 0, dA, nsp, kt, dD, db, dbad);
+                const int T = nT - kt - 1;
+                hipLaunchKernelGGL(k_chol_update, dim3(T * (T + 1) / 2 + 1), dim3(256), 0, 0, dA, nsp, kt, dD, db);
+            }
+            hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(SOLVE_THREADS), 0, 0, dA, nsp, db);
+        }
+        hipEventRecord(e1, 0);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        best = std::min(best, ms);
+    }
+    std::vector<double> A(S.size()), xo(nsp);
+    hipMemcpy(A.data(), dA, S.size() * 8, hipMemcpyDeviceToHost);
+    hipMemcpy(xo.data(), db, nsp * 8, hipMemcpyDeviceToHost);
+    int bad;
+    hipMemcpy(&bad, dbad, 4, hipMemcpyDeviceToHost);
+    double eL = 0, ex = 0, sx = 0;
+    int worst_i = -1, worst_j = -1;
+    for (int i = 0; i < nsp; ++i) {
+        for (int j = 0; j <= i; ++j) {
+            double e = fabs(A[(size_t)i * nsp + j] - L[(size_t)i * nsp + j]);
+            if (!std::isfinite(e)) e = 1e300;
+            if (e > eL) { eL = e; worst_i = i; worst_j = j; }
+        }
+        ex = std::max(ex, std::isfinite(xo[i]) ? fabs(xo[i] - x[i]) : 1e300);
+        sx = std::max(sx, fabs(x[i]));
+    }
+    printf("ns=%d nsp=%d bad=%d maxerr_L=%.3e at (%d,%d) maxerr_x=%.3e (|x|max %.3e) best_ms=%.4f\n", ns, nsp, bad, eL,
+           worst_i, worst_j, ex, sx, best);
+    return (bad == 0 && eL < 1e-8 && ex < 1e-6 * (1 + sx)) ? 0 : 1;
+}
+
+int main(int argc, char **argv) {
+    int fails = 0;
+    for (int ns : {48, 128, 256, 272, 300, 512, 1200}) {
+        fails += run(ns, ns > 600 ? 5 : 20);
+    }
+    printf("%s\n", fails ? "FAIL" : "OK");
+    return fails;
+}

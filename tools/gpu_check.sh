@@ -7,12 +7,13 @@ cd "$(dirname "$0")/.."
 make -s -j8 -C structure-from-motion-_amd
 make -s -C oracle
 TAG=${1:-}
-CMD='timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1; echo EXIT $? >> gpurun_out/gpu_tests.log; timeout -k 10 300 python tools/probe_ba.py > gpurun_out/probe.log 2>&1; echo EXIT $? >> gpurun_out/probe.log'
+# steps chained with && so nothing else touches the GPU after a failure
+CMD='timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1 && timeout -k 10 300 python tools/probe_ba.py > gpurun_out/probe.log 2>&1'
 if [ -n "$TAG" ]; then
-  CMD="$CMD; cd /tmp && export TMPDIR=/tmp && cd \$GRAFT_REPO_ROOT && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/$TAG -o run --output-format csv -- python bench.py --no-cpu-baseline > gpurun_out/bench_prof.log 2>&1"
+  CMD="$CMD && cd /tmp && export TMPDIR=/tmp && cd \$GRAFT_REPO_ROOT && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/$TAG -o run --output-format csv -- python bench.py --no-cpu-baseline > gpurun_out/bench_prof.log 2>&1"
 fi
 timeout 1700 /usr/local/graft/bin/gpurun --timeout 1000 -- "$CMD" 2>&1 | tail -1
-tail -2 gpurun_out/gpu_tests.log
+rm -f gpurun_out/probe.log.stale; tail -2 gpurun_out/gpu_tests.log
 grep -E "cfg|fixed|EXIT|Err" gpurun_out/probe.log || true
 if [ -n "$TAG" ]; then
 python3 - "$TAG" <<'PY'
