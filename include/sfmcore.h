@@ -81,6 +81,19 @@ int sfm_triangulate_dlt(const double *P1, const double *P2, const double *x1, co
                         int64_t N, double *X, int device);
 
 /* ---------------------------------------------------------------------
+ * NonLinearTriangulation (NonLinearTriangulation.py:53-121): per point,
+ * scipy least_squares(method='lm', max_nfev) of the 4-residual Loss
+ * (:5-50) from X0[i]; MINPACK lmdif semantics (diag = ones, factor 100,
+ * forward differences, ftol = xtol = gtol = 1e-8).  Rows where the
+ * reference's try/except keeps X0 (x0 with a NaN, non-finite residuals at
+ * x0) are copied through.  info (N, nullable): MINPACK info 1..8, or -1
+ * for a copied-through row.
+ * ------------------------------------------------------------------- */
+int sfm_triangulate_nonlinear(const double *P1, const double *P2, const double *x1, const double *x2,
+                              const double *X0, int64_t N, int32_t max_nfev, double *X, int32_t *info,
+                              int device);
+
+/* ---------------------------------------------------------------------
  * BundleAdjustment (BundleAdjustment.py:8-242)
  * Camera parameters are the reference's: [rotvec(3), t(3)] with
  * x_cam = R(rotvec) X + t, proj = K x_cam [:2] / (K x_cam [2] + 1e-8),

@@ -58,6 +58,7 @@ def lib():
                                 _d, _d, ctypes.POINTER(BAOpts), ctypes.POINTER(BAReport)]
         L.orc_ba_lm.restype = ctypes.c_int
         L.orc_rotvec_to_R.argtypes = [_d, _d]
+        L.orc_nltri.argtypes = [_d, _d, _d, _d, _d, ctypes.c_int64, ctypes.c_int32, _d, _i32]
         L.orc_R_to_rotvec.argtypes = [_d, _d]
         _LIB = L
     return _LIB
@@ -121,6 +122,17 @@ def triangulate(K, C1, R1, C2, R2, x1, x2):
     X = np.zeros((len(x1), 3))
     lib().orc_triangulate(_p(P1), _p(P2), _p(x1), _p(x2), len(x1), _p(X))
     return X
+
+
+def nltri(K, C1, R1, C2, R2, x1, x2, X0, max_nfev=50):
+    """NonLinearTriangulation.py:53-121 (per-point scipy 'lm').
+    Returns (X (N,3), info (N,) MINPACK info or -1 for the exception path)."""
+    P1, P2 = f64(projection(K, C1, R1)), f64(projection(K, C2, R2))
+    x1, x2, X0 = f64(np.reshape(x1, (-1, 2))), f64(np.reshape(x2, (-1, 2))), f64(np.reshape(X0, (-1, 3)))
+    X = np.zeros((len(x1), 3))
+    info = np.zeros(len(x1), dtype=np.int32)
+    lib().orc_nltri(_p(P1), _p(P2), _p(x1), _p(x2), _p(X0), len(x1), max_nfev, _p(X), _p(info, _i32))
+    return X, info
 
 
 def ba_residuals(cams, pts, cam_idx, pt_idx, obs, K):

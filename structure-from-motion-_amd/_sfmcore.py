@@ -62,6 +62,7 @@ SIGNATURES = [
     ("sfm_f8_general", _c, [_d, _d, _i, _d, _c]),
     ("sfm_ransac_f8", _c, [_d, _d, _i, _i32, _i, ctypes.c_double, _i32, _i64, _d, _u8, _c]),
     ("sfm_triangulate_dlt", _c, [_d, _d, _d, _d, _i, _d, _c]),
+    ("sfm_triangulate_nonlinear", _c, [_d, _d, _d, _d, _d, _i, ctypes.c_int32, _d, _i32, _c]),
     ("sfm_project_points", _c, [_d, _d, _i, _d, _c]),
     ("sfm_ba_residuals", _c, [ctypes.c_int32, _i, _i, _i32, _i32, _d, _d, _d, _d, _d, _c]),
     ("sfm_ba_lm", _c, [ctypes.c_int32, _i, _i, _i32, _i32, _d, _d, _d, _d, ctypes.POINTER(BAOpts),
@@ -180,6 +181,19 @@ def triangulate(P1, P2, x1, x2):
     X = np.zeros((len(x1), 3))
     _check(_lib.sfm_triangulate_dlt(_p(P1), _p(P2), _p(x1), _p(x2), len(x1), _p(X), DEVICE))
     return X
+
+
+def triangulate_nonlinear(P1, P2, x1, x2, X0, max_nfev=50):
+    """Returns (X (N,3), info (N,) int32): MINPACK info, -1 = x0 kept."""
+    require_device()
+    P1, P2 = _f64(P1), _f64(P2)
+    x1, x2 = _f64(np.reshape(x1, (-1, 2))), _f64(np.reshape(x2, (-1, 2)))
+    X0 = _f64(np.reshape(X0, (-1, 3)))
+    X = np.zeros((len(x1), 3))
+    info = np.zeros(len(x1), dtype=np.int32)
+    _check(_lib.sfm_triangulate_nonlinear(_p(P1), _p(P2), _p(x1), _p(x2), _p(X0), len(x1), int(max_nfev), _p(X),
+                                          _p(info, _i32), DEVICE))
+    return X, info
 
 
 def project(P, X):

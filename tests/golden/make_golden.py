@@ -22,6 +22,11 @@ Outputs (tests/golden/*.npz):
                      (s=0) and 2000 (s=1,2): outputs + per-hypothesis counts.
   triangulation.npz  LinearTriangulation on the four P3Data 1_2 pose
                      candidates and on cfg2's clean 5000 points.
+  nltri.npz          NonLinearTriangulation (per-point scipy 'lm', max_nfev=50)
+                     on the four P3Data 1_2 pose candidates, on cfg2's noisy
+                     inliers, on cfg2 outliers (hard, often non-converging
+                     cases) and on crafted edge rows (non-finite x0, x0 on a
+                     camera centre, points on a principal plane).
   ba.npz             perform_bundle_adjustment as shipped on tiny problems,
                      and the converged least-squares oracle on the same
                      residual function (scipy trf + jac_sparsity).
@@ -54,8 +59,9 @@ def _import_reference():
     import EssentialMatrixFromFundamentalMatrix as ref_e  # noqa
     import ExtractCameraPose as ref_p  # noqa
     import Utils as ref_u  # noqa
+    import NonLinearTriangulation as ref_nt  # noqa
     return types.SimpleNamespace(f=ref_f, r=ref_r, t=ref_t, ba=ref_ba, h=ref_h, e=ref_e,
-                                 p=ref_p, u=ref_u)
+                                 p=ref_p, u=ref_u, nt=ref_nt)
 
 
 def state_to_array(st):
@@ -246,6 +252,41 @@ def gen_ba(ref, skip_cfg3):
     np.savez_compressed(os.path.join(HERE, "ba.npz"), **out)
 
 
+def gen_nltri(ref):
+    K = syn.K_REF
+    tri = np.load(os.path.join(HERE, "triangulation.npz"))
+    out = {}
+    for i in range(4):  # P3Data 1_2, the four pose candidates, as Wrapper_dev.py:187 would
+        out[f"p3_X{i}"] = ref.nt.nonlinear_triangulation(K, np.zeros(3), np.eye(3), tri["p3_Cset"][i],
+                                                         tri["p3_Rset"][i], tri["p3_x1"], tri["p3_x2"],
+                                                         tri[f"p3_X{i}"])
+    # cfg2 noisy inliers (linear triangulation as x0), full 5000
+    x1, x2, X0 = tri["syn_x1"], tri["syn_x2"], tri["syn_X"]
+    t = time.time()
+    Xs = ref.nt.NonLinearTriangulation(K, np.zeros(3), np.eye(3), tri["syn_C2"], tri["syn_R2"], x1, x2, X0)
+    out["syn_seconds"] = np.array(time.time() - t)
+    out["syn_X"] = Xs
+    # cfg2 outliers: x2 replaced by uniform pixels -> x0 from linear triangulation is far off
+    ox1, ox2, _, meta = syn.two_view(seed=0)
+    sel = meta["outliers"][:1500]
+    oX0 = ref.t.LinearTriangulation(K, np.zeros(3), np.eye(3), meta["C2"], meta["R2"], ox1[sel], ox2[sel])
+    # crafted edge rows appended: non-finite x0, x0 on camera 1's centre,
+    # x0 on camera 2's centre, x0 on camera 1's principal plane, huge x0
+    C2 = meta["C2"]
+    e_x1 = np.array([[320.0, 240.0]] * 6)
+    e_x2 = np.array([[300.0, 250.0]] * 6)
+    e_X0 = np.array([[np.nan, 0, 5], [np.inf, 0, 5], [0.0, 0.0, 0.0], C2, [1.0, 2.0, 0.0], [1e12, -3e12, 4e12]])
+    ex1 = np.vstack([ox1[sel], e_x1])
+    ex2 = np.vstack([ox2[sel], e_x2])
+    eX0 = np.vstack([oX0, e_X0])
+    with np.errstate(all="ignore"):
+        eX = ref.nt.NonLinearTriangulation(K, np.zeros(3), np.eye(3), C2, meta["R2"], ex1, ex2, eX0)
+    out["out_x1"], out["out_x2"], out["out_X0"], out["out_C2"], out["out_R2"], out["out_X"] = \
+        ex1, ex2, eX0, C2, meta["R2"], eX
+    np.savez_compressed(os.path.join(HERE, "nltri.npz"), **out)
+    print(f"nltri: p3 4x{len(tri['p3_x1'])}, syn {len(Xs)} in {float(out['syn_seconds']):.1f}s, hard {len(eX)}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-cfg3", action="store_true")
@@ -262,6 +303,8 @@ def main():
         gen_cfg2(ref)
     if not only or "tri" in only:
         gen_triangulation(ref, p3)
+    if not only or "nltri" in only:
+        gen_nltri(ref)
     if not only or "ba" in only:
         gen_ba(ref, a.skip_cfg3)
 

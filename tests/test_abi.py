@@ -49,6 +49,9 @@ REFERENCE_SIGNATURES = {
     ("GetInliersRANSAC", "EstimateFundamentalMatrix"): "(points1, points2)",
     ("LinearTriangulation", "LinearTriangulation"): "(K, C1, R1, C2, R2, x1, x2)",
     ("LinearTriangulation", "linear_triangulation"): "(K, C1, R1, C2, R2, x1, x2)",
+    ("NonLinearTriangulation", "Loss"): "(X, x1, x2, P1, P2)",
+    ("NonLinearTriangulation", "NonLinearTriangulation"): "(K, C1, R1, C2, R2, x1, x2, x0)",
+    ("NonLinearTriangulation", "nonlinear_triangulation"): "(K, C1, R1, C2, R2, x1, x2, x0)",
     ("BundleAdjustment", "project_points"): "(K, C, R, X)",
     ("BundleAdjustment", "bundle_adjustment_residuals"):
         "(params, n_cameras, n_points, camera_indices, point_indices, points_2d, K, n_cam_params=6)",

@@ -83,6 +83,29 @@ def test_triangulation_matches_reference(golden):
     assert rel.max() < 1e-9
 
 
+def _nltri_sets(t, g):
+    """(label, C2, R2, x1, x2, X0, expected) for every nltri.npz case."""
+    for i in range(4):
+        yield (f"p3_{i}", t["p3_Cset"][i], t["p3_Rset"][i], t["p3_x1"], t["p3_x2"], t[f"p3_X{i}"], g[f"p3_X{i}"])
+    yield ("cfg2", t["syn_C2"], t["syn_R2"], t["syn_x1"], t["syn_x2"], t["syn_X"], g["syn_X"])
+    yield ("hard", g["out_C2"], g["out_R2"], g["out_x1"], g["out_x2"], g["out_X0"], g["out_X"])
+
+
+def test_nltri_oracle_bit_exact_vs_reference(golden):
+    """The lmdif restatement reproduces scipy's per-point 'lm' bit for bit,
+    including non-converging outliers and the x0-kept exception rows."""
+    t, g = golden("triangulation.npz"), golden("nltri.npz")
+    n = 0
+    for label, C2, R2, x1, x2, X0, Xr in _nltri_sets(t, g):
+        X, info = O.nltri(K, np.zeros(3), np.eye(3), C2, R2, x1, x2, X0)
+        assert np.array_equal(X, Xr, equal_nan=True), label
+        n += len(X)
+    assert n == 4 * 14 + 5000 + 1506
+    # the hard set exercises every exit: converged (1-3), max_nfev (5) and kept x0 (-1)
+    _, info = O.nltri(K, np.zeros(3), np.eye(3), g["out_C2"], g["out_R2"], g["out_x1"], g["out_x2"], g["out_X0"])
+    assert {-1, 1, 2, 3, 5} <= set(np.unique(info).tolist())
+
+
 @pytest.mark.parametrize("name,shape", [("tiny2", (2, 20, 2)), ("tiny", (3, 30, 3)),
                                         ("small", (6, 200, 4)), ("cfg3", (6, 2000, 5))])
 def test_ba_oracle_matches_converged_reference(golden, name, shape):
