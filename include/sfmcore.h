@@ -74,6 +74,23 @@ int sfm_ransac_f8(const double *x1, const double *x2, int64_t N, const int32_t *
                   uint8_t *best_mask, int device);
 
 /* ---------------------------------------------------------------------
+ * Homography (GetHomographyInliers.py)
+ * sfm_h4_batch: find_homography (:4-85) on H independent 4-point samples
+ *   (x1s, x2s: H x 4 x 2) -> Hout (H x 9), each normalised by H[2,2].
+ * sfm_homography_general: find_homography on N >= 4 points -> Hout (9).
+ * sfm_ransac_h4: get_homography_inliers' loop (:124-157) over a host-drawn
+ *   H x 4 sample table: per hypothesis the transfer error
+ *   |H x1 / (t2 + 1e-8) - x2| < thr is counted; the winner is the first
+ *   hypothesis with the strictly largest positive count (-1 if none);
+ *   H_best (9) and best_mask (N) are written when *best_iter >= 0.
+ * ------------------------------------------------------------------- */
+int sfm_h4_batch(const double *x1s, const double *x2s, int64_t H, double *Hout, int device);
+int sfm_homography_general(const double *x1, const double *x2, int64_t N, double *Hout, int device);
+int sfm_ransac_h4(const double *x1, const double *x2, int64_t N, const int32_t *samples, int64_t H,
+                  double thr, int32_t *counts_out, int64_t *best_iter, double *H_best,
+                  uint8_t *best_mask, int device);
+
+/* ---------------------------------------------------------------------
  * LinearTriangulation (LinearTriangulation.py:3-92)
  * P1, P2: 3 x 4 projection matrices K[R | -RC]; x1, x2: N x 2; X: N x 3.
  * ------------------------------------------------------------------- */

@@ -58,6 +58,11 @@ def lib():
                                 _d, _d, ctypes.POINTER(BAOpts), ctypes.POINTER(BAReport)]
         L.orc_ba_lm.restype = ctypes.c_int
         L.orc_rotvec_to_R.argtypes = [_d, _d]
+        L.orc_homography.argtypes = [_d, _d, ctypes.c_int64, _d]
+        L.orc_homography.restype = ctypes.c_int
+        L.orc_h_score.argtypes = [_d, _d, ctypes.c_int64, _d, ctypes.c_int64, ctypes.c_double, _i32]
+        L.orc_ransac_h.argtypes = [_d, _d, ctypes.c_int64, _i32, ctypes.c_int64, ctypes.c_double, _i32, _d, _u8]
+        L.orc_ransac_h.restype = ctypes.c_int64
         L.orc_nltri.argtypes = [_d, _d, _d, _d, _d, ctypes.c_int64, ctypes.c_int32, _d, _i32]
         L.orc_R_to_rotvec.argtypes = [_d, _d]
         _LIB = L
@@ -109,6 +114,35 @@ def ransac(x1, x2, samples, thr=0.06):
     best = lib().orc_ransac(_p(x1), _p(x2), len(x1), _p(samples, _i32), H, k, thr,
                             _p(counts, _i32), _p(F), _p(m, _u8))
     return int(best), counts, F.reshape(3, 3), m.astype(bool)
+
+
+def homography(p1, p2):
+    """find_homography (GetHomographyInliers.py:4-85)."""
+    p1, p2 = f64(p1), f64(p2)
+    H = np.zeros(9)
+    if lib().orc_homography(_p(p1), _p(p2), len(p1), _p(H)) != 0:
+        raise ValueError("At least 4 point correspondences are required for homography estimation")
+    return H.reshape(3, 3)
+
+
+def h_score(x1, x2, Hs, thr=30.0):
+    x1, x2 = f64(x1), f64(x2)
+    Hs = f64(np.reshape(Hs, (-1, 9)))
+    counts = np.zeros(len(Hs), dtype=np.int32)
+    lib().orc_h_score(_p(x1), _p(x2), len(x1), _p(Hs), len(Hs), thr, _p(counts, _i32))
+    return counts
+
+
+def ransac_h(x1, x2, samples, thr=30.0):
+    """Returns (best_iter or -1, counts, H_best, mask)."""
+    x1, x2 = f64(x1), f64(x2)
+    samples = np.ascontiguousarray(samples, dtype=np.int32)
+    counts = np.zeros(len(samples), dtype=np.int32)
+    H = np.zeros(9)
+    m = np.zeros(len(x1), dtype=np.uint8)
+    best = lib().orc_ransac_h(_p(x1), _p(x2), len(x1), _p(samples, _i32), len(samples), thr, _p(counts, _i32),
+                              _p(H), _p(m, _u8))
+    return int(best), counts, H.reshape(3, 3), m.astype(bool)
 
 
 def projection(K, C, R):

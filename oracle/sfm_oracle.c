@@ -19,6 +19,10 @@
  *                     distance, strict '<' threshold)
  *   orc_ransac        GetInliersRANSAC.py:53-106           (strict '>' best
  *                     update: earliest iteration wins ties)
+ *   orc_homography    GetHomographyInliers.py:4-85         (DLT on 2N x 9; the
+ *                     3x3 products reproduce OpenBLAS dgemm's fma chain)
+ *   orc_ransac_h      GetHomographyInliers.py:88-165       (transfer error
+ *                     |H x1 / (t2 + 1e-8) - x2| < thr, strict '>' update)
  *   orc_triangulate   LinearTriangulation.py:44-92         (4x4 DLT, Vt[-1])
  *   orc_ba_residuals  BundleAdjustment.py:43-110           (r = obs - proj,
  *                     proj = K(RX+t)[:2] / (K(RX+t)[2] + 1e-8))
@@ -238,6 +242,138 @@ int64_t orc_ransac(const double *x1, const double *x2, int64_t n, const int32_t 
         }
     }
     if (best >= 0 && mask) orc_ransac_mask(x1, x2, n, F_best, thr, mask);
+    return best;
+}
+
+/* ---------------------------------------------------------------- H */
+/* numpy 3x3 @ 3x3 (OpenBLAS dgemm): acc = a0 b0; acc = fma(a1, b1, acc);
+ * acc = fma(a2, b2, acc) -- measured against exact arithmetic */
+static void mm3_blas(const double *A, const double *B, double *C) {
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c)
+            C[r * 3 + c] = fma(A[r * 3 + 2], B[6 + c], fma(A[r * 3 + 1], B[3 + c], A[r * 3] * B[c]));
+}
+
+/* Null vector of an m x 9 row-major matrix (m >= 8): QR pre-reduction to
+ * 9 rows when m > 9, then one-sided Jacobi; A is destroyed. */
+static void null_vector_9(double *A, int64_t m, double *f) {
+    double V[81], s[9];
+    if (m > 9) {
+        for (int k = 0; k < 9; ++k) {
+            double nrm = 0;
+            for (int64_t i = k; i < m; ++i) nrm += A[i * 9 + k] * A[i * 9 + k];
+            nrm = sqrt(nrm);
+            if (nrm == 0) continue;
+            double alpha = A[k * 9 + k] > 0 ? -nrm : nrm;
+            double v0 = A[k * 9 + k] - alpha;
+            double vtv = v0 * v0;
+            for (int64_t i = k + 1; i < m; ++i) vtv += A[i * 9 + k] * A[i * 9 + k];
+            for (int j = k + 1; j < 9; ++j) {
+                double d = v0 * A[k * 9 + j];
+                for (int64_t i = k + 1; i < m; ++i) d += A[i * 9 + k] * A[i * 9 + j];
+                double fct = 2.0 * d / vtv;
+                A[k * 9 + j] -= fct * v0;
+                for (int64_t i = k + 1; i < m; ++i) A[i * 9 + j] -= fct * A[i * 9 + k];
+            }
+            A[k * 9 + k] = alpha;
+            for (int64_t i = k + 1; i < m; ++i) A[i * 9 + k] = 0.0;
+        }
+        jacobi_svd(A, 9, 9, V, s);
+    } else {
+        jacobi_svd(A, (int)m, 9, V, s);
+    }
+    int j = argmin(s, 9);
+    for (int k = 0; k < 9; ++k) f[k] = V[k * 9 + j];
+}
+
+/* find_homography (GetHomographyInliers.py:4-85) for n >= 4 points.
+ * Returns 0, or -1 if n < 4 (the reference raises ValueError). */
+int orc_homography(const double *p1, const double *p2, int64_t n, double *H_out) {
+    if (n < 4) return -1;
+    double m1x = 0, m1y = 0, m2x = 0, m2y = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        m1x += p1[2 * i]; m1y += p1[2 * i + 1];
+        m2x += p2[2 * i]; m2y += p2[2 * i + 1];
+    }
+    m1x /= (double)n; m1y /= (double)n; m2x /= (double)n; m2y /= (double)n;
+    double d1 = 0, d2 = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        double ax = p1[2 * i] - m1x, ay = p1[2 * i + 1] - m1y;
+        double bx = p2[2 * i] - m2x, by = p2[2 * i + 1] - m2y;
+        d1 += sqrt(ax * ax + ay * ay);
+        d2 += sqrt(bx * bx + by * by);
+    }
+    double s1 = sqrt(2.0) / (d1 / (double)n + 1e-8);
+    double s2 = sqrt(2.0) / (d2 / (double)n + 1e-8);
+    double o1x = -s1 * m1x, o1y = -s1 * m1y, o2x = -s2 * m2x, o2y = -s2 * m2y;
+    double *A = (double *)malloc(sizeof(double) * (size_t)(2 * n) * 9);
+    for (int64_t i = 0; i < n; ++i) {  /* :59-71 */
+        double a = s1 * p1[2 * i] + o1x, b = s1 * p1[2 * i + 1] + o1y;
+        double c = s2 * p2[2 * i] + o2x, d = s2 * p2[2 * i + 1] + o2y;
+        double *r0 = A + (2 * i) * 9, *r1 = r0 + 9;
+        r0[0] = 0; r0[1] = 0; r0[2] = 0; r0[3] = -a; r0[4] = -b; r0[5] = -1; r0[6] = d * a; r0[7] = d * b; r0[8] = d;
+        r1[0] = a; r1[1] = b; r1[2] = 1; r1[3] = 0; r1[4] = 0; r1[5] = 0; r1[6] = -c * a; r1[7] = -c * b; r1[8] = -c;
+    }
+    double f[9];
+    null_vector_9(A, 2 * n, f);
+    free(A);
+    /* inv(T2) as LAPACK getri forms it for this upper-triangular T2 */
+    double is = 1.0 / s2;
+    double Ti[9] = {is, -0.0, -(o2x * is), 0.0, is, -(o2y * is), 0.0, 0.0, 1.0};
+    double T1[9] = {s1, 0.0, o1x, 0.0, s1, o1y, 0.0, 0.0, 1.0};
+    double M[9], G[9];
+    mm3_blas(Ti, f, M);
+    mm3_blas(M, T1, G);
+    double d = G[8];
+    for (int k = 0; k < 9; ++k) H_out[k] = G[k] / d;  /* :83 */
+    return 0;
+}
+
+/* GetHomographyInliers.py:134-146: transfer error test of one point */
+static inline int hom_inlier(const double *H, double x, double y, double u, double v, double thr) {
+    double t0 = fma(H[1], y, H[0] * x) + H[2];
+    double t1 = fma(H[4], y, H[3] * x) + H[5];
+    double t2 = fma(H[7], y, H[6] * x) + H[8];
+    double w = t2 + 1e-8;
+    double d0 = t0 / w - u, d1 = t1 / w - v;
+    return sqrt(d0 * d0 + d1 * d1) < thr;
+}
+
+void orc_h_score(const double *x1, const double *x2, int64_t n, const double *Hs, int64_t nh, double thr,
+                 int32_t *counts) {
+    for (int64_t h = 0; h < nh; ++h) {
+        int32_t c = 0;
+        for (int64_t i = 0; i < n; ++i)
+            c += hom_inlier(Hs + 9 * h, x1[2 * i], x1[2 * i + 1], x2[2 * i], x2[2 * i + 1], thr);
+        counts[h] = c;
+    }
+}
+
+/* get_homography_inliers' loop over precomputed 4-point samples (H x 4).
+ * Returns the winning iteration or -1; mask (nullable) its inliers. */
+int64_t orc_ransac_h(const double *x1, const double *x2, int64_t n, const int32_t *samples, int64_t nh,
+                     double thr, int32_t *counts, double *H_best, uint8_t *mask) {
+    int64_t best = -1;
+    int32_t best_c = 0;
+    double p1[8], p2[8], Hm[9];
+    for (int64_t h = 0; h < nh; ++h) {
+        for (int j = 0; j < 4; ++j) {
+            int32_t s = samples[h * 4 + j];
+            p1[2 * j] = x1[2 * s]; p1[2 * j + 1] = x1[2 * s + 1];
+            p2[2 * j] = x2[2 * s]; p2[2 * j + 1] = x2[2 * s + 1];
+        }
+        int32_t c = 0;
+        orc_homography(p1, p2, 4, Hm);
+        orc_h_score(x1, x2, n, Hm, 1, thr, &c);
+        if (counts) counts[h] = c;
+        if (c > best_c) {
+            best_c = c; best = h;
+            memcpy(H_best, Hm, sizeof Hm);
+        }
+    }
+    if (best >= 0 && mask)
+        for (int64_t i = 0; i < n; ++i)
+            mask[i] = (uint8_t)hom_inlier(H_best, x1[2 * i], x1[2 * i + 1], x2[2 * i], x2[2 * i + 1], thr);
     return best;
 }
 

@@ -61,6 +61,9 @@ SIGNATURES = [
     ("sfm_f8_batch", _c, [_d, _d, _i, _d, _c]),
     ("sfm_f8_general", _c, [_d, _d, _i, _d, _c]),
     ("sfm_ransac_f8", _c, [_d, _d, _i, _i32, _i, ctypes.c_double, _i32, _i64, _d, _u8, _c]),
+    ("sfm_h4_batch", _c, [_d, _d, _i, _d, _c]),
+    ("sfm_homography_general", _c, [_d, _d, _i, _d, _c]),
+    ("sfm_ransac_h4", _c, [_d, _d, _i, _i32, _i, ctypes.c_double, _i32, _i64, _d, _u8, _c]),
     ("sfm_triangulate_dlt", _c, [_d, _d, _d, _d, _i, _d, _c]),
     ("sfm_triangulate_nonlinear", _c, [_d, _d, _d, _d, _d, _i, ctypes.c_int32, _d, _i32, _c]),
     ("sfm_project_points", _c, [_d, _d, _i, _d, _c]),
@@ -173,6 +176,43 @@ def ransac_f8(x1, x2, samples, thr, want_counts=False, device=None):
     if b < 0:
         return -1, None, np.zeros(N, dtype=bool), counts
     return b, F.reshape(3, 3), mask.astype(bool), counts
+
+
+def h4_batch(x1s, x2s):
+    """H independent 4-point homographies; x1s, x2s: (H, 4, 2)."""
+    require_device()
+    x1s, x2s = _f64(x1s), _f64(x2s)
+    H = x1s.shape[0]
+    out = np.zeros((H, 9))
+    _check(_lib.sfm_h4_batch(_p(x1s), _p(x2s), H, _p(out), DEVICE))
+    return out.reshape(H, 3, 3)
+
+
+def homography_general(x1, x2):
+    require_device()
+    x1, x2 = _f64(x1), _f64(x2)
+    out = np.zeros(9)
+    _check(_lib.sfm_homography_general(_p(x1), _p(x2), len(x1), _p(out), DEVICE))
+    return out.reshape(3, 3)
+
+
+def ransac_h4(x1, x2, samples, thr, want_counts=False, device=None):
+    """Returns (best_iter or -1, H_best (3,3) or None, mask (N,) bool, counts or None)."""
+    require_device()
+    x1, x2 = _f64(x1), _f64(x2)
+    samples = np.ascontiguousarray(samples, dtype=np.int32)
+    N, H = len(x1), len(samples)
+    counts = np.zeros(H, dtype=np.int32) if want_counts else None
+    best = np.zeros(1, dtype=np.int64)
+    Hb = np.zeros(9)
+    mask = np.zeros(N, dtype=np.uint8)
+    _check(_lib.sfm_ransac_h4(_p(x1), _p(x2), N, _p(samples, _i32), H, float(thr),
+                              _p(counts, _i32) if want_counts else None, _p(best, _i64), _p(Hb),
+                              _p(mask, _u8), DEVICE if device is None else device))
+    b = int(best[0])
+    if b < 0:
+        return -1, None, np.zeros(N, dtype=bool), counts
+    return b, Hb.reshape(3, 3), mask.astype(bool), counts
 
 
 def triangulate(P1, P2, x1, x2):

@@ -1,151 +1,6 @@
-// Batched fundamental-matrix RANSAC for gfx950 (GetInliersRANSAC.py:5-106).
-//
-//   k_f8_samples   one thread per hypothesis: gather the 8 sampled
-//                  correspondences, Hartley-normalise, LQ null vector,
-//                  rank-2 projection, denormalise (EstimateFundamentalMatrix).
-//   k_ransac_score one WAVE per hypothesis: F is wave-uniform (scalar
-//                  registers); correspondence tiles are staged once per
-//                  workgroup in LDS and every wave sweeps them, one
-//                  correspondence per lane; inlier count = popcount of the
-//                  wave ballot (scalar unit).
-//   k_ransac_select one workgroup: (max count, min iteration) reduction ==
-//                  the reference's strict '>' update (GetInliersRANSAC.py:85),
-//                  then the inlier mask of the winner.
-#include "sfm_common.hpp"
-#include "sfm_geom.hpp"
-
-namespace sfm {
-
-constexpr int SCORE_WAVES = 8;          // hypotheses per workgroup
-constexpr int SCORE_TILE = 1024;        // correspondences per LDS tile (32 KiB)
-
-__global__ void __launch_bounds__(256) k_f8_samples(const double2 *__restrict__ x1,
-                                                    const double2 *__restrict__ x2,
-                                                    const int32_t *__restrict__ samples, int64_t H,
-                                                    double *__restrict__ F) {
-    const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (h >= H) return;
-    double ax[8], ay[8], bx[8], by[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int32_t s = samples[h * 8 + i];
-        const double2 p = x1[s], q = x2[s];
-        ax[i] = p.x; ay[i] = p.y; bx[i] = q.x; by[i] = q.y;
-    }
-    f8_points(ax, ay, bx, by, F + 9 * h);
-}
-
-__global__ void __launch_bounds__(256) k_f8_points(const double2 *__restrict__ x1s,
-                                                   const double2 *__restrict__ x2s, int64_t H,
-                                                   double *__restrict__ F) {
-    const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (h >= H) return;
-    double ax[8], ay[8], bx[8], by[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const double2 p = x1s[h * 8 + i], q = x2s[h * 8 + i];
-        ax[i] = p.x; ay[i] = p.y; bx[i] = q.x; by[i] = q.y;
-    }
-    f8_points(ax, ay, bx, by, F + 9 * h);
-}
-
-__global__ void __launch_bounds__(64 * SCORE_WAVES) k_ransac_score(const double2 *__restrict__ x1,
-                                                                   const double2 *__restrict__ x2,
-                                                                   int64_t N, const double *__restrict__ F,
-                                                                   int64_t H, double thr,
-                                                                   int32_t *__restrict__ counts) {
-    __shared__ double2 s1[SCORE_TILE];
-    __shared__ double2 s2[SCORE_TILE];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t h = (int64_t)blockIdx.x * SCORE_WAVES + wave;
-    const bool active = h < H;
-    double f[9];
-    int finite = 1;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        f[k] = active ? F[9 * h + k] : 0.0;
-        finite &= isfinite(f[k]) ? 1 : 0;
-    }
-    int cnt = 0;
-    const double thr_lo = thr >= 0 ? thr * (1.0 - 1e-4) : thr * (1.0 + 1e-4);
-    const double thr_hi = thr >= 0 ? thr * (1.0 + 1e-4) : thr * (1.0 - 1e-4);
-    for (int64_t base = 0; base < N; base += SCORE_TILE) {
-        const int n = (int)min<int64_t>(SCORE_TILE, N - base);
-        for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            s1[i] = x1[base + i];
-            s2[i] = x2[base + i];
-        }
-        __syncthreads();
-        if (active && finite) {
-            for (int j = 0; j < n; j += 64) {
-                const int i = j + lane;
-                bool inl = false;
-                if (i < n) {
-                    const double2 p = s1[i], q = s2[i];
-                    inl = epi_inlier_fast(f, p.x, p.y, q.x, q.y, thr, thr_lo, thr_hi);
-                }
-                cnt += __popcll(__ballot(inl));
-            }
-        }
-        __syncthreads();
-    }
-    if (active && lane == 0) counts[h] = cnt;
-}
-
-// grid = 1 workgroup of 1024 threads
-__global__ void __launch_bounds__(1024) k_ransac_select(const double2 *__restrict__ x1,
-                                                        const double2 *__restrict__ x2, int64_t N,
-                                                        const double *__restrict__ F,
-                                                        const int32_t *__restrict__ counts, int64_t H,
-                                                        double thr, int64_t *__restrict__ best_out,
-                                                        double *__restrict__ F_best,
-                                                        uint8_t *__restrict__ mask) {
-    __shared__ int32_t sc[1024];
-    __shared__ int64_t sh[1024];
-    int32_t bc = 0;
-    int64_t bh = -1;
-    for (int64_t h = threadIdx.x; h < H; h += blockDim.x) {
-        const int32_t c = counts[h];
-        if (c > bc) { bc = c; bh = h; }  // ascending h per thread: first max kept
-    }
-    sc[threadIdx.x] = bc;
-    sh[threadIdx.x] = bh;
-    __syncthreads();
-    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) {
-            const int32_t c2 = sc[threadIdx.x + s];
-            const int64_t h2 = sh[threadIdx.x + s];
-            const int32_t c1 = sc[threadIdx.x];
-            const int64_t h1 = sh[threadIdx.x];
-            if (c2 > c1 || (c2 == c1 && c2 > 0 && h2 < h1)) {
-                sc[threadIdx.x] = c2;
-                sh[threadIdx.x] = h2;
-            }
-        }
-        __syncthreads();
-    }
-    const int64_t best = sc[0] > 0 ? sh[0] : -1;
-    if (threadIdx.x == 0) *best_out = best;
-    if (best < 0) return;
-    double f[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) f[k] = F[9 * best + k];
-    if (threadIdx.x < 9) F_best[threadIdx.x] = f[threadIdx.x];
-    for (int64_t i = threadIdx.x; i < N; i += blockDim.x) {
-        const double2 p = x1[i], q = x2[i];
-        mask[i] = epi_inlier(f, p.x, p.y, q.x, q.y, thr) ? 1 : 0;
-    }
-}
-
-// ------------------------------------------------------------------ host
-static inline float ev_ms(hipEvent_t a, hipEvent_t b) {
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, a, b);
-    return ms;
-}
-
-}  // namespace sfm
+// Fundamental-matrix RANSAC entry points (GetInliersRANSAC.py:5-106,
+// EstimateFundamentalMatrix.py:3-83) on the engine in ransac_engine.hpp.
+#include "ransac_engine.hpp"
 
 using namespace sfm;
 
@@ -162,7 +17,7 @@ extern "C" int sfm_f8_batch(const double *x1s, const double *x2s, int64_t H, dou
         return rc;
     SFM_HIP(hipMemcpyAsync(c->buf[0].p, x1s, pb, hipMemcpyHostToDevice, c->stream));
     SFM_HIP(hipMemcpyAsync(c->buf[1].p, x2s, pb, hipMemcpyHostToDevice, c->stream));
-    hipLaunchKernelGGL(k_f8_points, dim3(ceil_div(H, 256)), dim3(256), 0, c->stream, c->buf[0].as<double2>(),
+    hipLaunchKernelGGL(k_fit_points<EpiModel>, dim3(ceil_div(H, 256)), dim3(256), 0, c->stream, c->buf[0].as<double2>(),
                        c->buf[1].as<double2>(), H, c->buf[2].as<double>());
     SFM_HIP(hipGetLastError());
     SFM_HIP(hipMemcpyAsync(F, c->buf[2].p, (size_t)H * 9 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -173,52 +28,5 @@ extern "C" int sfm_f8_batch(const double *x1s, const double *x2s, int64_t H, dou
 extern "C" int sfm_ransac_f8(const double *x1, const double *x2, int64_t N, const int32_t *samples, int64_t H,
                              double thr, int32_t *counts_out, int64_t *best_iter, double *F_best,
                              uint8_t *best_mask, int device) {
-    SFM_CHECK_ARG(N >= 8 && H >= 0, "need N >= 8 and H >= 0");
-    SFM_CHECK_ARG(x1 && x2 && best_iter && F_best && best_mask && (samples || H == 0), "null pointer");
-    for (int64_t i = 0; i < H * 8; ++i)
-        SFM_CHECK_ARG(samples[i] >= 0 && samples[i] < N, "sample index out of range");
-    *best_iter = -1;
-    if (H == 0) return 0;
-    ThreadCtx *c = thread_ctx(device);
-    if (!c) return SFM_ERR_HIP;
-    const size_t pb = (size_t)N * sizeof(double2);
-    int rc;
-    if ((rc = c->buf[0].reserve(pb)) || (rc = c->buf[1].reserve(pb)) ||
-        (rc = c->buf[2].reserve((size_t)H * 8 * sizeof(int32_t))) ||
-        (rc = c->buf[3].reserve((size_t)H * 9 * sizeof(double))) ||
-        (rc = c->buf[4].reserve((size_t)H * sizeof(int32_t))) ||
-        (rc = c->buf[5].reserve(16 * sizeof(double) + (size_t)N)))
-        return rc;
-    double2 *d1 = c->buf[0].as<double2>(), *d2 = c->buf[1].as<double2>();
-    int32_t *ds = c->buf[2].as<int32_t>(), *dcnt = c->buf[4].as<int32_t>();
-    double *dF = c->buf[3].as<double>();
-    int64_t *dbest = c->buf[5].as<int64_t>();
-    double *dFb = c->buf[5].as<double>() + 2;
-    uint8_t *dmask = reinterpret_cast<uint8_t *>(c->buf[5].as<double>() + 16);
-    hipStream_t s = c->stream;
-    SFM_HIP(hipEventRecord(c->ev[0], s));
-    SFM_HIP(hipMemcpyAsync(d1, x1, pb, hipMemcpyHostToDevice, s));
-    SFM_HIP(hipMemcpyAsync(d2, x2, pb, hipMemcpyHostToDevice, s));
-    SFM_HIP(hipMemcpyAsync(ds, samples, (size_t)H * 8 * sizeof(int32_t), hipMemcpyHostToDevice, s));
-    SFM_HIP(hipEventRecord(c->ev[1], s));
-    hipLaunchKernelGGL(k_f8_samples, dim3(ceil_div(H, 256)), dim3(256), 0, s, d1, d2, ds, H, dF);
-    SFM_HIP(hipGetLastError());
-    SFM_HIP(hipEventRecord(c->ev[2], s));
-    hipLaunchKernelGGL(k_ransac_score, dim3(ceil_div(H, SCORE_WAVES)), dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
-                       dF, H, thr, dcnt);
-    SFM_HIP(hipGetLastError());
-    SFM_HIP(hipEventRecord(c->ev[3], s));
-    hipLaunchKernelGGL(k_ransac_select, dim3(1), dim3(1024), 0, s, d1, d2, N, dF, dcnt, H, thr, dbest, dFb, dmask);
-    SFM_HIP(hipGetLastError());
-    SFM_HIP(hipEventRecord(c->ev[4], s));
-    SFM_HIP(hipMemcpyAsync(best_iter, dbest, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    SFM_HIP(hipMemcpyAsync(F_best, dFb, 9 * sizeof(double), hipMemcpyDeviceToHost, s));
-    SFM_HIP(hipMemcpyAsync(best_mask, dmask, (size_t)N, hipMemcpyDeviceToHost, s));
-    if (counts_out) SFM_HIP(hipMemcpyAsync(counts_out, dcnt, (size_t)H * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    SFM_HIP(hipEventRecord(c->ev[5], s));
-    SFM_HIP(hipStreamSynchronize(s));
-    const double t[6] = {ev_ms(c->ev[0], c->ev[1]), ev_ms(c->ev[1], c->ev[4]), ev_ms(c->ev[4], c->ev[5]),
-                         ev_ms(c->ev[2], c->ev[3]), ev_ms(c->ev[1], c->ev[2]), ev_ms(c->ev[3], c->ev[4])};
-    set_timings(t, 6);
-    return 0;
+    return ransac_run<EpiModel>(x1, x2, N, samples, H, thr, counts_out, best_iter, F_best, best_mask, device);
 }

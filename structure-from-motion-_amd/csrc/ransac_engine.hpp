@@ -1,0 +1,239 @@
+// Batched RANSAC engine for gfx950, templated on the model:
+//   EpiModel  fundamental matrix, 8-point samples, symmetric epipolar
+//             distance (GetInliersRANSAC.py:5-106)
+//   HomModel  homography, 4-point samples, transfer error
+//             (GetHomographyInliers.py:88-165)
+// Kernels:
+//   k_fit_samples<M>   one thread per hypothesis: gather the K sampled
+//                      correspondences and fit the 3x3 model.
+//   k_ransac_score<M>  one WAVE per hypothesis: the model is wave-uniform
+//                      (scalar registers); correspondence tiles are staged
+//                      once per workgroup in LDS and every wave sweeps them,
+//                      one correspondence per lane; inlier count = popcount
+//                      of the wave ballot (scalar unit).
+//   k_ransac_select<M> one workgroup: (max count, min iteration) reduction ==
+//                      the reference's strict '>' update, then the inlier
+//                      mask of the winner.
+#pragma once
+#include "sfm_common.hpp"
+#include "sfm_geom.hpp"
+
+namespace sfm {
+
+constexpr int SCORE_WAVES = 8;          // hypotheses per workgroup
+constexpr int SCORE_TILE = 1024;        // correspondences per LDS tile (32 KiB)
+
+struct EpiModel {
+    static constexpr int K = 8;
+    __device__ static void fit(const double (&ax)[K], const double (&ay)[K], const double (&bx)[K],
+                               const double (&by)[K], double *out) {
+        f8_points(ax, ay, bx, by, out);
+    }
+    __device__ static bool inlier(const double *f, double2 p, double2 q, double thr) {
+        return epi_inlier(f, p.x, p.y, q.x, q.y, thr);
+    }
+    __device__ static bool inlier_fast(const double *f, double2 p, double2 q, double thr, double lo, double hi) {
+        return epi_inlier_fast(f, p.x, p.y, q.x, q.y, thr, lo, hi);
+    }
+};
+
+struct HomModel {
+    static constexpr int K = 4;
+    __device__ static void fit(const double (&ax)[K], const double (&ay)[K], const double (&bx)[K],
+                               const double (&by)[K], double *out) {
+        h4_points(ax, ay, bx, by, out);
+    }
+    __device__ static bool inlier(const double *f, double2 p, double2 q, double thr) {
+        return hom_inlier(f, p.x, p.y, q.x, q.y, thr);
+    }
+    __device__ static bool inlier_fast(const double *f, double2 p, double2 q, double thr, double, double) {
+        return hom_inlier(f, p.x, p.y, q.x, q.y, thr);
+    }
+};
+
+template <class M>
+__global__ void __launch_bounds__(256) k_fit_samples(const double2 *__restrict__ x1, const double2 *__restrict__ x2,
+                                                     const int32_t *__restrict__ samples, int64_t H,
+                                                     double *__restrict__ out) {
+    const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= H) return;
+    double ax[M::K], ay[M::K], bx[M::K], by[M::K];
+#pragma unroll
+    for (int i = 0; i < M::K; ++i) {
+        const int32_t s = samples[h * M::K + i];
+        const double2 p = x1[s], q = x2[s];
+        ax[i] = p.x; ay[i] = p.y; bx[i] = q.x; by[i] = q.y;
+    }
+    M::fit(ax, ay, bx, by, out + 9 * h);
+}
+
+// samples given as coordinates (H x K x 2 each): the batch fit entry points
+template <class M>
+__global__ void __launch_bounds__(256) k_fit_points(const double2 *__restrict__ x1s, const double2 *__restrict__ x2s,
+                                                    int64_t H, double *__restrict__ out) {
+    const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= H) return;
+    double ax[M::K], ay[M::K], bx[M::K], by[M::K];
+#pragma unroll
+    for (int i = 0; i < M::K; ++i) {
+        const double2 p = x1s[h * M::K + i], q = x2s[h * M::K + i];
+        ax[i] = p.x; ay[i] = p.y; bx[i] = q.x; by[i] = q.y;
+    }
+    M::fit(ax, ay, bx, by, out + 9 * h);
+}
+
+template <class M>
+__global__ void __launch_bounds__(64 * SCORE_WAVES) k_ransac_score(const double2 *__restrict__ x1,
+                                                                   const double2 *__restrict__ x2,
+                                                                   int64_t N, const double *__restrict__ F,
+                                                                   int64_t H, double thr,
+                                                                   int32_t *__restrict__ counts) {
+    __shared__ double2 s1[SCORE_TILE];
+    __shared__ double2 s2[SCORE_TILE];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t h = (int64_t)blockIdx.x * SCORE_WAVES + wave;
+    const bool active = h < H;
+    double f[9];
+    int finite = 1;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        f[k] = active ? F[9 * h + k] : 0.0;
+        finite &= isfinite(f[k]) ? 1 : 0;
+    }
+    int cnt = 0;
+    const double thr_lo = thr >= 0 ? thr * (1.0 - 1e-4) : thr * (1.0 + 1e-4);
+    const double thr_hi = thr >= 0 ? thr * (1.0 + 1e-4) : thr * (1.0 - 1e-4);
+    for (int64_t base = 0; base < N; base += SCORE_TILE) {
+        const int n = (int)min<int64_t>(SCORE_TILE, N - base);
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            s1[i] = x1[base + i];
+            s2[i] = x2[base + i];
+        }
+        __syncthreads();
+        if (active && finite) {
+            for (int j = 0; j < n; j += 64) {
+                const int i = j + lane;
+                bool inl = false;
+                if (i < n) {
+                    const double2 p = s1[i], q = s2[i];
+                    inl = M::inlier_fast(f, p, q, thr, thr_lo, thr_hi);
+                }
+                cnt += __popcll(__ballot(inl));
+            }
+        }
+        __syncthreads();
+    }
+    if (active && lane == 0) counts[h] = cnt;
+}
+
+// grid = 1 workgroup of 1024 threads
+template <class M>
+__global__ void __launch_bounds__(1024) k_ransac_select(const double2 *__restrict__ x1,
+                                                        const double2 *__restrict__ x2, int64_t N,
+                                                        const double *__restrict__ F,
+                                                        const int32_t *__restrict__ counts, int64_t H,
+                                                        double thr, int64_t *__restrict__ best_out,
+                                                        double *__restrict__ F_best,
+                                                        uint8_t *__restrict__ mask) {
+    __shared__ int32_t sc[1024];
+    __shared__ int64_t sh[1024];
+    int32_t bc = 0;
+    int64_t bh = -1;
+    for (int64_t h = threadIdx.x; h < H; h += blockDim.x) {
+        const int32_t c = counts[h];
+        if (c > bc) { bc = c; bh = h; }  // ascending h per thread: first max kept
+    }
+    sc[threadIdx.x] = bc;
+    sh[threadIdx.x] = bh;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            const int32_t c2 = sc[threadIdx.x + s];
+            const int64_t h2 = sh[threadIdx.x + s];
+            const int32_t c1 = sc[threadIdx.x];
+            const int64_t h1 = sh[threadIdx.x];
+            if (c2 > c1 || (c2 == c1 && c2 > 0 && h2 < h1)) {
+                sc[threadIdx.x] = c2;
+                sh[threadIdx.x] = h2;
+            }
+        }
+        __syncthreads();
+    }
+    const int64_t best = sc[0] > 0 ? sh[0] : -1;
+    if (threadIdx.x == 0) *best_out = best;
+    if (best < 0) return;
+    double f[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f[k] = F[9 * best + k];
+    if (threadIdx.x < 9) F_best[threadIdx.x] = f[threadIdx.x];
+    for (int64_t i = threadIdx.x; i < N; i += blockDim.x) {
+        const double2 p = x1[i], q = x2[i];
+        mask[i] = M::inlier(f, p, q, thr) ? 1 : 0;
+    }
+}
+
+// ------------------------------------------------------------------ host
+static inline float ev_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    return ms;
+}
+
+
+// Whole RANSAC on one device: upload, fit, score, select, download.
+// Timings (sfm_last_timings): upload, kernels, download, score, fit, select.
+template <class M>
+int ransac_run(const double *x1, const double *x2, int64_t N, const int32_t *samples, int64_t H, double thr,
+               int32_t *counts_out, int64_t *best_iter, double *F_best, uint8_t *best_mask, int device) {
+    SFM_CHECK_ARG(N >= M::K && H >= 0, "need N >= sample size and H >= 0");
+    SFM_CHECK_ARG(x1 && x2 && best_iter && F_best && best_mask && (samples || H == 0), "null pointer");
+    for (int64_t i = 0; i < H * M::K; ++i)
+        SFM_CHECK_ARG(samples[i] >= 0 && samples[i] < N, "sample index out of range");
+    *best_iter = -1;
+    if (H == 0) return 0;
+    ThreadCtx *c = thread_ctx(device);
+    if (!c) return SFM_ERR_HIP;
+    const size_t pb = (size_t)N * sizeof(double2);
+    int rc;
+    if ((rc = c->buf[0].reserve(pb)) || (rc = c->buf[1].reserve(pb)) ||
+        (rc = c->buf[2].reserve((size_t)H * M::K * sizeof(int32_t))) ||
+        (rc = c->buf[3].reserve((size_t)H * 9 * sizeof(double))) ||
+        (rc = c->buf[4].reserve((size_t)H * sizeof(int32_t))) ||
+        (rc = c->buf[5].reserve(16 * sizeof(double) + (size_t)N)))
+        return rc;
+    double2 *d1 = c->buf[0].as<double2>(), *d2 = c->buf[1].as<double2>();
+    int32_t *ds = c->buf[2].as<int32_t>(), *dcnt = c->buf[4].as<int32_t>();
+    double *dF = c->buf[3].as<double>();
+    int64_t *dbest = c->buf[5].as<int64_t>();
+    double *dFb = c->buf[5].as<double>() + 2;
+    uint8_t *dmask = reinterpret_cast<uint8_t *>(c->buf[5].as<double>() + 16);
+    hipStream_t s = c->stream;
+    SFM_HIP(hipEventRecord(c->ev[0], s));
+    SFM_HIP(hipMemcpyAsync(d1, x1, pb, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipMemcpyAsync(d2, x2, pb, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipMemcpyAsync(ds, samples, (size_t)H * M::K * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    SFM_HIP(hipEventRecord(c->ev[1], s));
+    hipLaunchKernelGGL(k_fit_samples<M>, dim3(ceil_div(H, 256)), dim3(256), 0, s, d1, d2, ds, H, dF);
+    SFM_HIP(hipGetLastError());
+    SFM_HIP(hipEventRecord(c->ev[2], s));
+    hipLaunchKernelGGL(k_ransac_score<M>, dim3(ceil_div(H, SCORE_WAVES)), dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
+                       dF, H, thr, dcnt);
+    SFM_HIP(hipGetLastError());
+    SFM_HIP(hipEventRecord(c->ev[3], s));
+    hipLaunchKernelGGL(k_ransac_select<M>, dim3(1), dim3(1024), 0, s, d1, d2, N, dF, dcnt, H, thr, dbest, dFb, dmask);
+    SFM_HIP(hipGetLastError());
+    SFM_HIP(hipEventRecord(c->ev[4], s));
+    SFM_HIP(hipMemcpyAsync(best_iter, dbest, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    SFM_HIP(hipMemcpyAsync(F_best, dFb, 9 * sizeof(double), hipMemcpyDeviceToHost, s));
+    SFM_HIP(hipMemcpyAsync(best_mask, dmask, (size_t)N, hipMemcpyDeviceToHost, s));
+    if (counts_out) SFM_HIP(hipMemcpyAsync(counts_out, dcnt, (size_t)H * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    SFM_HIP(hipEventRecord(c->ev[5], s));
+    SFM_HIP(hipStreamSynchronize(s));
+    const double t[6] = {ev_ms(c->ev[0], c->ev[1]), ev_ms(c->ev[1], c->ev[4]), ev_ms(c->ev[4], c->ev[5]),
+                         ev_ms(c->ev[2], c->ev[3]), ev_ms(c->ev[1], c->ev[2]), ev_ms(c->ev[3], c->ev[4])};
+    set_timings(t, 6);
+    return 0;
+}
+
+}  // namespace sfm

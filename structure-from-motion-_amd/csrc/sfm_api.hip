@@ -8,6 +8,7 @@
 
 #include "sfm_common.hpp"
 #include "sfm_geom.hpp"
+#include "dlt_general.hpp"
 
 namespace sfm {
 
@@ -64,115 +65,6 @@ ThreadCtx *thread_ctx(int device) {
 }
 
 // ---------------------------------------------------------------- kernels
-
-// EstimateFundamentalMatrix for N >= 8 (EstimateFundamentalMatrix.py:21-83):
-// one workgroup.  Hartley statistics by block reduction; the N x 9 design
-// matrix is reduced to a 9 x 9 triangular factor by per-thread Givens QR
-// plus a binary tree merge in LDS (same right singular vectors as A);
-// thread 0 then runs a 9-column one-sided Jacobi SVD for the null vector.
-constexpr int FG_THREADS = 128;
-
-__device__ __forceinline__ void givens_absorb(double (&R)[9][9], double (&a)[9]) {
-#pragma unroll
-    for (int j = 0; j < 9; ++j) {
-        if (a[j] != 0.0) {
-            const double r = sqrt(R[j][j] * R[j][j] + a[j] * a[j]);
-            const double c = R[j][j] / r, s = a[j] / r;
-#pragma unroll
-            for (int k = j; k < 9; ++k) {
-                const double u = R[j][k], v = a[k];
-                R[j][k] = c * u + s * v;
-                a[k] = -s * u + c * v;
-            }
-        }
-    }
-}
-
-__global__ void __launch_bounds__(FG_THREADS) k_f8_general(const double2 *__restrict__ x1,
-                                                           const double2 *__restrict__ x2, int64_t N,
-                                                           double *__restrict__ F) {
-    __shared__ double red[4][FG_THREADS];
-    __shared__ double Rs[FG_THREADS][45];
-    const int t = threadIdx.x;
-    double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-    for (int64_t i = t; i < N; i += FG_THREADS) {
-        const double2 p = x1[i], q = x2[i];
-        s0 += p.x; s1 += p.y; s2 += q.x; s3 += q.y;
-    }
-    red[0][t] = s0; red[1][t] = s1; red[2][t] = s2; red[3][t] = s3;
-    __syncthreads();
-    for (int w = FG_THREADS / 2; w > 0; w >>= 1) {
-        if (t < w)
-            for (int k = 0; k < 4; ++k) red[k][t] += red[k][t + w];
-        __syncthreads();
-    }
-    const double m1x = red[0][0] / (double)N, m1y = red[1][0] / (double)N;
-    const double m2x = red[2][0] / (double)N, m2y = red[3][0] / (double)N;
-    __syncthreads();
-    double d1 = 0, d2 = 0;
-    for (int64_t i = t; i < N; i += FG_THREADS) {
-        const double2 p = x1[i], q = x2[i];
-        const double ax = p.x - m1x, ay = p.y - m1y, bx = q.x - m2x, by = q.y - m2y;
-        d1 += sqrt(ax * ax + ay * ay);
-        d2 += sqrt(bx * bx + by * by);
-    }
-    red[0][t] = d1; red[1][t] = d2;
-    __syncthreads();
-    for (int w = FG_THREADS / 2; w > 0; w >>= 1) {
-        if (t < w) { red[0][t] += red[0][t + w]; red[1][t] += red[1][t + w]; }
-        __syncthreads();
-    }
-    Hartley h1, h2;
-    h1.s = 1.4142135623730951 / (red[0][0] / (double)N + 1e-8);
-    h2.s = 1.4142135623730951 / (red[1][0] / (double)N + 1e-8);
-    h1.ox = -h1.s * m1x; h1.oy = -h1.s * m1y; h2.ox = -h2.s * m2x; h2.oy = -h2.s * m2y;
-    double R[9][9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i)
-#pragma unroll
-        for (int j = 0; j < 9; ++j) R[i][j] = 0.0;
-    for (int64_t i = t; i < N; i += FG_THREADS) {
-        const double2 p = x1[i], q = x2[i];
-        const double a = h1.s * p.x + h1.ox, b = h1.s * p.y + h1.oy;
-        const double c = h2.s * q.x + h2.ox, d = h2.s * q.y + h2.oy;
-        double row[9] = {a * c, a * d, a, b * c, b * d, b, c, d, 1.0};
-        givens_absorb(R, row);
-    }
-    for (int w = FG_THREADS / 2; w > 0; w >>= 1) {
-        if (t >= w && t < 2 * w) {
-            int k = 0;
-#pragma unroll
-            for (int i = 0; i < 9; ++i)
-#pragma unroll
-                for (int j = i; j < 9; ++j) Rs[t][k++] = R[i][j];
-        }
-        __syncthreads();
-        if (t < w) {
-#pragma unroll
-            for (int i = 0; i < 9; ++i) {
-                double row[9];
-#pragma unroll
-                for (int j = 0; j < 9; ++j) row[j] = 0.0;
-#pragma unroll
-                for (int j = i; j < 9; ++j) row[j] = Rs[t + w][i * 9 - i * (i - 1) / 2 + (j - i)];
-                givens_absorb(R, row);
-            }
-        }
-        __syncthreads();
-    }
-    if (t != 0) return;
-    double a[9][9], V[9][9];  // a[col][row]
-#pragma unroll
-    for (int c = 0; c < 9; ++c)
-#pragma unroll
-        for (int r = 0; r < 9; ++r) a[c][r] = R[r][c];
-    jacobi_onesided<9, 9, 40>(a, V);
-    const int j = weakest_column<9, 9>(a);
-    double f[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) f[k] = V[k][j];
-    f8_finish(f, h1, h2, F);
-}
 
 // LinearTriangulation.py:54-90: one thread per point, 4x4 DLT system,
 // right singular vector of the smallest singular value by one-sided Jacobi.
@@ -365,7 +257,7 @@ extern "C" int sfm_f8_general(const double *x1, const double *x2, int64_t N, dou
         return rc;
     SFM_HIP(hipMemcpyAsync(c->buf[0].p, x1, pb, hipMemcpyHostToDevice, c->stream));
     SFM_HIP(hipMemcpyAsync(c->buf[1].p, x2, pb, hipMemcpyHostToDevice, c->stream));
-    hipLaunchKernelGGL(k_f8_general, dim3(1), dim3(FG_THREADS), 0, c->stream, c->buf[0].as<double2>(),
+    hipLaunchKernelGGL(k_dlt_general<FDesign>, dim3(1), dim3(FG_THREADS), 0, c->stream, c->buf[0].as<double2>(),
                        c->buf[1].as<double2>(), N, c->buf[2].as<double>());
     SFM_HIP(hipGetLastError());
     SFM_HIP(hipMemcpyAsync(F, c->buf[2].p, 9 * sizeof(double), hipMemcpyDeviceToHost, c->stream));

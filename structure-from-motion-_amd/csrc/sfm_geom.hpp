@@ -191,23 +191,12 @@ __device__ __forceinline__ void f8_finish(const double (&f)[9], const Hartley &h
         for (int c = 0; c < 3; ++c) F_out[r * 3 + c] = G[r][c] / d;
 }
 
-// 8-point F (EstimateFundamentalMatrix.py:21-83).  The null vector of the
-// 8 x 9 design matrix A (:58-67) is obtained from a Householder LQ of A:
-// A Q_0..Q_7 = [L 0], so n = Q_0 ... Q_7 e_8 spans null(A) whenever
-// rank(A) = 8 -- the same vector as Vt[-1] of the reference's SVD up to
-// sign, which F / F[2,2] removes.  ~0.6 kflop instead of a 9-column SVD.
-__device__ __forceinline__ void f8_points(const double (&x1)[8], const double (&y1)[8],
-                                          const double (&x2)[8], const double (&y2)[8], double *F_out) {
-    const Hartley h1 = hartley8(x1, y1), h2 = hartley8(x2, y2);
-    double A[8][9];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const double a = h1.s * x1[i] + h1.ox, b = h1.s * y1[i] + h1.oy;
-        const double c = h2.s * x2[i] + h2.ox, d = h2.s * y2[i] + h2.oy;
-        A[i][0] = a * c; A[i][1] = a * d; A[i][2] = a;
-        A[i][3] = b * c; A[i][4] = b * d; A[i][5] = b;
-        A[i][6] = c; A[i][7] = d; A[i][8] = 1.0;
-    }
+// Null vector of an 8 x 9 matrix A (rank 8) from a Householder LQ:
+// A Q_0..Q_7 = [L 0], so n = Q_0 ... Q_7 e_8 spans null(A) -- the same vector
+// as Vt[-1] of the reference's SVD up to sign (both the F and the H paths
+// divide by the [2,2] entry, which removes it).  ~0.6 kflop instead of a
+// 9-column SVD.  A is destroyed.
+__device__ __forceinline__ void null_vector_8x9(double (&A)[8][9], double (&n)[9]) {
     double tau[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -232,7 +221,6 @@ __device__ __forceinline__ void f8_points(const double (&x1)[8], const double (&
             for (int j = k; j < 9; ++j) A[i][j] -= d * A[k][j];
         }
     }
-    double n[9];
 #pragma unroll
     for (int j = 0; j < 9; ++j) n[j] = (j == 8) ? 1.0 : 0.0;
 #pragma unroll
@@ -244,7 +232,122 @@ __device__ __forceinline__ void f8_points(const double (&x1)[8], const double (&
 #pragma unroll
         for (int j = k; j < 9; ++j) n[j] -= d * A[k][j];
     }
+}
+
+// 8-point F (EstimateFundamentalMatrix.py:21-83): Hartley-normalised design
+// matrix (:58-62), its null vector, rank 2 and denormalisation (f8_finish).
+__device__ __forceinline__ void f8_points(const double (&x1)[8], const double (&y1)[8],
+                                          const double (&x2)[8], const double (&y2)[8], double *F_out) {
+    const Hartley h1 = hartley8(x1, y1), h2 = hartley8(x2, y2);
+    double A[8][9];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double a = h1.s * x1[i] + h1.ox, b = h1.s * y1[i] + h1.oy;
+        const double c = h2.s * x2[i] + h2.ox, d = h2.s * y2[i] + h2.oy;
+        A[i][0] = a * c; A[i][1] = a * d; A[i][2] = a;
+        A[i][3] = b * c; A[i][4] = b * d; A[i][5] = b;
+        A[i][6] = c; A[i][7] = d; A[i][8] = 1.0;
+    }
+    double n[9];
+    null_vector_8x9(A, n);
     f8_finish(n, h1, h2, F_out);
+}
+
+// ------------------------------------------------------------ homography
+// find_homography (GetHomographyInliers.py:4-85).  numpy's 3x3 @ 3xN and
+// 3x3 @ 3x3 products run through OpenBLAS dgemm, whose accumulation is an
+// FMA chain acc = a0*b0; acc = fma(a1, b1, acc); acc = fma(a2, b2, acc)
+// (measured against exact arithmetic, see tests/golden/make_golden.py);
+// the code below states those fma() calls explicitly and keeps every other
+// operation uncontracted.
+
+// Hartley-style normalisation of K points (:27-42): centroid, then
+// scale = sqrt(2) / (mean distance + 1e-8); x' = s x + ox
+template <int K>
+__device__ __forceinline__ Hartley hartley_k(const double (&x)[K], const double (&y)[K]) {
+#pragma clang fp contract(off)
+    double mx = 0, my = 0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) { mx += x[i]; my += y[i]; }
+    mx = mx / (double)K;
+    my = my / (double)K;
+    double d = 0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const double ax = x[i] - mx, ay = y[i] - my;
+        d += sqrt(ax * ax + ay * ay);
+    }
+    Hartley h;
+    h.s = 1.4142135623730951 / (d / (double)K + 1e-8);
+    h.ox = -h.s * mx;
+    h.oy = -h.s * my;
+    return h;
+}
+
+// C = A @ B, 3x3 row-major, dgemm accumulation order
+__device__ __forceinline__ void mm3_blas(const double (&A)[3][3], const double (&B)[3][3], double (&C)[3][3]) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) C[r][c] = fma(A[r][2], B[2][c], fma(A[r][1], B[1][c], A[r][0] * B[0][c]));
+}
+
+// H = inv(T2) @ Hn @ T1, H / H[2,2] (:79-83).  inv(T2) as LAPACK getri
+// forms it for this upper-triangular T2: 1/s on the diagonal and
+// -(o * (1/s)) in the last column.
+__device__ __forceinline__ void h_finish(const double (&n)[9], const Hartley &h1, const Hartley &h2, double *H_out) {
+#pragma clang fp contract(off)
+    const double is = 1.0 / h2.s;
+    const double Ti[3][3] = {{is, -0.0, -(h2.ox * is)}, {0.0, is, -(h2.oy * is)}, {0.0, 0.0, 1.0}};
+    const double Hn[3][3] = {{n[0], n[1], n[2]}, {n[3], n[4], n[5]}, {n[6], n[7], n[8]}};
+    const double T1[3][3] = {{h1.s, 0.0, h1.ox}, {0.0, h1.s, h1.oy}, {0.0, 0.0, 1.0}};
+    double M[3][3], G[3][3];
+    mm3_blas(Ti, Hn, M);
+    mm3_blas(M, T1, G);
+    const double d = G[2][2];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) H_out[r * 3 + c] = G[r][c] / d;
+}
+
+// The two DLT rows of one normalised correspondence (:59-71)
+__device__ __forceinline__ void h_rows(double a, double b, double c, double d, double (&r0)[9], double (&r1)[9]) {
+#pragma clang fp contract(off)
+    r0[0] = 0.0; r0[1] = 0.0; r0[2] = 0.0; r0[3] = -a; r0[4] = -b; r0[5] = -1.0;
+    r0[6] = d * a; r0[7] = d * b; r0[8] = d;
+    r1[0] = a; r1[1] = b; r1[2] = 1.0; r1[3] = 0.0; r1[4] = 0.0; r1[5] = 0.0;
+    r1[6] = -c * a; r1[7] = -c * b; r1[8] = -c;
+}
+
+// 4-point homography: 8 x 9 DLT system, LQ null vector, denormalisation
+__device__ __forceinline__ void h4_points(const double (&x1)[4], const double (&y1)[4], const double (&x2)[4],
+                                          const double (&y2)[4], double *H_out) {
+#pragma clang fp contract(off)
+    const Hartley h1 = hartley_k<4>(x1, y1), h2 = hartley_k<4>(x2, y2);
+    double A[8][9];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const double a = h1.s * x1[i] + h1.ox, b = h1.s * y1[i] + h1.oy;
+        const double c = h2.s * x2[i] + h2.ox, d = h2.s * y2[i] + h2.oy;
+        h_rows(a, b, c, d, A[2 * i], A[2 * i + 1]);
+    }
+    double n[9];
+    null_vector_8x9(A, n);
+    h_finish(n, h1, h2, H_out);
+}
+
+// get_homography_inliers' test (GetHomographyInliers.py:134-146):
+// t = H [x y 1]^T; (u, v) = t[:2] / (t[2] + 1e-8); |(u, v) - x2| < thr
+__device__ __forceinline__ bool hom_inlier(const double *H, double x, double y, double u, double v, double thr) {
+#pragma clang fp contract(off)
+    const double t0 = fma(H[1], y, H[0] * x) + H[2];
+    const double t1 = fma(H[4], y, H[3] * x) + H[5];
+    const double t2 = fma(H[7], y, H[6] * x) + H[8];
+    const double w = t2 + 1e-8;
+    const double d0 = t0 / w - u, d1 = t1 / w - v;
+    return sqrt(d0 * d0 + d1 * d1) < thr;
 }
 
 // Rodrigues (scipy Rotation.from_rotvec(...).as_matrix()), row-major.

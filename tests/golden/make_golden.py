@@ -22,6 +22,13 @@ Outputs (tests/golden/*.npz):
                      (s=0) and 2000 (s=1,2): outputs + per-hypothesis counts.
   triangulation.npz  LinearTriangulation on the four P3Data 1_2 pose
                      candidates and on cfg2's clean 5000 points.
+  homography.npz     get_homography_inliers (GetHomographyInliers.py:88-165) in
+                     the reference driver's pair loop (seeds 0, 1; MT state
+                     before/after each call; per-hypothesis counts for pair
+                     1_2 seed 0), on a synthetic plane scene (N=5000, 40 %
+                     outliers, n_max=4096) and on cfg2's non-planar scene,
+                     both with per-hypothesis counts; find_homography on
+                     random 4-point and N-point samples.
   nltri.npz          NonLinearTriangulation (per-point scipy 'lm', max_nfev=50)
                      on the four P3Data 1_2 pose candidates, on cfg2's noisy
                      inliers, on cfg2 outliers (hard, often non-converging
@@ -252,6 +259,96 @@ def gen_ba(ref, skip_cfg3):
     np.savez_compressed(os.path.join(HERE, "ba.npz"), **out)
 
 
+def per_hypothesis_counts_h(ref, p1, p2, thr, n_max, state):
+    """Homography RANSAC count of every hypothesis, each from the reference:
+    get_homography_inliers with n_max=1 from the MT state of iteration i."""
+    random.setstate(state)
+    idx = np.arange(len(p1))
+    counts = np.zeros(n_max, dtype=np.int32)
+    for i in range(n_max):
+        H, inl = ref.h.get_homography_inliers(p1, p2, idx, thr, 1)
+        counts[i] = len(inl) if H is not None else 0
+    return counts
+
+
+def plane_scene(n=5000, seed=0, outlier_frac=0.4, noise=0.5):
+    """Two views of a textured plane (Z = 8 + 0.1 X - 0.05 Y) with cfg2's
+    cameras, pixel noise and uniform outliers in view 2."""
+    rng = np.random.default_rng(seed)
+    X = rng.uniform(-3, 3, n)
+    Y = rng.uniform(-2, 2, n)
+    P = np.column_stack([X, Y, 8 + 0.1 * X - 0.05 * Y])
+    R2 = syn.rotvec_to_matrix([0.02, -0.15, 0.01])[0]
+    C2 = np.array([1.0, 0.05, 0.1])
+
+    def proj(R, C):
+        u = (syn.K_REF @ (R @ (P - C).T)).T
+        return u[:, :2] / u[:, 2:3]
+    x1 = proj(np.eye(3), np.zeros(3)) + rng.normal(0, noise, (n, 2))
+    x2 = proj(R2, C2) + rng.normal(0, noise, (n, 2))
+    k = int(round(outlier_frac * n))
+    o = rng.choice(n, k, replace=False)
+    x2[o] = np.column_stack([rng.uniform(0, 800, k), rng.uniform(0, 600, k)])
+    return np.ascontiguousarray(x1), np.ascontiguousarray(x2)
+
+
+def gen_homography(ref):
+    from itertools import combinations
+    data = os.path.join(HERE, "P3Data") + "/"
+    fx, fy, ff = ref.u.get_data(data, 5)
+    out = {}
+    for seed in (0, 1):
+        random.seed(seed)
+        for (a, b) in combinations(range(1, 6), 2):  # Wrapper_dev.py:67-123
+            key = f"s{seed}_{a}_{b}"
+            _idx = np.where(ff[:, a - 1] & ff[:, b - 1])
+            c1 = np.hstack((fx[_idx, a - 1].reshape((-1, 1)), fy[_idx, a - 1].reshape((-1, 1))))
+            c2 = np.hstack((fx[_idx, b - 1].reshape((-1, 1)), fy[_idx, b - 1].reshape((-1, 1))))
+            idx = np.array(_idx).reshape(-1)
+            st0 = random.getstate()
+            H, h_idx = ref.h.get_homography_inliers(c1, c2, idx, threshold=30, n_max=1000)
+            st1 = random.getstate()
+            out[key + "_x1"], out[key + "_x2"], out[key + "_index"] = c1, c2, idx
+            out[key + "_state_before"], out[key + "_state_after"] = state_to_array(st0), state_to_array(st1)
+            out[key + "_H"] = np.full((3, 3), np.nan) if H is None else H
+            out[key + "_inlier_idx"] = np.asarray(h_idx, dtype=np.int64)
+            if seed == 0 and (a, b) == (1, 2):
+                out[key + "_counts"] = per_hypothesis_counts_h(ref, c1, c2, 30, 1000, st0)
+                random.setstate(st1)
+            if H is None or len(h_idx) == 0:
+                continue
+            i1 = np.hstack((fx[h_idx, a - 1].reshape((-1, 1)), fy[h_idx, a - 1].reshape((-1, 1))))
+            i2 = np.hstack((fx[h_idx, b - 1].reshape((-1, 1)), fy[h_idx, b - 1].reshape((-1, 1))))
+            ref.r.get_inliers_ransac(i1, i2, h_idx, threshold=0.06, n_max=1000)  # keeps the RNG stream in step
+            print(key, len(idx), len(h_idx))
+    # synthetic plane scene and cfg2's non-planar scene
+    px1, px2 = plane_scene()
+    x1, x2, _, _ = syn.two_view(seed=0)
+    for name, (p1, p2, n_max, seed) in {"plane": (px1, px2, 4096, 0), "cfg2": (x1, x2, 2000, 1)}.items():
+        random.seed(seed)
+        st0 = random.getstate()
+        t = time.time()
+        H, inl = ref.h.get_homography_inliers(p1, p2, np.arange(len(p1)), threshold=30, n_max=n_max)
+        dt = time.time() - t
+        st1 = random.getstate()
+        out[name + "_x1"], out[name + "_x2"] = p1, p2
+        out[name + "_state_before"], out[name + "_state_after"] = state_to_array(st0), state_to_array(st1)
+        out[name + "_H"], out[name + "_inlier_idx"] = H, np.asarray(inl, dtype=np.int64)
+        out[name + "_counts"] = per_hypothesis_counts_h(ref, p1, p2, 30, n_max, st0)
+        out[name + "_ref_seconds"] = np.array(dt)
+        print(f"{name}: n_max={n_max} inliers={len(inl)} ref {dt:.2f}s")
+    # find_homography: 512 random 4-point samples of the plane scene, and N-point fits
+    rng = np.random.default_rng(11)
+    s4 = np.stack([rng.choice(len(px1), 4, replace=False) for _ in range(512)])
+    out["f4_p1"], out["f4_p2"] = px1[s4], px2[s4]
+    out["f4_H"] = np.stack([ref.h.find_homography(px1[s], px2[s]) for s in s4])
+    for n in (4, 5, 9, 64, 1000):
+        s = rng.choice(len(px1), n, replace=False)
+        out[f"fN{n}_p1"], out[f"fN{n}_p2"] = px1[s], px2[s]
+        out[f"fN{n}_H"] = ref.h.find_homography(px1[s], px2[s])
+    np.savez_compressed(os.path.join(HERE, "homography.npz"), **out)
+
+
 def gen_nltri(ref):
     K = syn.K_REF
     tri = np.load(os.path.join(HERE, "triangulation.npz"))
@@ -303,6 +400,8 @@ def main():
         gen_cfg2(ref)
     if not only or "tri" in only:
         gen_triangulation(ref, p3)
+    if not only or "homography" in only:
+        gen_homography(ref)
     if not only or "nltri" in only:
         gen_nltri(ref)
     if not only or "ba" in only:

@@ -47,6 +47,9 @@ REFERENCE_SIGNATURES = {
     ("GetInliersRANSAC", "GetInliersRANSAC"): "(points1, points2, index, threshold=0.06, n_max=1000)",
     ("GetInliersRANSAC", "get_inliers_ransac"): "(points1, points2, index, threshold=0.06, n_max=1000)",
     ("GetInliersRANSAC", "EstimateFundamentalMatrix"): "(points1, points2)",
+    ("GetHomographyInliers", "find_homography"): "(image1_coords, image2_coords)",
+    ("GetHomographyInliers", "get_homography_inliers"):
+        "(image1_coords_org, image2_coords_org, idx, threshold=30, n_max=1000)",
     ("LinearTriangulation", "LinearTriangulation"): "(K, C1, R1, C2, R2, x1, x2)",
     ("LinearTriangulation", "linear_triangulation"): "(K, C1, R1, C2, R2, x1, x2)",
     ("NonLinearTriangulation", "Loss"): "(X, x1, x2, P1, P2)",

@@ -249,6 +249,99 @@ def test_nonlinear_triangulation_large_vs_oracle(core):
     assert np.all(cost(X[ok], ok) <= cost(X0[ok], ok) * (1 + 1e-9) + 1e-12)
 
 
+# --------------------------------------------------------------- homography
+def _set_state(st):
+    random.setstate((3, tuple(int(v) for v in st), None))
+
+
+def _state_array():
+    return np.array(random.getstate()[1], dtype=np.uint64).astype(np.uint32)
+
+
+def test_find_homography_matches_reference(core, golden):
+    from GetHomographyInliers import find_homography
+    g = golden("homography.npz")
+    Hs = core.h4_batch(g["f4_p1"], g["f4_p2"])
+    r = np.abs(Hs - g["f4_H"]).max(axis=(1, 2)) / np.abs(g["f4_H"]).max(axis=(1, 2))
+    assert r.max() < 1e-9
+    for n in (4, 5, 9, 64, 1000):
+        assert rel(find_homography(g[f"fN{n}_p1"], g[f"fN{n}_p2"]), g[f"fN{n}_H"]) < 1e-9
+    with pytest.raises(ValueError):
+        find_homography(np.zeros((3, 2)), np.zeros((3, 2)))
+
+
+@pytest.mark.parametrize("key,H", [("s0_1_2", 1000), ("plane", 4096), ("cfg2", 2000)])
+def test_homography_ransac_counts_bit_exact(core, golden, key, H):
+    g = golden("homography.npz")
+    x1, x2 = g[key + "_x1"], g[key + "_x2"]
+    _set_state(g[key + "_state_before"])
+    samples = core.sample_table(len(x1), 4, H)
+    assert np.array_equal(_state_array(), g[key + "_state_after"])
+    best, Hb, mask, counts = core.ransac_h4(x1, x2, samples, 30.0, want_counts=True)
+    assert np.array_equal(counts, g[key + "_counts"])
+    assert best == int(np.argmax(g[key + "_counts"]))
+    assert rel(Hb, g[key + "_H"]) < 1e-9
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_p3data_pair_loop_homography_then_f(core, golden, seed):
+    """The driver's pair loop (Wrapper_dev.py:67-123) through the drop-ins:
+    homography RANSAC then F-RANSAC on its inliers, for all 10 pairs, with
+    one global random stream.  Every H, H-inlier set, MT state, F and
+    F-inlier set equals the reference's."""
+    from GetHomographyInliers import get_homography_inliers
+    from GetInliersRANSAC import get_inliers_ransac
+    from itertools import combinations
+    g, p = golden("homography.npz"), golden("ransac_p3data.npz")
+    fx, fy = p["feature_x"], p["feature_y"]
+    random.seed(seed)
+    for (a, b) in combinations(range(1, 6), 2):
+        key = f"s{seed}_{a}_{b}"
+        assert np.array_equal(_state_array(), g[key + "_state_before"]), key
+        H, h_idx = get_homography_inliers(g[key + "_x1"], g[key + "_x2"], g[key + "_index"], threshold=30,
+                                          n_max=1000)
+        assert np.array_equal(_state_array(), g[key + "_state_after"]), key
+        assert rel(H, g[key + "_H"]) < 1e-9, key
+        assert np.array_equal(h_idx, g[key + "_inlier_idx"]), key
+        i1 = np.hstack((fx[h_idx, a - 1].reshape((-1, 1)), fy[h_idx, a - 1].reshape((-1, 1))))
+        i2 = np.hstack((fx[h_idx, b - 1].reshape((-1, 1)), fy[h_idx, b - 1].reshape((-1, 1))))
+        F, f_idx = get_inliers_ransac(i1, i2, h_idx, threshold=0.06, n_max=1000)
+        assert np.array_equal(_state_array(), p[key + "_state_after"]), key
+        assert np.array_equal(np.asarray(f_idx, dtype=np.int64), p[key + "_inlier_idx"]), key
+
+
+def test_homography_ransac_edge_cases(core):
+    from GetHomographyInliers import get_homography_inliers
+    random.seed(3)
+    st = random.getstate()
+    H, inl = get_homography_inliers(np.zeros((3, 2)), np.zeros((3, 2)), np.arange(3))
+    assert H is None and len(inl) == 0 and random.getstate() == st  # no draw below 4 points
+    x1, x2, _, _ = syn.two_view(n=300, seed=2)
+    H, inl = get_homography_inliers(x1, x2, np.arange(300), threshold=0, n_max=50)
+    assert H is None and len(inl) == 0  # strict '<' against 0 never holds
+    H, inl = get_homography_inliers(x1, x2, np.arange(300), n_max=0)
+    assert H is None and len(inl) == 0
+    # ties: duplicated hypotheses keep the earliest
+    random.seed(5)
+    samples = core.sample_table(300, 4, 64)
+    samples = np.concatenate([samples, samples])
+    best, _, _, counts = core.ransac_h4(x1, x2, samples, 30.0, want_counts=True)
+    assert best == int(np.argmax(counts)) and best < 64
+
+
+def test_homography_ransac_large_vs_oracle(core):
+    """N = 200k points, 2048 hypotheses: counts equal the oracle's on every
+    hypothesis (the oracle sweeps all N), and the winner's mask reproduces
+    its count."""
+    x1, x2, _, _ = syn.two_view(n=200_000, seed=9, outlier_frac=0.3)
+    random.seed(9)
+    samples = core.sample_table(len(x1), 4, 2048)
+    best, Hb, mask, counts = core.ransac_h4(x1, x2, samples, 30.0, want_counts=True)
+    Hs = core.h4_batch(x1[samples[:256]], x2[samples[:256]])
+    assert np.array_equal(counts[:256], O.h_score(x1, x2, Hs, 30.0))
+    assert mask.sum() == counts[best] == counts.max()
+
+
 # ---------------------------------------------------------------------- BA
 def test_project_and_residuals_match_oracle(core):
     from BundleAdjustment import bundle_adjustment_residuals, project_points

@@ -83,6 +83,37 @@ def test_triangulation_matches_reference(golden):
     assert rel.max() < 1e-9
 
 
+def _h_samples(state, n, H):
+    random.setstate((3, tuple(int(v) for v in state), None))
+    return np.array([random.sample(range(n), 4) for _ in range(H)], dtype=np.int32)
+
+
+def test_homography_oracle_matches_reference(golden):
+    g = golden("homography.npz")
+    Hs = np.stack([O.homography(a, b) for a, b in zip(g["f4_p1"], g["f4_p2"])])
+    rel = np.abs(Hs - g["f4_H"]).max(axis=(1, 2)) / np.abs(g["f4_H"]).max(axis=(1, 2))
+    assert rel.max() < 1e-9
+    for n in (4, 5, 9, 64, 1000):
+        Hr = g[f"fN{n}_H"]
+        assert np.abs(O.homography(g[f"fN{n}_p1"], g[f"fN{n}_p2"]) - Hr).max() / np.abs(Hr).max() < 1e-9
+    with pytest.raises(ValueError):
+        O.homography(np.zeros((3, 2)), np.zeros((3, 2)))
+
+
+@pytest.mark.parametrize("key,H", [("s0_1_2", 1000), ("plane", 4096), ("cfg2", 2000)])
+def test_homography_ransac_oracle_counts(golden, key, H):
+    """Every hypothesis count equals the reference's own (n_max=1 replays)."""
+    g = golden("homography.npz")
+    x1, x2 = g[key + "_x1"], g[key + "_x2"]
+    samples = _h_samples(g[key + "_state_before"], len(x1), H)
+    best, counts, Hb, mask = O.ransac_h(x1, x2, samples)
+    assert np.array_equal(counts, g[key + "_counts"])
+    assert best == int(np.argmax(g[key + "_counts"]))
+    if key != "s0_1_2":
+        assert np.array_equal(np.where(mask)[0], g[key + "_inlier_idx"])
+        assert np.abs(Hb - g[key + "_H"]).max() / np.abs(g[key + "_H"]).max() < 1e-9
+
+
 def _nltri_sets(t, g):
     """(label, C2, R2, x1, x2, X0, expected) for every nltri.npz case."""
     for i in range(4):
