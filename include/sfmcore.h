@@ -91,6 +91,29 @@ int sfm_ransac_h4(const double *x1, const double *x2, int64_t N, const int32_t *
                   uint8_t *best_mask, int device);
 
 /* ---------------------------------------------------------------------
+ * PnP (LinearPnP.py, PnPRANSAC.py, NonlinearPnP.py); K is 3x3 row-major.
+ * sfm_linear_pnp: LinearPnP on N >= 4 points (X: N x 3, x: N x 2) ->
+ *   C (3), R (9); *branch (nullable) = 1 where R's final orthogonalisation
+ *   is the LAPACK-noise-defined case (det(R) < 0).
+ * sfm_pnp_ransac: PnPRANSAC's loop (:48-80) over a host-drawn H x 4 sample
+ *   table: LinearPnP per hypothesis, reprojection error < thr counted;
+ *   *best_iter = first strict maximum (-1 if every count is 0) and
+ *   *best_count its count -- the caller applies the reference's fallback
+ *   (:82-87, LinearPnP on all points when best_count < 4).
+ * sfm_nonlinear_pnp: NonlinearPnP (:47-123), scipy 'lm' semantics with
+ *   max_nfev on the 2N-residual loss (:5-44); info: MINPACK info, 0 for the
+ *   N < 4 early return, -1 where the reference's except keeps (C0, R0).
+ * ------------------------------------------------------------------- */
+int sfm_linear_pnp(const double *X, const double *x, int64_t N, const double *K, double *C_out,
+                   double *R_out, int32_t *branch, int device);
+int sfm_pnp_ransac(const double *X, const double *x, int64_t N, const double *K, const int32_t *samples,
+                   int64_t H, double thr, int32_t *counts_out, int32_t *branch_out, int64_t *best_iter,
+                   int64_t *best_count, double *C_best, double *R_best, int device);
+int sfm_nonlinear_pnp(const double *X, const double *x, int64_t N, const double *K, const double *C0,
+                      const double *R0, int32_t max_nfev, double *C_out, double *R_out, int32_t *info,
+                      int device);
+
+/* ---------------------------------------------------------------------
  * LinearTriangulation (LinearTriangulation.py:3-92)
  * P1, P2: 3 x 4 projection matrices K[R | -RC]; x1, x2: N x 2; X: N x 3.
  * ------------------------------------------------------------------- */

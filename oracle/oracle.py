@@ -63,6 +63,15 @@ def lib():
         L.orc_h_score.argtypes = [_d, _d, ctypes.c_int64, _d, ctypes.c_int64, ctypes.c_double, _i32]
         L.orc_ransac_h.argtypes = [_d, _d, ctypes.c_int64, _i32, ctypes.c_int64, ctypes.c_double, _i32, _d, _u8]
         L.orc_ransac_h.restype = ctypes.c_int64
+        L.orc_linear_pnp.argtypes = [_d, _d, ctypes.c_int64, _d, _d, _d, ctypes.POINTER(ctypes.c_int)]
+        L.orc_linear_pnp.restype = ctypes.c_int
+        L.orc_pnp_count.argtypes = [_d, _d, ctypes.c_int64, _d, _d, _d, ctypes.c_double]
+        L.orc_pnp_count.restype = ctypes.c_int64
+        L.orc_pnp_ransac.argtypes = [_d, _d, ctypes.c_int64, _d, _i32, ctypes.c_int64, ctypes.c_double, _i32, _i32,
+                                     _d, _d]
+        L.orc_pnp_ransac.restype = ctypes.c_int64
+        L.orc_nonlinear_pnp.argtypes = [_d, _d, ctypes.c_int64, _d, _d, _d, ctypes.c_int32, _d, _d]
+        L.orc_nonlinear_pnp.restype = ctypes.c_int
         L.orc_nltri.argtypes = [_d, _d, _d, _d, _d, ctypes.c_int64, ctypes.c_int32, _d, _i32]
         L.orc_R_to_rotvec.argtypes = [_d, _d]
         _LIB = L
@@ -143,6 +152,41 @@ def ransac_h(x1, x2, samples, thr=30.0):
     best = lib().orc_ransac_h(_p(x1), _p(x2), len(x1), _p(samples, _i32), len(samples), thr, _p(counts, _i32),
                               _p(H), _p(m, _u8))
     return int(best), counts, H.reshape(3, 3), m.astype(bool)
+
+
+def linear_pnp(X, x, K):
+    """LinearPnP.py:3-96.  Returns (C, R, branch): branch 1 = the
+    LAPACK-noise-defined orthogonalisation (see sfm_oracle_pnp.c)."""
+    X, x, K = f64(np.reshape(X, (-1, 3))), f64(np.reshape(x, (-1, 2))), f64(K)
+    C, R, br = np.zeros(3), np.zeros(9), ctypes.c_int(0)
+    if lib().orc_linear_pnp(_p(X), _p(x), len(X), _p(K), _p(C), _p(R), ctypes.byref(br)) != 0:
+        raise ValueError("At least 4 point correspondences are required for PnP")
+    return C, R.reshape(3, 3), br.value
+
+
+def pnp_count(X, x, K, C, R, thr):
+    X, x, K, C, R = f64(X), f64(x), f64(K), f64(C), f64(R)
+    return int(lib().orc_pnp_count(_p(X), _p(x), len(X), _p(K), _p(C), _p(R), thr))
+
+
+def pnp_ransac(X, x, K, samples, thr):
+    """Returns (best or -1 for the all-point fallback, counts, branches, C, R)."""
+    X, x, K = f64(X), f64(x), f64(K)
+    samples = np.ascontiguousarray(samples, dtype=np.int32)
+    H = len(samples)
+    counts, branches = np.zeros(H, dtype=np.int32), np.zeros(H, dtype=np.int32)
+    C, R = np.zeros(3), np.zeros(9)
+    best = lib().orc_pnp_ransac(_p(X), _p(x), len(X), _p(K), _p(samples, _i32), H, thr, _p(counts, _i32),
+                                _p(branches, _i32), _p(C), _p(R))
+    return int(best), counts, branches, C, R.reshape(3, 3)
+
+
+def nonlinear_pnp(X, x, K, C0, R0, max_nfev=100):
+    """NonlinearPnP.py:47-123.  Returns (C, R, info)."""
+    X, x, K, C0, R0 = f64(np.reshape(X, (-1, 3))), f64(np.reshape(x, (-1, 2))), f64(K), f64(C0), f64(R0)
+    C, R = np.zeros(3), np.zeros(9)
+    info = lib().orc_nonlinear_pnp(_p(X), _p(x), len(X), _p(K), _p(C0), _p(R0), max_nfev, _p(C), _p(R))
+    return C, R.reshape(3, 3), int(info)
 
 
 def projection(K, C, R):

@@ -40,7 +40,7 @@
 /* On return A's columns are U*S, V (n x n, row-major) the right        */
 /* singular vectors as columns, s the column norms.                    */
 /* ------------------------------------------------------------------ */
-static void jacobi_svd(double *A, int m, int n, double *V, double *s) {
+void orc_jacobi_svd(double *A, int m, int n, double *V, double *s) {
     for (int i = 0; i < n; ++i)
         for (int j = 0; j < n; ++j) V[i * n + j] = (i == j) ? 1.0 : 0.0;
     for (int sweep = 0; sweep < 60; ++sweep) {
@@ -141,9 +141,9 @@ int orc_f8(const double *p1, const double *p2, int64_t n, double *F_out) {
             A[k * 9 + k] = alpha;
             for (int64_t i = k + 1; i < n; ++i) A[i * 9 + k] = 0.0;
         }
-        jacobi_svd(A, 9, 9, V, s);
+        orc_jacobi_svd(A, 9, 9, V, s);
     } else {
-        jacobi_svd(A, (int)n, 9, V, s);
+        orc_jacobi_svd(A, (int)n, 9, V, s);
     }
     free(A);
     int j = argmin(s, 9);
@@ -153,7 +153,7 @@ int orc_f8(const double *p1, const double *p2, int64_t n, double *F_out) {
      * largest singular triplets = B V^T with the weakest column of B zeroed */
     double B[9], W[9], sw[3];
     memcpy(B, f, sizeof B);
-    jacobi_svd(B, 3, 3, W, sw);
+    orc_jacobi_svd(B, 3, 3, W, sw);
     int z = argmin(sw, 3);
     double F2[9];
     for (int r = 0; r < 3; ++r)
@@ -278,9 +278,9 @@ static void null_vector_9(double *A, int64_t m, double *f) {
             A[k * 9 + k] = alpha;
             for (int64_t i = k + 1; i < m; ++i) A[i * 9 + k] = 0.0;
         }
-        jacobi_svd(A, 9, 9, V, s);
+        orc_jacobi_svd(A, 9, 9, V, s);
     } else {
-        jacobi_svd(A, (int)m, 9, V, s);
+        orc_jacobi_svd(A, (int)m, 9, V, s);
     }
     int j = argmin(s, 9);
     for (int k = 0; k < 9; ++k) f[k] = V[k * 9 + j];
@@ -389,7 +389,7 @@ void orc_triangulate(const double *P1, const double *P2, const double *x1, const
             A[2 * 4 + c] = v2 * P2[8 + c] - P2[4 + c];
             A[3 * 4 + c] = P2[0 + c] - u2 * P2[8 + c];
         }
-        jacobi_svd(A, 4, 4, V, s);
+        orc_jacobi_svd(A, 4, 4, V, s);
         int j = argmin(s, 4);
         double h0 = V[0 * 4 + j], h1 = V[1 * 4 + j], h2 = V[2 * 4 + j], h3 = V[3 * 4 + j];
         if (fabs(h3) > 1e-8) {

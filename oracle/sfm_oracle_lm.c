@@ -16,8 +16,9 @@
 #include <stdint.h>
 #include <string.h>
 
-#define LM_MAXM 8
-#define LM_MAXN 6
+#include <stdlib.h>
+
+#define LM_MAXN 8  /* parameters; residual count m is dynamic */
 
 typedef void (*lm_fcn)(const double *x, double *f, const void *ctx);
 
@@ -61,11 +62,13 @@ static double enorm(int n, const double *x) {
     return x3max * sqrt(s3);
 }
 
-/* a is m x n column-major with leading dimension LM_MAXM: a[j][i] = A(i,j) */
-static void qrfac(int m, int n, double a[LM_MAXN][LM_MAXM], int *ipvt, double *rdiag, double *acnorm) {
+/* column-major with leading dimension lda: COL(a, j)[i] = A(i, j) */
+#define COL(a, j) ((a) + (size_t)(j) * lda)
+
+static void qrfac(int m, int n, double *a, int lda, int *ipvt, double *rdiag, double *acnorm) {
     double wa[LM_MAXN];
     for (int j = 0; j < n; ++j) {
-        acnorm[j] = enorm(m, a[j]);
+        acnorm[j] = enorm(m, COL(a, j));
         rdiag[j] = acnorm[j];
         wa[j] = rdiag[j];
         ipvt[j] = j;
@@ -77,9 +80,9 @@ static void qrfac(int m, int n, double a[LM_MAXN][LM_MAXM], int *ipvt, double *r
             if (rdiag[k] > rdiag[kmax]) kmax = k;
         if (kmax != j) {
             for (int i = 0; i < m; ++i) {
-                const double t = a[j][i];
-                a[j][i] = a[kmax][i];
-                a[kmax][i] = t;
+                const double t = COL(a, j)[i];
+                COL(a, j)[i] = COL(a, kmax)[i];
+                COL(a, kmax)[i] = t;
             }
             rdiag[kmax] = rdiag[j];
             wa[kmax] = wa[j];
@@ -87,23 +90,23 @@ static void qrfac(int m, int n, double a[LM_MAXN][LM_MAXM], int *ipvt, double *r
             ipvt[j] = ipvt[kmax];
             ipvt[kmax] = k;
         }
-        double ajnorm = enorm(m - j, &a[j][j]);
+        double ajnorm = enorm(m - j, COL(a, j) + j);
         if (ajnorm != 0.0) {
-            if (a[j][j] < 0.0) ajnorm = -ajnorm;
-            for (int i = j; i < m; ++i) a[j][i] /= ajnorm;
-            a[j][j] += 1.0;
+            if (COL(a, j)[j] < 0.0) ajnorm = -ajnorm;
+            for (int i = j; i < m; ++i) COL(a, j)[i] /= ajnorm;
+            COL(a, j)[j] += 1.0;
             for (int k = j + 1; k < n; ++k) {
                 double sum = 0.0;
-                for (int i = j; i < m; ++i) sum += a[j][i] * a[k][i];
-                const double temp = sum / a[j][j];
-                for (int i = j; i < m; ++i) a[k][i] -= temp * a[j][i];
+                for (int i = j; i < m; ++i) sum += COL(a, j)[i] * COL(a, k)[i];
+                const double temp = sum / COL(a, j)[j];
+                for (int i = j; i < m; ++i) COL(a, k)[i] -= temp * COL(a, j)[i];
                 if (rdiag[k] != 0.0) {
-                    const double t = a[k][j] / rdiag[k];
+                    const double t = COL(a, k)[j] / rdiag[k];
                     const double t2 = 1.0 - t * t;
                     rdiag[k] *= sqrt(t2 > 0.0 ? t2 : 0.0);
                     const double q = rdiag[k] / wa[k];
                     if (0.05 * (q * q) <= EPSMCH) {
-                        rdiag[k] = enorm(m - j - 1, &a[k][j + 1]);
+                        rdiag[k] = enorm(m - j - 1, COL(a, k) + j + 1);
                         wa[k] = rdiag[k];
                     }
                 }
@@ -113,12 +116,12 @@ static void qrfac(int m, int n, double a[LM_MAXN][LM_MAXM], int *ipvt, double *r
     }
 }
 
-static void qrsolv(int n, double r[LM_MAXN][LM_MAXM], const int *ipvt, const double *diag, const double *qtb,
+static void qrsolv(int n, double *r, int lda, const int *ipvt, const double *diag, const double *qtb,
                    double *x, double *sdiag) {
     double wa[LM_MAXN];
     for (int j = 0; j < n; ++j) {
-        for (int i = j; i < n; ++i) r[j][i] = r[i][j];
-        x[j] = r[j][j];
+        for (int i = j; i < n; ++i) COL(r, j)[i] = COL(r, i)[j];
+        x[j] = COL(r, j)[j];
         wa[j] = qtb[j];
     }
     for (int j = 0; j < n; ++j) {
@@ -130,28 +133,28 @@ static void qrsolv(int n, double r[LM_MAXN][LM_MAXM], const int *ipvt, const dou
             for (int k = j; k < n; ++k) {
                 if (sdiag[k] == 0.0) continue;
                 double sn, cs;
-                if (fabs(r[k][k]) < fabs(sdiag[k])) {
-                    const double cotan = r[k][k] / sdiag[k];
+                if (fabs(COL(r, k)[k]) < fabs(sdiag[k])) {
+                    const double cotan = COL(r, k)[k] / sdiag[k];
                     sn = 0.5 / sqrt(0.25 + 0.25 * cotan * cotan);
                     cs = sn * cotan;
                 } else {
-                    const double tn = sdiag[k] / r[k][k];
+                    const double tn = sdiag[k] / COL(r, k)[k];
                     cs = 0.5 / sqrt(0.25 + 0.25 * tn * tn);
                     sn = cs * tn;
                 }
-                r[k][k] = cs * r[k][k] + sn * sdiag[k];
+                COL(r, k)[k] = cs * COL(r, k)[k] + sn * sdiag[k];
                 const double temp = cs * wa[k] + sn * qtbpj;
                 qtbpj = -sn * wa[k] + cs * qtbpj;
                 wa[k] = temp;
                 for (int i = k + 1; i < n; ++i) {
-                    const double t = cs * r[k][i] + sn * sdiag[i];
-                    sdiag[i] = -sn * r[k][i] + cs * sdiag[i];
-                    r[k][i] = t;
+                    const double t = cs * COL(r, k)[i] + sn * sdiag[i];
+                    sdiag[i] = -sn * COL(r, k)[i] + cs * sdiag[i];
+                    COL(r, k)[i] = t;
                 }
             }
         }
-        sdiag[j] = r[j][j];
-        r[j][j] = x[j];
+        sdiag[j] = COL(r, j)[j];
+        COL(r, j)[j] = x[j];
     }
     int nsing = n;
     for (int j = 0; j < n; ++j) {
@@ -160,25 +163,25 @@ static void qrsolv(int n, double r[LM_MAXN][LM_MAXM], const int *ipvt, const dou
     }
     for (int j = nsing - 1; j >= 0; --j) {
         double sum = 0.0;
-        for (int i = j + 1; i < nsing; ++i) sum += r[j][i] * wa[i];
+        for (int i = j + 1; i < nsing; ++i) sum += COL(r, j)[i] * wa[i];
         wa[j] = (wa[j] - sum) / sdiag[j];
     }
     for (int j = 0; j < n; ++j) x[ipvt[j]] = wa[j];
 }
 
-static void lmpar(int n, double r[LM_MAXN][LM_MAXM], const int *ipvt, const double *diag, const double *qtb,
+static void lmpar(int n, double *r, int lda, const int *ipvt, const double *diag, const double *qtb,
                   double delta, double *par, double *x, double *sdiag) {
     double wa1[LM_MAXN], wa2[LM_MAXN];
     int nsing = n;
     for (int j = 0; j < n; ++j) {
         wa1[j] = qtb[j];
-        if (r[j][j] == 0.0 && nsing == n) nsing = j;
+        if (COL(r, j)[j] == 0.0 && nsing == n) nsing = j;
         if (nsing < n) wa1[j] = 0.0;
     }
     for (int j = nsing - 1; j >= 0; --j) {
-        wa1[j] /= r[j][j];
+        wa1[j] /= COL(r, j)[j];
         const double temp = wa1[j];
-        for (int i = 0; i < j; ++i) wa1[i] -= r[j][i] * temp;
+        for (int i = 0; i < j; ++i) wa1[i] -= COL(r, j)[i] * temp;
     }
     for (int j = 0; j < n; ++j) x[ipvt[j]] = wa1[j];
     int iter = 0;
@@ -197,15 +200,15 @@ static void lmpar(int n, double r[LM_MAXN][LM_MAXM], const int *ipvt, const doub
         }
         for (int j = 0; j < n; ++j) {
             double sum = 0.0;
-            for (int i = 0; i < j; ++i) sum += r[j][i] * wa1[i];
-            wa1[j] = (wa1[j] - sum) / r[j][j];
+            for (int i = 0; i < j; ++i) sum += COL(r, j)[i] * wa1[i];
+            wa1[j] = (wa1[j] - sum) / COL(r, j)[j];
         }
         const double temp = enorm(n, wa1);
         parl = ((fp / delta) / temp) / temp;
     }
     for (int j = 0; j < n; ++j) {
         double sum = 0.0;
-        for (int i = 0; i <= j; ++i) sum += r[j][i] * qtb[i];
+        for (int i = 0; i <= j; ++i) sum += COL(r, j)[i] * qtb[i];
         wa1[j] = sum / diag[ipvt[j]];
     }
     const double gnorm = enorm(n, wa1);
@@ -219,7 +222,7 @@ static void lmpar(int n, double r[LM_MAXN][LM_MAXM], const int *ipvt, const doub
         if (*par == 0.0) *par = DWARF > 0.001 * paru ? DWARF : 0.001 * paru;
         const double temp = sqrt(*par);
         for (int j = 0; j < n; ++j) wa1[j] = temp * diag[j];
-        qrsolv(n, r, ipvt, wa1, qtb, x, sdiag);
+        qrsolv(n, r, lda, ipvt, wa1, qtb, x, sdiag);
         for (int j = 0; j < n; ++j) wa2[j] = diag[j] * x[j];
         dxnorm = enorm(n, wa2);
         const double fp_old = fp;
@@ -232,7 +235,7 @@ static void lmpar(int n, double r[LM_MAXN][LM_MAXM], const int *ipvt, const doub
         for (int j = 0; j < n; ++j) {
             wa1[j] /= sdiag[j];
             const double t = wa1[j];
-            for (int i = j + 1; i < n; ++i) wa1[i] -= r[j][i] * t;
+            for (int i = j + 1; i < n; ++i) wa1[i] -= COL(r, j)[i] * t;
         }
         const double t = enorm(n, wa1);
         const double parc = ((fp / delta) / t) / t;
@@ -247,9 +250,11 @@ static void lmpar(int n, double r[LM_MAXN][LM_MAXM], const int *ipvt, const doub
  * epsfcn = EPS).  Returns MINPACK's info; *nfev_out the evaluations. */
 int orc_lmdif(lm_fcn fcn, const void *ctx, int m, int n, double *x, double ftol, double xtol, double gtol,
               int maxfev, int *nfev_out) {
-    double fvec[LM_MAXM], fjac[LM_MAXN][LM_MAXM], diag[LM_MAXN], qtf[LM_MAXN];
-    double wa1[LM_MAXN], wa2[LM_MAXN], wa3[LM_MAXN], wa4[LM_MAXM];
+    double diag[LM_MAXN], qtf[LM_MAXN], wa1[LM_MAXN], wa2[LM_MAXN], wa3[LM_MAXN];
     int ipvt[LM_MAXN];
+    const int lda = m;
+    double *buf = (double *)malloc(sizeof(double) * (size_t)m * (n + 3));
+    double *fvec = buf, *wa4 = buf + m, *wf = buf + 2 * (size_t)m, *fjac = buf + 3 * (size_t)m;
     const double factor = 100.0;
     int info = 0, nfev = 0;
     for (int j = 0; j < n; ++j) diag[j] = 1.0;
@@ -266,13 +271,12 @@ int orc_lmdif(lm_fcn fcn, const void *ctx, int m, int n, double *x, double ftol,
             double h = eps * fabs(temp);
             if (h == 0.0) h = eps;
             x[j] = temp + h;
-            double wf[LM_MAXM];
             fcn(x, wf, ctx);
             x[j] = temp;
-            for (int i = 0; i < m; ++i) fjac[j][i] = (wf[i] - fvec[i]) / h;
+            for (int i = 0; i < m; ++i) COL(fjac, j)[i] = (wf[i] - fvec[i]) / h;
         }
         nfev += n;
-        qrfac(m, n, fjac, ipvt, wa1, wa2);
+        qrfac(m, n, fjac, lda, ipvt, wa1, wa2);
         if (iter == 1) {
             for (int j = 0; j < n; ++j) wa3[j] = diag[j] * x[j];
             xnorm = enorm(n, wa3);
@@ -281,13 +285,13 @@ int orc_lmdif(lm_fcn fcn, const void *ctx, int m, int n, double *x, double ftol,
         }
         for (int i = 0; i < m; ++i) wa4[i] = fvec[i];
         for (int j = 0; j < n; ++j) {
-            if (fjac[j][j] != 0.0) {
+            if (COL(fjac, j)[j] != 0.0) {
                 double sum = 0.0;
-                for (int i = j; i < m; ++i) sum += fjac[j][i] * wa4[i];
-                const double temp = -sum / fjac[j][j];
-                for (int i = j; i < m; ++i) wa4[i] += fjac[j][i] * temp;
+                for (int i = j; i < m; ++i) sum += COL(fjac, j)[i] * wa4[i];
+                const double temp = -sum / COL(fjac, j)[j];
+                for (int i = j; i < m; ++i) wa4[i] += COL(fjac, j)[i] * temp;
             }
-            fjac[j][j] = wa1[j];
+            COL(fjac, j)[j] = wa1[j];
             qtf[j] = wa4[j];
         }
         double gnorm = 0.0;
@@ -296,7 +300,7 @@ int orc_lmdif(lm_fcn fcn, const void *ctx, int m, int n, double *x, double ftol,
                 const int l = ipvt[j];
                 if (wa2[l] != 0.0) {
                     double sum = 0.0;
-                    for (int i = 0; i <= j; ++i) sum += fjac[j][i] * (qtf[i] / fnorm);
+                    for (int i = 0; i <= j; ++i) sum += COL(fjac, j)[i] * (qtf[i] / fnorm);
                     const double g = fabs(sum / wa2[l]);
                     if (g > gnorm) gnorm = g;
                 }
@@ -307,7 +311,7 @@ int orc_lmdif(lm_fcn fcn, const void *ctx, int m, int n, double *x, double ftol,
         /* inner loop */
         double ratio;
         do {
-            lmpar(n, fjac, ipvt, diag, qtf, delta, &par, wa1, wa2);
+            lmpar(n, fjac, lda, ipvt, diag, qtf, delta, &par, wa1, wa2);
             for (int j = 0; j < n; ++j) {
                 wa1[j] = -wa1[j];
                 wa2[j] = x[j] + wa1[j];
@@ -326,7 +330,7 @@ int orc_lmdif(lm_fcn fcn, const void *ctx, int m, int n, double *x, double ftol,
             for (int j = 0; j < n; ++j) {
                 wa3[j] = 0.0;
                 const double temp = wa1[ipvt[j]];
-                for (int i = 0; i <= j; ++i) wa3[i] += fjac[j][i] * temp;
+                for (int i = 0; i <= j; ++i) wa3[i] += COL(fjac, j)[i] * temp;
             }
             const double temp1 = enorm(n, wa3) / fnorm;
             const double temp2 = (sqrt(par) * pnorm) / fnorm;
@@ -369,6 +373,7 @@ int orc_lmdif(lm_fcn fcn, const void *ctx, int m, int n, double *x, double ftol,
         if (info != 0) break;
     }
     if (nfev_out) *nfev_out = nfev;
+    free(buf);
     return info;
 }
 

@@ -64,6 +64,9 @@ SIGNATURES = [
     ("sfm_h4_batch", _c, [_d, _d, _i, _d, _c]),
     ("sfm_homography_general", _c, [_d, _d, _i, _d, _c]),
     ("sfm_ransac_h4", _c, [_d, _d, _i, _i32, _i, ctypes.c_double, _i32, _i64, _d, _u8, _c]),
+    ("sfm_linear_pnp", _c, [_d, _d, _i, _d, _d, _d, _i32, _c]),
+    ("sfm_pnp_ransac", _c, [_d, _d, _i, _d, _i32, _i, ctypes.c_double, _i32, _i32, _i64, _i64, _d, _d, _c]),
+    ("sfm_nonlinear_pnp", _c, [_d, _d, _i, _d, _d, _d, ctypes.c_int32, _d, _d, _i32, _c]),
     ("sfm_triangulate_dlt", _c, [_d, _d, _d, _d, _i, _d, _c]),
     ("sfm_triangulate_nonlinear", _c, [_d, _d, _d, _d, _d, _i, ctypes.c_int32, _d, _i32, _c]),
     ("sfm_project_points", _c, [_d, _d, _i, _d, _c]),
@@ -213,6 +216,43 @@ def ransac_h4(x1, x2, samples, thr, want_counts=False, device=None):
     if b < 0:
         return -1, None, np.zeros(N, dtype=bool), counts
     return b, Hb.reshape(3, 3), mask.astype(bool), counts
+
+
+def linear_pnp(X, x, K):
+    """Returns (C (3,), R (3,3), branch)."""
+    require_device()
+    X, x, K = _f64(np.reshape(X, (-1, 3))), _f64(np.reshape(x, (-1, 2))), _f64(K)
+    C, R, br = np.zeros(3), np.zeros(9), np.zeros(1, dtype=np.int32)
+    _check(_lib.sfm_linear_pnp(_p(X), _p(x), len(X), _p(K), _p(C), _p(R), _p(br, _i32), DEVICE))
+    return C, R.reshape(3, 3), int(br[0])
+
+
+def pnp_ransac(X, x, K, samples, thr, want_counts=False):
+    """Returns (best_iter or -1, best_count, C, R, counts or None, branches or None)."""
+    require_device()
+    X, x, K = _f64(np.reshape(X, (-1, 3))), _f64(np.reshape(x, (-1, 2))), _f64(K)
+    samples = np.ascontiguousarray(samples, dtype=np.int32)
+    H = len(samples)
+    counts = np.zeros(H, dtype=np.int32) if want_counts else None
+    branches = np.zeros(H, dtype=np.int32) if want_counts else None
+    best, bc = np.zeros(1, dtype=np.int64), np.zeros(1, dtype=np.int64)
+    C, R = np.zeros(3), np.zeros(9)
+    _check(_lib.sfm_pnp_ransac(_p(X), _p(x), len(X), _p(K), _p(samples, _i32), H, float(thr),
+                               _p(counts, _i32) if want_counts else None,
+                               _p(branches, _i32) if want_counts else None, _p(best, _i64), _p(bc, _i64),
+                               _p(C), _p(R), DEVICE))
+    return int(best[0]), int(bc[0]), C, R.reshape(3, 3), counts, branches
+
+
+def nonlinear_pnp(X, x, K, C0, R0, max_nfev=100):
+    """Returns (C (3,), R (3,3), info)."""
+    require_device()
+    X, x, K = _f64(np.reshape(X, (-1, 3))), _f64(np.reshape(x, (-1, 2))), _f64(K)
+    C0, R0 = _f64(np.reshape(C0, 3)), _f64(np.reshape(R0, (3, 3)))
+    C, R, info = np.zeros(3), np.zeros(9), np.zeros(1, dtype=np.int32)
+    _check(_lib.sfm_nonlinear_pnp(_p(X), _p(x), len(X), _p(K), _p(C0), _p(R0), int(max_nfev), _p(C), _p(R),
+                                  _p(info, _i32), DEVICE))
+    return C, R.reshape(3, 3), int(info[0])
 
 
 def triangulate(P1, P2, x1, x2):

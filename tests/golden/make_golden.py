@@ -29,6 +29,12 @@ Outputs (tests/golden/*.npz):
                      outliers, n_max=4096) and on cfg2's non-planar scene,
                      both with per-hypothesis counts; find_homography on
                      random 4-point and N-point samples.
+  pnp.npz            LinearPnP on random 4-point samples and on N-point sets;
+                     PnPRANSAC (random.seed, MT state before/after, final
+                     pose) with every hypothesis' pose from the reference's
+                     own LinearPnP and its count by the reference's scoring
+                     expression (PnPRANSAC.py:60-70); NonlinearPnP on noisy
+                     starts, with outliers, and its n < 4 early return.
   nltri.npz          NonLinearTriangulation (per-point scipy 'lm', max_nfev=50)
                      on the four P3Data 1_2 pose candidates, on cfg2's noisy
                      inliers, on cfg2 outliers (hard, often non-converging
@@ -67,8 +73,11 @@ def _import_reference():
     import ExtractCameraPose as ref_p  # noqa
     import Utils as ref_u  # noqa
     import NonLinearTriangulation as ref_nt  # noqa
+    import LinearPnP as ref_lp  # noqa
+    import PnPRANSAC as ref_pr  # noqa
+    import NonlinearPnP as ref_np  # noqa
     return types.SimpleNamespace(f=ref_f, r=ref_r, t=ref_t, ba=ref_ba, h=ref_h, e=ref_e,
-                                 p=ref_p, u=ref_u, nt=ref_nt)
+                                 p=ref_p, u=ref_u, nt=ref_nt, lp=ref_lp, pr=ref_pr, np_=ref_np)
 
 
 def state_to_array(st):
@@ -349,6 +358,90 @@ def gen_homography(ref):
     np.savez_compressed(os.path.join(HERE, "homography.npz"), **out)
 
 
+def pnp_scene(n, seed, outlier_frac=0.0, noise=0.5):
+    """World points seen by cfg2's second camera: (X (n,3), x (n,2), C, R)."""
+    rng = np.random.default_rng(seed)
+    X = np.column_stack([rng.uniform(-3, 3, n), rng.uniform(-2, 2, n), rng.uniform(5, 12, n)])
+    R = syn.rotvec_to_matrix([0.02, -0.15, 0.01])[0]
+    C = np.array([1.0, 0.05, 0.1])
+    u = (syn.K_REF @ (R @ (X - C).T)).T
+    x = u[:, :2] / u[:, 2:3] + rng.normal(0, noise, (n, 2))
+    k = int(round(outlier_frac * n))
+    if k:
+        o = rng.choice(n, k, replace=False)
+        x[o] = np.column_stack([rng.uniform(0, 1280, k), rng.uniform(0, 960, k)])
+    return np.ascontiguousarray(X), np.ascontiguousarray(x), C, R
+
+
+def pnp_count(X, x, K, C, R, thr):
+    """PnPRANSAC.py:60-70's scoring expression for one pose."""
+    n = len(X)
+    X_hom = np.hstack([X, np.ones((n, 1))])
+    P = K @ np.hstack([R, -R @ C.reshape(3, 1)])
+    x_proj_hom = (P @ X_hom.T).T
+    x_proj = x_proj_hom[:, :2] / (x_proj_hom[:, 2:3] + 1e-8)
+    errors = np.sqrt(np.sum((x - x_proj) ** 2, axis=1))
+    return int(np.sum(errors < thr))
+
+
+def gen_pnp(ref):
+    K = syn.K_REF
+    out = {}
+    X, x, C, R = pnp_scene(500, 0, outlier_frac=0.3)
+    rng = np.random.default_rng(21)
+    s4 = np.stack([rng.choice(len(X), 4, replace=False) for _ in range(512)])
+    Cs, Rs = zip(*[ref.lp.LinearPnP(X[s], x[s], K) for s in s4])
+    out["lp4_X"], out["lp4_x"], out["lp4_C"], out["lp4_R"] = X[s4], x[s4], np.array(Cs), np.array(Rs)
+    for n in (5, 6, 10, 100, 500):
+        s = rng.choice(len(X), n, replace=False) if n < 500 else np.arange(500)
+        Xc, xc, _, _ = pnp_scene(n, 100 + n) if n < 500 else (X, x, None, None)
+        c_, r_ = ref.lp.LinearPnP(Xc, xc, K)
+        out[f"lpN{n}_X"], out[f"lpN{n}_x"], out[f"lpN{n}_C"], out[f"lpN{n}_R"] = Xc, xc, c_, r_
+    # PnPRANSAC: scenes x thresholds x seeds
+    cases = {"o30_t200": (500, 0, 0.3, 200.0, 1000), "o30_t8": (500, 0, 0.3, 8.0, 1000),
+             "o60_t4": (2000, 1, 0.6, 4.0, 2000)}
+    for name, (n, sseed, of, thr, n_max) in cases.items():
+        X, x, Ct, Rt = pnp_scene(n, sseed, outlier_frac=of)
+        for seed in (0, 1):
+            key = f"{name}_s{seed}"
+            random.seed(seed)
+            st0 = random.getstate()
+            t = time.time()
+            Cb, Rb = ref.pr.PnPRANSAC(X, x, K, threshold=thr, n_max=n_max)
+            dt = time.time() - t
+            st1 = random.getstate()
+            random.setstate(st0)
+            counts = np.zeros(n_max, dtype=np.int32)
+            hC = np.zeros((n_max, 3))
+            hR = np.zeros((n_max, 3, 3))
+            for h in range(n_max):
+                si = random.sample(range(n), 4)
+                hC[h], hR[h] = ref.lp.LinearPnP(X[si], x[si], K)
+                counts[h] = pnp_count(X, x, K, hC[h], hR[h], thr)
+            assert random.getstate() == st1
+            out[key + "_state_before"], out[key + "_state_after"] = state_to_array(st0), state_to_array(st1)
+            out[key + "_C"], out[key + "_R"], out[key + "_counts"] = Cb, Rb, counts
+            out[key + "_hC"], out[key + "_hR"] = hC[:256], hR[:256]  # first hypotheses' poses
+            out[key + "_ref_seconds"] = np.array(dt)
+            print(f"pnp {key}: best count {counts.max()} at {int(np.argmax(counts))}, ref {dt:.2f}s")
+        out[name + "_X"], out[name + "_x"], out[name + "_thr"] = X, x, np.array(thr)
+    # NonlinearPnP
+    for name, (n, sseed, of, pert) in {"clean50": (50, 5, 0.0, 0.02), "clean2000": (2000, 6, 0.0, 0.05),
+                                        "out500": (500, 7, 0.2, 0.02), "tiny3": (3, 8, 0.0, 0.02),
+                                        "four": (4, 9, 0.0, 0.01)}.items():
+        X, x, Ct, Rt = pnp_scene(n, sseed, outlier_frac=of)
+        rng = np.random.default_rng(sseed)
+        C0 = Ct + rng.normal(0, pert, 3)
+        R0 = syn.rotvec_to_matrix(rng.normal(0, pert, 3))[0] @ Rt
+        t = time.time()
+        Cn, Rn = ref.np_.nonlinear_PnP(K, C0, R0, x, X)
+        out["nl_" + name + "_seconds"] = np.array(time.time() - t)
+        out["nl_" + name + "_X"], out["nl_" + name + "_x"] = X, x
+        out["nl_" + name + "_C0"], out["nl_" + name + "_R0"] = C0, R0
+        out["nl_" + name + "_C"], out["nl_" + name + "_R"] = Cn, Rn
+    np.savez_compressed(os.path.join(HERE, "pnp.npz"), **out)
+
+
 def gen_nltri(ref):
     K = syn.K_REF
     tri = np.load(os.path.join(HERE, "triangulation.npz"))
@@ -404,6 +497,8 @@ def main():
         gen_homography(ref)
     if not only or "nltri" in only:
         gen_nltri(ref)
+    if not only or "pnp" in only:
+        gen_pnp(ref)
     if not only or "ba" in only:
         gen_ba(ref, a.skip_cfg3)
 

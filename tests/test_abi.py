@@ -50,6 +50,11 @@ REFERENCE_SIGNATURES = {
     ("GetHomographyInliers", "find_homography"): "(image1_coords, image2_coords)",
     ("GetHomographyInliers", "get_homography_inliers"):
         "(image1_coords_org, image2_coords_org, idx, threshold=30, n_max=1000)",
+    ("LinearPnP", "LinearPnP"): "(Xset, xset, K)",
+    ("PnPRANSAC", "PnPRANSAC"): "(X, x, K, threshold=200, n_max=1000)",
+    ("NonlinearPnP", "NonLinearPnPLoss"): "(X0, X, x, K)",
+    ("NonlinearPnP", "NonLinearPnP"): "(X, x, K, C, R)",
+    ("NonlinearPnP", "nonlinear_PnP"): "(K, C, R, x, X)",
     ("LinearTriangulation", "LinearTriangulation"): "(K, C1, R1, C2, R2, x1, x2)",
     ("LinearTriangulation", "linear_triangulation"): "(K, C1, R1, C2, R2, x1, x2)",
     ("NonLinearTriangulation", "Loss"): "(X, x1, x2, P1, P2)",

@@ -342,6 +342,128 @@ def test_homography_ransac_large_vs_oracle(core):
     assert mask.sum() == counts[best] == counts.max()
 
 
+# ---------------------------------------------------------------------- PnP
+def test_linear_pnp_matches_reference(core, golden):
+    from LinearPnP import LinearPnP
+    g = golden("pnp.npz")
+    well = agree = 0
+    for X, x, C, R in zip(g["lp4_X"], g["lp4_x"], g["lp4_C"], g["lp4_R"]):
+        c, r, br = core.linear_pnp(X, x, K)
+        co, ro, bro = O.linear_pnp(X, x, K)
+        assert br == bro
+        if br == 0:  # well-defined branch: the reference's pose
+            well += 1
+            assert np.abs(c - C).max() <= 1e-9 * max(1.0, np.abs(C).max())
+            assert np.abs(r - R).max() <= 1e-9
+        else:
+            agree += np.abs(r - ro).max() < 1e-6
+    assert well >= 256
+    for n in (5, 6, 10, 100, 500):
+        C, R = LinearPnP(g[f"lpN{n}_X"], g[f"lpN{n}_x"], K)
+        if core.linear_pnp(g[f"lpN{n}_X"], g[f"lpN{n}_x"], K)[2] == 0:
+            assert np.abs(C - g[f"lpN{n}_C"]).max() <= 1e-9 * max(1.0, np.abs(g[f"lpN{n}_C"]).max()), n
+            assert np.abs(R - g[f"lpN{n}_R"]).max() <= 1e-9, n
+    with pytest.raises(ValueError):
+        LinearPnP(np.zeros((3, 3)), np.zeros((3, 2)), K)
+
+
+@pytest.mark.parametrize("name", ["o30_t200", "o30_t8", "o60_t4"])
+@pytest.mark.parametrize("seed", [0, 1])
+def test_pnp_ransac_matches_reference(core, golden, name, seed):
+    """PnPRANSAC through the drop-in: the global random stream, the winner
+    and the final pose equal the reference's; per-hypothesis counts equal on
+    every well-defined hypothesis."""
+    from PnPRANSAC import PnPRANSAC
+    g = golden("pnp.npz")
+    X, x, thr = g[name + "_X"], g[name + "_x"], float(g[name + "_thr"])
+    key = f"{name}_s{seed}"
+    ref_counts = g[key + "_counts"]
+    _set_state(g[key + "_state_before"])
+    C, R = PnPRANSAC(X, x, K, threshold=thr, n_max=len(ref_counts))
+    assert np.array_equal(_state_array(), g[key + "_state_after"])
+    assert np.abs(C - g[key + "_C"]).max() <= 1e-9 * max(1.0, np.abs(g[key + "_C"]).max())
+    assert np.abs(R - g[key + "_R"]).max() <= 1e-9
+    _set_state(g[key + "_state_before"])
+    samples = core.sample_table(len(X), 4, len(ref_counts))
+    best, bc, _, _, counts, branches = core.pnp_ransac(X, x, K, samples, thr, want_counts=True)
+    well = branches == 0
+    assert np.array_equal(counts[well], ref_counts[well])
+    assert best == int(np.argmax(ref_counts)) and bc == ref_counts.max()
+
+
+def test_pnp_ransac_fallback_and_edges(core, capsys):
+    from PnPRANSAC import PnPRANSAC
+    X, x, _, _ = _pnp_scene(300, 3)
+    random.seed(4)
+    C, R = PnPRANSAC(X, x, K, threshold=1e-12, n_max=20)  # no hypothesis reaches 4 inliers
+    assert "Warning: PnP RANSAC failed, using linear PnP on all points" in capsys.readouterr().out
+    Co, Ro, br = O.linear_pnp(X, x, K)
+    assert core.linear_pnp(X, x, K)[2] == br
+    if br == 0:  # the det(R) < 0 branch is LAPACK-noise defined (DESIGN.md)
+        assert np.abs(C - Co).max() <= 1e-8 * np.abs(Co).max() and np.abs(R - Ro).max() <= 1e-8
+    assert np.abs(R @ R.T - np.eye(3)).max() < 1e-12 and np.linalg.det(R) > 0
+    with pytest.raises(ValueError):
+        PnPRANSAC(X[:3], x[:3], K)
+
+
+def _pnp_scene(n, seed, outlier_frac=0.0):
+    rng = np.random.default_rng(seed)
+    X = np.column_stack([rng.uniform(-3, 3, n), rng.uniform(-2, 2, n), rng.uniform(5, 12, n)])
+    R = syn.rotvec_to_matrix([0.02, -0.15, 0.01])[0]
+    C = np.array([1.0, 0.05, 0.1])
+    u = (K @ (R @ (X - C).T)).T
+    x = u[:, :2] / u[:, 2:3] + rng.normal(0, 0.5, (n, 2))
+    k = int(round(outlier_frac * n))
+    if k:
+        o = rng.choice(n, k, replace=False)
+        x[o] = np.column_stack([rng.uniform(0, 1280, k), rng.uniform(0, 960, k)])
+    return X, x, C, R
+
+
+def test_nonlinear_pnp_matches_reference(core, golden, capsys):
+    """Device sin/cos are not correctly rounded and the m-long reductions
+    run in parallel, so the GPU lmdif is not bit-identical: it stops at the
+    same minimum (cost within 1e-9 relative of the reference's) with the pose
+    within 1e-5 (ftol-terminated LM pins flat directions only that far)."""
+    from NonlinearPnP import NonLinearPnPLoss, nonlinear_PnP
+    from scipy.spatial.transform import Rotation
+    g = golden("pnp.npz")
+
+    def cost(C, R, X, x):
+        p = np.hstack([Rotation.from_matrix(R).as_rotvec(), -R @ C])
+        r = NonLinearPnPLoss(p, X, x, K)
+        return 0.5 * r @ r
+    for name in ("clean50", "clean2000", "out500", "tiny3", "four"):
+        k = "nl_" + name
+        C, R = nonlinear_PnP(K, g[k + "_C0"], g[k + "_R0"], g[k + "_x"], g[k + "_X"])
+        assert np.abs(C - g[k + "_C"]).max() <= 1e-5 * max(1.0, np.abs(g[k + "_C"]).max()), name
+        assert np.abs(R - g[k + "_R"]).max() <= 1e-5, name
+        if len(g[k + "_X"]) >= 4:
+            cg, cr = cost(C, R, g[k + "_X"], g[k + "_x"]), cost(g[k + "_C"], g[k + "_R"], g[k + "_X"], g[k + "_x"])
+            assert abs(cg - cr) <= 1e-9 * cr + 1e-12, name
+    # the reference's except path: non-finite start -> inputs back, message printed
+    X, x, C0, R0 = _pnp_scene(50, 2)
+    C, R = nonlinear_PnP(K, np.array([np.nan, 0, 0]), R0, x, X)
+    assert np.isnan(C[0]) and np.array_equal(R, R0)
+    assert "Non-linear PnP optimization failed" in capsys.readouterr().out
+
+
+def test_pnp_large_vs_oracle(core):
+    """100k points, 30 % outliers: RANSAC winner / counts vs the oracle on
+    the well-defined hypotheses, then NonlinearPnP from the winner."""
+    X, x, Ct, Rt = _pnp_scene(100_000, 11, outlier_frac=0.3)
+    random.seed(11)
+    samples = core.sample_table(len(X), 4, 512)
+    best, bc, C, R, counts, branches = core.pnp_ransac(X, x, K, samples, 8.0, want_counts=True)
+    ob, oc, obr, oC, oR = O.pnp_ransac(X, x, K, samples, 8.0)
+    well = (branches == 0) & (obr == 0)
+    assert np.array_equal(counts[well], oc[well])
+    assert best == ob or branches[best] == 1 or obr[ob] == 1
+    Cn, Rn, info = core.nonlinear_pnp(X[:20000], x[:20000], K, C, R)
+    Co, Ro, info_o = O.nonlinear_pnp(X[:20000], x[:20000], K, C, R)
+    assert info > 0 and np.abs(Cn - Co).max() <= 1e-6 * max(1.0, np.abs(Co).max())
+
+
 # ---------------------------------------------------------------------- BA
 def test_project_and_residuals_match_oracle(core):
     from BundleAdjustment import bundle_adjustment_residuals, project_points
