@@ -114,6 +114,20 @@ int sfm_nonlinear_pnp(const double *X, const double *x, int64_t N, const double 
                       int device);
 
 /* ---------------------------------------------------------------------
+ * Matching files (Utils.py:8-64 get_data) -> COO observation store.
+ * sfm_matching_parse: reads data_path/matching1..(no_of_images-1).txt with
+ *   get_data's semantics (header skipped; primary x, y as floats; match
+ *   coordinates int()-truncated; last write per image wins) using
+ *   n_threads host threads (0 = up to 16); returns an opaque store with
+ *   n_features rows and n_obs observations (feature-major, image ascending).
+ * sfm_matching_read: copies the COO arrays (feature, image 0-based, x, y).
+ * ------------------------------------------------------------------- */
+int sfm_matching_parse(const char *data_path, int32_t no_of_images, int32_t n_threads, void **handle,
+                       int64_t *n_features, int64_t *n_obs);
+int sfm_matching_read(void *handle, int32_t *feature, int32_t *image, double *x, double *y);
+int sfm_matching_free(void *handle);
+
+/* ---------------------------------------------------------------------
  * LinearTriangulation (LinearTriangulation.py:3-92)
  * P1, P2: 3 x 4 projection matrices K[R | -RC]; x1, x2: N x 2; X: N x 3.
  * ------------------------------------------------------------------- */

@@ -113,10 +113,32 @@ def perform_bundle_adjustment(all_world_coords, filtered_world_coords, feature_x
     valid_point_indices = np.where(np.asarray(filtered_world_coords).flatten() == 1)[0]
     if len(valid_point_indices) == 0:  # :152-153
         return R_set, C_set, all_world_coords
+    obs = _observations(filtered_world_coords, feature_x, feature_y, filtered_feature_flags, len(R_set))
+    return _adjust(all_world_coords, obs, R_set, C_set, K, max_iterations, function_tolerance,
+                   parameter_tolerance, initial_lambda)
+
+
+def perform_bundle_adjustment_coo(all_world_coords, filtered_world_coords, store, R_set, C_set, K, *,
+                                  max_iterations=100, function_tolerance=1e-10, parameter_tolerance=1e-12,
+                                  initial_lambda=1e-4):
+    """perform_bundle_adjustment fed from a sfm_io.MatchStore (its ``flag``
+    plays filtered_feature_flags) instead of dense n_features x n_images
+    matrices; same observations, order, solver, prints and failure
+    behaviour."""
+    valid_point_indices = np.where(np.asarray(filtered_world_coords).flatten() == 1)[0]
+    if len(valid_point_indices) == 0:
+        return R_set, C_set, all_world_coords
+    obs = store.observations(filtered_world_coords, len(R_set))
+    return _adjust(all_world_coords, obs, R_set, C_set, K, max_iterations, function_tolerance,
+                   parameter_tolerance, initial_lambda)
+
+
+def _adjust(all_world_coords, obs, R_set, C_set, K, max_iterations, function_tolerance, parameter_tolerance,
+            initial_lambda):
+    """BundleAdjustment.py:156-242 from COO observations."""
+    valid_point_indices, camera_indices, point_indices, points_2d = obs
     n_cameras = len(R_set)
     n_points = len(valid_point_indices)
-    valid_point_indices, camera_indices, point_indices, points_2d = _observations(
-        filtered_world_coords, feature_x, feature_y, filtered_feature_flags, n_cameras)
     if len(camera_indices) == 0:  # :171-172
         return R_set, C_set, all_world_coords
     cams0 = np.zeros((n_cameras, 6))

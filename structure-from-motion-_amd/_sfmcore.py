@@ -67,6 +67,10 @@ SIGNATURES = [
     ("sfm_linear_pnp", _c, [_d, _d, _i, _d, _d, _d, _i32, _c]),
     ("sfm_pnp_ransac", _c, [_d, _d, _i, _d, _i32, _i, ctypes.c_double, _i32, _i32, _i64, _i64, _d, _d, _c]),
     ("sfm_nonlinear_pnp", _c, [_d, _d, _i, _d, _d, _d, ctypes.c_int32, _d, _d, _i32, _c]),
+    ("sfm_matching_parse", _c, [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p),
+                                _i64, _i64]),
+    ("sfm_matching_read", _c, [ctypes.c_void_p, _i32, _i32, _d, _d]),
+    ("sfm_matching_free", _c, [ctypes.c_void_p]),
     ("sfm_triangulate_dlt", _c, [_d, _d, _d, _d, _i, _d, _c]),
     ("sfm_triangulate_nonlinear", _c, [_d, _d, _d, _d, _d, _i, ctypes.c_int32, _d, _i32, _c]),
     ("sfm_project_points", _c, [_d, _d, _i, _d, _c]),
@@ -253,6 +257,23 @@ def nonlinear_pnp(X, x, K, C0, R0, max_nfev=100):
     _check(_lib.sfm_nonlinear_pnp(_p(X), _p(x), len(X), _p(K), _p(C0), _p(R0), int(max_nfev), _p(C), _p(R),
                                   _p(info, _i32), DEVICE))
     return C, R.reshape(3, 3), int(info[0])
+
+
+def parse_matching(data_path, no_of_images, n_threads=0):
+    """Native matching-file reader (host threads, no device needed).
+    Returns (n_features, feature, image, x, y) -- COO, feature-major."""
+    h = ctypes.c_void_p()
+    nf, no = np.zeros(1, dtype=np.int64), np.zeros(1, dtype=np.int64)
+    _check(_lib.sfm_matching_parse(os.fsencode(str(data_path)), int(no_of_images), int(n_threads), ctypes.byref(h),
+                                   _p(nf, _i64), _p(no, _i64)))
+    try:
+        n = int(no[0])
+        feat, img = np.empty(n, dtype=np.int32), np.empty(n, dtype=np.int32)
+        x, y = np.empty(n), np.empty(n)
+        _check(_lib.sfm_matching_read(h, _p(feat, _i32), _p(img, _i32), _p(x), _p(y)))
+    finally:
+        _lib.sfm_matching_free(h)
+    return int(nf[0]), feat, img, x, y
 
 
 def triangulate(P1, P2, x1, x2):

@@ -537,6 +537,26 @@ def test_ba_cfg4_full_size_properties(core):
     assert abs(0.5 * r @ r - r1["cost"]) <= 1e-8 * r1["cost"]
 
 
+def test_perform_bundle_adjustment_coo_equals_dense(core, capsys):
+    """The COO store path (no dense n_features x n_images matrices) gives the
+    dense path's observations, solve and outputs."""
+    from BundleAdjustment import perform_bundle_adjustment, perform_bundle_adjustment_coo
+    import sfm_io
+    p = syn.ba_problem(6, 400, 4, seed=8, dense=True)
+    ff = p["flags"]
+    f_idx, i_idx = np.nonzero(ff)
+    st = sfm_io.MatchStore(ff.shape[0], ff.shape[1], f_idx.astype(np.int32), i_idx.astype(np.int32),
+                           p["feature_x"][f_idx, i_idx], p["feature_y"][f_idx, i_idx])
+    st.flag[:] = 1
+    a = perform_bundle_adjustment(p["X0"], p["filtered_world_coords"], p["feature_x"], p["feature_y"], ff,
+                                  list(p["R0"]), list(p["C0"]), K, 2)
+    b = perform_bundle_adjustment_coo(p["X0"], p["filtered_world_coords"], st, list(p["R0"]), list(p["C0"]), K)
+    assert np.array_equal(a[2], b[2])
+    assert all(np.array_equal(u, v) for u, v in zip(a[0], b[0]))
+    out = capsys.readouterr().out
+    assert out.count("Bundle adjustment completed") == 2
+
+
 def test_ba_failure_contract(core, capsys):
     from BundleAdjustment import perform_bundle_adjustment
     p = syn.ba_problem(3, 30, 2, seed=2)  # 2*60 residuals < 18 + 90 params? no: 120 >= 108
