@@ -18,9 +18,9 @@
 //                    deterministic, no atomics.
 //   [RCCL all-reduce of the packed partial system across ranks]
 //   k_assemble       S += lambda*clamp(diag U), b = -g_c + sum Z q, padded.
-//   k_chol_panel / k_chol_update / k_chol_solve
-//                    blocked right-looking fp64 Cholesky of the reduced
-//                    camera system + triangular solves.
+//   k_chol_col       one launch per 16-wide tile column: trailing update
+//                    by the previous column + factor/TRSM of this one
+//                    (+ folded forward solve); k_chol_backsolve.
 //   k_camera_trial   R' = exp([dtheta]x) R, t' = t + dt; camera part of the
 //                    model decrease.
 //   k_backsub_trial  thread per point: dp = L L^T(-g_p - sum W^T dc),
@@ -482,16 +482,10 @@ __global__ void k_assemble(int32_t ns, int32_t nsp, const double *__restrict__ p
 }
 
 // --------------------------------------------------------------- Cholesky
-// Right-looking blocked Cholesky of the padded nsp x nsp reduced camera
-// system with the forward substitution folded in (b is carried as an extra
-// column).  Per tile column kt:
-//   k_chol_panel   one wave per tile row kt..nT-1: every wave factors the
-//                  diagonal tile in LDS (lane = row, column broadcast);
-//                  wave 0 also solves L_kk y_k = b_k, the others solve their
-//                  tile row L_rk = A_rk L_kk^-T and write it plus its mirror.
-//   k_chol_update  block 0 stores L_kk and updates b_r -= L_rk y_k; the
-//                  others apply the trailing update A_rc -= L_rk L_ck^T.
-// k_chol_backsolve then solves L^T x = y in one workgroup.
+// Blocked (NB = 16) right-looking fp64 Cholesky of the padded nsp x nsp
+// reduced camera system with the forward substitution folded in (b is
+// carried along); one k_chol_col launch per tile column (below), then
+// k_chol_backsolve solves L^T x = y in one workgroup.
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -506,125 +500,176 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
     return __longlong_as_double(((unsigned long long)hi << 32) | lo);
 }
 
-__global__ void __launch_bounds__(64) k_chol_panel(double *__restrict__ A, int32_t nsp, int kt,
-                                                   double *__restrict__ D, double *__restrict__ bvec,
-                                                   int *__restrict__ bad) {
-    __shared__ double Ls[NB][NB + 1];
-    const int lane = threadIdx.x;
-    const int k0 = kt * NB;
-    const int li = lane < NB ? lane : NB - 1;
-    double r[NB];  // lane i: row i of the diagonal tile -> row i of L_kk
-#pragma unroll
-    for (int j = 0; j < NB; ++j) r[j] = A[(int64_t)(k0 + li) * nsp + k0 + j];
-    // updates hit every lane's whole row: above the diagonal they only touch
-    // the unused upper triangle, which saves the predication
-    double dinv[NB];  // 1 / L_jj, kept for the solves below
+// ---- merged step kernel: one launch per tile column s (nT launches).
+// Launch s applies column s-1's trailing update to every lower tile (r, c),
+// c >= s, and factors column s in the same launch:
+//   tile (r, c), c > s : A_rc -= L_r,s-1 L_c,s-1^T
+//   tile (r, s), r > s : C_rs = A_rs - L_r,s-1 L_s,s-1^T, C_ss likewise
+//                        (recomputed identically by every column block),
+//                        wave 0 factors C_ss, then L_rs = C_rs L_ss^-T,
+//                        written with its mirror;
+//   tile (s, s)        : C_ss, factor, y_s = L_ss^-1 (b_s - L_s,s-1 y_s-1),
+//                        L_ss -> D[s & 1] (read-only copy of A_ss is still
+//                        in use by the other column blocks);
+//   block 0 (s >= 1)   : D[(s-1) & 1] -> A's diagonal tile s-1 and
+//                        b_i -= L_i,s-1 y_s-1 for rows past column s.
+__device__ __forceinline__ void chol_factor16(double (&r)[NB], double (&dinv)[NB], int lane, int *bad) {
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
         const double d = readlane_f64(r[k], k);
         if (lane == 0 && !(d > 0.0)) *bad = 1;
-        const double lkk = sqrt(d);
-        dinv[k] = 1.0 / lkk;
-        r[k] = (lane == k) ? lkk : r[k] * dinv[k];
+        // 1/sqrt(d): v_rsq_f64 then two Newton steps (~1 ulp), off the
+        // long IEEE sqrt + divide sequences of the serial chain
+        double g = __builtin_amdgcn_rsq(d);
+        g = g * (1.5 - 0.5 * d * g * g);
+        g = g * (1.5 - 0.5 * d * g * g);
+        dinv[k] = g;
+        r[k] = (lane == k) ? d * g : r[k] * g;
 #pragma unroll
         for (int j = k + 1; j < NB; ++j) r[j] -= r[k] * readlane_f64(r[k], j);
     }
-    if (blockIdx.x == 0) {
-        // forward substitution of this tile: L_kk y = b_k (b_k already updated)
-        double y = bvec[k0 + li];
+}
+
+__global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_t nsp, int s,
+                                                  double *__restrict__ D, double *__restrict__ bvec,
+                                                  int *__restrict__ bad) {
+    __shared__ double Lr[NB][NB + 1], Lc[NB][NB + 1], Ct[NB][NB + 1], Cd[NB][NB + 1];
+    __shared__ double yk[NB];
+    const int t = threadIdx.x;
+    const int nT = nsp / NB;
+    const bool upd = s >= 1;
+    const int kp = (s - 1) * NB;  // previous column's first index
+    int blk = blockIdx.x;
+    if (upd && blk == 0) {
+        const double *Dp = D + ((s - 1) & 1) * NB * NB;
+        for (int e = t; e < NB * NB; e += blockDim.x) {
+            const int i = e / NB, j = e % NB;
+            A[(int64_t)(kp + i) * nsp + kp + j] = i >= j ? Dp[i * NB + j] : Dp[j * NB + i];
+        }
+        if (t < NB) yk[t] = bvec[kp + t];
+        __syncthreads();
+        for (int i = (s + 1) * NB + t; i < nsp; i += blockDim.x) {
+            double acc = 0;
+#pragma unroll 8
+            for (int m = 0; m < NB; ++m) acc += A[(int64_t)(kp + m) * nsp + i] * yk[m];  // L[i][kp+m] (mirror)
+            bvec[i] -= acc;
+        }
+        return;
+    }
+    if (upd) --blk;
+    int rr = 0;
+    while (blk > rr) { blk -= rr + 1; ++rr; }
+    const int r = s + rr, c = s + blk;  // lower tile (r, c), r >= c >= s
+    const int r0 = r * NB, c0 = c * NB, s0 = s * NB;
+    const bool colblk = c == s, need_d = colblk && r > s;
+    // every global load of the block in one round: L_r,s-1, L_c,s-1, A_rc, A_ss
+    {
+        const int i = t / NB, j = t % NB;
+        const double lr = upd ? A[(int64_t)(r0 + i) * nsp + kp + j] : 0.0;
+        const double lc = upd ? A[(int64_t)(c0 + i) * nsp + kp + j] : 0.0;
+        const double arc = A[(int64_t)(r0 + i) * nsp + c0 + j];
+        const double ass = need_d ? A[(int64_t)(s0 + i) * nsp + s0 + j] : 0.0;
+        Lr[i][j] = lr;
+        Lc[i][j] = lc;
+        __syncthreads();
+        double v = arc, w = ass;
+        if (upd) {
+            double a1 = 0, a2 = 0;
+#pragma unroll 8
+            for (int m = 0; m < NB; ++m) {
+                a1 += Lr[i][m] * Lc[j][m];
+                a2 += Lc[i][m] * Lc[j][m];
+            }
+            v -= a1;
+            w -= a2;
+        }
+        if (!colblk) {  // trailing tile: done
+            A[(int64_t)(r0 + i) * nsp + c0 + j] = v;
+            return;
+        }
+        Ct[i][j] = v;
+        if (need_d) Cd[i][j] = w;
+    }
+    // column s: C_ss (Cd, or Ct in the diagonal block) is bitwise the same in
+    // every column block -- same inputs, same operation order
+    __syncthreads();
+    if (t >= 64) return;
+    const int lane = t;
+    const int li = lane < NB ? lane : NB - 1;
+    double (*Cdd)[NB + 1] = (r > s) ? Cd : Ct;
+    double rw[NB], dinv[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) rw[j] = Cdd[li][j];
+    chol_factor16(rw, dinv, lane, bad);
+    if (r == s) {
+        double y = bvec[s0 + li];
+        if (upd) {
+            double acc = 0;
+#pragma unroll
+            for (int m = 0; m < NB; ++m) acc += Lc[li][m] * bvec[kp + m];
+            y -= acc;
+        }
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
             const double yj = readlane_f64(y, j) * dinv[j];
             if (lane == j) y = yj;
-            if (lane > j) y -= r[j] * yj;
+            if (lane > j) y -= rw[j] * yj;
         }
         if (lane < NB) {
-            bvec[k0 + lane] = y;
+            bvec[s0 + lane] = y;
+            double *Dn = D + (s & 1) * NB * NB;
 #pragma unroll
-            for (int j = 0; j < NB; ++j) D[lane * NB + j] = j <= lane ? r[j] : 0.0;
+            for (int j = 0; j < NB; ++j) Dn[lane * NB + j] = j <= lane ? rw[j] : 0.0;
         }
         return;
     }
-    // tile row r: X L_kk^T = A_rk, lane = row of X; L_jm = lane j's r[m]
-    const int r0 = (kt + blockIdx.x) * NB;
+    // L_rs = C_rs L_ss^-T, one tile row per lane (L_jm = lane j's rw[m])
     double x[NB];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) x[j] = A[(int64_t)(r0 + li) * nsp + k0 + j];
+    for (int j = 0; j < NB; ++j) x[j] = Ct[li][j];
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-        double v0 = x[j], v1 = 0.0, v2 = 0.0, v3 = 0.0;  // 4 chains
+        double v0 = x[j], v1 = 0.0, v2 = 0.0, v3 = 0.0;
 #pragma unroll
         for (int m = 0; m < j; ++m) {
-            const double t = x[m] * readlane_f64(r[m], j);
-            if ((m & 3) == 0) v0 -= t;
-            else if ((m & 3) == 1) v1 -= t;
-            else if ((m & 3) == 2) v2 -= t;
-            else v3 -= t;
+            const double tt = x[m] * readlane_f64(rw[m], j);
+            if ((m & 3) == 0) v0 -= tt;
+            else if ((m & 3) == 1) v1 -= tt;
+            else if ((m & 3) == 2) v2 -= tt;
+            else v3 -= tt;
         }
         x[j] = ((v0 + v1) + (v2 + v3)) * dinv[j];
     }
     wave_sync_lds();
     if (lane < NB)
 #pragma unroll
-        for (int j = 0; j < NB; ++j) Ls[lane][j] = x[j];
+        for (int j = 0; j < NB; ++j) Lr[lane][j] = x[j];
     wave_sync_lds();
     for (int e = lane; e < NB * NB; e += 64)
-        A[(int64_t)(r0 + e / NB) * nsp + k0 + e % NB] = Ls[e / NB][e % NB];
+        A[(int64_t)(r0 + e / NB) * nsp + s0 + e % NB] = Lr[e / NB][e % NB];
     for (int e = lane; e < NB * NB; e += 64)  // mirror into the upper triangle
-        A[(int64_t)(k0 + e / NB) * nsp + r0 + e % NB] = Ls[e % NB][e / NB];
-}
-
-__global__ void __launch_bounds__(256) k_chol_update(double *__restrict__ A, int32_t nsp, int kt,
-                                                     const double *__restrict__ D, double *__restrict__ bvec) {
-    __shared__ double Lr[NB][NB + 1];
-    __shared__ double Lc[NB][NB + 1];
-    const int k0 = kt * NB;
-    if (blockIdx.x == 0) {
-        for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-            const int i = e / NB, j = e % NB;
-            A[(int64_t)(k0 + i) * nsp + k0 + j] = i >= j ? D[i * NB + j] : D[j * NB + i];
-        }
-        __shared__ double yk[NB];
-        if (threadIdx.x < NB) yk[threadIdx.x] = bvec[k0 + threadIdx.x];
-        __syncthreads();
-        for (int i = k0 + NB + threadIdx.x; i < nsp; i += blockDim.x) {
-            double s = 0;
-#pragma unroll 8
-            for (int m = 0; m < NB; ++m) s += A[(int64_t)(k0 + m) * nsp + i] * yk[m];  // L[i][k0+m] (mirror)
-            bvec[i] -= s;
-        }
-        return;
-    }
-    int t = blockIdx.x - 1, r = 0;
-    while (t > r) { t -= r + 1; ++r; }
-    const int c = t;
-    const int rr = (kt + 1 + r) * NB, cc = (kt + 1 + c) * NB;
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-        const int i = e / NB, j = e % NB;
-        Lr[i][j] = A[(int64_t)(rr + i) * nsp + k0 + j];
-        Lc[i][j] = A[(int64_t)(cc + i) * nsp + k0 + j];
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-        const int i = e / NB, j = e % NB;
-        double s = 0;
-#pragma unroll 8
-        for (int m = 0; m < NB; ++m) s += Lr[i][m] * Lc[j][m];
-        A[(int64_t)(rr + i) * nsp + cc + j] -= s;
-    }
+        A[(int64_t)(s0 + e / NB) * nsp + r0 + e % NB] = Lr[e % NB][e / NB];
 }
 
 // L^T x = y (y already in xg from the folded forward substitution).
 constexpr int SOLVE_THREADS = 256;
 constexpr int SOLVE_MAX = 4096;
 
-__global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(const double *__restrict__ A, int32_t nsp,
-                                                                  double *__restrict__ xg) {
+__global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(double *__restrict__ A, int32_t nsp,
+                                                                  double *__restrict__ xg,
+                                                                  const double *__restrict__ Dlast) {
     __shared__ double x[SOLVE_MAX];
     __shared__ double yt[NB];
     const int t = threadIdx.x, lane = t & 63;
     const int nT = nsp / NB;
     for (int i = t; i < nsp; i += SOLVE_THREADS) x[i] = xg[i];
+    if (Dlast) {  // the last diagonal factor is still in the step kernel's scratch
+        const int k0 = nsp - NB;
+        for (int e = t; e < NB * NB; e += SOLVE_THREADS) {
+            const int i = e / NB, j = e % NB;
+            A[(int64_t)(k0 + i) * nsp + k0 + j] = i >= j ? Dlast[i * NB + j] : Dlast[j * NB + i];
+        }
+    }
     __syncthreads();
     for (int kt = nT - 1; kt >= 0; --kt) {
         const int k0 = kt * NB;
@@ -652,6 +697,21 @@ __global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(const double *
         __syncthreads();
     }
     for (int i = t; i < nsp; i += SOLVE_THREADS) xg[i] = x[i];
+}
+
+// Factor + forward solve (nT launches of k_chol_col) and backward solve of
+// the padded reduced camera system; A, b on the device, D = 2 NB^2 scratch.
+static int launch_cholesky(double *A, int32_t nsp, double *b, double *D, int *bad, hipStream_t s) {
+    const int nT = nsp / NB;
+    for (int st = 0; st < nT; ++st) {
+        const int T = nT - st;
+        hipLaunchKernelGGL(k_chol_col, dim3(T * (T + 1) / 2 + (st >= 1 ? 1 : 0)), dim3(256), 0, s, A, nsp, st, D, b,
+                           bad);
+        SFM_HIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(SOLVE_THREADS), 0, s, A, nsp, b, D + ((nT - 1) & 1) * NB * NB);
+    SFM_HIP(hipGetLastError());
+    return 0;
 }
 
 // one workgroup: trial cameras + camera part of model decrease / norms.
@@ -1049,7 +1109,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = p->alloc(p->d_J, (int64_t)JS * no)) || (rc = p->alloc(p->d_Vg, 9 * np_)) || (rc = p->alloc(p->d_Lq, 9 * np_)) ||
         (rc = p->alloc(p->d_Z, (int64_t)ZS * no)) || (rc = p->alloc(p->d_payload, p->payload_len + 8)) ||
         (rc = p->alloc(p->d_A, (int64_t)p->nsp * p->nsp)) || (rc = p->alloc(p->d_b, p->nsp)) ||
-        (rc = p->alloc(p->d_D, NB * NB)) ||
+        (rc = p->alloc(p->d_D, 2 * NB * NB)) ||
         (rc = p->alloc(p->d_partial, 4 * (int64_t)p->pt_blocks)) || (rc = p->alloc(p->d_scal, 16)) ||
         (rc = p->alloc(p->d_bad, 4)))
         return rc;
@@ -1183,16 +1243,7 @@ static int run_step(sfm_ba_problem *p, double lambda, bool timed) {
     hipLaunchKernelGGL(k_assemble, dim3(ceil_div(nA, 256)), dim3(256), 0, s, p->ns, p->nsp, p->d_payload, lambda,
                        p->d_A, p->d_b);
     SFM_HIP(hipGetLastError());
-    for (int kt = 0; kt < p->nT; ++kt) {
-        hipLaunchKernelGGL(k_chol_panel, dim3(p->nT - kt), dim3(64), 0, s, p->d_A, p->nsp, kt, p->d_D, p->d_b,
-                           p->d_bad);
-        SFM_HIP(hipGetLastError());
-        const int T = p->nT - kt - 1;
-        hipLaunchKernelGGL(k_chol_update, dim3(T * (T + 1) / 2 + 1), dim3(256), 0, s, p->d_A, p->nsp, kt, p->d_D,
-                           p->d_b);
-        SFM_HIP(hipGetLastError());
-    }
-    hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(SOLVE_THREADS), 0, s, p->d_A, p->nsp, p->d_b);
+    if ((rc = launch_cholesky(p->d_A, p->nsp, p->d_b, p->d_D, p->d_bad, s))) return rc;
     SFM_HIP(hipGetLastError());
     if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_SOLVE + 1], s));
     if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_TRIAL], s));

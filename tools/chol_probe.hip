@@ -45,7 +45,7 @@ static int run(int ns, int reps) {
     double *dA, *dA0, *db, *db0;
     int *dbad;
     double *dD;
-    hipMalloc(&dD, NB * NB * 8);
+    hipMalloc(&dD, 2 * NB * NB * 8);
     hipMalloc(&dA, S.size() * 8); hipMalloc(&dA0, S.size() * 8);
     hipMalloc(&db, nsp * 8); hipMalloc(&db0, nsp * 8);
     hipMalloc(&dbad, 4); hipMemset(dbad, 0, 4);
@@ -58,14 +58,7 @@ static int run(int ns, int reps) {
         hipMemcpy(dA, dA0, S.size() * 8, hipMemcpyDeviceToDevice);
         hipMemcpy(db, db0, nsp * 8, hipMemcpyDeviceToDevice);
         hipEventRecord(e0, 0);
-        {
-            for (int kt = 0; kt < nT; ++kt) {
-                hipLaunchKernelGGL(k_chol_panel, dim3(nT - kt), dim3(64), 0, 0, dA, nsp, kt, dD, db, dbad);
-                const int T = nT - kt - 1;
-                hipLaunchKernelGGL(k_chol_update, dim3(T * (T + 1) / 2 + 1), dim3(256), 0, 0, dA, nsp, kt, dD, db);
-            }
-            hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(SOLVE_THREADS), 0, 0, dA, nsp, db);
-        }
+        launch_cholesky(dA, nsp, db, dD, dbad, 0);
         hipEventRecord(e1, 0);
         hipEventSynchronize(e1);
         float ms;
