@@ -652,7 +652,7 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
 }
 
 // L^T x = y (y already in xg from the folded forward substitution).
-constexpr int SOLVE_THREADS = 256;
+constexpr int SOLVE_THREADS = 512;
 constexpr int SOLVE_MAX = 4096;
 
 __global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(double *__restrict__ A, int32_t nsp,
@@ -673,6 +673,12 @@ __global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(double *__rest
     __syncthreads();
     for (int kt = nT - 1; kt >= 0; --kt) {
         const int k0 = kt * NB;
+        // L rows of this step for this thread's first column, issued before the
+        // diagonal solve they do not depend on (one load round per step)
+        double lpre[NB];
+        const bool pre = t < k0;
+#pragma unroll
+        for (int m = 0; m < NB; ++m) lpre[m] = pre ? A[(int64_t)(k0 + m) * nsp + t] : 0.0;
         if (t < 64) {
             const int li = lane < NB ? lane : NB - 1;
             double cl[NB];  // cl[m] = L[k0+m][k0+li]
@@ -688,7 +694,13 @@ __global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(double *__rest
             if (lane < NB) { x[k0 + lane] = v; yt[lane] = v; }
         }
         __syncthreads();
-        for (int i = t; i < k0; i += SOLVE_THREADS) {
+        if (pre) {
+            double s = 0;
+#pragma unroll
+            for (int m = 0; m < NB; ++m) s += lpre[m] * yt[m];  // L[k0+m][t]
+            x[t] -= s;
+        }
+        for (int i = t + SOLVE_THREADS; i < k0; i += SOLVE_THREADS) {
             double s = 0;
 #pragma unroll 8
             for (int m = 0; m < NB; ++m) s += A[(int64_t)(k0 + m) * nsp + i] * yt[m];  // L[k0+m][i]
