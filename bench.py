@@ -90,6 +90,81 @@ def cpu_baseline_ransac(x1, x2, samples):
     return len(samples) / dt, dt
 
 
+K = syn.K_REF
+
+
+def next_rows(core, local_rank, cpu):
+    """§8(f) rows, rank 0: GPU throughput of each (kernel-only and end to
+    end through the C-ABI), and -- in the cpu_baseline leg only -- the C
+    oracle on a bounded sample of the same workload."""
+    if cpu:
+        import oracle as O  # test infrastructure: the CPU restatement, timed as the baseline
+    out = {}
+    x1, x2, _, m = syn.two_view(n=1_000_000, seed=6, outlier_frac=0.2)
+    P1 = K @ np.hstack([np.eye(3), np.zeros((3, 1))])
+    P2 = K @ np.hstack([m["R2"], (-m["R2"] @ m["C2"]).reshape(3, 1)])
+    X0 = core.triangulate(P1, P2, x1, x2)
+    core.triangulate_nonlinear(P1, P2, x1[:1000], x2[:1000], X0[:1000])
+    t = time.perf_counter()
+    core.triangulate_nonlinear(P1, P2, x1, x2, X0)
+    te = time.perf_counter() - t
+    tk = core.last_timings()[1] * 1e-3
+    r = {"workload": "1M two-view points, 20% outliers, DLT start, max_nfev=50",
+         "points_per_s_kernel": round(len(x1) / tk, 1), "points_per_s_end_to_end": round(len(x1) / te, 1)}
+    if cpu:
+        t = time.perf_counter()
+        O.nltri(K, np.zeros(3), np.eye(3), m["C2"], m["R2"], x1[:200_000], x2[:200_000], X0[:200_000])
+        r["cpu_oracle_points_per_s"] = round(200_000 / (time.perf_counter() - t), 1)
+        r["cpu_sample"] = "C oracle lmdif (oracle/sfm_oracle_lm.c), 200k points, 1 thread"
+    out["nonlinear_triangulation"] = r
+    # homography RANSAC, cfg2 correspondences, 16384 hypotheses, thr 30
+    h1, h2, _, _ = syn.two_view(n=5000, seed=0)
+    random.seed(0)
+    hs = core.sample_table(5000, 4, 16384)
+    core.ransac_h4(h1, h2, hs, 30.0)
+    t = time.perf_counter()
+    core.ransac_h4(h1, h2, hs, 30.0)
+    te = time.perf_counter() - t
+    tk = core.last_timings()[1] * 1e-3
+    r = {"workload": "cfg2 5000 corr, 16384 4-point hypotheses, thr 30",
+         "hyps_per_s_kernels": round(16384 / tk, 1), "hyps_per_s_end_to_end": round(16384 / te, 1)}
+    if cpu:
+        t = time.perf_counter()
+        O.ransac_h(h1, h2, hs[:1024], 30.0)
+        r["cpu_oracle_hyps_per_s"] = round(1024 / (time.perf_counter() - t), 1)
+    out["homography_ransac"] = r
+    # PnP RANSAC + NonlinearPnP on 5000 world points (30 % outliers)
+    rng = np.random.default_rng(12)
+    n = 5000
+    Xw = np.column_stack([rng.uniform(-3, 3, n), rng.uniform(-2, 2, n), rng.uniform(5, 12, n)])
+    u = (K @ (m["R2"] @ (Xw - m["C2"]).T)).T
+    xw = u[:, :2] / u[:, 2:3] + rng.normal(0, 0.5, (n, 2))
+    o = rng.choice(n, n * 3 // 10, replace=False)
+    xw[o] = rng.uniform(0, 1000, (len(o), 2))
+    random.seed(1)
+    ps = core.sample_table(n, 4, 16384)
+    core.pnp_ransac(Xw, xw, K, ps, 8.0)
+    t = time.perf_counter()
+    _, _, C, R, _, _ = core.pnp_ransac(Xw, xw, K, ps, 8.0)
+    te = time.perf_counter() - t
+    tk = core.last_timings()[1] * 1e-3
+    t = time.perf_counter()
+    core.nonlinear_pnp(Xw, xw, K, C, R)
+    tn = time.perf_counter() - t
+    r = {"workload": "5000 points, 30% outliers, 16384 4-point hypotheses, thr 8; NonlinearPnP max_nfev=100",
+         "hyps_per_s_kernels": round(16384 / tk, 1), "hyps_per_s_end_to_end": round(16384 / te, 1),
+         "nonlinear_pnp_ms": round(tn * 1e3, 3)}
+    if cpu:
+        t = time.perf_counter()
+        O.pnp_ransac(Xw, xw, K, ps[:1024], 8.0)
+        r["cpu_oracle_hyps_per_s"] = round(1024 / (time.perf_counter() - t), 1)
+        t = time.perf_counter()
+        O.nonlinear_pnp(Xw, xw, K, C, R)
+        r["cpu_oracle_nonlinear_pnp_ms"] = round((time.perf_counter() - t) * 1e3, 3)
+    out["pnp"] = r
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -99,6 +174,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ransac-hyps", type=int, default=16384)
     ap.add_argument("--force-comm", action="store_true", help="use the RCCL communicator even with one rank")
+    ap.add_argument("--no-next-rows", action="store_true", help="skip the SURVEY §8(f) row measurements")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -228,8 +304,12 @@ def main():
                    "hyps_per_s_kernels": round(args.ransac_hyps / (k_all * 1e-3), 1),
                    "score_kernel_ms": round(float(k_score), 4), "best_iter": int(best), "inliers": int(mask.sum())},
     }
-    if world == 1 and not args.no_cpu_baseline:
+    cpu_leg = world == 1 and not args.no_cpu_baseline
+    if cpu_leg:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
+    if not args.no_next_rows:
+        out["next_rows"] = next_rows(core, local_rank, cpu_leg)
+    if cpu_leg:
         v, crep, cdt = cpu_baseline_ba(prob, K)
         hs = samples[:1024]
         rv, rdt = cpu_baseline_ransac(x1, x2, hs)
