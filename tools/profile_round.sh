@@ -10,6 +10,6 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kernel_trace -o run --output-format csv -- python bench.py --no-cpu-baseline > $OUT/prof.log 2>&1
 for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
   tag=$(echo $C | tr ' ' '_')
-  timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/$tag -o run -- python bench.py --no-cpu-baseline --steps 5 --warmup 1 > $OUT/pmc_$tag.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/$tag -o run -- python bench.py --no-cpu-baseline --no-next-rows --steps 5 --warmup 1 > $OUT/pmc_$tag.log 2>&1
 done
 echo DONE
