@@ -36,6 +36,7 @@
 #include <mutex>
 #include <thread>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <numeric>
@@ -67,6 +68,16 @@ namespace sfm {
 
 constexpr int NB = 16;            // Cholesky tile
 constexpr int PT_THREADS = 128;   // per-point kernels
+constexpr int PT_GROUP = 8;       // max lanes per point in k_linearize / k_backsub_trial
+
+// sum over an aligned group of G lanes (fixed butterfly order; every lane of
+// the group ends with the same total)
+template <int G>
+__device__ __forceinline__ double group_sum(double v) {
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
 
 __device__ __forceinline__ double clampd(double x) { return fmin(fmax(x, 1e-6), 1e32); }
 
@@ -163,21 +174,24 @@ struct Kmat {
     double k[9];
 };
 
+template <int G>
 __global__ void __launch_bounds__(PT_THREADS) k_linearize(int64_t np_, const int32_t *__restrict__ pstart,
                                                           const int32_t *__restrict__ cam,
                                                           const double2 *__restrict__ obs, Kmat Km,
                                                           const double *__restrict__ Rt,
                                                           const double *__restrict__ X, double *__restrict__ J,
                                                           double *__restrict__ Vg, double *__restrict__ partial) {
-    const int64_t p = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x;
+    const int64_t gt = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x;
+    const int64_t p = gt / G;  // G lanes per point, striding over its observations
+    const int sub = (int)(gt % G);
     double K[9];
 #pragma unroll
     for (int i = 0; i < 9; ++i) K[i] = Km.k[i];
     double acc[1] = {0.0};
+    double V[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
     if (p < np_) {
         double x[3] = {X[3 * p], X[3 * p + 1], X[3 * p + 2]};
-        double V[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
-        for (int32_t o = pstart[p]; o < pstart[p + 1]; ++o) {
+        for (int32_t o = pstart[p] + sub; o < pstart[p + 1]; o += G) {
             const double *Rt_c = Rt + 12 * cam[o];
             double r[2], A[2][3], q[3];
             obs_model(Rt_c, x, K, obs[o], r, A, q);
@@ -201,6 +215,12 @@ __global__ void __launch_bounds__(PT_THREADS) k_linearize(int64_t np_, const int
 #pragma unroll
             for (int i = 0; i < 3; ++i) g[i] += Jp[0][i] * r[0] + Jp[1][i] * r[1];
         }
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) V[i] = group_sum<G>(V[i]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) g[i] = group_sum<G>(g[i]);
+    if (p < np_ && sub == 0) {
         double *vg = Vg + 9 * p;
 #pragma unroll
         for (int i = 0; i < 6; ++i) vg[i] = V[i];
@@ -212,14 +232,23 @@ __global__ void __launch_bounds__(PT_THREADS) k_linearize(int64_t np_, const int
 
 // Lq layout per point (9 doubles): L00 L01 L02 L11 L12 L22 | q0 q1 q2
 // Z_o = W_o L = E_o G_o with G_o = A^T (A R L): the Schur record is (p, G).
-__global__ void __launch_bounds__(PT_THREADS) k_point_prep(int64_t np_, const int32_t *__restrict__ pstart,
-                                                           const int32_t *__restrict__ cam,
-                                                           const double *__restrict__ Rt,
-                                                           const double *__restrict__ J,
-                                                           const double *__restrict__ Vg, double lambda,
-                                                           double *__restrict__ Lq, double *__restrict__ Z) {
-    const int64_t p = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x;
-    if (p >= np_) return;
+// Thread per OBSERVATION (a thread per point leaves ~1.5 waves per SIMD at
+// cfg4 walking k observations serially): each thread rebuilds its point's
+// 3x3 factor from V (72 B, shared in cache by the point's k threads -- the
+// same arithmetic, so bitwise the same L), the point's first observation
+// also stores (L, q).
+constexpr int OBS_THREADS = 256;
+
+__global__ void __launch_bounds__(OBS_THREADS) k_point_prep(int64_t no, const int32_t *__restrict__ pt,
+                                                            const int32_t *__restrict__ pstart,
+                                                            const int32_t *__restrict__ cam,
+                                                            const double *__restrict__ Rt,
+                                                            const double *__restrict__ J,
+                                                            const double *__restrict__ Vg, double lambda,
+                                                            double *__restrict__ Lq, double *__restrict__ Z) {
+    const int64_t o = (int64_t)blockIdx.x * OBS_THREADS + threadIdx.x;
+    if (o >= no) return;
+    const int64_t p = pt[o];
     const double *vg = Vg + 9 * p;
     const double v00 = vg[0] + lambda * clampd(vg[0]), v01 = vg[1], v02 = vg[2];
     const double v11 = vg[3] + lambda * clampd(vg[3]), v12 = vg[4];
@@ -233,32 +262,32 @@ __global__ void __launch_bounds__(PT_THREADS) k_point_prep(int64_t np_, const in
     const double i20 = -(c20 * i00 + c21 * i10) * i22;
     // L = Cinv^T (upper): Vd^-1 = L L^T
     const double L[3][3] = {{i00, i10, i20}, {0.0, i11, i21}, {0.0, 0.0, i22}};
-    const double g0 = vg[6], g1 = vg[7], g2 = vg[8];
-    double *lq = Lq + 9 * p;
-    lq[0] = L[0][0]; lq[1] = L[0][1]; lq[2] = L[0][2]; lq[3] = L[1][1]; lq[4] = L[1][2]; lq[5] = L[2][2];
-    lq[6] = L[0][0] * g0;
-    lq[7] = L[0][1] * g0 + L[1][1] * g1;
-    lq[8] = L[0][2] * g0 + L[1][2] * g1 + L[2][2] * g2;
-    for (int32_t o = pstart[p]; o < pstart[p + 1]; ++o) {
-        double r[2], A[2][3], q[3];
-        load_j(J + (int64_t)JS * o, r, A, q);
-        const double *R = Rt + 12 * cam[o];
-        double T[2][3];  // (A R) L
-#pragma unroll
-        for (int a = 0; a < 2; ++a) {
-            double ar[3];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) ar[c] = A[a][0] * R[c] + A[a][1] * R[3 + c] + A[a][2] * R[6 + c];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) T[a][c] = ar[0] * L[0][c] + ar[1] * L[1][c] + ar[2] * L[2][c];
-        }
-        double *z = Z + (int64_t)ZS * o;
-        z[0] = q[0]; z[1] = q[1]; z[2] = q[2];
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int c = 0; c < 3; ++c) z[3 + 3 * i + c] = A[0][i] * T[0][c] + A[1][i] * T[1][c];
+    if (o == pstart[p]) {
+        const double g0 = vg[6], g1 = vg[7], g2 = vg[8];
+        double *lq = Lq + 9 * p;
+        lq[0] = L[0][0]; lq[1] = L[0][1]; lq[2] = L[0][2]; lq[3] = L[1][1]; lq[4] = L[1][2]; lq[5] = L[2][2];
+        lq[6] = L[0][0] * g0;
+        lq[7] = L[0][1] * g0 + L[1][1] * g1;
+        lq[8] = L[0][2] * g0 + L[1][2] * g1 + L[2][2] * g2;
     }
+    double r[2], A[2][3], q[3];
+    load_j(J + (int64_t)JS * o, r, A, q);
+    const double *R = Rt + 12 * cam[o];
+    double T[2][3];  // (A R) L
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        double ar[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) ar[c] = A[a][0] * R[c] + A[a][1] * R[3 + c] + A[a][2] * R[6 + c];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) T[a][c] = ar[0] * L[0][c] + ar[1] * L[1][c] + ar[2] * L[2][c];
+    }
+    double *z = Z + (int64_t)ZS * o;
+    z[0] = q[0]; z[1] = q[1]; z[2] = q[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) z[3 + 3 * i + c] = A[0][i] * T[0][c] + A[1][i] * T[1][c];
 }
 
 // Payload layout (doubles): S[ns*ns] | diagU[ns] | gc[ns] | bZ[ns] | cost
@@ -711,6 +740,14 @@ __global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(double *__rest
     for (int i = t; i < nsp; i += SOLVE_THREADS) xg[i] = x[i];
 }
 
+// Lanes per point for the grouped per-point kernels (1, 2, 4 or 8; an
+// environment override is read once, for tuning).
+static int lanes_per_point(const char *env, int dflt) {
+    const char *v = std::getenv(env);
+    const int g = v ? std::atoi(v) : dflt;
+    return (g == 1 || g == 2 || g == 4 || g == 8) ? g : dflt;
+}
+
 // Factor + forward solve (nT launches of k_chol_col) and backward solve of
 // the padded reduced camera system; A, b on the device, D = 2 NB^2 scratch.
 static int launch_cholesky(double *A, int32_t nsp, double *b, double *D, int *bad, hipStream_t s) {
@@ -763,6 +800,7 @@ __global__ void __launch_bounds__(256) k_camera_trial(int32_t nc, const double *
 }
 
 // partial[block][4] = {trial cost, model_p, |dp|^2, |X|^2}
+template <int G>
 __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const int32_t *__restrict__ pstart,
                                                               const int32_t *__restrict__ cam,
                                                               const double2 *__restrict__ obs, Kmat Km,
@@ -774,34 +812,40 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
                                                               const double *__restrict__ Rt_new,
                                                               const double *__restrict__ X,
                                                               double *__restrict__ X_new, double *__restrict__ partial) {
-    const int64_t p = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x;
+    const int64_t gt = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x;
+    const int64_t p = gt / G;  // G lanes per point, striding over its observations
+    const int sub = (int)(gt % G);
     double K[9];
 #pragma unroll
     for (int i = 0; i < 9; ++i) K[i] = Km.k[i];
     double acc[4] = {0, 0, 0, 0};
-    if (p < np_) {
+    const bool live = p < np_;
+    const int32_t o0 = live ? pstart[p] : 0, o1 = live ? pstart[p + 1] : 0;
+    // W^T dc = Jp^T (Jc dc) = R^T A^T (A (dtheta x p + dt)), summed over the point's observations
+    double wt[3] = {0, 0, 0};
+    for (int32_t o = o0 + sub; o < o1; o += G) {
+        double rr[2], A[2][3], q[3];
+        load_j(J + (int64_t)JS * o, rr, A, q);
+        const double *d = dc + 6 * cam[o];
+        const double *R = Rt + 12 * cam[o];
+        const double v0 = d[1] * q[2] - d[2] * q[1] + d[3];
+        const double v1 = d[2] * q[0] - d[0] * q[2] + d[4];
+        const double v2 = d[0] * q[1] - d[1] * q[0] + d[5];
+        const double s0 = A[0][0] * v0 + A[0][1] * v1 + A[0][2] * v2;
+        const double s1 = A[1][0] * v0 + A[1][1] * v1 + A[1][2] * v2;
+        double w[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) w[i] = A[0][i] * s0 + A[1][i] * s1;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) wt[i] += R[i] * w[0] + R[3 + i] * w[1] + R[6 + i] * w[2];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) wt[i] = group_sum<G>(wt[i]);
+    if (live) {
         const double *vg = Vg + 9 * p;
-        double rhs[3] = {-vg[6], -vg[7], -vg[8]};
-        const int32_t o0 = pstart[p], o1 = pstart[p + 1];
-        for (int32_t o = o0; o < o1; ++o) {
-            // W^T dc = Jp^T (Jc dc) = R^T A^T (A (dtheta x p + dt))
-            double rr[2], A[2][3], q[3];
-            load_j(J + (int64_t)JS * o, rr, A, q);
-            const double *d = dc + 6 * cam[o];
-            const double *R = Rt + 12 * cam[o];
-            const double v0 = d[1] * q[2] - d[2] * q[1] + d[3];
-            const double v1 = d[2] * q[0] - d[0] * q[2] + d[4];
-            const double v2 = d[0] * q[1] - d[1] * q[0] + d[5];
-            const double s0 = A[0][0] * v0 + A[0][1] * v1 + A[0][2] * v2;
-            const double s1 = A[1][0] * v0 + A[1][1] * v1 + A[1][2] * v2;
-            double w[3];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) w[i] = A[0][i] * s0 + A[1][i] * s1;
-#pragma unroll
-            for (int i = 0; i < 3; ++i) rhs[i] -= R[i] * w[0] + R[3 + i] * w[1] + R[6 + i] * w[2];
-        }
+        const double rhs[3] = {-vg[6] - wt[0], -vg[7] - wt[1], -vg[8] - wt[2]};
         const double *l = Lq + 9 * p;  // L upper: 00 01 02 11 12 22
-        // y = L^T rhs ; dp = L y
+        // y = L^T rhs ; dp = L y  (every lane of the group, identically)
         const double y0 = l[0] * rhs[0];
         const double y1 = l[1] * rhs[0] + l[3] * rhs[1];
         const double y2 = l[2] * rhs[0] + l[4] * rhs[1] + l[5] * rhs[2];
@@ -810,14 +854,17 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
         double xn[3];
         const double dg[3] = {vg[0], vg[3], vg[5]};
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            xn[i] = x[i] + dp[i];
-            X_new[3 * p + i] = xn[i];
-            acc[1] += dp[i] * (lambda * clampd(dg[i]) * dp[i] - vg[6 + i]);
-            acc[2] += dp[i] * dp[i];
-            acc[3] += x[i] * x[i];
+        for (int i = 0; i < 3; ++i) xn[i] = x[i] + dp[i];
+        if (sub == 0) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                X_new[3 * p + i] = xn[i];
+                acc[1] += dp[i] * (lambda * clampd(dg[i]) * dp[i] - vg[6 + i]);
+                acc[2] += dp[i] * dp[i];
+                acc[3] += x[i] * x[i];
+            }
         }
-        for (int32_t o = o0; o < o1; ++o) acc[0] += obs_cost(Rt_new + 12 * cam[o], xn, K, obs[o]);
+        for (int32_t o = o0 + sub; o < o1; o += G) acc[0] += obs_cost(Rt_new + 12 * cam[o], xn, K, obs[o]);
     }
     block_sum_store<4>(acc, partial + 4 * (int64_t)blockIdx.x);
 }
@@ -1107,7 +1154,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     p->npairs = tot;
     p->nitems = (int32_t)items.size();
     p->nblocks = (int32_t)blocks.size();
-    p->pt_blocks = std::max(1, ceil_div(np_, PT_THREADS));
+    p->pt_blocks = std::max(1, ceil_div(np_ * PT_GROUP, PT_THREADS));
     p->payload_len = (int64_t)p->ns * p->ns + 3 * p->ns + 1;
     int rc;
     if ((rc = p->alloc(p->d_cam, no)) || (rc = p->alloc(p->d_pt, no)) || (rc = p->alloc(p->d_pstart, np_ + 1)) ||
@@ -1209,10 +1256,15 @@ static int allreduce(sfm_ba_problem *p, double *buf, int64_t n) {
 static int run_linearize(sfm_ba_problem *p) {
     hipStream_t s = p->stream;
 
-    hipLaunchKernelGGL(k_linearize, dim3(p->pt_blocks), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam, p->d_obs,
-                       p->K, p->d_Rt, p->d_X, p->d_J, p->d_Vg, p->d_partial);
+    const int gl = lanes_per_point("SFM_LINEARIZE_LANES", 4);
+    const int nbl = std::max(1, ceil_div(p->np * gl, PT_THREADS));
+#define SFM_LIN(G)                                                                                                \
+    hipLaunchKernelGGL(k_linearize<G>, dim3(nbl), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam, p->d_obs, \
+                       p->K, p->d_Rt, p->d_X, p->d_J, p->d_Vg, p->d_partial)
+    switch (gl) { case 1: SFM_LIN(1); break; case 2: SFM_LIN(2); break; case 4: SFM_LIN(4); break; default: SFM_LIN(8); }
+#undef SFM_LIN
     SFM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, p->d_partial, p->pt_blocks, 1, p->d_scal + 8);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, p->d_partial, nbl, 1, p->d_scal + 8);
     SFM_HIP(hipGetLastError());
     if (p->ndiag_items) {
         hipLaunchKernelGGL(k_camera_lin, dim3(p->ndiag_items), dim3(256), 0, s, p->d_items, p->d_pairs, p->d_J,
@@ -1233,8 +1285,8 @@ static int run_step(sfm_ba_problem *p, double lambda, bool timed) {
     if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_PREP], s));
     SFM_HIP(hipMemsetAsync(p->d_payload, 0, p->payload_len * sizeof(double), s));
     SFM_HIP(hipMemsetAsync(p->d_bad, 0, sizeof(int), s));
-    hipLaunchKernelGGL(k_point_prep, dim3(p->pt_blocks), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam,
-                       p->d_Rt, p->d_J, p->d_Vg, lambda, p->d_Lq, p->d_Z);
+    hipLaunchKernelGGL(k_point_prep, dim3(std::max(1, ceil_div(p->no, OBS_THREADS))), dim3(OBS_THREADS), 0, s, (int64_t)p->no,
+                       p->d_pt, p->d_pstart, p->d_cam, p->d_Rt, p->d_J, p->d_Vg, lambda, p->d_Lq, p->d_Z);
     SFM_HIP(hipGetLastError());
     if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_PREP + 1], s));
     if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_SCHUR], s));
@@ -1262,11 +1314,16 @@ static int run_step(sfm_ba_problem *p, double lambda, bool timed) {
     hipLaunchKernelGGL(k_camera_trial, dim3(1), dim3(256), 0, s, p->nc, p->d_b, p->d_payload, p->ns, lambda, p->d_Rt,
                        p->d_Rt2, p->d_scal + 4);
     SFM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_backsub_trial, dim3(p->pt_blocks), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam,
-                       p->d_obs, p->K, p->d_J, p->d_Vg, p->d_Lq, p->d_b, lambda, p->d_Rt, p->d_Rt2, p->d_X, p->d_X2,
-                       p->d_partial);
+    const int gb = lanes_per_point("SFM_BACKSUB_LANES", 2);
+    const int nbb = std::max(1, ceil_div(p->np * gb, PT_THREADS));
+#define SFM_BS(G)                                                                                                  \
+    hipLaunchKernelGGL(k_backsub_trial<G>, dim3(nbb), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam,        \
+                       p->d_obs, p->K, p->d_J, p->d_Vg, p->d_Lq, p->d_b, lambda, p->d_Rt, p->d_Rt2, p->d_X, p->d_X2, \
+                       p->d_partial)
+    switch (gb) { case 1: SFM_BS(1); break; case 2: SFM_BS(2); break; case 4: SFM_BS(4); break; default: SFM_BS(8); }
+#undef SFM_BS
     SFM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, p->d_partial, p->pt_blocks, 4, p->d_scal);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, p->d_partial, nbb, 4, p->d_scal);
     SFM_HIP(hipGetLastError());
     if ((rc = allreduce(p, p->d_scal, 4))) return rc;
     if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_TRIAL + 1], s));
