@@ -13,6 +13,8 @@ MI355X, exactly as GetInliersRANSAC does for F:
    inliers of every hypothesis (one wavefront each, LDS tiles, ballot
    popcount) and keeps the first hypothesis with the strictly largest count.
 """
+import random  # noqa: F401  (part of the reference module's star-import surface)
+
 import numpy as np
 
 import _sfmcore as _core
