@@ -180,7 +180,8 @@ __global__ void __launch_bounds__(PT_THREADS) k_linearize(int64_t np_, const int
                                                           const double2 *__restrict__ obs, Kmat Km,
                                                           const double *__restrict__ Rt,
                                                           const double *__restrict__ X, double *__restrict__ J,
-                                                          double *__restrict__ Vg, double *__restrict__ partial) {
+                                                          double *__restrict__ Vg, double *__restrict__ partial, const int *__restrict__ gate) {
+    if (gate && !*gate) return;  // device-side LM control: iteration gated off
     const int64_t gt = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x;
     const int64_t p = gt / G;  // G lanes per point, striding over its observations
     const int sub = (int)(gt % G);
@@ -244,8 +245,10 @@ __global__ void __launch_bounds__(OBS_THREADS) k_point_prep(int64_t no, const in
                                                             const int32_t *__restrict__ cam,
                                                             const double *__restrict__ Rt,
                                                             const double *__restrict__ J,
-                                                            const double *__restrict__ Vg, double lambda,
-                                                            double *__restrict__ Lq, double *__restrict__ Z) {
+                                                            const double *__restrict__ Vg, const double *__restrict__ lam,
+                                                            double *__restrict__ Lq, double *__restrict__ Z, const int *__restrict__ gate) {
+    if (gate && !*gate) return;  // device-side LM control: iteration gated off
+    const double lambda = *lam;
     const int64_t o = (int64_t)blockIdx.x * OBS_THREADS + threadIdx.x;
     if (o >= no) return;
     const int64_t p = pt[o];
@@ -328,7 +331,8 @@ __global__ void __launch_bounds__(PAIR_THREADS) k_schur_pairs(const PairItem *__
                                                               const int32_t *__restrict__ pt,
                                                               const double *__restrict__ Z,
                                                               const double *__restrict__ Lq,
-                                                              double *__restrict__ slab) {
+                                                              double *__restrict__ slab, const int *__restrict__ gate) {
+    if (gate && !*gate) return;  // device-side LM control: iteration gated off
     __shared__ double red[PAIR_THREADS / 64][ITEM_W];
     const PairItem it = items[blockIdx.x];
     const int h = threadIdx.x & 1;
@@ -411,7 +415,8 @@ __global__ void __launch_bounds__(PAIR_THREADS) k_schur_pairs(const PairItem *__
 // and k_camera_lin_finish adds a camera's items in order (deterministic).
 __global__ void __launch_bounds__(256) k_camera_lin(const PairItem *__restrict__ items,
                                                     const int2 *__restrict__ pairs,
-                                                    const double *__restrict__ J, double *__restrict__ slab2) {
+                                                    const double *__restrict__ J, double *__restrict__ slab2, const int *__restrict__ gate) {
+    if (gate && !*gate) return;  // device-side LM control: iteration gated off
     __shared__ double red[4][CAMLIN];
     const PairItem it = items[blockIdx.x];
     double acc[CAMLIN];
@@ -452,7 +457,8 @@ struct BlockInfo {
 
 __global__ void __launch_bounds__(64) k_camera_lin_finish(const BlockInfo *__restrict__ blocks,
                                                           const double *__restrict__ slab2,
-                                                          double *__restrict__ camlin) {
+                                                          double *__restrict__ camlin, const int *__restrict__ gate) {
+    if (gate && !*gate) return;  // device-side LM control: iteration gated off
     const BlockInfo bi = blocks[blockIdx.x];  // diagonal blocks come first
     if (threadIdx.x >= CAMLIN) return;
     double v = 0;
@@ -463,7 +469,8 @@ __global__ void __launch_bounds__(64) k_camera_lin_finish(const BlockInfo *__res
 __global__ void __launch_bounds__(64) k_schur_finish(int32_t ns, const BlockInfo *__restrict__ blocks,
                                                      const double *__restrict__ slab,
                                                      const double *__restrict__ camlin,
-                                                     double *__restrict__ payload) {
+                                                     double *__restrict__ payload, const int *__restrict__ gate) {
+    if (gate && !*gate) return;  // device-side LM control: iteration gated off
     const BlockInfo bi = blocks[blockIdx.x];
     const int t = threadIdx.x;
     const bool diag = bi.i == bi.j;
@@ -491,8 +498,10 @@ __global__ void __launch_bounds__(64) k_schur_finish(int32_t ns, const BlockInfo
 }
 
 // A (nsp x nsp, padded with identity), bvec (nsp)
-__global__ void k_assemble(int32_t ns, int32_t nsp, const double *__restrict__ payload, double lambda,
-                           double *__restrict__ A, double *__restrict__ bvec) {
+__global__ void k_assemble(int32_t ns, int32_t nsp, const double *__restrict__ payload, const double *__restrict__ lam,
+                           double *__restrict__ A, double *__restrict__ bvec, const int *__restrict__ gate) {
+    if (gate && !*gate) return;  // device-side LM control: iteration gated off
+    const double lambda = *lam;
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (int64_t)nsp * nsp) return;
     const int r = (int)(idx / nsp), c = (int)(idx % nsp);
@@ -561,7 +570,8 @@ __device__ __forceinline__ void chol_factor16(double (&r)[NB], double (&dinv)[NB
 
 __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_t nsp, int s,
                                                   double *__restrict__ D, double *__restrict__ bvec,
-                                                  int *__restrict__ bad) {
+                                                  int *__restrict__ bad, const int *__restrict__ gate) {
+    if (gate && !*gate) return;  // device-side LM control: iteration gated off
     __shared__ double Lr[NB][NB + 1], Lc[NB][NB + 1], Ct[NB][NB + 1], Cd[NB][NB + 1];
     __shared__ double yk[NB];
     const int t = threadIdx.x;
@@ -686,7 +696,8 @@ constexpr int SOLVE_MAX = 4096;
 
 __global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(double *__restrict__ A, int32_t nsp,
                                                                   double *__restrict__ xg,
-                                                                  const double *__restrict__ Dlast) {
+                                                                  const double *__restrict__ Dlast, const int *__restrict__ gate) {
+    if (gate && !*gate) return;  // device-side LM control: iteration gated off
     __shared__ double x[SOLVE_MAX];
     __shared__ double yt[NB];
     const int t = threadIdx.x, lane = t & 63;
@@ -740,6 +751,79 @@ __global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(double *__rest
     for (int i = t; i < nsp; i += SOLVE_THREADS) xg[i] = x[i];
 }
 
+// ------------------------------------------------- device-side LM control
+// The accept/reject decision and the damping update run on the device, so
+// the host can enqueue many iterations without reading anything back; each
+// kernel of an iteration is gated on run_lin / run_step (set by the previous
+// decision), and the host polls `done` once per batch.
+struct LMState {
+    double lambda, nu, cost, cost0;
+    int status, accepted, iters, done;
+    int run_lin, run_step, accept_now, pad;
+};
+
+__global__ void k_lm_reset(LMState *lm, double lambda0) {
+    lm->lambda = lambda0; lm->nu = 2.0; lm->cost = 0.0; lm->cost0 = 0.0;
+    lm->status = 4; lm->accepted = 0; lm->iters = 0; lm->done = 0;
+    lm->run_lin = 1; lm->run_step = 1; lm->accept_now = 0;
+}
+
+__global__ void k_lm_init(LMState *lm, const double *lin_cost) { lm->cost = lm->cost0 = *lin_cost; }
+
+// sfm_ba_solve's host logic, verbatim: Nielsen's lambda update on the gain
+// ratio of the trial step; scal = [cost_trial, model_p, dn_p, xn_p, model_c,
+// dn_c, xn_c]
+__global__ void k_lm_decide(LMState *lm, const double *__restrict__ h, const int *__restrict__ badp,
+                            int max_iterations, int fixed, double ftol, double ptol, double lambda0) {
+#pragma clang fp contract(off)
+    if (lm->done) { lm->accept_now = 0; return; }
+    const int bad = *badp;
+    const double cost = lm->cost;
+    const double cost_new = h[0];
+    const double model = 0.5 * (h[1] + h[4]);
+    const double dnorm = sqrt(h[2] + h[5]), xnorm = sqrt(h[3] + h[6]);
+    const double rho = (!bad && model > 0) ? (cost - cost_new) / model : -1.0;
+    lm->iters += 1;
+    int done = 0;
+    if (!bad && isfinite(cost_new) && rho > 1e-3) {
+        lm->accept_now = 1;
+        const double dcost = cost - cost_new;
+        lm->cost = cost_new;
+        lm->accepted += 1;
+        double f = 2.0 * rho - 1.0;
+        f = 1.0 - f * f * f;
+        lm->lambda *= (f > 1.0 / 3.0 ? f : 1.0 / 3.0);
+        lm->nu = 2.0;
+        lm->run_lin = 1;
+        if (!fixed) {
+            if (dcost < ftol * cost_new) { lm->status = 1; done = 1; }
+            else if (dnorm < ptol * (xnorm + ptol)) { lm->status = 3; done = 1; }
+        }
+    } else {
+        lm->accept_now = 0;
+        lm->lambda *= lm->nu;
+        lm->nu *= 2.0;
+        lm->run_lin = 0;
+        if (lm->lambda > 1e32) {
+            if (!fixed) { lm->status = 5; done = 1; }
+            else { lm->lambda = lambda0; lm->nu = 2.0; }
+        }
+    }
+    if (lm->iters >= max_iterations) done = 1;
+    lm->done = done;
+    lm->run_step = !done;
+    lm->run_lin = lm->run_lin && !done;
+}
+
+// accepted step: the trial state becomes the current one
+__global__ void k_lm_accept(const LMState *__restrict__ lm, int64_t np_, int32_t nc, double *__restrict__ X,
+                            const double *__restrict__ X2, double *__restrict__ Rt, const double *__restrict__ Rt2) {
+    if (!lm->accept_now) return;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 3 * np_) X[i] = X2[i];
+    if (i < 12 * (int64_t)nc) Rt[i] = Rt2[i];
+}
+
 // Lanes per point for the grouped per-point kernels (1, 2, 4 or 8; an
 // environment override is read once, for tuning).
 static int lanes_per_point(const char *env, int dflt) {
@@ -750,15 +834,17 @@ static int lanes_per_point(const char *env, int dflt) {
 
 // Factor + forward solve (nT launches of k_chol_col) and backward solve of
 // the padded reduced camera system; A, b on the device, D = 2 NB^2 scratch.
-static int launch_cholesky(double *A, int32_t nsp, double *b, double *D, int *bad, hipStream_t s) {
+static int launch_cholesky(double *A, int32_t nsp, double *b, double *D, int *bad, hipStream_t s,
+                           const int *gate = nullptr) {
     const int nT = nsp / NB;
     for (int st = 0; st < nT; ++st) {
         const int T = nT - st;
         hipLaunchKernelGGL(k_chol_col, dim3(T * (T + 1) / 2 + (st >= 1 ? 1 : 0)), dim3(256), 0, s, A, nsp, st, D, b,
-                           bad);
+                           bad, gate);
         SFM_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(SOLVE_THREADS), 0, s, A, nsp, b, D + ((nT - 1) & 1) * NB * NB);
+    hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(SOLVE_THREADS), 0, s, A, nsp, b, D + ((nT - 1) & 1) * NB * NB,
+                       gate);
     SFM_HIP(hipGetLastError());
     return 0;
 }
@@ -766,9 +852,11 @@ static int launch_cholesky(double *A, int32_t nsp, double *b, double *D, int *ba
 // one workgroup: trial cameras + camera part of model decrease / norms.
 // cam_out[0..3) = {model_c, |dc|^2, |t|^2}
 __global__ void __launch_bounds__(256) k_camera_trial(int32_t nc, const double *__restrict__ dc,
-                                                      const double *__restrict__ payload, int32_t ns, double lambda,
+                                                      const double *__restrict__ payload, int32_t ns, const double *__restrict__ lam,
                                                       const double *__restrict__ Rt, double *__restrict__ Rt_new,
-                                                      double *__restrict__ cam_out) {
+                                                      double *__restrict__ cam_out, const int *__restrict__ gate) {
+    if (gate && !*gate) return;  // device-side LM control: iteration gated off
+    const double lambda = *lam;
     __shared__ double red[3][256];
     double m = 0, dn = 0, xn = 0;
     const double *diagU = payload + (int64_t)ns * ns, *gc = diagU + ns;
@@ -807,11 +895,13 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
                                                               const double *__restrict__ J,
                                                               const double *__restrict__ Vg,
                                                               const double *__restrict__ Lq,
-                                                              const double *__restrict__ dc, double lambda,
+                                                              const double *__restrict__ dc, const double *__restrict__ lam,
                                                               const double *__restrict__ Rt,
                                                               const double *__restrict__ Rt_new,
                                                               const double *__restrict__ X,
-                                                              double *__restrict__ X_new, double *__restrict__ partial) {
+                                                              double *__restrict__ X_new, double *__restrict__ partial, const int *__restrict__ gate) {
+    if (gate && !*gate) return;  // device-side LM control: iteration gated off
+    const double lambda = *lam;
     const int64_t gt = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x;
     const int64_t p = gt / G;  // G lanes per point, striding over its observations
     const int sub = (int)(gt % G);
@@ -871,7 +961,8 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
 
 // fixed-order sum of nblk partials of width w into out[0..w)
 __global__ void __launch_bounds__(256) k_finalize(const double *__restrict__ partial, int nblk, int w,
-                                                  double *__restrict__ out) {
+                                                  double *__restrict__ out, const int *__restrict__ gate) {
+    if (gate && !*gate) return;  // device-side LM control: iteration gated off
     __shared__ double red[256];
     for (int k = 0; k < w; ++k) {
         double s = 0;
@@ -934,6 +1025,7 @@ using namespace sfm;
 
 // ------------------------------------------------------------ problem
 enum { T_LIN, T_PREP, T_SCHUR, T_COMM, T_SOLVE, T_TRIAL, T_NT };
+constexpr int kEvSlots = 16;  // max iterations per batch between host polls
 static const char *kTimerNames = "linearize;point_prep;schur_blocks;allreduce;cholesky;backsub_trial";
 
 struct sfm_ba_problem {
@@ -961,6 +1053,8 @@ struct sfm_ba_problem {
     int64_t payload_len = 0;
     int pt_blocks = 0;
     hipEvent_t ev[2 * T_NT] = {};
+    hipEvent_t ev_it[2 * T_NT * kEvSlots] = {};  // per-iteration timing slots of a batch
+    LMState *d_lm = nullptr;
     double t_acc[T_NT] = {};
     int t_iters = 0;
     std::vector<void *> allocs;
@@ -969,6 +1063,8 @@ struct sfm_ba_problem {
         for (void *p : allocs) (void)hipFree(p);
         if (h_scal) (void)hipHostFree(h_scal);
         for (auto &e : ev)
+            if (e) (void)hipEventDestroy(e);
+        for (auto &e : ev_it)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -1086,6 +1182,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     p->pts0.assign(pts, pts + 3 * (size_t)np_);
     SFM_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
     for (auto &e : p->ev) SFM_HIP(hipEventCreate(&e));
+    for (auto &e : p->ev_it) SFM_HIP(hipEventCreate(&e));
     // point CSR
     std::vector<int32_t> pstart(np_ + 1, 0);
     for (int64_t o = 0; o < no; ++o) pstart[pt[o] + 1]++;
@@ -1170,6 +1267,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = p->alloc(p->d_A, (int64_t)p->nsp * p->nsp)) || (rc = p->alloc(p->d_b, p->nsp)) ||
         (rc = p->alloc(p->d_D, 2 * NB * NB)) ||
         (rc = p->alloc(p->d_partial, 4 * (int64_t)p->pt_blocks)) || (rc = p->alloc(p->d_scal, 16)) ||
+        (rc = p->alloc(p->d_lm, 1)) ||
         (rc = p->alloc(p->d_bad, 4)))
         return rc;
     SFM_HIP(hipHostMalloc((void **)&p->h_scal, 16 * sizeof(double)));
@@ -1255,166 +1353,146 @@ static int allreduce(sfm_ba_problem *p, double *buf, int64_t n) {
 // launches one linearisation (J, V, g) and, into d_scal[8], the cost.
 static int run_linearize(sfm_ba_problem *p) {
     hipStream_t s = p->stream;
+    const int *glin = &p->d_lm->run_lin;
 
     const int gl = lanes_per_point("SFM_LINEARIZE_LANES", 4);
     const int nbl = std::max(1, ceil_div(p->np * gl, PT_THREADS));
 #define SFM_LIN(G)                                                                                                \
     hipLaunchKernelGGL(k_linearize<G>, dim3(nbl), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam, p->d_obs, \
-                       p->K, p->d_Rt, p->d_X, p->d_J, p->d_Vg, p->d_partial)
+                       p->K, p->d_Rt, p->d_X, p->d_J, p->d_Vg, p->d_partial, glin)
     switch (gl) { case 1: SFM_LIN(1); break; case 2: SFM_LIN(2); break; case 4: SFM_LIN(4); break; default: SFM_LIN(8); }
 #undef SFM_LIN
     SFM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, p->d_partial, nbl, 1, p->d_scal + 8);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, p->d_partial, nbl, 1, p->d_scal + 8, glin);
     SFM_HIP(hipGetLastError());
     if (p->ndiag_items) {
         hipLaunchKernelGGL(k_camera_lin, dim3(p->ndiag_items), dim3(256), 0, s, p->d_items, p->d_pairs, p->d_J,
-                           p->d_slab2);
+                           p->d_slab2, glin);
         SFM_HIP(hipGetLastError());
         hipLaunchKernelGGL(k_camera_lin_finish, dim3(p->ndiag_blocks), dim3(64), 0, s, p->d_blocks, p->d_slab2,
-                           p->d_camlin);
+                           p->d_camlin, glin);
         SFM_HIP(hipGetLastError());
     }
     return allreduce(p, p->d_scal + 8, 1);
 }
 
-// one damped solve + trial evaluation; on return h_scal holds
-// [cost_trial, model_p, dn_p, xn_p, model_c, dn_c, xn_c, bad]
-static int run_step(sfm_ba_problem *p, double lambda, bool timed) {
+// one damped solve + trial evaluation (gated on the device LM state); leaves
+// d_scal = [cost_trial, model_p, dn_p, xn_p, model_c, dn_c, xn_c] and d_bad for
+// k_lm_decide.  ev: this iteration's timing-event slot (nullable).
+static int run_step(sfm_ba_problem *p, hipEvent_t *ev) {
     hipStream_t s = p->stream;
     int rc;
-    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_PREP], s));
+    const bool timed = ev != nullptr;
+    const int *gst = &p->d_lm->run_step;
+    const double *lam = &p->d_lm->lambda;
+    if (timed) SFM_HIP(hipEventRecord(ev[2 * T_PREP], s));
     SFM_HIP(hipMemsetAsync(p->d_payload, 0, p->payload_len * sizeof(double), s));
     SFM_HIP(hipMemsetAsync(p->d_bad, 0, sizeof(int), s));
     hipLaunchKernelGGL(k_point_prep, dim3(std::max(1, ceil_div(p->no, OBS_THREADS))), dim3(OBS_THREADS), 0, s, (int64_t)p->no,
-                       p->d_pt, p->d_pstart, p->d_cam, p->d_Rt, p->d_J, p->d_Vg, lambda, p->d_Lq, p->d_Z);
+                       p->d_pt, p->d_pstart, p->d_cam, p->d_Rt, p->d_J, p->d_Vg, lam, p->d_Lq, p->d_Z, gst);
     SFM_HIP(hipGetLastError());
-    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_PREP + 1], s));
-    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_SCHUR], s));
+    if (timed) SFM_HIP(hipEventRecord(ev[2 * T_PREP + 1], s));
+    if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SCHUR], s));
     if (p->nitems) {
         hipLaunchKernelGGL(k_schur_pairs, dim3(p->nitems), dim3(PAIR_THREADS), 0, s, p->d_items, p->d_pairs, p->d_pt,
-                           p->d_Z, p->d_Lq, p->d_slab);
+                           p->d_Z, p->d_Lq, p->d_slab, gst);
         SFM_HIP(hipGetLastError());
         hipLaunchKernelGGL(k_schur_finish, dim3(p->nblocks), dim3(64), 0, s, p->ns, p->d_blocks, p->d_slab,
-                           p->d_camlin, p->d_payload);
+                           p->d_camlin, p->d_payload, gst);
         SFM_HIP(hipGetLastError());
     }
-    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_SCHUR + 1], s));
-    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_COMM], s));
+    if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SCHUR + 1], s));
+    if (timed) SFM_HIP(hipEventRecord(ev[2 * T_COMM], s));
     if ((rc = allreduce(p, p->d_payload, p->payload_len - 1))) return rc;
-    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_COMM + 1], s));
-    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_SOLVE], s));
+    if (timed) SFM_HIP(hipEventRecord(ev[2 * T_COMM + 1], s));
+    if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SOLVE], s));
     const int64_t nA = (int64_t)p->nsp * p->nsp;
-    hipLaunchKernelGGL(k_assemble, dim3(ceil_div(nA, 256)), dim3(256), 0, s, p->ns, p->nsp, p->d_payload, lambda,
-                       p->d_A, p->d_b);
+    hipLaunchKernelGGL(k_assemble, dim3(ceil_div(nA, 256)), dim3(256), 0, s, p->ns, p->nsp, p->d_payload, lam,
+                       p->d_A, p->d_b, gst);
     SFM_HIP(hipGetLastError());
-    if ((rc = launch_cholesky(p->d_A, p->nsp, p->d_b, p->d_D, p->d_bad, s))) return rc;
+    if ((rc = launch_cholesky(p->d_A, p->nsp, p->d_b, p->d_D, p->d_bad, s, gst))) return rc;
     SFM_HIP(hipGetLastError());
-    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_SOLVE + 1], s));
-    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_TRIAL], s));
-    hipLaunchKernelGGL(k_camera_trial, dim3(1), dim3(256), 0, s, p->nc, p->d_b, p->d_payload, p->ns, lambda, p->d_Rt,
-                       p->d_Rt2, p->d_scal + 4);
+    if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SOLVE + 1], s));
+    if (timed) SFM_HIP(hipEventRecord(ev[2 * T_TRIAL], s));
+    hipLaunchKernelGGL(k_camera_trial, dim3(1), dim3(256), 0, s, p->nc, p->d_b, p->d_payload, p->ns, lam, p->d_Rt,
+                       p->d_Rt2, p->d_scal + 4, gst);
     SFM_HIP(hipGetLastError());
     const int gb = lanes_per_point("SFM_BACKSUB_LANES", 2);
     const int nbb = std::max(1, ceil_div(p->np * gb, PT_THREADS));
 #define SFM_BS(G)                                                                                                  \
     hipLaunchKernelGGL(k_backsub_trial<G>, dim3(nbb), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam,        \
-                       p->d_obs, p->K, p->d_J, p->d_Vg, p->d_Lq, p->d_b, lambda, p->d_Rt, p->d_Rt2, p->d_X, p->d_X2, \
-                       p->d_partial)
+                       p->d_obs, p->K, p->d_J, p->d_Vg, p->d_Lq, p->d_b, lam, p->d_Rt, p->d_Rt2, p->d_X, p->d_X2, \
+                       p->d_partial, gst)
     switch (gb) { case 1: SFM_BS(1); break; case 2: SFM_BS(2); break; case 4: SFM_BS(4); break; default: SFM_BS(8); }
 #undef SFM_BS
     SFM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, p->d_partial, nbb, 4, p->d_scal);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, p->d_partial, nbb, 4, p->d_scal, gst);
     SFM_HIP(hipGetLastError());
     if ((rc = allreduce(p, p->d_scal, 4))) return rc;
-    if (timed) SFM_HIP(hipEventRecord(p->ev[2 * T_TRIAL + 1], s));
-    SFM_HIP(hipMemcpyAsync(p->h_scal, p->d_scal, 7 * sizeof(double), hipMemcpyDeviceToHost, s));
-    SFM_HIP(hipMemcpyAsync(p->h_scal + 7, p->d_bad, sizeof(int), hipMemcpyDeviceToHost, s));
-    SFM_HIP(hipStreamSynchronize(s));
-    if (timed) {
-        for (int k = T_PREP; k < T_NT; ++k) {
-            float ms = 0;
-            (void)hipEventElapsedTime(&ms, p->ev[2 * k], p->ev[2 * k + 1]);
-            p->t_acc[k] += ms;
-        }
-    }
+    if (timed) SFM_HIP(hipEventRecord(ev[2 * T_TRIAL + 1], s));
     return 0;
 }
 
 extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_report *rep) {
     SFM_CHECK_ARG(p && o, "null pointer");
+    SFM_CHECK_ARG(o->max_iterations >= 0, "max_iterations < 0");
     SFM_HIP(hipSetDevice(p->device));
     (void)hipGetLastError();
     const auto t0 = std::chrono::steady_clock::now();
     for (double &t : p->t_acc) t = 0;
     p->t_iters = 0;
+    hipStream_t s = p->stream;
     int rc;
-    double lambda = o->initial_lambda, nu = 2.0, cost = 0, cost0 = 0;
-    int status = 4, accepted = 0, it = 0;
-    bool need_lin = true, first = true;
-    for (it = 0; it < o->max_iterations; ++it) {
-        if (need_lin) {
-            SFM_HIP(hipEventRecord(p->ev[2 * T_LIN], p->stream));
-            if ((rc = run_linearize(p))) return rc;
-            SFM_HIP(hipEventRecord(p->ev[2 * T_LIN + 1], p->stream));
-            if (first) {
-                SFM_HIP(hipMemcpyAsync(p->h_scal + 8, p->d_scal + 8, sizeof(double), hipMemcpyDeviceToHost, p->stream));
-                SFM_HIP(hipStreamSynchronize(p->stream));
-                cost = cost0 = p->h_scal[8];
-                first = false;
-            }
-            need_lin = false;
+    // iterations enqueued between two reads of the device LM state
+    int batch = 8;
+    if (const char *e = std::getenv("SFM_LM_BATCH")) batch = std::atoi(e);
+    batch = std::min(std::max(batch, 1), kEvSlots);
+    hipLaunchKernelGGL(k_lm_reset, dim3(1), dim3(1), 0, s, p->d_lm, o->initial_lambda);
+    SFM_HIP(hipGetLastError());
+    LMState h{};
+    h.lambda = o->initial_lambda;
+    h.status = 4;
+    const int64_t nacc = std::max<int64_t>(3 * p->np, 12 * (int64_t)p->nc);
+    for (int it = 0; it < o->max_iterations; ++it) {
+        hipEvent_t *ev = p->ev_it + (size_t)(it % batch) * 2 * T_NT;
+        SFM_HIP(hipEventRecord(ev[2 * T_LIN], s));
+        if ((rc = run_linearize(p))) return rc;
+        SFM_HIP(hipEventRecord(ev[2 * T_LIN + 1], s));
+        if (it == 0) {
+            hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(1), 0, s, p->d_lm, p->d_scal + 8);
+            SFM_HIP(hipGetLastError());
         }
-        if ((rc = run_step(p, lambda, true))) return rc;
-        {
-            float ms = 0;
-            if (hipEventElapsedTime(&ms, p->ev[2 * T_LIN], p->ev[2 * T_LIN + 1]) == hipSuccess) p->t_acc[T_LIN] += ms;
-        }
-        p->t_iters++;
-        const double *h = p->h_scal;
-        int bad = 0;
-        std::memcpy(&bad, h + 7, sizeof(int));
-        const double cost_new = h[0];
-        const double model = 0.5 * (h[1] + h[4]);
-        const double dnorm = std::sqrt(h[2] + h[5]), xnorm = std::sqrt(h[3] + h[6]);
-        const double rho = (!bad && model > 0) ? (cost - cost_new) / model : -1.0;
-        if (!bad && std::isfinite(cost_new) && rho > 1e-3) {
-            std::swap(p->d_Rt, p->d_Rt2);
-            std::swap(p->d_X, p->d_X2);
-            const double dcost = cost - cost_new;
-            cost = cost_new;
-            accepted++;
-            double f = 2.0 * rho - 1.0;
-            f = 1.0 - f * f * f;
-            lambda *= std::max(f, 1.0 / 3.0);
-            nu = 2.0;
-            need_lin = true;
-            if (!o->fixed_iterations) {
-                if (dcost < o->function_tolerance * cost) { status = 1; ++it; break; }
-                if (dnorm < o->parameter_tolerance * (xnorm + o->parameter_tolerance)) { status = 3; ++it; break; }
+        if ((rc = run_step(p, ev))) return rc;
+        hipLaunchKernelGGL(k_lm_decide, dim3(1), dim3(1), 0, s, p->d_lm, p->d_scal, p->d_bad, o->max_iterations,
+                           o->fixed_iterations, o->function_tolerance, o->parameter_tolerance, o->initial_lambda);
+        SFM_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_lm_accept, dim3(ceil_div(nacc, 256)), dim3(256), 0, s, p->d_lm, p->np, p->nc, p->d_X,
+                           p->d_X2, p->d_Rt, p->d_Rt2);
+        SFM_HIP(hipGetLastError());
+        if ((it + 1) % batch == 0 || it + 1 == o->max_iterations) {
+            SFM_HIP(hipMemcpyAsync(&h, p->d_lm, sizeof h, hipMemcpyDeviceToHost, s));
+            SFM_HIP(hipStreamSynchronize(s));
+            for (int j = it - it % batch; j <= it && j < h.iters; ++j) {  // iterations that ran
+                hipEvent_t *e = p->ev_it + (size_t)(j % batch) * 2 * T_NT;
+                for (int k = 0; k < T_NT; ++k) {
+                    float ms = 0;
+                    if (hipEventElapsedTime(&ms, e[2 * k], e[2 * k + 1]) == hipSuccess) p->t_acc[k] += ms;
+                }
+                p->t_iters++;
             }
-        } else {
-            lambda *= nu;
-            nu *= 2.0;
-            if (lambda > 1e32) {
-                if (!o->fixed_iterations) { status = 5; ++it; break; }
-                lambda = o->initial_lambda;
-                nu = 2.0;
-            }
+            if (h.done) break;
         }
-        // the timing event for linearize is re-recorded only on the next accepted step
-        SFM_HIP(hipEventRecord(p->ev[2 * T_LIN], p->stream));
-        SFM_HIP(hipEventRecord(p->ev[2 * T_LIN + 1], p->stream));
     }
     const auto t1 = std::chrono::steady_clock::now();
     if (rep) {
-        rep->iterations = it;
-        rep->accepted = accepted;
-        rep->status = status;
+        rep->iterations = h.iters;
+        rep->accepted = h.accepted;
+        rep->status = h.status;
         rep->n_ranks = p->comm ? p->comm->nranks : 1;
-        rep->cost0 = cost0;
-        rep->cost = cost;
+        rep->cost0 = h.cost0;
+        rep->cost = h.cost;
         rep->t_loop_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-        rep->lambda = lambda;
+        rep->lambda = h.lambda;
     }
     return 0;
 }
