@@ -551,9 +551,10 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
 //                        in use by the other column blocks);
 //   block 0 (s >= 1)   : D[(s-1) & 1] -> A's diagonal tile s-1 and
 //                        b_i -= L_i,s-1 y_s-1 for rows past column s.
-__device__ __forceinline__ void chol_factor16(double (&r)[NB], double (&dinv)[NB], int lane, int *bad) {
+template <int TB>
+__device__ __forceinline__ void chol_factor(double (&r)[TB], double (&dinv)[TB], int lane, int *bad) {
 #pragma unroll
-    for (int k = 0; k < NB; ++k) {
+    for (int k = 0; k < TB; ++k) {
         const double d = readlane_f64(r[k], k);
         if (lane == 0 && !(d > 0.0)) *bad = 1;
         // 1/sqrt(d): v_rsq_f64 then two Newton steps (~1 ulp), off the
@@ -564,33 +565,34 @@ __device__ __forceinline__ void chol_factor16(double (&r)[NB], double (&dinv)[NB
         dinv[k] = g;
         r[k] = (lane == k) ? d * g : r[k] * g;
 #pragma unroll
-        for (int j = k + 1; j < NB; ++j) r[j] -= r[k] * readlane_f64(r[k], j);
+        for (int j = k + 1; j < TB; ++j) r[j] -= r[k] * readlane_f64(r[k], j);
     }
 }
 
+template <int TB>
 __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_t nsp, int s,
                                                   double *__restrict__ D, double *__restrict__ bvec,
                                                   int *__restrict__ bad, const int *__restrict__ gate) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
-    __shared__ double Lr[NB][NB + 1], Lc[NB][NB + 1], Ct[NB][NB + 1], Cd[NB][NB + 1];
-    __shared__ double yk[NB];
+    __shared__ double Lr[TB][TB + 1], Lc[TB][TB + 1], Ct[TB][TB + 1], Cd[TB][TB + 1];
+    __shared__ double yk[TB];
     const int t = threadIdx.x;
-    const int nT = nsp / NB;
+    const int nT = nsp / TB;
     const bool upd = s >= 1;
-    const int kp = (s - 1) * NB;  // previous column's first index
+    const int kp = (s - 1) * TB;  // previous column's first index
     int blk = blockIdx.x;
     if (upd && blk == 0) {
-        const double *Dp = D + ((s - 1) & 1) * NB * NB;
-        for (int e = t; e < NB * NB; e += blockDim.x) {
-            const int i = e / NB, j = e % NB;
-            A[(int64_t)(kp + i) * nsp + kp + j] = i >= j ? Dp[i * NB + j] : Dp[j * NB + i];
+        const double *Dp = D + ((s - 1) & 1) * TB * TB;
+        for (int e = t; e < TB * TB; e += blockDim.x) {
+            const int i = e / TB, j = e % TB;
+            A[(int64_t)(kp + i) * nsp + kp + j] = i >= j ? Dp[i * TB + j] : Dp[j * TB + i];
         }
-        if (t < NB) yk[t] = bvec[kp + t];
+        if (t < TB) yk[t] = bvec[kp + t];
         __syncthreads();
-        for (int i = (s + 1) * NB + t; i < nsp; i += blockDim.x) {
+        for (int i = (s + 1) * TB + t; i < nsp; i += blockDim.x) {
             double acc = 0;
 #pragma unroll 8
-            for (int m = 0; m < NB; ++m) acc += A[(int64_t)(kp + m) * nsp + i] * yk[m];  // L[i][kp+m] (mirror)
+            for (int m = 0; m < TB; ++m) acc += A[(int64_t)(kp + m) * nsp + i] * yk[m];  // L[i][kp+m] (mirror)
             bvec[i] -= acc;
         }
         return;
@@ -599,75 +601,83 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
     int rr = 0;
     while (blk > rr) { blk -= rr + 1; ++rr; }
     const int r = s + rr, c = s + blk;  // lower tile (r, c), r >= c >= s
-    const int r0 = r * NB, c0 = c * NB, s0 = s * NB;
+    const int r0 = r * TB, c0 = c * TB, s0 = s * TB;
     const bool colblk = c == s, need_d = colblk && r > s;
     // every global load of the block in one round: L_r,s-1, L_c,s-1, A_rc, A_ss
+    constexpr int EPT = TB * TB / 256;  // tile elements per thread
     {
-        const int i = t / NB, j = t % NB;
-        const double lr = upd ? A[(int64_t)(r0 + i) * nsp + kp + j] : 0.0;
-        const double lc = upd ? A[(int64_t)(c0 + i) * nsp + kp + j] : 0.0;
-        const double arc = A[(int64_t)(r0 + i) * nsp + c0 + j];
-        const double ass = need_d ? A[(int64_t)(s0 + i) * nsp + s0 + j] : 0.0;
-        Lr[i][j] = lr;
-        Lc[i][j] = lc;
+        double arc[EPT], ass[EPT];
+#pragma unroll
+        for (int q = 0; q < EPT; ++q) {
+            const int e = t + 256 * q, i = e / TB, j = e % TB;
+            Lr[i][j] = upd ? A[(int64_t)(r0 + i) * nsp + kp + j] : 0.0;
+            Lc[i][j] = upd ? A[(int64_t)(c0 + i) * nsp + kp + j] : 0.0;
+            arc[q] = A[(int64_t)(r0 + i) * nsp + c0 + j];
+            ass[q] = need_d ? A[(int64_t)(s0 + i) * nsp + s0 + j] : 0.0;
+        }
         __syncthreads();
-        double v = arc, w = ass;
-        if (upd) {
-            double a1 = 0, a2 = 0;
+#pragma unroll
+        for (int q = 0; q < EPT; ++q) {
+            const int e = t + 256 * q, i = e / TB, j = e % TB;
+            double v = arc[q], w = ass[q];
+            if (upd) {
+                double a1 = 0, a2 = 0;
 #pragma unroll 8
-            for (int m = 0; m < NB; ++m) {
-                a1 += Lr[i][m] * Lc[j][m];
-                a2 += Lc[i][m] * Lc[j][m];
+                for (int m = 0; m < TB; ++m) {
+                    a1 += Lr[i][m] * Lc[j][m];
+                    a2 += Lc[i][m] * Lc[j][m];
+                }
+                v -= a1;
+                w -= a2;
             }
-            v -= a1;
-            w -= a2;
+            if (!colblk) {
+                A[(int64_t)(r0 + i) * nsp + c0 + j] = v;
+            } else {
+                Ct[i][j] = v;
+                if (need_d) Cd[i][j] = w;
+            }
         }
-        if (!colblk) {  // trailing tile: done
-            A[(int64_t)(r0 + i) * nsp + c0 + j] = v;
-            return;
-        }
-        Ct[i][j] = v;
-        if (need_d) Cd[i][j] = w;
+        if (!colblk) return;  // trailing tile: done
     }
     // column s: C_ss (Cd, or Ct in the diagonal block) is bitwise the same in
     // every column block -- same inputs, same operation order
     __syncthreads();
     if (t >= 64) return;
     const int lane = t;
-    const int li = lane < NB ? lane : NB - 1;
-    double (*Cdd)[NB + 1] = (r > s) ? Cd : Ct;
-    double rw[NB], dinv[NB];
+    const int li = lane < TB ? lane : TB - 1;
+    double (*Cdd)[TB + 1] = (r > s) ? Cd : Ct;
+    double rw[TB], dinv[TB];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) rw[j] = Cdd[li][j];
-    chol_factor16(rw, dinv, lane, bad);
+    for (int j = 0; j < TB; ++j) rw[j] = Cdd[li][j];
+    chol_factor<TB>(rw, dinv, lane, bad);
     if (r == s) {
         double y = bvec[s0 + li];
         if (upd) {
             double acc = 0;
 #pragma unroll
-            for (int m = 0; m < NB; ++m) acc += Lc[li][m] * bvec[kp + m];
+            for (int m = 0; m < TB; ++m) acc += Lc[li][m] * bvec[kp + m];
             y -= acc;
         }
 #pragma unroll
-        for (int j = 0; j < NB; ++j) {
+        for (int j = 0; j < TB; ++j) {
             const double yj = readlane_f64(y, j) * dinv[j];
             if (lane == j) y = yj;
             if (lane > j) y -= rw[j] * yj;
         }
-        if (lane < NB) {
+        if (lane < TB) {
             bvec[s0 + lane] = y;
-            double *Dn = D + (s & 1) * NB * NB;
+            double *Dn = D + (s & 1) * TB * TB;
 #pragma unroll
-            for (int j = 0; j < NB; ++j) Dn[lane * NB + j] = j <= lane ? rw[j] : 0.0;
+            for (int j = 0; j < TB; ++j) Dn[lane * TB + j] = j <= lane ? rw[j] : 0.0;
         }
         return;
     }
     // L_rs = C_rs L_ss^-T, one tile row per lane (L_jm = lane j's rw[m])
-    double x[NB];
+    double x[TB];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) x[j] = Ct[li][j];
+    for (int j = 0; j < TB; ++j) x[j] = Ct[li][j];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
+    for (int j = 0; j < TB; ++j) {
         double v0 = x[j], v1 = 0.0, v2 = 0.0, v3 = 0.0;
 #pragma unroll
         for (int m = 0; m < j; ++m) {
@@ -680,70 +690,71 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
         x[j] = ((v0 + v1) + (v2 + v3)) * dinv[j];
     }
     wave_sync_lds();
-    if (lane < NB)
+    if (lane < TB)
 #pragma unroll
-        for (int j = 0; j < NB; ++j) Lr[lane][j] = x[j];
+        for (int j = 0; j < TB; ++j) Lr[lane][j] = x[j];
     wave_sync_lds();
-    for (int e = lane; e < NB * NB; e += 64)
-        A[(int64_t)(r0 + e / NB) * nsp + s0 + e % NB] = Lr[e / NB][e % NB];
-    for (int e = lane; e < NB * NB; e += 64)  // mirror into the upper triangle
-        A[(int64_t)(s0 + e / NB) * nsp + r0 + e % NB] = Lr[e % NB][e / NB];
+    for (int e = lane; e < TB * TB; e += 64)
+        A[(int64_t)(r0 + e / TB) * nsp + s0 + e % TB] = Lr[e / TB][e % TB];
+    for (int e = lane; e < TB * TB; e += 64)  // mirror into the upper triangle
+        A[(int64_t)(s0 + e / TB) * nsp + r0 + e % TB] = Lr[e % TB][e / TB];
 }
 
 // L^T x = y (y already in xg from the folded forward substitution).
 constexpr int SOLVE_THREADS = 512;
 constexpr int SOLVE_MAX = 4096;
 
+template <int TB>
 __global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(double *__restrict__ A, int32_t nsp,
                                                                   double *__restrict__ xg,
                                                                   const double *__restrict__ Dlast, const int *__restrict__ gate) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
     __shared__ double x[SOLVE_MAX];
-    __shared__ double yt[NB];
+    __shared__ double yt[TB];
     const int t = threadIdx.x, lane = t & 63;
-    const int nT = nsp / NB;
+    const int nT = nsp / TB;
     for (int i = t; i < nsp; i += SOLVE_THREADS) x[i] = xg[i];
     if (Dlast) {  // the last diagonal factor is still in the step kernel's scratch
-        const int k0 = nsp - NB;
-        for (int e = t; e < NB * NB; e += SOLVE_THREADS) {
-            const int i = e / NB, j = e % NB;
-            A[(int64_t)(k0 + i) * nsp + k0 + j] = i >= j ? Dlast[i * NB + j] : Dlast[j * NB + i];
+        const int k0 = nsp - TB;
+        for (int e = t; e < TB * TB; e += SOLVE_THREADS) {
+            const int i = e / TB, j = e % TB;
+            A[(int64_t)(k0 + i) * nsp + k0 + j] = i >= j ? Dlast[i * TB + j] : Dlast[j * TB + i];
         }
     }
     __syncthreads();
     for (int kt = nT - 1; kt >= 0; --kt) {
-        const int k0 = kt * NB;
+        const int k0 = kt * TB;
         // L rows of this step for this thread's first column, issued before the
         // diagonal solve they do not depend on (one load round per step)
-        double lpre[NB];
+        double lpre[TB];
         const bool pre = t < k0;
 #pragma unroll
-        for (int m = 0; m < NB; ++m) lpre[m] = pre ? A[(int64_t)(k0 + m) * nsp + t] : 0.0;
+        for (int m = 0; m < TB; ++m) lpre[m] = pre ? A[(int64_t)(k0 + m) * nsp + t] : 0.0;
         if (t < 64) {
-            const int li = lane < NB ? lane : NB - 1;
-            double cl[NB];  // cl[m] = L[k0+m][k0+li]
+            const int li = lane < TB ? lane : TB - 1;
+            double cl[TB];  // cl[m] = L[k0+m][k0+li]
 #pragma unroll
-            for (int m = 0; m < NB; ++m) cl[m] = A[(int64_t)(k0 + m) * nsp + k0 + li];
+            for (int m = 0; m < TB; ++m) cl[m] = A[(int64_t)(k0 + m) * nsp + k0 + li];
             double v = x[k0 + li];
 #pragma unroll
-            for (int j = NB - 1; j >= 0; --j) {
+            for (int j = TB - 1; j >= 0; --j) {
                 const double vj = readlane_f64(v, j) / readlane_f64(cl[j], j);
                 if (lane == j) v = vj;
                 if (lane < j) v -= cl[j] * vj;
             }
-            if (lane < NB) { x[k0 + lane] = v; yt[lane] = v; }
+            if (lane < TB) { x[k0 + lane] = v; yt[lane] = v; }
         }
         __syncthreads();
         if (pre) {
             double s = 0;
 #pragma unroll
-            for (int m = 0; m < NB; ++m) s += lpre[m] * yt[m];  // L[k0+m][t]
+            for (int m = 0; m < TB; ++m) s += lpre[m] * yt[m];  // L[k0+m][t]
             x[t] -= s;
         }
         for (int i = t + SOLVE_THREADS; i < k0; i += SOLVE_THREADS) {
             double s = 0;
 #pragma unroll 8
-            for (int m = 0; m < NB; ++m) s += A[(int64_t)(k0 + m) * nsp + i] * yt[m];  // L[k0+m][i]
+            for (int m = 0; m < TB; ++m) s += A[(int64_t)(k0 + m) * nsp + i] * yt[m];  // L[k0+m][i]
             x[i] -= s;
         }
         __syncthreads();
@@ -833,20 +844,40 @@ static int lanes_per_point(const char *env, int dflt) {
 }
 
 // Factor + forward solve (nT launches of k_chol_col) and backward solve of
-// the padded reduced camera system; A, b on the device, D = 2 NB^2 scratch.
-static int launch_cholesky(double *A, int32_t nsp, double *b, double *D, int *bad, hipStream_t s,
-                           const int *gate = nullptr) {
-    const int nT = nsp / NB;
+// the padded reduced camera system with tiles of tb (16 or 32) columns; A, b
+// on the device, D = 2 tb^2 scratch; nsp a multiple of tb.
+template <int TB>
+static int launch_cholesky_t(double *A, int32_t nsp, double *b, double *D, int *bad, hipStream_t s,
+                             const int *gate) {
+    const int nT = nsp / TB;
     for (int st = 0; st < nT; ++st) {
         const int T = nT - st;
-        hipLaunchKernelGGL(k_chol_col, dim3(T * (T + 1) / 2 + (st >= 1 ? 1 : 0)), dim3(256), 0, s, A, nsp, st, D, b,
-                           bad, gate);
+        hipLaunchKernelGGL(k_chol_col<TB>, dim3(T * (T + 1) / 2 + (st >= 1 ? 1 : 0)), dim3(256), 0, s, A, nsp, st, D,
+                           b, bad, gate);
         SFM_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(SOLVE_THREADS), 0, s, A, nsp, b, D + ((nT - 1) & 1) * NB * NB,
-                       gate);
+    hipLaunchKernelGGL(k_chol_backsolve<TB>, dim3(1), dim3(SOLVE_THREADS), 0, s, A, nsp, b,
+                       D + ((nT - 1) & 1) * TB * TB, gate);
     SFM_HIP(hipGetLastError());
     return 0;
+}
+
+static int launch_cholesky(double *A, int32_t nsp, double *b, double *D, int *bad, hipStream_t s, int tb,
+                           const int *gate = nullptr) {
+    return tb == 32 ? launch_cholesky_t<32>(A, nsp, b, D, bad, s, gate)
+                    : launch_cholesky_t<16>(A, nsp, b, D, bad, s, gate);
+}
+
+// Cholesky tile width (env SFM_CHOL_TILE = 32 for experiments).  Measured
+// on MI355X at ns = 300: 16 -> 0.167 ms, 32 -> 0.267 ms; each launch is bound
+// by its column's serial factor + TRSM chain, which grows as tb^2, not by the
+// launch count.
+static int chol_tile(int64_t) {
+    if (const char *e = std::getenv("SFM_CHOL_TILE")) {
+        const int v = std::atoi(e);
+        if (v == 16 || v == 32) return v;
+    }
+    return 16;
 }
 
 // one workgroup: trial cameras + camera part of model decrease / norms.
@@ -1032,7 +1063,7 @@ struct sfm_ba_problem {
     int device = 0;
     hipStream_t stream = nullptr;
     sfm_comm *comm = nullptr;
-    int32_t nc = 0, ns = 0, nsp = 0, nT = 0;
+    int32_t nc = 0, ns = 0, nsp = 0, nT = 0, tb = 16;
     int64_t np = 0, no = 0, npairs = 0;
     int32_t nitems = 0, nblocks = 0, ndiag_items = 0, ndiag_blocks = 0;
     Kmat K;
@@ -1175,8 +1206,9 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     p->np = np_;
     p->no = no;
     p->ns = 6 * nc;
-    p->nT = (p->ns + NB - 1) / NB;
-    p->nsp = p->nT * NB;
+    p->tb = chol_tile(p->ns);
+    p->nT = (p->ns + p->tb - 1) / p->tb;
+    p->nsp = p->nT * p->tb;
     std::memcpy(p->K.k, K, sizeof p->K.k);
     p->cams0.assign(cams, cams + 6 * (size_t)nc);
     p->pts0.assign(pts, pts + 3 * (size_t)np_);
@@ -1265,7 +1297,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = p->alloc(p->d_J, (int64_t)JS * no)) || (rc = p->alloc(p->d_Vg, 9 * np_)) || (rc = p->alloc(p->d_Lq, 9 * np_)) ||
         (rc = p->alloc(p->d_Z, (int64_t)ZS * no)) || (rc = p->alloc(p->d_payload, p->payload_len + 8)) ||
         (rc = p->alloc(p->d_A, (int64_t)p->nsp * p->nsp)) || (rc = p->alloc(p->d_b, p->nsp)) ||
-        (rc = p->alloc(p->d_D, 2 * NB * NB)) ||
+        (rc = p->alloc(p->d_D, 2 * 32 * 32)) ||
         (rc = p->alloc(p->d_partial, 4 * (int64_t)p->pt_blocks)) || (rc = p->alloc(p->d_scal, 16)) ||
         (rc = p->alloc(p->d_lm, 1)) ||
         (rc = p->alloc(p->d_bad, 4)))
@@ -1410,7 +1442,7 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev) {
     hipLaunchKernelGGL(k_assemble, dim3(ceil_div(nA, 256)), dim3(256), 0, s, p->ns, p->nsp, p->d_payload, lam,
                        p->d_A, p->d_b, gst);
     SFM_HIP(hipGetLastError());
-    if ((rc = launch_cholesky(p->d_A, p->nsp, p->d_b, p->d_D, p->d_bad, s, gst))) return rc;
+    if ((rc = launch_cholesky(p->d_A, p->nsp, p->d_b, p->d_D, p->d_bad, s, p->tb, gst))) return rc;
     SFM_HIP(hipGetLastError());
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SOLVE + 1], s));
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_TRIAL], s));

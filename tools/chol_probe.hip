@@ -6,8 +6,8 @@
 #include <random>
 #include <vector>
 
-static int run(int ns, int reps) {
-    const int nT = (ns + NB - 1) / NB, nsp = nT * NB;
+static int run(int ns, int reps, int tb) {
+    const int nT = (ns + tb - 1) / tb, nsp = nT * tb;
     std::mt19937_64 g(ns);
     std::normal_distribution<double> nd;
     std::vector<double> M((size_t)nsp * (nsp + 8)), S((size_t)nsp * nsp, 0.0), b(nsp);
@@ -45,7 +45,7 @@ static int run(int ns, int reps) {
     double *dA, *dA0, *db, *db0;
     int *dbad;
     double *dD;
-    hipMalloc(&dD, 2 * NB * NB * 8);
+    hipMalloc(&dD, 2 * 32 * 32 * 8);
     hipMalloc(&dA, S.size() * 8); hipMalloc(&dA0, S.size() * 8);
     hipMalloc(&db, nsp * 8); hipMalloc(&db0, nsp * 8);
     hipMalloc(&dbad, 4); hipMemset(dbad, 0, 4);
@@ -58,7 +58,7 @@ static int run(int ns, int reps) {
         hipMemcpy(dA, dA0, S.size() * 8, hipMemcpyDeviceToDevice);
         hipMemcpy(db, db0, nsp * 8, hipMemcpyDeviceToDevice);
         hipEventRecord(e0, 0);
-        launch_cholesky(dA, nsp, db, dD, dbad, 0);
+        launch_cholesky(dA, nsp, db, dD, dbad, 0, tb);
         hipEventRecord(e1, 0);
         hipEventSynchronize(e1);
         float ms;
@@ -81,7 +81,7 @@ static int run(int ns, int reps) {
         ex = std::max(ex, std::isfinite(xo[i]) ? fabs(xo[i] - x[i]) : 1e300);
         sx = std::max(sx, fabs(x[i]));
     }
-    printf("ns=%d nsp=%d bad=%d maxerr_L=%.3e at (%d,%d) maxerr_x=%.3e (|x|max %.3e) best_ms=%.4f\n", ns, nsp, bad, eL,
+    printf("tb=%d ns=%d nsp=%d bad=%d maxerr_L=%.3e at (%d,%d) maxerr_x=%.3e (|x|max %.3e) best_ms=%.4f\n", tb, ns, nsp, bad, eL,
            worst_i, worst_j, ex, sx, best);
     return (bad == 0 && eL < 1e-8 && ex < 1e-6 * (1 + sx)) ? 0 : 1;
 }
@@ -89,7 +89,8 @@ static int run(int ns, int reps) {
 int main(int argc, char **argv) {
     int fails = 0;
     for (int ns : {48, 128, 256, 272, 300, 512, 1200}) {
-        fails += run(ns, ns > 600 ? 5 : 20);
+        fails += run(ns, ns > 600 ? 5 : 20, 16);
+        fails += run(ns, ns > 600 ? 5 : 20, 32);
     }
     printf("%s\n", fails ? "FAIL" : "OK");
     return fails;
