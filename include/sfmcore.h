@@ -215,6 +215,11 @@ int sfm_ba_download(sfm_ba_problem *p, double *cam_params, double *points);
 /* average device time per LM iteration of each kernel family over the
  * last solve (ms): names are written ';'-separated into `names`. */
 int sfm_ba_kernel_times(sfm_ba_problem *p, double *ms, int n, char *names, int names_len);
+/* Diagnostic: x = S^-1 rhs for an SPD n x n S (row-major) with the reduced
+ * camera system solver of sfm_ba_solve (the scipy 'lm' reference solves the
+ * same normal equations inside least_squares, BundleAdjustment.py:205-213).
+ * SFM_ERR_SOLVE if a pivot is not positive. */
+int sfm_reduced_solve(const double *S, const double *rhs, int32_t n, double *x, int device);
 int sfm_ba_destroy(sfm_ba_problem *p);
 
 /* single-process multi-GPU BA: points split over `devices` (n_ranks

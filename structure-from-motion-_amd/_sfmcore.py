@@ -74,6 +74,7 @@ SIGNATURES = [
     ("sfm_triangulate_dlt", _c, [_d, _d, _d, _d, _i, _d, _c]),
     ("sfm_triangulate_nonlinear", _c, [_d, _d, _d, _d, _d, _i, ctypes.c_int32, _d, _i32, _c]),
     ("sfm_project_points", _c, [_d, _d, _i, _d, _c]),
+    ("sfm_reduced_solve", _c, [_d, _d, ctypes.c_int32, _d, _c]),
     ("sfm_ba_residuals", _c, [ctypes.c_int32, _i, _i, _i32, _i32, _d, _d, _d, _d, _d, _c]),
     ("sfm_ba_lm", _c, [ctypes.c_int32, _i, _i, _i32, _i32, _d, _d, _d, _d, ctypes.POINTER(BAOpts),
                        ctypes.POINTER(BAReport), _c]),
@@ -295,6 +296,20 @@ def triangulate_nonlinear(P1, P2, x1, x2, X0, max_nfev=50):
     _check(_lib.sfm_triangulate_nonlinear(_p(P1), _p(P2), _p(x1), _p(x2), _p(X0), len(x1), int(max_nfev), _p(X),
                                           _p(info, _i32), DEVICE))
     return X, info
+
+
+def reduced_solve(S, rhs):
+    """Diagnostic: x = S^-1 rhs with the bundle adjuster's reduced-camera
+    solver (k_assemble + tiled Cholesky + substitutions)."""
+    require_device()
+    S = _f64(np.asarray(S))
+    rhs = _f64(np.asarray(rhs).reshape(-1))
+    n = len(rhs)
+    if S.shape != (n, n):
+        raise ValueError("S must be n x n")
+    x = np.zeros(n)
+    _check(_lib.sfm_reduced_solve(_p(S), _p(rhs), n, _p(x), DEVICE))
+    return x
 
 
 def project(P, X):

@@ -66,7 +66,6 @@ struct sfm_comm {
 
 namespace sfm {
 
-constexpr int NB = 16;            // Cholesky tile
 constexpr int PT_THREADS = 128;   // per-point kernels
 constexpr int PT_GROUP = 8;       // max lanes per point in k_linearize / k_backsub_trial
 
@@ -577,7 +576,6 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
     __shared__ double Lr[TB][TB + 1], Lc[TB][TB + 1], Ct[TB][TB + 1], Cd[TB][TB + 1];
     __shared__ double yk[TB];
     const int t = threadIdx.x;
-    const int nT = nsp / TB;
     const bool upd = s >= 1;
     const int kp = (s - 1) * TB;  // previous column's first index
     int blk = blockIdx.x;
@@ -700,7 +698,12 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
         A[(int64_t)(s0 + e / TB) * nsp + r0 + e % TB] = Lr[e % TB][e / TB];
 }
 
-// L^T x = y (y already in xg from the folded forward substitution).
+// L^T x = y (y already in xg from the folded forward substitution), one
+// workgroup, tile rows from the bottom.  Per step the serial part is one
+// wave's 16-deep triangular solve on the diagonal tile; everything it waits
+// on is fetched one step ahead (the next diagonal tile and this thread's L
+// rows of the next step), and the pivots enter as reciprocals computed off
+// the chain, so the chain is readlane -> mul -> fma per column.
 constexpr int SOLVE_THREADS = 512;
 constexpr int SOLVE_MAX = 4096;
 
@@ -713,6 +716,7 @@ __global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(double *__rest
     __shared__ double yt[TB];
     const int t = threadIdx.x, lane = t & 63;
     const int nT = nsp / TB;
+    const int li = lane < TB ? lane : TB - 1;
     for (int i = t; i < nsp; i += SOLVE_THREADS) x[i] = xg[i];
     if (Dlast) {  // the last diagonal factor is still in the step kernel's scratch
         const int k0 = nsp - TB;
@@ -722,42 +726,56 @@ __global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(double *__rest
         }
     }
     __syncthreads();
+    // step nT-1 operands
+    double lpre[TB], cl[TB];  // lpre[m] = L[k0+m][t]; cl[m] = L[k0+m][k0+li] (wave 0)
+    {
+        const int k0 = (nT - 1) * TB;
+#pragma unroll
+        for (int m = 0; m < TB; ++m) {
+            lpre[m] = t < k0 ? A[(int64_t)(k0 + m) * nsp + t] : 0.0;
+            cl[m] = t < 64 ? A[(int64_t)(k0 + m) * nsp + k0 + li] : 0.0;
+        }
+    }
     for (int kt = nT - 1; kt >= 0; --kt) {
         const int k0 = kt * TB;
-        // L rows of this step for this thread's first column, issued before the
-        // diagonal solve they do not depend on (one load round per step)
-        double lpre[TB];
-        const bool pre = t < k0;
+        // next step's operands, in flight during this step
+        double lnx[TB], cnx[TB];
+        const int k1 = k0 - TB;
 #pragma unroll
-        for (int m = 0; m < TB; ++m) lpre[m] = pre ? A[(int64_t)(k0 + m) * nsp + t] : 0.0;
+        for (int m = 0; m < TB; ++m) {
+            lnx[m] = (kt > 0 && t < k1) ? A[(int64_t)(k1 + m) * nsp + t] : 0.0;
+            cnx[m] = (kt > 0 && t < 64) ? A[(int64_t)(k1 + m) * nsp + k1 + li] : 0.0;
+        }
         if (t < 64) {
-            const int li = lane < TB ? lane : TB - 1;
-            double cl[TB];  // cl[m] = L[k0+m][k0+li]
-#pragma unroll
-            for (int m = 0; m < TB; ++m) cl[m] = A[(int64_t)(k0 + m) * nsp + k0 + li];
+            const double rinv = 1.0 / cl[li];  // 1 / L[k0+li][k0+li], off the chain
             double v = x[k0 + li];
 #pragma unroll
             for (int j = TB - 1; j >= 0; --j) {
-                const double vj = readlane_f64(v, j) / readlane_f64(cl[j], j);
+                const double vj = readlane_f64(v, j) * readlane_f64(rinv, j);
                 if (lane == j) v = vj;
                 if (lane < j) v -= cl[j] * vj;
             }
             if (lane < TB) { x[k0 + lane] = v; yt[lane] = v; }
         }
         __syncthreads();
-        if (pre) {
-            double s = 0;
+        if (t < k0) {
+            double sacc = 0;
 #pragma unroll
-            for (int m = 0; m < TB; ++m) s += lpre[m] * yt[m];  // L[k0+m][t]
-            x[t] -= s;
+            for (int m = 0; m < TB; ++m) sacc += lpre[m] * yt[m];  // L[k0+m][t]
+            x[t] -= sacc;
         }
         for (int i = t + SOLVE_THREADS; i < k0; i += SOLVE_THREADS) {
-            double s = 0;
+            double sacc = 0;
 #pragma unroll 8
-            for (int m = 0; m < TB; ++m) s += A[(int64_t)(k0 + m) * nsp + i] * yt[m];  // L[k0+m][i]
-            x[i] -= s;
+            for (int m = 0; m < TB; ++m) sacc += A[(int64_t)(k0 + m) * nsp + i] * yt[m];  // L[k0+m][i]
+            x[i] -= sacc;
         }
         __syncthreads();
+#pragma unroll
+        for (int m = 0; m < TB; ++m) {
+            lpre[m] = lnx[m];
+            cl[m] = cnx[m];
+        }
     }
     for (int i = t; i < nsp; i += SOLVE_THREADS) xg[i] = x[i];
 }
@@ -878,6 +896,22 @@ static int chol_tile(int64_t) {
         if (v == 16 || v == 32) return v;
     }
     return 16;
+}
+
+// S + lambda diag(clamp(diag U)) x = b from the Schur payload (k_assemble +
+// tiled Cholesky); x -> b.
+//
+// Measured alternative, not kept: a single-workgroup solve (whole lower
+// triangle resident in one CU's registers + LDS, fp64 MFMA trailing updates,
+// one launch) ran 0.246 ms at ns = 300 against 0.167 ms here -- one CU's fp64
+// MFMA issue rate bounds its trailing updates and its per-tile factor chain
+// is as latency-bound as this path's.
+static int launch_reduced_solve(int32_t ns, int32_t nsp, const double *payload, const double *lam, double *A,
+                                double *b, double *D, int *bad, hipStream_t s, int tb, const int *gate) {
+    const int64_t nA = (int64_t)nsp * nsp;
+    hipLaunchKernelGGL(k_assemble, dim3(ceil_div(nA, 256)), dim3(256), 0, s, ns, nsp, payload, lam, A, b, gate);
+    SFM_HIP(hipGetLastError());
+    return launch_cholesky(A, nsp, b, D, bad, s, tb, gate);
 }
 
 // one workgroup: trial cameras + camera part of model decrease / norms.
@@ -1438,12 +1472,9 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev) {
     if ((rc = allreduce(p, p->d_payload, p->payload_len - 1))) return rc;
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_COMM + 1], s));
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SOLVE], s));
-    const int64_t nA = (int64_t)p->nsp * p->nsp;
-    hipLaunchKernelGGL(k_assemble, dim3(ceil_div(nA, 256)), dim3(256), 0, s, p->ns, p->nsp, p->d_payload, lam,
-                       p->d_A, p->d_b, gst);
-    SFM_HIP(hipGetLastError());
-    if ((rc = launch_cholesky(p->d_A, p->nsp, p->d_b, p->d_D, p->d_bad, s, p->tb, gst))) return rc;
-    SFM_HIP(hipGetLastError());
+    if ((rc = launch_reduced_solve(p->ns, p->nsp, p->d_payload, lam, p->d_A, p->d_b, p->d_D, p->d_bad, s, p->tb,
+                                   gst)))
+        return rc;
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SOLVE + 1], s));
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_TRIAL], s));
     hipLaunchKernelGGL(k_camera_trial, dim3(1), dim3(256), 0, s, p->nc, p->d_b, p->d_payload, p->ns, lam, p->d_Rt,
@@ -1525,6 +1556,44 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
         rep->cost = h.cost;
         rep->t_loop_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
         rep->lambda = h.lambda;
+    }
+    return 0;
+}
+
+// Diagnostic entry: solves the SPD system S x = rhs (n x n, row-major) with
+// the reduced-camera solver of sfm_ba_solve (k_assemble + tiled Cholesky).
+extern "C" int sfm_reduced_solve(const double *S, const double *rhs, int32_t n, double *x, int device) {
+    SFM_CHECK_ARG(S && rhs && x, "null pointer");
+    SFM_CHECK_ARG(n >= 1, "n < 1");
+    ThreadCtx *c = thread_ctx(device);
+    if (!c) return SFM_ERR_HIP;
+    const int tb = chol_tile(n);
+    const int32_t nsp = (n + tb - 1) / tb * tb;
+    const size_t nn = (size_t)n * n;
+    int rc;
+    if ((rc = c->buf[0].reserve((nn + 3 * (size_t)n + 1) * sizeof(double))) ||
+        (rc = c->buf[1].reserve((size_t)nsp * nsp * sizeof(double))) ||
+        (rc = c->buf[2].reserve((size_t)nsp * sizeof(double))) ||
+        (rc = c->buf[3].reserve(2 * 32 * 32 * sizeof(double))) || (rc = c->buf[4].reserve(sizeof(int))))
+        return rc;
+    // payload = [S, diag U = 0, g = -rhs, sum Z q = 0], lambda = 0 (last slot)
+    std::vector<double> pay(nn + 3 * (size_t)n + 1, 0.0);
+    std::memcpy(pay.data(), S, nn * sizeof(double));
+    for (int32_t i = 0; i < n; ++i) pay[nn + n + i] = -rhs[i];
+    double *d_pay = c->buf[0].as<double>();
+    SFM_HIP(hipMemcpyAsync(d_pay, pay.data(), pay.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    SFM_HIP(hipMemsetAsync(c->buf[4].p, 0, sizeof(int), c->stream));
+    if ((rc = launch_reduced_solve(n, nsp, d_pay, d_pay + nn + 3 * (size_t)n, c->buf[1].as<double>(),
+                                   c->buf[2].as<double>(), c->buf[3].as<double>(), c->buf[4].as<int>(), c->stream,
+                                   tb, nullptr)))
+        return rc;
+    int bad = 0;
+    SFM_HIP(hipMemcpyAsync(x, c->buf[2].p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    SFM_HIP(hipMemcpyAsync(&bad, c->buf[4].p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    SFM_HIP(hipStreamSynchronize(c->stream));
+    if (bad) {
+        set_error("reduced camera system not positive definite");
+        return SFM_ERR_SOLVE;
     }
     return 0;
 }
