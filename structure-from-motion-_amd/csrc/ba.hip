@@ -12,9 +12,10 @@
 //                    L = C^-T (so Vd^-1 = L L^T), q = L^T g_p,
 //                    Z_o = (Jc^T Jp)_o L per observation.
 //   k_camera_lin     (after linearize) workgroup per camera: U_c, g_c.
-//   k_schur_pairs    S_ij = U_i [i==j] - sum_p Z_pi Z_pj^T from static
-//                    co-observation pair lists, sliced into work items;
-//   k_schur_finish   fixed-order sum of the items of each camera block ->
+//   k_schur_sweep    S_ij = U_i [i==j] - sum_p Z_pi Z_pj^T: workgroups own
+//                    camera-block rows and sweep XCD-local point ranges
+//                    (a records staged in LDS, b records from L2);
+//   k_schur_finish   fixed-order sum of the ranges of each camera block ->
 //                    deterministic, no atomics.
 //   [RCCL all-reduce of the packed partial system across ranks]
 //   k_assemble       S += lambda*clamp(diag U), b = -g_c + sum Z q, padded.
@@ -116,7 +117,7 @@ __device__ __forceinline__ void block_sum_store(double (&v)[NV], double *out) {
 //   W  = Jc^T Jp = E (A^T A R),  E = [[p]x ; I]  (6x3)
 // so the J cache stores only r, A, p: 96 B per observation instead of 160.
 constexpr int JS = 12;  // r0 r1 | A row0 (3) | A row1 (3) | p (3) | pad
-constexpr int ZS = 16;  // Schur record: p (3) | G = A^T A R L (9, row-major) | pad -> one 128-B line
+constexpr int ZS = 16;  // Schur record: p (3) | G = A^T A R L (9, row-major) | q = L^T g_p (3) | pad: one 128-B line
 
 __device__ __forceinline__ void obs_model(const double *__restrict__ Rt, const double *X, const double (&K)[9],
                                           double2 ob, double (&r)[2], double (&A)[2][3], double (&p)[3]) {
@@ -231,7 +232,9 @@ __global__ void __launch_bounds__(PT_THREADS) k_linearize(int64_t np_, const int
 }
 
 // Lq layout per point (9 doubles): L00 L01 L02 L11 L12 L22 | q0 q1 q2
-// Z_o = W_o L = E_o G_o with G_o = A^T (A R L): the Schur record is (p, G).
+// Z_o = W_o L = E_o G_o with G_o = A^T (A R L): the Schur record is (p, G, q),
+// q = L^T g_p repeated in every record of the point (k_schur_sweep's
+// diagonal term reads it from the staged record).
 // Thread per OBSERVATION (a thread per point leaves ~1.5 waves per SIMD at
 // cfg4 walking k observations serially): each thread rebuilds its point's
 // 3x3 factor from V (72 B, shared in cache by the point's k threads -- the
@@ -264,13 +267,12 @@ __global__ void __launch_bounds__(OBS_THREADS) k_point_prep(int64_t no, const in
     const double i20 = -(c20 * i00 + c21 * i10) * i22;
     // L = Cinv^T (upper): Vd^-1 = L L^T
     const double L[3][3] = {{i00, i10, i20}, {0.0, i11, i21}, {0.0, 0.0, i22}};
+    const double g0 = vg[6], g1 = vg[7], g2 = vg[8];
+    const double qp[3] = {L[0][0] * g0, L[0][1] * g0 + L[1][1] * g1, L[0][2] * g0 + L[1][2] * g1 + L[2][2] * g2};
     if (o == pstart[p]) {
-        const double g0 = vg[6], g1 = vg[7], g2 = vg[8];
         double *lq = Lq + 9 * p;
         lq[0] = L[0][0]; lq[1] = L[0][1]; lq[2] = L[0][2]; lq[3] = L[1][1]; lq[4] = L[1][2]; lq[5] = L[2][2];
-        lq[6] = L[0][0] * g0;
-        lq[7] = L[0][1] * g0 + L[1][1] * g1;
-        lq[8] = L[0][2] * g0 + L[1][2] * g1 + L[2][2] * g2;
+        lq[6] = qp[0]; lq[7] = qp[1]; lq[8] = qp[2];
     }
     double r[2], A[2][3], q[3];
     load_j(J + (int64_t)JS * o, r, A, q);
@@ -290,31 +292,78 @@ __global__ void __launch_bounds__(OBS_THREADS) k_point_prep(int64_t no, const in
     for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int c = 0; c < 3; ++c) z[3 + 3 * i + c] = A[0][i] * T[0][c] + A[1][i] * T[1][c];
+    z[12] = qp[0]; z[13] = qp[1]; z[14] = qp[2]; z[15] = 0.0;
 }
 
 // Payload layout (doubles): S[ns*ns] | diagU[ns] | gc[ns] | bZ[ns] | cost
 constexpr int CAMLIN = 27;  // U_c (21, upper) | g_c (6)
-
-// Reduced camera system S_ij = [i==j](U_i) - sum_{p seen by i and j} Z_pi Z_pj^T.
-// Static pair lists (a, b) grouped by camera block (i <= j); a work item
-// is a slice of <= PAIR_CHUNK pairs of one block, so the large diagonal
-// blocks do not form a tail.  Each item writes its partial 6x6 block (+ the
-// diagonal block's sum Z_a q_p) to a slab; k_schur_finish sums the items of
-// a block in item order: deterministic, no atomics.  Z is the only large
-// array read here (144 B / observation), so with the pair list it stays
-// resident in the 256 MiB Infinity Cache at the BASELINE sizes.
-constexpr int PAIR_CHUNK = 4096;
-constexpr int PAIR_THREADS = 256;
 constexpr int ITEM_W = 42;  // 36 block + 6 bZ
+
+// Camera items: a camera's observations (camera-major list) cut into chunks
+// of <= CAM_CHUNK; BlockInfo groups the items of one camera.
+constexpr int CAM_CHUNK = 4096;
 
 struct PairItem {
     int32_t blk, k0, k1, diag;
 };
 
-// Two lanes per pair: lane parity h computes rows 3h..3h+2 of the 6x6
-// block S_ab = E_a (G_a G_b^T) E_b^T (E = [[p]x; I]): h = 0 the rotation
-// rows ([p_a]x H), h = 1 the translation rows (H).  Each pair reads two
-// 128-B records (one cache line each); the two lanes' loads coalesce.
+struct BlockInfo {
+    int32_t i, j, first_item, last_item;
+};
+
+// ---------------------------------------------------------------------
+// Reduced camera system S_ij = [i==j] U_i - sum_{p seen by i and j} Z_pi Z_pj^T
+// as a sweep over point ranges (the Schur record of an observation is
+// (p, G, q): Z = E G with E = [[p]x; I], q = L^T g_p; pair term
+// S_ab = E_a (G_a G_b^T) E_b^T).
+//
+// The points (with their observations, point-major) are cut into NR
+// ranges of equal observation count and every range into chunks whose
+// records fit an XCD's L2.  A workgroup owns a fixed set of camera-block
+// rows (a "spec": cameras i and nc-1-i, so every spec has the same pair
+// work) and sweeps one range chunk by chunk:
+//   * the chunk's records of the spec's own cameras (the "a" side of every
+//     pair) are staged in LDS by LDS-DMA, double-buffered one chunk ahead;
+//   * every block (i, j) of the spec is owned by one lane group (2 lanes
+//     per pair slot, group size proportional to the block's pair count)
+//     that accumulates its 6x6 block in registers over the whole range;
+//     the "b" records are gathered from global memory -- the range's
+//     workgroups all run on one XCD (blockIdx % 8) and walk the same
+//     chunks at the same pace, so those gathers hit that XCD's L2;
+//   * at the end every group reduces its slots (fixed butterfly) and writes
+//     its block to slab[range][block]; k_schur_finish sums the ranges in
+//     order.  Deterministic, no atomics.
+// Compared with one gather of both records per pair from a pair list sorted
+// by camera block, the a side comes from LDS and the b side from L2.
+constexpr int SW_THREADS = 768;
+constexpr int SW_MAX_STAGED = 512;  // records per (chunk, spec): 2 x 64 KiB of LDS
+constexpr int SW_MAX_COLS = SW_THREADS / 2 - 32;  // blocks per spec (2 lanes each, one loader wave)
+constexpr int NXCD = 8;
+
+struct SweepGroup {
+    int32_t blk, lane_base, G, flags;  // flags: 1 = diagonal block, 2 = a side is the spec's second camera
+};
+
+// record piece k (16 B) of staged slot s, XOR-swizzled against bank conflicts
+__device__ __forceinline__ double2 lds_piece(const double2 *buf, int s, int k) { return buf[s * 8 + (k ^ (s & 7))]; }
+
+__device__ __forceinline__ void load_rec_lds(const double2 *buf, int s, double (&p)[3], double (&G)[3][3]) {
+    const double2 v0 = lds_piece(buf, s, 0), v1 = lds_piece(buf, s, 1), v2 = lds_piece(buf, s, 2);
+    const double2 v3 = lds_piece(buf, s, 3), v4 = lds_piece(buf, s, 4), v5 = lds_piece(buf, s, 5);
+    p[0] = v0.x; p[1] = v0.y; p[2] = v1.x;
+    G[0][0] = v1.y; G[0][1] = v2.x; G[0][2] = v2.y;
+    G[1][0] = v3.x; G[1][1] = v3.y; G[1][2] = v4.x;
+    G[2][0] = v4.y; G[2][1] = v5.x; G[2][2] = v5.y;
+}
+
+__device__ __forceinline__ void load_rec_glb(const double2 *__restrict__ z, double (&p)[3], double (&G)[3][3]) {
+    const double2 v0 = z[0], v1 = z[1], v2 = z[2], v3 = z[3], v4 = z[4], v5 = z[5];
+    p[0] = v0.x; p[1] = v0.y; p[2] = v1.x;
+    G[0][0] = v1.y; G[0][1] = v2.x; G[0][2] = v2.y;
+    G[1][0] = v3.x; G[1][1] = v3.y; G[1][2] = v4.x;
+    G[2][0] = v4.y; G[2][1] = v5.x; G[2][2] = v5.y;
+}
+
 __device__ __forceinline__ void cross_rows(const double (&p)[3], const double (&H)[3][3], double (&X)[3][3]) {
     // X = [p]x H, [p]x = [[0,-p2,p1],[p2,0,-p0],[-p1,p0,0]]
 #pragma unroll
@@ -325,95 +374,213 @@ __device__ __forceinline__ void cross_rows(const double (&p)[3], const double (&
     }
 }
 
-__global__ void __launch_bounds__(PAIR_THREADS) k_schur_pairs(const PairItem *__restrict__ items,
-                                                              const int2 *__restrict__ pairs,
-                                                              const int32_t *__restrict__ pt,
-                                                              const double *__restrict__ Z,
-                                                              const double *__restrict__ Lq,
-                                                              double *__restrict__ slab, const int *__restrict__ gate) {
-    if (gate && !*gate) return;  // device-side LM control: iteration gated off
-    __shared__ double red[PAIR_THREADS / 64][ITEM_W];
-    const PairItem it = items[blockIdx.x];
-    const int h = threadIdx.x & 1;
-    double acc[21];
+// rows 3h..3h+2 of S_ab = E_a (G_a G_b^T) E_b^T into acc[0..18)
+__device__ __forceinline__ void pair_block(int h, const double (&pa)[3], const double (&Ga)[3][3],
+                                           const double (&pb)[3], const double (&Gb)[3][3], double (&acc)[21]) {
+    double H[3][3];  // G_a G_b^T
 #pragma unroll
-    for (int k = 0; k < 21; ++k) acc[k] = 0.0;
-    for (int32_t k = it.k0 + (threadIdx.x >> 1); k < it.k1; k += PAIR_THREADS / 2) {
-        const int2 pr = pairs[k];
-        const double *za = Z + (int64_t)ZS * pr.x;
-        const double *zb = Z + (int64_t)ZS * pr.y;
-        double pa[3], pb[3], Ga[3][3], Gb[3][3];
+    for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int i = 0; i < 3; ++i) { pa[i] = za[i]; pb[i] = zb[i]; }
+        for (int j = 0; j < 3; ++j) H[i][j] = Ga[i][0] * Gb[j][0] + Ga[i][1] * Gb[j][1] + Ga[i][2] * Gb[j][2];
+    double X[3][3];
+    if (h == 0) {
+        cross_rows(pa, H, X);
+    } else {
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) { Ga[i][c] = za[3 + 3 * i + c]; Gb[i][c] = zb[3 + 3 * i + c]; }
-        double H[3][3];  // G_a G_b^T
+            for (int j = 0; j < 3; ++j) X[i][j] = H[i][j];
+    }
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
+    for (int r = 0; r < 3; ++r) {  // row r of X E_b^T = [X [p_b]x^T | X]
+        acc[6 * r + 0] += -pb[2] * X[r][1] + pb[1] * X[r][2];
+        acc[6 * r + 1] += pb[2] * X[r][0] - pb[0] * X[r][2];
+        acc[6 * r + 2] += -pb[1] * X[r][0] + pb[0] * X[r][1];
+        acc[6 * r + 3] += X[r][0];
+        acc[6 * r + 4] += X[r][1];
+        acc[6 * r + 5] += X[r][2];
+    }
+}
+
+// Staging is done by LOADER waves: the waves that hold the diagonal groups
+// (those read only LDS), or one wave of their own when a spec has no
+// diagonal block.  vmcnt is per wave and counts LDS-DMA with ordinary loads
+// in issue order, so a wave gathering b records from global memory with
+// LDS-DMA in flight would wait for the whole staging at every use of its
+// prefetched record; the off-diagonal (gathering) waves never issue any.
+//
+// LDS per buffer (4-B words): records [buf_slots][32] | pairs [pair_cap] |
+// header [hdr_cap] (group pair offsets (ngroups + 1), n0, n1, chunk obs0) |
+// list [list_cap] (absolute record index of every staged slot).  Chunk q
+// uses buffer q & 1; its list is fetched one chunk earlier.
+struct SweepLds {
+    int buf_slots, pair_cap, hdr_cap, list_cap;
+    __device__ int words() const { return buf_slots * 32 + pair_cap + hdr_cap + list_cap; }
+};
+
+__device__ __forceinline__ void glds4(const void *src, void *lds) {
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void *)lds, 4, 0, 0);
+}
+
+// loader lanes (t < 64 nload): the list words of region qw
+__device__ __forceinline__ void sweep_fetch_list(int t, int nload, int64_t qw, const SweepLds &L,
+                                                 const int32_t *__restrict__ list, uint32_t *bufw) {
+    uint32_t *lw = bufw + L.buf_slots * 32 + L.pair_cap + L.hdr_cap;
+    for (int base = (t & ~63); base < L.list_cap; base += 64 * nload) glds4(list + qw * L.list_cap + base + (t & 63), lw + base);
+}
+
+// loader lanes: records (16-B pieces; swizzle applied on the global side,
+// LDS image linear), pairs and header of region qw; the list is in LDS
+__device__ __forceinline__ void sweep_fetch(int t, int nload, int64_t qw, const SweepLds &L,
+                                            const double *__restrict__ Z, const uint32_t *__restrict__ pairs,
+                                            const int32_t *__restrict__ hdr, uint32_t *bufw) {
+    const int lane = t & 63, step = 64 * nload;
+    const int32_t *lw = reinterpret_cast<const int32_t *>(bufw + L.buf_slots * 32 + L.pair_cap + L.hdr_cap);
+    const int npc = L.buf_slots * 8;
+    for (int base = (t & ~63); base < npc; base += 8 * step) {
+        int32_t rec[8];
 #pragma unroll
-            for (int j = 0; j < 3; ++j) H[i][j] = Ga[i][0] * Gb[j][0] + Ga[i][1] * Gb[j][1] + Ga[i][2] * Gb[j][2];
-        double X[3][3];
-        if (h == 0) {
-            cross_rows(pa, H, X);
-        } else {
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-#pragma unroll
-                for (int j = 0; j < 3; ++j) X[i][j] = H[i][j];
+        for (int u = 0; u < 8; ++u) {
+            const int idx = base + u * step + lane;
+            rec[u] = idx < npc ? lw[idx >> 3] : 0;
         }
 #pragma unroll
-        for (int r = 0; r < 3; ++r) {  // row r of X E_b^T = [X [p_b]x^T | X]
-            acc[6 * r + 0] += -pb[2] * X[r][1] + pb[1] * X[r][2];
-            acc[6 * r + 1] += pb[2] * X[r][0] - pb[0] * X[r][2];
-            acc[6 * r + 2] += -pb[1] * X[r][0] + pb[0] * X[r][1];
-            acc[6 * r + 3] += X[r][0];
-            acc[6 * r + 4] += X[r][1];
-            acc[6 * r + 5] += X[r][2];
-        }
-        if (it.diag) {  // sum Z_a q_p = E_a (G_a q)
-            const double *q = Lq + 9 * (int64_t)pt[pr.x] + 6;
-            double gq[3];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) gq[i] = Ga[i][0] * q[0] + Ga[i][1] * q[1] + Ga[i][2] * q[2];
-            if (h == 0) {
-                acc[18] += -pa[2] * gq[1] + pa[1] * gq[2];
-                acc[19] += pa[2] * gq[0] - pa[0] * gq[2];
-                acc[20] += -pa[1] * gq[0] + pa[0] * gq[1];
-            } else {
-                acc[18] += gq[0]; acc[19] += gq[1]; acc[20] += gq[2];
+        for (int u = 0; u < 8; ++u) {
+            const int b0 = base + u * step;
+            if (b0 < npc) {
+                const int idx = b0 + lane, s = idx >> 3, k = (idx & 7) ^ (s & 7);
+                __builtin_amdgcn_global_load_lds(Z + (int64_t)rec[u] * 16 + 2 * k,
+                                                 (__attribute__((address_space(3))) void *)(bufw + 4 * b0), 16, 0, 0);
             }
         }
     }
-    // lanes of equal parity hold the same outputs: reduce over the other 32
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t *pw = bufw + L.buf_slots * 32;
+    for (int base = (t & ~63); base < L.pair_cap; base += step) glds4(pairs + qw * L.pair_cap + base + lane, pw + base);
+    uint32_t *hw = pw + L.pair_cap;
+    for (int base = (t & ~63); base < L.hdr_cap; base += step) glds4(hdr + qw * L.hdr_cap + base + lane, hw + base);
+}
+
+__global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
+    int32_t nspec, int32_t nrange, int32_t nbd, SweepLds L, const int32_t *__restrict__ rchunk,
+    const int32_t *__restrict__ spec_nload,
+    const int32_t *__restrict__ spec_goff, const SweepGroup *__restrict__ groups, const int16_t *__restrict__ lanegrp,
+    const int32_t *__restrict__ list, const uint32_t *__restrict__ pairs, const int32_t *__restrict__ hdr,
+    const double *__restrict__ Z, double *__restrict__ slab, const int *__restrict__ gate, int dbg) {
+    if (gate && !*gate) return;  // device-side LM control: iteration gated off
+    extern __shared__ double2 sw_lds[];
+    uint32_t *ldsw = reinterpret_cast<uint32_t *>(sw_lds);
+    const int loc = blockIdx.x / NXCD;
+    const int w = loc % nspec, r = (loc / nspec) * NXCD + (int)(blockIdx.x % NXCD);
+    if (r >= nrange) return;  // whole workgroup
+    const int t = threadIdx.x;
+    const int nload = spec_nload[w];
+    const bool loader = (t >> 6) < nload;
+    const int gi = lanegrp[w * SW_THREADS + t];
+    const int ng = spec_goff[w + 1] - spec_goff[w];
+    SweepGroup grp = {0, 0, 2, 0};
+    if (gi >= 0) grp = groups[spec_goff[w] + gi];
+    const int h = (t - grp.lane_base) & 1, slot = (t - grp.lane_base) >> 1, nslot = grp.G >> 1;
+    const bool diag = grp.flags & 1, second = grp.flags & 2;
+    const int bw = L.words();
+    double acc[21];
+#pragma unroll
+    for (int k = 0; k < 21; ++k) acc[k] = 0.0;
+    const int q0 = rchunk[r], q1 = rchunk[r + 1];
+    if (loader && q0 < q1) sweep_fetch_list(t, nload, (int64_t)q0 * nspec + w, L, list, ldsw);
+    __syncthreads();
+    if (loader && q0 < q1) {
+        sweep_fetch(t, nload, (int64_t)q0 * nspec + w, L, Z, pairs, hdr, ldsw);
+        if (q0 + 1 < q1) sweep_fetch_list(t, nload, (int64_t)(q0 + 1) * nspec + w, L, list, ldsw + bw);
+    }
+    __syncthreads();
+    for (int q = q0; q < q1; ++q) {
+        const int cur = (q - q0) & 1;
+        const uint32_t *bufw = ldsw + cur * bw;
+        if (loader && q + 1 < q1 && !(dbg & 4)) {
+            sweep_fetch(t, nload, (int64_t)(q + 1) * nspec + w, L, Z, pairs, hdr, ldsw + (cur ^ 1) * bw);
+            if (q + 2 < q1) sweep_fetch_list(t, nload, (int64_t)(q + 2) * nspec + w, L, list, ldsw + cur * bw);
+        }
+        if (gi >= 0) {
+            const double2 *buf = reinterpret_cast<const double2 *>(bufw);
+            const uint32_t *pl = bufw + L.buf_slots * 32;
+            const int32_t *hd = reinterpret_cast<const int32_t *>(pl + L.pair_cap);
+            const int n0 = hd[ng + 1], n1 = hd[ng + 2];
+            if (diag) {  // S_ii: the camera's own records, b = a; plus sum Z_a q_p
+                const int a0 = second ? n0 : 0, a1 = (dbg & 2) ? a0 : second ? n0 + n1 : n0;
+                for (int a = a0 + slot; a < a1; a += nslot) {
+                    double pa[3], Ga[3][3];
+                    load_rec_lds(buf, a, pa, Ga);
+                    pair_block(h, pa, Ga, pa, Ga, acc);
+                    const double2 v6 = lds_piece(buf, a, 6), v7 = lds_piece(buf, a, 7);
+                    const double qv[3] = {v6.x, v6.y, v7.x};
+                    double gq[3];
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) gq[i] = Ga[i][0] * qv[0] + Ga[i][1] * qv[1] + Ga[i][2] * qv[2];
+                    if (h == 0) {
+                        acc[18] += -pa[2] * gq[1] + pa[1] * gq[2];
+                        acc[19] += pa[2] * gq[0] - pa[0] * gq[2];
+                        acc[20] += -pa[1] * gq[0] + pa[0] * gq[1];
+                    } else {
+                        acc[18] += gq[0]; acc[19] += gq[1]; acc[20] += gq[2];
+                    }
+                }
+            } else {
+                const int k0 = hd[gi], k1 = (dbg & 1) ? k0 : hd[gi + 1];
+                const double2 *zc = reinterpret_cast<const double2 *>(Z) + (int64_t)hd[ng + 3] * 8;
+                // b records prefetched one pair ahead (L2 latency off the
+                // chain), two register sets used alternately
+                int k = k0 + slot;
+                uint32_t pr0 = k < k1 ? pl[k] : 0u, pr1 = 0u;
+                double pb0[3] = {0, 0, 0}, Gb0[3][3] = {}, pb1[3] = {0, 0, 0}, Gb1[3][3] = {};
+                if (k < k1) load_rec_glb(zc + (int64_t)(pr0 & 0xffffu) * 8, pb0, Gb0);
+                for (; k < k1; k += 2 * nslot) {
+                    const int k1n = k + nslot, k2n = k + 2 * nslot;
+                    if (k1n < k1) {
+                        pr1 = pl[k1n];
+                        load_rec_glb(zc + (int64_t)(pr1 & 0xffffu) * 8, pb1, Gb1);
+                    }
+                    double pa[3], Ga[3][3];
+                    load_rec_lds(buf, (int)(pr0 >> 16), pa, Ga);
+                    pair_block(h, pa, Ga, pb0, Gb0, acc);
+                    if (k1n >= k1) break;
+                    if (k2n < k1) {
+                        pr0 = pl[k2n];
+                        load_rec_glb(zc + (int64_t)(pr0 & 0xffffu) * 8, pb0, Gb0);
+                    }
+                    load_rec_lds(buf, (int)(pr1 >> 16), pa, Ga);
+                    pair_block(h, pa, Ga, pb1, Gb1, acc);
+                }
+            }
+        }
+        __syncthreads();  // chunk q's buffer is free; chunk q+1's staging has landed
+    }
+    // reduce the group's slots (lanes of equal parity), fixed butterfly
 #pragma unroll
     for (int k = 0; k < 21; ++k) {
         double v = acc[k];
 #pragma unroll
-        for (int o = 32; o > 1; o >>= 1) v += __shfl_xor(v, o);
-        if (lane < 2) {
-            const int idx = k < 18 ? 18 * lane + k : 36 + 3 * lane + (k - 18);
-            red[w][idx] = v;
+        for (int o = 2; o < 64; o <<= 1) {
+            const double u = __shfl_xor(v, o);
+            if (o < grp.G) v += u;
         }
+        acc[k] = v;
     }
-    __syncthreads();
-    const int nv = it.diag ? ITEM_W : 36;
-    if ((int)threadIdx.x < nv) {
-        double v = 0;
+    if (gi >= 0 && slot == 0) {
+        double *out = slab + ((int64_t)r * nbd + grp.blk) * ITEM_W;
 #pragma unroll
-        for (int i = 0; i < PAIR_THREADS / 64; ++i) v += red[i][threadIdx.x];
-        slab[(int64_t)ITEM_W * blockIdx.x + threadIdx.x] = v;
+        for (int k = 0; k < 18; ++k) out[18 * h + k] = acc[k];
+        if (diag)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) out[36 + 3 * h + k] = acc[18 + k];
     }
 }
 
-// Camera blocks of the normal equations, once per linearisation: the
-// diagonal pair items are exactly chunks of one camera's observations, so
-// each item sums U = sum Jc^T Jc (21) and g = sum Jc^T r (6) over its chunk
-// and k_camera_lin_finish adds a camera's items in order (deterministic).
+// Camera blocks of the normal equations, once per linearisation: each item
+// sums U = sum Jc^T Jc (21) and g = sum Jc^T r (6) over a chunk of one
+// camera's observations and k_camera_lin_finish adds a camera's items in
+// order (deterministic).
 __global__ void __launch_bounds__(256) k_camera_lin(const PairItem *__restrict__ items,
-                                                    const int2 *__restrict__ pairs,
+                                                    const int32_t *__restrict__ cam_obs,
                                                     const double *__restrict__ J, double *__restrict__ slab2, const int *__restrict__ gate) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
     __shared__ double red[4][CAMLIN];
@@ -423,7 +590,7 @@ __global__ void __launch_bounds__(256) k_camera_lin(const PairItem *__restrict__
     for (int k = 0; k < CAMLIN; ++k) acc[k] = 0.0;
     for (int32_t k = it.k0 + threadIdx.x; k < it.k1; k += 256) {
         double rr[2], A[2][3], q[3], Jc[2][6];
-        load_j(J + (int64_t)JS * pairs[k].x, rr, A, q);
+        load_j(J + (int64_t)JS * cam_obs[k], rr, A, q);
         jc_of(A, q, Jc);
         const double r0 = rr[0], r1 = rr[1];
         double a[6], b[6];
@@ -449,40 +616,39 @@ __global__ void __launch_bounds__(256) k_camera_lin(const PairItem *__restrict__
             red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 
-// one 64-thread workgroup per camera block: fixed-order sum of its items
-struct BlockInfo {
-    int32_t i, j, first_item, last_item;
-};
-
+// one 64-thread workgroup per camera: fixed-order sum of its items
 __global__ void __launch_bounds__(64) k_camera_lin_finish(const BlockInfo *__restrict__ blocks,
                                                           const double *__restrict__ slab2,
                                                           double *__restrict__ camlin, const int *__restrict__ gate) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
-    const BlockInfo bi = blocks[blockIdx.x];  // diagonal blocks come first
+    const BlockInfo bi = blocks[blockIdx.x];
     if (threadIdx.x >= CAMLIN) return;
     double v = 0;
     for (int k = bi.first_item; k < bi.last_item; ++k) v += slab2[(int64_t)CAMLIN * k + threadIdx.x];
     camlin[CAMLIN * bi.i + threadIdx.x] = v;
 }
 
-__global__ void __launch_bounds__(64) k_schur_finish(int32_t ns, const BlockInfo *__restrict__ blocks,
-                                                     const double *__restrict__ slab,
+// one 64-thread workgroup per camera block (i <= j, dense upper-triangle
+// index): fixed-order sum over the ranges, then U_i - S (diagonal) / -S
+// (off-diagonal, mirrored), g_c and sum Z q into the payload
+__global__ void __launch_bounds__(64) k_schur_finish(int32_t ns, int32_t nbd, int32_t nrange,
+                                                     const int2 *__restrict__ blkij, const double *__restrict__ slab,
                                                      const double *__restrict__ camlin,
                                                      double *__restrict__ payload, const int *__restrict__ gate) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
-    const BlockInfo bi = blocks[blockIdx.x];
+    const int2 ij = blkij[blockIdx.x];
     const int t = threadIdx.x;
-    const bool diag = bi.i == bi.j;
+    const bool diag = ij.x == ij.y;
     if (t >= (diag ? ITEM_W : 36)) return;
     double v = 0;
-    for (int k = bi.first_item; k < bi.last_item; ++k) v += slab[(int64_t)ITEM_W * k + t];
+    for (int r = 0; r < nrange; ++r) v += slab[((int64_t)r * nbd + blockIdx.x) * ITEM_W + t];
     const int64_t base = (int64_t)ns * ns;
     if (t < 36) {
         const int r = t / 6, c = t % 6;
-        const int64_t row = 6 * bi.i + r, col = 6 * bi.j + c;
+        const int64_t row = 6 * ij.x + r, col = 6 * ij.y + c;
         if (diag) {
             const int lo = r < c ? r : c, hi = r < c ? c : r;
-            const double u = camlin[CAMLIN * bi.i + lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];
+            const double u = camlin[CAMLIN * ij.x + lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];
             payload[row * ns + col] = u - v;
             if (r == c) payload[base + row] = u;  // diag(U)
         } else {
@@ -491,8 +657,8 @@ __global__ void __launch_bounds__(64) k_schur_finish(int32_t ns, const BlockInfo
         }
     } else {
         const int r = t - 36;
-        payload[base + ns + 6 * bi.i + r] = camlin[CAMLIN * bi.i + 21 + r];  // g_c
-        payload[base + 2 * ns + 6 * bi.i + r] = v;                           // sum Z q
+        payload[base + ns + 6 * ij.x + r] = camlin[CAMLIN * ij.x + 21 + r];  // g_c
+        payload[base + 2 * ns + 6 * ij.x + r] = v;                           // sum Z q
     }
 }
 
@@ -1088,6 +1254,219 @@ static void h_R_to_rotvec(const double *R, double *w) {
 
 using namespace sfm;
 
+// ------------------------------------------------------ Schur sweep plan
+// Host-side construction of k_schur_sweep's static structure (DESIGN.md
+// section 4): ranges, chunks, specs (camera-row sets with their lane
+// groups) and, per (chunk, spec), fixed-capacity regions so that the
+// kernel computes every staging address without a dependent load: the
+// staged record indices, the pair list (a slot << 16 | b offset in chunk,
+// grouped by lane group, point order) and the header (group offsets, n0, n1,
+// chunk obs0).
+struct SweepPlan {
+    int32_t nrange = 0, nspec = 0, nbd = 0, buf_slots = 0, pair_cap = 0, hdr_cap = 0, list_cap = 0, nchunk = 0;
+    std::vector<int32_t> rchunk, goff, nload, list, hdr;
+    std::vector<SweepGroup> groups;
+    std::vector<int16_t> lanegrp;
+    std::vector<uint32_t> pairs;
+    std::vector<int2> blkij;
+    size_t lds_bytes() const { return (size_t)2 * (buf_slots * 128 + (size_t)(pair_cap + hdr_cap + list_cap) * 4); }
+};
+
+static int env_int(const char *name, int dflt) {
+    const char *v = std::getenv(name);
+    return v ? std::atoi(v) : dflt;
+}
+
+static int32_t dense_blk(int nc, int i, int j) { return i * nc - i * (i - 1) / 2 + (j - i); }
+
+static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt,
+                       const std::vector<int32_t> &pstart, const std::vector<int64_t> &cnt, SweepPlan &P) {
+    P.nbd = nc * (nc + 1) / 2;
+    P.blkij.resize(P.nbd);
+    for (int i = 0; i < nc; ++i)
+        for (int j = i; j < nc; ++j) P.blkij[dense_blk(nc, i, j)] = make_int2(i, j);
+    // specs: rows (camera c, blocks j in [j0, j1)); cameras i and nc-1-i
+    // share a spec so that every spec carries about the same pair work
+    struct Row { int c, j0, j1; };
+    std::vector<std::vector<Row>> specs;
+    if (nc - 1 <= SW_MAX_COLS) {
+        for (int i = 0; i < nc / 2; ++i) specs.push_back({{i, i, nc}, {nc - 1 - i, nc - 1 - i, nc}});
+        if (nc % 2) specs.push_back({{nc / 2, nc / 2, nc}});
+    } else {  // long rows: split into parts of <= SW_MAX_COLS blocks
+        for (int i = 0; i < nc; ++i)
+            for (int j0 = i; j0 < nc; j0 += SW_MAX_COLS) specs.push_back({{i, j0, std::min(nc, j0 + SW_MAX_COLS)}});
+    }
+    P.nspec = (int32_t)specs.size();
+    // block (i <= j) -> spec that owns it
+    std::vector<int32_t> spec_of((size_t)nc * nc, -1);
+    for (int w = 0; w < P.nspec; ++w)
+        for (size_t rr = 0; rr < specs[w].size(); ++rr)
+            for (int j = specs[w][rr].j0; j < specs[w][rr].j1; ++j) spec_of[(size_t)specs[w][rr].c * nc + j] = w;
+    P.lanegrp.assign((size_t)P.nspec * SW_THREADS, (int16_t)-1);
+    // per spec: diagonal groups first (they only read LDS, so their waves
+    // are the loader waves), then the off-diagonal groups sorted by size
+    // (power-of-two lane counts, so every group is aligned inside its wave)
+    std::vector<std::vector<int>> gid_of(P.nspec);  // (row, j - j0) -> group index within spec
+    int max_ng = 0;
+    for (int w = 0; w < P.nspec; ++w) {
+        struct G0 { int blk, flags, slots; double work; int key; };
+        std::vector<G0> gd, g;
+        double tot = 0;
+        for (size_t rr = 0; rr < specs[w].size(); ++rr) {
+            const Row &R = specs[w][rr];
+            for (int j = R.j0; j < R.j1; ++j) {
+                const double work = (double)cnt[(size_t)R.c * nc + j];
+                G0 x = {dense_blk(nc, R.c, j), (j == R.c ? 1 : 0) | (rr == 1 ? 2 : 0), 1, work,
+                        (int)(rr * nc + (j - R.j0))};
+                if (j == R.c) {
+                    gd.push_back(x);
+                } else {
+                    g.push_back(x);
+                    tot += work;
+                }
+            }
+        }
+        const int nd = (int)gd.size(), noff = (int)g.size();
+        int Gd = 64, nload = 1, budget = 0;
+        for (; Gd >= 2; Gd /= 2) {
+            nload = std::max(1, (nd * Gd + 63) / 64);
+            budget = (SW_THREADS - 64 * nload) / 2;
+            if (noff <= budget) break;
+        }
+        int sum = 0;
+        for (auto &x : g) {
+            const double raw = tot > 0 ? x.work / tot * budget : 1.0;
+            int sl = 1;
+            while (sl * 2 <= raw && sl < 32) sl *= 2;
+            x.slots = sl;
+            sum += sl;
+        }
+        while (sum > budget) {  // over budget: halve the largest
+            auto it = std::max_element(g.begin(), g.end(), [](const G0 &a, const G0 &b) { return a.slots < b.slots; });
+            it->slots /= 2;
+            sum -= it->slots;
+        }
+        std::stable_sort(g.begin(), g.end(), [](const G0 &a, const G0 &b) { return a.slots > b.slots; });
+        for (auto &x : gd) x.slots = Gd / 2;
+        g.insert(g.begin(), gd.begin(), gd.end());
+        P.goff.push_back((int32_t)P.groups.size());
+        P.nload.push_back(nload);
+        gid_of[w].assign(specs[w].size() * nc, -1);
+        int lane = 0;
+        for (size_t k = 0; k < g.size(); ++k) {
+            if (k == gd.size()) lane = 64 * nload;  // off-diagonal groups after the loader waves
+            const int G = 2 * g[k].slots;
+            P.groups.push_back({g[k].blk, lane, G, g[k].flags});
+            for (int l = lane; l < lane + G; ++l) P.lanegrp[(size_t)w * SW_THREADS + l] = (int16_t)k;
+            gid_of[w][g[k].key] = (int)k;
+            lane += G;
+        }
+        max_ng = std::max(max_ng, (int)g.size());
+    }
+    P.goff.push_back((int32_t)P.groups.size());
+    P.hdr_cap = (max_ng + 4 + 63) / 64 * 64;
+    // ranges of equal observation count; chunks small enough that two
+    // (chunk, spec) buffers fit the LDS and the chunk's records an XCD's L2
+    P.nrange = std::max(NXCD, env_int("SFM_SWEEP_RANGES", 8) / NXCD * NXCD);
+    int chunk_obs = std::max(64, std::min(env_int("SFM_SWEEP_CHUNK", 11264), 65535));
+    std::vector<int32_t> ccount(nc), cpairs(P.nspec);
+    std::vector<int64_t> cut;  // chunk first points
+    for (;;) {
+        P.rchunk.assign(1, 0);
+        cut.clear();
+        int max_staged = 0, max_pairs = 0;
+        bool ok = true;
+        int64_t pcur = 0;
+        for (int r = 0; r < P.nrange && ok; ++r) {
+            const int64_t oend = no * (r + 1) / P.nrange;
+            while (pcur < np_ && pstart[pcur] < oend) {  // one chunk
+                const int32_t o0 = pstart[pcur];
+                std::fill(ccount.begin(), ccount.end(), 0);
+                std::fill(cpairs.begin(), cpairs.end(), 0);
+                int64_t pe = pcur;
+                while (pe < np_ && pstart[pe] < oend && (pe == pcur || pstart[pe + 1] - o0 <= chunk_obs)) {
+                    for (int32_t a = pstart[pe]; a < pstart[pe + 1]; ++a) {
+                        ccount[cam[a]]++;
+                        for (int32_t b = pstart[pe]; b < pstart[pe + 1]; ++b)
+                            if (cam[b] > cam[a]) cpairs[spec_of[(size_t)cam[a] * nc + cam[b]]]++;
+                    }
+                    ++pe;
+                }
+                if (pstart[pe] - o0 > 65535) { ok = false; break; }
+                for (int w = 0; w < P.nspec; ++w) {
+                    int st = 0;
+                    for (auto &R : specs[w]) st += ccount[R.c];
+                    max_staged = std::max(max_staged, st);
+                    max_pairs = std::max(max_pairs, cpairs[w]);
+                }
+                cut.push_back(pcur);
+                pcur = pe;
+            }
+            P.rchunk.push_back((int32_t)cut.size());
+        }
+        P.buf_slots = std::max(8, (max_staged + 7) / 8 * 8);
+        P.pair_cap = std::max(64, (max_pairs + 63) / 64 * 64);
+        P.list_cap = (P.buf_slots + 63) / 64 * 64;
+        if ((ok && max_staged <= SW_MAX_STAGED && P.lds_bytes() <= 160 * 1024) || chunk_obs <= 64) break;
+        chunk_obs /= 2;
+    }
+    P.nchunk = (int32_t)cut.size();
+    const size_t nqw = (size_t)P.nchunk * P.nspec;
+    P.list.assign(nqw * P.list_cap, 0);
+    P.pairs.assign(nqw * P.pair_cap, 0u);
+    P.hdr.assign(nqw * P.hdr_cap, 0);
+    std::vector<std::vector<int32_t>> per_cam(nc);
+    std::vector<int32_t> slot_of;  // chunk-local obs offset -> position in its camera's list
+    std::vector<std::vector<uint32_t>> glist;
+    for (int32_t q = 0; q < P.nchunk; ++q) {
+        const int32_t o0 = pstart[cut[q]];
+        const int32_t o1 = q + 1 < P.nchunk ? pstart[cut[q + 1]] : (int32_t)no;
+        for (auto &v : per_cam) v.clear();
+        slot_of.assign(o1 - o0, 0);
+        for (int32_t o = o0; o < o1; ++o) {
+            slot_of[o - o0] = (int32_t)per_cam[cam[o]].size();
+            per_cam[cam[o]].push_back(o - o0);
+        }
+        for (int w = 0; w < P.nspec; ++w) {
+            const auto &sp = specs[w];
+            const size_t qw = (size_t)q * P.nspec + w;
+            int32_t *lst = &P.list[qw * P.list_cap];
+            const int32_t n0 = (int32_t)per_cam[sp[0].c].size();
+            const int32_t n1 = sp.size() > 1 ? (int32_t)per_cam[sp[1].c].size() : 0;
+            int ns_ = 0;
+            for (size_t rr = 0; rr < sp.size(); ++rr)
+                for (int32_t off : per_cam[sp[rr].c]) lst[ns_++] = o0 + off;
+            for (; ns_ < P.list_cap; ++ns_) lst[ns_] = o0;  // padding: any valid record
+            const int ng = P.goff[w + 1] - P.goff[w];
+            glist.assign(ng, {});
+            for (size_t rr = 0; rr < sp.size(); ++rr) {
+                const Row &R = sp[rr];
+                const int32_t abase = rr == 0 ? 0 : n0;
+                for (int32_t off : per_cam[R.c]) {
+                    const int32_t a = o0 + off, pnt = pt[a];
+                    for (int32_t b = pstart[pnt]; b < pstart[pnt + 1]; ++b) {
+                        const int cj = cam[b];
+                        if (cj <= R.c || cj < R.j0 || cj >= R.j1) continue;
+                        const int g = gid_of[w][rr * nc + (cj - R.j0)];
+                        glist[g].push_back(((uint32_t)(abase + slot_of[off]) << 16) | (uint32_t)(b - o0));
+                    }
+                }
+            }
+            int32_t *hd = &P.hdr[qw * P.hdr_cap];
+            uint32_t *pp = &P.pairs[qw * P.pair_cap];
+            int32_t np2 = 0;
+            for (int g = 0; g < ng; ++g) {
+                hd[g] = np2;
+                for (uint32_t v : glist[g]) pp[np2++] = v;
+            }
+            hd[ng] = np2;
+            hd[ng + 1] = n0;
+            hd[ng + 2] = n1;
+            hd[ng + 3] = o0;
+        }
+    }
+}
+
 // ------------------------------------------------------------ problem
 enum { T_LIN, T_PREP, T_SCHUR, T_COMM, T_SOLVE, T_TRIAL, T_NT };
 constexpr int kEvSlots = 16;  // max iterations per batch between host polls
@@ -1099,15 +1478,23 @@ struct sfm_ba_problem {
     sfm_comm *comm = nullptr;
     int32_t nc = 0, ns = 0, nsp = 0, nT = 0, tb = 16;
     int64_t np = 0, no = 0, npairs = 0;
-    int32_t nitems = 0, nblocks = 0, ndiag_items = 0, ndiag_blocks = 0;
+    int32_t ndiag_items = 0, ndiag_blocks = 0;
+    // Schur sweep plan (k_schur_sweep): ranges, chunks, specs
+    int32_t sw_nrange = 0, sw_nspec = 0, sw_nbd = 0, sw_nchunk = 0;
+    SweepLds sw_L = {};
+    size_t sw_lds_bytes = 0;
     Kmat K;
     std::vector<double> cams0, pts0;
     // device
     int32_t *d_cam = nullptr, *d_pt = nullptr, *d_pstart = nullptr, *d_cam_obs = nullptr, *d_cstart = nullptr;
-    int2 *d_pairs = nullptr;
     PairItem *d_items = nullptr;
     BlockInfo *d_blocks = nullptr;
     double *d_slab = nullptr, *d_slab2 = nullptr, *d_camlin = nullptr;
+    int32_t *d_sw_rchunk = nullptr, *d_sw_goff = nullptr, *d_sw_nload = nullptr, *d_sw_list = nullptr, *d_sw_hdr = nullptr;
+    SweepGroup *d_sw_groups = nullptr;
+    int16_t *d_sw_lanegrp = nullptr;
+    uint32_t *d_sw_pairs = nullptr;
+    int2 *d_sw_blkij = nullptr;
     double2 *d_obs = nullptr;
     double *d_Rt = nullptr, *d_Rt2 = nullptr, *d_X = nullptr, *d_X2 = nullptr;
     double *d_J = nullptr, *d_Vg = nullptr, *d_Lq = nullptr, *d_Z = nullptr;
@@ -1265,65 +1652,51 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         for (int32_t a = pstart[i]; a < pstart[i + 1]; ++a)
             for (int32_t b = a + 1; b < pstart[i + 1]; ++b)
                 SFM_CHECK_ARG(cam[a] != cam[b], "a point is observed twice by the same camera");
-    // camera-pair lists (static sparsity of the reduced camera system)
+    // co-observation counts per camera block (static sparsity of the reduced camera system)
     std::vector<int64_t> cnt((size_t)nc * nc, 0);
+    int64_t tot = 0;
     for (int64_t i = 0; i < np_; ++i)
         for (int32_t a = pstart[i]; a < pstart[i + 1]; ++a)
             for (int32_t b = a; b < pstart[i + 1]; ++b) {
                 int ci = cam[a], cj = cam[b];
                 if (ci > cj) std::swap(ci, cj);
                 cnt[(size_t)ci * nc + cj]++;
-            }
-    std::vector<BlockInfo> blocks;
-    std::vector<PairItem> items;
-    std::vector<int64_t> boff((size_t)nc * nc, -1);
-    int64_t tot = 0;
-    // diagonal blocks first: they are the largest
-    for (int pass = 0; pass < 2; ++pass) {
-        for (int i = 0; i < nc; ++i)
-            for (int j = i; j < nc; ++j) {
-                if ((pass == 0) != (i == j)) continue;
-                const int64_t n = cnt[(size_t)i * nc + j];
-                if (n == 0) continue;
-                boff[(size_t)i * nc + j] = tot;
-                BlockInfo bi;
-                bi.i = i; bi.j = j; bi.first_item = (int32_t)items.size();
-                for (int64_t k = 0; k < n; k += PAIR_CHUNK) {
-                    PairItem it;
-                    it.blk = (int32_t)blocks.size();
-                    it.k0 = (int32_t)(tot + k);
-                    it.k1 = (int32_t)(tot + std::min<int64_t>(n, k + PAIR_CHUNK));
-                    it.diag = i == j;
-                    items.push_back(it);
-                }
-                bi.last_item = (int32_t)items.size();
-                blocks.push_back(bi);
-                tot += n;
-            }
-        if (pass == 0) {
-            p->ndiag_items = (int32_t)items.size();
-            p->ndiag_blocks = (int32_t)blocks.size();
-        }
-    }
-    SFM_CHECK_ARG(tot < ((int64_t)1 << 31), "too many co-observation pairs");
-    std::vector<int2> pairs(tot);
-    for (int64_t i = 0; i < np_; ++i)
-        for (int32_t a = pstart[i]; a < pstart[i + 1]; ++a)
-            for (int32_t b = a; b < pstart[i + 1]; ++b) {
-                int32_t oa = a, ob = b;
-                if (cam[oa] > cam[ob]) std::swap(oa, ob);
-                pairs[boff[(size_t)cam[oa] * nc + cam[ob]]++] = make_int2(oa, ob);
+                ++tot;
             }
     p->npairs = tot;
-    p->nitems = (int32_t)items.size();
-    p->nblocks = (int32_t)blocks.size();
+    // camera items for k_camera_lin: chunks of each camera's observations
+    std::vector<BlockInfo> blocks;
+    std::vector<PairItem> items;
+    for (int c = 0; c < nc; ++c) {
+        BlockInfo bi;
+        bi.i = c; bi.j = c; bi.first_item = (int32_t)items.size();
+        for (int32_t k = cstart[c]; k < cstart[c + 1]; k += CAM_CHUNK)
+            items.push_back({c, k, std::min<int32_t>(cstart[c + 1], k + CAM_CHUNK), 1});
+        bi.last_item = (int32_t)items.size();
+        if (bi.last_item > bi.first_item) blocks.push_back(bi);
+    }
+    p->ndiag_items = (int32_t)items.size();
+    p->ndiag_blocks = (int32_t)blocks.size();
+    SweepPlan sw;
+    plan_sweep(nc, np_, no, cam, pt, pstart, cnt, sw);
+    p->sw_nrange = sw.nrange;
+    p->sw_nspec = sw.nspec;
+    p->sw_nbd = sw.nbd;
+    p->sw_L = {sw.buf_slots, sw.pair_cap, sw.hdr_cap, sw.list_cap};
+    p->sw_nchunk = sw.nchunk;
+    p->sw_lds_bytes = sw.lds_bytes();
     p->pt_blocks = std::max(1, ceil_div(np_ * PT_GROUP, PT_THREADS));
     p->payload_len = (int64_t)p->ns * p->ns + 3 * p->ns + 1;
     int rc;
     if ((rc = p->alloc(p->d_cam, no)) || (rc = p->alloc(p->d_pt, no)) || (rc = p->alloc(p->d_pstart, np_ + 1)) ||
         (rc = p->alloc(p->d_obs, no)) || (rc = p->alloc(p->d_cam_obs, no)) || (rc = p->alloc(p->d_cstart, nc + 1)) ||
-        (rc = p->alloc(p->d_pairs, tot)) || (rc = p->alloc(p->d_items, p->nitems)) ||
-        (rc = p->alloc(p->d_blocks, p->nblocks)) || (rc = p->alloc(p->d_slab, (int64_t)ITEM_W * p->nitems)) ||
+        (rc = p->alloc(p->d_items, p->ndiag_items)) || (rc = p->alloc(p->d_blocks, p->ndiag_blocks)) ||
+        (rc = p->alloc(p->d_slab, (int64_t)ITEM_W * sw.nrange * sw.nbd)) ||
+        (rc = p->alloc(p->d_sw_rchunk, sw.rchunk.size())) || (rc = p->alloc(p->d_sw_goff, sw.goff.size())) ||
+        (rc = p->alloc(p->d_sw_nload, sw.nload.size())) ||
+        (rc = p->alloc(p->d_sw_groups, sw.groups.size())) || (rc = p->alloc(p->d_sw_lanegrp, sw.lanegrp.size())) ||
+        (rc = p->alloc(p->d_sw_list, sw.list.size())) || (rc = p->alloc(p->d_sw_hdr, sw.hdr.size())) ||
+        (rc = p->alloc(p->d_sw_pairs, sw.pairs.size())) || (rc = p->alloc(p->d_sw_blkij, sw.blkij.size())) ||
         (rc = p->alloc(p->d_camlin, (int64_t)CAMLIN * nc)) ||
         (rc = p->alloc(p->d_slab2, (int64_t)CAMLIN * std::max<int64_t>(1, p->ndiag_items))) ||
         (rc = p->alloc(p->d_Rt, 12 * (int64_t)nc)) || (rc = p->alloc(p->d_Rt2, 12 * (int64_t)nc)) ||
@@ -1347,11 +1720,26 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     if (no) SFM_HIP(hipMemcpyAsync(p->d_cam_obs, cam_obs.data(), no * 4, hipMemcpyHostToDevice, s));
     SFM_HIP(hipMemcpyAsync(p->d_cstart, cstart.data(), cstart.size() * 4, hipMemcpyHostToDevice, s));
     SFM_HIP(hipMemsetAsync(p->d_camlin, 0, (size_t)CAMLIN * nc * sizeof(double), s));
-    if (tot) SFM_HIP(hipMemcpyAsync(p->d_pairs, pairs.data(), tot * sizeof(int2), hipMemcpyHostToDevice, s));
-    if (p->nitems) {
+    if (p->ndiag_items) {
         SFM_HIP(hipMemcpyAsync(p->d_items, items.data(), items.size() * sizeof(PairItem), hipMemcpyHostToDevice, s));
         SFM_HIP(hipMemcpyAsync(p->d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), hipMemcpyHostToDevice, s));
     }
+    auto up = [&](void *dst, const void *src, size_t bytes) -> int {
+        if (bytes) SFM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+        return 0;
+    };
+    if ((rc = up(p->d_sw_rchunk, sw.rchunk.data(), sw.rchunk.size() * 4)) ||
+        (rc = up(p->d_sw_goff, sw.goff.data(), sw.goff.size() * 4)) ||
+        (rc = up(p->d_sw_nload, sw.nload.data(), sw.nload.size() * 4)) ||
+        (rc = up(p->d_sw_groups, sw.groups.data(), sw.groups.size() * sizeof(SweepGroup))) ||
+        (rc = up(p->d_sw_lanegrp, sw.lanegrp.data(), sw.lanegrp.size() * 2)) ||
+        (rc = up(p->d_sw_list, sw.list.data(), sw.list.size() * 4)) ||
+        (rc = up(p->d_sw_hdr, sw.hdr.data(), sw.hdr.size() * 4)) ||
+        (rc = up(p->d_sw_pairs, sw.pairs.data(), sw.pairs.size() * 4)) ||
+        (rc = up(p->d_sw_blkij, sw.blkij.data(), sw.blkij.size() * sizeof(int2))))
+        return rc;
+    SFM_HIP(hipFuncSetAttribute((const void *)k_schur_sweep, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)p->sw_lds_bytes));
     if ((rc = upload_state(p.get()))) return rc;
     *out = p.release();
     return 0;
@@ -1432,7 +1820,7 @@ static int run_linearize(sfm_ba_problem *p) {
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, p->d_partial, nbl, 1, p->d_scal + 8, glin);
     SFM_HIP(hipGetLastError());
     if (p->ndiag_items) {
-        hipLaunchKernelGGL(k_camera_lin, dim3(p->ndiag_items), dim3(256), 0, s, p->d_items, p->d_pairs, p->d_J,
+        hipLaunchKernelGGL(k_camera_lin, dim3(p->ndiag_items), dim3(256), 0, s, p->d_items, p->d_cam_obs, p->d_J,
                            p->d_slab2, glin);
         SFM_HIP(hipGetLastError());
         hipLaunchKernelGGL(k_camera_lin_finish, dim3(p->ndiag_blocks), dim3(64), 0, s, p->d_blocks, p->d_slab2,
@@ -1459,14 +1847,14 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev) {
     SFM_HIP(hipGetLastError());
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_PREP + 1], s));
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SCHUR], s));
-    if (p->nitems) {
-        hipLaunchKernelGGL(k_schur_pairs, dim3(p->nitems), dim3(PAIR_THREADS), 0, s, p->d_items, p->d_pairs, p->d_pt,
-                           p->d_Z, p->d_Lq, p->d_slab, gst);
-        SFM_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_schur_finish, dim3(p->nblocks), dim3(64), 0, s, p->ns, p->d_blocks, p->d_slab,
-                           p->d_camlin, p->d_payload, gst);
-        SFM_HIP(hipGetLastError());
-    }
+    hipLaunchKernelGGL(k_schur_sweep, dim3(NXCD * p->sw_nspec * ceil_div(p->sw_nrange, NXCD)), dim3(SW_THREADS),
+                       p->sw_lds_bytes, s, p->sw_nspec, p->sw_nrange, p->sw_nbd, p->sw_L, p->d_sw_rchunk,
+                       p->d_sw_nload, p->d_sw_goff, p->d_sw_groups, p->d_sw_lanegrp, p->d_sw_list,
+                       p->d_sw_pairs, p->d_sw_hdr, p->d_Z, p->d_slab, gst, env_int("SFM_SWEEP_DEBUG", 0));
+    SFM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_schur_finish, dim3(p->sw_nbd), dim3(64), 0, s, p->ns, p->sw_nbd, p->sw_nrange,
+                       p->d_sw_blkij, p->d_slab, p->d_camlin, p->d_payload, gst);
+    SFM_HIP(hipGetLastError());
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SCHUR + 1], s));
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_COMM], s));
     if ((rc = allreduce(p, p->d_payload, p->payload_len - 1))) return rc;
