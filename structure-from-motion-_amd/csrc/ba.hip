@@ -18,17 +18,23 @@
 //   k_schur_finish   fixed-order sum of the ranges of each camera block ->
 //                    deterministic, no atomics.
 //   [RCCL all-reduce of the packed partial system across ranks]
-//   k_assemble       S += lambda*clamp(diag U), b = -g_c + sum Z q, padded.
+//   (assembly of S + lambda*clamp(diag U), b = -g_c + sum Z q folded into the
+//    first Cholesky launch)
 //   k_chol_col       one launch per 16-wide tile column: trailing update
 //                    by the previous column + factor/TRSM of this one
 //                    (+ folded forward solve); k_chol_backsolve.
-//   k_camera_trial   R' = exp([dtheta]x) R, t' = t + dt; camera part of the
+//   (backsolve epilogue) R' = exp([dtheta]x) R, t' = t + dt; camera part of the
 //                    model decrease.
 //   k_backsub_trial  thread per point: dp = L L^T(-g_p - sum W^T dc),
 //                    X' = X + dp, trial cost of its observations.
-//   k_finalize       fixed-order reduction of per-block partials.
-// The host reads 8 scalars per iteration and applies Nielsen's damping
-// update; on a rejected step only k_point_prep onwards is repeated.
+//   k_lm_step        the accept/reject decision and Nielsen's damping update
+//                    on the device (state double-buffered by iteration
+//                    parity), the accepted step's copy trial -> current.
+// Per-point partial sums are finished by the last block of their kernel
+// (grid_sum_last), so an iteration is linearize / camera_lin (accepted
+// steps only), point_prep, schur_sweep, schur_finish, the Cholesky launches,
+// backsub_trial and lm_step; the host polls the device state once per batch
+// of iterations.  On a rejected step only k_point_prep onwards is repeated.
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -109,6 +115,64 @@ __device__ __forceinline__ void block_sum_store(double (&v)[NV], double *out) {
     }
 }
 
+// Grid-wide fixed-order sum without a second launch.  Every block of
+// PT_THREADS threads reduces its NV values, thread 0 stores them write-through
+// (agent-scope relaxed stores = sc1) to partial[block][NV], waits for the
+// stores and counts itself in with an agent-scope atomic; the block whose add
+// returns nblk - 1 sums all partials in block order (sc1 loads) into
+// out[0..NV) and re-arms the counter.  The same summation order as a separate
+// k_finalize launch, so the result is deterministic.
+template <int NV>
+__device__ __forceinline__ void grid_sum_last(double (&v)[NV], double *partial, unsigned *counter, double *out) {
+    __shared__ double red[PT_THREADS / 64][NV];
+    __shared__ int last;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned nblk = gridDim.x;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const double s = wave_sum(v[k]);
+        if (lane == 0) red[w][k] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            double s = 0;
+            for (int i = 0; i < PT_THREADS / 64; ++i) s += red[i][k];
+            __hip_atomic_store(partial + (int64_t)NV * blockIdx.x + k, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __shared__ double tot[PT_THREADS];
+    for (int k = 0; k < NV; ++k) {
+        double s = 0;
+        for (unsigned b0 = threadIdx.x; b0 < nblk; b0 += 16 * PT_THREADS) {
+            double v16[16];  // 16 independent sc1 loads in flight, summed in block order
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const unsigned b = b0 + u * PT_THREADS;
+                v16[u] = b < nblk ? __hip_atomic_load(partial + (int64_t)NV * b + k, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT)
+                                  : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) s += v16[u];
+        }
+        tot[threadIdx.x] = s;
+        __syncthreads();
+        for (int st = PT_THREADS / 2; st > 0; st >>= 1) {
+            if ((int)threadIdx.x < st) tot[threadIdx.x] += tot[threadIdx.x + st];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) out[k] = tot[0];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *counter = 0u;
+}
+
 // ------------------------------------------------------ observation model
 // Every Jacobian block of an observation follows from A = dr/dx_cam (2x3),
 // p = R X (the rotated point) and the camera's R:
@@ -180,7 +244,9 @@ __global__ void __launch_bounds__(PT_THREADS) k_linearize(int64_t np_, const int
                                                           const double2 *__restrict__ obs, Kmat Km,
                                                           const double *__restrict__ Rt,
                                                           const double *__restrict__ X, double *__restrict__ J,
-                                                          double *__restrict__ Vg, double *__restrict__ partial, const int *__restrict__ gate) {
+                                                          double *__restrict__ Vg, double *__restrict__ partial,
+                                                          unsigned *__restrict__ counter, double *__restrict__ cost_out,
+                                                          int want_cost, const int *__restrict__ gate) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
     const int64_t gt = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x;
     const int64_t p = gt / G;  // G lanes per point, striding over its observations
@@ -228,7 +294,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_linearize(int64_t np_, const int
 #pragma unroll
         for (int i = 0; i < 3; ++i) vg[6 + i] = g[i];
     }
-    block_sum_store<1>(acc, partial + blockIdx.x);
+    if (want_cost) grid_sum_last<1>(acc, partial, counter, cost_out);  // only the initial cost is used
 }
 
 // Lq layout per point (9 doubles): L00 L01 L02 L11 L12 L22 | q0 q1 q2
@@ -577,13 +643,17 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
 
 // Camera blocks of the normal equations, once per linearisation: each item
 // sums U = sum Jc^T Jc (21) and g = sum Jc^T r (6) over a chunk of one
-// camera's observations and k_camera_lin_finish adds a camera's items in
-// order (deterministic).
+// camera's observations (write-through to slab2); the item that arrives last
+// adds every camera's items in order into camlin (deterministic, one launch).
 __global__ void __launch_bounds__(256) k_camera_lin(const PairItem *__restrict__ items,
                                                     const int32_t *__restrict__ cam_obs,
-                                                    const double *__restrict__ J, double *__restrict__ slab2, const int *__restrict__ gate) {
+                                                    const double *__restrict__ J, double *__restrict__ slab2,
+                                                    const BlockInfo *__restrict__ blocks, int32_t nblocks,
+                                                    double *__restrict__ camlin, unsigned *__restrict__ counter,
+                                                    const int *__restrict__ gate) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
     __shared__ double red[4][CAMLIN];
+    __shared__ int last;
     const PairItem it = items[blockIdx.x];
     double acc[CAMLIN];
 #pragma unroll
@@ -612,20 +682,24 @@ __global__ void __launch_bounds__(256) k_camera_lin(const PairItem *__restrict__
     }
     __syncthreads();
     if (threadIdx.x < CAMLIN)
-        slab2[(int64_t)CAMLIN * blockIdx.x + threadIdx.x] =
-            red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-}
-
-// one 64-thread workgroup per camera: fixed-order sum of its items
-__global__ void __launch_bounds__(64) k_camera_lin_finish(const BlockInfo *__restrict__ blocks,
-                                                          const double *__restrict__ slab2,
-                                                          double *__restrict__ camlin, const int *__restrict__ gate) {
-    if (gate && !*gate) return;  // device-side LM control: iteration gated off
-    const BlockInfo bi = blocks[blockIdx.x];
-    if (threadIdx.x >= CAMLIN) return;
-    double v = 0;
-    for (int k = bi.first_item; k < bi.last_item; ++k) v += slab2[(int64_t)CAMLIN * k + threadIdx.x];
-    camlin[CAMLIN * bi.i + threadIdx.x] = v;
+        __hip_atomic_store(slab2 + (int64_t)CAMLIN * blockIdx.x + threadIdx.x,
+                           red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    for (int e = threadIdx.x; e < nblocks * CAMLIN; e += 256) {
+        const BlockInfo bi = blocks[e / CAMLIN];
+        const int k = e % CAMLIN;
+        double v = 0;
+        for (int i = bi.first_item; i < bi.last_item; ++i)
+            v += __hip_atomic_load(slab2 + (int64_t)CAMLIN * i + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        camlin[CAMLIN * bi.i + k] = v;
+    }
+    if (threadIdx.x == 0) *counter = 0u;
 }
 
 // one 64-thread workgroup per camera block (i <= j, dense upper-triangle
@@ -659,28 +733,6 @@ __global__ void __launch_bounds__(64) k_schur_finish(int32_t ns, int32_t nbd, in
         const int r = t - 36;
         payload[base + ns + 6 * ij.x + r] = camlin[CAMLIN * ij.x + 21 + r];  // g_c
         payload[base + 2 * ns + 6 * ij.x + r] = v;                           // sum Z q
-    }
-}
-
-// A (nsp x nsp, padded with identity), bvec (nsp)
-__global__ void k_assemble(int32_t ns, int32_t nsp, const double *__restrict__ payload, const double *__restrict__ lam,
-                           double *__restrict__ A, double *__restrict__ bvec, const int *__restrict__ gate) {
-    if (gate && !*gate) return;  // device-side LM control: iteration gated off
-    const double lambda = *lam;
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (int64_t)nsp * nsp) return;
-    const int r = (int)(idx / nsp), c = (int)(idx % nsp);
-    double v;
-    if (r < ns && c < ns) {
-        v = payload[(int64_t)r * ns + c];
-        if (r == c) v += lambda * clampd(payload[(int64_t)ns * ns + r]);
-    } else {
-        v = (r == c) ? 1.0 : 0.0;
-    }
-    A[idx] = v;
-    if (c == 0) {
-        const int64_t base = (int64_t)ns * ns;
-        bvec[r] = r < ns ? -payload[base + ns + r] + payload[base + 2 * ns + r] : 0.0;
     }
 }
 
@@ -734,11 +786,31 @@ __device__ __forceinline__ void chol_factor(double (&r)[TB], double (&dinv)[TB],
     }
 }
 
+// element (i, j) of the damped, identity-padded system S + lambda clamp(diag U)
+// read straight from the Schur payload (launch 0 assembles as it loads)
+__device__ __forceinline__ double assembled(const double *__restrict__ payload, int32_t ns, double lambda, int i,
+                                            int j) {
+    if (i < ns && j < ns) {
+        double v = payload[(int64_t)i * ns + j];
+        if (i == j) v += lambda * clampd(payload[(int64_t)ns * ns + i]);
+        return v;
+    }
+    return i == j ? 1.0 : 0.0;
+}
+
+__device__ __forceinline__ double assembled_b(const double *__restrict__ payload, int32_t ns, int i) {
+    const int64_t base = (int64_t)ns * ns;
+    return i < ns ? -payload[base + ns + i] + payload[base + 2 * ns + i] : 0.0;
+}
+
 template <int TB>
 __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_t nsp, int s,
                                                   double *__restrict__ D, double *__restrict__ bvec,
-                                                  int *__restrict__ bad, const int *__restrict__ gate) {
+                                                  int *__restrict__ bad, const double *__restrict__ payload,
+                                                  int32_t ns, const double *__restrict__ lam,
+                                                  const int *__restrict__ gate) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
+    const double lambda = s == 0 ? *lam : 0.0;
     __shared__ double Lr[TB][TB + 1], Lc[TB][TB + 1], Ct[TB][TB + 1], Cd[TB][TB + 1];
     __shared__ double yk[TB];
     const int t = threadIdx.x;
@@ -776,8 +848,13 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
             const int e = t + 256 * q, i = e / TB, j = e % TB;
             Lr[i][j] = upd ? A[(int64_t)(r0 + i) * nsp + kp + j] : 0.0;
             Lc[i][j] = upd ? A[(int64_t)(c0 + i) * nsp + kp + j] : 0.0;
-            arc[q] = A[(int64_t)(r0 + i) * nsp + c0 + j];
-            ass[q] = need_d ? A[(int64_t)(s0 + i) * nsp + s0 + j] : 0.0;
+            if (upd) {
+                arc[q] = A[(int64_t)(r0 + i) * nsp + c0 + j];
+                ass[q] = need_d ? A[(int64_t)(s0 + i) * nsp + s0 + j] : 0.0;
+            } else {
+                arc[q] = assembled(payload, ns, lambda, r0 + i, c0 + j);
+                ass[q] = need_d ? assembled(payload, ns, lambda, s0 + i, s0 + j) : 0.0;
+            }
         }
         __syncthreads();
 #pragma unroll
@@ -805,6 +882,8 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
     }
     // column s: C_ss (Cd, or Ct in the diagonal block) is bitwise the same in
     // every column block -- same inputs, same operation order
+    if (!upd && r == s)  // launch 0: the right-hand side of the rows past tile 0
+        for (int i = TB + t; i < nsp; i += blockDim.x) bvec[i] = assembled_b(payload, ns, i);
     __syncthreads();
     if (t >= 64) return;
     const int lane = t;
@@ -815,7 +894,7 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
     for (int j = 0; j < TB; ++j) rw[j] = Cdd[li][j];
     chol_factor<TB>(rw, dinv, lane, bad);
     if (r == s) {
-        double y = bvec[s0 + li];
+        double y = upd ? bvec[s0 + li] : assembled_b(payload, ns, li);
         if (upd) {
             double acc = 0;
 #pragma unroll
@@ -873,10 +952,54 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
 constexpr int SOLVE_THREADS = 512;
 constexpr int SOLVE_MAX = 4096;
 
+// trial cameras + camera part of the model decrease / norms, by one
+// workgroup of THREADS threads (run at the end of k_chol_backsolve, which
+// holds the camera step dc in LDS).  cam_out[0..3) = {model_c, |dc|^2, |t|^2}
+template <int THREADS>
+__device__ __forceinline__ void camera_trial(int32_t nc, const double *dc, const double *__restrict__ payload,
+                                             int32_t ns, double lambda, const double *__restrict__ Rt,
+                                             double *__restrict__ Rt_new, double *__restrict__ cam_out,
+                                             double (*red)[THREADS]) {
+    double m = 0, dn = 0, xn = 0;
+    const double *diagU = payload + (int64_t)ns * ns, *gc = diagU + ns;
+    for (int c = threadIdx.x; c < nc; c += THREADS) {
+        const double *d = dc + 6 * c;
+        double dR[9];
+        rotvec_to_R(d[0], d[1], d[2], dR);
+        const double *R = Rt + 12 * c;
+        double *Rn = Rt_new + 12 * c;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) Rn[3 * i + j] = dR[3 * i] * R[j] + dR[3 * i + 1] * R[3 + j] + dR[3 * i + 2] * R[6 + j];
+        for (int i = 0; i < 3; ++i) {
+            Rn[9 + i] = R[9 + i] + d[3 + i];
+            xn += R[9 + i] * R[9 + i];
+        }
+        for (int i = 0; i < 6; ++i) {
+            m += d[i] * (lambda * clampd(diagU[6 * c + i]) * d[i] - gc[6 * c + i]);
+            dn += d[i] * d[i];
+        }
+    }
+    red[0][threadIdx.x] = m; red[1][threadIdx.x] = dn; red[2][threadIdx.x] = xn;
+    __syncthreads();
+    for (int s = THREADS / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s)
+            for (int k = 0; k < 3; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x < 3) cam_out[threadIdx.x] = red[threadIdx.x][0];
+}
+
+struct CamTrialArgs {  // k_chol_backsolve's epilogue (nc = 0: none)
+    int32_t nc, ns;
+    const double *payload, *lam, *Rt;
+    double *Rt_new, *cam_out;
+};
+
 template <int TB>
 __global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(double *__restrict__ A, int32_t nsp,
                                                                   double *__restrict__ xg,
-                                                                  const double *__restrict__ Dlast, const int *__restrict__ gate) {
+                                                                  const double *__restrict__ Dlast, CamTrialArgs ct,
+                                                                  const int *__restrict__ gate) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
     __shared__ double x[SOLVE_MAX];
     __shared__ double yt[TB];
@@ -944,6 +1067,10 @@ __global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(double *__rest
         }
     }
     for (int i = t; i < nsp; i += SOLVE_THREADS) xg[i] = x[i];
+    if (ct.nc > 0) {
+        __shared__ double red[3][SOLVE_THREADS];
+        camera_trial<SOLVE_THREADS>(ct.nc, x, ct.payload, ct.ns, *ct.lam, ct.Rt, ct.Rt_new, ct.cam_out, red);
+    }
 }
 
 // ------------------------------------------------- device-side LM control
@@ -957,63 +1084,77 @@ struct LMState {
     int run_lin, run_step, accept_now, pad;
 };
 
-__global__ void k_lm_reset(LMState *lm, double lambda0) {
+__global__ void k_lm_reset(LMState *lm, double lambda0, int *bad) {
     lm->lambda = lambda0; lm->nu = 2.0; lm->cost = 0.0; lm->cost0 = 0.0;
     lm->status = 4; lm->accepted = 0; lm->iters = 0; lm->done = 0;
     lm->run_lin = 1; lm->run_step = 1; lm->accept_now = 0;
+    bad[0] = 0;
 }
 
 __global__ void k_lm_init(LMState *lm, const double *lin_cost) { lm->cost = lm->cost0 = *lin_cost; }
 
 // sfm_ba_solve's host logic, verbatim: Nielsen's lambda update on the gain
 // ratio of the trial step; scal = [cost_trial, model_p, dn_p, xn_p, model_c,
-// dn_c, xn_c]
-__global__ void k_lm_decide(LMState *lm, const double *__restrict__ h, const int *__restrict__ badp,
-                            int max_iterations, int fixed, double ftol, double ptol, double lambda0) {
+// dn_c, xn_c].  Returns the new state from the old one (a pure function, so
+// every block of k_lm_step computes the same decision).
+__device__ __forceinline__ LMState lm_decide(LMState lm, const double *__restrict__ h, int bad, int max_iterations,
+                                             int fixed, double ftol, double ptol, double lambda0) {
 #pragma clang fp contract(off)
-    if (lm->done) { lm->accept_now = 0; return; }
-    const int bad = *badp;
-    const double cost = lm->cost;
+    if (lm.done) { lm.accept_now = 0; return lm; }
+    const double cost = lm.cost;
     const double cost_new = h[0];
     const double model = 0.5 * (h[1] + h[4]);
     const double dnorm = sqrt(h[2] + h[5]), xnorm = sqrt(h[3] + h[6]);
     const double rho = (!bad && model > 0) ? (cost - cost_new) / model : -1.0;
-    lm->iters += 1;
+    lm.iters += 1;
     int done = 0;
     if (!bad && isfinite(cost_new) && rho > 1e-3) {
-        lm->accept_now = 1;
+        lm.accept_now = 1;
         const double dcost = cost - cost_new;
-        lm->cost = cost_new;
-        lm->accepted += 1;
+        lm.cost = cost_new;
+        lm.accepted += 1;
         double f = 2.0 * rho - 1.0;
         f = 1.0 - f * f * f;
-        lm->lambda *= (f > 1.0 / 3.0 ? f : 1.0 / 3.0);
-        lm->nu = 2.0;
-        lm->run_lin = 1;
+        lm.lambda *= (f > 1.0 / 3.0 ? f : 1.0 / 3.0);
+        lm.nu = 2.0;
+        lm.run_lin = 1;
         if (!fixed) {
-            if (dcost < ftol * cost_new) { lm->status = 1; done = 1; }
-            else if (dnorm < ptol * (xnorm + ptol)) { lm->status = 3; done = 1; }
+            if (dcost < ftol * cost_new) { lm.status = 1; done = 1; }
+            else if (dnorm < ptol * (xnorm + ptol)) { lm.status = 3; done = 1; }
         }
     } else {
-        lm->accept_now = 0;
-        lm->lambda *= lm->nu;
-        lm->nu *= 2.0;
-        lm->run_lin = 0;
-        if (lm->lambda > 1e32) {
-            if (!fixed) { lm->status = 5; done = 1; }
-            else { lm->lambda = lambda0; lm->nu = 2.0; }
+        lm.accept_now = 0;
+        lm.lambda *= lm.nu;
+        lm.nu *= 2.0;
+        lm.run_lin = 0;
+        if (lm.lambda > 1e32) {
+            if (!fixed) { lm.status = 5; done = 1; }
+            else { lm.lambda = lambda0; lm.nu = 2.0; }
         }
     }
-    if (lm->iters >= max_iterations) done = 1;
-    lm->done = done;
-    lm->run_step = !done;
-    lm->run_lin = lm->run_lin && !done;
+    if (lm.iters >= max_iterations) done = 1;
+    lm.done = done;
+    lm.run_step = !done;
+    lm.run_lin = lm.run_lin && !done;
+    return lm;
 }
 
-// accepted step: the trial state becomes the current one
-__global__ void k_lm_accept(const LMState *__restrict__ lm, int64_t np_, int32_t nc, double *__restrict__ X,
-                            const double *__restrict__ X2, double *__restrict__ Rt, const double *__restrict__ Rt2) {
-    if (!lm->accept_now) return;
+// One launch per LM iteration end: the decision (recomputed by every block
+// from the old state lm_in, written by block 0 to lm_out -- the state is
+// double-buffered by iteration parity, so no block reads what another
+// writes), the accepted step's copy trial -> current, and the reset of the
+// next iteration's not-positive-definite flag.
+__global__ void k_lm_step(const LMState *__restrict__ lm_in, LMState *__restrict__ lm_out,
+                          const double *__restrict__ h, const int *__restrict__ bad_in, int *__restrict__ bad_next,
+                          int max_iterations, int fixed, double ftol, double ptol, double lambda0, int64_t np_,
+                          int32_t nc, double *__restrict__ X, const double *__restrict__ X2, double *__restrict__ Rt,
+                          const double *__restrict__ Rt2) {
+    const LMState lm = lm_decide(*lm_in, h, *bad_in, max_iterations, fixed, ftol, ptol, lambda0);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *lm_out = lm;
+        *bad_next = 0;
+    }
+    if (!lm.accept_now) return;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < 3 * np_) X[i] = X2[i];
     if (i < 12 * (int64_t)nc) Rt[i] = Rt2[i];
@@ -1031,25 +1172,25 @@ static int lanes_per_point(const char *env, int dflt) {
 // the padded reduced camera system with tiles of tb (16 or 32) columns; A, b
 // on the device, D = 2 tb^2 scratch; nsp a multiple of tb.
 template <int TB>
-static int launch_cholesky_t(double *A, int32_t nsp, double *b, double *D, int *bad, hipStream_t s,
-                             const int *gate) {
+static int launch_cholesky_t(const double *payload, int32_t ns, const double *lam, double *A, int32_t nsp, double *b,
+                             double *D, int *bad, hipStream_t s, const int *gate, const CamTrialArgs &ct) {
     const int nT = nsp / TB;
     for (int st = 0; st < nT; ++st) {
         const int T = nT - st;
         hipLaunchKernelGGL(k_chol_col<TB>, dim3(T * (T + 1) / 2 + (st >= 1 ? 1 : 0)), dim3(256), 0, s, A, nsp, st, D,
-                           b, bad, gate);
+                           b, bad, payload, ns, lam, gate);
         SFM_HIP(hipGetLastError());
     }
     hipLaunchKernelGGL(k_chol_backsolve<TB>, dim3(1), dim3(SOLVE_THREADS), 0, s, A, nsp, b,
-                       D + ((nT - 1) & 1) * TB * TB, gate);
+                       D + ((nT - 1) & 1) * TB * TB, ct, gate);
     SFM_HIP(hipGetLastError());
     return 0;
 }
 
-static int launch_cholesky(double *A, int32_t nsp, double *b, double *D, int *bad, hipStream_t s, int tb,
-                           const int *gate = nullptr) {
-    return tb == 32 ? launch_cholesky_t<32>(A, nsp, b, D, bad, s, gate)
-                    : launch_cholesky_t<16>(A, nsp, b, D, bad, s, gate);
+static int launch_cholesky(const double *payload, int32_t ns, const double *lam, double *A, int32_t nsp, double *b,
+                           double *D, int *bad, hipStream_t s, int tb, const int *gate, const CamTrialArgs &ct) {
+    return tb == 32 ? launch_cholesky_t<32>(payload, ns, lam, A, nsp, b, D, bad, s, gate, ct)
+                    : launch_cholesky_t<16>(payload, ns, lam, A, nsp, b, D, bad, s, gate, ct);
 }
 
 // Cholesky tile width (env SFM_CHOL_TILE = 32 for experiments).  Measured
@@ -1064,58 +1205,21 @@ static int chol_tile(int64_t) {
     return 16;
 }
 
-// S + lambda diag(clamp(diag U)) x = b from the Schur payload (k_assemble +
+// S + lambda diag(clamp(diag U)) x = b from the Schur payload (assembled by the
 // tiled Cholesky); x -> b.
 //
-// Measured alternative, not kept: a single-workgroup solve (whole lower
-// triangle resident in one CU's registers + LDS, fp64 MFMA trailing updates,
-// one launch) ran 0.246 ms at ns = 300 against 0.167 ms here -- one CU's fp64
-// MFMA issue rate bounds its trailing updates and its per-tile factor chain
-// is as latency-bound as this path's.
+// Measured alternatives, not kept (MI355X, ns = 300): a single-workgroup
+// solve with the lower triangle resident in one CU's registers + LDS and fp64
+// MFMA trailing updates ran 0.246 ms; a single-workgroup LEFT-looking solve
+// (L tiles in L2, MFMA updates from a 4-deep load ring, explicit diagonal-tile
+// inverses so the TRSM and both substitutions are MFMA / mat-vec work) ran
+// 0.258 ms (updates 108 us, diagonal factor + inverse chains 78 us, back
+// substitution 40 us) against 0.177 ms for this multi-launch path: one CU's
+// fp64 MFMA rate and its serial per-tile chains bound both.
 static int launch_reduced_solve(int32_t ns, int32_t nsp, const double *payload, const double *lam, double *A,
-                                double *b, double *D, int *bad, hipStream_t s, int tb, const int *gate) {
-    const int64_t nA = (int64_t)nsp * nsp;
-    hipLaunchKernelGGL(k_assemble, dim3(ceil_div(nA, 256)), dim3(256), 0, s, ns, nsp, payload, lam, A, b, gate);
-    SFM_HIP(hipGetLastError());
-    return launch_cholesky(A, nsp, b, D, bad, s, tb, gate);
-}
-
-// one workgroup: trial cameras + camera part of model decrease / norms.
-// cam_out[0..3) = {model_c, |dc|^2, |t|^2}
-__global__ void __launch_bounds__(256) k_camera_trial(int32_t nc, const double *__restrict__ dc,
-                                                      const double *__restrict__ payload, int32_t ns, const double *__restrict__ lam,
-                                                      const double *__restrict__ Rt, double *__restrict__ Rt_new,
-                                                      double *__restrict__ cam_out, const int *__restrict__ gate) {
-    if (gate && !*gate) return;  // device-side LM control: iteration gated off
-    const double lambda = *lam;
-    __shared__ double red[3][256];
-    double m = 0, dn = 0, xn = 0;
-    const double *diagU = payload + (int64_t)ns * ns, *gc = diagU + ns;
-    for (int c = threadIdx.x; c < nc; c += blockDim.x) {
-        const double *d = dc + 6 * c;
-        double dR[9];
-        rotvec_to_R(d[0], d[1], d[2], dR);
-        const double *R = Rt + 12 * c;
-        double *Rn = Rt_new + 12 * c;
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) Rn[3 * i + j] = dR[3 * i] * R[j] + dR[3 * i + 1] * R[3 + j] + dR[3 * i + 2] * R[6 + j];
-        for (int i = 0; i < 3; ++i) {
-            Rn[9 + i] = R[9 + i] + d[3 + i];
-            xn += R[9 + i] * R[9 + i];
-        }
-        for (int i = 0; i < 6; ++i) {
-            m += d[i] * (lambda * clampd(diagU[6 * c + i]) * d[i] - gc[6 * c + i]);
-            dn += d[i] * d[i];
-        }
-    }
-    red[0][threadIdx.x] = m; red[1][threadIdx.x] = dn; red[2][threadIdx.x] = xn;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s)
-            for (int k = 0; k < 3; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + s];
-        __syncthreads();
-    }
-    if (threadIdx.x < 3) cam_out[threadIdx.x] = red[threadIdx.x][0];
+                                double *b, double *D, int *bad, hipStream_t s, int tb, const int *gate,
+                                const CamTrialArgs &ct) {
+    return launch_cholesky(payload, ns, lam, A, nsp, b, D, bad, s, tb, gate, ct);
 }
 
 // partial[block][4] = {trial cost, model_p, |dp|^2, |X|^2}
@@ -1130,7 +1234,9 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
                                                               const double *__restrict__ Rt,
                                                               const double *__restrict__ Rt_new,
                                                               const double *__restrict__ X,
-                                                              double *__restrict__ X_new, double *__restrict__ partial, const int *__restrict__ gate) {
+                                                              double *__restrict__ X_new, double *__restrict__ partial,
+                                                              unsigned *__restrict__ counter, double *__restrict__ out,
+                                                              const int *__restrict__ gate) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
     const double lambda = *lam;
     const int64_t gt = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x;
@@ -1187,26 +1293,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
         }
         for (int32_t o = o0 + sub; o < o1; o += G) acc[0] += obs_cost(Rt_new + 12 * cam[o], xn, K, obs[o]);
     }
-    block_sum_store<4>(acc, partial + 4 * (int64_t)blockIdx.x);
-}
-
-// fixed-order sum of nblk partials of width w into out[0..w)
-__global__ void __launch_bounds__(256) k_finalize(const double *__restrict__ partial, int nblk, int w,
-                                                  double *__restrict__ out, const int *__restrict__ gate) {
-    if (gate && !*gate) return;  // device-side LM control: iteration gated off
-    __shared__ double red[256];
-    for (int k = 0; k < w; ++k) {
-        double s = 0;
-        for (int b = threadIdx.x; b < nblk; b += 256) s += partial[(int64_t)b * w + k];
-        red[threadIdx.x] = s;
-        __syncthreads();
-        for (int st = 128; st > 0; st >>= 1) {
-            if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) out[k] = red[0];
-        __syncthreads();
-    }
+    grid_sum_last<4>(acc, partial, counter, out);
 }
 
 // ---------------------------------------------------------------- host math
@@ -1501,6 +1588,7 @@ struct sfm_ba_problem {
     double *d_payload = nullptr, *d_A = nullptr, *d_b = nullptr, *d_D = nullptr;
     double *d_partial = nullptr, *d_scal = nullptr;
     int *d_bad = nullptr;
+    unsigned *d_count = nullptr;  // grid_sum_last arrival counters
     double *h_scal = nullptr;  // pinned
     int64_t payload_len = 0;
     int pt_blocks = 0;
@@ -1706,8 +1794,8 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = p->alloc(p->d_A, (int64_t)p->nsp * p->nsp)) || (rc = p->alloc(p->d_b, p->nsp)) ||
         (rc = p->alloc(p->d_D, 2 * 32 * 32)) ||
         (rc = p->alloc(p->d_partial, 4 * (int64_t)p->pt_blocks)) || (rc = p->alloc(p->d_scal, 16)) ||
-        (rc = p->alloc(p->d_lm, 1)) ||
-        (rc = p->alloc(p->d_bad, 4)))
+        (rc = p->alloc(p->d_lm, 2)) ||
+        (rc = p->alloc(p->d_bad, 4)) || (rc = p->alloc(p->d_count, 8)))
         return rc;
     SFM_HIP(hipHostMalloc((void **)&p->h_scal, 16 * sizeof(double)));
     hipStream_t s = p->stream;
@@ -1720,6 +1808,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     if (no) SFM_HIP(hipMemcpyAsync(p->d_cam_obs, cam_obs.data(), no * 4, hipMemcpyHostToDevice, s));
     SFM_HIP(hipMemcpyAsync(p->d_cstart, cstart.data(), cstart.size() * 4, hipMemcpyHostToDevice, s));
     SFM_HIP(hipMemsetAsync(p->d_camlin, 0, (size_t)CAMLIN * nc * sizeof(double), s));
+    SFM_HIP(hipMemsetAsync(p->d_count, 0, 8 * sizeof(unsigned), s));
     if (p->ndiag_items) {
         SFM_HIP(hipMemcpyAsync(p->d_items, items.data(), items.size() * sizeof(PairItem), hipMemcpyHostToDevice, s));
         SFM_HIP(hipMemcpyAsync(p->d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), hipMemcpyHostToDevice, s));
@@ -1805,43 +1894,39 @@ static int allreduce(sfm_ba_problem *p, double *buf, int64_t n) {
 }
 
 // launches one linearisation (J, V, g) and, into d_scal[8], the cost.
-static int run_linearize(sfm_ba_problem *p) {
+// want_cost: also sum the cost into d_scal[8] (the LM state takes it from
+// the first linearisation only; later costs come from the accepted trials)
+static int run_linearize(sfm_ba_problem *p, int par, int want_cost) {
     hipStream_t s = p->stream;
-    const int *glin = &p->d_lm->run_lin;
+    const int *glin = &p->d_lm[par].run_lin;
 
     const int gl = lanes_per_point("SFM_LINEARIZE_LANES", 4);
     const int nbl = std::max(1, ceil_div(p->np * gl, PT_THREADS));
 #define SFM_LIN(G)                                                                                                \
     hipLaunchKernelGGL(k_linearize<G>, dim3(nbl), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam, p->d_obs, \
-                       p->K, p->d_Rt, p->d_X, p->d_J, p->d_Vg, p->d_partial, glin)
+                       p->K, p->d_Rt, p->d_X, p->d_J, p->d_Vg, p->d_partial, p->d_count, p->d_scal + 8, want_cost, glin)
     switch (gl) { case 1: SFM_LIN(1); break; case 2: SFM_LIN(2); break; case 4: SFM_LIN(4); break; default: SFM_LIN(8); }
 #undef SFM_LIN
     SFM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, p->d_partial, nbl, 1, p->d_scal + 8, glin);
-    SFM_HIP(hipGetLastError());
     if (p->ndiag_items) {
         hipLaunchKernelGGL(k_camera_lin, dim3(p->ndiag_items), dim3(256), 0, s, p->d_items, p->d_cam_obs, p->d_J,
-                           p->d_slab2, glin);
-        SFM_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_camera_lin_finish, dim3(p->ndiag_blocks), dim3(64), 0, s, p->d_blocks, p->d_slab2,
-                           p->d_camlin, glin);
+                           p->d_slab2, p->d_blocks, p->ndiag_blocks, p->d_camlin, p->d_count + 2, glin);
         SFM_HIP(hipGetLastError());
     }
-    return allreduce(p, p->d_scal + 8, 1);
+    return want_cost ? allreduce(p, p->d_scal + 8, 1) : 0;
 }
 
 // one damped solve + trial evaluation (gated on the device LM state); leaves
 // d_scal = [cost_trial, model_p, dn_p, xn_p, model_c, dn_c, xn_c] and d_bad for
-// k_lm_decide.  ev: this iteration's timing-event slot (nullable).
-static int run_step(sfm_ba_problem *p, hipEvent_t *ev) {
+// k_lm_step.  ev: this iteration's timing-event slot (nullable).
+static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     hipStream_t s = p->stream;
     int rc;
     const bool timed = ev != nullptr;
-    const int *gst = &p->d_lm->run_step;
-    const double *lam = &p->d_lm->lambda;
+    const int *gst = &p->d_lm[par].run_step;
+    const double *lam = &p->d_lm[par].lambda;
+    int *bad = p->d_bad + par;
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_PREP], s));
-    SFM_HIP(hipMemsetAsync(p->d_payload, 0, p->payload_len * sizeof(double), s));
-    SFM_HIP(hipMemsetAsync(p->d_bad, 0, sizeof(int), s));
     hipLaunchKernelGGL(k_point_prep, dim3(std::max(1, ceil_div(p->no, OBS_THREADS))), dim3(OBS_THREADS), 0, s, (int64_t)p->no,
                        p->d_pt, p->d_pstart, p->d_cam, p->d_Rt, p->d_J, p->d_Vg, lam, p->d_Lq, p->d_Z, gst);
     SFM_HIP(hipGetLastError());
@@ -1860,24 +1945,21 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev) {
     if ((rc = allreduce(p, p->d_payload, p->payload_len - 1))) return rc;
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_COMM + 1], s));
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SOLVE], s));
-    if ((rc = launch_reduced_solve(p->ns, p->nsp, p->d_payload, lam, p->d_A, p->d_b, p->d_D, p->d_bad, s, p->tb,
-                                   gst)))
+    // the back substitution's epilogue forms the trial cameras (k_camera_trial's work)
+    const CamTrialArgs ct = {p->nc, p->ns, p->d_payload, lam, p->d_Rt, p->d_Rt2, p->d_scal + 4};
+    if ((rc = launch_reduced_solve(p->ns, p->nsp, p->d_payload, lam, p->d_A, p->d_b, p->d_D, bad, s, p->tb, gst,
+                                   ct)))
         return rc;
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SOLVE + 1], s));
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_TRIAL], s));
-    hipLaunchKernelGGL(k_camera_trial, dim3(1), dim3(256), 0, s, p->nc, p->d_b, p->d_payload, p->ns, lam, p->d_Rt,
-                       p->d_Rt2, p->d_scal + 4, gst);
-    SFM_HIP(hipGetLastError());
     const int gb = lanes_per_point("SFM_BACKSUB_LANES", 2);
     const int nbb = std::max(1, ceil_div(p->np * gb, PT_THREADS));
 #define SFM_BS(G)                                                                                                  \
     hipLaunchKernelGGL(k_backsub_trial<G>, dim3(nbb), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam,        \
                        p->d_obs, p->K, p->d_J, p->d_Vg, p->d_Lq, p->d_b, lam, p->d_Rt, p->d_Rt2, p->d_X, p->d_X2, \
-                       p->d_partial, gst)
+                       p->d_partial, p->d_count + 1, p->d_scal, gst)
     switch (gb) { case 1: SFM_BS(1); break; case 2: SFM_BS(2); break; case 4: SFM_BS(4); break; default: SFM_BS(8); }
 #undef SFM_BS
-    SFM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, p->d_partial, nbb, 4, p->d_scal, gst);
     SFM_HIP(hipGetLastError());
     if ((rc = allreduce(p, p->d_scal, 4))) return rc;
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_TRIAL + 1], s));
@@ -1898,7 +1980,7 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
     int batch = 8;
     if (const char *e = std::getenv("SFM_LM_BATCH")) batch = std::atoi(e);
     batch = std::min(std::max(batch, 1), kEvSlots);
-    hipLaunchKernelGGL(k_lm_reset, dim3(1), dim3(1), 0, s, p->d_lm, o->initial_lambda);
+    hipLaunchKernelGGL(k_lm_reset, dim3(1), dim3(1), 0, s, p->d_lm, o->initial_lambda, p->d_bad);
     SFM_HIP(hipGetLastError());
     LMState h{};
     h.lambda = o->initial_lambda;
@@ -1907,21 +1989,21 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
     for (int it = 0; it < o->max_iterations; ++it) {
         hipEvent_t *ev = p->ev_it + (size_t)(it % batch) * 2 * T_NT;
         SFM_HIP(hipEventRecord(ev[2 * T_LIN], s));
-        if ((rc = run_linearize(p))) return rc;
+        const int par = it & 1;  // the state of iteration it lives in d_lm[par]
+        if ((rc = run_linearize(p, par, it == 0))) return rc;
         SFM_HIP(hipEventRecord(ev[2 * T_LIN + 1], s));
         if (it == 0) {
             hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(1), 0, s, p->d_lm, p->d_scal + 8);
             SFM_HIP(hipGetLastError());
         }
-        if ((rc = run_step(p, ev))) return rc;
-        hipLaunchKernelGGL(k_lm_decide, dim3(1), dim3(1), 0, s, p->d_lm, p->d_scal, p->d_bad, o->max_iterations,
-                           o->fixed_iterations, o->function_tolerance, o->parameter_tolerance, o->initial_lambda);
-        SFM_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_lm_accept, dim3(ceil_div(nacc, 256)), dim3(256), 0, s, p->d_lm, p->np, p->nc, p->d_X,
+        if ((rc = run_step(p, ev, par))) return rc;
+        hipLaunchKernelGGL(k_lm_step, dim3(ceil_div(nacc, 256)), dim3(256), 0, s, p->d_lm + par, p->d_lm + (par ^ 1),
+                           p->d_scal, p->d_bad + par, p->d_bad + (par ^ 1), o->max_iterations, o->fixed_iterations,
+                           o->function_tolerance, o->parameter_tolerance, o->initial_lambda, p->np, p->nc, p->d_X,
                            p->d_X2, p->d_Rt, p->d_Rt2);
         SFM_HIP(hipGetLastError());
         if ((it + 1) % batch == 0 || it + 1 == o->max_iterations) {
-            SFM_HIP(hipMemcpyAsync(&h, p->d_lm, sizeof h, hipMemcpyDeviceToHost, s));
+            SFM_HIP(hipMemcpyAsync(&h, p->d_lm + ((it + 1) & 1), sizeof h, hipMemcpyDeviceToHost, s));
             SFM_HIP(hipStreamSynchronize(s));
             for (int j = it - it % batch; j <= it && j < h.iters; ++j) {  // iterations that ran
                 hipEvent_t *e = p->ev_it + (size_t)(j % batch) * 2 * T_NT;
@@ -1949,7 +2031,7 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
 }
 
 // Diagnostic entry: solves the SPD system S x = rhs (n x n, row-major) with
-// the reduced-camera solver of sfm_ba_solve (k_assemble + tiled Cholesky).
+// the reduced-camera solver of sfm_ba_solve (tiled Cholesky).
 extern "C" int sfm_reduced_solve(const double *S, const double *rhs, int32_t n, double *x, int device) {
     SFM_CHECK_ARG(S && rhs && x, "null pointer");
     SFM_CHECK_ARG(n >= 1, "n < 1");
@@ -1973,7 +2055,7 @@ extern "C" int sfm_reduced_solve(const double *S, const double *rhs, int32_t n, 
     SFM_HIP(hipMemsetAsync(c->buf[4].p, 0, sizeof(int), c->stream));
     if ((rc = launch_reduced_solve(n, nsp, d_pay, d_pay + nn + 3 * (size_t)n, c->buf[1].as<double>(),
                                    c->buf[2].as<double>(), c->buf[3].as<double>(), c->buf[4].as<int>(), c->stream,
-                                   tb, nullptr)))
+                                   tb, nullptr, CamTrialArgs{})))
         return rc;
     int bad = 0;
     SFM_HIP(hipMemcpyAsync(x, c->buf[2].p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
