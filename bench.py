@@ -40,15 +40,21 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 vector
 
 
+SWEEP_RANGES = 8  # k_schur_sweep's point ranges (SFM_SWEEP_RANGES default)
+
+
 def algorithmic_bytes(name, n_obs, n_pts, n_pairs, nblocks, ns):
     """Compulsory bytes one launch of each single-kernel family moves
-    (DESIGN.md §4): every array the kernel must read or write, once."""
-    if name == "schur_blocks":  # k_schur_pairs: Schur records (p, G) 128 B/obs, pair list, q, slab
-        return 128 * n_obs + 8 * n_pairs + 24 * n_pts + 16 * nblocks + 8 * (ns * ns + 3 * ns)
+    (DESIGN.md §4): every array the kernel must read or write, once.
+    n_pairs: off-diagonal co-observation pairs; nblocks: camera blocks i <= j."""
+    if name == "schur_blocks":  # k_schur_sweep + finish: Schur records (p, G, q) 128 B/obs staged once,
+        # staged-slot list 4 B/obs, pair list 4 B/pair, range slab written + read, payload written
+        return 128 * n_obs + 4 * n_obs + 4 * n_pairs + 2 * 336 * SWEEP_RANGES * nblocks + 8 * (ns * ns + 3 * ns)
     if name == "point_prep":    # J 96 B + cam 4 B read, Schur record 128 B written per obs; V,g / L,q per pt
         return (96 + 4 + 128) * n_obs + (72 + 72 + 4) * n_pts
-    if name == "linearize":     # obs, cam read, J 96 B written per obs; X, V,g per pt
-        return (16 + 4 + 96) * n_obs + (24 + 72 + 4) * n_pts
+    if name == "linearize":     # k_linearize: obs, cam read, J 96 B written per obs; X, V,g per pt
+        # + k_camera_lin: J 96 B + camera-major index 4 B per obs
+        return (16 + 4 + 96) * n_obs + (24 + 72 + 4) * n_pts + (96 + 4) * n_obs
     if name == "backsub_trial": # J, obs, cam per obs; V,g, L,q, X, X' per pt
         return (96 + 16 + 4) * n_obs + (72 + 72 + 24 + 24 + 4) * n_pts
     return None
@@ -57,7 +63,7 @@ def algorithmic_bytes(name, n_obs, n_pts, n_pairs, nblocks, ns):
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass
     (tools/profile_round.sh + tools/pmc_summary.py), or None."""
-    names = {"schur_blocks": "k_schur_pairs", "point_prep": "k_point_prep", "linearize": "k_linearize",
+    names = {"schur_blocks": "k_schur_sweep", "point_prep": "k_point_prep", "linearize": "k_linearize",
              "backsub_trial": "k_backsub_trial"}
     path = os.path.join(REPO, "profiles", "round1", "pmc_traffic.json")
     try:
@@ -69,8 +75,9 @@ def pmc_traffic(kernel):
 
 
 def n_pairs_of(pt_idx):
+    """off-diagonal co-observation pairs (two observations of one point)"""
     k = np.bincount(pt_idx)
-    return int((k * (k + 1) // 2).sum())
+    return int((k * (k - 1) // 2).sum())
 
 
 def cpu_baseline_ba(prob, K):
