@@ -761,8 +761,9 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
 //   tile (r, c), c > s : A_rc -= L_r,s-1 L_c,s-1^T
 //   tile (r, s), r > s : C_rs = A_rs - L_r,s-1 L_s,s-1^T, C_ss likewise
 //                        (recomputed identically by every column block),
-//                        wave 0 factors C_ss, then L_rs = C_rs L_ss^-T,
-//                        written with its mirror;
+//                        wave 0 factors C_ss and, in the same chain on its
+//                        other lanes, forms L_rs = C_rs L_ss^-T, written with
+//                        its mirror;
 //   tile (s, s)        : C_ss, factor, y_s = L_ss^-1 (b_s - L_s,s-1 y_s-1),
 //                        L_ss -> D[s & 1] (read-only copy of A_ss is still
 //                        in use by the other column blocks);
@@ -889,9 +890,15 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
     const int lane = t;
     const int li = lane < TB ? lane : TB - 1;
     double (*Cdd)[TB + 1] = (r > s) ? Cd : Ct;
+    // lanes [0, TB) hold the rows of C_ss; in a panel block lanes [TB, 2 TB)
+    // hold the rows of C_rs.  The right-looking factor step (scale column k
+    // by 1/L_kk, subtract L_jk times it from column j > k) is also the
+    // right-looking forward substitution x L_ss^T = c of a panel row, so one
+    // chain factors L_ss and forms L_rs = C_rs L_ss^-T
+    const bool prow = r > s && lane >= TB && lane < 2 * TB;
     double rw[TB], dinv[TB];
 #pragma unroll
-    for (int j = 0; j < TB; ++j) rw[j] = Cdd[li][j];
+    for (int j = 0; j < TB; ++j) rw[j] = prow ? Ct[lane - TB][j] : Cdd[li][j];
     chol_factor<TB>(rw, dinv, lane, bad);
     if (r == s) {
         double y = upd ? bvec[s0 + li] : assembled_b(payload, ns, li);
@@ -915,27 +922,10 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
         }
         return;
     }
-    // L_rs = C_rs L_ss^-T, one tile row per lane (L_jm = lane j's rw[m])
-    double x[TB];
-#pragma unroll
-    for (int j = 0; j < TB; ++j) x[j] = Ct[li][j];
-#pragma unroll
-    for (int j = 0; j < TB; ++j) {
-        double v0 = x[j], v1 = 0.0, v2 = 0.0, v3 = 0.0;
-#pragma unroll
-        for (int m = 0; m < j; ++m) {
-            const double tt = x[m] * readlane_f64(rw[m], j);
-            if ((m & 3) == 0) v0 -= tt;
-            else if ((m & 3) == 1) v1 -= tt;
-            else if ((m & 3) == 2) v2 -= tt;
-            else v3 -= tt;
-        }
-        x[j] = ((v0 + v1) + (v2 + v3)) * dinv[j];
-    }
     wave_sync_lds();
-    if (lane < TB)
+    if (prow)
 #pragma unroll
-        for (int j = 0; j < TB; ++j) Lr[lane][j] = x[j];
+        for (int j = 0; j < TB; ++j) Lr[lane - TB][j] = rw[j];
     wave_sync_lds();
     for (int e = lane; e < TB * TB; e += 64)
         A[(int64_t)(r0 + e / TB) * nsp + s0 + e % TB] = Lr[e / TB][e % TB];
