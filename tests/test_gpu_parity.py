@@ -522,6 +522,18 @@ def test_ba_matches_oracle_midsize(core):
     assert abs(ro_r - rg_r) <= 1e-4 * ro_r
 
 
+def test_ba_many_cameras_split_rows(core):
+    """356 cameras: the Schur sweep splits camera rows over several specs
+    (rows longer than a workgroup's lane budget) and the reduced system is
+    2136 x 2136 (134 tile columns); three LM iterations against the C oracle."""
+    p = syn.ba_problem(356, 2000, 3, seed=11, dense=False)
+    cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
+    _, _, ro = O.ba_lm(cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K, max_iterations=3)
+    _, _, rg = core.ba_lm(cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K, max_iterations=3)
+    assert rg["iterations"] == ro["iterations"] and rg["accepted"] == ro["accepted"]
+    assert abs(rg["cost"] - ro["cost"]) <= 1e-7 * ro["cost"], (rg["cost"], ro["cost"])
+
+
 def test_ba_cfg4_full_size_properties(core):
     """cfg4 (50 cams / 100k pts / 1M obs): converges to the noise floor,
     deterministic run to run."""
