@@ -129,10 +129,14 @@ def next_rows(core, local_rank, cpu):
     random.seed(0)
     hs = core.sample_table(5000, 4, 16384)
     core.ransac_h4(h1, h2, hs, 30.0)
-    t = time.perf_counter()
     core.ransac_h4(h1, h2, hs, 30.0)
-    te = time.perf_counter() - t
     tk = core.last_timings()[1] * 1e-3
+    random.seed(0)
+    core.ransac_h4_pyrandom(h1, h2, 16384, 30.0)  # the drop-in's call: in-call sampling
+    random.seed(0)
+    t = time.perf_counter()
+    core.ransac_h4_pyrandom(h1, h2, 16384, 30.0)
+    te = time.perf_counter() - t
     r = {"workload": "cfg2 5000 corr, 16384 4-point hypotheses, thr 30",
          "hyps_per_s_kernels": round(16384 / tk, 1), "hyps_per_s_end_to_end": round(16384 / te, 1)}
     if cpu:
@@ -248,12 +252,18 @@ def main():
     for _ in range(3):
         core.ransac_f8(x1, x2, samples, 0.06, device=local_rank)
     reps = 20
+    # end to end = the drop-in's whole call: the samples drawn from the global
+    # random stream inside it (chunked, overlapped with the GPU), upload,
+    # kernels, mask download
+    for _ in range(3):
+        random.seed(0)
+        core.ransac_f8_pyrandom(x1, x2, args.ransac_hyps, 0.06, device=local_rank)
     t = time.perf_counter()
     for _ in range(reps):
         random.seed(0)
-        s = core.sample_table(5000, 8, args.ransac_hyps)
-        best, F, mask, _ = core.ransac_f8(x1, x2, s, 0.06, device=local_rank)
+        best, F, mask, _, _ = core.ransac_f8_pyrandom(x1, x2, args.ransac_hyps, 0.06, device=local_rank)
     t_e2e = (time.perf_counter() - t) / reps
+    t_draw = core.last_timings()[6]
     kt = []
     for _ in range(reps):
         core.ransac_f8(x1, x2, samples, 0.06, device=local_rank)
@@ -308,6 +318,7 @@ def main():
                  "note": "cfg3 parity vs the reference least-squares oracle in tests/test_gpu_parity.py"},
         "ransac": {"workload": "cfg2: 5000 corr, 40% outliers", "hypotheses": args.ransac_hyps,
                    "hyps_per_s_end_to_end": round(args.ransac_hyps / t_e2e, 1),
+                   "host_sampling_ms": round(float(t_draw), 3),
                    "hyps_per_s_kernels": round(args.ransac_hyps / (k_all * 1e-3), 1),
                    "score_kernel_ms": round(float(k_score), 4), "best_iter": int(best), "inliers": int(mask.sum())},
     }

@@ -72,6 +72,15 @@ int sfm_f8_general(const double *x1, const double *x2, int64_t N, double *F, int
 int sfm_ransac_f8(const double *x1, const double *x2, int64_t N, const int32_t *samples, int64_t H,
                   double thr, int32_t *counts_out, int64_t *best_iter, double *F_best,
                   uint8_t *best_mask, int device);
+/* The same call with the H x 8 samples drawn inside it from the CPython
+ * random state st[625] (random.getstate()[1]: 624 MT19937 words + position;
+ * advanced in place exactly as H calls of random.sample(range(N), 8) would
+ * advance it).  The draw is replayed on the host in chunks and each chunk's
+ * upload / fit / score is enqueued as soon as it is drawn, so the GPU works
+ * while the host draws.  samples_out (H x 8, nullable) receives the table. */
+int sfm_ransac_f8_pyrandom(const double *x1, const double *x2, int64_t N, uint32_t *st, int64_t H,
+                           double thr, int32_t *counts_out, int64_t *best_iter, double *F_best,
+                           uint8_t *best_mask, int32_t *samples_out, int device);
 
 /* ---------------------------------------------------------------------
  * Homography (GetHomographyInliers.py)
@@ -89,6 +98,10 @@ int sfm_homography_general(const double *x1, const double *x2, int64_t N, double
 int sfm_ransac_h4(const double *x1, const double *x2, int64_t N, const int32_t *samples, int64_t H,
                   double thr, int32_t *counts_out, int64_t *best_iter, double *H_best,
                   uint8_t *best_mask, int device);
+/* sfm_ransac_h4 with in-call sampling (H x 4), as sfm_ransac_f8_pyrandom. */
+int sfm_ransac_h4_pyrandom(const double *x1, const double *x2, int64_t N, uint32_t *st, int64_t H,
+                           double thr, int32_t *counts_out, int64_t *best_iter, double *H_best,
+                           uint8_t *best_mask, int32_t *samples_out, int device);
 
 /* ---------------------------------------------------------------------
  * PnP (LinearPnP.py, PnPRANSAC.py, NonlinearPnP.py); K is 3x3 row-major.

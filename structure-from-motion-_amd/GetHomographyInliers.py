@@ -68,9 +68,10 @@ def get_homography_inliers(image1_coords_org, image2_coords_org, idx, threshold=
     if n_points < 4:  # :108-110, before any draw from the stream
         return None, np.array([])
     n_iter = max(int(n_max), 0)
-    samples = _core.sample_table(n_points, min(4, n_points), n_iter)
-    best, H_best, mask, _ = _core.ransac_h4(image1_coords_org.reshape(n_points, 2),
-                                            image2_coords_org.reshape(n_points, 2), samples, threshold)
+    # n_iter draws of random.sample(range(N), 4) from the global stream,
+    # replayed inside the call while the GPU scores the drawn chunks
+    best, H_best, mask, _, _ = _core.ransac_h4_pyrandom(image1_coords_org.reshape(n_points, 2),
+                                                        image2_coords_org.reshape(n_points, 2), n_iter, threshold)
     if best < 0:  # :159-161
         return None, np.array([])
     return H_best, idx[np.where(mask)[0]]

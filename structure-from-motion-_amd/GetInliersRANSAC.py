@@ -6,9 +6,10 @@ update) becomes one batched evaluation on the MI355X:
 
 1. the n_max samples are drawn from the GLOBAL ``random`` instance exactly as
    the reference draws them (n_max calls of random.sample(range(N), 8) in
-   iteration order, replayed natively and written back with setstate), so
-   the stream seen by later callers (PnPRANSAC, the next image pair) is
-   unchanged;
+   iteration order, replayed natively inside the C-ABI call, chunk by chunk
+   while the GPU scores the chunks already drawn, and written back with
+   setstate), so the stream seen by later callers (PnPRANSAC, the next image
+   pair) is unchanged;
 2. libsfmcore builds every hypothesis F (one thread each), scores every
    (hypothesis, correspondence) pair (one wavefront per hypothesis, LDS
    tiles, ballot popcount) and picks the first hypothesis with the strictly
@@ -53,9 +54,10 @@ def GetInliersRANSAC(points1, points2, index, threshold=0.06, n_max=1000):
     if n_points < 8:  # :38-40
         return np.array([]), index, None
     n_iter = max(int(n_max), 0)
-    samples = _core.sample_table(n_points, min(8, n_points), n_iter)
-    best, F_best, mask, _ = _core.ransac_f8(points1.reshape(n_points, 2), points2.reshape(n_points, 2),
-                                            samples, threshold)
+    # n_iter draws of random.sample(range(N), 8) from the global stream,
+    # replayed inside the call while the GPU scores the drawn chunks
+    best, F_best, mask, _, _ = _core.ransac_f8_pyrandom(points1.reshape(n_points, 2), points2.reshape(n_points, 2),
+                                                        n_iter, threshold)
     if best < 0:  # :95-96 (no hypothesis with a positive count)
         return np.array([]), index, None
     inlier_index = np.where(mask)[0]

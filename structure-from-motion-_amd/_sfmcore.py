@@ -61,9 +61,11 @@ SIGNATURES = [
     ("sfm_f8_batch", _c, [_d, _d, _i, _d, _c]),
     ("sfm_f8_general", _c, [_d, _d, _i, _d, _c]),
     ("sfm_ransac_f8", _c, [_d, _d, _i, _i32, _i, ctypes.c_double, _i32, _i64, _d, _u8, _c]),
+    ("sfm_ransac_f8_pyrandom", _c, [_d, _d, _i, _u32, _i, ctypes.c_double, _i32, _i64, _d, _u8, _i32, _c]),
     ("sfm_h4_batch", _c, [_d, _d, _i, _d, _c]),
     ("sfm_homography_general", _c, [_d, _d, _i, _d, _c]),
     ("sfm_ransac_h4", _c, [_d, _d, _i, _i32, _i, ctypes.c_double, _i32, _i64, _d, _u8, _c]),
+    ("sfm_ransac_h4_pyrandom", _c, [_d, _d, _i, _u32, _i, ctypes.c_double, _i32, _i64, _d, _u8, _i32, _c]),
     ("sfm_linear_pnp", _c, [_d, _d, _i, _d, _d, _d, _i32, _c]),
     ("sfm_pnp_ransac", _c, [_d, _d, _i, _d, _i32, _i, ctypes.c_double, _i32, _i32, _i64, _i64, _d, _d, _c]),
     ("sfm_nonlinear_pnp", _c, [_d, _d, _i, _d, _d, _d, ctypes.c_int32, _d, _d, _i32, _c]),
@@ -144,7 +146,7 @@ def sample_table(n, k, H):
     st = np.array(internal, dtype=np.uint32)
     out = np.empty((H, k), dtype=np.int32)
     _check(_lib.sfm_pyrandom_sample_table(_p(st, _u32), int(n), int(k), int(H), _p(out, _i32)))
-    random.setstate((version_, tuple(int(v) for v in st), gauss))
+    random.setstate((version_, tuple(st.tolist()), gauss))
     return out
 
 
@@ -184,6 +186,41 @@ def ransac_f8(x1, x2, samples, thr, want_counts=False, device=None):
     if b < 0:
         return -1, None, np.zeros(N, dtype=bool), counts
     return b, F.reshape(3, 3), mask.astype(bool), counts
+
+
+def _ransac_pyrandom(fn, x1, x2, H, thr, want_counts, want_samples, device):
+    """Shared body of the in-call-sampling RANSAC entries: the GLOBAL random
+    state goes in, comes back advanced as H random.sample draws would."""
+    require_device()
+    x1, x2 = _f64(x1), _f64(x2)
+    N = len(x1)
+    version_, internal, gauss = random.getstate()
+    st = np.array(internal, dtype=np.uint32)
+    counts = np.zeros(H, dtype=np.int32) if want_counts else None
+    samples = np.zeros((H, fn[1]), dtype=np.int32) if want_samples else None
+    best = np.zeros(1, dtype=np.int64)
+    M = np.zeros(9)
+    mask = np.zeros(N, dtype=np.uint8)
+    _check(fn[0](_p(x1), _p(x2), N, _p(st, _u32), int(H), float(thr), _p(counts, _i32) if want_counts else None,
+                 _p(best, _i64), _p(M), _p(mask, _u8), _p(samples, _i32) if want_samples else None,
+                 DEVICE if device is None else device))
+    random.setstate((version_, tuple(st.tolist()), gauss))
+    b = int(best[0])
+    if b < 0:
+        return -1, None, np.zeros(N, dtype=bool), counts, samples
+    return b, M.reshape(3, 3), mask.astype(bool), counts, samples
+
+
+def ransac_f8_pyrandom(x1, x2, H, thr, want_counts=False, want_samples=False, device=None):
+    """GetInliersRANSAC's whole loop with the H 8-point samples drawn inside
+    the call from the global random stream (sfm_ransac_f8_pyrandom).
+    Returns (best_iter or -1, F_best or None, mask, counts or None, samples or None)."""
+    return _ransac_pyrandom((_lib.sfm_ransac_f8_pyrandom, 8), x1, x2, H, thr, want_counts, want_samples, device)
+
+
+def ransac_h4_pyrandom(x1, x2, H, thr, want_counts=False, want_samples=False, device=None):
+    """get_homography_inliers' loop with in-call sampling (sfm_ransac_h4_pyrandom)."""
+    return _ransac_pyrandom((_lib.sfm_ransac_h4_pyrandom, 4), x1, x2, H, thr, want_counts, want_samples, device)
 
 
 def h4_batch(x1s, x2s):

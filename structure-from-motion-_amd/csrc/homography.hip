@@ -51,3 +51,12 @@ extern "C" int sfm_ransac_h4(const double *x1, const double *x2, int64_t N, cons
                              int device) {
     return ransac_run<HomModel>(x1, x2, N, samples, H, thr, counts_out, best_iter, H_best, best_mask, device);
 }
+
+// sfm_ransac_h4 with the samples drawn inside the call from the CPython
+// random state st[625] (in/out), pipelined with the GPU work.
+extern "C" int sfm_ransac_h4_pyrandom(const double *x1, const double *x2, int64_t N, uint32_t *st, int64_t H,
+                                      double thr, int32_t *counts_out, int64_t *best_iter, double *H_best,
+                                      uint8_t *best_mask, int32_t *samples_out, int device) {
+    return ransac_run_pysample<HomModel>(x1, x2, N, st, H, thr, counts_out, best_iter, H_best, best_mask,
+                                         samples_out, device);
+}

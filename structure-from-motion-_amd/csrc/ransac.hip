@@ -30,3 +30,13 @@ extern "C" int sfm_ransac_f8(const double *x1, const double *x2, int64_t N, cons
                              uint8_t *best_mask, int device) {
     return ransac_run<EpiModel>(x1, x2, N, samples, H, thr, counts_out, best_iter, F_best, best_mask, device);
 }
+
+// sfm_ransac_f8 with the samples drawn inside the call from the CPython
+// random state st[625] (in/out), pipelined with the GPU work.
+extern "C" int sfm_ransac_f8_pyrandom(const double *x1, const double *x2, int64_t N, uint32_t *st, int64_t H,
+                                      double thr, int32_t *counts_out, int64_t *best_iter, double *F_best,
+                                      uint8_t *best_mask, int32_t *samples_out, int device) {
+    return ransac_run_pysample<EpiModel>(x1, x2, N, st, H, thr, counts_out, best_iter, F_best, best_mask,
+                                         samples_out, device);
+}
+

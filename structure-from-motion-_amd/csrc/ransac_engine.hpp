@@ -15,8 +15,14 @@
 //                      the reference's strict '>' update, then the inlier
 //                      mask of the winner.
 #pragma once
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+
 #include "sfm_common.hpp"
 #include "sfm_geom.hpp"
+#include "pyrandom.hpp"
 
 namespace sfm {
 
@@ -54,9 +60,10 @@ struct HomModel {
 template <class M>
 __global__ void __launch_bounds__(256) k_fit_samples(const double2 *__restrict__ x1, const double2 *__restrict__ x2,
                                                      const int32_t *__restrict__ samples, int64_t H,
-                                                     double *__restrict__ out) {
+                                                     double *__restrict__ out, int32_t *__restrict__ counts) {
     const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (h >= H) return;
+    if (counts) counts[h] = 0;  // the point-sliced score accumulates into it
     double ax[M::K], ay[M::K], bx[M::K], by[M::K];
 #pragma unroll
     for (int i = 0; i < M::K; ++i) {
@@ -87,7 +94,7 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES) k_ransac_score(const double2
                                                                    const double2 *__restrict__ x2,
                                                                    int64_t N, const double *__restrict__ F,
                                                                    int64_t H, double thr,
-                                                                   int32_t *__restrict__ counts) {
+                                                                   int32_t *__restrict__ counts, int64_t slice) {
     __shared__ double2 s1[SCORE_TILE];
     __shared__ double2 s2[SCORE_TILE];
     const int lane = threadIdx.x & 63;
@@ -104,8 +111,10 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES) k_ransac_score(const double2
     int cnt = 0;
     const double thr_lo = thr >= 0 ? thr * (1.0 - 1e-4) : thr * (1.0 + 1e-4);
     const double thr_hi = thr >= 0 ? thr * (1.0 + 1e-4) : thr * (1.0 - 1e-4);
-    for (int64_t base = 0; base < N; base += SCORE_TILE) {
-        const int n = (int)min<int64_t>(SCORE_TILE, N - base);
+    // gridDim.y > 1: this workgroup scores correspondences [y*slice, (y+1)*slice)
+    const int64_t p0 = (int64_t)blockIdx.y * slice, p1 = min<int64_t>(N, p0 + slice);
+    for (int64_t base = p0; base < p1; base += SCORE_TILE) {
+        const int n = (int)min<int64_t>(SCORE_TILE, p1 - base);
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
             s1[i] = x1[base + i];
             s2[i] = x2[base + i];
@@ -124,7 +133,25 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES) k_ransac_score(const double2
         }
         __syncthreads();
     }
-    if (active && lane == 0) counts[h] = cnt;
+    if (active && lane == 0) {
+        if (gridDim.y == 1)
+            counts[h] = cnt;
+        else
+            atomicAdd(counts + h, cnt);
+    }
+}
+
+// Point slices for scoring nh hypotheses: enough workgroups to put ~4 on
+// every CU (a lone 8-wave group per CU leaves the DP pipes latency-bound),
+// slices a whole number of LDS tiles.
+static inline int64_t score_slice(int64_t nh, int64_t N, int *ny) {
+    const int64_t wg = (nh + SCORE_WAVES - 1) / SCORE_WAVES;
+    const int64_t tiles = (N + SCORE_TILE - 1) / SCORE_TILE;
+    int64_t y = std::min<int64_t>(tiles, std::max<int64_t>(1, (1024 + wg - 1) / wg));
+    const int64_t per = (tiles + y - 1) / y;
+    y = (tiles + per - 1) / per;
+    *ny = (int)y;
+    return per * SCORE_TILE;
 }
 
 // grid = 1 workgroup of 1024 threads
@@ -214,11 +241,14 @@ int ransac_run(const double *x1, const double *x2, int64_t N, const int32_t *sam
     SFM_HIP(hipMemcpyAsync(d2, x2, pb, hipMemcpyHostToDevice, s));
     SFM_HIP(hipMemcpyAsync(ds, samples, (size_t)H * M::K * sizeof(int32_t), hipMemcpyHostToDevice, s));
     SFM_HIP(hipEventRecord(c->ev[1], s));
-    hipLaunchKernelGGL(k_fit_samples<M>, dim3(ceil_div(H, 256)), dim3(256), 0, s, d1, d2, ds, H, dF);
+    int ny;
+    const int64_t slice = score_slice(H, N, &ny);
+    hipLaunchKernelGGL(k_fit_samples<M>, dim3(ceil_div(H, 64)), dim3(64), 0, s, d1, d2, ds, H, dF,
+                       ny > 1 ? dcnt : nullptr);
     SFM_HIP(hipGetLastError());
     SFM_HIP(hipEventRecord(c->ev[2], s));
-    hipLaunchKernelGGL(k_ransac_score<M>, dim3(ceil_div(H, SCORE_WAVES)), dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
-                       dF, H, thr, dcnt);
+    hipLaunchKernelGGL(k_ransac_score<M>, dim3(ceil_div(H, SCORE_WAVES), ny), dim3(64 * SCORE_WAVES), 0, s, d1, d2,
+                       N, dF, H, thr, dcnt, slice);
     SFM_HIP(hipGetLastError());
     SFM_HIP(hipEventRecord(c->ev[3], s));
     hipLaunchKernelGGL(k_ransac_select<M>, dim3(1), dim3(1024), 0, s, d1, d2, N, dF, dcnt, H, thr, dbest, dFb, dmask);
@@ -233,6 +263,103 @@ int ransac_run(const double *x1, const double *x2, int64_t N, const int32_t *sam
     const double t[6] = {ev_ms(c->ev[0], c->ev[1]), ev_ms(c->ev[1], c->ev[4]), ev_ms(c->ev[4], c->ev[5]),
                          ev_ms(c->ev[2], c->ev[3]), ev_ms(c->ev[1], c->ev[2]), ev_ms(c->ev[3], c->ev[4])};
     set_timings(t, 6);
+    return 0;
+}
+
+// The drop-in's whole call with the samples drawn inside it: the CPython
+// random stream (MT19937 state st[625], in/out) is replayed on the host in
+// chunks of RP_CHUNK hypotheses into pinned memory, and each chunk's fit
+// (reading the rows in place, zero-copy) and score are enqueued as soon as
+// it is drawn, so the GPU works on
+// chunk c while the host draws chunk c + 1 (the draw is sequential by
+// construction: every hypothesis consumes a data-dependent number of MT
+// outputs).  samples_out (nullable) receives the table.  Timings as
+// ransac_run, plus [6] = host sampling ms.
+constexpr int64_t RP_CHUNK = 4096;
+static inline int64_t rp_chunk() {
+    static const int64_t c = [] {
+        const char *e = std::getenv("SFM_RP_CHUNK");
+        const long v = e ? std::atol(e) : 0;
+        return v > 0 ? (int64_t)v : RP_CHUNK;
+    }();
+    return c;
+}
+
+template <class M>
+int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t *st, int64_t H, double thr,
+                        int32_t *counts_out, int64_t *best_iter, double *F_best, uint8_t *best_mask,
+                        int32_t *samples_out, int device) {
+    SFM_CHECK_ARG(N >= M::K && H >= 0, "need N >= sample size and H >= 0");
+    SFM_CHECK_ARG(x1 && x2 && st && best_iter && F_best && best_mask, "null pointer");
+    SFM_CHECK_ARG(N < ((int64_t)1 << 31) && st[624] <= 624, "bad sizes / MT19937 position");
+    *best_iter = -1;
+    if (H == 0) return 0;
+    ThreadCtx *c = thread_ctx(device);
+    if (!c) return SFM_ERR_HIP;
+    const size_t pb = (size_t)N * sizeof(double2);
+    const size_t sb = (size_t)H * M::K * sizeof(int32_t);
+    const size_t sbp = (sb + 255) & ~(size_t)255;
+    int rc;
+    if ((rc = c->buf[0].reserve(pb)) || (rc = c->buf[1].reserve(pb)) ||
+        (rc = c->buf[3].reserve((size_t)H * 9 * sizeof(double))) ||
+        (rc = c->buf[4].reserve((size_t)H * sizeof(int32_t))) ||
+        (rc = c->pinned.reserve(sbp + 16 * sizeof(double) + (size_t)N)))
+        return rc;
+    double2 *d1 = c->buf[0].as<double2>(), *d2 = c->buf[1].as<double2>();
+    int32_t *dcnt = c->buf[4].as<int32_t>();
+    double *dF = c->buf[3].as<double>();
+    // Zero-copy through pinned host memory: the fit kernels read each chunk's
+    // sample rows straight from where the host replay wrote them, and the
+    // select kernel writes (best, F, mask) back the same way, so no SDMA copy
+    // (and no copy-engine/compute-queue handoff) sits between host and kernels.
+    int32_t *hs = c->pinned.as<int32_t>();
+    char *hout = c->pinned.as<char>() + sbp;
+    int64_t *dbest = reinterpret_cast<int64_t *>(hout);
+    double *dFb = reinterpret_cast<double *>(hout) + 2;
+    uint8_t *dmask = reinterpret_cast<uint8_t *>(hout) + 16 * sizeof(double);
+    hipStream_t s = c->stream;
+    const auto t0 = std::chrono::steady_clock::now();
+    SFM_HIP(hipEventRecord(c->ev[0], s));
+    SFM_HIP(hipMemcpyAsync(d1, x1, pb, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipMemcpyAsync(d2, x2, pb, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipEventRecord(c->ev[1], s));
+    PySampler ps(st, N, M::K);
+    double t_draw = 0;
+    const int64_t chunk = rp_chunk();
+    for (int64_t h0 = 0; h0 < H; h0 += chunk) {
+        const int64_t h1 = std::min(H, h0 + chunk), nh = h1 - h0;
+        const auto ta = std::chrono::steady_clock::now();
+        ps.draw(h0, h1, hs);
+        t_draw += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
+        int ny;
+        const int64_t slice = score_slice(nh, N, &ny);
+        hipLaunchKernelGGL(k_fit_samples<M>, dim3(ceil_div(nh, 64)), dim3(64), 0, s, d1, d2, hs + h0 * M::K, nh,
+                           dF + h0 * 9, ny > 1 ? dcnt + h0 : nullptr);
+        SFM_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_ransac_score<M>, dim3(ceil_div(nh, SCORE_WAVES), ny), dim3(64 * SCORE_WAVES), 0, s, d1,
+                           d2, N, dF + h0 * 9, nh, thr, dcnt + h0, slice);
+        SFM_HIP(hipGetLastError());
+    }
+    ps.save(st);
+    SFM_HIP(hipEventRecord(c->ev[3], s));
+    hipLaunchKernelGGL(k_ransac_select<M>, dim3(1), dim3(1024), 0, s, d1, d2, N, dF, dcnt, H, thr, dbest, dFb, dmask);
+    SFM_HIP(hipGetLastError());
+    SFM_HIP(hipEventRecord(c->ev[4], s));
+    if (counts_out) SFM_HIP(hipMemcpyAsync(counts_out, dcnt, (size_t)H * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    SFM_HIP(hipEventRecord(c->ev[5], s));
+    SFM_HIP(hipStreamSynchronize(s));
+    *best_iter = *dbest;
+    if (*best_iter >= 0) {
+        std::memcpy(F_best, dFb, 9 * sizeof(double));
+        std::memcpy(best_mask, dmask, (size_t)N);
+    } else {
+        std::memset(best_mask, 0, (size_t)N);
+    }
+    if (samples_out) std::memcpy(samples_out, hs, sb);
+    (void)t0;
+    const double t[7] = {ev_ms(c->ev[0], c->ev[1]), ev_ms(c->ev[1], c->ev[4]), ev_ms(c->ev[4], c->ev[5]),
+                         ev_ms(c->ev[1], c->ev[3]), 0.0, ev_ms(c->ev[3], c->ev[4]), t_draw};
+    set_timings(t, 7);
     return 0;
 }
 

@@ -9,6 +9,7 @@
 #include "sfm_common.hpp"
 #include "sfm_geom.hpp"
 #include "dlt_general.hpp"
+#include "pyrandom.hpp"
 
 namespace sfm {
 
@@ -149,48 +150,6 @@ __global__ void __launch_bounds__(256) k_ba_residuals(int64_t n_obs, const int32
     r[o] = make_double2(ob.x - u / (w + 1e-8), ob.y - v / (w + 1e-8));
 }
 
-// ------------------------------------------------------ CPython random replay
-// MT19937 exactly as CPython's _randommodule.c genrand_uint32, plus
-// random.py (3.10) _randbelow_with_getrandbits and sample()'s branches.
-struct PyMT {
-    uint32_t mt[624];
-    int idx;
-    uint32_t next() {
-        static const uint32_t mag01[2] = {0x0U, 0x9908b0dfU};
-        if (idx >= 624) {
-            int kk;
-            uint32_t y;
-            for (kk = 0; kk < 624 - 397; kk++) {
-                y = (mt[kk] & 0x80000000U) | (mt[kk + 1] & 0x7fffffffU);
-                mt[kk] = mt[kk + 397] ^ (y >> 1) ^ mag01[y & 0x1U];
-            }
-            for (; kk < 623; kk++) {
-                y = (mt[kk] & 0x80000000U) | (mt[kk + 1] & 0x7fffffffU);
-                mt[kk] = mt[kk + (397 - 624)] ^ (y >> 1) ^ mag01[y & 0x1U];
-            }
-            y = (mt[623] & 0x80000000U) | (mt[0] & 0x7fffffffU);
-            mt[623] = mt[396] ^ (y >> 1) ^ mag01[y & 0x1U];
-            idx = 0;
-        }
-        uint32_t y = mt[idx++];
-        y ^= (y >> 11);
-        y ^= (y << 7) & 0x9d2c5680U;
-        y ^= (y << 15) & 0xefc60000U;
-        y ^= (y >> 18);
-        return y;
-    }
-    uint32_t getrandbits(int k) { return k == 0 ? 0u : next() >> (32 - k); }
-    int64_t randbelow(int64_t n) {
-        if (n == 0) return 0;
-        int k = 0;
-        for (uint64_t m = (uint64_t)n; m; m >>= 1) ++k;  // n.bit_length()
-        if (k > 32) return -1;  // not needed for N < 2^31
-        uint32_t r = getrandbits(k);
-        while ((int64_t)r >= n) r = getrandbits(k);
-        return r;
-    }
-};
-
 }  // namespace sfm
 
 using namespace sfm;
@@ -212,37 +171,9 @@ extern "C" int sfm_pyrandom_sample_table(uint32_t *st, int64_t n, int32_t k, int
     SFM_CHECK_ARG(st && (out || H == 0), "null pointer");
     SFM_CHECK_ARG(k >= 0 && k <= n && n < (int64_t)1 << 31, "need 0 <= k <= n < 2^31");
     SFM_CHECK_ARG(st[624] <= 624, "bad MT19937 position");
-    PyMT m;
-    std::memcpy(m.mt, st, sizeof m.mt);
-    m.idx = (int)st[624];
-    int64_t setsize = 21;
-    if (k > 5) setsize += (int64_t)std::pow(4.0, std::ceil(std::log((double)k * 3) / std::log(4.0)));
-    std::vector<int32_t> pool;
-    for (int64_t h = 0; h < H; ++h) {
-        int32_t *res = out + h * k;
-        if (n <= setsize) {
-            pool.resize(n);
-            for (int64_t i = 0; i < n; ++i) pool[i] = (int32_t)i;
-            for (int32_t i = 0; i < k; ++i) {
-                const int64_t j = m.randbelow(n - i);
-                res[i] = pool[j];
-                pool[j] = pool[n - i - 1];
-            }
-        } else {
-            for (int32_t i = 0; i < k; ++i) {
-                int64_t j;
-                for (;;) {
-                    j = m.randbelow(n);
-                    bool dup = false;
-                    for (int32_t q = 0; q < i; ++q) dup |= (res[q] == (int32_t)j);
-                    if (!dup) break;
-                }
-                res[i] = (int32_t)j;
-            }
-        }
-    }
-    std::memcpy(st, m.mt, sizeof m.mt);
-    st[624] = (uint32_t)m.idx;
+    PySampler ps(st, n, k);
+    ps.draw(0, H, out);
+    ps.save(st);
     return 0;
 }
 

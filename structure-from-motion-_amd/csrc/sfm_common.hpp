@@ -57,12 +57,36 @@ struct DevBuf {
     }
 };
 
+// Pinned host scratch that only grows (async uploads from it overlap host work).
+struct HostBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    int reserve(size_t n) {
+        if (n <= bytes) return 0;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+        size_t want = n + n / 4 + 256;
+        if (hipHostMalloc(&p, want) != hipSuccess) {
+            set_error("hipHostMalloc(%zu) failed", want);
+            return SFM_ERR_NOMEM;
+        }
+        bytes = want;
+        return 0;
+    }
+    template <class T> T *as() const { return reinterpret_cast<T *>(p); }
+    ~HostBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+
 // One per (host thread, device): its own stream makes entry points reentrant.
 struct ThreadCtx {
     int device = -1;
     hipStream_t stream = nullptr;
     hipEvent_t ev[8] = {};
     DevBuf buf[12];
+    HostBuf pinned;
     ~ThreadCtx() {
         if (stream) {
             (void)hipSetDevice(device);

@@ -82,7 +82,10 @@ def test_perform_bundle_adjustment_signature():
 
 
 @pytest.mark.parametrize("n,k,H", [(5000, 8, 3000), (86, 8, 500), (85, 8, 500), (8, 8, 100), (558, 8, 1000),
-                                   (20, 4, 300), (3, 2, 50), (2 ** 20 + 3, 8, 200)])
+                                   (20, 4, 300), (3, 2, 50), (2 ** 20 + 3, 8, 200),
+                                   # set-rejection with frequent duplicates, every unrolled k
+                                   (25, 5, 800), (30, 4, 2000), (200, 7, 800), (100, 6, 800), (90, 8, 800),
+                                   (5000, 4, 3000), (9, 3, 200), (40, 12, 100)])
 def test_sample_table_replays_python_random(n, k, H):
     import _sfmcore
     random.seed(n * 31 + k)

@@ -134,6 +134,27 @@ def test_ransac_matches_oracle_random_inputs(core):
             assert rel(F2, F) < 1e-9
 
 
+@pytest.mark.parametrize("H", [1, 7, 2048, 5000])
+def test_ransac_pyrandom_matches_host_table(core, H):
+    """In-call sampling (chunked MT19937 replay pipelined with the GPU work)
+    draws exactly sample_table's table, gives the same counts / winner /
+    mask, and leaves the global random stream where sample_table leaves it."""
+    x1, x2, _, _ = syn.two_view(n=3000, seed=4)
+    for run, (tbl_fn, pyr_fn, kk, thr) in enumerate([(core.ransac_f8, core.ransac_f8_pyrandom, 8, 0.06),
+                                                     (core.ransac_h4, core.ransac_h4_pyrandom, 4, 30.0)]):
+        random.seed(100 + H + run)
+        samples = core.sample_table(3000, kk, H)
+        st_ref = random.getstate()
+        b0, M0, m0, c0 = tbl_fn(x1, x2, samples, thr, want_counts=True)
+        random.seed(100 + H + run)
+        b1, M1, m1, c1, s1 = pyr_fn(x1, x2, H, thr, want_counts=True, want_samples=True)
+        assert random.getstate() == st_ref
+        assert np.array_equal(s1, samples)
+        assert np.array_equal(c1, c0) and b1 == b0 and np.array_equal(m1, m0)
+        if b0 >= 0:
+            assert np.array_equal(M1, M0)
+
+
 def test_ransac_edge_cases(core):
     from GetInliersRANSAC import GetInliersRANSAC, get_inliers_ransac
     x1, x2, idx, _ = syn.two_view(n=200, seed=3)
