@@ -934,13 +934,95 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
 }
 
 // L^T x = y (y already in xg from the folded forward substitution), one
-// workgroup, tile rows from the bottom.  Per step the serial part is one
-// wave's 16-deep triangular solve on the diagonal tile; everything it waits
-// on is fetched one step ahead (the next diagonal tile and this thread's L
-// rows of the next step), and the pivots enter as reciprocals computed off
-// the chain, so the chain is readlane -> mul -> fma per column.
+// workgroup, tile rows from the bottom, with the critical path on one wave:
+//   wave 0 ("chain wave") solves tile k (16-deep readlane chain, pivots as
+//   reciprocals off the chain), then forms tile k's contribution to the
+//   rows of tile k-1 itself (acc, kept in registers), so the next solve
+//   only waits for that and for one barrier;
+//   waves 1.. ("row waves", row r = t - 64) apply tile k to the rows below
+//   tile k-1 one barrier later, overlapped with wave 0's next solve.
+// Every operand is fetched two steps ahead by the wave that uses it, with
+// branch-free clamped loads, and the barriers order LDS only (lds_barrier),
+// so the loads stay in flight across them.
 constexpr int SOLVE_THREADS = 512;
+constexpr int SOLVE_ROWS = SOLVE_THREADS - 64;  // rows owned by the row waves per pass
 constexpr int SOLVE_MAX = 4096;
+
+// workgroup barrier ordering LDS only: outstanding global loads stay in flight
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+template <int TB>
+struct ChainOps {
+    double c[TB];  // L[k0+m][k0+li]       (the diagonal tile, column li)
+    double p[TB];  // L[k0+m][k0-TB+li]    (tile k's block left of it: contribution to tile k-1)
+    double d;      // L[k0+li][k0+li]
+};
+
+template <int TB>
+__device__ __forceinline__ void chain_fetch(ChainOps<TB> &o, const double *__restrict__ A, int32_t nsp, int kt,
+                                            int li) {
+    const int kb = kt >= 0 ? kt * TB : 0, pc = kb >= TB ? kb - TB + li : 0;
+#pragma unroll
+    for (int m = 0; m < TB; ++m) {
+        const double *row = A + (int64_t)(kb + m) * nsp;
+        o.c[m] = row[kb + li];
+        o.p[m] = row[pc];
+    }
+    o.d = A[(int64_t)(kb + li) * nsp + kb + li];
+}
+
+template <int TB>
+__device__ __forceinline__ void chain_step(ChainOps<TB> &o, const double *__restrict__ A, int32_t nsp, int kt,
+                                           double *x, double &acc, int lane, int li) {
+    const int k0 = kt * TB;
+    const double rinv = 1.0 / o.d;  // off the chain
+    double v = x[k0 + li] - acc;
+#pragma unroll
+    for (int j = TB - 1; j >= 0; --j) {
+        const double vj = readlane_f64(v, j) * readlane_f64(rinv, j);
+        if (lane == j) v = vj;
+        if (lane < j) v -= o.c[j] * vj;
+    }
+    if (lane < TB) x[k0 + lane] = v;
+    double a = 0;
+#pragma unroll
+    for (int m = 0; m < TB; ++m) a += o.p[m] * readlane_f64(v, m);  // L[k0+m][k0-TB+li] x[k0+m]
+    acc = a;
+    chain_fetch<TB>(o, A, nsp, kt - 2, li);
+    lds_barrier();
+}
+
+template <int TB>
+__device__ __forceinline__ void rows_fetch(double (&l)[TB], const double *__restrict__ A, int32_t nsp, int kt,
+                                           int r) {
+    const int kb = kt >= 0 ? kt * TB : 0, col = r < nsp ? r : 0;
+#pragma unroll
+    for (int m = 0; m < TB; ++m) l[m] = A[(int64_t)(kb + m) * nsp + col];
+}
+
+template <int TB>
+__device__ __forceinline__ void rows_step(double (&l)[TB], const double *__restrict__ A, int32_t nsp, int kt,
+                                          double *x, int r) {
+    const int k0 = kt * TB, lim = k0 - TB;  // rows of tile k-1 get tile k from the chain wave
+    lds_barrier();
+    if (r < lim) {
+        double sacc = 0;
+#pragma unroll
+        for (int m = 0; m < TB; ++m) sacc += l[m] * x[k0 + m];
+        x[r] -= sacc;
+    }
+    for (int i = r + SOLVE_ROWS; i < lim; i += SOLVE_ROWS) {  // nsp > SOLVE_ROWS only
+        double sacc = 0;
+#pragma unroll 8
+        for (int m = 0; m < TB; ++m) sacc += A[(int64_t)(k0 + m) * nsp + i] * x[k0 + m];
+        x[i] -= sacc;
+    }
+    rows_fetch<TB>(l, A, nsp, kt - 2, r);
+}
 
 // trial cameras + camera part of the model decrease / norms, by one
 // workgroup of THREADS threads (run at the end of k_chol_backsolve, which
@@ -992,70 +1074,39 @@ __global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(double *__rest
                                                                   const int *__restrict__ gate) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
     __shared__ double x[SOLVE_MAX];
-    __shared__ double yt[TB];
-    const int t = threadIdx.x, lane = t & 63;
+    const int t = threadIdx.x;
     const int nT = nsp / TB;
-    const int li = lane < TB ? lane : TB - 1;
     for (int i = t; i < nsp; i += SOLVE_THREADS) x[i] = xg[i];
-    if (Dlast) {  // the last diagonal factor is still in the step kernel's scratch
-        const int k0 = nsp - TB;
-        for (int e = t; e < TB * TB; e += SOLVE_THREADS) {
-            const int i = e / TB, j = e % TB;
-            A[(int64_t)(k0 + i) * nsp + k0 + j] = i >= j ? Dlast[i * TB + j] : Dlast[j * TB + i];
+    if (t < 64) {  // chain wave
+        const int lane = t, li = lane < TB ? lane : TB - 1;
+        ChainOps<TB> oa, ob;
+        chain_fetch<TB>(oa, A, nsp, nT - 1, li);
+#pragma unroll
+        for (int m = 0; m < TB; ++m) oa.c[m] = Dlast[m * TB + li];  // the last diagonal factor is
+        oa.d = Dlast[li * TB + li];                                 // still in the step kernel's scratch
+        chain_fetch<TB>(ob, A, nsp, nT - 2, li);
+        double acc = 0;
+        lds_barrier();  // x staged
+        int kt = nT - 1;
+        for (; kt >= 1; kt -= 2) {
+            chain_step<TB>(oa, A, nsp, kt, x, acc, lane, li);
+            chain_step<TB>(ob, A, nsp, kt - 1, x, acc, lane, li);
         }
+        if (kt == 0) chain_step<TB>(oa, A, nsp, 0, x, acc, lane, li);
+    } else {  // row waves
+        const int r = t - 64;
+        double la[TB], lb[TB];
+        rows_fetch<TB>(la, A, nsp, nT - 1, r);
+        rows_fetch<TB>(lb, A, nsp, nT - 2, r);
+        lds_barrier();  // x staged
+        int kt = nT - 1;
+        for (; kt >= 1; kt -= 2) {
+            rows_step<TB>(la, A, nsp, kt, x, r);
+            rows_step<TB>(lb, A, nsp, kt - 1, x, r);
+        }
+        if (kt == 0) rows_step<TB>(la, A, nsp, 0, x, r);
     }
-    __syncthreads();
-    // step nT-1 operands
-    double lpre[TB], cl[TB];  // lpre[m] = L[k0+m][t]; cl[m] = L[k0+m][k0+li] (wave 0)
-    {
-        const int k0 = (nT - 1) * TB;
-#pragma unroll
-        for (int m = 0; m < TB; ++m) {
-            lpre[m] = t < k0 ? A[(int64_t)(k0 + m) * nsp + t] : 0.0;
-            cl[m] = t < 64 ? A[(int64_t)(k0 + m) * nsp + k0 + li] : 0.0;
-        }
-    }
-    for (int kt = nT - 1; kt >= 0; --kt) {
-        const int k0 = kt * TB;
-        // next step's operands, in flight during this step
-        double lnx[TB], cnx[TB];
-        const int k1 = k0 - TB;
-#pragma unroll
-        for (int m = 0; m < TB; ++m) {
-            lnx[m] = (kt > 0 && t < k1) ? A[(int64_t)(k1 + m) * nsp + t] : 0.0;
-            cnx[m] = (kt > 0 && t < 64) ? A[(int64_t)(k1 + m) * nsp + k1 + li] : 0.0;
-        }
-        if (t < 64) {
-            const double rinv = 1.0 / cl[li];  // 1 / L[k0+li][k0+li], off the chain
-            double v = x[k0 + li];
-#pragma unroll
-            for (int j = TB - 1; j >= 0; --j) {
-                const double vj = readlane_f64(v, j) * readlane_f64(rinv, j);
-                if (lane == j) v = vj;
-                if (lane < j) v -= cl[j] * vj;
-            }
-            if (lane < TB) { x[k0 + lane] = v; yt[lane] = v; }
-        }
-        __syncthreads();
-        if (t < k0) {
-            double sacc = 0;
-#pragma unroll
-            for (int m = 0; m < TB; ++m) sacc += lpre[m] * yt[m];  // L[k0+m][t]
-            x[t] -= sacc;
-        }
-        for (int i = t + SOLVE_THREADS; i < k0; i += SOLVE_THREADS) {
-            double sacc = 0;
-#pragma unroll 8
-            for (int m = 0; m < TB; ++m) sacc += A[(int64_t)(k0 + m) * nsp + i] * yt[m];  // L[k0+m][i]
-            x[i] -= sacc;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int m = 0; m < TB; ++m) {
-            lpre[m] = lnx[m];
-            cl[m] = cnx[m];
-        }
-    }
+    lds_barrier();
     for (int i = t; i < nsp; i += SOLVE_THREADS) xg[i] = x[i];
     if (ct.nc > 0) {
         __shared__ double red[3][SOLVE_THREADS];
