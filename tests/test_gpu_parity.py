@@ -570,6 +570,20 @@ def test_ba_cfg4_full_size_properties(core):
     assert abs(0.5 * r @ r - r1["cost"]) <= 1e-8 * r1["cost"]
 
 
+def test_ba_cfg5_full_size_properties(core):
+    """cfg5 (200 cams / 500k pts / ~4M obs, reduced system 1200 x 1200 =
+    75 tile columns, rows split across specs): converges to the noise floor
+    and the reported cost is the cost of the returned parameters."""
+    p = syn.ba_problem_cfg("cfg5", dense=False)
+    cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
+    c1, x1, r1 = core.ba_lm(cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K, max_iterations=30)
+    n = len(p["cam_idx"])
+    assert r1["cost"] < r1["cost0"]
+    assert syn.rmse_from_cost(r1["cost"], n) < 0.75  # pixel noise sigma 0.5 per axis
+    r = core.ba_residuals(c1, x1, p["cam_idx"], p["pt_idx"], p["obs"], K)
+    assert abs(0.5 * r @ r - r1["cost"]) <= 1e-8 * r1["cost"]
+
+
 def test_perform_bundle_adjustment_coo_equals_dense(core, capsys):
     """The COO store path (no dense n_features x n_images matrices) gives the
     dense path's observations, solve and outputs."""
