@@ -146,30 +146,38 @@ __device__ __forceinline__ void grid_sum_last(double (&v)[NV], double *partial, 
     }
     __syncthreads();
     if (!last) return;
-    __shared__ double tot[PT_THREADS];
-    for (int k = 0; k < NV; ++k) {
-        double s = 0;
-        for (unsigned b0 = threadIdx.x; b0 < nblk; b0 += 16 * PT_THREADS) {
-            double v16[16];  // 16 independent sc1 loads in flight, summed in block order
+    // all NV sums at once: NV x 16 independent sc1 loads in flight per
+    // thread, one tree -- per value the same order as summing them one by one
+    __shared__ double tot[NV][PT_THREADS];
+    double s[NV];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const unsigned b = b0 + u * PT_THREADS;
-                v16[u] = b < nblk ? __hip_atomic_load(partial + (int64_t)NV * b + k, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT)
-                                  : 0.0;
-            }
+    for (int k = 0; k < NV; ++k) s[k] = 0;
+    for (unsigned b0 = threadIdx.x; b0 < nblk; b0 += 16 * PT_THREADS) {
+        double v16[NV][16];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) s += v16[u];
+        for (int u = 0; u < 16; ++u) {
+            const unsigned b = b0 + u * PT_THREADS;
+#pragma unroll
+            for (int k = 0; k < NV; ++k)
+                v16[k][u] = b < nblk ? __hip_atomic_load(partial + (int64_t)NV * b + k, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)
+                                     : 0.0;
         }
-        tot[threadIdx.x] = s;
-        __syncthreads();
-        for (int st = PT_THREADS / 2; st > 0; st >>= 1) {
-            if ((int)threadIdx.x < st) tot[threadIdx.x] += tot[threadIdx.x + st];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) out[k] = tot[0];
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+#pragma unroll
+            for (int u = 0; u < 16; ++u) s[k] += v16[k][u];
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) tot[k][threadIdx.x] = s[k];
+    __syncthreads();
+    for (int st = PT_THREADS / 2; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) tot[k][threadIdx.x] += tot[k][threadIdx.x + st];
         __syncthreads();
     }
+    if (threadIdx.x < NV) out[threadIdx.x] = tot[threadIdx.x][0];
     if (threadIdx.x == 0) *counter = 0u;
 }
 
