@@ -703,8 +703,16 @@ __global__ void __launch_bounds__(256) k_camera_lin(const PairItem *__restrict__
         const BlockInfo bi = blocks[e / CAMLIN];
         const int k = e % CAMLIN;
         double v = 0;
-        for (int i = bi.first_item; i < bi.last_item; ++i)
-            v += __hip_atomic_load(slab2 + (int64_t)CAMLIN * i + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int i0 = bi.first_item; i0 < bi.last_item; i0 += 8) {  // 8 sc1 loads in flight, summed in order
+            double v8[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                v8[u] = i0 + u < bi.last_item ? __hip_atomic_load(slab2 + (int64_t)CAMLIN * (i0 + u) + k,
+                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                              : 0.0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v += v8[u];
+        }
         camlin[CAMLIN * bi.i + k] = v;
     }
     if (threadIdx.x == 0) *counter = 0u;
@@ -1804,11 +1812,12 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     // camera items for k_camera_lin: chunks of each camera's observations
     std::vector<BlockInfo> blocks;
     std::vector<PairItem> items;
+    const int cam_chunk = std::max(64, env_int("SFM_CAM_CHUNK", CAM_CHUNK));
     for (int c = 0; c < nc; ++c) {
         BlockInfo bi;
         bi.i = c; bi.j = c; bi.first_item = (int32_t)items.size();
-        for (int32_t k = cstart[c]; k < cstart[c + 1]; k += CAM_CHUNK)
-            items.push_back({c, k, std::min<int32_t>(cstart[c + 1], k + CAM_CHUNK), 1});
+        for (int32_t k = cstart[c]; k < cstart[c + 1]; k += cam_chunk)
+            items.push_back({c, k, std::min<int32_t>(cstart[c + 1], k + cam_chunk), 1});
         bi.last_item = (int32_t)items.size();
         if (bi.last_item > bi.first_item) blocks.push_back(bi);
     }
