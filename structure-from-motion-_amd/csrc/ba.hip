@@ -386,7 +386,25 @@ __global__ void __launch_bounds__(OBS_THREADS) k_point_prep(int64_t no, const in
     }
 }
 
-// Payload layout (doubles): S[ns*ns] | diagU[ns] | gc[ns] | bZ[ns] | cost
+// Payload layout (doubles): S as its upper-triangle 6x6 camera blocks
+// (block (i <= j) at 36 * dense index, row-major) | diagU[ns] | gc[ns] |
+// bZ[ns] | cost.  Half the dense ns x ns, which is what the multi-GPU
+// all-reduce moves each iteration.
+__host__ __device__ __forceinline__ int64_t pay_nblk(int32_t ns) {
+    const int64_t nc = (ns + 5) / 6;
+    return nc * (nc + 1) / 2;
+}
+__host__ __device__ __forceinline__ int64_t pay_vec_base(int32_t ns) { return 36 * pay_nblk(ns); }
+// element (i, j) of the symmetric S
+__host__ __device__ __forceinline__ int64_t pay_index(int32_t ns, int i, int j) {
+    int bi = i / 6, bj = j / 6, ri = i % 6, rj = j % 6;
+    if (bi > bj) {
+        const int tb = bi; bi = bj; bj = tb;
+        const int tr = ri; ri = rj; rj = tr;
+    }
+    const int64_t nc = (ns + 5) / 6;
+    return 36 * ((int64_t)bi * nc - (int64_t)bi * (bi - 1) / 2 + (bj - bi)) + ri * 6 + rj;
+}
 constexpr int CAMLIN = 27;  // U_c (21, upper) | g_c (6)
 constexpr int ITEM_W = 42;  // 36 block + 6 bZ
 
@@ -749,18 +767,18 @@ __global__ void __launch_bounds__(64) k_schur_finish(int32_t ns, int32_t nbd, in
     if (t >= (diag ? ITEM_W : 36)) return;
     double v = 0;
     for (int r = 0; r < nrange; ++r) v += slab[((int64_t)r * nbd + blockIdx.x) * ITEM_W + t];
-    const int64_t base = (int64_t)ns * ns;
+    const int64_t base = pay_vec_base(ns);
     if (t < 36) {
         const int r = t / 6, c = t % 6;
-        const int64_t row = 6 * ij.x + r, col = 6 * ij.y + c;
+        const int64_t row = 6 * ij.x + r;
+        double *blk = payload + pay_index(ns, 6 * ij.x, 6 * ij.y);  // the block's (0, 0)
         if (diag) {
             const int lo = r < c ? r : c, hi = r < c ? c : r;
             const double u = camlin[CAMLIN * ij.x + lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];
-            payload[row * ns + col] = u - v;
+            blk[t] = u - v;
             if (r == c) payload[base + row] = u;  // diag(U)
         } else {
-            payload[row * ns + col] = -v;
-            payload[col * ns + row] = -v;
+            blk[t] = -v;
         }
     } else {
         const int r = t - 36;
@@ -825,15 +843,15 @@ __device__ __forceinline__ void chol_factor(double (&r)[TB], double (&dinv)[TB],
 __device__ __forceinline__ double assembled(const double *__restrict__ payload, int32_t ns, double lambda, int i,
                                             int j) {
     if (i < ns && j < ns) {
-        double v = payload[(int64_t)i * ns + j];
-        if (i == j) v += lambda * clampd(payload[(int64_t)ns * ns + i]);
+        double v = payload[pay_index(ns, i, j)];
+        if (i == j) v += lambda * clampd(payload[pay_vec_base(ns) + i]);
         return v;
     }
     return i == j ? 1.0 : 0.0;
 }
 
 __device__ __forceinline__ double assembled_b(const double *__restrict__ payload, int32_t ns, int i) {
-    const int64_t base = (int64_t)ns * ns;
+    const int64_t base = pay_vec_base(ns);
     return i < ns ? -payload[base + ns + i] + payload[base + 2 * ns + i] : 0.0;
 }
 
@@ -1066,7 +1084,7 @@ __device__ __forceinline__ void camera_trial(int32_t nc, const double *dc, const
                                              double *__restrict__ Rt_new, double *__restrict__ cam_out,
                                              double (*red)[THREADS]) {
     double m = 0, dn = 0, xn = 0;
-    const double *diagU = payload + (int64_t)ns * ns, *gc = diagU + ns;
+    const double *diagU = payload + pay_vec_base(ns), *gc = diagU + ns;
     for (int c = threadIdx.x; c < nc; c += THREADS) {
         const double *d = dc + 6 * c;
         double dR[9];
@@ -1849,7 +1867,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     p->sw_nchunk = sw.nchunk;
     p->sw_lds_bytes = sw.lds_bytes();
     p->pt_blocks = std::max(1, ceil_div(np_ * PT_GROUP, PT_THREADS));
-    p->payload_len = (int64_t)p->ns * p->ns + 3 * p->ns + 1;
+    p->payload_len = pay_vec_base(p->ns) + 3 * p->ns + 1;
     int rc;
     if ((rc = p->alloc(p->d_cam, no)) || (rc = p->alloc(p->d_pt, no)) || (rc = p->alloc(p->d_pstart, np_ + 1)) ||
         (rc = p->alloc(p->d_obs, no)) || (rc = p->alloc(p->d_cam_obs, no)) || (rc = p->alloc(p->d_cstart, nc + 1)) ||
@@ -2114,21 +2132,23 @@ extern "C" int sfm_reduced_solve(const double *S, const double *rhs, int32_t n, 
     if (!c) return SFM_ERR_HIP;
     const int tb = chol_tile(n);
     const int32_t nsp = (n + tb - 1) / tb * tb;
-    const size_t nn = (size_t)n * n;
     int rc;
-    if ((rc = c->buf[0].reserve((nn + 3 * (size_t)n + 1) * sizeof(double))) ||
+    const size_t pb = (size_t)pay_vec_base(n);
+    if ((rc = c->buf[0].reserve((pb + 3 * (size_t)n + 1) * sizeof(double))) ||
         (rc = c->buf[1].reserve((size_t)nsp * nsp * sizeof(double))) ||
         (rc = c->buf[2].reserve((size_t)nsp * sizeof(double))) ||
         (rc = c->buf[3].reserve(2 * 32 * 32 * sizeof(double))) || (rc = c->buf[4].reserve(sizeof(int))))
         return rc;
-    // payload = [S, diag U = 0, g = -rhs, sum Z q = 0], lambda = 0 (last slot)
-    std::vector<double> pay(nn + 3 * (size_t)n + 1, 0.0);
-    std::memcpy(pay.data(), S, nn * sizeof(double));
-    for (int32_t i = 0; i < n; ++i) pay[nn + n + i] = -rhs[i];
+    // payload = [S (upper camera blocks), diag U = 0, g = -rhs, sum Z q = 0], lambda = 0 (last slot)
+    std::vector<double> pay(pb + 3 * (size_t)n + 1, 0.0);
+    for (int32_t i = 0; i < n; ++i)
+        for (int32_t j = 0; j < n; ++j)
+            if (i / 6 <= j / 6) pay[pay_index(n, i, j)] = S[(size_t)i * n + j];
+    for (int32_t i = 0; i < n; ++i) pay[pb + n + i] = -rhs[i];
     double *d_pay = c->buf[0].as<double>();
     SFM_HIP(hipMemcpyAsync(d_pay, pay.data(), pay.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
     SFM_HIP(hipMemsetAsync(c->buf[4].p, 0, sizeof(int), c->stream));
-    if ((rc = launch_reduced_solve(n, nsp, d_pay, d_pay + nn + 3 * (size_t)n, c->buf[1].as<double>(),
+    if ((rc = launch_reduced_solve(n, nsp, d_pay, d_pay + pb + 3 * (size_t)n, c->buf[1].as<double>(),
                                    c->buf[2].as<double>(), c->buf[3].as<double>(), c->buf[4].as<int>(), c->stream,
                                    tb, nullptr, CamTrialArgs{})))
         return rc;
