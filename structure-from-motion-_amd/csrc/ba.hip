@@ -146,16 +146,17 @@ __device__ __forceinline__ void grid_sum_last(double (&v)[NV], double *partial, 
     }
     __syncthreads();
     if (!last) return;
-    // all NV sums at once: NV x 16 independent sc1 loads in flight per
-    // thread, one tree -- per value the same order as summing them one by one
+    // all NV sums at once: NV x GS_BATCH independent sc1 loads in flight
+    // per thread, one tree -- per value the same order as summing them one by one
     __shared__ double tot[NV][PT_THREADS];
     double s[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) s[k] = 0;
-    for (unsigned b0 = threadIdx.x; b0 < nblk; b0 += 16 * PT_THREADS) {
-        double v16[NV][16];
+    constexpr int GS_BATCH = NV > 1 ? 8 : 16;  // bounded so the tail does not set the kernel's VGPR count
+    for (unsigned b0 = threadIdx.x; b0 < nblk; b0 += GS_BATCH * PT_THREADS) {
+        double v16[NV][GS_BATCH];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
+        for (int u = 0; u < GS_BATCH; ++u) {
             const unsigned b = b0 + u * PT_THREADS;
 #pragma unroll
             for (int k = 0; k < NV; ++k)
@@ -166,7 +167,7 @@ __device__ __forceinline__ void grid_sum_last(double (&v)[NV], double *partial, 
 #pragma unroll
         for (int k = 0; k < NV; ++k)
 #pragma unroll
-            for (int u = 0; u < 16; ++u) s[k] += v16[k][u];
+            for (int u = 0; u < GS_BATCH; ++u) s[k] += v16[k][u];
     }
 #pragma unroll
     for (int k = 0; k < NV; ++k) tot[k][threadIdx.x] = s[k];
@@ -328,7 +329,7 @@ __global__ void __launch_bounds__(OBS_THREADS) k_point_prep(int64_t no, const in
     // with lane-consecutive 16-B pieces (a thread's own 128 B record written
     // directly is 8 stores at a 128-B lane stride: measured 58 -> 23 us when
     // the stores are dropped, i.e. the strided write was the bound)
-    __shared__ double2 zs[OBS_THREADS * 9];  // 8 pieces + 1 pad per record
+    __shared__ double2 zs[OBS_THREADS * 8];  // 8 pieces per record, XOR-swizzled against bank conflicts
     const double lambda = *lam;
     const int64_t o0 = (int64_t)blockIdx.x * OBS_THREADS;
     const int64_t o = o0 + threadIdx.x;
@@ -375,14 +376,14 @@ __global__ void __launch_bounds__(OBS_THREADS) k_point_prep(int64_t no, const in
         for (int c = 0; c < 3; ++c) z[3 + 3 * i + c] = A[0][i] * T[0][c] + A[1][i] * T[1][c];
     z[12] = qp[0]; z[13] = qp[1]; z[14] = qp[2]; z[15] = 0.0;
 #pragma unroll
-    for (int k = 0; k < ZS / 2; ++k) zs[threadIdx.x * 9 + k] = make_double2(z[2 * k], z[2 * k + 1]);
+    for (int k = 0; k < ZS / 2; ++k) zs[threadIdx.x * 8 + (k ^ (threadIdx.x & 7))] = make_double2(z[2 * k], z[2 * k + 1]);
     }
     __syncthreads();
     double2 *zout = reinterpret_cast<double2 *>(Z + (int64_t)ZS * o0);
 #pragma unroll
     for (int u = 0; u < ZS / 2; ++u) {
         const int k = threadIdx.x + OBS_THREADS * u, rec = k >> 3;
-        if (rec < nrec) zout[k] = zs[rec * 9 + (k & 7)];
+        if (rec < nrec) zout[k] = zs[rec * 8 + ((k & 7) ^ (rec & 7))];
     }
 }
 
