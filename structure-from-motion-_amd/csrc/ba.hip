@@ -1332,13 +1332,16 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
                                                               const int *__restrict__ gate) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
     const double lambda = *lam;
-    const int64_t gt = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x;
-    const int64_t p = gt / G;  // G lanes per point, striding over its observations
-    const int sub = (int)(gt % G);
     double K[9];
 #pragma unroll
     for (int i = 0; i < 9; ++i) K[i] = Km.k[i];
     double acc[4] = {0, 0, 0, 0};
+    // grid-stride over points (a bounded grid keeps the per-block partial
+    // store + arrival count, and the last block's sum, small)
+    for (int64_t gt = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x; gt / G < np_;
+         gt += (int64_t)gridDim.x * PT_THREADS) {
+    const int64_t p = gt / G;  // G lanes per point, striding over its observations
+    const int sub = (int)(gt % G);
     const bool live = p < np_;
     const int32_t o0 = live ? pstart[p] : 0, o1 = live ? pstart[p + 1] : 0;
     // W^T dc = Jp^T (Jc dc) = R^T A^T (A (dtheta x p + dt)), summed over the point's observations
@@ -1385,6 +1388,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
             }
         }
         for (int32_t o = o0 + sub; o < o1; o += G) acc[0] += obs_cost(Rt_new + 12 * cam[o], xn, K, obs[o]);
+    }
     }
     grid_sum_last<4>(acc, partial, counter, out);
 }
@@ -2047,7 +2051,9 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SOLVE + 1], s));
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_TRIAL], s));
     const int gb = lanes_per_point("SFM_BACKSUB_LANES", 2);
-    const int nbb = std::max(1, ceil_div(p->np * gb, PT_THREADS));
+    // grid-stride: 1024 workgroups (4 per CU); measured at cfg4 (1563 needed
+    // without the stride): 512 -> 49 us, 896..1152 -> 43 us, 2048+ -> 51 us
+    const int nbb = std::max(1, std::min(ceil_div(p->np * gb, PT_THREADS), env_int("SFM_BACKSUB_BLOCKS", 1024)));
 #define SFM_BS(G)                                                                                                  \
     hipLaunchKernelGGL(k_backsub_trial<G>, dim3(nbb), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam,        \
                        p->d_obs, p->K, p->d_J, p->d_Vg, p->d_Lq, p->d_b, lam, p->d_Rt, p->d_Rt2, p->d_X, p->d_X2, \
