@@ -1551,7 +1551,11 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     P.hdr_cap = (max_ng + 4 + 63) / 64 * 64;
     // ranges of equal observation count; chunks small enough that two
     // (chunk, spec) buffers fit the LDS and the chunk's records an XCD's L2
-    P.nrange = std::max(NXCD, env_int("SFM_SWEEP_RANGES", 8) / NXCD * NXCD);
+    // 8 ranges while nspec x 8 workgroups fit one pass over the 256 CUs
+    // (cfg4: 25 specs, 200 workgroups); past that 16, which halves the last
+    // partial pass (cfg5, 100 specs: 0.969 -> 0.885 ms; cfg4 at 16: 0.145 -> 0.161 ms)
+    const int nr_dflt = P.nspec * NXCD <= 256 ? 8 : 16;
+    P.nrange = std::max(NXCD, env_int("SFM_SWEEP_RANGES", nr_dflt) / NXCD * NXCD);
     int chunk_obs = std::max(64, std::min(env_int("SFM_SWEEP_CHUNK", 11264), 65535));
     std::vector<int32_t> ccount(nc), cpairs(P.nspec);
     std::vector<int64_t> cut;  // chunk first points
