@@ -38,10 +38,14 @@ __device__ __forceinline__ bool epi_inlier_fast(const double *F, double x, doubl
     const double e = u * a0 + v * a1 + a2;
     const double ae = fabs(e);
     const double qa = a0 * a0 + a1 * a1, qb = b0 * b0 + b1 * b1;
-    const double sa = qa * __builtin_amdgcn_rsq(qa), sb = qb * __builtin_amdgcn_rsq(qb);
-    const double ap = (ae * __builtin_amdgcn_rcp(sa + 1e-8) + ae * __builtin_amdgcn_rcp(sb + 1e-8)) * 0.5;
-    const bool sure_in = ap < thr_lo && qa > 1e-280 && qb > 1e-280;
-    const bool sure_out = ap > thr_hi && qa > 1e-280 && qb > 1e-280 && qa < 1e280 && qb < 1e280;
+    // 1 / (sqrt(q) + 1e-8) = r (1 - 1e-8 r + ...), r = rsq(q): first order,
+    // whose error (1e-8 r)^2 <= 1e-6 relative while q > 1e-10 -- no v_rcp
+    const double ra = __builtin_amdgcn_rsq(qa), rb = __builtin_amdgcn_rsq(qb);
+    const double ia = fma(-1e-8 * ra, ra, ra), ib = fma(-1e-8 * rb, rb, rb);
+    const double ap = ae * (ia + ib) * 0.5;
+    const bool ok = qa > 1e-10 && qb > 1e-10 && qa < 1e280 && qb < 1e280;
+    const bool sure_in = ap < thr_lo && ok;
+    const bool sure_out = ap > thr_hi && ok;
     if (sure_in) return true;
     if (sure_out) return false;
     const double d1 = ae / (sqrt(qa) + 1e-8);
