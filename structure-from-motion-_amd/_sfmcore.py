@@ -6,6 +6,7 @@ call raises ``SfmCoreError`` if no MI355X is visible.
 
 The device is ``$SFM_DEVICE`` (default 0).
 """
+import array
 import ctypes
 import os
 import random
@@ -138,15 +139,33 @@ def last_timings():
 
 
 # ------------------------------------------------------------------ random
+assert array.array("I").itemsize == 4
+
+
+def _mt_state():
+    """The global MT19937 state as a C uint32[625] (key + position) plus the
+    parts random.setstate needs back (array.array: ~3x cheaper than numpy
+    for the 625-int round trip, which sits inside every RANSAC call)."""
+    version_, internal, gauss = random.getstate()
+    return version_, array.array("I", internal), gauss
+
+
+def _mt_ptr(st):
+    return ctypes.cast(st.buffer_info()[0], _u32)
+
+
+def _mt_restore(version_, st, gauss):
+    random.setstate((version_, tuple(st), gauss))
+
+
 def sample_table(n, k, H):
     """H draws of random.sample(range(n), k) on the GLOBAL random instance,
     replayed natively; the global state is advanced exactly as the
     reference's loop (GetInliersRANSAC.py:53-55) would advance it."""
-    version_, internal, gauss = random.getstate()
-    st = np.array(internal, dtype=np.uint32)
+    version_, st, gauss = _mt_state()
     out = np.empty((H, k), dtype=np.int32)
-    _check(_lib.sfm_pyrandom_sample_table(_p(st, _u32), int(n), int(k), int(H), _p(out, _i32)))
-    random.setstate((version_, tuple(st.tolist()), gauss))
+    _check(_lib.sfm_pyrandom_sample_table(_mt_ptr(st), int(n), int(k), int(H), _p(out, _i32)))
+    _mt_restore(version_, st, gauss)
     return out
 
 
@@ -194,17 +213,16 @@ def _ransac_pyrandom(fn, x1, x2, H, thr, want_counts, want_samples, device):
     require_device()
     x1, x2 = _f64(x1), _f64(x2)
     N = len(x1)
-    version_, internal, gauss = random.getstate()
-    st = np.array(internal, dtype=np.uint32)
+    version_, st, gauss = _mt_state()
     counts = np.zeros(H, dtype=np.int32) if want_counts else None
     samples = np.zeros((H, fn[1]), dtype=np.int32) if want_samples else None
     best = np.zeros(1, dtype=np.int64)
     M = np.zeros(9)
     mask = np.zeros(N, dtype=np.uint8)
-    _check(fn[0](_p(x1), _p(x2), N, _p(st, _u32), int(H), float(thr), _p(counts, _i32) if want_counts else None,
+    _check(fn[0](_p(x1), _p(x2), N, _mt_ptr(st), int(H), float(thr), _p(counts, _i32) if want_counts else None,
                  _p(best, _i64), _p(M), _p(mask, _u8), _p(samples, _i32) if want_samples else None,
                  DEVICE if device is None else device))
-    random.setstate((version_, tuple(st.tolist()), gauss))
+    _mt_restore(version_, st, gauss)
     b = int(best[0])
     if b < 0:
         return -1, None, np.zeros(N, dtype=bool), counts, samples
