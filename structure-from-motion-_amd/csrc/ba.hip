@@ -122,6 +122,12 @@ __device__ __forceinline__ void block_sum_store(double (&v)[NV], double *out) {
 // returns nblk - 1 sums all partials in block order (sc1 loads) into
 // out[0..NV) and re-arms the counter.  The same summation order as a separate
 // k_finalize launch, so the result is deterministic.
+// counter block of grid_sum_last: [0] top, [1 + g] blocks with blockIdx % 8 == g,
+// one 128-B line each (arrivals on ONE word serialise at ~11-13 ns each:
+// 1024 blocks cost ~12 us; eight group words take them in parallel)
+constexpr int GS_STRIDE = 32;
+constexpr int GS_WORDS = 9 * GS_STRIDE;
+
 template <int NV>
 __device__ __forceinline__ void grid_sum_last(double (&v)[NV], double *partial, unsigned *counter, double *out) {
     __shared__ double red[PT_THREADS / 64][NV];
@@ -142,7 +148,14 @@ __device__ __forceinline__ void grid_sum_last(double (&v)[NV], double *partial, 
             __hip_atomic_store(partial + (int64_t)NV * blockIdx.x + k, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1;
+        // two-level arrival: the block counts in at its group's word; the
+        // group's last arriver counts the group in at the top word
+        const unsigned g = blockIdx.x % 8, ng = (nblk - g + 7) / 8, ngroups = nblk < 8 ? nblk : 8;
+        int l = 0;
+        if (__hip_atomic_fetch_add(counter + GS_STRIDE * (1 + g), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            ng - 1)
+            l = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1;
+        last = l;
     }
     __syncthreads();
     if (!last) return;
@@ -179,7 +192,7 @@ __device__ __forceinline__ void grid_sum_last(double (&v)[NV], double *partial, 
         __syncthreads();
     }
     if (threadIdx.x < NV) out[threadIdx.x] = tot[threadIdx.x][0];
-    if (threadIdx.x == 0) *counter = 0u;
+    if (threadIdx.x < 9) __hip_atomic_store(counter + GS_STRIDE * threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------ observation model
@@ -1897,7 +1910,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = p->alloc(p->d_D, 2 * 32 * 32)) ||
         (rc = p->alloc(p->d_partial, 4 * (int64_t)p->pt_blocks)) || (rc = p->alloc(p->d_scal, 16)) ||
         (rc = p->alloc(p->d_lm, 2)) ||
-        (rc = p->alloc(p->d_bad, 4)) || (rc = p->alloc(p->d_count, 8)))
+        (rc = p->alloc(p->d_bad, 4)) || (rc = p->alloc(p->d_count, 3 * GS_WORDS)))
         return rc;
     SFM_HIP(hipHostMalloc((void **)&p->h_scal, 16 * sizeof(double)));
     hipStream_t s = p->stream;
@@ -1910,7 +1923,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     if (no) SFM_HIP(hipMemcpyAsync(p->d_cam_obs, cam_obs.data(), no * 4, hipMemcpyHostToDevice, s));
     SFM_HIP(hipMemcpyAsync(p->d_cstart, cstart.data(), cstart.size() * 4, hipMemcpyHostToDevice, s));
     SFM_HIP(hipMemsetAsync(p->d_camlin, 0, (size_t)CAMLIN * nc * sizeof(double), s));
-    SFM_HIP(hipMemsetAsync(p->d_count, 0, 8 * sizeof(unsigned), s));
+    SFM_HIP(hipMemsetAsync(p->d_count, 0, 3 * GS_WORDS * sizeof(unsigned), s));
     if (p->ndiag_items) {
         SFM_HIP(hipMemcpyAsync(p->d_items, items.data(), items.size() * sizeof(PairItem), hipMemcpyHostToDevice, s));
         SFM_HIP(hipMemcpyAsync(p->d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), hipMemcpyHostToDevice, s));
@@ -2012,7 +2025,7 @@ static int run_linearize(sfm_ba_problem *p, int par, int want_cost) {
     SFM_HIP(hipGetLastError());
     if (p->ndiag_items) {
         hipLaunchKernelGGL(k_camera_lin, dim3(p->ndiag_items), dim3(256), 0, s, p->d_items, p->d_cam_obs, p->d_J,
-                           p->d_slab2, p->d_blocks, p->ndiag_blocks, p->d_camlin, p->d_count + 2, glin);
+                           p->d_slab2, p->d_blocks, p->ndiag_blocks, p->d_camlin, p->d_count + 2 * GS_WORDS, glin);
         SFM_HIP(hipGetLastError());
     }
     return want_cost ? allreduce(p, p->d_scal + 8, 1) : 0;
@@ -2061,7 +2074,7 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
 #define SFM_BS(G)                                                                                                  \
     hipLaunchKernelGGL(k_backsub_trial<G>, dim3(nbb), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam,        \
                        p->d_obs, p->K, p->d_J, p->d_Vg, p->d_Lq, p->d_b, lam, p->d_Rt, p->d_Rt2, p->d_X, p->d_X2, \
-                       p->d_partial, p->d_count + 1, p->d_scal, gst)
+                       p->d_partial, p->d_count + GS_WORDS, p->d_scal, gst)
     switch (gb) { case 1: SFM_BS(1); break; case 2: SFM_BS(2); break; case 4: SFM_BS(4); break; default: SFM_BS(8); }
 #undef SFM_BS
     SFM_HIP(hipGetLastError());
