@@ -121,7 +121,17 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES) k_ransac_score(const double2
         }
         __syncthreads();
         if (active && finite) {
-            for (int j = 0; j < n; j += 64) {
+            // two correspondences per lane per pass: independent chains for the
+            // FP64 pipe (the tile length is a multiple of 128 except the last)
+            int j = 0;
+            for (; j + 128 <= n; j += 128) {
+                const double2 p0 = s1[j + lane], q0 = s2[j + lane];
+                const double2 p1 = s1[j + 64 + lane], q1 = s2[j + 64 + lane];
+                const bool in0 = M::inlier_fast(f, p0, q0, thr, thr_lo, thr_hi);
+                const bool in1 = M::inlier_fast(f, p1, q1, thr, thr_lo, thr_hi);
+                cnt += __popcll(__ballot(in0)) + __popcll(__ballot(in1));
+            }
+            for (; j < n; j += 64) {
                 const int i = j + lane;
                 bool inl = false;
                 if (i < n) {
