@@ -428,7 +428,15 @@ __global__ void __launch_bounds__(64 * PNP_WAVES) k_pnp_score(const double *__re
         for (int i = threadIdx.x; i < n; i += blockDim.x) sx[i] = x[base + i];
         __syncthreads();
         if (active) {
-            for (int j = 0; j < n; j += 64) {
+            int j = 0;
+            for (; j + 128 <= n; j += 128) {  // two points per lane per pass: independent FP64 chains
+                const int i0 = j + lane, i1 = i0 + 64;
+                const double2 q0 = sx[i0], q1 = sx[i1];
+                const bool in0 = pnp_inlier(P, sX[3 * i0], sX[3 * i0 + 1], sX[3 * i0 + 2], q0.x, q0.y, thr);
+                const bool in1 = pnp_inlier(P, sX[3 * i1], sX[3 * i1 + 1], sX[3 * i1 + 2], q1.x, q1.y, thr);
+                cnt += __popcll(__ballot(in0)) + __popcll(__ballot(in1));
+            }
+            for (; j < n; j += 64) {
                 const int i = j + lane;
                 bool inl = false;
                 if (i < n) {
