@@ -671,17 +671,18 @@ __device__ void nlpnp_projection(const Cam3 &K, const double *p, double *P) {
 
 struct WGReduce {
     double *red;  // LDS, NL_THREADS
+    // wave totals by shuffles, then the NL_THREADS / 64 of them in a fixed
+    // order: two barriers per m-long sum instead of a 10-barrier LDS tree
     __device__ double sum(double v) const {
         const int t = threadIdx.x;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        __syncthreads();  // the previous sum's readers are done with red
+        if ((t & 63) == 0) red[t >> 6] = v;
         __syncthreads();
-        red[t] = v;
-        __syncthreads();
-        for (int w = NL_THREADS / 2; w > 0; w >>= 1) {
-            if (t < w) red[t] += red[t + w];
-            __syncthreads();
-        }
-        const double r = red[0];
-        __syncthreads();
+        double r = 0;
+#pragma unroll
+        for (int k = 0; k < NL_THREADS / 64; ++k) r += red[k];
         return r;
     }
 };
