@@ -286,6 +286,7 @@ int ransac_run(const double *x1, const double *x2, int64_t N, const int32_t *sam
 // outputs).  samples_out (nullable) receives the table.  Timings as
 // ransac_run, plus [6] = host sampling ms.
 constexpr int64_t RP_CHUNK = 4096;
+static inline size_t xoff_of(int64_t N) { return ((size_t)16 * sizeof(double) + (size_t)N + 255) & ~(size_t)255; }
 static inline int64_t rp_chunk() {
     static const int64_t c = [] {
         const char *e = std::getenv("SFM_RP_CHUNK");
@@ -313,7 +314,7 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
     if ((rc = c->buf[0].reserve(pb)) || (rc = c->buf[1].reserve(pb)) ||
         (rc = c->buf[3].reserve((size_t)H * 9 * sizeof(double))) ||
         (rc = c->buf[4].reserve((size_t)H * sizeof(int32_t))) ||
-        (rc = c->pinned.reserve(sbp + 16 * sizeof(double) + (size_t)N)))
+        (rc = c->pinned.reserve(sbp + xoff_of(N) + 2 * pb)))
         return rc;
     double2 *d1 = c->buf[0].as<double2>(), *d2 = c->buf[1].as<double2>();
     int32_t *dcnt = c->buf[4].as<int32_t>();
@@ -324,14 +325,20 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
     // (and no copy-engine/compute-queue handoff) sits between host and kernels.
     int32_t *hs = c->pinned.as<int32_t>();
     char *hout = c->pinned.as<char>() + sbp;
+    // the correspondences are staged through pinned memory as well, so their
+    // upload is a true async copy that overlaps the first chunk's draw (from
+    // pageable memory the copy would hold the host until it lands)
+    char *hx = hout + xoff_of(N);
+    std::memcpy(hx, x1, pb);
+    std::memcpy(hx + pb, x2, pb);
     int64_t *dbest = reinterpret_cast<int64_t *>(hout);
     double *dFb = reinterpret_cast<double *>(hout) + 2;
     uint8_t *dmask = reinterpret_cast<uint8_t *>(hout) + 16 * sizeof(double);
     hipStream_t s = c->stream;
     const auto t0 = std::chrono::steady_clock::now();
     SFM_HIP(hipEventRecord(c->ev[0], s));
-    SFM_HIP(hipMemcpyAsync(d1, x1, pb, hipMemcpyHostToDevice, s));
-    SFM_HIP(hipMemcpyAsync(d2, x2, pb, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipMemcpyAsync(d1, hx, pb, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipMemcpyAsync(d2, hx + pb, pb, hipMemcpyHostToDevice, s));
     SFM_HIP(hipEventRecord(c->ev[1], s));
     PySampler ps(st, N, M::K);
     double t_draw = 0;
