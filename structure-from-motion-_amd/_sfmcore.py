@@ -34,6 +34,7 @@ _i64 = ctypes.POINTER(ctypes.c_int64)
 _u8 = ctypes.POINTER(ctypes.c_uint8)
 _c = ctypes.c_int
 _i = ctypes.c_int64
+_v = ctypes.c_void_p
 
 
 class BAOpts(ctypes.Structure):
@@ -62,11 +63,13 @@ SIGNATURES = [
     ("sfm_f8_batch", _c, [_d, _d, _i, _d, _c]),
     ("sfm_f8_general", _c, [_d, _d, _i, _d, _c]),
     ("sfm_ransac_f8", _c, [_d, _d, _i, _i32, _i, ctypes.c_double, _i32, _i64, _d, _u8, _c]),
-    ("sfm_ransac_f8_pyrandom", _c, [_d, _d, _i, _u32, _i, ctypes.c_double, _i32, _i64, _d, _u8, _i32, _c]),
+    # the in-call-sampling entries take raw addresses (c_void_p): the drop-in
+    # calls them once per image pair and .ctypes.data_as costs ~4 us a pointer
+    ("sfm_ransac_f8_pyrandom", _c, [_v, _v, _i, _v, _i, ctypes.c_double, _v, _v, _v, _v, _v, _c]),
     ("sfm_h4_batch", _c, [_d, _d, _i, _d, _c]),
     ("sfm_homography_general", _c, [_d, _d, _i, _d, _c]),
     ("sfm_ransac_h4", _c, [_d, _d, _i, _i32, _i, ctypes.c_double, _i32, _i64, _d, _u8, _c]),
-    ("sfm_ransac_h4_pyrandom", _c, [_d, _d, _i, _u32, _i, ctypes.c_double, _i32, _i64, _d, _u8, _i32, _c]),
+    ("sfm_ransac_h4_pyrandom", _c, [_v, _v, _i, _v, _i, ctypes.c_double, _v, _v, _v, _v, _v, _c]),
     ("sfm_linear_pnp", _c, [_d, _d, _i, _d, _d, _d, _i32, _c]),
     ("sfm_pnp_ransac", _c, [_d, _d, _i, _d, _i32, _i, ctypes.c_double, _i32, _i32, _i64, _i64, _d, _d, _c]),
     ("sfm_nonlinear_pnp", _c, [_d, _d, _i, _d, _d, _d, ctypes.c_int32, _d, _d, _i32, _c]),
@@ -218,15 +221,15 @@ def _ransac_pyrandom(fn, x1, x2, H, thr, want_counts, want_samples, device):
     samples = np.zeros((H, fn[1]), dtype=np.int32) if want_samples else None
     best = np.zeros(1, dtype=np.int64)
     M = np.zeros(9)
-    mask = np.zeros(N, dtype=np.uint8)
-    _check(fn[0](_p(x1), _p(x2), N, _mt_ptr(st), int(H), float(thr), _p(counts, _i32) if want_counts else None,
-                 _p(best, _i64), _p(M), _p(mask, _u8), _p(samples, _i32) if want_samples else None,
-                 DEVICE if device is None else device))
+    mask = np.zeros(N, dtype=bool)  # written as 0/1 bytes by the library
+    _check(fn[0](x1.ctypes.data, x2.ctypes.data, N, st.buffer_info()[0], int(H), float(thr),
+                 counts.ctypes.data if want_counts else None, best.ctypes.data, M.ctypes.data, mask.ctypes.data,
+                 samples.ctypes.data if want_samples else None, DEVICE if device is None else device))
     _mt_restore(version_, st, gauss)
     b = int(best[0])
     if b < 0:
         return -1, None, np.zeros(N, dtype=bool), counts, samples
-    return b, M.reshape(3, 3), mask.astype(bool), counts, samples
+    return b, M.reshape(3, 3), mask, counts, samples
 
 
 def ransac_f8_pyrandom(x1, x2, H, thr, want_counts=False, want_samples=False, device=None):
