@@ -8,6 +8,11 @@
 #pragma once
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
 #include <vector>
 
 namespace sfm {
@@ -78,6 +83,18 @@ struct PySampler {
     }
     void draw(int64_t h0, int64_t h1, int32_t *out) {
         if (n > setsize) {
+#if defined(__x86_64__)
+            static const bool simd = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512vl") &&
+                                     __builtin_cpu_supports("avx512cd") && !std::getenv("SFM_PYRANDOM_SCALAR");
+            if (simd) switch (k) {
+                case 4: draw_set_512<4>(h0, h1, out); return;
+                case 5: draw_set_512<5>(h0, h1, out); return;
+                case 6: draw_set_512<6>(h0, h1, out); return;
+                case 7: draw_set_512<7>(h0, h1, out); return;
+                case 8: draw_set_512<8>(h0, h1, out); return;
+                default: break;
+                }
+#endif
             switch (k) {
             case 4: draw_set<4>(h0, h1, out); return;
             case 5: draw_set<5>(h0, h1, out); return;
@@ -186,8 +203,80 @@ struct PySampler {
             }
         }
     }
+#if defined(__x86_64__)
+    // The same stream walk with AVX-512: the twist and tempering vectorise
+    // under this target, each block is compacted 16 outputs at a time with
+    // vpcompressd, and a group's duplicate test is one vpconflictd.  Chosen at
+    // run time (draw) when the CPU has AVX-512 F/VL/CD; bit-identical output.
+    template <int K> __attribute__((target("avx512f,avx512vl,avx512cd"))) void draw_set_512(int64_t h0, int64_t h1,
+                                                                                         int32_t *out) {
+        static_assert(K <= 8, "one 8-lane conflict test per group");
+        const int sh = 32 - (64 - __builtin_clzll((unsigned long long)n));
+        const __m512i vnn = _mm512_set1_epi32((int)(uint32_t)n);
+        const __m512i iota = _mm512_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+        const __m128i vsh = _mm_cvtsi32_si128(sh);
+        int32_t *res = out + h0 * K;
+        int32_t *const end = out + h1 * K;
+        if (res >= end) return;
+        int i0 = m.idx;
+        int c = 0, p = 0;
+        for (;;) {
+            if (i0 >= 624) {
+                m.twist();
+                i0 = 0;
+            }
+            if (p > 0) {  // carry the unfinished group to the front
+                std::memmove(vals.data(), vals.data() + p, (size_t)(c - p) * sizeof(uint32_t));
+                std::memmove(pos.data(), pos.data() + p, (size_t)(c - p) * sizeof(int32_t));
+                c -= p;
+                p = 0;
+            }
+            if ((int)vals.size() < c + 624 + 16) {
+                vals.resize(c + 624 + 16);
+                pos.resize(c + 624 + 16);
+            }
+            uint32_t *v = vals.data();
+            int32_t *a = pos.data();  // index within the current block
+            for (int i = i0; i < 624; i += 16) {
+                const __mmask16 lm = 624 - i >= 16 ? (__mmask16)0xFFFF : (__mmask16)((1u << (624 - i)) - 1);
+                const __m512i u = _mm512_srl_epi32(_mm512_maskz_loadu_epi32(lm, m.tmp + i), vsh);
+                const __mmask16 kin = _mm512_mask_cmplt_epu32_mask(lm, u, vnn);
+                _mm512_mask_compressstoreu_epi32(v + c, kin, u);
+                _mm512_mask_compressstoreu_epi32(a + c, kin, _mm512_add_epi32(_mm512_set1_epi32(i), iota));
+                c += _mm_popcnt_u32((unsigned)kin);
+            }
+            i0 = 624;
+            while (res < end && c - p >= K) {
+                const uint32_t *g = v + p;
+                const __m256i gv = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(g));
+                const __m256i cf = _mm256_conflict_epi32(gv);
+                if (_mm256_mask_test_epi32_mask((__mmask8)((1u << K) - 1), cf, cf) == 0) {
+#pragma unroll
+                    for (int x = 0; x < K; ++x) res[x] = (int32_t)g[x];
+                    res += K;
+                    p += K;
+                    continue;
+                }
+                int na = 0, q = p;
+                for (; q < c && na < K; ++q) {
+                    bool seen = false;
+                    for (int y = 0; y < na; ++y) seen |= (uint32_t)res[y] == v[q];
+                    if (!seen) res[na++] = (int32_t)v[q];
+                }
+                if (na < K) break;  // needs outputs of the next block
+                res += K;
+                p = q;
+            }
+            if (res >= end) {  // the last consumed output is in this block (see draw_set)
+                m.idx = a[p - 1] + 1;
+                return;
+            }
+        }
+    }
+#endif
     std::vector<uint32_t> vals;
     std::vector<int64_t> at;
+    std::vector<int32_t> pos;
 };
 
 }  // namespace sfm
