@@ -117,3 +117,22 @@ def test_ba_observation_order_matches_reference_loop():
                 ref_p.append(np.where(vp == pt_idx)[0][0])
                 ref_2d.append([fx[pt_idx, cam_idx], fy[pt_idx, cam_idx]])
     assert np.array_equal(cams, ref_c) and np.array_equal(pts, ref_p) and np.array_equal(p2d, ref_2d)
+
+
+def test_sample_table_scalar_variant_replays_python_random():
+    """The scalar set-rejection replay (the AVX-512 one is chosen at run time
+    when the CPU has it) gives the same draws: forced in a child process."""
+    import subprocess
+    import sys
+    code = (
+        "import random, numpy as np, _sfmcore\n"
+        "for n, k, H in [(5000, 8, 2000), (30, 4, 1500), (25, 5, 800), (200, 7, 800)]:\n"
+        "    random.seed(n + k); random.random(); st = random.getstate()\n"
+        "    t = _sfmcore.sample_table(n, k, H); after = random.getstate(); random.setstate(st)\n"
+        "    ref = np.array([random.sample(range(n), k) for _ in range(H)], dtype=np.int32)\n"
+        "    assert np.array_equal(t, ref) and after == random.getstate(), (n, k)\n"
+        "print('ok')\n")
+    env = dict(os.environ, SFM_PYRANDOM_SCALAR="1")
+    env["PYTHONPATH"] = os.pathsep.join([os.path.join(REPO, "structure-from-motion-_amd"), env.get("PYTHONPATH", "")])
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
