@@ -707,7 +707,7 @@ __device__ void nlpnp_eval(const Cam3 &K, const double *p, double *sP, const dou
 }
 
 struct NlShared {
-    double p[6], pt[6], sP[12], h;
+    double p[6], pt[6], sP[12];
     double red[NL_THREADS];
     double rdiag[6], acnorm[6], wa[6], qtf[6], wa1[6], wa2[6], wa3[6];
     double r6[6][6];  // upper triangle of the QR factor, column-major r6[col][row]
@@ -768,12 +768,15 @@ __global__ void __launch_bounds__(NL_THREADS) k_nonlinear_pnp(const double *__re
                 const double temp = S.p[j];
                 double h = eps * fabs(temp);
                 if (h == 0.0) h = eps;
-                S.h = h;
                 for (int k = 0; k < 6; ++k) S.pt[k] = S.p[k];
                 S.pt[j] = temp + h;
             }
+            // every thread forms h itself from S.p (stable during fdjac2): reading
+            // S.h after the eval's barrier would race with lane 0 writing the
+            // next column's step
+            double h = eps * fabs(S.p[j]);
+            if (h == 0.0) h = eps;
             nlpnp_eval(K, S.pt, S.sP, X, x, n, wf);
-            const double h = S.h;
             double *cj = col(j);
             for (int64_t i = t; i < m; i += NL_THREADS) cj[i] = (wf[i] - fvec[i]) / h;
         }
@@ -809,9 +812,12 @@ __global__ void __launch_bounds__(NL_THREADS) k_nonlinear_pnp(const double *__re
             double *cj = col(j);
             double s2 = 0;
             for (int64_t i = j + t; i < m; i += NL_THREADS) s2 += cj[i] * cj[i];
+            // the pivot's sign is read before the sum's barriers: after them
+            // lane 0 may already have divided cj[j] (its loop starts at i = j)
+            const double cjj = cj[j];
             double ajnorm = sqrt(rd.sum(s2));
             if (ajnorm != 0.0) {
-                if (cj[j] < 0.0) ajnorm = -ajnorm;
+                if (cjj < 0.0) ajnorm = -ajnorm;
                 for (int64_t i = j + t; i < m; i += NL_THREADS) cj[i] /= ajnorm;
                 __syncthreads();
                 if (t == 0) cj[j] += 1.0;
