@@ -178,7 +178,8 @@ typedef struct {
     int32_t max_iterations;      /* LM iterations (damped solve + trial)        */
     int32_t fixed_iterations;    /* 1: run exactly max_iterations (benchmark)   */
     double function_tolerance;   /* stop: accepted step with dcost < ftol*cost  */
-    double gradient_tolerance;   /* stop: max |J^T r| < gtol                     */
+    double gradient_tolerance;   /* stop after a linearisation when max |J^T r| < gtol
+                                    (status 2; 0 = off; < 0 is SFM_ERR_ARG)      */
     double parameter_tolerance;  /* stop: |dx| < xtol (|x| + xtol)               */
     double initial_lambda;       /* Marquardt damping on clamp(diag(J^T J))      */
 } sfm_ba_opts;

@@ -63,6 +63,7 @@ struct LocalGroup {
     std::vector<std::vector<double>> bufs;
     std::vector<double> result;
     int refs = 0;
+    bool aborted = false;  // a rank failed: the others stop waiting and return SFM_ERR_COMM
 };
 
 struct sfm_comm {
@@ -147,6 +148,14 @@ __device__ __forceinline__ void grid_sum_last(double (&v)[NV], double *partial, 
             for (int i = 0; i < PT_THREADS / 64; ++i) s += red[i][k];
             __hip_atomic_store(partial + (int64_t)NV * blockIdx.x + k, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        // Release side.  The partials are agent-scope atomic stores (sc1,
+        // written through to the coherence point), and the wait below holds
+        // the arrival until they have completed; the asm's memory clobber
+        // keeps the compiler from moving them past it.  A formal agent-scope
+        // release (an acq_rel add or a release fence) would add buffer_wbl2,
+        // a write-back of the whole XCD L2, to every block's arrival:
+        // measured at cfg4, k_backsub_trial 0.042 -> 0.074 ms and
+        // k_camera_lin +8 us per iteration, so it is not used.
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         // two-level arrival: the block counts in at its group's word; the
         // group's last arriver counts the group in at the top word
@@ -159,6 +168,9 @@ __device__ __forceinline__ void grid_sum_last(double (&v)[NV], double *partial, 
     }
     __syncthreads();
     if (!last) return;
+    // acquire side: the last block's reads (agent-scope atomic loads) come
+    // after an agent-scope acquire fence (buffer_inv sc1, cheap)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     // all NV sums at once: NV x GS_BATCH independent sc1 loads in flight
     // per thread, one tree -- per value the same order as summing them one by one
     __shared__ double tot[NV][PT_THREADS];
@@ -268,7 +280,8 @@ __global__ void __launch_bounds__(PT_THREADS) k_linearize(int64_t np_, const int
                                                           const double *__restrict__ X, double *__restrict__ J,
                                                           double *__restrict__ Vg, double *__restrict__ partial,
                                                           unsigned *__restrict__ counter, double *__restrict__ cost_out,
-                                                          int want_cost, const int *__restrict__ gate) {
+                                                          int want_cost, const int *__restrict__ gate, double gtol,
+                                                          unsigned *__restrict__ nbig) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
     const int64_t gt = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x;
     const int64_t p = gt / G;  // G lanes per point, striding over its observations
@@ -315,6 +328,15 @@ __global__ void __launch_bounds__(PT_THREADS) k_linearize(int64_t np_, const int
         for (int i = 0; i < 6; ++i) vg[i] = V[i];
 #pragma unroll
         for (int i = 0; i < 3; ++i) vg[6 + i] = g[i];
+    }
+    if (gtol > 0.0) {  // gradient_tolerance: count point-gradient entries >= gtol (an exact integer sum)
+        int big = 0;
+        if (p < np_ && sub == 0)
+#pragma unroll
+            for (int i = 0; i < 3; ++i) big += fabs(g[i]) >= gtol;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) big += __shfl_xor(big, o);
+        if ((threadIdx.x & 63) == 0 && big) atomicAdd(nbig, (unsigned)big);
     }
     if (want_cost) grid_sum_last<1>(acc, partial, counter, cost_out);  // only the initial cost is used
 }
@@ -742,12 +764,15 @@ __global__ void __launch_bounds__(256) k_camera_lin(const PairItem *__restrict__
         __hip_atomic_store(slab2 + (int64_t)CAMLIN * blockIdx.x + threadIdx.x,
                            red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x],
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // release as in grid_sum_last: sc1 atomic stores completed before the
+    // arrival (no buffer_wbl2 on every block)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
         last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     __syncthreads();
     if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     for (int e = threadIdx.x; e < nblocks * CAMLIN; e += 256) {
         const BlockInfo bi = blocks[e / CAMLIN];
         const int k = e % CAMLIN;
@@ -1245,6 +1270,39 @@ __device__ __forceinline__ LMState lm_decide(LMState lm, const double *__restric
     return lm;
 }
 
+// gradient_tolerance (orc_ba_lm's stop after a linearisation: max |g| < gtol
+// over the camera and point gradients, status 2, the iteration not counted).
+// k_gtol_pack moves the point count and g_c into gbuf (all-reduced across
+// ranks: a sum of counts and of the per-rank g_c partials); k_gtol_check
+// stops the LM state of this iteration, which gates off the rest of it.
+__global__ void k_gtol_pack(int32_t nc, const double *__restrict__ camlin, unsigned *__restrict__ nbig,
+                            double *__restrict__ gbuf, const int *__restrict__ gate) {
+    if (!*gate) return;
+    for (int i = threadIdx.x; i < 6 * nc; i += blockDim.x) gbuf[1 + i] = camlin[CAMLIN * (i / 6) + 21 + i % 6];
+    if (threadIdx.x == 0) {
+        gbuf[0] = (double)*nbig;
+        *nbig = 0u;
+    }
+}
+
+__global__ void k_gtol_check(int32_t nc, double gtol, const double *__restrict__ gbuf, LMState *__restrict__ lm,
+                             const int *__restrict__ gate) {
+    if (!*gate) return;  // gate = lm->run_lin: only right after a linearisation
+    __shared__ int big;
+    if (threadIdx.x == 0) big = 0;
+    __syncthreads();
+    int b = 0;
+    for (int i = threadIdx.x; i < 6 * nc; i += blockDim.x) b += fabs(gbuf[1 + i]) >= gtol;
+    if (b) atomicAdd(&big, b);
+    __syncthreads();
+    if (threadIdx.x == 0 && big == 0 && gbuf[0] == 0.0) {
+        lm->status = 2;
+        lm->done = 1;
+        lm->run_step = 0;
+        lm->run_lin = 0;
+    }
+}
+
 // One launch per LM iteration end: the decision (recomputed by every block
 // from the old state lm_in, written by block 0 to lm_out -- the state is
 // double-buffered by iteration parity, so no block reads what another
@@ -1703,6 +1761,9 @@ struct sfm_ba_problem {
     double *d_partial = nullptr, *d_scal = nullptr;
     int *d_bad = nullptr;
     unsigned *d_count = nullptr;  // grid_sum_last arrival counters
+    unsigned *d_nbig = nullptr;   // gradient_tolerance: point-gradient entries >= gtol
+    double *d_gbuf = nullptr;     // gradient_tolerance: [count, g_c (6 nc)]
+    double gtol = 0.0;            // this solve's gradient_tolerance (k_linearize counts when > 0)
     double *h_scal = nullptr;  // pinned
     int64_t payload_len = 0;
     int pt_blocks = 0;
@@ -1910,7 +1971,8 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = p->alloc(p->d_D, 2 * 32 * 32)) ||
         (rc = p->alloc(p->d_partial, 4 * (int64_t)p->pt_blocks)) || (rc = p->alloc(p->d_scal, 16)) ||
         (rc = p->alloc(p->d_lm, 2)) ||
-        (rc = p->alloc(p->d_bad, 4)) || (rc = p->alloc(p->d_count, 3 * GS_WORDS)))
+        (rc = p->alloc(p->d_bad, 4)) || (rc = p->alloc(p->d_count, 3 * GS_WORDS)) ||
+        (rc = p->alloc(p->d_nbig, 1)) || (rc = p->alloc(p->d_gbuf, 6 * (int64_t)nc + 1)))
         return rc;
     SFM_HIP(hipHostMalloc((void **)&p->h_scal, 16 * sizeof(double)));
     hipStream_t s = p->stream;
@@ -1924,6 +1986,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     SFM_HIP(hipMemcpyAsync(p->d_cstart, cstart.data(), cstart.size() * 4, hipMemcpyHostToDevice, s));
     SFM_HIP(hipMemsetAsync(p->d_camlin, 0, (size_t)CAMLIN * nc * sizeof(double), s));
     SFM_HIP(hipMemsetAsync(p->d_count, 0, 3 * GS_WORDS * sizeof(unsigned), s));
+    SFM_HIP(hipMemsetAsync(p->d_nbig, 0, sizeof(unsigned), s));
     if (p->ndiag_items) {
         SFM_HIP(hipMemcpyAsync(p->d_items, items.data(), items.size() * sizeof(PairItem), hipMemcpyHostToDevice, s));
         SFM_HIP(hipMemcpyAsync(p->d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), hipMemcpyHostToDevice, s));
@@ -1965,10 +2028,28 @@ static int local_allreduce(sfm_ba_problem *p, double *buf, int64_t n) {
     LocalGroup *g = c->local;
     std::vector<double> &mine = g->bufs[c->rank];
     mine.resize((size_t)n);
-    SFM_HIP(hipMemcpyAsync(mine.data(), buf, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, p->stream));
-    SFM_HIP(hipStreamSynchronize(p->stream));
+    // any failure on this rank aborts the group, so no rank waits for an
+    // arrival that never comes
+    auto abort_group = [&](int rc) {
+        {
+            std::lock_guard<std::mutex> lk(g->mu);
+            g->aborted = true;
+        }
+        g->cv.notify_all();
+        return rc;
+    };
+    auto aborted_err = [&]() {
+        set_error("in-process all-reduce: another rank failed");
+        return SFM_ERR_COMM;
+    };
+    if (hipMemcpyAsync(mine.data(), buf, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, p->stream) != hipSuccess ||
+        hipStreamSynchronize(p->stream) != hipSuccess) {
+        set_error("in-process all-reduce: device-to-host copy failed");
+        return abort_group(SFM_ERR_HIP);
+    }
     {
         std::unique_lock<std::mutex> lk(g->mu);
+        if (g->aborted) return aborted_err();
         const long gen = g->generation;
         if (++g->arrived == g->nranks) {
             g->result.assign((size_t)n, 0.0);
@@ -1978,10 +2059,17 @@ static int local_allreduce(sfm_ba_problem *p, double *buf, int64_t n) {
             g->generation++;
             g->cv.notify_all();
         } else {
-            g->cv.wait(lk, [&] { return g->generation != gen; });
+            g->cv.wait(lk, [&] { return g->generation != gen || g->aborted; });
+            if (g->aborted) return aborted_err();
         }
-        SFM_HIP(hipMemcpyAsync(buf, g->result.data(), (size_t)n * sizeof(double), hipMemcpyHostToDevice, p->stream));
-        SFM_HIP(hipStreamSynchronize(p->stream));
+        if (hipMemcpyAsync(buf, g->result.data(), (size_t)n * sizeof(double), hipMemcpyHostToDevice, p->stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(p->stream) != hipSuccess) {
+            g->aborted = true;
+            g->cv.notify_all();
+            set_error("in-process all-reduce: host-to-device copy failed");
+            return SFM_ERR_HIP;
+        }
         // second rendezvous: nobody may overwrite `result` before all copied it
         const long gen2 = g->generation;
         if (++g->arrived == g->nranks) {
@@ -1989,10 +2077,94 @@ static int local_allreduce(sfm_ba_problem *p, double *buf, int64_t n) {
             g->generation++;
             g->cv.notify_all();
         } else {
-            g->cv.wait(lk, [&] { return g->generation != gen2; });
+            g->cv.wait(lk, [&] { return g->generation != gen2 || g->aborted; });
+            if (g->aborted) return aborted_err();
         }
     }
     return 0;
+}
+
+// RANSAC shard combine: max of the ranks' keys, then the
+// winner's model (the rank whose key equals the max contributes it, the
+// others zeros, summed).  Keys are unique across ranks when nonzero (the
+// iteration is in the low word), so exactly one rank contributes.
+extern "C" int sfm_ransac_combine(sfm_comm *c, uint64_t *key, double *model) {
+    SFM_CHECK_ARG(c && key && model, "null pointer");
+    if (c->nranks == 1) return 0;
+    if (c->local) {
+        LocalGroup *g = c->local;
+        std::unique_lock<std::mutex> lk(g->mu);
+        if (g->aborted) { set_error("in-process group aborted"); return SFM_ERR_COMM; }
+        std::vector<double> &mine = g->bufs[c->rank];
+        mine.assign(10, 0.0);
+        std::memcpy(&mine[0], key, 8);
+        std::memcpy(&mine[1], model, 72);
+        const long gen = g->generation;
+        if (++g->arrived == g->nranks) {
+            uint64_t best = 0;
+            int who = -1;
+            for (int r = 0; r < g->nranks; ++r) {
+                uint64_t k;
+                std::memcpy(&k, &g->bufs[r][0], 8);
+                if (k > best) { best = k; who = r; }
+            }
+            g->result.assign(10, 0.0);
+            std::memcpy(&g->result[0], &best, 8);
+            if (who >= 0) std::copy(g->bufs[who].begin() + 1, g->bufs[who].end(), g->result.begin() + 1);
+            g->arrived = 0;
+            g->generation++;
+            g->cv.notify_all();
+        } else {
+            g->cv.wait(lk, [&] { return g->generation != gen || g->aborted; });
+            if (g->aborted) { set_error("in-process group aborted"); return SFM_ERR_COMM; }
+        }
+        std::memcpy(key, &g->result[0], 8);
+        if (*key != 0) std::memcpy(model, &g->result[1], 72);
+        // second rendezvous: result stays intact until every rank has read it
+        const long gen2 = g->generation;
+        if (++g->arrived == g->nranks) {
+            g->arrived = 0;
+            g->generation++;
+            g->cv.notify_all();
+        } else {
+            g->cv.wait(lk, [&] { return g->generation != gen2 || g->aborted; });
+            if (g->aborted) { set_error("in-process group aborted"); return SFM_ERR_COMM; }
+        }
+        return 0;
+    }
+    SFM_HIP(hipSetDevice(c->device));
+    // device scratch: [key (u64) | model (9 f64)]
+    void *d = nullptr;
+    SFM_HIP(hipMalloc(&d, 80));
+    hipStream_t s = nullptr;
+    int rc = 0;
+    uint64_t gkey = 0;
+    double m[9];
+    auto fail = [&](ncclResult_t r, const char *what) {
+        set_error("%s: %s", what, ncclGetErrorString(r));
+        rc = SFM_ERR_COMM;
+    };
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) rc = SFM_ERR_HIP;
+    if (!rc && hipMemcpyAsync(d, key, 8, hipMemcpyHostToDevice, s) != hipSuccess) rc = SFM_ERR_HIP;
+    ncclResult_t r;
+    if (!rc && (r = ncclAllReduce(d, d, 1, ncclUint64, ncclMax, c->comm, s)) != ncclSuccess) fail(r, "ncclAllReduce(max)");
+    if (!rc && (hipMemcpyAsync(&gkey, d, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess))
+        rc = SFM_ERR_HIP;
+    if (!rc && gkey != 0) {
+        for (int k = 0; k < 9; ++k) m[k] = (*key == gkey) ? model[k] : 0.0;
+        double *dm = reinterpret_cast<double *>(static_cast<char *>(d) + 8);
+        if (hipMemcpyAsync(dm, m, 72, hipMemcpyHostToDevice, s) != hipSuccess) rc = SFM_ERR_HIP;
+        if (!rc && (r = ncclAllReduce(dm, dm, 9, ncclDouble, ncclSum, c->comm, s)) != ncclSuccess)
+            fail(r, "ncclAllReduce(sum)");
+        if (!rc && (hipMemcpyAsync(m, dm, 72, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess))
+            rc = SFM_ERR_HIP;
+        if (!rc) std::memcpy(model, m, 72);
+    }
+    if (!rc) *key = gkey;
+    if (s) (void)hipStreamDestroy(s);
+    (void)hipFree(d);
+    if (rc == SFM_ERR_HIP) set_error("sfm_ransac_combine: HIP call failed");
+    return rc;
 }
 
 static int allreduce(sfm_ba_problem *p, double *buf, int64_t n) {
@@ -2019,7 +2191,8 @@ static int run_linearize(sfm_ba_problem *p, int par, int want_cost) {
     const int nbl = std::max(1, ceil_div(p->np * gl, PT_THREADS));
 #define SFM_LIN(G)                                                                                                \
     hipLaunchKernelGGL(k_linearize<G>, dim3(nbl), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam, p->d_obs, \
-                       p->K, p->d_Rt, p->d_X, p->d_J, p->d_Vg, p->d_partial, p->d_count, p->d_scal + 8, want_cost, glin)
+                       p->K, p->d_Rt, p->d_X, p->d_J, p->d_Vg, p->d_partial, p->d_count, p->d_scal + 8, want_cost, glin, \
+                       p->gtol, p->d_nbig)
     switch (gl) { case 1: SFM_LIN(1); break; case 2: SFM_LIN(2); break; case 4: SFM_LIN(4); break; default: SFM_LIN(8); }
 #undef SFM_LIN
     SFM_HIP(hipGetLastError());
@@ -2086,7 +2259,9 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
 extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_report *rep) {
     SFM_CHECK_ARG(p && o, "null pointer");
     SFM_CHECK_ARG(o->max_iterations >= 0, "max_iterations < 0");
+    SFM_CHECK_ARG(o->gradient_tolerance >= 0.0, "gradient_tolerance < 0");
     SFM_HIP(hipSetDevice(p->device));
+    p->gtol = o->gradient_tolerance;
     (void)hipGetLastError();
     const auto t0 = std::chrono::steady_clock::now();
     for (double &t : p->t_acc) t = 0;
@@ -2111,6 +2286,15 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
         SFM_HIP(hipEventRecord(ev[2 * T_LIN + 1], s));
         if (it == 0) {
             hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(1), 0, s, p->d_lm, p->d_scal + 8);
+            SFM_HIP(hipGetLastError());
+        }
+        if (o->gradient_tolerance > 0.0) {
+            const int *glin = &p->d_lm[par].run_lin;
+            hipLaunchKernelGGL(k_gtol_pack, dim3(1), dim3(256), 0, s, p->nc, p->d_camlin, p->d_nbig, p->d_gbuf, glin);
+            SFM_HIP(hipGetLastError());
+            if ((rc = allreduce(p, p->d_gbuf, 6 * (int64_t)p->nc + 1))) return rc;
+            hipLaunchKernelGGL(k_gtol_check, dim3(1), dim3(256), 0, s, p->nc, o->gradient_tolerance, p->d_gbuf,
+                               p->d_lm + par, glin);
             SFM_HIP(hipGetLastError());
         }
         if ((rc = run_step(p, ev, par))) return rc;
@@ -2264,17 +2448,30 @@ extern "C" int sfm_ba_lm_multi(int32_t nc, int64_t np_, int64_t no, const int32_
         if (!e) e = sfm_ba_download(p, r == 0 ? cams_out.data() : nullptr, pts + 3 * lo);
         if (p) sfm_ba_destroy(p);
         rcs[r] = e;
-        if (e) errs[r] = sfm_last_error();
+        if (e) {
+            errs[r] = sfm_last_error();
+            // a rank that fails outside the all-reduce (create, a launch)
+            // releases the ranks waiting for it there
+            LocalGroup *g = comms[r]->local;
+            {
+                std::lock_guard<std::mutex> lk(g->mu);
+                g->aborted = true;
+            }
+            g->cv.notify_all();
+        }
     };
     std::vector<std::thread> th;
     for (int r = 0; r < n_ranks; ++r) th.emplace_back(worker, r);
     for (auto &t : th) t.join();
     for (auto *c : comms) sfm_comm_destroy(c);
-    for (int r = 0; r < n_ranks; ++r)
-        if (rcs[r]) {
-            set_error("rank %d: %s", r, errs[r].c_str());
-            return rcs[r];
-        }
+    // report the first rank that failed on its own (not the SFM_ERR_COMM of
+    // the ranks it released)
+    for (int pass = 0; pass < 2; ++pass)
+        for (int r = 0; r < n_ranks; ++r)
+            if (rcs[r] && (pass == 1 || rcs[r] != SFM_ERR_COMM)) {
+                set_error("rank %d: %s", r, errs[r].c_str());
+                return rcs[r];
+            }
     std::memcpy(cams, cams_out.data(), cams_out.size() * sizeof(double));
     if (rep) *rep = reps[0];
     return 0;

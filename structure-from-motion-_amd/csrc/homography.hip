@@ -60,3 +60,16 @@ extern "C" int sfm_ransac_h4_pyrandom(const double *x1, const double *x2, int64_
     return ransac_run_pysample<HomModel>(x1, x2, N, st, H, thr, counts_out, best_iter, H_best, best_mask,
                                          samples_out, device);
 }
+
+// Hypothesis shard [h0, h1) of the homography RANSAC (as sfm_ransac_f8_range).
+extern "C" int sfm_ransac_h4_pyrandom_range(const double *x1, const double *x2, int64_t N, uint32_t *st, int64_t H,
+                                            int64_t h0, int64_t h1, double thr, int32_t *counts_out,
+                                            uint64_t *best_key, double *H_best, int device) {
+    SFM_CHECK_ARG(st, "null MT19937 state");
+    return ransac_run_range<HomModel>(x1, x2, N, nullptr, st, H, h0, h1, thr, counts_out, best_key, H_best, device);
+}
+
+extern "C" int sfm_ransac_h4_mask(const double *x1, const double *x2, int64_t N, const double *Hm, double thr,
+                                  uint8_t *mask, int device) {
+    return ransac_mask_run<HomModel>(x1, x2, N, Hm, thr, mask, device);
+}

@@ -40,3 +40,28 @@ extern "C" int sfm_ransac_f8_pyrandom(const double *x1, const double *x2, int64_
                                          samples_out, device);
 }
 
+
+// One hypothesis shard [h0, h1) of sfm_ransac_f8 / sfm_ransac_f8_pyrandom
+// (SURVEY §8(e)): the shard's key (count << 32 | 0xFFFFFFFF - iteration,
+// 0 = none) and model.  Ranks combine keys with max (sfm_ransac_combine);
+// the winner's model gives the mask (sfm_ransac_f8_mask).  The _pyrandom
+// form draws all H rows from st, so every rank's stream ends where the
+// unsharded call leaves it.
+extern "C" int sfm_ransac_f8_range(const double *x1, const double *x2, int64_t N, const int32_t *samples, int64_t H,
+                                   int64_t h0, int64_t h1, double thr, int32_t *counts_out, uint64_t *best_key,
+                                   double *F_best, int device) {
+    return ransac_run_range<EpiModel>(x1, x2, N, samples, nullptr, H, h0, h1, thr, counts_out, best_key, F_best,
+                                      device);
+}
+
+extern "C" int sfm_ransac_f8_pyrandom_range(const double *x1, const double *x2, int64_t N, uint32_t *st, int64_t H,
+                                            int64_t h0, int64_t h1, double thr, int32_t *counts_out,
+                                            uint64_t *best_key, double *F_best, int device) {
+    SFM_CHECK_ARG(st, "null MT19937 state");
+    return ransac_run_range<EpiModel>(x1, x2, N, nullptr, st, H, h0, h1, thr, counts_out, best_key, F_best, device);
+}
+
+extern "C" int sfm_ransac_f8_mask(const double *x1, const double *x2, int64_t N, const double *F, double thr,
+                                  uint8_t *mask, int device) {
+    return ransac_mask_run<EpiModel>(x1, x2, N, F, thr, mask, device);
+}

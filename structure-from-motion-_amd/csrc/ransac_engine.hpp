@@ -198,12 +198,16 @@ __global__ void __launch_bounds__(1024) k_ransac_select(const double2 *__restric
         __syncthreads();
     }
     const int64_t best = sc[0] > 0 ? sh[0] : -1;
-    if (threadIdx.x == 0) *best_out = best;
+    if (threadIdx.x == 0) {
+        best_out[0] = best;
+        best_out[1] = sc[0];  // its count (the shard key's high word)
+    }
     if (best < 0) return;
     double f[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) f[k] = F[9 * best + k];
     if (threadIdx.x < 9) F_best[threadIdx.x] = f[threadIdx.x];
+    if (!mask) return;  // a hypothesis shard: the mask is emitted after the combine
     for (int64_t i = threadIdx.x; i < N; i += blockDim.x) {
         const double2 p = x1[i], q = x2[i];
         mask[i] = M::inlier(f, p, q, thr) ? 1 : 0;
@@ -377,6 +381,151 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
     const double t[7] = {ev_ms(c->ev[0], c->ev[1]), ev_ms(c->ev[1], c->ev[4]), ev_ms(c->ev[4], c->ev[5]),
                          ev_ms(c->ev[1], c->ev[3]), 0.0, ev_ms(c->ev[3], c->ev[4]), t_draw};
     set_timings(t, 7);
+    return 0;
+}
+
+// The inlier mask of one model (the winner's emit after a sharded combine).
+template <class M>
+__global__ void __launch_bounds__(256) k_ransac_mask(const double2 *__restrict__ x1, const double2 *__restrict__ x2,
+                                                     int64_t N, const double *__restrict__ F, double thr,
+                                                     uint8_t *__restrict__ mask) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    double f[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f[k] = F[k];
+    mask[i] = M::inlier(f, x1[i], x2[i], thr) ? 1 : 0;
+}
+
+// Shard key of a (count, iteration) winner: the reference's strict '>'
+// update keeps the max count and, among equal counts, the earliest
+// iteration, which is the max of (count << 32) | (0xFFFFFFFF - iteration);
+// key 0 = no hypothesis with an inlier.  Ranks combine keys with max.
+static inline uint64_t shard_key(int64_t count, int64_t iter) {
+    return count > 0 ? ((uint64_t)count << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)iter) : 0;
+}
+
+// One hypothesis shard [r0, r1) of an H-hypothesis RANSAC
+// (GetInliersRANSAC.py:53-92 split over ranks).  The sample
+// table is either given (samples: the whole H x K table) or drawn in the
+// call from the CPython MT19937 state st (all H rows are drawn, in the
+// reference's order, so st advances exactly as the unsharded call; only the
+// shard's rows are fitted and scored).  Out: counts of the shard (nullable),
+// the shard key and the shard winner's model (untouched when key = 0).
+template <class M>
+int ransac_run_range(const double *x1, const double *x2, int64_t N, const int32_t *samples, uint32_t *st, int64_t H,
+                     int64_t r0, int64_t r1, double thr, int32_t *counts_out, uint64_t *key_out, double *F_best,
+                     int device) {
+    SFM_CHECK_ARG(N >= M::K && H >= 0 && H < ((int64_t)1 << 32), "need N >= sample size and 0 <= H < 2^32");
+    SFM_CHECK_ARG(0 <= r0 && r0 <= r1 && r1 <= H, "need 0 <= h0 <= h1 <= H");
+    SFM_CHECK_ARG(x1 && x2 && key_out && F_best && (samples || st || H == 0), "null pointer");
+    SFM_CHECK_ARG(!st || (N < ((int64_t)1 << 31) && st[624] <= 624), "bad sizes / MT19937 position");
+    if (samples)
+        for (int64_t i = r0 * M::K; i < r1 * M::K; ++i)
+            SFM_CHECK_ARG(samples[i] >= 0 && samples[i] < N, "sample index out of range");
+    *key_out = 0;
+    const int64_t nh = r1 - r0;
+    ThreadCtx *c = thread_ctx(device);
+    if (!c) return SFM_ERR_HIP;
+    const size_t pb = (size_t)N * sizeof(double2);
+    const size_t sb = (size_t)(st ? H : nh) * M::K * sizeof(int32_t);
+    const size_t sbp = (sb + 255) & ~(size_t)255;
+    int rc;
+    if ((rc = c->buf[0].reserve(pb)) || (rc = c->buf[1].reserve(pb)) ||
+        (rc = c->buf[3].reserve((size_t)std::max<int64_t>(nh, 1) * 9 * sizeof(double))) ||
+        (rc = c->buf[4].reserve((size_t)std::max<int64_t>(nh, 1) * sizeof(int32_t))) ||
+        (rc = c->pinned.reserve(sbp + xoff_of(N) + 2 * pb)))
+        return rc;
+    double2 *d1 = c->buf[0].as<double2>(), *d2 = c->buf[1].as<double2>();
+    int32_t *dcnt = c->buf[4].as<int32_t>();
+    double *dF = c->buf[3].as<double>();
+    int32_t *hs = c->pinned.as<int32_t>();
+    char *hout = c->pinned.as<char>() + sbp;
+    char *hx = hout + xoff_of(N);
+    std::memcpy(hx, x1, pb);
+    std::memcpy(hx + pb, x2, pb);
+    int64_t *dbest = reinterpret_cast<int64_t *>(hout);
+    double *dFb = reinterpret_cast<double *>(hout) + 2;
+    hipStream_t s = c->stream;
+    SFM_HIP(hipEventRecord(c->ev[0], s));
+    SFM_HIP(hipMemcpyAsync(d1, hx, pb, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipMemcpyAsync(d2, hx + pb, pb, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipEventRecord(c->ev[1], s));
+    double t_draw = 0;
+    // fit + score the hypotheses [a, b) of the shard whose rows sit at rows
+    auto launch = [&](int64_t a, int64_t b, const int32_t *rows) -> int {
+        if (b <= a) return 0;
+        const int64_t n = b - a;
+        int ny;
+        const int64_t slice = score_slice(n, N, &ny);
+        hipLaunchKernelGGL(k_fit_samples<M>, dim3(ceil_div(n, 64)), dim3(64), 0, s, d1, d2, rows, n,
+                           dF + (a - r0) * 9, ny > 1 ? dcnt + (a - r0) : nullptr);
+        SFM_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_ransac_score<M>, dim3(ceil_div(n, SCORE_WAVES), ny), dim3(64 * SCORE_WAVES), 0, s, d1, d2,
+                           N, dF + (a - r0) * 9, n, thr, dcnt + (a - r0), slice);
+        SFM_HIP(hipGetLastError());
+        return 0;
+    };
+    if (st) {
+        PySampler ps(st, N, M::K);
+        const int64_t chunk = rp_chunk();
+        for (int64_t h0 = 0; h0 < H; h0 += chunk) {
+            const int64_t h1 = std::min(H, h0 + chunk);
+            const auto ta = std::chrono::steady_clock::now();
+            ps.draw(h0, h1, hs);
+            t_draw += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
+            const int64_t a = std::max(h0, r0), b = std::min(h1, r1);
+            if ((rc = launch(a, b, hs + a * M::K))) return rc;
+        }
+        ps.save(st);
+    } else {
+        std::memcpy(hs, samples + r0 * M::K, sb);
+        if ((rc = launch(r0, r1, hs))) return rc;
+    }
+    SFM_HIP(hipEventRecord(c->ev[3], s));
+    if (nh > 0) {
+        hipLaunchKernelGGL(k_ransac_select<M>, dim3(1), dim3(1024), 0, s, d1, d2, N, dF, dcnt, nh, thr, dbest, dFb,
+                           (uint8_t *)nullptr);
+        SFM_HIP(hipGetLastError());
+    }
+    SFM_HIP(hipEventRecord(c->ev[4], s));
+    if (counts_out && nh)
+        SFM_HIP(hipMemcpyAsync(counts_out, dcnt, (size_t)nh * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    SFM_HIP(hipEventRecord(c->ev[5], s));
+    SFM_HIP(hipStreamSynchronize(s));
+    if (nh > 0 && dbest[0] >= 0) {
+        *key_out = shard_key(dbest[1], r0 + dbest[0]);
+        std::memcpy(F_best, dFb, 9 * sizeof(double));
+    }
+    const double t[7] = {ev_ms(c->ev[0], c->ev[1]), ev_ms(c->ev[1], c->ev[4]), ev_ms(c->ev[4], c->ev[5]),
+                         ev_ms(c->ev[1], c->ev[3]), 0.0, ev_ms(c->ev[3], c->ev[4]), t_draw};
+    set_timings(t, 7);
+    return 0;
+}
+
+template <class M>
+int ransac_mask_run(const double *x1, const double *x2, int64_t N, const double *F, double thr, uint8_t *mask,
+                    int device) {
+    SFM_CHECK_ARG(x1 && x2 && F && (mask || N == 0) && N >= 0, "null pointer");
+    if (N == 0) return 0;
+    ThreadCtx *c = thread_ctx(device);
+    if (!c) return SFM_ERR_HIP;
+    const size_t pb = (size_t)N * sizeof(double2);
+    int rc;
+    if ((rc = c->buf[0].reserve(pb)) || (rc = c->buf[1].reserve(pb)) ||
+        (rc = c->buf[5].reserve(16 * sizeof(double) + (size_t)N)))
+        return rc;
+    double2 *d1 = c->buf[0].as<double2>(), *d2 = c->buf[1].as<double2>();
+    double *dF = c->buf[5].as<double>();
+    uint8_t *dm = reinterpret_cast<uint8_t *>(dF + 16);
+    hipStream_t s = c->stream;
+    SFM_HIP(hipMemcpyAsync(d1, x1, pb, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipMemcpyAsync(d2, x2, pb, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipMemcpyAsync(dF, F, 9 * sizeof(double), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_ransac_mask<M>, dim3(ceil_div(N, 256)), dim3(256), 0, s, d1, d2, N, dF, thr, dm);
+    SFM_HIP(hipGetLastError());
+    SFM_HIP(hipMemcpyAsync(mask, dm, (size_t)N, hipMemcpyDeviceToHost, s));
+    SFM_HIP(hipStreamSynchronize(s));
     return 0;
 }
 
