@@ -218,6 +218,37 @@ int sfm_comm_init(const char id[128], int nranks, int rank, int device, sfm_comm
 int sfm_comm_init_local(int nranks, sfm_comm **out);
 int sfm_comm_destroy(sfm_comm *comm);
 
+/* ---- hypothesis-sharded RANSAC: the loop of
+ * GetInliersRANSAC.py:53-92 (and GetHomographyInliers.py:124-156) split into
+ * contiguous hypothesis ranges [h0, h1), one per rank.
+ * Shard key = (count << 32) | (0xFFFFFFFF - iteration), 0 when no hypothesis
+ * of the shard has an inlier: the max over ranks is the reference's winner
+ * (max count, earliest iteration: the strict '>' update at :85-88).
+ * _pyrandom_range draws ALL H rows from the CPython MT19937 state st[625]
+ * (in/out) in the reference's order, so st ends where the unsharded call
+ * leaves it, and fits/scores only [h0, h1).  counts_out: h1 - h0 entries
+ * (nullable).  F_best/H_best: the shard winner's model (untouched when the
+ * key is 0).  Requires H < 2^32. */
+int sfm_ransac_f8_range(const double *x1, const double *x2, int64_t N, const int32_t *samples /* H x 8 */,
+                        int64_t H, int64_t h0, int64_t h1, double thr, int32_t *counts_out,
+                        uint64_t *best_key, double *F_best, int device);
+int sfm_ransac_f8_pyrandom_range(const double *x1, const double *x2, int64_t N, uint32_t *st, int64_t H,
+                                 int64_t h0, int64_t h1, double thr, int32_t *counts_out,
+                                 uint64_t *best_key, double *F_best, int device);
+int sfm_ransac_h4_pyrandom_range(const double *x1, const double *x2, int64_t N, uint32_t *st, int64_t H,
+                                 int64_t h0, int64_t h1, double thr, int32_t *counts_out,
+                                 uint64_t *best_key, double *H_best, int device);
+/* max of the ranks' keys (in/out) and the winner's model (in/out, 9) over
+ * comm: RCCL all-reduce(max, u64) then a sum in which only the winner
+ * contributes; or the in-process group.  Every rank returns the same. */
+int sfm_ransac_combine(sfm_comm *comm, uint64_t *key, double *model);
+/* inlier mask of one model (GetInliersRANSAC.py:67-81 /
+ * GetHomographyInliers.py:135-146): the winner's emit after the combine */
+int sfm_ransac_f8_mask(const double *x1, const double *x2, int64_t N, const double *F, double thr,
+                       uint8_t *mask, int device);
+int sfm_ransac_h4_mask(const double *x1, const double *x2, int64_t N, const double *Hm, double thr,
+                       uint8_t *mask, int device);
+
 int sfm_ba_create(int32_t n_cams, int64_t n_pts, int64_t n_obs, const int32_t *cam_idx,
                   const int32_t *pt_idx, const double *obs, const double *K,
                   const double *cam_params, const double *points, int device, sfm_comm *comm,

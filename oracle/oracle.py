@@ -34,6 +34,11 @@ class BAReport(ctypes.Structure):
                 ("status", ctypes.c_int32), ("cost0", ctypes.c_double), ("cost", ctypes.c_double)]
 
 
+class CSReport(ctypes.Structure):
+    _fields_ = [("iterations", ctypes.c_int32), ("accepted", ctypes.c_int32), ("status", ctypes.c_int32),
+                ("threads", ctypes.c_int32), ("cost0", ctypes.c_double), ("cost", ctypes.c_double)]
+
+
 def build():
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
 
@@ -74,6 +79,9 @@ def lib():
         L.orc_nonlinear_pnp.restype = ctypes.c_int
         L.orc_nltri.argtypes = [_d, _d, _d, _d, _d, ctypes.c_int64, ctypes.c_int32, _d, _i32]
         L.orc_R_to_rotvec.argtypes = [_d, _d]
+        L.cs_ba_lm.argtypes = [ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, _i32, _i32, _d, _d,
+                               _d, _d, ctypes.POINTER(BAOpts), ctypes.POINTER(CSReport)]
+        L.cs_ba_lm.restype = ctypes.c_int
         _LIB = L
     return _LIB
 
@@ -238,6 +246,24 @@ def ba_lm(cams, pts, cam_idx, pt_idx, obs, K, max_iterations=100, ftol=1e-10, gt
         raise RuntimeError(f"orc_ba_lm failed: {rc}")
     return cams, pts, dict(iterations=rep.iterations, accepted=rep.accepted, status=rep.status,
                            cost0=rep.cost0, cost=rep.cost)
+
+
+def ba_lm_cpu_strong(cams, pts, cam_idx, pt_idx, obs, K, max_iterations=100, ftol=1e-10, gtol=1e-10,
+                     xtol=1e-12, initial_lambda=1e-4):
+    """The OpenMP Schur-LM (sfm_cpu_strong.c): the same LM as ba_lm on all
+    OMP_NUM_THREADS host threads -- bench.py's "CPU-strong" baseline."""
+    cams, pts = f64(cams).copy(), f64(pts).copy()
+    obs, K = f64(obs), f64(K)
+    ci = np.ascontiguousarray(cam_idx, dtype=np.int32)
+    pi = np.ascontiguousarray(pt_idx, dtype=np.int32)
+    o = BAOpts(max_iterations, ftol, gtol, xtol, initial_lambda)
+    rep = CSReport()
+    rc = lib().cs_ba_lm(len(cams), len(pts), len(ci), _p(ci, _i32), _p(pi, _i32), _p(obs), _p(K),
+                        _p(cams), _p(pts), ctypes.byref(o), ctypes.byref(rep))
+    if rc != 0:
+        raise RuntimeError(f"cs_ba_lm failed: {rc}")
+    return cams, pts, dict(iterations=rep.iterations, accepted=rep.accepted, status=rep.status,
+                           threads=rep.threads, cost0=rep.cost0, cost=rep.cost)
 
 
 def rotvec_to_R(w):

@@ -32,6 +32,7 @@ _i32 = ctypes.POINTER(ctypes.c_int32)
 _u32 = ctypes.POINTER(ctypes.c_uint32)
 _i64 = ctypes.POINTER(ctypes.c_int64)
 _u8 = ctypes.POINTER(ctypes.c_uint8)
+_u64 = ctypes.POINTER(ctypes.c_uint64)
 _c = ctypes.c_int
 _i = ctypes.c_int64
 _v = ctypes.c_void_p
@@ -66,6 +67,12 @@ SIGNATURES = [
     # the in-call-sampling entries take raw addresses (c_void_p): the drop-in
     # calls them once per image pair and .ctypes.data_as costs ~4 us a pointer
     ("sfm_ransac_f8_pyrandom", _c, [_v, _v, _i, _v, _i, ctypes.c_double, _v, _v, _v, _v, _v, _c]),
+    ("sfm_ransac_f8_range", _c, [_d, _d, _i, _i32, _i, _i, _i, ctypes.c_double, _i32, _u64, _d, _c]),
+    ("sfm_ransac_f8_pyrandom_range", _c, [_d, _d, _i, _u32, _i, _i, _i, ctypes.c_double, _i32, _u64, _d, _c]),
+    ("sfm_ransac_f8_mask", _c, [_d, _d, _i, _d, ctypes.c_double, _u8, _c]),
+    ("sfm_ransac_h4_pyrandom_range", _c, [_d, _d, _i, _u32, _i, _i, _i, ctypes.c_double, _i32, _u64, _d, _c]),
+    ("sfm_ransac_h4_mask", _c, [_d, _d, _i, _d, ctypes.c_double, _u8, _c]),
+    ("sfm_ransac_combine", _c, [ctypes.c_void_p, _u64, _d]),
     ("sfm_h4_batch", _c, [_d, _d, _i, _d, _c]),
     ("sfm_homography_general", _c, [_d, _d, _i, _d, _c]),
     ("sfm_ransac_h4", _c, [_d, _d, _i, _i32, _i, ctypes.c_double, _i32, _i64, _d, _u8, _c]),
@@ -242,6 +249,82 @@ def ransac_f8_pyrandom(x1, x2, H, thr, want_counts=False, want_samples=False, de
 def ransac_h4_pyrandom(x1, x2, H, thr, want_counts=False, want_samples=False, device=None):
     """get_homography_inliers' loop with in-call sampling (sfm_ransac_h4_pyrandom)."""
     return _ransac_pyrandom((_lib.sfm_ransac_h4_pyrandom, 4), x1, x2, H, thr, want_counts, want_samples, device)
+
+
+# ------------------------------------------- hypothesis-sharded RANSAC (§8(e))
+def _ransac_range(model, x1, x2, H, h0, h1, thr, samples=None, want_counts=False, device=None):
+    require_device()
+    x1, x2 = _f64(x1), _f64(x2)
+    N = len(x1)
+    counts = np.zeros(max(h1 - h0, 0), dtype=np.int32) if want_counts else None
+    key = np.zeros(1, dtype=np.uint64)
+    M = np.zeros(9)
+    dev = DEVICE if device is None else device
+    cp = _p(counts, _i32) if want_counts else None
+    if samples is not None:
+        assert model == 8, "a given sample table is supported for the F model"
+        samples = np.ascontiguousarray(samples, dtype=np.int32)
+        assert samples.shape == (H, 8)
+        _check(_lib.sfm_ransac_f8_range(_p(x1), _p(x2), N, _p(samples, _i32), int(H), int(h0), int(h1), float(thr),
+                                        cp, _p(key, _u64), _p(M), dev))
+    else:
+        fn = _lib.sfm_ransac_f8_pyrandom_range if model == 8 else _lib.sfm_ransac_h4_pyrandom_range
+        version_, st, gauss = _mt_state()
+        _check(fn(_p(x1), _p(x2), N, _mt_ptr(st), int(H), int(h0), int(h1), float(thr), cp, _p(key, _u64), _p(M), dev))
+        _mt_restore(version_, st, gauss)
+    return int(key[0]), M.reshape(3, 3), counts
+
+
+def ransac_f8_range(x1, x2, H, h0, h1, thr, samples=None, want_counts=False, device=None):
+    """One hypothesis shard [h0, h1) of an H-hypothesis F-RANSAC.  Without
+    `samples` the whole table is drawn from the GLOBAL random stream (which
+    ends where the unsharded call leaves it) and only the shard is scored.
+    Returns (key, F of the shard winner, counts or None); key = count << 32 |
+    (0xFFFFFFFF - iteration), 0 if no hypothesis has an inlier."""
+    return _ransac_range(8, x1, x2, H, h0, h1, thr, samples, want_counts, device)
+
+
+def ransac_h4_range(x1, x2, H, h0, h1, thr, want_counts=False, device=None):
+    """Homography counterpart of ransac_f8_range (in-call sampling)."""
+    return _ransac_range(4, x1, x2, H, h0, h1, thr, None, want_counts, device)
+
+
+def ransac_mask(x1, x2, M, thr, model=8, device=None):
+    """Inlier mask of one model (the winner's emit after the combine)."""
+    require_device()
+    x1, x2, M = _f64(x1), _f64(x2), _f64(M)
+    mask = np.zeros(len(x1), dtype=np.uint8)
+    fn = _lib.sfm_ransac_f8_mask if model == 8 else _lib.sfm_ransac_h4_mask
+    _check(fn(_p(x1), _p(x2), len(x1), _p(M), float(thr), _p(mask, _u8), DEVICE if device is None else device))
+    return mask.astype(bool)
+
+
+def ransac_combine(comm, key, M):
+    """Max of the ranks' keys over `comm` (RCCL or an in-process group) and
+    the winner's model.  Returns (key, model)."""
+    k = np.array([key], dtype=np.uint64)
+    M = np.array(M, dtype=np.float64).reshape(9).copy()
+    _check(_lib.sfm_ransac_combine(comm.h if hasattr(comm, "h") else comm, _p(k, _u64), _p(M)))
+    return int(k[0]), M.reshape(3, 3)
+
+
+def local_group(nranks):
+    """An in-process rank group (sfm_comm_init_local): one handle per rank,
+    for N host threads sharing one process (and possibly one GPU)."""
+    hs = (ctypes.c_void_p * nranks)()
+    _check(_lib.sfm_comm_init_local(nranks, hs))
+    return [LocalComm(h, nranks, r) for r, h in enumerate(hs)]
+
+
+class LocalComm:
+    def __init__(self, h, nranks, rank):
+        self.h = ctypes.c_void_p(h)
+        self.nranks, self.rank = nranks, rank
+
+    def close(self):
+        if self.h:
+            _lib.sfm_comm_destroy(self.h)
+            self.h = ctypes.c_void_p()
 
 
 def h4_batch(x1s, x2s):

@@ -6,10 +6,12 @@ systems with one all-reduce per LM iteration.  Here a numpy restatement of
 that partial system (test infrastructure, built on the oracle's residual)
 runs on two gloo ranks and must equal the single-process system; a full
 distributed LM loop must reproduce the single-process oracle's converged
-cost.  RANSAC hypothesis sharding is checked with the (max count, min
-iteration) combine.
+cost.  RANSAC hypothesis sharding runs sfm_dist.ransac_sharded with the
+packed-key combine over gloo and must give the unsharded winner, model and
+mask.
 """
 import os
+import random
 import socket
 
 import numpy as np
@@ -23,6 +25,7 @@ import sfm_dist
 import sfm_synthetic as syn
 
 K = syn.K_REF
+H_RANSAC = 601  # odd: uneven shards
 
 
 def _free_port():
@@ -106,15 +109,23 @@ def _rank_main(rank, world, port, q):
         payload = torch.from_numpy(np.concatenate([part["S"].ravel(), part["diagU"], part["gc"], part["bZ"],
                                                    [part["cost"]]]))
         dist.all_reduce(payload)
-        # RANSAC: shard hypotheses, combine (max count, min iteration)
-        rng = np.random.default_rng(3)
-        counts = rng.integers(0, 7, 1000)
-        lo, hi = sfm_dist.hypothesis_range(1000, world, rank)
-        c = counts[lo:hi]
-        local = (int(c.max()), lo + int(np.argmax(c))) if c.max() > 0 else (0, -1)
-        gathered = [None] * world
-        dist.all_gather_object(gathered, local)
-        q.put((rank, payload.numpy(), sfm_dist.combine_ransac(gathered), (int(counts.max()), int(np.argmax(counts)))))
+        # RANSAC: the real sharding code (sfm_dist.ransac_sharded + the
+        # torch.distributed key combine) with the oracle as each shard's
+        # fit/score (on the GPU: sfm_ransac_f8_pyrandom_range)
+        x1, x2, _, _ = syn.two_view(n=400, seed=4)
+        random.seed(7)
+        table = np.array([random.sample(range(400), 8) for _ in range(H_RANSAC)], dtype=np.int32)
+        st_after = random.getstate()
+
+        def shard_fn(h0, h1):
+            if h1 <= h0:
+                return 0, np.zeros(9)
+            b, counts, F, _ = O.ransac(x1, x2, table[h0:h1], 0.06)
+            return (sfm_dist.shard_key(counts[b], h0 + b), F) if b >= 0 else (0, np.zeros(9))
+
+        it, F, mask = sfm_dist.ransac_sharded(len(x1), H_RANSAC, rank, world, shard_fn,
+                                              sfm_dist.combine_keys_torch, lambda M: O.ransac_mask(x1, x2, M, 0.06))
+        q.put((rank, payload.numpy(), (it, F, mask, st_after)))
     finally:
         dist.destroy_process_group()
 
@@ -136,9 +147,16 @@ def test_sharded_reduced_system_equals_full_gloo():
     t = np.einsum("nij,nj->ni", -R, prob["C0"])
     full = partial_system(R, t, prob["X0"], prob["cam_idx"], prob["pt_idx"], prob["obs"], 4, 1e-3)
     ref = np.concatenate([full["S"].ravel(), full["diagU"], full["gc"], full["bZ"], [full["cost"]]])
-    for rank, payload, ransac, ransac_ref in out:
+    # the unsharded RANSAC on the same table
+    x1, x2, _, _ = syn.two_view(n=400, seed=4)
+    random.seed(7)
+    table = np.array([random.sample(range(400), 8) for _ in range(H_RANSAC)], dtype=np.int32)
+    b_ref, _, F_ref, mask_ref = O.ransac(x1, x2, table, 0.06)
+    assert b_ref >= 0
+    for rank, payload, (it, F, mask, st_after) in out:
         assert np.allclose(payload, ref, rtol=1e-10, atol=1e-9 * np.abs(ref).max())
-        assert ransac == ransac_ref
+        assert it == b_ref and np.array_equal(F, F_ref) and np.array_equal(mask, mask_ref)
+        assert st_after == random.getstate()  # every rank's stream ends where the unsharded draw leaves it
 
 
 def distributed_lm(shards, nc, iters=30, lam=1e-4):
@@ -223,3 +241,24 @@ def test_shard_covers_every_observation_once():
             tot += len(ci)
         seen.append(tot)
     assert all(s == len(prob["cam_idx"]) for s in seen)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_combine_keys_keeps_first_strict_max(world):
+    """The packed key's max over any split of the hypotheses equals the
+    reference's scan: max count, earliest iteration on ties; key 0 when no
+    hypothesis has an inlier."""
+    rng = np.random.default_rng(world)
+    for counts in (rng.integers(0, 5, 997), np.zeros(50, dtype=int), np.array([3, 7, 7, 1, 7])):
+        H = len(counts)
+        keys = []
+        for rank in range(world):
+            h0, h1 = sfm_dist.hypothesis_range(H, world, rank)
+            c = counts[h0:h1]
+            keys.append(sfm_dist.shard_key(c.max(), h0 + int(np.argmax(c))) if len(c) else 0)
+        cnt, it = sfm_dist.key_iter(max(keys))
+        best, best_i = 0, -1
+        for i, c in enumerate(counts):  # GetInliersRANSAC.py:85-88
+            if c > best:
+                best, best_i = c, i
+        assert (cnt, it) == (best, best_i)

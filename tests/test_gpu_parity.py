@@ -155,6 +155,77 @@ def test_ransac_pyrandom_matches_host_table(core, H):
             assert np.array_equal(M1, M0)
 
 
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_ransac_sharded_matches_single_rank_cfg2(core, golden, world):
+    """Hypothesis-sharded F-RANSAC on cfg2 (16384 hypotheses):
+    every rank draws the whole table from the global stream and scores its
+    range (sfm_ransac_f8_pyrandom_range); the keys are combined across
+    `world` in-process ranks sharing the GPU (sfm_ransac_combine, one host
+    thread per rank); the winner's F gives the mask.  Counts, winner, F,
+    mask and the RNG state equal the unsharded reference fixture."""
+    import threading
+    import sfm_dist
+    c = golden("ransac_cfg2.npz")
+    x1, x2 = c["x1"], c["x2"]
+    H = int(c["s0_n_max"])
+    shards, counts = [], []
+    for rank in range(world):  # each rank's own process would do exactly this
+        random.seed(0)
+        h0, h1 = sfm_dist.hypothesis_range(H, world, rank)
+        key, F, cnt = core.ransac_f8_range(x1, x2, H, h0, h1, 0.06, want_counts=True)
+        assert np.array_equal(np.array(random.getstate()[1], dtype=np.uint32), c["s0_state_after"])
+        shards.append((key, F))
+        counts.append(cnt)
+    assert np.array_equal(np.concatenate(counts), c["s0_counts"].astype(np.int32))
+    comms = core.local_group(world)
+    out = [None] * world
+
+    def run(rank):
+        out[rank] = sfm_dist.ransac_sharded(
+            len(x1), H, rank, world, lambda h0, h1: shards[rank],
+            lambda k, M: core.ransac_combine(comms[rank], k, M),
+            lambda M: core.ransac_mask(x1, x2, M, 0.06))
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=60)
+    for cm in comms:
+        cm.close()
+    for it, F, mask in out:
+        assert it == int(c["s0_best_iter"])
+        assert rel(F, c["s0_F"]) < 1e-9
+        assert np.array_equal(np.nonzero(mask)[0], c["s0_inlier_pos"])
+    # the given-table form agrees shard by shard
+    random.seed(0)
+    table = core.sample_table(len(x1), 8, H)
+    for rank in range(world):
+        h0, h1 = sfm_dist.hypothesis_range(H, world, rank)
+        k2, F2, _ = core.ransac_f8_range(x1, x2, H, h0, h1, 0.06, samples=table)
+        assert k2 == shards[rank][0] and (k2 == 0 or np.array_equal(F2, shards[rank][1]))
+
+
+def test_ransac_h4_sharded_matches_single_rank(core):
+    """Homography shards: concatenated counts and the combined key equal the
+    unsharded in-call RANSAC's."""
+    import sfm_dist
+    x1, x2, _, _ = syn.two_view(n=3000, seed=4)
+    random.seed(11)
+    b0, M0, m0, c0, _ = core.ransac_h4_pyrandom(x1, x2, 3001, 30.0, want_counts=True)
+    keys, cnts = [], []
+    for rank in range(3):
+        random.seed(11)
+        h0, h1 = sfm_dist.hypothesis_range(3001, 3, rank)
+        k, M, cnt = core.ransac_h4_range(x1, x2, 3001, h0, h1, 30.0, want_counts=True)
+        keys.append((k, M))
+        cnts.append(cnt)
+    assert np.array_equal(np.concatenate(cnts), c0)
+    k, M = max(keys, key=lambda km: km[0])
+    assert sfm_dist.key_iter(k)[1] == b0 and np.array_equal(M, M0)
+    assert np.array_equal(core.ransac_mask(x1, x2, M, 30.0, model=4), m0)
+
+
 def test_ransac_edge_cases(core):
     from GetInliersRANSAC import GetInliersRANSAC, get_inliers_ransac
     x1, x2, idx, _ = syn.two_view(n=200, seed=3)

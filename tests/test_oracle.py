@@ -221,3 +221,33 @@ def test_rotvec_roundtrip():
         R = O.rotvec_to_R(w)
         assert np.allclose(R, Rotation.from_rotvec(w).as_matrix(), atol=1e-14)
         assert np.allclose(O.R_to_rotvec(R), Rotation.from_matrix(R).as_rotvec(), atol=1e-12)
+
+
+def test_cpu_strong_schur_lm_matches_oracle():
+    """bench.py's CPU-strong baseline (OpenMP Schur-LM, sfm_cpu_strong.c)
+    runs the oracle's LM: same iterations / accepted steps / status and the
+    same cost up to summation order."""
+    import sfm_synthetic as syn
+    K = syn.K_REF
+    for nc, npt, k, seed in ((6, 2000, 5, 3), (12, 3000, 4, 1)):
+        p = syn.ba_problem(nc, npt, k, seed=seed, dense=False)
+        cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
+        a = (cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K)
+        _, x1, r1 = O.ba_lm(*a, max_iterations=30)
+        _, x2, r2 = O.ba_lm_cpu_strong(*a, max_iterations=30)
+        assert (r1["iterations"], r1["accepted"], r1["status"]) == (r2["iterations"], r2["accepted"], r2["status"])
+        assert abs(r1["cost"] - r2["cost"]) <= 1e-9 * r1["cost"]
+        assert np.abs(x1 - x2).max() <= 1e-6
+
+
+def test_reference_loop_restatement_values():
+    """oracle/ref_loop.py (bench's timing restatement of the reference
+    residual loop) computes the oracle's residuals."""
+    import ref_loop
+    import sfm_synthetic as syn
+    p = syn.ba_problem(5, 60, 3, seed=2, dense=False)
+    cams = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
+    params = np.concatenate([cams.ravel(), p["X0"].ravel()])
+    r1 = ref_loop.residuals(params, 5, 60, p["cam_idx"], p["pt_idx"], p["obs"], syn.K_REF)
+    r2 = O.ba_residuals(cams, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], syn.K_REF)
+    assert np.abs(r1 - r2).max() <= 1e-9 * np.abs(r2).max()

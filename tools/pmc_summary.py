@@ -1,6 +1,6 @@
 """Summarise rocprofv3 runs into profiles/<round>/ (committed evidence).
 
-  python tools/pmc_summary.py gpurun_out/<dir> profiles/round1
+  python tools/pmc_summary.py gpurun_out/<dir> profiles/round2 [ITERATIONS]
 
 <dir> holds: kernel_trace/ (rocprofv3 --kernel-trace --stats) and
 FETCH_SIZE/, WRITE_SIZE/, TCC_HIT_sum_TCC_MISS_sum/ (separate --pmc passes).
@@ -8,6 +8,9 @@ Writes kernel_stats.csv (copy), kernel_stats.md and pmc_traffic.json with
 per-launch averages per kernel.  HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) *
 1024: FETCH_SIZE/WRITE_SIZE are KiB, and on gfx950 FETCH_SIZE reports half
 of a wide coalesced read (MI355X_MICROARCH.md, HBM section).
+With ITERATIONS (the PMC passes profiled tools/ba_once.py running that many
+LM iterations), also pmc_iteration.json: every kernel's bytes summed over
+its launches / ITERATIONS -- the HBM traffic of one LM iteration.
 """
 import collections
 import csv
@@ -21,7 +24,7 @@ def short(name):
     return name.split("(")[0].replace("sfm::", "")
 
 
-def main(src, dst):
+def main(src, dst, iterations=0):
     os.makedirs(dst, exist_ok=True)
     ks = os.path.join(src, "kernel_trace", "run_kernel_stats.csv")
     out = {}
@@ -43,14 +46,22 @@ def main(src, dst):
         for k, d in agg.items():
             for c, v in d.items():
                 out.setdefault(k, {})[c] = sum(v) / len(v)
+                out[k][c + "_total"] = sum(v)
+                out[k]["launches"] = len(v)
     for k, d in out.items():
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
             d["hbm_bytes_per_launch"] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
         if "TCC_HIT_sum" in d:
             d["l2_hit_rate"] = d["TCC_HIT_sum"] / max(1.0, d["TCC_HIT_sum"] + d.get("TCC_MISS_sum", 0))
     json.dump(out, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1, sort_keys=True)
+    if iterations:
+        per = {k: (2 * d["FETCH_SIZE_total"] + d["WRITE_SIZE_total"]) * 1024 / iterations
+               for k, d in out.items() if "FETCH_SIZE_total" in d and "WRITE_SIZE_total" in d}
+        json.dump({"iterations": iterations, "source": src, "total_bytes_per_iteration": sum(per.values()),
+                   "bytes_per_iteration": per}, open(os.path.join(dst, "pmc_iteration.json"), "w"),
+                  indent=1, sort_keys=True)
     print(json.dumps({k: {c: round(v, 1) for c, v in d.items()} for k, d in out.items() if "k_" in k}, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 0)
