@@ -27,3 +27,9 @@ for fn in (core.ransac_f8_pyrandom, core.ransac_h4_pyrandom):
         tm.append(core.last_timings())
     tm = np.median(np.array(tm), axis=0)
     print(fn.__name__, "wall ms %.3f" % np.median(w), "timings", np.round(tm, 4).tolist())
+# Python glue alone: the MT state round trip the drop-in does per call
+t = time.perf_counter()
+for _ in range(200):
+    v, st, g = core._mt_state()
+    core._mt_restore(v, st, g)
+print("mt state round trip ms %.4f" % ((time.perf_counter() - t) / 200 * 1e3))
