@@ -216,8 +216,8 @@ __device__ __forceinline__ void grid_sum_last(double (&v)[NV], double *partial, 
 //   Jc = [A (-[p]x) | A]  (2x6, rotation perturbed on the left: R <- exp([d]x) R)
 //   Jp = A R              (2x3)
 //   W  = Jc^T Jp = E (A^T A R),  E = [[p]x ; I]  (6x3)
-// so the J cache stores only r, A, p: 96 B per observation instead of 160.
-constexpr int JS = 12;  // r0 r1 | A row0 (3) | A row1 (3) | p (3) | pad
+// so (r, A, p) is all an observation needs, and it is recomputed from X and
+// the camera wherever it is used (no stored Jacobians).
 constexpr int ZS = 16;  // Schur record: p (3) | G = A^T A R L (9, row-major) | q = L^T g_p (3) | pad: one 128-B line
 
 __device__ __forceinline__ void obs_model(const double *__restrict__ Rt, const double *X, const double (&K)[9],
@@ -239,6 +239,26 @@ __device__ __forceinline__ void obs_model(const double *__restrict__ Rt, const d
     }
 }
 
+// (A, p) of obs_model without the residual: the same expression trees, so
+// the same values bit for bit (no J cache: every consumer recomputes them
+// from X and the camera instead of re-reading 96 B per observation)
+__device__ __forceinline__ void obs_Ap(const double *__restrict__ Rt, const double *X, const double (&K)[9],
+                                       double (&A)[2][3], double (&p)[3]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) p[i] = Rt[3 * i] * X[0] + Rt[3 * i + 1] * X[1] + Rt[3 * i + 2] * X[2];
+    const double xc0 = p[0] + Rt[9], xc1 = p[1] + Rt[10], xc2 = p[2] + Rt[11];
+    double u[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) u[i] = K[3 * i] * xc0 + K[3 * i + 1] * xc1 + K[3 * i + 2] * xc2;
+    const double iw = 1.0 / (u[2] + 1e-8);
+    const double pu = u[0] * iw, pv = u[1] * iw;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        A[0][c] = -(iw * K[c] - pu * iw * K[6 + c]);
+        A[1][c] = -(iw * K[3 + c] - pv * iw * K[6 + c]);
+    }
+}
+
 __device__ __forceinline__ void jc_of(const double (&A)[2][3], const double (&p)[3], double (&Jc)[2][6]) {
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
@@ -249,13 +269,6 @@ __device__ __forceinline__ void jc_of(const double (&A)[2][3], const double (&p)
         Jc[a][4] = A[a][1];
         Jc[a][5] = A[a][2];
     }
-}
-
-__device__ __forceinline__ void load_j(const double *__restrict__ j, double (&r)[2], double (&A)[2][3],
-                                       double (&p)[3]) {
-    r[0] = j[0]; r[1] = j[1];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) { A[0][c] = j[2 + c]; A[1][c] = j[5 + c]; p[c] = j[8 + c]; }
 }
 
 __device__ __forceinline__ double obs_cost(const double *__restrict__ Rt, const double *X, const double (&K)[9],
@@ -280,7 +293,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_linearize(int64_t np_, const int
                                                           const int32_t *__restrict__ cam,
                                                           const double2 *__restrict__ obs, Kmat Km,
                                                           const double *__restrict__ Rt,
-                                                          const double *__restrict__ X, double *__restrict__ J,
+                                                          const double *__restrict__ X,
                                                           double *__restrict__ Vg, double *__restrict__ partial,
                                                           unsigned *__restrict__ counter, double *__restrict__ cost_out,
                                                           int want_cost, const int *__restrict__ gate, double gtol,
@@ -300,11 +313,6 @@ __global__ void __launch_bounds__(PT_THREADS) k_linearize(int64_t np_, const int
             const double *Rt_c = Rt + 12 * cam[o];
             double r[2], A[2][3], q[3];
             obs_model(Rt_c, x, K, obs[o], r, A, q);
-            double *j = J + (int64_t)JS * o;
-            j[0] = r[0]; j[1] = r[1];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) { j[2 + c] = A[0][c]; j[5 + c] = A[1][c]; j[8 + c] = q[c]; }
-            j[11] = 0.0;
             double Jp[2][3];
 #pragma unroll
             for (int a = 0; a < 2; ++a)
@@ -359,7 +367,7 @@ __global__ void __launch_bounds__(OBS_THREADS) k_point_prep(int64_t no, const in
                                                             const int32_t *__restrict__ pstart,
                                                             const int32_t *__restrict__ cam,
                                                             const double *__restrict__ Rt,
-                                                            const double *__restrict__ J,
+                                                            const double *__restrict__ X, Kmat Km,
                                                             const double *__restrict__ Vg, const double *__restrict__ lam,
                                                             double *__restrict__ Lq, double *__restrict__ Z, const int *__restrict__ gate) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
@@ -394,9 +402,13 @@ __global__ void __launch_bounds__(OBS_THREADS) k_point_prep(int64_t no, const in
         lq[0] = L[0][0]; lq[1] = L[0][1]; lq[2] = L[0][2]; lq[3] = L[1][1]; lq[4] = L[1][2]; lq[5] = L[2][2];
         lq[6] = qp[0]; lq[7] = qp[1]; lq[8] = qp[2];
     }
-    double r[2], A[2][3], q[3];
-    load_j(J + (int64_t)JS * o, r, A, q);
+    double K[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) K[i] = Km.k[i];
     const double *R = Rt + 12 * cam[o];
+    const double xp[3] = {X[3 * p], X[3 * p + 1], X[3 * p + 2]};
+    double A[2][3], q[3];
+    obs_Ap(R, xp, K, A, q);
     double T[2][3];  // (A R) L
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
@@ -729,7 +741,9 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
 // adds every camera's items in order into camlin (deterministic, one launch).
 __global__ void __launch_bounds__(256) k_camera_lin(const PairItem *__restrict__ items,
                                                     const int32_t *__restrict__ cam_obs,
-                                                    const double *__restrict__ J, double *__restrict__ slab2,
+                                                    const int32_t *__restrict__ pt, const double2 *__restrict__ obs,
+                                                    const double *__restrict__ X, const double *__restrict__ Rt,
+                                                    Kmat Km, double *__restrict__ slab2,
                                                     const BlockInfo *__restrict__ blocks, int32_t nblocks,
                                                     double *__restrict__ camlin, unsigned *__restrict__ counter,
                                                     const int *__restrict__ gate) {
@@ -737,12 +751,19 @@ __global__ void __launch_bounds__(256) k_camera_lin(const PairItem *__restrict__
     __shared__ double red[4][CAMLIN];
     __shared__ int last;
     const PairItem it = items[blockIdx.x];
+    double K[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) K[i] = Km.k[i];
+    const double *Rc = Rt + 12 * it.blk;  // the item's camera
     double acc[CAMLIN];
 #pragma unroll
     for (int k = 0; k < CAMLIN; ++k) acc[k] = 0.0;
     for (int32_t k = it.k0 + threadIdx.x; k < it.k1; k += 256) {
+        const int32_t o = cam_obs[k];
+        const int64_t p = pt[o];
+        const double xp[3] = {X[3 * p], X[3 * p + 1], X[3 * p + 2]};
         double rr[2], A[2][3], q[3], Jc[2][6];
-        load_j(J + (int64_t)JS * cam_obs[k], rr, A, q);
+        obs_model(Rc, xp, K, obs[o], rr, A, q);
         jc_of(A, q, Jc);
         const double r0 = rr[0], r1 = rr[1];
         double a[6], b[6];
@@ -1393,7 +1414,6 @@ template <int G>
 __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const int32_t *__restrict__ pstart,
                                                               const int32_t *__restrict__ cam,
                                                               const double2 *__restrict__ obs, Kmat Km,
-                                                              const double *__restrict__ J,
                                                               const double *__restrict__ Vg,
                                                               const double *__restrict__ Lq,
                                                               const double *__restrict__ dc, const double *__restrict__ lam,
@@ -1419,11 +1439,12 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
     const int32_t o0 = live ? pstart[p] : 0, o1 = live ? pstart[p + 1] : 0;
     // W^T dc = Jp^T (Jc dc) = R^T A^T (A (dtheta x p + dt)), summed over the point's observations
     double wt[3] = {0, 0, 0};
+    const double x[3] = {live ? X[3 * p] : 0.0, live ? X[3 * p + 1] : 0.0, live ? X[3 * p + 2] : 0.0};
     for (int32_t o = o0 + sub; o < o1; o += G) {
-        double rr[2], A[2][3], q[3];
-        load_j(J + (int64_t)JS * o, rr, A, q);
         const double *d = dc + 6 * cam[o];
         const double *R = Rt + 12 * cam[o];
+        double A[2][3], q[3];
+        obs_Ap(R, x, K, A, q);
         const double v0 = d[1] * q[2] - d[2] * q[1] + d[3];
         const double v1 = d[2] * q[0] - d[0] * q[2] + d[4];
         const double v2 = d[0] * q[1] - d[1] * q[0] + d[5];
@@ -1446,7 +1467,6 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
         const double y1 = l[1] * rhs[0] + l[3] * rhs[1];
         const double y2 = l[2] * rhs[0] + l[4] * rhs[1] + l[5] * rhs[2];
         const double dp[3] = {l[0] * y0 + l[1] * y1 + l[2] * y2, l[3] * y1 + l[4] * y2, l[5] * y2};
-        const double x[3] = {X[3 * p], X[3 * p + 1], X[3 * p + 2]};
         double xn[3];
         const double dg[3] = {vg[0], vg[3], vg[5]};
 #pragma unroll
@@ -1758,7 +1778,7 @@ struct sfm_ba_problem {
     int2 *d_sw_blkij = nullptr;
     double2 *d_obs = nullptr;
     double *d_Rt = nullptr, *d_Rt2 = nullptr, *d_X = nullptr, *d_X2 = nullptr;
-    double *d_J = nullptr, *d_Vg = nullptr, *d_Lq = nullptr, *d_Z = nullptr;
+    double *d_Vg = nullptr, *d_Lq = nullptr, *d_Z = nullptr;
     double *d_payload = nullptr, *d_A = nullptr, *d_b = nullptr, *d_D = nullptr;
     double *d_partial = nullptr, *d_scal = nullptr;
     int *d_bad = nullptr;
@@ -1967,7 +1987,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = p->alloc(p->d_slab2, (int64_t)CAMLIN * std::max<int64_t>(1, p->ndiag_items))) ||
         (rc = p->alloc(p->d_Rt, 12 * (int64_t)nc)) || (rc = p->alloc(p->d_Rt2, 12 * (int64_t)nc)) ||
         (rc = p->alloc(p->d_X, 3 * np_)) || (rc = p->alloc(p->d_X2, 3 * np_)) ||
-        (rc = p->alloc(p->d_J, (int64_t)JS * no)) || (rc = p->alloc(p->d_Vg, 9 * np_)) || (rc = p->alloc(p->d_Lq, 9 * np_)) ||
+        (rc = p->alloc(p->d_Vg, 9 * np_)) || (rc = p->alloc(p->d_Lq, 9 * np_)) ||
         (rc = p->alloc(p->d_Z, (int64_t)ZS * no)) || (rc = p->alloc(p->d_payload, p->payload_len + 8)) ||
         (rc = p->alloc(p->d_A, (int64_t)p->nsp * p->nsp)) || (rc = p->alloc(p->d_b, p->nsp)) ||
         (rc = p->alloc(p->d_D, 2 * 32 * 32)) ||
@@ -2193,13 +2213,14 @@ static int run_linearize(sfm_ba_problem *p, int par, int want_cost) {
     const int nbl = std::max(1, ceil_div(p->np * gl, PT_THREADS));
 #define SFM_LIN(G)                                                                                                \
     hipLaunchKernelGGL(k_linearize<G>, dim3(nbl), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam, p->d_obs, \
-                       p->K, p->d_Rt, p->d_X, p->d_J, p->d_Vg, p->d_partial, p->d_count, p->d_scal + 8, want_cost, glin, \
+                       p->K, p->d_Rt, p->d_X, p->d_Vg, p->d_partial, p->d_count, p->d_scal + 8, want_cost, glin, \
                        p->gtol, p->d_nbig)
     switch (gl) { case 1: SFM_LIN(1); break; case 2: SFM_LIN(2); break; case 4: SFM_LIN(4); break; default: SFM_LIN(8); }
 #undef SFM_LIN
     SFM_HIP(hipGetLastError());
     if (p->ndiag_items) {
-        hipLaunchKernelGGL(k_camera_lin, dim3(p->ndiag_items), dim3(256), 0, s, p->d_items, p->d_cam_obs, p->d_J,
+        hipLaunchKernelGGL(k_camera_lin, dim3(p->ndiag_items), dim3(256), 0, s, p->d_items, p->d_cam_obs, p->d_pt,
+                           p->d_obs, p->d_X, p->d_Rt, p->K,
                            p->d_slab2, p->d_blocks, p->ndiag_blocks, p->d_camlin, p->d_count + 2 * GS_WORDS, glin);
         SFM_HIP(hipGetLastError());
     }
@@ -2218,7 +2239,7 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     int *bad = p->d_bad + par;
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_PREP], s));
     hipLaunchKernelGGL(k_point_prep, dim3(std::max(1, ceil_div(p->no, OBS_THREADS))), dim3(OBS_THREADS), 0, s, (int64_t)p->no,
-                       p->d_pt, p->d_pstart, p->d_cam, p->d_Rt, p->d_J, p->d_Vg, lam, p->d_Lq, p->d_Z, gst);
+                       p->d_pt, p->d_pstart, p->d_cam, p->d_Rt, p->d_X, p->K, p->d_Vg, lam, p->d_Lq, p->d_Z, gst);
     SFM_HIP(hipGetLastError());
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_PREP + 1], s));
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SCHUR], s));
@@ -2248,7 +2269,7 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     const int nbb = std::max(1, std::min(ceil_div(p->np * gb, PT_THREADS), env_int("SFM_BACKSUB_BLOCKS", 1024)));
 #define SFM_BS(G)                                                                                                  \
     hipLaunchKernelGGL(k_backsub_trial<G>, dim3(nbb), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam,        \
-                       p->d_obs, p->K, p->d_J, p->d_Vg, p->d_Lq, p->d_b, lam, p->d_Rt, p->d_Rt2, p->d_X, p->d_X2, \
+                       p->d_obs, p->K, p->d_Vg, p->d_Lq, p->d_b, lam, p->d_Rt, p->d_Rt2, p->d_X, p->d_X2, \
                        p->d_partial, p->d_count + GS_WORDS, p->d_scal, gst)
     switch (gb) { case 1: SFM_BS(1); break; case 2: SFM_BS(2); break; case 4: SFM_BS(4); break; default: SFM_BS(8); }
 #undef SFM_BS
