@@ -14,10 +14,11 @@
 //   k_pnp_general  LinearPnP on all N points (one wave): Givens QR of the
 //                  2N x 12 system to 12 x 12, Jacobi SVD for the (unique,
 //                  N >= 6) null vector; N = 4, 5 take the dgebd2 path.
-//   k_nonlinear_pnp one workgroup per problem: MINPACK lmdif (scipy 'lm',
-//                  forward differences, max_nfev) on the 2N-residual loss;
-//                  residuals, Jacobian columns and every m-long reduction
-//                  run across the workgroup, the 6 x 6 lmpar on one lane.
+//   k_nonlinear_pnp one 512-thread workgroup per problem: MINPACK lmdif
+//                  (scipy 'lm', forward differences, max_nfev) on the
+//                  2N-residual loss; the Jacobian rows stay in registers and
+//                  are reduced to their 6 x 6 R factor by CholeskyQR2, then
+//                  qrfac (column pivoting) and lmpar run on lane 0.
 //
 // numpy evaluates the small products through OpenBLAS; the operation orders
 // used here are the measured ones (oracle/sfm_oracle_pnp.c header), with FP
@@ -606,8 +607,6 @@ __global__ void __launch_bounds__(PG_THREADS) k_pnp_general(const double *__rest
 }
 
 // ---------------------------------------------------------- NonlinearPnP
-constexpr int NL_THREADS = 256;
-
 // scipy Rotation.from_rotvec(...).as_matrix() (quaternion path)
 __device__ __forceinline__ void scipy_rotvec_to_R(const double *rv, double (&R)[9]) {
     const double x = rv[0], y = rv[1], z = rv[2];
@@ -669,66 +668,114 @@ __device__ void nlpnp_projection(const Cam3 &K, const double *p, double *P) {
     pnp_projection(K, C, R, P);
 }
 
-struct WGReduce {
-    double *red;  // LDS, NL_THREADS
-    // wave totals by shuffles, then the NL_THREADS / 64 of them in a fixed
-    // order: two barriers per m-long sum instead of a 10-barrier LDS tree
-    __device__ double sum(double v) const {
-        const int t = threadIdx.x;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        __syncthreads();  // the previous sum's readers are done with red
-        if ((t & 63) == 0) red[t >> 6] = v;
-        __syncthreads();
-        double r = 0;
-#pragma unroll
-        for (int k = 0; k < NL_THREADS / 64; ++k) r += red[k];
-        return r;
-    }
-};
+// ---- NonlinearPnP: MINPACK lmdif (NonlinearPnP.py:98-123 via scipy 'lm')
+// in one 512-thread workgroup.  The m = 2N residual rows never leave
+// registers: each forward-difference Jacobian (fdjac2: the base and the six
+// perturbed projections of every point, in one pass) is reduced to its
+// 6 x 6 R factor and Q^T f by CholeskyQR2 -- pass 1 sums the Gram matrix
+// J^T J (fixed-order block sums), R1 = chol; pass 2 recomputes the rows,
+// q = J R1^-1, sums q^T q and q^T f, R2 = chol, R = R2 R1, Q^T f = R2^-T q^T f
+// (orthogonal to working precision for cond(J) up to ~1e8).  MINPACK's
+// qrfac with column pivoting then runs on R (6 x 6, lane 0): the trailing
+// column norms it pivots on are invariant under Q, so it picks the pivots
+// qrfac would pick on J.  lmpar, the trust region and the stopping tests are
+// lmdif's (the same code as before), one trial evaluation per inner
+// iteration (one pass + a block sum).
+constexpr int NL2_THREADS = 512;  // 256 VGPRs per lane: the row pass holds 27 sums + two Jacobian rows
+constexpr int NL2_WAVES = NL2_THREADS / 64;
 
-// Residuals of pose p (LDS, 6) into f (2N): (x - proj).flatten()
-__device__ void nlpnp_eval(const Cam3 &K, const double *p, double *sP, const double *X, const double2 *x, int64_t n,
-                           double *f) {
-    __syncthreads();
-    if (threadIdx.x == 0) nlpnp_projection(K, p, sP);
-    __syncthreads();
-    double P[12];
+// fixed-order block sum of NV values per thread; every thread gets the totals
+template <int NV>
+__device__ __forceinline__ void nl2_sum(double (&v)[NV], double (*red)[NV]) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-    for (int k = 0; k < 12; ++k) P[k] = sP[k];
-    for (int64_t i = threadIdx.x; i < n; i += NL_THREADS) {
-        double u, v;
-        pnp_project(P, X[3 * i], X[3 * i + 1], X[3 * i + 2], u, v);
-        const double2 q = x[i];
-        f[2 * i] = q.x - u;
-        f[2 * i + 1] = q.y - v;
+    for (int k = 0; k < NV; ++k) {
+        double x = v[k];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+        v[k] = x;
     }
+    __syncthreads();  // the previous sum's readers are done with red
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) red[w][k] = v[k];
     __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        double x = 0;
+#pragma unroll
+        for (int i = 0; i < NL2_WAVES; ++i) x += red[i][k];
+        v[k] = x;
+    }
+}
+
+// Cholesky of a 6 x 6 SPD matrix given as its upper triangle (21, row-major
+// packed); R upper with R^T R = G.  false on a non-positive pivot.
+__device__ __forceinline__ bool chol6(const double *G, double (&R)[6][6]) {
+    double A[6][6];
+    int u = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = i; j < 6; ++j) { A[i][j] = G[u++]; A[j][i] = A[i][j]; }
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        double d = A[j][j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) d -= R[k][j] * R[k][j];
+        ok = ok && d > 0.0;
+        d = sqrt(d);
+        R[j][j] = d;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            if (i < j) R[j][i] = 0.0;
+            if (i <= j) continue;
+            double v = A[j][i];
+#pragma unroll
+            for (int k = 0; k < j; ++k) v -= R[k][j] * R[k][i];
+            R[j][i] = v / d;
+        }
+    }
+    return ok;
 }
 
 struct NlShared {
-    double p[6], pt[6], sP[12];
-    double red[NL_THREADS];
-    double rdiag[6], acnorm[6], wa[6], qtf[6], wa1[6], wa2[6], wa3[6];
-    double r6[6][6];  // upper triangle of the QR factor, column-major r6[col][row]
-    double par, delta, xnorm, fnorm, fnorm1, gnorm, ratio, ajnorm, temp;
+    double p[6], pt[6], sP[7][12], R1[6][6];
+    double g[28];  // Gram sums; [21..27) pass 2's 1 / R1[j][j]
+    double rdiag[6], acnorm[6], wa1[6], wa3[6], qtf[6];
+    double r6[6][6];  // upper triangle of the pivoted QR factor, column-major r6[col][row]
+    double par, delta, xnorm, fnorm, gnorm, ratio, temp;
     int ipvt[6], info, nfev, iter, flag;
 };
 
-// One workgroup per problem.  scratch: 9 m doubles (fvec, wa4, wf, fjac).
-// out: C (3) | R (9) | info (as double)
-__global__ void __launch_bounds__(NL_THREADS) k_nonlinear_pnp(const double *__restrict__ X,
-                                                              const double2 *__restrict__ x, int64_t n, Cam3 K,
-                                                              const double *__restrict__ C0,
-                                                              const double *__restrict__ R0, int32_t maxfev,
-                                                              double *__restrict__ scratch,
-                                                              double *__restrict__ out) {
+// Residual rows of point i under projection P: f = (x - proj).flatten()
+// (one reciprocal of w instead of two divides: the rows are within an ulp
+// of numpy's, and the row passes are FP64-throughput bound on one CU)
+__device__ __forceinline__ void nl2_res(const double *P, double X, double Y, double Z, double2 q, double &f0,
+                                        double &f1) {
+    const double h0 = fma(P[3], 1.0, fma(P[2], Z, fma(P[1], Y, P[0] * X)));
+    const double h1 = fma(P[7], 1.0, fma(P[6], Z, fma(P[5], Y, P[4] * X)));
+    const double h2 = fma(P[11], 1.0, fma(P[10], Z, fma(P[9], Y, P[8] * X)));
+    const double iw = 1.0 / (h2 + 1e-8);
+    f0 = q.x - h0 * iw;
+    f1 = q.y - h1 * iw;
+}
+__device__ __forceinline__ void nl2_res(const double *P, const double *X, const double2 *x, int64_t i, double &f0,
+                                        double &f1) {
+    nl2_res(P, X[3 * i], X[3 * i + 1], X[3 * i + 2], x[i], f0, f1);
+}
+
+// One workgroup per problem.  out: C (3) | R (9) | info (as double)
+__global__ void __launch_bounds__(NL2_THREADS) k_nonlinear_pnp(const double *__restrict__ X,
+                                                               const double2 *__restrict__ x, int64_t n, Cam3 K,
+                                                               const double *__restrict__ C0,
+                                                               const double *__restrict__ R0, int32_t maxfev,
+                                                               double *__restrict__ out) {
     __shared__ NlShared S;
-    const WGReduce rd{S.red};
+    __shared__ double red27[NL2_WAVES][27];
+    __shared__ double red1[NL2_WAVES][1];
     const int t = threadIdx.x;
-    const int64_t m = 2 * n;
-    double *fvec = scratch, *wa4 = scratch + m, *wf = scratch + 2 * m, *fjac = scratch + 3 * m;
-    auto col = [&](int j) { return fjac + (int64_t)j * m; };
     if (t == 0) {
         for (int k = 0; k < 3; ++k) out[k] = C0[k];
         for (int k = 0; k < 9; ++k) out[3 + k] = R0[k];
@@ -740,6 +787,7 @@ __global__ void __launch_bounds__(NL_THREADS) k_nonlinear_pnp(const double *__re
                 S.p[3 + i] = fma(-R0[i * 3 + 2], C0[2], fma(-R0[i * 3], C0[0], (-R0[i * 3 + 1]) * C0[1]));
             for (int k = 0; k < 6; ++k)
                 if (isnan(S.p[k])) S.flag = 1;
+            nlpnp_projection(K, S.p, S.sP[0]);
         } else {
             S.flag = 2;
         }
@@ -747,134 +795,176 @@ __global__ void __launch_bounds__(NL_THREADS) k_nonlinear_pnp(const double *__re
     __syncthreads();
     if (S.flag == 2) return;                                      // n < 4: C, R unchanged
     if (S.flag == 1) { if (t == 0) out[12] = -1.0; return; }      // except path
-    nlpnp_eval(K, S.p, S.sP, X, x, n, fvec);
+    // initial residual norm and finiteness
     {
+        double v[1] = {0.0};
         int fin = 1;
-        for (int64_t i = t; i < m; i += NL_THREADS) fin &= isfinite(fvec[i]) ? 1 : 0;
-        if (rd.sum((double)(1 - fin)) != 0.0) { if (t == 0) out[12] = -1.0; return; }
-    }
-    double ss = 0;
-    for (int64_t i = t; i < m; i += NL_THREADS) ss += fvec[i] * fvec[i];
-    const double fn0 = sqrt(rd.sum(ss));
-    if (t == 0) {
-        S.fnorm = fn0; S.par = 0.0; S.delta = 0.0; S.xnorm = 0.0; S.iter = 1; S.nfev = 1; S.info = 0;
+        for (int64_t i = t; i < n; i += NL2_THREADS) {
+            double f0, f1;
+            nl2_res(S.sP[0], X, x, i, f0, f1);
+            fin &= (isfinite(f0) && isfinite(f1)) ? 1 : 0;
+            v[0] += f0 * f0 + f1 * f1;
+        }
+        double nf[1] = {(double)(1 - fin)};
+        nl2_sum<1>(nf, red1);
+        if (nf[0] != 0.0) { if (t == 0) out[12] = -1.0; return; }
+        nl2_sum<1>(v, red1);
+        if (t == 0) {
+            S.fnorm = sqrt(v[0]); S.par = 0.0; S.delta = 0.0; S.xnorm = 0.0; S.iter = 1; S.nfev = 1; S.info = 0;
+        }
     }
     __syncthreads();
     const double eps = 1.4901161193847656e-08;
     for (;;) {
-        // ---- forward-difference Jacobian (fdjac2)
+        // ---- fdjac2's seven projections: the base and p + h_j e_j
+        double h[6], ih[6];
+#pragma unroll
         for (int j = 0; j < 6; ++j) {
-            if (t == 0) {
-                const double temp = S.p[j];
-                double h = eps * fabs(temp);
-                if (h == 0.0) h = eps;
-                for (int k = 0; k < 6; ++k) S.pt[k] = S.p[k];
-                S.pt[j] = temp + h;
-            }
-            // every thread forms h itself from S.p (stable during fdjac2): reading
-            // S.h after the eval's barrier would race with lane 0 writing the
-            // next column's step
-            double h = eps * fabs(S.p[j]);
-            if (h == 0.0) h = eps;
-            nlpnp_eval(K, S.pt, S.sP, X, x, n, wf);
-            double *cj = col(j);
-            for (int64_t i = t; i < m; i += NL_THREADS) cj[i] = (wf[i] - fvec[i]) / h;
+            h[j] = eps * fabs(S.p[j]);
+            if (h[j] == 0.0) h[j] = eps;
+            ih[j] = 1.0 / h[j];
         }
-        if (t == 0) S.nfev += 6;
-        // ---- qrfac with column pivoting
-        for (int j = 0; j < 6; ++j) {
-            double s2 = 0;
-            const double *cj = col(j);
-            for (int64_t i = t; i < m; i += NL_THREADS) s2 += cj[i] * cj[i];
-            const double nrm = sqrt(rd.sum(s2));
-            if (t == 0) { S.acnorm[j] = nrm; S.rdiag[j] = nrm; S.wa[j] = nrm; S.ipvt[j] = j; }
+        if (t < 7) {
+            double pp[6];
+            for (int k = 0; k < 6; ++k) pp[k] = S.p[k];
+            if (t > 0) pp[t - 1] = S.p[t - 1] + h[t - 1];
+            nlpnp_projection(K, pp, S.sP[t]);
         }
         __syncthreads();
-        for (int j = 0; j < 6; ++j) {
-            if (t == 0) {
-                int kmax = j;
-                for (int k = j; k < 6; ++k)
-                    if (S.rdiag[k] > S.rdiag[kmax]) kmax = k;
-                S.flag = kmax;
-                if (kmax != j) {
-                    S.rdiag[kmax] = S.rdiag[j];
-                    S.wa[kmax] = S.wa[j];
-                    const int tp = S.ipvt[j]; S.ipvt[j] = S.ipvt[kmax]; S.ipvt[kmax] = tp;
-                }
+        // ---- pass 1: Gram matrix of the Jacobian rows
+        double gsum[27];
+#pragma unroll
+        for (int k = 0; k < 27; ++k) gsum[k] = 0.0;
+        for (int64_t i = t; i < n; i += NL2_THREADS) {
+            double b0, b1, J0[6], J1[6];
+            const double Xi = X[3 * i], Yi = X[3 * i + 1], Zi = X[3 * i + 2];
+            const double2 qi = x[i];
+            nl2_res(S.sP[0], Xi, Yi, Zi, qi, b0, b1);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                double w0, w1;
+                nl2_res(S.sP[1 + j], Xi, Yi, Zi, qi, w0, w1);
+                J0[j] = (w0 - b0) * ih[j];
+                J1[j] = (w1 - b1) * ih[j];
             }
-            __syncthreads();
-            const int kmax = S.flag;
-            if (kmax != j) {
-                double *a = col(j), *b = col(kmax);
-                for (int64_t i = t; i < m; i += NL_THREADS) { const double tv = a[i]; a[i] = b[i]; b[i] = tv; }
-            }
-            __syncthreads();
-            double *cj = col(j);
-            double s2 = 0;
-            for (int64_t i = j + t; i < m; i += NL_THREADS) s2 += cj[i] * cj[i];
-            // the pivot's sign is read before the sum's barriers: after them
-            // lane 0 may already have divided cj[j] (its loop starts at i = j)
-            const double cjj = cj[j];
-            double ajnorm = sqrt(rd.sum(s2));
-            if (ajnorm != 0.0) {
-                if (cjj < 0.0) ajnorm = -ajnorm;
-                for (int64_t i = j + t; i < m; i += NL_THREADS) cj[i] /= ajnorm;
-                __syncthreads();
-                if (t == 0) cj[j] += 1.0;
-                __syncthreads();
-                for (int k = j + 1; k < 6; ++k) {
-                    double *ck = col(k);
-                    double d = 0;
-                    for (int64_t i = j + t; i < m; i += NL_THREADS) d += cj[i] * ck[i];
-                    const double temp = rd.sum(d) / cj[j];
-                    for (int64_t i = j + t; i < m; i += NL_THREADS) ck[i] -= temp * cj[i];
-                    __syncthreads();
-                    if (t == 0) S.flag = 0;
-                    if (t == 0 && S.rdiag[k] != 0.0) {
-                        const double tt = ck[j] / S.rdiag[k];
-                        const double t2 = 1.0 - tt * tt;
-                        S.rdiag[k] *= sqrt(t2 > 0.0 ? t2 : 0.0);
-                        const double q = S.rdiag[k] / S.wa[k];
-                        if (0.05 * (q * q) <= lm::EPSMCH) S.flag = 1;
-                    }
-                    __syncthreads();
-                    if (S.flag) {
-                        double s3 = 0;
-                        for (int64_t i = j + 1 + t; i < m; i += NL_THREADS) s3 += ck[i] * ck[i];
-                        const double nr = sqrt(rd.sum(s3));
-                        if (t == 0) { S.rdiag[k] = nr; S.wa[k] = nr; }
-                        __syncthreads();
-                    }
-                }
-            }
-            if (t == 0) S.rdiag[j] = -ajnorm;
-            __syncthreads();
+            int u = 0;
+#pragma unroll
+            for (int a2 = 0; a2 < 6; ++a2)
+#pragma unroll
+                for (int c2 = a2; c2 < 6; ++c2) gsum[u++] += J0[a2] * J0[c2] + J1[a2] * J1[c2];
         }
-        // ---- first iteration scaling; Q^T f
-        if (t == 0 && S.iter == 1) {
-            double s3 = 0;
-            for (int k = 0; k < 6; ++k) s3 += S.p[k] * S.p[k];
-            S.xnorm = sqrt(s3);
-            S.delta = 100.0 * S.xnorm;
-            if (S.delta == 0.0) S.delta = 100.0;
-        }
-        for (int64_t i = t; i < m; i += NL_THREADS) wa4[i] = fvec[i];
-        __syncthreads();
-        for (int j = 0; j < 6; ++j) {
-            double *cj = col(j);
-            if (cj[j] != 0.0) {
-                double d = 0;
-                for (int64_t i = j + t; i < m; i += NL_THREADS) d += cj[i] * wa4[i];
-                const double temp = -rd.sum(d) / cj[j];
-                for (int64_t i = j + t; i < m; i += NL_THREADS) wa4[i] += cj[i] * temp;
-            }
-            __syncthreads();
-            if (t == 0) { cj[j] = S.rdiag[j]; S.qtf[j] = wa4[j]; }
-            __syncthreads();
-        }
+        nl2_sum<27>(gsum, red27);
         if (t == 0) {
-            for (int j = 0; j < 6; ++j)
-                for (int i = 0; i < 6; ++i) S.r6[j][i] = col(j)[i];
+#pragma unroll
+            for (int k = 0; k < 21; ++k) S.g[k] = gsum[k];
+            double R1[6][6];
+            if (!chol6(S.g, R1)) {  // numerically rank-deficient: shifted factor, pass 2 corrects
+                double tr = 0;
+                int u = 0;
+                for (int a2 = 0; a2 < 6; ++a2)
+                    for (int c2 = a2; c2 < 6; ++c2, ++u)
+                        if (a2 == c2) tr += S.g[u];
+                u = 0;
+                for (int a2 = 0; a2 < 6; ++a2)
+                    for (int c2 = a2; c2 < 6; ++c2, ++u)
+                        if (a2 == c2) S.g[u] += 1e-12 * tr + 1e-300;
+                chol6(S.g, R1);
+            }
+#pragma unroll
+            for (int a2 = 0; a2 < 6; ++a2) {
+#pragma unroll
+                for (int c2 = 0; c2 < 6; ++c2) S.R1[a2][c2] = R1[a2][c2];
+                S.g[21 + a2] = 1.0 / R1[a2][a2];  // pivot reciprocals for pass 2
+            }
+        }
+        __syncthreads();
+        // ---- pass 2: q = J R1^-1 rows (R1 read from LDS): q^T q and q^T f
+#pragma unroll
+        for (int k = 0; k < 27; ++k) gsum[k] = 0.0;
+        for (int64_t i = t; i < n; i += NL2_THREADS) {
+            double b0, b1, J0[6], J1[6];
+            const double Xi = X[3 * i], Yi = X[3 * i + 1], Zi = X[3 * i + 2];
+            const double2 qi = x[i];
+            nl2_res(S.sP[0], Xi, Yi, Zi, qi, b0, b1);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                double w0, w1;
+                nl2_res(S.sP[1 + j], Xi, Yi, Zi, qi, w0, w1);
+                J0[j] = (w0 - b0) * ih[j];
+                J1[j] = (w1 - b1) * ih[j];
+            }
+            double q0[6], q1[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                double a0 = J0[j], a1 = J1[j];
+#pragma unroll
+                for (int k = 0; k < j; ++k) { a0 -= q0[k] * S.R1[k][j]; a1 -= q1[k] * S.R1[k][j]; }
+                q0[j] = a0 * S.g[21 + j];
+                q1[j] = a1 * S.g[21 + j];
+            }
+            int u = 0;
+#pragma unroll
+            for (int a2 = 0; a2 < 6; ++a2)
+#pragma unroll
+                for (int c2 = a2; c2 < 6; ++c2) gsum[u++] += q0[a2] * q0[c2] + q1[a2] * q1[c2];
+#pragma unroll
+            for (int a2 = 0; a2 < 6; ++a2) gsum[21 + a2] += q0[a2] * b0 + q1[a2] * b1;
+        }
+        nl2_sum<27>(gsum, red27);
+        if (t == 0) {
+            double R2[6][6];
+            if (!chol6(gsum, R2)) {  // cannot happen for a full-rank J; keep R1
+                for (int a2 = 0; a2 < 6; ++a2)
+                    for (int c2 = 0; c2 < 6; ++c2) R2[a2][c2] = a2 == c2 ? 1.0 : 0.0;
+            }
+            // R = R2 R1 (column-major a[col][row] for qrfac), Q^T f = R2^-T (q^T f)
+            double a[6][6], qtu[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+#pragma unroll
+                for (int j = 0; j < 6; ++j) {
+                    double v = 0;
+#pragma unroll
+                    for (int k = 0; k < 6; ++k)
+                        if (k >= i && k <= j) v += R2[i][k] * S.R1[k][j];
+                    a[j][i] = i <= j ? v : 0.0;
+                }
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                double v = gsum[21 + i];
+#pragma unroll
+                for (int k = 0; k < i; ++k) v -= R2[k][i] * qtu[k];
+                qtu[i] = v / R2[i][i];
+            }
+            // ---- qrfac with column pivoting on R, Q'^T applied to Q^T f (lmdif's qtf loop)
+            int ipvt[6];
+            double rdiag[6], acnorm[6];
+            lm::qrfac<6, 6>(a, ipvt, rdiag, acnorm);
+            if (S.iter == 1) {
+                double s3 = 0;
+                for (int k = 0; k < 6; ++k) s3 += S.p[k] * S.p[k];
+                S.xnorm = sqrt(s3);
+                S.delta = 100.0 * S.xnorm;
+                if (S.delta == 0.0) S.delta = 100.0;
+            }
+            double wa4[6];
+            for (int i = 0; i < 6; ++i) wa4[i] = qtu[i];
+            for (int j = 0; j < 6; ++j) {
+                if (a[j][j] != 0.0) {
+                    double sum = 0.0;
+                    for (int i = j; i < 6; ++i) sum += a[j][i] * wa4[i];
+                    const double temp = -sum / a[j][j];
+                    for (int i = j; i < 6; ++i) wa4[i] += a[j][i] * temp;
+                }
+                a[j][j] = rdiag[j];
+                S.qtf[j] = wa4[j];
+            }
+            for (int j = 0; j < 6; ++j) {
+                S.ipvt[j] = ipvt[j];
+                S.acnorm[j] = acnorm[j];
+                for (int i = 0; i < 6; ++i) S.r6[j][i] = a[j][i];
+            }
+            S.nfev += 6;
             double gnorm = 0.0;
             if (S.fnorm != 0.0)
                 for (int j = 0; j < 6; ++j) {
@@ -913,11 +1003,17 @@ __global__ void __launch_bounds__(NL_THREADS) k_nonlinear_pnp(const double *__re
                 for (int j = 0; j < 6; ++j) s3 += S.wa3[j] * S.wa3[j];
                 S.temp = sqrt(s3);  // pnorm
                 if (S.iter == 1 && S.temp < S.delta) S.delta = S.temp;
+                nlpnp_projection(K, S.pt, S.sP[0]);
             }
-            nlpnp_eval(K, S.pt, S.sP, X, x, n, wa4);
-            double s4 = 0;
-            for (int64_t i = t; i < m; i += NL_THREADS) s4 += wa4[i] * wa4[i];
-            const double fnorm1 = sqrt(rd.sum(s4));
+            __syncthreads();
+            double v[1] = {0.0};
+            for (int64_t i = t; i < n; i += NL2_THREADS) {
+                double f0, f1;
+                nl2_res(S.sP[0], X, x, i, f0, f1);
+                v[0] += f0 * f0 + f1 * f1;
+            }
+            nl2_sum<1>(v, red1);
+            const double fnorm1 = sqrt(v[0]);
             if (t == 0) {
                 S.nfev += 1;
                 const double pnorm = S.temp, fnorm = S.fnorm;
@@ -952,7 +1048,6 @@ __global__ void __launch_bounds__(NL_THREADS) k_nonlinear_pnp(const double *__re
                     S.delta = pnorm / 0.5;
                     S.par = 0.5 * S.par;
                 }
-                S.flag = 0;
                 if (ratio >= 1e-4) {
                     for (int j = 0; j < 6; ++j) S.p[j] = S.pt[j];
                     double s6 = 0;
@@ -960,7 +1055,6 @@ __global__ void __launch_bounds__(NL_THREADS) k_nonlinear_pnp(const double *__re
                     S.xnorm = sqrt(s6);
                     S.fnorm = fnorm1;
                     S.iter += 1;
-                    S.flag = 1;  // accepted: copy wa4 -> fvec
                 }
                 int info = 0;
                 if (fabs(actred) <= 1e-8 && prered <= 1e-8 && 0.5 * ratio <= 1.0) info = 1;
@@ -975,9 +1069,6 @@ __global__ void __launch_bounds__(NL_THREADS) k_nonlinear_pnp(const double *__re
                 S.info = info;
                 S.ratio = ratio;
             }
-            __syncthreads();
-            if (S.flag)
-                for (int64_t i = t; i < m; i += NL_THREADS) fvec[i] = wa4[i];
             __syncthreads();
             if (S.info != 0 || S.ratio >= 1e-4) break;
         }
@@ -1109,8 +1200,9 @@ extern "C" int sfm_nonlinear_pnp(const double *X, const double *x, int64_t N, co
     if (!c) return SFM_ERR_HIP;
     int rc;
     const size_t m = (size_t)2 * N;
+    (void)m;
     if ((rc = c->buf[0].reserve((size_t)N * 24)) || (rc = c->buf[1].reserve((size_t)N * 16)) ||
-        (rc = c->buf[2].reserve(32 * sizeof(double))) || (rc = c->buf[3].reserve(9 * m * sizeof(double))))
+        (rc = c->buf[2].reserve(32 * sizeof(double))))
         return rc;
     Cam3 cam;
     load_cam(K, cam);
@@ -1124,9 +1216,8 @@ extern "C" int sfm_nonlinear_pnp(const double *X, const double *x, int64_t N, co
     SFM_HIP(hipMemcpyAsync(c->buf[1].p, x, (size_t)N * 16, hipMemcpyHostToDevice, s));
     SFM_HIP(hipMemcpyAsync(dIn, hin, sizeof hin, hipMemcpyHostToDevice, s));
     SFM_HIP(hipEventRecord(c->ev[1], s));
-    hipLaunchKernelGGL(k_nonlinear_pnp, dim3(1), dim3(NL_THREADS), 0, s, c->buf[0].as<double>(),
-                       c->buf[1].as<double2>(), (int64_t)N, cam, dIn, dIn + 3, max_nfev, c->buf[3].as<double>(),
-                       dIn + 16);
+    hipLaunchKernelGGL(k_nonlinear_pnp, dim3(1), dim3(NL2_THREADS), 0, s, c->buf[0].as<double>(),
+                       c->buf[1].as<double2>(), (int64_t)N, cam, dIn, dIn + 3, max_nfev, dIn + 16);
     SFM_HIP(hipGetLastError());
     SFM_HIP(hipEventRecord(c->ev[2], s));
     double out[13];
