@@ -146,26 +146,85 @@ __device__ __forceinline__ Hartley hartley8(const double (&x)[8], const double (
 // Rank-2 projection (EstimateFundamentalMatrix.py:70-72), denormalisation
 // F = T2^T F T1 (:75, as shipped) and F / F[2,2] (:78).
 // f: normalised null vector, row-major 3x3.
+// Unit right singular vector of F (3x3, row-major) for its smallest singular
+// value: the eigenvector of A = F^T F for its smallest eigenvalue, from the
+// closed-form (trigonometric) eigenvalue and the largest cross product of
+// two rows of A - lambda I.  Its error is ~eps * lambda_1 / (lambda_2 -
+// lambda_3), i.e. ~eps unless F is nearly rank 1 (false: use Jacobi).
+__device__ __forceinline__ bool smallest_right_sv(const double (&f)[9], double (&v)[3]) {
+    double a[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) a[i][j] = f[i] * f[j] + f[3 + i] * f[3 + j] + f[6 + i] * f[6 + j];
+    const double p1 = a[0][1] * a[0][1] + a[0][2] * a[0][2] + a[1][2] * a[1][2];
+    const double q = (a[0][0] + a[1][1] + a[2][2]) / 3.0;
+    const double b0 = a[0][0] - q, b1 = a[1][1] - q, b2 = a[2][2] - q;
+    const double p2 = b0 * b0 + b1 * b1 + b2 * b2 + 2.0 * p1;
+    if (!(p2 > 0.0)) return false;
+    const double pp = sqrt(p2 / 6.0), ip = 1.0 / pp;
+    const double B00 = b0 * ip, B11 = b1 * ip, B22 = b2 * ip;
+    const double B01 = a[0][1] * ip, B02 = a[0][2] * ip, B12 = a[1][2] * ip;
+    double r = 0.5 * (B00 * (B11 * B22 - B12 * B12) - B01 * (B01 * B22 - B12 * B02) + B02 * (B01 * B12 - B11 * B02));
+    r = fmin(1.0, fmax(-1.0, r));
+    const double phi = acos(r) / 3.0;
+    const double lam = q + 2.0 * pp * cos(phi + 2.0943951023931957);  // the smallest eigenvalue
+    const double m[3][3] = {{a[0][0] - lam, a[0][1], a[0][2]},
+                            {a[0][1], a[1][1] - lam, a[1][2]},
+                            {a[0][2], a[1][2], a[2][2] - lam}};
+    double c[3][3];  // cross products of row pairs (0,1), (0,2), (1,2)
+    const int pr[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+    double best = -1.0;
+    int bi = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double *u = m[pr[k][0]], *w = m[pr[k][1]];
+        c[k][0] = u[1] * w[2] - u[2] * w[1];
+        c[k][1] = u[2] * w[0] - u[0] * w[2];
+        c[k][2] = u[0] * w[1] - u[1] * w[0];
+        const double n = c[k][0] * c[k][0] + c[k][1] * c[k][1] + c[k][2] * c[k][2];
+        if (n > best) { best = n; bi = k; }
+    }
+    // nearly rank 1 (two eigenvalues meet the smallest): leave it to Jacobi
+    if (!(best > 1e-20 * p2 * p2)) return false;
+    const double in = 1.0 / sqrt(best);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) v[i] = (bi == 0 ? c[0][i] : bi == 1 ? c[1][i] : c[2][i]) * in;
+    return true;
+}
+
 __device__ __forceinline__ void f8_finish(const double (&f)[9], const Hartley &h1, const Hartley &h2,
                                           double *F_out) {
-    double b[3][3], W[3][3];  // b[col][row]
-#pragma unroll
-    for (int c = 0; c < 3; ++c)
-#pragma unroll
-        for (int r = 0; r < 3; ++r) b[c][r] = f[r * 3 + c];
-    jacobi_onesided<3, 3, 24>(b, W);
-    const int z = weakest_column<3, 3>(b);
+    // rank 2 (EstimateFundamentalMatrix.py:70-72): U diag(s1, s2, 0) V^T =
+    // F - (F v3) v3^T with v3 the smallest right singular vector
     double F2[3][3];
+    double v3[3];
+    if (smallest_right_sv(f, v3)) {
 #pragma unroll
-    for (int r = 0; r < 3; ++r)
+        for (int r = 0; r < 3; ++r) {
+            const double fv = f[r * 3] * v3[0] + f[r * 3 + 1] * v3[1] + f[r * 3 + 2] * v3[2];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            double acc = 0;
-#pragma unroll
-            for (int k = 0; k < 3; ++k)
-                if (k != z) acc += b[k][r] * W[c][k];
-            F2[r][c] = acc;
+            for (int c = 0; c < 3; ++c) F2[r][c] = f[r * 3 + c] - fv * v3[c];
         }
+    } else {
+        double b[3][3], W[3][3];  // b[col][row]
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int r = 0; r < 3; ++r) b[c][r] = f[r * 3 + c];
+        jacobi_onesided<3, 3, 24>(b, W);
+        const int z = weakest_column<3, 3>(b);
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                double acc = 0;
+#pragma unroll
+                for (int k = 0; k < 3; ++k)
+                    if (k != z) acc += b[k][r] * W[c][k];
+                F2[r][c] = acc;
+            }
+    }
     // T = [[s,0,ox],[0,s,oy],[0,0,1]] ; G = T2^T F2 T1
     const double T1[3][3] = {{h1.s, 0, h1.ox}, {0, h1.s, h1.oy}, {0, 0, 1}};
     const double T2[3][3] = {{h2.s, 0, h2.ox}, {0, h2.s, h2.oy}, {0, 0, 1}};

@@ -33,3 +33,19 @@ for _ in range(200):
     v, st, g = core._mt_state()
     core._mt_restore(v, st, g)
 print("mt state round trip ms %.4f" % ((time.perf_counter() - t) / 200 * 1e3))
+# kernel split of the given-table path (upload, kernels, download, score, fit, select)
+random.seed(0)
+tbl = core.sample_table(len(x1), 8, H)
+for _ in range(3):
+    core.ransac_f8(x1, x2, tbl, 0.06)
+tm = []
+for _ in range(20):
+    core.ransac_f8(x1, x2, tbl, 0.06)
+    tm.append(core.last_timings())
+print("table path ms (up, kernels, down, score, fit, select)", np.round(np.median(np.array(tm), axis=0), 4).tolist())
+for h in (512, 2048, 4096):
+    t4 = []
+    for _ in range(10):
+        core.ransac_f8(x1, x2, tbl[:h], 0.06)
+        t4.append(core.last_timings()[4])
+    print("fit ms at H=%d: %.4f" % (h, np.median(t4)))
