@@ -246,8 +246,9 @@ def next_rows(core, local_rank, cpu):
 
 def ransac_leg(args, world, rank, local_rank, comm):
     """RANSAC on config 2 (5000 correspondences, 40 % outliers, H = 16384).
-    N = 1: the drop-in's whole call (in-call sampling from the global random
-    stream, upload, kernels, mask download).  N > 1: hypothesis-sharded
+    Without a communicator: the drop-in's whole call (in-call sampling from
+    the global random stream, upload, kernels, mask download).  With one
+    (N > 1, or --force-comm): hypothesis-sharded
     (SURVEY §8(e)): every rank draws the whole table, fits and scores its
     contiguous range, the keys are combined over RCCL and the winner's F
     gives the mask; value = H / (max over ranks of the sharded call)."""
@@ -258,7 +259,7 @@ def ransac_leg(args, world, rank, local_rank, comm):
     samples = core.sample_table(5000, 8, H)
     reps = 20
     out = {"workload": "cfg2: 5000 corr, 40% outliers", "hypotheses": H}
-    if world == 1:
+    if comm is None:
         for _ in range(3):
             core.ransac_f8(x1, x2, samples, 0.06, device=local_rank)
         for _ in range(3):
@@ -282,14 +283,16 @@ def ransac_leg(args, world, rank, local_rank, comm):
                 lambda M: core.ransac_mask(x1, x2, M, 0.06, device=local_rank))
         for _ in range(3):
             one()
-        torch.distributed.barrier()
+        if world > 1:
+            torch.distributed.barrier()
         t = time.perf_counter()
         for _ in range(reps):
             best, F, mask = one()
         t_e2e = (time.perf_counter() - t) / reps
-        t_t = torch.tensor([t_e2e], dtype=torch.float64)
-        torch.distributed.all_reduce(t_t, op=torch.distributed.ReduceOp.MAX)
-        t_e2e = float(t_t.item())
+        if world > 1:
+            t_t = torch.tensor([t_e2e], dtype=torch.float64)
+            torch.distributed.all_reduce(t_t, op=torch.distributed.ReduceOp.MAX)
+            t_e2e = float(t_t.item())
         out["sharding"] = f"hypotheses [{h0}, {h1}) on rank {rank} of {world}; packed-key max all-reduce (RCCL)"
     kt = []
     for _ in range(reps):

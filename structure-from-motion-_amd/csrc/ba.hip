@@ -70,6 +70,8 @@ struct sfm_comm {
     ncclComm_t comm = nullptr;   // RCCL (one process per GPU)
     LocalGroup *local = nullptr; // or an in-process group
     int nranks = 1, rank = 0, device = 0;
+    void *scratch = nullptr;     // sfm_ransac_combine's device words (RCCL)
+    hipStream_t stream = nullptr;
 };
 
 namespace sfm {
@@ -1879,6 +1881,8 @@ extern "C" int sfm_comm_init_local(int nranks, sfm_comm **out) {
 
 extern "C" int sfm_comm_destroy(sfm_comm *c) {
     if (!c) return 0;
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->scratch) (void)hipFree(c->scratch);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->local) {
         bool last;
@@ -2112,8 +2116,8 @@ static int local_allreduce(sfm_ba_problem *p, double *buf, int64_t n) {
 // iteration is in the low word), so exactly one rank contributes.
 extern "C" int sfm_ransac_combine(sfm_comm *c, uint64_t *key, double *model) {
     SFM_CHECK_ARG(c && key && model, "null pointer");
-    if (c->nranks == 1) return 0;
     if (c->local) {
+        if (c->nranks == 1) return 0;
         LocalGroup *g = c->local;
         std::unique_lock<std::mutex> lk(g->mu);
         if (g->aborted) { set_error("in-process group aborted"); return SFM_ERR_COMM; }
@@ -2154,11 +2158,16 @@ extern "C" int sfm_ransac_combine(sfm_comm *c, uint64_t *key, double *model) {
         }
         return 0;
     }
+    // RCCL: also with a single rank (in-place no-ops), so one-GPU runs
+    // exercise the transport.  Device scratch [key (u64) | model (9 f64)]
+    // and a stream are kept on the communicator.
     SFM_HIP(hipSetDevice(c->device));
-    // device scratch: [key (u64) | model (9 f64)]
-    void *d = nullptr;
-    SFM_HIP(hipMalloc(&d, 80));
-    hipStream_t s = nullptr;
+    if (!c->scratch) {
+        SFM_HIP(hipMalloc(&c->scratch, 80));
+        SFM_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    }
+    void *d = c->scratch;
+    hipStream_t s = c->stream;
     int rc = 0;
     uint64_t gkey = 0;
     double m[9];
@@ -2166,8 +2175,7 @@ extern "C" int sfm_ransac_combine(sfm_comm *c, uint64_t *key, double *model) {
         set_error("%s: %s", what, ncclGetErrorString(r));
         rc = SFM_ERR_COMM;
     };
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) rc = SFM_ERR_HIP;
-    if (!rc && hipMemcpyAsync(d, key, 8, hipMemcpyHostToDevice, s) != hipSuccess) rc = SFM_ERR_HIP;
+    if (hipMemcpyAsync(d, key, 8, hipMemcpyHostToDevice, s) != hipSuccess) rc = SFM_ERR_HIP;
     ncclResult_t r;
     if (!rc && (r = ncclAllReduce(d, d, 1, ncclUint64, ncclMax, c->comm, s)) != ncclSuccess) fail(r, "ncclAllReduce(max)");
     if (!rc && (hipMemcpyAsync(&gkey, d, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess))
@@ -2183,8 +2191,6 @@ extern "C" int sfm_ransac_combine(sfm_comm *c, uint64_t *key, double *model) {
         if (!rc) std::memcpy(model, m, 72);
     }
     if (!rc) *key = gkey;
-    if (s) (void)hipStreamDestroy(s);
-    (void)hipFree(d);
     if (rc == SFM_ERR_HIP) set_error("sfm_ransac_combine: HIP call failed");
     return rc;
 }

@@ -809,3 +809,27 @@ def test_ba_gradient_tolerance_stop(core, gtol):
         assert np.array_equal(x1, p["X0"]) and rg["cost"] == rg["cost0"]
     with pytest.raises(Exception):
         core.ba_lm(*args, max_iterations=5, gradient_tolerance=-1.0)
+
+
+def test_ransac_combine_through_rccl_communicator(core):
+    """sfm_ransac_combine's RCCL path (all-reduce(max, u64) of the key, then
+    the winner's model as a sum) with a one-rank communicator: the shard's
+    key and model come back unchanged, repeatedly (cached scratch)."""
+    import sfm_dist
+    x1, x2, _, _ = syn.two_view(n=2000, seed=9)
+    random.seed(5)
+    key, F, _ = core.ransac_f8_range(x1, x2, 700, 0, 700, 0.06)
+    assert key != 0
+    comm = core.Comm(core.Comm.unique_id(), 1, 0)
+    try:
+        for _ in range(3):
+            k2, F2 = core.ransac_combine(comm, key, F)
+            assert k2 == key and np.array_equal(F2, F)
+        k0, _ = core.ransac_combine(comm, 0, np.zeros(9))
+        assert k0 == 0
+    finally:
+        comm.close()
+    random.seed(5)
+    b, Fb, mask, _, _ = core.ransac_f8_pyrandom(x1, x2, 700, 0.06)
+    assert sfm_dist.key_iter(key)[1] == b and np.array_equal(F, Fb)
+    assert np.array_equal(core.ransac_mask(x1, x2, F, 0.06), mask)
