@@ -380,7 +380,14 @@ def main():
     torch.cuda.synchronize()
     barrier()
     dt = allmax(time.perf_counter() - t0)
+    # per-phase times from a second, separate run of the same K iterations with
+    # HIP events on (each event record costs the stream a few us, so the timed
+    # run above has none)
+    ba.reset()
+    ba.set_timing(True)
+    ba.solve(max_iterations=args.steps, fixed_iterations=True)
     ktimes = ba.kernel_times()
+    ba.set_timing(False)
     ba.close()
 
     # ---------------- RANSAC (config 2)

@@ -257,8 +257,12 @@ int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *opts, sfm_ba_report *repo
 /* reset the device state to the initial parameters given at create time */
 int sfm_ba_reset(sfm_ba_problem *p);
 int sfm_ba_download(sfm_ba_problem *p, double *cam_params, double *points);
+/* per-phase HIP events in the following solves (off by default: each event
+ * record costs the stream a few microseconds) */
+int sfm_ba_set_timing(sfm_ba_problem *p, int on);
 /* average device time per LM iteration of each kernel family over the
- * last solve (ms): names are written ';'-separated into `names`. */
+ * last solve with timing on (ms; zeros otherwise): names are written
+ * ';'-separated into `names`. */
 int sfm_ba_kernel_times(sfm_ba_problem *p, double *ms, int n, char *names, int names_len);
 /* Diagnostic: x = S^-1 rhs for an SPD n x n S (row-major) with the reduced
  * camera system solver of sfm_ba_solve (the scipy 'lm' reference solves the

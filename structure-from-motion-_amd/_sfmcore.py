@@ -101,6 +101,7 @@ SIGNATURES = [
     ("sfm_ba_reset", _c, [ctypes.c_void_p]),
     ("sfm_ba_download", _c, [ctypes.c_void_p, _d, _d]),
     ("sfm_ba_kernel_times", _c, [ctypes.c_void_p, _d, _c, ctypes.c_char_p, _c]),
+    ("sfm_ba_set_timing", _c, [ctypes.c_void_p, _c]),
     ("sfm_ba_destroy", _c, [ctypes.c_void_p]),
     ("sfm_ba_lm_multi", _c, [ctypes.c_int32, _i, _i, _i32, _i32, _d, _d, _d, _d, ctypes.POINTER(BAOpts),
                              ctypes.POINTER(BAReport), ctypes.POINTER(ctypes.c_int), _c]),
@@ -555,6 +556,10 @@ class BAProblem:
         pts = np.zeros((self.n_pts, 3))
         _check(_lib.sfm_ba_download(self.h, _p(cams), _p(pts)))
         return cams, pts
+
+    def set_timing(self, on=True):
+        """Per-phase HIP events in the following solves (kernel_times)."""
+        _check(_lib.sfm_ba_set_timing(self.h, int(bool(on))))
 
     def kernel_times(self):
         ms = np.zeros(16)

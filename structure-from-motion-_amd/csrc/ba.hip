@@ -1240,6 +1240,16 @@ struct LMState {
     int run_lin, run_step, accept_now, pad;
 };
 
+// The host's view of the LM state: k_lm_step of iteration it publishes its
+// decision to pinned host memory (slot it % kHostRing, seq = it + 1 written
+// last, system scope), so the host can stop enqueuing iterations once the
+// solve is done without draining the stream (sfm_ba_solve).
+struct HostLM {
+    LMState st;
+    int seq, pad[3];
+};
+constexpr int kHostRing = 4;
+
 __global__ void k_lm_reset(LMState *lm, double lambda0, int *bad) {
     lm->lambda = lambda0; lm->nu = 2.0; lm->cost = 0.0; lm->cost0 = 0.0;
     lm->status = 4; lm->accepted = 0; lm->iters = 0; lm->done = 0;
@@ -1337,11 +1347,16 @@ __global__ void k_lm_step(const LMState *__restrict__ lm_in, LMState *__restrict
                           const double *__restrict__ h, const int *__restrict__ bad_in, int *__restrict__ bad_next,
                           int max_iterations, int fixed, double ftol, double ptol, double lambda0, int64_t np_,
                           int32_t nc, double *__restrict__ X, const double *__restrict__ X2, double *__restrict__ Rt,
-                          const double *__restrict__ Rt2) {
+                          const double *__restrict__ Rt2, HostLM *__restrict__ ring, int seq) {
     const LMState lm = lm_decide(*lm_in, h, *bad_in, max_iterations, fixed, ftol, ptol, lambda0);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         *lm_out = lm;
         *bad_next = 0;
+        if (ring) {  // publish to the host: the state, then (system-scope release) its sequence number
+            HostLM *r = ring + (seq - 1) % kHostRing;
+            r->st = lm;
+            __hip_atomic_store(&r->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     if (!lm.accept_now) return;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1788,7 +1803,8 @@ struct sfm_ba_problem {
     unsigned *d_nbig = nullptr;   // gradient_tolerance: point-gradient entries >= gtol
     double *d_gbuf = nullptr;     // gradient_tolerance: [count, g_c (6 nc)]
     double gtol = 0.0;            // this solve's gradient_tolerance (k_linearize counts when > 0)
-    double *h_scal = nullptr;  // pinned
+    HostLM *h_ring = nullptr, *d_ring = nullptr;  // pinned host ring of published LM states (+ device alias)
+    bool timing = false;                         // per-phase HIP events (sfm_ba_set_timing)
     int64_t payload_len = 0;
     int pt_blocks = 0;
     hipEvent_t ev[2 * T_NT] = {};
@@ -1800,7 +1816,7 @@ struct sfm_ba_problem {
     ~sfm_ba_problem() {
         (void)hipSetDevice(device);
         for (void *p : allocs) (void)hipFree(p);
-        if (h_scal) (void)hipHostFree(h_scal);
+        if (h_ring) (void)hipHostFree(h_ring);
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
         for (auto &e : ev_it)
@@ -2000,7 +2016,9 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = p->alloc(p->d_bad, 4)) || (rc = p->alloc(p->d_count, 3 * GS_WORDS)) ||
         (rc = p->alloc(p->d_nbig, 1)) || (rc = p->alloc(p->d_gbuf, 6 * (int64_t)nc + 1)))
         return rc;
-    SFM_HIP(hipHostMalloc((void **)&p->h_scal, 16 * sizeof(double)));
+    SFM_HIP(hipHostMalloc((void **)&p->h_ring, kHostRing * sizeof(HostLM), hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset((void *)p->h_ring, 0, kHostRing * sizeof(HostLM));
+    SFM_HIP(hipHostGetDevicePointer((void **)&p->d_ring, p->h_ring, 0));
     hipStream_t s = p->stream;
     if (no) {
         SFM_HIP(hipMemcpyAsync(p->d_cam, cam, no * 4, hipMemcpyHostToDevice, s));
@@ -2285,6 +2303,34 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     return 0;
 }
 
+// Wait until iteration j's k_lm_step has published its LM state to the
+// pinned ring.  A stream that stopped with an error, or drained without the
+// state arriving, ends the wait with an error instead of spinning forever.
+static int wait_lm_state(sfm_ba_problem *p, int j) {
+    const int *seq = &p->h_ring[j % kHostRing].seq;
+    for (unsigned spin = 1;; ++spin) {
+        if (__atomic_load_n(seq, __ATOMIC_ACQUIRE) == j + 1) return 0;
+        if (spin % 256 == 0) {
+            const hipError_t q = hipStreamQuery(p->stream);
+            if (q == hipErrorNotReady) {
+                std::this_thread::yield();
+                continue;
+            }
+            if (__atomic_load_n(seq, __ATOMIC_ACQUIRE) == j + 1) return 0;
+            set_error("LM iteration %d: state not published (%s)", j, hipGetErrorString(q));
+            return SFM_ERR_HIP;
+        }
+    }
+}
+
+// Per-phase HIP events in sfm_ba_solve (sfm_ba_kernel_times); off by default
+// (each event record costs the stream a few microseconds).
+extern "C" int sfm_ba_set_timing(sfm_ba_problem *p, int on) {
+    SFM_CHECK_ARG(p, "null pointer");
+    p->timing = on != 0;
+    return 0;
+}
+
 extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_report *rep) {
     SFM_CHECK_ARG(p && o, "null pointer");
     SFM_CHECK_ARG(o->max_iterations >= 0, "max_iterations < 0");
@@ -2297,22 +2343,40 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
     p->t_iters = 0;
     hipStream_t s = p->stream;
     int rc;
-    // iterations enqueued between two reads of the device LM state
-    int batch = 8;
-    if (const char *e = std::getenv("SFM_LM_BATCH")) batch = std::atoi(e);
-    batch = std::min(std::max(batch, 1), kEvSlots);
+    // The host enqueues iteration it once it has read the published state of
+    // iteration it - depth (pinned ring, no stream sync), so at most depth
+    // gated-off iterations follow the one that ends the solve, and the device
+    // always has the next iteration queued.
+    int depth = 2;
+    if (const char *e = std::getenv("SFM_LM_DEPTH")) depth = std::atoi(e);
+    depth = std::min(std::max(depth, 1), kHostRing - 1);
+    const bool timed = p->timing;
+    for (int k = 0; k < kHostRing; ++k) __atomic_store_n(&p->h_ring[k].seq, 0, __ATOMIC_RELAXED);
     hipLaunchKernelGGL(k_lm_reset, dim3(1), dim3(1), 0, s, p->d_lm, o->initial_lambda, p->d_bad);
     SFM_HIP(hipGetLastError());
-    LMState h{};
-    h.lambda = o->initial_lambda;
-    h.status = 4;
+    auto account = [&](int j) {  // per-phase event times of iteration j (complete once its state is published)
+        const hipEvent_t *e = p->ev_it + (size_t)(j % kEvSlots) * 2 * T_NT;
+        for (int k = 0; k < T_NT; ++k) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, e[2 * k], e[2 * k + 1]) == hipSuccess) p->t_acc[k] += ms;
+        }
+        p->t_iters++;
+    };
     const int64_t nacc = std::max<int64_t>(3 * p->np, 12 * (int64_t)p->nc);
-    for (int it = 0; it < o->max_iterations; ++it) {
-        hipEvent_t *ev = p->ev_it + (size_t)(it % batch) * 2 * T_NT;
-        SFM_HIP(hipEventRecord(ev[2 * T_LIN], s));
+    int it = 0;
+    for (; it < o->max_iterations; ++it) {
+        if (it >= depth) {
+            const int j = it - depth;
+            if ((rc = wait_lm_state(p, j))) return rc;
+            const LMState &st = p->h_ring[j % kHostRing].st;
+            if (timed && st.iters == j + 1) account(j);
+            if (st.done) break;
+        }
+        hipEvent_t *ev = timed ? p->ev_it + (size_t)(it % kEvSlots) * 2 * T_NT : nullptr;
+        if (timed) SFM_HIP(hipEventRecord(ev[2 * T_LIN], s));
         const int par = it & 1;  // the state of iteration it lives in d_lm[par]
         if ((rc = run_linearize(p, par, it == 0))) return rc;
-        SFM_HIP(hipEventRecord(ev[2 * T_LIN + 1], s));
+        if (timed) SFM_HIP(hipEventRecord(ev[2 * T_LIN + 1], s));
         if (it == 0) {
             hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(1), 0, s, p->d_lm, p->d_scal + 8);
             SFM_HIP(hipGetLastError());
@@ -2330,22 +2394,16 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
         hipLaunchKernelGGL(k_lm_step, dim3(ceil_div(nacc, 256)), dim3(256), 0, s, p->d_lm + par, p->d_lm + (par ^ 1),
                            p->d_scal, p->d_bad + par, p->d_bad + (par ^ 1), o->max_iterations, o->fixed_iterations,
                            o->function_tolerance, o->parameter_tolerance, o->initial_lambda, p->np, p->nc, p->d_X,
-                           p->d_X2, p->d_Rt, p->d_Rt2);
+                           p->d_X2, p->d_Rt, p->d_Rt2, p->d_ring, it + 1);
         SFM_HIP(hipGetLastError());
-        if ((it + 1) % batch == 0 || it + 1 == o->max_iterations) {
-            SFM_HIP(hipMemcpyAsync(&h, p->d_lm + ((it + 1) & 1), sizeof h, hipMemcpyDeviceToHost, s));
-            SFM_HIP(hipStreamSynchronize(s));
-            for (int j = it - it % batch; j <= it && j < h.iters; ++j) {  // iterations that ran
-                hipEvent_t *e = p->ev_it + (size_t)(j % batch) * 2 * T_NT;
-                for (int k = 0; k < T_NT; ++k) {
-                    float ms = 0;
-                    if (hipEventElapsedTime(&ms, e[2 * k], e[2 * k + 1]) == hipSuccess) p->t_acc[k] += ms;
-                }
-                p->t_iters++;
-            }
-            if (h.done) break;
-        }
     }
+    // the iterations still in flight (gated off if the solve ended earlier)
+    LMState h{};
+    SFM_HIP(hipMemcpyAsync(&h, p->d_lm + (it & 1), sizeof h, hipMemcpyDeviceToHost, s));
+    SFM_HIP(hipStreamSynchronize(s));
+    if (timed)
+        for (int j = std::max(0, it - depth); j < it && j < h.iters; ++j)
+            if (p->h_ring[j % kHostRing].st.iters == j + 1) account(j);
     const auto t1 = std::chrono::steady_clock::now();
     if (rep) {
         rep->iterations = h.iters;

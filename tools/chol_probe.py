@@ -8,6 +8,7 @@ import numpy as np, _sfmcore as c, sfm_synthetic as syn
 p = syn.ba_problem_cfg(sys.argv[1] if len(sys.argv) > 1 else "cfg4", dense=False)
 cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
 prob = c.BAProblem(cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], syn.K_REF)
+prob.set_timing()
 prob.solve(max_iterations=3, fixed_iterations=True)
 prob.reset()
 rep = prob.solve(max_iterations=20, fixed_iterations=True)

@@ -12,6 +12,7 @@ for name in ("cfg3","cfg4","cfg5"):
     cams0=np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
     t=time.perf_counter()
     prob=c.BAProblem(cams0,p["X0"],p["cam_idx"],p["pt_idx"],p["obs"],syn.K_REF)
+    prob.set_timing()
     tc=time.perf_counter()-t
     rep=prob.solve(max_iterations=30)
     n=len(p["cam_idx"])

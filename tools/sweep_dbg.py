@@ -9,6 +9,7 @@ cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"]
 for dbg in (0, 1, 2, 3, 4, 5, 7):
     os.environ["SFM_SWEEP_DEBUG"] = str(dbg)
     prob = c.BAProblem(cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], syn.K_REF)
+    prob.set_timing()
     prob.solve(max_iterations=3, fixed_iterations=True)
     prob.reset()
     rep = prob.solve(max_iterations=10, fixed_iterations=True)

@@ -14,6 +14,7 @@ for name in ("cfg4", "cfg5"):
     p = syn.ba_problem_cfg(name, dense=False)
     cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
     prob = c.BAProblem(cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], syn.K_REF)
+    prob.set_timing()
     for g in [int(v) for v in os.environ.get("SWEEP", "1,2,4,8").split(",")]:
         os.environ["SFM_LINEARIZE_LANES"] = str(g)
         os.environ["SFM_BACKSUB_LANES"] = str(g)

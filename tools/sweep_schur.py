@@ -15,6 +15,7 @@ for name in cfgs:
             os.environ["SFM_SWEEP_RANGES"] = str(nr)
             os.environ["SFM_SWEEP_CHUNK"] = str(ch)
             prob = c.BAProblem(cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], syn.K_REF)
+            prob.set_timing()
             prob.solve(max_iterations=3, fixed_iterations=True)
             prob.reset()
             rep = prob.solve(max_iterations=10, fixed_iterations=True)
