@@ -473,6 +473,132 @@ struct BlockInfo {
     int32_t i, j, first_item, last_item;
 };
 
+// Camera blocks of the normal equations, once per linearisation: each item
+// (a run of one camera's camera-major observations) sums U = sum Jc^T Jc (21)
+// and g = sum Jc^T r (6).  A workgroup takes the items [wg_first[g],
+// wg_first[g+1]) in order.  direct (every camera is one item of its own
+// workgroup): the workgroup writes its camera's camlin row.  Otherwise the
+// items go write-through to slab2 and the workgroup that arrives last adds
+// every camera's items in order into camlin (deterministic).  Run as
+// k_camera_lin, or by extra workgroups of k_schur_sweep (the CUs the sweep
+// leaves idle), which then needs no launch of its own.
+struct CamLinArgs {
+    const PairItem *items;
+    const int32_t *wg_first;
+    const int32_t *cm_pt;
+    const double2 *cm_obs;
+    const double *X, *Rt;
+    Kmat Km;
+    double *slab2;
+    const BlockInfo *blocks;
+    int32_t nblocks, nwg, direct;
+    double *camlin;
+    unsigned *counter;
+    const int *glin;  // gate: run only after an accepted step (LM state run_lin)
+};
+
+template <int THREADS>
+__device__ __forceinline__ void camera_lin_wg(const CamLinArgs &a, int g, double (*red)[CAMLIN], int *last) {
+    constexpr int NW = THREADS / 64;
+    double K[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) K[i] = a.Km.k[i];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int itx = a.wg_first[g]; itx < a.wg_first[g + 1]; ++itx) {
+        const PairItem it = a.items[itx];
+        const double *Rc = a.Rt + 12 * it.blk;  // the item's camera
+        double acc[CAMLIN];
+#pragma unroll
+        for (int k = 0; k < CAMLIN; ++k) acc[k] = 0.0;
+        // camera-major copies of the point index and the observation (static):
+        // coalesced loads, one dependent gather (X); the next observation's
+        // loads are issued before this one's arithmetic
+        int32_t k = it.k0 + threadIdx.x;
+        double2 on = {0.0, 0.0};
+        double xn[3] = {0.0, 0.0, 0.0};
+        if (k < it.k1) {
+            const int64_t p = a.cm_pt[k];
+            on = a.cm_obs[k];
+            xn[0] = a.X[3 * p]; xn[1] = a.X[3 * p + 1]; xn[2] = a.X[3 * p + 2];
+        }
+        for (; k < it.k1; k += THREADS) {
+            const double2 ob = on;
+            const double xp[3] = {xn[0], xn[1], xn[2]};
+            if (k + THREADS < it.k1) {
+                const int64_t p = a.cm_pt[k + THREADS];
+                on = a.cm_obs[k + THREADS];
+                xn[0] = a.X[3 * p]; xn[1] = a.X[3 * p + 1]; xn[2] = a.X[3 * p + 2];
+            }
+            double rr[2], A[2][3], q[3], Jc[2][6];
+            obs_model(Rc, xp, K, ob, rr, A, q);
+            jc_of(A, q, Jc);
+            const double r0 = rr[0], r1 = rr[1];
+            double u6[6], v6[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) { u6[i] = Jc[0][i]; v6[i] = Jc[1][i]; }
+            int u = 0;
+#pragma unroll
+            for (int r = 0; r < 6; ++r) {
+#pragma unroll
+                for (int s2 = r; s2 < 6; ++s2) acc[u++] += u6[r] * u6[s2] + v6[r] * v6[s2];
+                acc[21 + r] += u6[r] * r0 + v6[r] * r1;
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < CAMLIN; ++e) {
+            const double v = wave_sum(acc[e]);
+            if (lane == 0) red[w][e] = v;
+        }
+        __syncthreads();
+        double tot = 0.0;
+        if (threadIdx.x < CAMLIN)
+#pragma unroll
+            for (int v = 0; v < NW; ++v) tot += red[v][threadIdx.x];
+        if (threadIdx.x < CAMLIN) {
+            if (a.direct)
+                a.camlin[CAMLIN * it.blk + threadIdx.x] = tot;
+            else
+                __hip_atomic_store(a.slab2 + (int64_t)CAMLIN * itx + threadIdx.x, tot, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();  // red is reused by the next item
+    }
+    if (a.direct) return;
+    // release as in grid_sum_last: sc1 atomic stores completed before the
+    // arrival (no buffer_wbl2 on every workgroup)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        *last = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)a.nwg - 1;
+    __syncthreads();
+    if (!*last) return;  // sc1 loads below stand in for the acquire, as in grid_sum_last
+    for (int e = threadIdx.x; e < a.nblocks * CAMLIN; e += THREADS) {
+        const BlockInfo bi = a.blocks[e / CAMLIN];
+        const int k = e % CAMLIN;
+        double v = 0;
+        for (int i0 = bi.first_item; i0 < bi.last_item; i0 += 8) {  // 8 sc1 loads in flight, summed in order
+            double v8[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                v8[u] = i0 + u < bi.last_item ? __hip_atomic_load(a.slab2 + (int64_t)CAMLIN * (i0 + u) + k,
+                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                              : 0.0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v += v8[u];
+        }
+        a.camlin[CAMLIN * bi.i + k] = v;
+    }
+    if (threadIdx.x == 0) *a.counter = 0u;
+}
+
+template <int THREADS>
+__global__ void __launch_bounds__(THREADS) k_camera_lin(CamLinArgs a) {
+    if (!*a.glin) return;  // device-side LM control: iteration gated off
+    __shared__ double red[THREADS / 64][CAMLIN];
+    __shared__ int last;
+    camera_lin_wg<THREADS>(a, blockIdx.x, red, &last);
+}
+
 // ---------------------------------------------------------------------
 // Reduced camera system S_ij = [i==j] U_i - sum_{p seen by i and j} Z_pi Z_pj^T
 // as a sweep over point ranges (the Schur record of an observation is
@@ -627,9 +753,17 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     const int32_t *__restrict__ spec_nload,
     const int32_t *__restrict__ spec_goff, const SweepGroup *__restrict__ groups, const int16_t *__restrict__ lanegrp,
     const int32_t *__restrict__ list, const uint32_t *__restrict__ pairs, const int32_t *__restrict__ hdr,
-    const double *__restrict__ Z, double *__restrict__ slab, const int *__restrict__ gate, int dbg) {
-    if (gate && !*gate) return;  // device-side LM control: iteration gated off
+    const double *__restrict__ Z, double *__restrict__ slab, const int *__restrict__ gate, int dbg, int nsweep,
+    CamLinArgs cl) {
     extern __shared__ double2 sw_lds[];
+    if ((int)blockIdx.x >= nsweep) {  // camera blocks of the normal equations on the CUs the sweep leaves idle
+        if (!*cl.glin) return;
+        double(*red)[CAMLIN] = reinterpret_cast<double(*)[CAMLIN]>(sw_lds);
+        camera_lin_wg<SW_THREADS>(cl, (int)blockIdx.x - nsweep, red,
+                                  reinterpret_cast<int *>(sw_lds + SW_THREADS / 64 * CAMLIN / 2 + 1));
+        return;
+    }
+    if (gate && !*gate) return;  // device-side LM control: iteration gated off
     uint32_t *ldsw = reinterpret_cast<uint32_t *>(sw_lds);
     const int loc = blockIdx.x / NXCD;
     const int w = loc % nspec, r = (loc / nspec) * NXCD + (int)(blockIdx.x % NXCD);
@@ -735,86 +869,6 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
 #pragma unroll
             for (int k = 0; k < 3; ++k) out[36 + 3 * h + k] = acc[18 + k];
     }
-}
-
-// Camera blocks of the normal equations, once per linearisation: each item
-// sums U = sum Jc^T Jc (21) and g = sum Jc^T r (6) over a chunk of one
-// camera's observations (write-through to slab2); the item that arrives last
-// adds every camera's items in order into camlin (deterministic, one launch).
-__global__ void __launch_bounds__(256) k_camera_lin(const PairItem *__restrict__ items,
-                                                    const int32_t *__restrict__ cam_obs,
-                                                    const int32_t *__restrict__ pt, const double2 *__restrict__ obs,
-                                                    const double *__restrict__ X, const double *__restrict__ Rt,
-                                                    Kmat Km, double *__restrict__ slab2,
-                                                    const BlockInfo *__restrict__ blocks, int32_t nblocks,
-                                                    double *__restrict__ camlin, unsigned *__restrict__ counter,
-                                                    const int *__restrict__ gate) {
-    if (gate && !*gate) return;  // device-side LM control: iteration gated off
-    __shared__ double red[4][CAMLIN];
-    __shared__ int last;
-    const PairItem it = items[blockIdx.x];
-    double K[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) K[i] = Km.k[i];
-    const double *Rc = Rt + 12 * it.blk;  // the item's camera
-    double acc[CAMLIN];
-#pragma unroll
-    for (int k = 0; k < CAMLIN; ++k) acc[k] = 0.0;
-    for (int32_t k = it.k0 + threadIdx.x; k < it.k1; k += 256) {
-        const int32_t o = cam_obs[k];
-        const int64_t p = pt[o];
-        const double xp[3] = {X[3 * p], X[3 * p + 1], X[3 * p + 2]};
-        double rr[2], A[2][3], q[3], Jc[2][6];
-        obs_model(Rc, xp, K, obs[o], rr, A, q);
-        jc_of(A, q, Jc);
-        const double r0 = rr[0], r1 = rr[1];
-        double a[6], b[6];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) { a[i] = Jc[0][i]; b[i] = Jc[1][i]; }
-        int u = 0;
-#pragma unroll
-        for (int r = 0; r < 6; ++r) {
-#pragma unroll
-            for (int s2 = r; s2 < 6; ++s2) acc[u++] += a[r] * a[s2] + b[r] * b[s2];
-            acc[21 + r] += a[r] * r0 + b[r] * r1;
-        }
-    }
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < CAMLIN; ++k) {
-        const double v = wave_sum(acc[k]);
-        if (lane == 0) red[w][k] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x < CAMLIN)
-        __hip_atomic_store(slab2 + (int64_t)CAMLIN * blockIdx.x + threadIdx.x,
-                           red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x],
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // release as in grid_sum_last: sc1 atomic stores completed before the
-    // arrival (no buffer_wbl2 on every block)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-        last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;  // sc1 loads below stand in for the acquire, as in grid_sum_last
-    for (int e = threadIdx.x; e < nblocks * CAMLIN; e += 256) {
-        const BlockInfo bi = blocks[e / CAMLIN];
-        const int k = e % CAMLIN;
-        double v = 0;
-        for (int i0 = bi.first_item; i0 < bi.last_item; i0 += 8) {  // 8 sc1 loads in flight, summed in order
-            double v8[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                v8[u] = i0 + u < bi.last_item ? __hip_atomic_load(slab2 + (int64_t)CAMLIN * (i0 + u) + k,
-                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                              : 0.0;
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v += v8[u];
-        }
-        camlin[CAMLIN * bi.i + k] = v;
-    }
-    if (threadIdx.x == 0) *counter = 0u;
 }
 
 // one 64-thread workgroup per camera block (i <= j, dense upper-triangle
@@ -1571,6 +1625,39 @@ static int env_int(const char *name, int dflt) {
     return v ? std::atoi(v) : dflt;
 }
 
+// camera items for camera_lin_wg from workgroup cuts (camera-major
+// observation offsets, ascending, first 0, last n_obs): every item is the
+// part of one camera inside one workgroup's range.  by_wg: workgroup g takes
+// the items of range g (wg_first); otherwise one item per workgroup.
+struct CamPlan {
+    std::vector<PairItem> items;
+    std::vector<BlockInfo> blocks;
+    std::vector<int32_t> wg_first;
+};
+
+static void plan_camera_items(int nc, const std::vector<int32_t> &cstart, const std::vector<int32_t> &cuts, bool by_wg,
+                              CamPlan &P) {
+    std::vector<std::vector<int32_t>> cam_items(nc);
+    P.wg_first.push_back(0);
+    for (size_t g = 0; g + 1 < cuts.size(); ++g) {
+        const int32_t a = cuts[g], b = cuts[g + 1];
+        for (int c = 0; c < nc; ++c) {
+            const int32_t k0 = std::max(a, cstart[c]), k1 = std::min(b, cstart[c + 1]);
+            if (k0 >= k1) continue;
+            cam_items[c].push_back((int32_t)P.items.size());
+            P.items.push_back({c, k0, k1, 1});
+        }
+        if (by_wg) P.wg_first.push_back((int32_t)P.items.size());
+    }
+    if (!by_wg)
+        for (size_t i = 1; i <= P.items.size(); ++i) P.wg_first.push_back((int32_t)i);
+    // items are in camera-major order already (cuts ascend), so each camera's
+    // items are contiguous
+    for (int c = 0; c < nc; ++c)
+        if (!cam_items[c].empty())
+            P.blocks.push_back({c, c, cam_items[c].front(), cam_items[c].back() + 1});
+}
+
 static int32_t dense_blk(int nc, int i, int j) { return i * nc - i * (i - 1) / 2 + (j - i); }
 
 static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt,
@@ -1776,7 +1863,10 @@ struct sfm_ba_problem {
     sfm_comm *comm = nullptr;
     int32_t nc = 0, ns = 0, nsp = 0, nT = 0, tb = 16;
     int64_t np = 0, no = 0, npairs = 0;
-    int32_t ndiag_items = 0, ndiag_blocks = 0;
+    int32_t ndiag_items = 0, ndiag_blocks = 0;  // k_camera_lin items (one per workgroup) / cameras
+    int32_t cl_fused_wg = 0, cl_fused_items = 0;  // k_schur_sweep's camera workgroups / their items
+    bool cl_fused = false;                         // this solve: camera blocks inside the sweep launch
+    int sw_debug = 0;                              // SFM_SWEEP_DEBUG (read once per solve)
     // Schur sweep plan (k_schur_sweep): ranges, chunks, specs
     int32_t sw_nrange = 0, sw_nspec = 0, sw_nbd = 0, sw_nchunk = 0;
     SweepLds sw_L = {};
@@ -1784,9 +1874,11 @@ struct sfm_ba_problem {
     Kmat K;
     std::vector<double> cams0, pts0;
     // device
-    int32_t *d_cam = nullptr, *d_pt = nullptr, *d_pstart = nullptr, *d_cam_obs = nullptr, *d_cstart = nullptr;
-    PairItem *d_items = nullptr;
-    BlockInfo *d_blocks = nullptr;
+    int32_t *d_cam = nullptr, *d_pt = nullptr, *d_pstart = nullptr, *d_cm_pt = nullptr, *d_cstart = nullptr;
+    double2 *d_cm_obs = nullptr;  // camera-major observations (with d_cm_pt: k_camera_lin)
+    PairItem *d_items = nullptr, *d_fitems = nullptr;  // camera items: k_camera_lin / the sweep's camera workgroups
+    BlockInfo *d_blocks = nullptr, *d_fblocks = nullptr;
+    int32_t *d_wg_first = nullptr, *d_fwg_first = nullptr;
     double *d_slab = nullptr, *d_slab2 = nullptr, *d_camlin = nullptr;
     int32_t *d_sw_rchunk = nullptr, *d_sw_goff = nullptr, *d_sw_nload = nullptr, *d_sw_list = nullptr, *d_sw_hdr = nullptr;
     SweepGroup *d_sw_groups = nullptr;
@@ -1969,22 +2061,32 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
                 ++tot;
             }
     p->npairs = tot;
-    // camera items for k_camera_lin: chunks of each camera's observations
-    std::vector<BlockInfo> blocks;
-    std::vector<PairItem> items;
-    const int cam_chunk = std::max(64, env_int("SFM_CAM_CHUNK", CAM_CHUNK));
-    for (int c = 0; c < nc; ++c) {
-        BlockInfo bi;
-        bi.i = c; bi.j = c; bi.first_item = (int32_t)items.size();
-        for (int32_t k = cstart[c]; k < cstart[c + 1]; k += cam_chunk)
-            items.push_back({c, k, std::min<int32_t>(cstart[c + 1], k + cam_chunk), 1});
-        bi.last_item = (int32_t)items.size();
-        if (bi.last_item > bi.first_item) blocks.push_back(bi);
-    }
-    p->ndiag_items = (int32_t)items.size();
-    p->ndiag_blocks = (int32_t)blocks.size();
     SweepPlan sw;
     plan_sweep(nc, np_, no, cam, pt, pstart, cnt, sw);
+    // camera items (the camera blocks of the normal equations): for
+    // k_camera_lin, chunks of <= CAM_CHUNK of each camera's observations, one
+    // per workgroup; for the camera workgroups of k_schur_sweep, the
+    // camera-major list cut into equal contiguous ranges (one per workgroup:
+    // as many as the CUs the sweep leaves idle), each cut again at camera
+    // boundaries
+    const int cam_chunk = std::max(64, env_int("SFM_CAM_CHUNK", CAM_CHUNK));
+    const int busy = sw.nspec * sw.nrange, idle = (256 - busy % 256) % 256;
+    p->cl_fused_wg = (int32_t)std::min<int64_t>(std::max<int64_t>(1, ceil_div(no, SW_THREADS)),
+                                                env_int("SFM_CAMLIN_WG", idle >= 32 ? idle : 64));
+    CamPlan csa, cfu;
+    {
+        std::vector<int32_t> cuts;
+        for (int c = 0; c < nc; ++c)
+            for (int32_t k = cstart[c]; k < cstart[c + 1]; k += cam_chunk) cuts.push_back(k);
+        cuts.push_back((int32_t)no);
+        plan_camera_items(nc, cstart, cuts, false, csa);
+        cuts.clear();
+        for (int g = 0; g <= p->cl_fused_wg; ++g) cuts.push_back((int32_t)(no * g / p->cl_fused_wg));
+        plan_camera_items(nc, cstart, cuts, true, cfu);
+    }
+    p->ndiag_items = (int32_t)csa.items.size();
+    p->ndiag_blocks = (int32_t)csa.blocks.size();
+    p->cl_fused_items = (int32_t)cfu.items.size();
     p->sw_nrange = sw.nrange;
     p->sw_nspec = sw.nspec;
     p->sw_nbd = sw.nbd;
@@ -1995,8 +2097,11 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     p->payload_len = pay_vec_base(p->ns) + 3 * p->ns + 1;
     int rc;
     if ((rc = p->alloc(p->d_cam, no)) || (rc = p->alloc(p->d_pt, no)) || (rc = p->alloc(p->d_pstart, np_ + 1)) ||
-        (rc = p->alloc(p->d_obs, no)) || (rc = p->alloc(p->d_cam_obs, no)) || (rc = p->alloc(p->d_cstart, nc + 1)) ||
+        (rc = p->alloc(p->d_obs, no)) || (rc = p->alloc(p->d_cm_pt, no)) ||
+        (rc = p->alloc(p->d_cm_obs, no)) || (rc = p->alloc(p->d_cstart, nc + 1)) ||
         (rc = p->alloc(p->d_items, p->ndiag_items)) || (rc = p->alloc(p->d_blocks, p->ndiag_blocks)) ||
+        (rc = p->alloc(p->d_wg_first, csa.wg_first.size())) || (rc = p->alloc(p->d_fitems, cfu.items.size())) ||
+        (rc = p->alloc(p->d_fblocks, cfu.blocks.size())) || (rc = p->alloc(p->d_fwg_first, cfu.wg_first.size())) ||
         (rc = p->alloc(p->d_slab, (int64_t)ITEM_W * sw.nrange * sw.nbd)) ||
         (rc = p->alloc(p->d_sw_rchunk, sw.rchunk.size())) || (rc = p->alloc(p->d_sw_goff, sw.goff.size())) ||
         (rc = p->alloc(p->d_sw_nload, sw.nload.size())) ||
@@ -2004,7 +2109,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = p->alloc(p->d_sw_list, sw.list.size())) || (rc = p->alloc(p->d_sw_hdr, sw.hdr.size())) ||
         (rc = p->alloc(p->d_sw_pairs, sw.pairs.size())) || (rc = p->alloc(p->d_sw_blkij, sw.blkij.size())) ||
         (rc = p->alloc(p->d_camlin, (int64_t)CAMLIN * nc)) ||
-        (rc = p->alloc(p->d_slab2, (int64_t)CAMLIN * std::max<int64_t>(1, p->ndiag_items))) ||
+        (rc = p->alloc(p->d_slab2, (int64_t)CAMLIN * std::max<int64_t>(1, std::max(p->ndiag_items, p->cl_fused_items)))) ||
         (rc = p->alloc(p->d_Rt, 12 * (int64_t)nc)) || (rc = p->alloc(p->d_Rt2, 12 * (int64_t)nc)) ||
         (rc = p->alloc(p->d_X, 3 * np_)) || (rc = p->alloc(p->d_X2, 3 * np_)) ||
         (rc = p->alloc(p->d_Vg, 9 * np_)) || (rc = p->alloc(p->d_Lq, 9 * np_)) ||
@@ -2026,14 +2131,29 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         SFM_HIP(hipMemcpyAsync(p->d_obs, obs, no * 16, hipMemcpyHostToDevice, s));
     }
     SFM_HIP(hipMemcpyAsync(p->d_pstart, pstart.data(), pstart.size() * 4, hipMemcpyHostToDevice, s));
-    if (no) SFM_HIP(hipMemcpyAsync(p->d_cam_obs, cam_obs.data(), no * 4, hipMemcpyHostToDevice, s));
+    std::vector<int32_t> cm_pt(no);
+    std::vector<double> cm_obs(2 * (size_t)no);
+    for (int64_t k = 0; k < no; ++k) {
+        const int32_t o = cam_obs[k];
+        cm_pt[k] = pt[o];
+        cm_obs[2 * k] = obs[2 * (size_t)o];
+        cm_obs[2 * k + 1] = obs[2 * (size_t)o + 1];
+    }
+    if (no) {
+        SFM_HIP(hipMemcpyAsync(p->d_cm_pt, cm_pt.data(), no * 4, hipMemcpyHostToDevice, s));
+        SFM_HIP(hipMemcpyAsync(p->d_cm_obs, cm_obs.data(), no * 16, hipMemcpyHostToDevice, s));
+    }
     SFM_HIP(hipMemcpyAsync(p->d_cstart, cstart.data(), cstart.size() * 4, hipMemcpyHostToDevice, s));
     SFM_HIP(hipMemsetAsync(p->d_camlin, 0, (size_t)CAMLIN * nc * sizeof(double), s));
     SFM_HIP(hipMemsetAsync(p->d_count, 0, 3 * GS_WORDS * sizeof(unsigned), s));
     SFM_HIP(hipMemsetAsync(p->d_nbig, 0, sizeof(unsigned), s));
     if (p->ndiag_items) {
-        SFM_HIP(hipMemcpyAsync(p->d_items, items.data(), items.size() * sizeof(PairItem), hipMemcpyHostToDevice, s));
-        SFM_HIP(hipMemcpyAsync(p->d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), hipMemcpyHostToDevice, s));
+        SFM_HIP(hipMemcpyAsync(p->d_items, csa.items.data(), csa.items.size() * sizeof(PairItem), hipMemcpyHostToDevice, s));
+        SFM_HIP(hipMemcpyAsync(p->d_blocks, csa.blocks.data(), csa.blocks.size() * sizeof(BlockInfo), hipMemcpyHostToDevice, s));
+        SFM_HIP(hipMemcpyAsync(p->d_wg_first, csa.wg_first.data(), csa.wg_first.size() * 4, hipMemcpyHostToDevice, s));
+        SFM_HIP(hipMemcpyAsync(p->d_fitems, cfu.items.data(), cfu.items.size() * sizeof(PairItem), hipMemcpyHostToDevice, s));
+        SFM_HIP(hipMemcpyAsync(p->d_fblocks, cfu.blocks.data(), cfu.blocks.size() * sizeof(BlockInfo), hipMemcpyHostToDevice, s));
+        SFM_HIP(hipMemcpyAsync(p->d_fwg_first, cfu.wg_first.data(), cfu.wg_first.size() * 4, hipMemcpyHostToDevice, s));
     }
     auto up = [&](void *dst, const void *src, size_t bytes) -> int {
         if (bytes) SFM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
@@ -2226,6 +2346,28 @@ static int allreduce(sfm_ba_problem *p, double *buf, int64_t n) {
     return 0;
 }
 
+// camera_lin_wg's arguments: k_camera_lin's items (one per workgroup; direct
+// when every camera is a single item) or the sweep's camera workgroups
+static CamLinArgs camlin_args(const sfm_ba_problem *p, bool fused, const int *glin) {
+    CamLinArgs a;
+    a.items = fused ? p->d_fitems : p->d_items;
+    a.wg_first = fused ? p->d_fwg_first : p->d_wg_first;
+    a.cm_pt = p->d_cm_pt;
+    a.cm_obs = p->d_cm_obs;
+    a.X = p->d_X;
+    a.Rt = p->d_Rt;
+    a.Km = p->K;
+    a.slab2 = p->d_slab2;
+    a.blocks = fused ? p->d_fblocks : p->d_blocks;
+    a.nblocks = p->ndiag_blocks;
+    a.nwg = fused ? p->cl_fused_wg : p->ndiag_items;
+    a.direct = !fused && p->ndiag_items == p->ndiag_blocks;
+    a.camlin = p->d_camlin;
+    a.counter = p->d_count + 2 * GS_WORDS;
+    a.glin = glin;
+    return a;
+}
+
 // launches one linearisation (J, V, g) and, into d_scal[8], the cost.
 // want_cost: also sum the cost into d_scal[8] (the LM state takes it from
 // the first linearisation only; later costs come from the accepted trials)
@@ -2242,10 +2384,9 @@ static int run_linearize(sfm_ba_problem *p, int par, int want_cost) {
     switch (gl) { case 1: SFM_LIN(1); break; case 2: SFM_LIN(2); break; case 4: SFM_LIN(4); break; default: SFM_LIN(8); }
 #undef SFM_LIN
     SFM_HIP(hipGetLastError());
-    if (p->ndiag_items) {
-        hipLaunchKernelGGL(k_camera_lin, dim3(p->ndiag_items), dim3(256), 0, s, p->d_items, p->d_cam_obs, p->d_pt,
-                           p->d_obs, p->d_X, p->d_Rt, p->K,
-                           p->d_slab2, p->d_blocks, p->ndiag_blocks, p->d_camlin, p->d_count + 2 * GS_WORDS, glin);
+    if (p->ndiag_items && !p->cl_fused) {
+        const CamLinArgs cl = camlin_args(p, false, glin);
+        hipLaunchKernelGGL(k_camera_lin<256>, dim3(p->ndiag_items), dim3(256), 0, s, cl);
         SFM_HIP(hipGetLastError());
     }
     return want_cost ? allreduce(p, p->d_scal + 8, 1) : 0;
@@ -2267,10 +2408,13 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     SFM_HIP(hipGetLastError());
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_PREP + 1], s));
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SCHUR], s));
-    hipLaunchKernelGGL(k_schur_sweep, dim3(NXCD * p->sw_nspec * ceil_div(p->sw_nrange, NXCD)), dim3(SW_THREADS),
+    const int nsweep = NXCD * p->sw_nspec * ceil_div(p->sw_nrange, NXCD);
+    const bool fused = p->cl_fused && p->ndiag_items;  // + the camera blocks (after an accepted step)
+    hipLaunchKernelGGL(k_schur_sweep, dim3(nsweep + (fused ? p->cl_fused_wg : 0)), dim3(SW_THREADS),
                        p->sw_lds_bytes, s, p->sw_nspec, p->sw_nrange, p->sw_nbd, p->sw_L, p->d_sw_rchunk,
                        p->d_sw_nload, p->d_sw_goff, p->d_sw_groups, p->d_sw_lanegrp, p->d_sw_list,
-                       p->d_sw_pairs, p->d_sw_hdr, p->d_Z, p->d_slab, gst, env_int("SFM_SWEEP_DEBUG", 0));
+                       p->d_sw_pairs, p->d_sw_hdr, p->d_Z, p->d_slab, gst, p->sw_debug, nsweep,
+                       camlin_args(p, true, &p->d_lm[par].run_lin));
     SFM_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_schur_finish, dim3(p->sw_nbd), dim3(64), 0, s, p->ns, p->sw_nbd, p->sw_nrange,
                        p->d_sw_blkij, p->d_slab, p->d_camlin, p->d_payload, gst);
@@ -2337,6 +2481,10 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
     SFM_CHECK_ARG(o->gradient_tolerance >= 0.0, "gradient_tolerance < 0");
     SFM_HIP(hipSetDevice(p->device));
     p->gtol = o->gradient_tolerance;
+    // camera blocks inside the sweep launch, except when gradient_tolerance
+    // needs g_c right after the linearisation
+    p->cl_fused = o->gradient_tolerance == 0.0 && env_int("SFM_CAMLIN_FUSED", 1) != 0;
+    p->sw_debug = env_int("SFM_SWEEP_DEBUG", 0);
     (void)hipGetLastError();
     const auto t0 = std::chrono::steady_clock::now();
     for (double &t : p->t_acc) t = 0;
