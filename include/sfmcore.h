@@ -40,6 +40,9 @@ int sfm_device_count(void);
  * [0] host->device upload, [1] kernels, [2] device->host download,
  * [3] kernel-only time of the dominant kernel.  Returns the count written. */
 int sfm_last_timings(double *out, int n);
+/* device-side timings (HIP events) in the in-call-sampling and shard RANSAC
+ * calls; off by default (host sampling time is always reported) */
+int sfm_set_call_timing(int on);
 
 /* ---------------------------------------------------------------------
  * Python `random` replay (host code, no GPU).

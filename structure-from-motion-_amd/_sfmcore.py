@@ -60,6 +60,7 @@ SIGNATURES = [
     ("sfm_last_error", ctypes.c_char_p, []),
     ("sfm_device_count", _c, []),
     ("sfm_last_timings", _c, [_d, _c]),
+    ("sfm_set_call_timing", _c, [_c]),
     ("sfm_pyrandom_sample_table", _c, [_u32, _i, ctypes.c_int32, _i, _i32]),
     ("sfm_f8_batch", _c, [_d, _d, _i, _d, _c]),
     ("sfm_f8_general", _c, [_d, _d, _i, _d, _c]),
@@ -141,6 +142,11 @@ def _f64(a, shape=None):
     if shape is not None:
         a = a.reshape(shape)
     return a
+
+
+def set_call_timing(on=True):
+    """Device-side timings (HIP events) in the drop-in RANSAC calls."""
+    _check(_lib.sfm_set_call_timing(int(bool(on))))
 
 
 def last_timings():

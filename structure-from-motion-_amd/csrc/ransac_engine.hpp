@@ -41,6 +41,13 @@ struct EpiModel {
     __device__ static bool inlier_fast(const double *f, double2 p, double2 q, double thr, double lo, double hi) {
         return epi_inlier_fast(f, p.x, p.y, q.x, q.y, thr, lo, hi);
     }
+    using Part = EpiPart;
+    __device__ static Part fast(const double *f, double2 p, double2 q, double, double lo, double hi) {
+        return epi_fast(f, p.x, p.y, q.x, q.y, lo, hi);
+    }
+    __device__ static bool exact(const Part &r, double2, double2, const double *, double thr) {
+        return epi_exact(r, thr);
+    }
 };
 
 struct HomModel {
@@ -55,6 +62,13 @@ struct HomModel {
     __device__ static bool inlier_fast(const double *f, double2 p, double2 q, double thr, double, double) {
         return hom_inlier(f, p.x, p.y, q.x, q.y, thr);
     }
+    struct Part {
+        bool in, unsure;
+    };
+    __device__ static Part fast(const double *f, double2 p, double2 q, double thr, double, double) {
+        return {hom_inlier(f, p.x, p.y, q.x, q.y, thr), false};
+    }
+    __device__ static bool exact(const Part &r, double2, double2, const double *, double) { return r.in; }
 };
 
 template <class M>
@@ -72,6 +86,15 @@ __global__ void __launch_bounds__(256) k_fit_samples(const double2 *__restrict__
         ax[i] = p.x; ay[i] = p.y; bx[i] = q.x; by[i] = q.y;
     }
     M::fit(ax, ay, bx, by, out + 9 * h);
+}
+
+// fit H hypotheses whose sample rows are at rows (device-readable)
+template <class M>
+static int launch_fit(const double2 *d1, const double2 *d2, const int32_t *rows, int64_t H, double *dF,
+                      int32_t *counts, hipStream_t s) {
+    hipLaunchKernelGGL(k_fit_samples<M>, dim3(ceil_div(H, 64)), dim3(64), 0, s, d1, d2, rows, H, dF, counts);
+    SFM_HIP(hipGetLastError());
+    return 0;
 }
 
 // samples given as coordinates (H x K x 2 each): the batch fit entry points
@@ -109,8 +132,10 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES) k_ransac_score(const double2
         finite &= isfinite(f[k]) ? 1 : 0;
     }
     int cnt = 0;
-    const double thr_lo = thr >= 0 ? thr * (1.0 - 1e-4) : thr * (1.0 + 1e-4);
-    const double thr_hi = thr >= 0 ? thr * (1.0 + 1e-4) : thr * (1.0 - 1e-4);
+    // the fast decision's band around 2 thr (epi_inlier_fast compares the
+    // doubled mean)
+    const double thr_lo = 2.0 * (thr >= 0 ? thr * (1.0 - 1e-4) : thr * (1.0 + 1e-4));
+    const double thr_hi = 2.0 * (thr >= 0 ? thr * (1.0 + 1e-4) : thr * (1.0 - 1e-4));
     // gridDim.y > 1: this workgroup scores correspondences [y*slice, (y+1)*slice)
     const int64_t p0 = (int64_t)blockIdx.y * slice, p1 = min<int64_t>(N, p0 + slice);
     for (int64_t base = p0; base < p1; base += SCORE_TILE) {
@@ -127,8 +152,12 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES) k_ransac_score(const double2
             for (; j + 128 <= n; j += 128) {
                 const double2 p0 = s1[j + lane], q0 = s2[j + lane];
                 const double2 p1 = s1[j + 64 + lane], q1 = s2[j + 64 + lane];
-                const bool in0 = M::inlier_fast(f, p0, q0, thr, thr_lo, thr_hi);
-                const bool in1 = M::inlier_fast(f, p1, q1, thr, thr_lo, thr_hi);
+                // both fast decisions before either branch to the exact tail
+                const typename M::Part r0 = M::fast(f, p0, q0, thr, thr_lo, thr_hi);
+                const typename M::Part r1 = M::fast(f, p1, q1, thr, thr_lo, thr_hi);
+                bool in0 = r0.in, in1 = r1.in;
+                if (r0.unsure) in0 = M::exact(r0, p0, q0, f, thr);
+                if (r1.unsure) in1 = M::exact(r1, p1, q1, f, thr);
                 cnt += __popcll(__ballot(in0)) + __popcll(__ballot(in1));
             }
             for (; j < n; j += 64) {
@@ -257,9 +286,7 @@ int ransac_run(const double *x1, const double *x2, int64_t N, const int32_t *sam
     SFM_HIP(hipEventRecord(c->ev[1], s));
     int ny;
     const int64_t slice = score_slice(H, N, &ny);
-    hipLaunchKernelGGL(k_fit_samples<M>, dim3(ceil_div(H, 64)), dim3(64), 0, s, d1, d2, ds, H, dF,
-                       ny > 1 ? dcnt : nullptr);
-    SFM_HIP(hipGetLastError());
+    if ((rc = launch_fit<M>(d1, d2, ds, H, dF, ny > 1 ? dcnt : nullptr, s))) return rc;
     SFM_HIP(hipEventRecord(c->ev[2], s));
     hipLaunchKernelGGL(k_ransac_score<M>, dim3(ceil_div(H, SCORE_WAVES), ny), dim3(64 * SCORE_WAVES), 0, s, d1, d2,
                        N, dF, H, thr, dcnt, slice);
@@ -280,6 +307,18 @@ int ransac_run(const double *x1, const double *x2, int64_t N, const int32_t *sam
     return 0;
 }
 
+// Correspondences from the pinned host staging buffer into device memory
+// with a kernel on the compute queue (two SDMA copies plus the copy-engine
+// to compute handoff cost ~24 us before the first fit; this ~3 us).
+static __global__ void __launch_bounds__(256) k_stage_pts(const double2 *__restrict__ h, int64_t N, double2 *__restrict__ d1,
+                                                   double2 *__restrict__ d2) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < N) {
+        d1[i] = h[i];
+        d2[i] = h[N + i];
+    }
+}
+
 // The drop-in's whole call with the samples drawn inside it: the CPython
 // random stream (MT19937 state st[625], in/out) is replayed on the host in
 // chunks of RP_CHUNK hypotheses into pinned memory, and each chunk's fit
@@ -298,6 +337,26 @@ static inline int64_t rp_chunk() {
         return v > 0 ? (int64_t)v : RP_CHUNK;
     }();
     return c;
+}
+// chunk sizes ramp up from RP_FIRST (doubling to rp_chunk()): the device
+// waits for the first draw (the pipeline fill), and every later draw has to
+// finish within the previous chunk's kernels
+constexpr int64_t RP_FIRST = 1024;
+static inline int64_t rp_next(int64_t h0, int64_t H) {
+    static const int64_t first = [] {
+        const char *e = std::getenv("SFM_RP_FIRST");
+        const long v = e ? std::atol(e) : 0;
+        return v > 0 ? (int64_t)v : RP_FIRST;
+    }();
+    static const bool ramp = std::getenv("SFM_RP_RAMP") && std::atoi(std::getenv("SFM_RP_RAMP"));
+    const int64_t chunk = rp_chunk();
+    if (!ramp) return std::min(H, h0 + (h0 == 0 ? std::min(first, chunk) : chunk));
+    int64_t size = std::min(first, chunk), pos = 0;
+    while (size < chunk && pos + size <= h0) {
+        pos += size;
+        size = std::min(chunk, 2 * size);
+    }
+    return std::min(H, h0 + size);
 }
 
 template <class M>
@@ -339,35 +398,35 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
     double *dFb = reinterpret_cast<double *>(hout) + 2;
     uint8_t *dmask = reinterpret_cast<uint8_t *>(hout) + 16 * sizeof(double);
     hipStream_t s = c->stream;
-    const auto t0 = std::chrono::steady_clock::now();
-    SFM_HIP(hipEventRecord(c->ev[0], s));
-    SFM_HIP(hipMemcpyAsync(d1, hx, pb, hipMemcpyHostToDevice, s));
-    SFM_HIP(hipMemcpyAsync(d2, hx + pb, pb, hipMemcpyHostToDevice, s));
-    SFM_HIP(hipEventRecord(c->ev[1], s));
+    const bool tm = call_timing();
+    if (tm) SFM_HIP(hipEventRecord(c->ev[0], s));
+    hipLaunchKernelGGL(k_stage_pts, dim3(ceil_div(N, 256)), dim3(256), 0, s, reinterpret_cast<const double2 *>(hx), N,
+                       d1, d2);
+    SFM_HIP(hipGetLastError());
+    if (tm) SFM_HIP(hipEventRecord(c->ev[1], s));
     PySampler ps(st, N, M::K);
     double t_draw = 0;
-    const int64_t chunk = rp_chunk();
-    for (int64_t h0 = 0; h0 < H; h0 += chunk) {
-        const int64_t h1 = std::min(H, h0 + chunk), nh = h1 - h0;
+    for (int64_t h0 = 0, h1; h0 < H; h0 = h1) {
+        h1 = rp_next(h0, H);
+        const int64_t nh = h1 - h0;
         const auto ta = std::chrono::steady_clock::now();
         ps.draw(h0, h1, hs);
         t_draw += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
         int ny;
         const int64_t slice = score_slice(nh, N, &ny);
-        hipLaunchKernelGGL(k_fit_samples<M>, dim3(ceil_div(nh, 64)), dim3(64), 0, s, d1, d2, hs + h0 * M::K, nh,
-                           dF + h0 * 9, ny > 1 ? dcnt + h0 : nullptr);
-        SFM_HIP(hipGetLastError());
+        if ((rc = launch_fit<M>(d1, d2, hs + h0 * M::K, nh, dF + h0 * 9, ny > 1 ? dcnt + h0 : nullptr, s)))
+            return rc;
         hipLaunchKernelGGL(k_ransac_score<M>, dim3(ceil_div(nh, SCORE_WAVES), ny), dim3(64 * SCORE_WAVES), 0, s, d1,
                            d2, N, dF + h0 * 9, nh, thr, dcnt + h0, slice);
         SFM_HIP(hipGetLastError());
     }
     ps.save(st);
-    SFM_HIP(hipEventRecord(c->ev[3], s));
+    if (tm) SFM_HIP(hipEventRecord(c->ev[3], s));
     hipLaunchKernelGGL(k_ransac_select<M>, dim3(1), dim3(1024), 0, s, d1, d2, N, dF, dcnt, H, thr, dbest, dFb, dmask);
     SFM_HIP(hipGetLastError());
-    SFM_HIP(hipEventRecord(c->ev[4], s));
+    if (tm) SFM_HIP(hipEventRecord(c->ev[4], s));
     if (counts_out) SFM_HIP(hipMemcpyAsync(counts_out, dcnt, (size_t)H * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    SFM_HIP(hipEventRecord(c->ev[5], s));
+    if (tm) SFM_HIP(hipEventRecord(c->ev[5], s));
     SFM_HIP(hipStreamSynchronize(s));
     *best_iter = *dbest;
     if (*best_iter >= 0) {
@@ -377,9 +436,11 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
         std::memset(best_mask, 0, (size_t)N);
     }
     if (samples_out) std::memcpy(samples_out, hs, sb);
-    (void)t0;
-    const double t[7] = {ev_ms(c->ev[0], c->ev[1]), ev_ms(c->ev[1], c->ev[4]), ev_ms(c->ev[4], c->ev[5]),
-                         ev_ms(c->ev[1], c->ev[3]), 0.0, ev_ms(c->ev[3], c->ev[4]), t_draw};
+    double t[7] = {0, 0, 0, 0, 0, 0, t_draw};
+    if (tm) {
+        t[0] = ev_ms(c->ev[0], c->ev[1]); t[1] = ev_ms(c->ev[1], c->ev[4]); t[2] = ev_ms(c->ev[4], c->ev[5]);
+        t[3] = ev_ms(c->ev[1], c->ev[3]); t[5] = ev_ms(c->ev[3], c->ev[4]);
+    }
     set_timings(t, 7);
     return 0;
 }
@@ -447,10 +508,12 @@ int ransac_run_range(const double *x1, const double *x2, int64_t N, const int32_
     int64_t *dbest = reinterpret_cast<int64_t *>(hout);
     double *dFb = reinterpret_cast<double *>(hout) + 2;
     hipStream_t s = c->stream;
-    SFM_HIP(hipEventRecord(c->ev[0], s));
-    SFM_HIP(hipMemcpyAsync(d1, hx, pb, hipMemcpyHostToDevice, s));
-    SFM_HIP(hipMemcpyAsync(d2, hx + pb, pb, hipMemcpyHostToDevice, s));
-    SFM_HIP(hipEventRecord(c->ev[1], s));
+    const bool tm = call_timing();
+    if (tm) SFM_HIP(hipEventRecord(c->ev[0], s));
+    hipLaunchKernelGGL(k_stage_pts, dim3(ceil_div(N, 256)), dim3(256), 0, s, reinterpret_cast<const double2 *>(hx), N,
+                       d1, d2);
+    SFM_HIP(hipGetLastError());
+    if (tm) SFM_HIP(hipEventRecord(c->ev[1], s));
     double t_draw = 0;
     // fit + score the hypotheses [a, b) of the shard whose rows sit at rows
     auto launch = [&](int64_t a, int64_t b, const int32_t *rows) -> int {
@@ -458,9 +521,9 @@ int ransac_run_range(const double *x1, const double *x2, int64_t N, const int32_
         const int64_t n = b - a;
         int ny;
         const int64_t slice = score_slice(n, N, &ny);
-        hipLaunchKernelGGL(k_fit_samples<M>, dim3(ceil_div(n, 64)), dim3(64), 0, s, d1, d2, rows, n,
-                           dF + (a - r0) * 9, ny > 1 ? dcnt + (a - r0) : nullptr);
-        SFM_HIP(hipGetLastError());
+        int rc2;
+        if ((rc2 = launch_fit<M>(d1, d2, rows, n, dF + (a - r0) * 9, ny > 1 ? dcnt + (a - r0) : nullptr, s)))
+            return rc2;
         hipLaunchKernelGGL(k_ransac_score<M>, dim3(ceil_div(n, SCORE_WAVES), ny), dim3(64 * SCORE_WAVES), 0, s, d1, d2,
                            N, dF + (a - r0) * 9, n, thr, dcnt + (a - r0), slice);
         SFM_HIP(hipGetLastError());
@@ -468,9 +531,8 @@ int ransac_run_range(const double *x1, const double *x2, int64_t N, const int32_
     };
     if (st) {
         PySampler ps(st, N, M::K);
-        const int64_t chunk = rp_chunk();
-        for (int64_t h0 = 0; h0 < H; h0 += chunk) {
-            const int64_t h1 = std::min(H, h0 + chunk);
+        for (int64_t h0 = 0, h1; h0 < H; h0 = h1) {
+            h1 = rp_next(h0, H);
             const auto ta = std::chrono::steady_clock::now();
             ps.draw(h0, h1, hs);
             t_draw += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
@@ -482,23 +544,26 @@ int ransac_run_range(const double *x1, const double *x2, int64_t N, const int32_
         std::memcpy(hs, samples + r0 * M::K, sb);
         if ((rc = launch(r0, r1, hs))) return rc;
     }
-    SFM_HIP(hipEventRecord(c->ev[3], s));
+    if (tm) SFM_HIP(hipEventRecord(c->ev[3], s));
     if (nh > 0) {
         hipLaunchKernelGGL(k_ransac_select<M>, dim3(1), dim3(1024), 0, s, d1, d2, N, dF, dcnt, nh, thr, dbest, dFb,
                            (uint8_t *)nullptr);
         SFM_HIP(hipGetLastError());
     }
-    SFM_HIP(hipEventRecord(c->ev[4], s));
+    if (tm) SFM_HIP(hipEventRecord(c->ev[4], s));
     if (counts_out && nh)
         SFM_HIP(hipMemcpyAsync(counts_out, dcnt, (size_t)nh * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    SFM_HIP(hipEventRecord(c->ev[5], s));
+    if (tm) SFM_HIP(hipEventRecord(c->ev[5], s));
     SFM_HIP(hipStreamSynchronize(s));
     if (nh > 0 && dbest[0] >= 0) {
         *key_out = shard_key(dbest[1], r0 + dbest[0]);
         std::memcpy(F_best, dFb, 9 * sizeof(double));
     }
-    const double t[7] = {ev_ms(c->ev[0], c->ev[1]), ev_ms(c->ev[1], c->ev[4]), ev_ms(c->ev[4], c->ev[5]),
-                         ev_ms(c->ev[1], c->ev[3]), 0.0, ev_ms(c->ev[3], c->ev[4]), t_draw};
+    double t[7] = {0, 0, 0, 0, 0, 0, t_draw};
+    if (tm) {
+        t[0] = ev_ms(c->ev[0], c->ev[1]); t[1] = ev_ms(c->ev[1], c->ev[4]); t[2] = ev_ms(c->ev[4], c->ev[5]);
+        t[3] = ev_ms(c->ev[1], c->ev[3]); t[5] = ev_ms(c->ev[3], c->ev[4]);
+    }
     set_timings(t, 7);
     return 0;
 }

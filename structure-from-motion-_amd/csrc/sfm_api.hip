@@ -1,6 +1,7 @@
 // libsfmcore: C-ABI plumbing + the small entry points
 // (EstimateFundamentalMatrix general-N, LinearTriangulation, project_points,
 // bundle_adjustment_residuals) and the host-side CPython random replay.
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -26,6 +27,8 @@ void set_error(const char *fmt, ...) {
     g_err = buf;
 }
 void clear_error() { g_err.clear(); }
+static std::atomic<int> g_call_timing{0};
+bool call_timing() { return g_call_timing.load(std::memory_order_relaxed) != 0; }
 void set_timings(const double *t, int n) {
     g_ntimings = n < 8 ? n : 8;
     for (int i = 0; i < g_ntimings; ++i) g_timings[i] = t[i];
@@ -160,6 +163,10 @@ extern "C" int sfm_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
+}
+extern "C" int sfm_set_call_timing(int on) {
+    g_call_timing.store(on != 0, std::memory_order_relaxed);
+    return 0;
 }
 extern "C" int sfm_last_timings(double *out, int n) {
     const int m = n < g_ntimings ? n : g_ntimings;

@@ -16,6 +16,9 @@ namespace sfm {
 void set_error(const char *fmt, ...);
 void clear_error();
 void set_timings(const double *t, int n);
+// HIP events for sfm_last_timings in the drop-in RANSAC calls (off by
+// default: each event record costs the stream a few microseconds)
+bool call_timing();
 
 #define SFM_HIP(call)                                                                        \
     do {                                                                                     \

@@ -23,34 +23,57 @@ __device__ __forceinline__ bool epi_inlier(const double *F, double x, double y, 
     return (d1 + d2) * 0.5 < thr;
 }
 
-// Same decision, cheaper: approximate sqrt / reciprocal (v_rsq_f64,
-// v_rcp_f64, ~1e-7 relative) decide every pair whose approximate error is
-// farther than 1e-4 relative from the threshold; the rest (and any
-// non-finite / tiny operand) take the exact expression above.  The
-// decision is therefore always the exact one.
-__device__ __forceinline__ bool epi_inlier_fast(const double *F, double x, double y, double u, double v,
-                                                double thr, double thr_lo, double thr_hi) {
+// Same decision, cheaper: approximate sqrt / reciprocal (v_rsq_f64, ~1e-7
+// relative) decide every pair whose approximate error is farther than 1e-4
+// relative from the threshold; the rest (and any non-finite / tiny
+// operand) take the exact expression (epi_exact).  The decision is
+// therefore always the exact one.  Split in two so a caller can run the
+// fast part of several pairs before any branch to the exact tail.
+struct EpiPart {
+    double ae, qa, qb;  // |x2^T F x1|, |Fx1|_xy^2, |F^T x2|_xy^2
+    bool in, unsure;    // fast decision; unsure: take epi_exact
+};
+
+__device__ __forceinline__ EpiPart epi_fast(const double *F, double x, double y, double u, double v, double thr_lo2,
+                                            double thr_hi2) {
     const double a0 = F[0] * x + F[1] * y + F[2];
     const double a1 = F[3] * x + F[4] * y + F[5];
     const double a2 = F[6] * x + F[7] * y + F[8];
     const double b0 = F[0] * u + F[3] * v + F[6];
     const double b1 = F[1] * u + F[4] * v + F[7];
     const double e = u * a0 + v * a1 + a2;
-    const double ae = fabs(e);
-    const double qa = a0 * a0 + a1 * a1, qb = b0 * b0 + b1 * b1;
+    EpiPart r;
+    r.ae = fabs(e);
+    r.qa = a0 * a0 + a1 * a1;
+    r.qb = b0 * b0 + b1 * b1;
     // 1 / (sqrt(q) + 1e-8) = r (1 - 1e-8 r + ...), r = rsq(q): first order,
-    // whose error (1e-8 r)^2 <= 1e-6 relative while q > 1e-10 -- no v_rcp
-    const double ra = __builtin_amdgcn_rsq(qa), rb = __builtin_amdgcn_rsq(qb);
-    const double ia = fma(-1e-8 * ra, ra, ra), ib = fma(-1e-8 * rb, rb, rb);
-    const double ap = ae * (ia + ib) * 0.5;
-    const bool ok = qa > 1e-10 && qb > 1e-10 && qa < 1e280 && qb < 1e280;
-    const bool sure_in = ap < thr_lo && ok;
-    const bool sure_out = ap > thr_hi && ok;
-    if (sure_in) return true;
-    if (sure_out) return false;
-    const double d1 = ae / (sqrt(qa) + 1e-8);
-    const double d2 = ae / (sqrt(qb) + 1e-8);
+    // whose error (1e-8 r)^2 <= 1e-6 relative while r < 1e5 (q > 1e-10) --
+    // no v_rcp.  ok = ra + rb < 1e5 holds exactly when both r are finite and
+    // below 1e5 (a NaN fails it), so it also guards q = 0 / NaN; q = inf
+    // gives r = 0, the exact limit.  thr_lo2 / thr_hi2 are the band around
+    // 2 thr (the 1/2 of the mean is folded in).
+    const double ra = __builtin_amdgcn_rsq(r.qa), rb = __builtin_amdgcn_rsq(r.qb);
+    const double srr = ra + rb;
+    const double ap2 = r.ae * fma(-1e-8, fma(ra, ra, rb * rb), srr);  // ae (ia + ib)
+    const bool ok = srr < 1e5;
+    const bool sure_in = ap2 < thr_lo2 && ok;
+    const bool sure_out = ap2 > thr_hi2 && ok;
+    r.in = sure_in;
+    r.unsure = !(sure_in || sure_out);
+    return r;
+}
+
+// the exact tail of epi_inlier from epi_fast's terms (same operations)
+__device__ __forceinline__ bool epi_exact(const EpiPart &r, double thr) {
+    const double d1 = r.ae / (sqrt(r.qa) + 1e-8);
+    const double d2 = r.ae / (sqrt(r.qb) + 1e-8);
     return (d1 + d2) * 0.5 < thr;
+}
+
+__device__ __forceinline__ bool epi_inlier_fast(const double *F, double x, double y, double u, double v,
+                                                double thr, double thr_lo2, double thr_hi2) {
+    const EpiPart r = epi_fast(F, x, y, u, v, thr_lo2, thr_hi2);
+    return r.unsure ? epi_exact(r, thr) : r.in;
 }
 
 // --------------------------------------------------------------------
