@@ -728,8 +728,10 @@ def test_reduced_solve(core, n):
     assert np.array_equal(x, core.reduced_solve(S, b))
 
 
-def test_reduced_solve_not_spd(core):
-    S, b = _spd(40, seed=1)
+@pytest.mark.parametrize("n", [40, 300])
+def test_reduced_solve_not_spd(core, n):
+    """A non-positive pivot is reported (n = 300: the one-workgroup factor)."""
+    S, b = _spd(n, seed=1)
     S[7, 7] = -1.0
     with pytest.raises(RuntimeError, match="positive definite"):
         core.reduced_solve(S, b)
