@@ -176,10 +176,15 @@ def next_rows(core, local_rank, cpu):
     P2 = K @ np.hstack([m["R2"], (-m["R2"] @ m["C2"]).reshape(3, 1)])
     X0 = core.triangulate(P1, P2, x1, x2)
     core.triangulate_nonlinear(P1, P2, x1[:1000], x2[:1000], X0[:1000])
+    # kernel times from a call with HIP events on (sfm_set_call_timing),
+    # end-to-end from a call without them
+    core.set_call_timing(True)
+    core.triangulate_nonlinear(P1, P2, x1, x2, X0)
+    tk = core.last_timings()[1] * 1e-3
+    core.set_call_timing(False)
     t = time.perf_counter()
     core.triangulate_nonlinear(P1, P2, x1, x2, X0)
     te = time.perf_counter() - t
-    tk = core.last_timings()[1] * 1e-3
     r = {"workload": "1M two-view points, 20% outliers, DLT start, max_nfev=50",
          "points_per_s_kernel": round(len(x1) / tk, 1), "points_per_s_end_to_end": round(len(x1) / te, 1)}
     if cpu:
@@ -219,10 +224,13 @@ def next_rows(core, local_rank, cpu):
     random.seed(1)
     ps = core.sample_table(n, 4, 16384)
     core.pnp_ransac(Xw, xw, K, ps, 8.0)
+    core.set_call_timing(True)
+    core.pnp_ransac(Xw, xw, K, ps, 8.0)
+    tk = core.last_timings()[1] * 1e-3
+    core.set_call_timing(False)
     t = time.perf_counter()
     _, _, C, R, _, _ = core.pnp_ransac(Xw, xw, K, ps, 8.0)
     te = time.perf_counter() - t
-    tk = core.last_timings()[1] * 1e-3
     core.nonlinear_pnp(Xw, xw, K, C, R)  # warm
     tl = []
     for _ in range(5):

@@ -94,24 +94,25 @@ extern "C" int sfm_triangulate_nonlinear(const double *P1, const double *P2, con
     std::memcpy(cams.p, P1, 12 * sizeof(double));
     std::memcpy(cams.p + 12, P2, 12 * sizeof(double));
     hipStream_t s = c->stream;
-    SFM_HIP(hipEventRecord(c->ev[0], s));
+    const bool tm = call_timing();  // HIP events only when asked (each costs the stream us)
+    if (tm) SFM_HIP(hipEventRecord(c->ev[0], s));
     SFM_HIP(hipMemcpyAsync(c->buf[0].p, x1, pb, hipMemcpyHostToDevice, s));
     SFM_HIP(hipMemcpyAsync(c->buf[1].p, x2, pb, hipMemcpyHostToDevice, s));
     SFM_HIP(hipMemcpyAsync(c->buf[2].p, X0, xb, hipMemcpyHostToDevice, s));
-    SFM_HIP(hipEventRecord(c->ev[1], s));
+    if (tm) SFM_HIP(hipEventRecord(c->ev[1], s));
     hipLaunchKernelGGL(k_nltri, dim3(ceil_div(N, 256)), dim3(256), 0, s, cams, c->buf[0].as<double2>(),
                        c->buf[1].as<double2>(), c->buf[2].as<double>(), N, max_nfev, c->buf[3].as<double>(),
                        c->buf[4].as<int32_t>());
     SFM_HIP(hipGetLastError());
-    SFM_HIP(hipEventRecord(c->ev[2], s));
+    if (tm) SFM_HIP(hipEventRecord(c->ev[2], s));
     SFM_HIP(hipMemcpyAsync(X, c->buf[3].p, xb, hipMemcpyDeviceToHost, s));
     if (info) SFM_HIP(hipMemcpyAsync(info, c->buf[4].p, (size_t)N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    SFM_HIP(hipEventRecord(c->ev[3], s));
+    if (tm) SFM_HIP(hipEventRecord(c->ev[3], s));
     SFM_HIP(hipStreamSynchronize(s));
     float a = 0, b = 0, d = 0;
-    (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
-    (void)hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
-    (void)hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
+    if (tm) (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
+    if (tm) (void)hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
+    if (tm) (void)hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
     const double t[4] = {a, b, d, b};
     set_timings(t, 4);
     return 0;

@@ -1145,28 +1145,29 @@ extern "C" int sfm_pnp_ransac(const double *X, const double *x, int64_t N, const
     int32_t *ds = c->buf[2].as<int32_t>(), *dcnt = c->buf[4].as<int32_t>(), *dbr = c->buf[5].as<int32_t>();
     int64_t *dbest = reinterpret_cast<int64_t *>(dOut + 24);
     hipStream_t s = c->stream;
-    SFM_HIP(hipEventRecord(c->ev[0], s));
+    const bool tm = call_timing();  // HIP events only when asked (each costs the stream us)
+    if (tm) SFM_HIP(hipEventRecord(c->ev[0], s));
     SFM_HIP(hipMemcpyAsync(dX, X, (size_t)N * 24, hipMemcpyHostToDevice, s));
     SFM_HIP(hipMemcpyAsync(dx, x, (size_t)N * 16, hipMemcpyHostToDevice, s));
     SFM_HIP(hipMemcpyAsync(ds, samples, (size_t)H * 4 * sizeof(int32_t), hipMemcpyHostToDevice, s));
-    SFM_HIP(hipEventRecord(c->ev[1], s));
+    if (tm) SFM_HIP(hipEventRecord(c->ev[1], s));
     hipLaunchKernelGGL(k_pnp_fit, dim3(ceil_div(H, 64)), dim3(64), 0, s, dX, dx, ds, H, cam, dM, dbr);
     SFM_HIP(hipGetLastError());
-    SFM_HIP(hipEventRecord(c->ev[2], s));
+    if (tm) SFM_HIP(hipEventRecord(c->ev[2], s));
     hipLaunchKernelGGL(k_pnp_score, dim3(ceil_div(H, PNP_WAVES)), dim3(64 * PNP_WAVES), 0, s, dX, dx, N, dM, H, thr,
                        dcnt);
     SFM_HIP(hipGetLastError());
-    SFM_HIP(hipEventRecord(c->ev[3], s));
+    if (tm) SFM_HIP(hipEventRecord(c->ev[3], s));
     hipLaunchKernelGGL(k_pnp_select, dim3(1), dim3(1024), 0, s, dM, dcnt, H, dbest, dOut);
     SFM_HIP(hipGetLastError());
-    SFM_HIP(hipEventRecord(c->ev[4], s));
+    if (tm) SFM_HIP(hipEventRecord(c->ev[4], s));
     double out[24];
     int64_t best[2];
     SFM_HIP(hipMemcpyAsync(out, dOut, sizeof out, hipMemcpyDeviceToHost, s));
     SFM_HIP(hipMemcpyAsync(best, dbest, sizeof best, hipMemcpyDeviceToHost, s));
     if (counts_out) SFM_HIP(hipMemcpyAsync(counts_out, dcnt, (size_t)H * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     if (branch_out) SFM_HIP(hipMemcpyAsync(branch_out, dbr, (size_t)H * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    SFM_HIP(hipEventRecord(c->ev[5], s));
+    if (tm) SFM_HIP(hipEventRecord(c->ev[5], s));
     SFM_HIP(hipStreamSynchronize(s));
     *best_iter = best[0];
     if (best_count) *best_count = best[1];
@@ -1175,11 +1176,11 @@ extern "C" int sfm_pnp_ransac(const double *X, const double *x, int64_t N, const
         std::memcpy(R_best, out + 15, 9 * sizeof(double));
     }
     float a = 0, b = 0, d = 0, e = 0, f = 0;
-    (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
-    (void)hipEventElapsedTime(&b, c->ev[1], c->ev[4]);
-    (void)hipEventElapsedTime(&d, c->ev[4], c->ev[5]);
-    (void)hipEventElapsedTime(&e, c->ev[2], c->ev[3]);
-    (void)hipEventElapsedTime(&f, c->ev[1], c->ev[2]);
+    if (tm) (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
+    if (tm) (void)hipEventElapsedTime(&b, c->ev[1], c->ev[4]);
+    if (tm) (void)hipEventElapsedTime(&d, c->ev[4], c->ev[5]);
+    if (tm) (void)hipEventElapsedTime(&e, c->ev[2], c->ev[3]);
+    if (tm) (void)hipEventElapsedTime(&f, c->ev[1], c->ev[2]);
     const double t[5] = {a, b, d, e, f};
     set_timings(t, 5);
     return 0;

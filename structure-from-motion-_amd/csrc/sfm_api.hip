@@ -218,21 +218,22 @@ extern "C" int sfm_triangulate_dlt(const double *P1, const double *P2_, const do
     std::memcpy(P.p, P1, 12 * sizeof(double));
     std::memcpy(P.p + 12, P2_, 12 * sizeof(double));
     hipStream_t s = c->stream;
-    SFM_HIP(hipEventRecord(c->ev[0], s));
+    const bool tm = call_timing();  // HIP events only when asked (each costs the stream us)
+    if (tm) SFM_HIP(hipEventRecord(c->ev[0], s));
     SFM_HIP(hipMemcpyAsync(c->buf[0].p, x1, pb, hipMemcpyHostToDevice, s));
     SFM_HIP(hipMemcpyAsync(c->buf[1].p, x2, pb, hipMemcpyHostToDevice, s));
-    SFM_HIP(hipEventRecord(c->ev[1], s));
+    if (tm) SFM_HIP(hipEventRecord(c->ev[1], s));
     hipLaunchKernelGGL(k_triangulate, dim3(ceil_div(N, 256)), dim3(256), 0, s, P, c->buf[0].as<double2>(),
                        c->buf[1].as<double2>(), N, c->buf[2].as<double>());
     SFM_HIP(hipGetLastError());
-    SFM_HIP(hipEventRecord(c->ev[2], s));
+    if (tm) SFM_HIP(hipEventRecord(c->ev[2], s));
     SFM_HIP(hipMemcpyAsync(X, c->buf[2].p, (size_t)N * 24, hipMemcpyDeviceToHost, s));
-    SFM_HIP(hipEventRecord(c->ev[3], s));
+    if (tm) SFM_HIP(hipEventRecord(c->ev[3], s));
     SFM_HIP(hipStreamSynchronize(s));
     float a = 0, b = 0, d = 0;
-    (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
-    (void)hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
-    (void)hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
+    if (tm) (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
+    if (tm) (void)hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
+    if (tm) (void)hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
     const double t[4] = {a, b, d, b};
     set_timings(t, 4);
     return 0;

@@ -13,6 +13,7 @@ import sfm_synthetic as syn  # noqa: E402
 
 x1, x2, _, _ = syn.two_view(n=5000, outlier_frac=0.4, seed=2)
 H = int(os.environ.get("H", 16384))
+core.set_call_timing(True)  # device split of the in-call path
 for fn in (core.ransac_f8_pyrandom, core.ransac_h4_pyrandom):
     for _ in range(3):
         random.seed(0)
