@@ -835,3 +835,68 @@ def test_ransac_combine_through_rccl_communicator(core):
     b, Fb, mask, _, _ = core.ransac_f8_pyrandom(x1, x2, 700, 0.06)
     assert sfm_dist.key_iter(key)[1] == b and np.array_equal(F, Fb)
     assert np.array_equal(core.ransac_mask(x1, x2, F, 0.06), mask)
+
+
+def test_ba_camera_blocks_fused_equal_standalone(core, monkeypatch):
+    """The camera blocks of the normal equations computed by extra workgroups
+    of the Schur sweep (default) and by the standalone k_camera_lin
+    (SFM_CAMLIN_FUSED=0): the same LM trajectory (counts, status) and final
+    cost within 1e-10 (the two cut each camera's observations into different
+    items, so the sums differ in order only)."""
+    p = syn.ba_problem_cfg("cfg3", dense=False)
+    cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
+    args = (cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K)
+    reps = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("SFM_CAMLIN_FUSED", fused)
+        _, _, reps[fused] = core.ba_lm(*args, max_iterations=30)
+    a, b = reps["1"], reps["0"]
+    assert (a["iterations"], a["accepted"], a["status"]) == (b["iterations"], b["accepted"], b["status"])
+    assert abs(a["cost"] - b["cost"]) <= 1e-10 * b["cost"]
+
+
+def test_ba_timing_and_lm_state_polling(core):
+    """Per-phase kernel times are recorded only with sfm_ba_set_timing on,
+    and turning them on does not change the solve; a solve that converges
+    early stops there (the host reads the LM state from the pinned ring, at
+    most two gated-off iterations follow) and a repeated solve is bitwise
+    the same."""
+    p = syn.ba_problem_cfg("cfg3", dense=False)
+    cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
+    prob = core.BAProblem(cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K)
+    try:
+        r0 = prob.solve(max_iterations=200)
+        assert r0["status"] in (1, 3) and r0["iterations"] < 200
+        assert all(v == 0.0 for v in prob.kernel_times().values())
+        c0, x0 = prob.download()
+        prob.reset()
+        prob.set_timing(True)
+        r1 = prob.solve(max_iterations=200)
+        kt = prob.kernel_times()
+        assert kt["schur_blocks"] > 0 and kt["cholesky"] > 0
+        c1, x1 = prob.download()
+        assert (r1["iterations"], r1["accepted"], r1["cost"]) == (r0["iterations"], r0["accepted"], r0["cost"])
+        assert np.array_equal(c0, c1) and np.array_equal(x0, x1)
+        prob.set_timing(False)
+        for it in (1, 2, 3):  # stops exactly at max_iterations when it has not converged
+            prob.reset()
+            assert prob.solve(max_iterations=it, fixed_iterations=True)["iterations"] == it
+    finally:
+        prob.close()
+
+
+def test_call_timing_switch(core):
+    """The drop-in RANSAC call records device timings only with
+    sfm_set_call_timing on; the host sampling time is always reported, and
+    the result does not depend on the switch."""
+    x1, x2, _, _ = syn.two_view(n=1500, seed=3)
+    out = []
+    for on in (False, True, False):
+        core.set_call_timing(on)
+        random.seed(11)
+        out.append(core.ransac_f8_pyrandom(x1, x2, 900, 0.06, want_counts=True))
+        t = core.last_timings()
+        assert (t[1] > 0) == on and t[6] > 0
+    b0, M0, m0, c0 = out[0][:4]
+    for b, M, m, c in (o[:4] for o in out[1:]):
+        assert b == b0 and np.array_equal(c, c0) and np.array_equal(m, m0) and np.array_equal(M, M0)
