@@ -850,24 +850,27 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
         }
         __syncthreads();  // chunk q's buffer is free; chunk q+1's staging has landed
     }
-    // reduce the group's slots (lanes of equal parity), fixed butterfly
+    // reduce the group's slots (lanes of equal parity) in slot order through
+    // LDS (the staging buffers are free now), 7 accumulators per round;
+    // groups of any size and position
+    double *red = reinterpret_cast<double *>(sw_lds);
+    double *out = slab + ((int64_t)r * nbd + grp.blk) * ITEM_W;
 #pragma unroll
-    for (int k = 0; k < 21; ++k) {
-        double v = acc[k];
+    for (int k0 = 0; k0 < 21; k0 += 7) {
 #pragma unroll
-        for (int o = 2; o < 64; o <<= 1) {
-            const double u = __shfl_xor(v, o);
-            if (o < grp.G) v += u;
+        for (int k = 0; k < 7; ++k) red[k * SW_THREADS + t] = acc[k0 + k];
+        __syncthreads();
+        if (gi >= 0 && slot == 0) {
+#pragma unroll
+            for (int k = 0; k < 7; ++k) {
+                double v = 0.0;
+                for (int sl = 0; sl < nslot; ++sl) v += red[k * SW_THREADS + grp.lane_base + 2 * sl + h];
+                const int kk = k0 + k;
+                if (kk < 18) out[18 * h + kk] = v;
+                else if (diag) out[36 + 3 * h + (kk - 18)] = v;
+            }
         }
-        acc[k] = v;
-    }
-    if (gi >= 0 && slot == 0) {
-        double *out = slab + ((int64_t)r * nbd + grp.blk) * ITEM_W;
-#pragma unroll
-        for (int k = 0; k < 18; ++k) out[18 * h + k] = acc[k];
-        if (diag)
-#pragma unroll
-            for (int k = 0; k < 3; ++k) out[36 + 3 * h + k] = acc[18 + k];
+        __syncthreads();
     }
 }
 
@@ -1685,8 +1688,8 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
             for (int j = specs[w][rr].j0; j < specs[w][rr].j1; ++j) spec_of[(size_t)specs[w][rr].c * nc + j] = w;
     P.lanegrp.assign((size_t)P.nspec * SW_THREADS, (int16_t)-1);
     // per spec: diagonal groups first (they only read LDS, so their waves
-    // are the loader waves), then the off-diagonal groups sorted by size
-    // (power-of-two lane counts, so every group is aligned inside its wave)
+    // are the loader waves; power-of-two sizes), then the off-diagonal groups
+    // sorted by size
     std::vector<std::vector<int>> gid_of(P.nspec);  // (row, j - j0) -> group index within spec
     int max_ng = 0;
     for (int w = 0; w < P.nspec; ++w) {
@@ -1714,18 +1717,34 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
             budget = (SW_THREADS - 64 * nload) / 2;
             if (noff <= budget) break;
         }
+        // slots in proportion to the block's pair work, the whole budget
+        // used: floor shares (at least one), then the remaining slots one at
+        // a time to the group with the most work per slot (any group size:
+        // the end-of-range reduction goes through LDS, so groups need not be
+        // powers of two nor stay inside one wave).  SFM_SWEEP_POW2=1 keeps
+        // the earlier power-of-two sizes (61 % of the budget at cfg4).
         int sum = 0;
+        const bool pow2 = env_int("SFM_SWEEP_POW2", 0) != 0;
         for (auto &x : g) {
-            const double raw = tot > 0 ? x.work / tot * budget : 1.0;
-            int sl = 1;
-            while (sl * 2 <= raw && sl < 32) sl *= 2;
-            x.slots = sl;
-            sum += sl;
+            x.slots = std::max(1, (int)(tot > 0 ? x.work / tot * budget : 1.0));
+            if (pow2) {
+                int sl = 1;
+                while (sl * 2 <= x.slots && sl < 32) sl *= 2;
+                x.slots = sl;
+            }
+            sum += x.slots;
         }
-        while (sum > budget) {  // over budget: halve the largest
+        while (sum > budget) {  // rounding up to one slot overshot: trim the largest
             auto it = std::max_element(g.begin(), g.end(), [](const G0 &a, const G0 &b) { return a.slots < b.slots; });
-            it->slots /= 2;
-            sum -= it->slots;
+            it->slots -= 1;
+            sum -= 1;
+        }
+        while (!pow2 && sum < budget && !g.empty()) {
+            auto it = std::max_element(g.begin(), g.end(), [](const G0 &a, const G0 &b) {
+                return a.work * b.slots < b.work * a.slots;  // a.work / a.slots < b.work / b.slots
+            });
+            it->slots += 1;
+            sum += 1;
         }
         std::stable_sort(g.begin(), g.end(), [](const G0 &a, const G0 &b) { return a.slots > b.slots; });
         for (auto &x : gd) x.slots = Gd / 2;
@@ -2092,7 +2111,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     p->sw_nbd = sw.nbd;
     p->sw_L = {sw.buf_slots, sw.pair_cap, sw.hdr_cap, sw.list_cap};
     p->sw_nchunk = sw.nchunk;
-    p->sw_lds_bytes = sw.lds_bytes();
+    p->sw_lds_bytes = std::max(sw.lds_bytes(), (size_t)7 * SW_THREADS * sizeof(double));  // + the end-of-range reduction
     p->pt_blocks = std::max(1, ceil_div(np_ * PT_GROUP, PT_THREADS));
     p->payload_len = pay_vec_base(p->ns) + 3 * p->ns + 1;
     int rc;
