@@ -4,8 +4,9 @@
 //   HomModel  homography, 4-point samples, transfer error
 //             (GetHomographyInliers.py:88-165)
 // Kernels:
-//   k_fit_samples<M>   one thread per hypothesis: gather the K sampled
-//                      correspondences and fit the 3x3 model.
+//   k_fit_samples<M>   gather the K sampled correspondences and fit the 3x3
+//                      model: 8 lanes per hypothesis for F (f8_points_group8),
+//                      one thread per hypothesis for H.
 //   k_ransac_score<M>  one WAVE per hypothesis: the model is wave-uniform
 //                      (scalar registers); correspondence tiles are staged
 //                      once per workgroup in LDS and every wave sweeps them,
@@ -19,6 +20,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "sfm_common.hpp"
 #include "sfm_geom.hpp"
@@ -31,6 +33,7 @@ constexpr int SCORE_TILE = 1024;        // correspondences per LDS tile (32 KiB)
 
 struct EpiModel {
     static constexpr int K = 8;
+    static constexpr bool GROUP_FIT = true;  // has an 8-lane fit (f8_points_group8)
     __device__ static void fit(const double (&ax)[K], const double (&ay)[K], const double (&bx)[K],
                                const double (&by)[K], double *out) {
         f8_points(ax, ay, bx, by, out);
@@ -52,6 +55,7 @@ struct EpiModel {
 
 struct HomModel {
     static constexpr int K = 4;
+    static constexpr bool GROUP_FIT = false;
     __device__ static void fit(const double (&ax)[K], const double (&ay)[K], const double (&bx)[K],
                                const double (&by)[K], double *out) {
         h4_points(ax, ay, bx, by, out);
@@ -75,6 +79,16 @@ template <class M>
 __global__ void __launch_bounds__(256) k_fit_samples(const double2 *__restrict__ x1, const double2 *__restrict__ x2,
                                                      const int32_t *__restrict__ samples, int64_t H,
                                                      double *__restrict__ out, int32_t *__restrict__ counts) {
+    if constexpr (M::GROUP_FIT) {  // 8 lanes per hypothesis, as in the fused launches (same bits)
+        const int64_t h = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
+        if (h >= H) return;
+        const int i = threadIdx.x & 7;
+        if (counts && i == 0) counts[h] = 0;
+        const int32_t sidx = samples[h * 8 + i];
+        const double2 p = x1[sidx], q = x2[sidx];
+        f8_points_group8(p.x, p.y, q.x, q.y, out + 9 * h);
+        return;
+    }
     const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (h >= H) return;
     if (counts) counts[h] = 0;  // the point-sliced score accumulates into it
@@ -92,7 +106,10 @@ __global__ void __launch_bounds__(256) k_fit_samples(const double2 *__restrict__
 template <class M>
 static int launch_fit(const double2 *d1, const double2 *d2, const int32_t *rows, int64_t H, double *dF,
                       int32_t *counts, hipStream_t s) {
-    hipLaunchKernelGGL(k_fit_samples<M>, dim3(ceil_div(H, 64)), dim3(64), 0, s, d1, d2, rows, H, dF, counts);
+    if constexpr (M::GROUP_FIT)
+        hipLaunchKernelGGL(k_fit_samples<M>, dim3(ceil_div(H * 8, 256)), dim3(256), 0, s, d1, d2, rows, H, dF, counts);
+    else
+        hipLaunchKernelGGL(k_fit_samples<M>, dim3(ceil_div(H, 64)), dim3(64), 0, s, d1, d2, rows, H, dF, counts);
     SFM_HIP(hipGetLastError());
     return 0;
 }
@@ -112,17 +129,58 @@ __global__ void __launch_bounds__(256) k_fit_points(const double2 *__restrict__ 
     M::fit(ax, ay, bx, by, out + 9 * h);
 }
 
+// The next chunk's fit, carried by the first nfb workgroups of a score
+// launch (row y = 0): 8 lanes per hypothesis (f8_points_group8), so the
+// launch keeps the score's register budget, and the fit runs beside the
+// score instead of between two score launches.
+struct FitNext {
+    const int32_t *rows;  // nh x K sample rows (pinned, zero-copy)
+    int64_t nh;
+    double *F;            // nh x 9
+    int32_t *counts;      // zeroed when the next score is point-sliced, else null
+    int nfb;              // fit workgroups (64 hypotheses each)
+};
+constexpr int FIT_PER_WG = 64 * SCORE_WAVES / 8;
+
 template <class M>
-__global__ void __launch_bounds__(64 * SCORE_WAVES) k_ransac_score(const double2 *__restrict__ x1,
+__device__ __forceinline__ void fit_next_group(const double2 *__restrict__ x1, const double2 *__restrict__ x2,
+                                               const FitNext &fn) {
+    const int64_t h = (int64_t)blockIdx.x * FIT_PER_WG + (threadIdx.x >> 3);
+    if (h >= fn.nh) return;
+    const int i = threadIdx.x & 7;
+    if (fn.counts && i == 0) fn.counts[h] = 0;
+    const int32_t sidx = fn.rows[h * 8 + i];
+    const double2 p = x1[sidx], q = x2[sidx];
+    f8_points_group8(p.x, p.y, q.x, q.y, fn.F + 9 * h);
+}
+
+// waves per SIMD the fused launch is compiled for: the score alone needs 50
+// VGPRs, the fit's rank-2 step (with its Jacobi fallback) ~120, so the cap
+// makes the fit spill (off the critical path) rather than the score lose
+// occupancy
+#ifndef SFM_SCORE_FIT_OCC
+#define SFM_SCORE_FIT_OCC 8
+#endif
+template <class M, bool FIT = false>
+__global__ void __launch_bounds__(64 * SCORE_WAVES, FIT ? SFM_SCORE_FIT_OCC : 1) k_ransac_score(const double2 *__restrict__ x1,
                                                                    const double2 *__restrict__ x2,
                                                                    int64_t N, const double *__restrict__ F,
                                                                    int64_t H, double thr,
-                                                                   int32_t *__restrict__ counts, int64_t slice) {
+                                                                   int32_t *__restrict__ counts, int64_t slice,
+                                                                   FitNext fn) {
     __shared__ double2 s1[SCORE_TILE];
     __shared__ double2 s2[SCORE_TILE];
+    int bx = blockIdx.x;
+    if (FIT) {
+        if (bx < fn.nfb) {
+            if (blockIdx.y == 0) fit_next_group<M>(x1, x2, fn);
+            return;
+        }
+        bx -= fn.nfb;
+    }
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t h = (int64_t)blockIdx.x * SCORE_WAVES + wave;
+    const int64_t h = (int64_t)bx * SCORE_WAVES + wave;
     const bool active = h < H;
     double f[9];
     int finite = 1;
@@ -288,8 +346,8 @@ int ransac_run(const double *x1, const double *x2, int64_t N, const int32_t *sam
     const int64_t slice = score_slice(H, N, &ny);
     if ((rc = launch_fit<M>(d1, d2, ds, H, dF, ny > 1 ? dcnt : nullptr, s))) return rc;
     SFM_HIP(hipEventRecord(c->ev[2], s));
-    hipLaunchKernelGGL(k_ransac_score<M>, dim3(ceil_div(H, SCORE_WAVES), ny), dim3(64 * SCORE_WAVES), 0, s, d1, d2,
-                       N, dF, H, thr, dcnt, slice);
+    hipLaunchKernelGGL((k_ransac_score<M, false>), dim3(ceil_div(H, SCORE_WAVES), ny), dim3(64 * SCORE_WAVES), 0, s,
+                       d1, d2, N, dF, H, thr, dcnt, slice, FitNext{});
     SFM_HIP(hipGetLastError());
     SFM_HIP(hipEventRecord(c->ev[3], s));
     hipLaunchKernelGGL(k_ransac_select<M>, dim3(1), dim3(1024), 0, s, d1, d2, N, dF, dcnt, H, thr, dbest, dFb, dmask);
@@ -349,6 +407,27 @@ static inline int64_t rp_next(int64_t h0, int64_t H) {
         return v > 0 ? (int64_t)v : RP_FIRST;
     }();
     static const bool ramp = std::getenv("SFM_RP_RAMP") && std::atoi(std::getenv("SFM_RP_RAMP"));
+    // SFM_RP_SCHEDULE="a,b,c": explicit chunk sizes, the last one repeated
+    static const std::vector<int64_t> sched = [] {
+        std::vector<int64_t> v;
+        if (const char *e = std::getenv("SFM_RP_SCHEDULE"))
+            for (const char *q = e; *q;) {
+                char *nx;
+                const long x = std::strtol(q, &nx, 10);
+                if (nx == q) break;
+                if (x > 0) v.push_back(x);
+                q = *nx ? nx + 1 : nx;
+            }
+        return v;
+    }();
+    if (!sched.empty()) {
+        int64_t pos = 0;
+        for (size_t k = 0;; ++k) {
+            const int64_t sz = sched[std::min(k, sched.size() - 1)];
+            if (pos + sz > h0) return std::min(H, pos + sz);
+            pos += sz;
+        }
+    }
     const int64_t chunk = rp_chunk();
     if (!ramp) return std::min(H, h0 + (h0 == 0 ? std::min(first, chunk) : chunk));
     int64_t size = std::min(first, chunk), pos = 0;
@@ -358,6 +437,75 @@ static inline int64_t rp_next(int64_t h0, int64_t H) {
     }
     return std::min(H, h0 + size);
 }
+
+// Fit + score of the drawn chunks.  With a group fit (EpiModel) a chunk's
+// score is enqueued only once the next chunk is drawn, and that launch fits
+// the next chunk in extra workgroups (FitNext): only the first chunk's fit
+// runs on its own.  SFM_RANSAC_FUSED=0 restores fit-then-score per chunk.
+static inline bool ransac_fused() {
+    static const bool on = [] {
+        const char *e = std::getenv("SFM_RANSAC_FUSED");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
+template <class M>
+struct ScorePipe {
+    const double2 *d1, *d2;
+    int64_t N;
+    double thr;
+    hipStream_t s;
+    double *dF;      // models of hypotheses off..: dF + 9 (h - off)
+    int32_t *dcnt;   // counts likewise
+    int64_t off;
+    int64_t pa = 0, pb = 0;  // the fitted, not yet scored piece
+    bool fused = M::GROUP_FIT && ransac_fused();
+
+    int score(int64_t a, int64_t b, const FitNext *fn) {
+        int ny;
+        const int64_t n = b - a, slice = score_slice(n, N, &ny);
+        const dim3 grid((unsigned)(ceil_div(n, SCORE_WAVES) + (fn ? fn->nfb : 0)), ny);
+        if constexpr (M::GROUP_FIT) {
+            if (fn) {
+                hipLaunchKernelGGL((k_ransac_score<M, true>), grid, dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
+                                   dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, *fn);
+                SFM_HIP(hipGetLastError());
+                return 0;
+            }
+        }
+        hipLaunchKernelGGL((k_ransac_score<M, false>), grid, dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
+                           dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, FitNext{});
+        SFM_HIP(hipGetLastError());
+        return 0;
+    }
+    // hypotheses [a, b), sample rows at rows (device-readable)
+    int add(int64_t a, int64_t b, const int32_t *rows) {
+        if (b <= a) return 0;
+        int ny, rc;
+        (void)score_slice(b - a, N, &ny);
+        int32_t *cz = ny > 1 ? dcnt + (a - off) : nullptr;
+        if (!fused) {
+            if ((rc = launch_fit<M>(d1, d2, rows, b - a, dF + (a - off) * 9, cz, s))) return rc;
+            return score(a, b, nullptr);
+        }
+        if (pb > pa) {
+            const FitNext fn{rows, b - a, dF + (a - off) * 9, cz, (int)ceil_div(b - a, FIT_PER_WG)};
+            if ((rc = score(pa, pb, &fn))) return rc;
+        } else if ((rc = launch_fit<M>(d1, d2, rows, b - a, dF + (a - off) * 9, cz, s))) {
+            return rc;
+        }
+        pa = a;
+        pb = b;
+        return 0;
+    }
+    int flush() {
+        int rc = 0;
+        if (pb > pa) rc = score(pa, pb, nullptr);
+        pa = pb = 0;
+        return rc;
+    }
+};
 
 template <class M>
 int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t *st, int64_t H, double thr,
@@ -406,20 +554,15 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
     if (tm) SFM_HIP(hipEventRecord(c->ev[1], s));
     PySampler ps(st, N, M::K);
     double t_draw = 0;
+    ScorePipe<M> pipe{d1, d2, N, thr, s, dF, dcnt, 0};
     for (int64_t h0 = 0, h1; h0 < H; h0 = h1) {
         h1 = rp_next(h0, H);
-        const int64_t nh = h1 - h0;
         const auto ta = std::chrono::steady_clock::now();
         ps.draw(h0, h1, hs);
         t_draw += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
-        int ny;
-        const int64_t slice = score_slice(nh, N, &ny);
-        if ((rc = launch_fit<M>(d1, d2, hs + h0 * M::K, nh, dF + h0 * 9, ny > 1 ? dcnt + h0 : nullptr, s)))
-            return rc;
-        hipLaunchKernelGGL(k_ransac_score<M>, dim3(ceil_div(nh, SCORE_WAVES), ny), dim3(64 * SCORE_WAVES), 0, s, d1,
-                           d2, N, dF + h0 * 9, nh, thr, dcnt + h0, slice);
-        SFM_HIP(hipGetLastError());
+        if ((rc = pipe.add(h0, h1, hs + h0 * M::K))) return rc;
     }
+    if ((rc = pipe.flush())) return rc;
     ps.save(st);
     if (tm) SFM_HIP(hipEventRecord(c->ev[3], s));
     hipLaunchKernelGGL(k_ransac_select<M>, dim3(1), dim3(1024), 0, s, d1, d2, N, dF, dcnt, H, thr, dbest, dFb, dmask);
@@ -515,20 +658,8 @@ int ransac_run_range(const double *x1, const double *x2, int64_t N, const int32_
     SFM_HIP(hipGetLastError());
     if (tm) SFM_HIP(hipEventRecord(c->ev[1], s));
     double t_draw = 0;
-    // fit + score the hypotheses [a, b) of the shard whose rows sit at rows
-    auto launch = [&](int64_t a, int64_t b, const int32_t *rows) -> int {
-        if (b <= a) return 0;
-        const int64_t n = b - a;
-        int ny;
-        const int64_t slice = score_slice(n, N, &ny);
-        int rc2;
-        if ((rc2 = launch_fit<M>(d1, d2, rows, n, dF + (a - r0) * 9, ny > 1 ? dcnt + (a - r0) : nullptr, s)))
-            return rc2;
-        hipLaunchKernelGGL(k_ransac_score<M>, dim3(ceil_div(n, SCORE_WAVES), ny), dim3(64 * SCORE_WAVES), 0, s, d1, d2,
-                           N, dF + (a - r0) * 9, n, thr, dcnt + (a - r0), slice);
-        SFM_HIP(hipGetLastError());
-        return 0;
-    };
+    // fit + score the hypotheses of the shard, hypothesis h at dF + 9 (h - r0)
+    ScorePipe<M> pipe{d1, d2, N, thr, s, dF, dcnt, r0};
     if (st) {
         PySampler ps(st, N, M::K);
         for (int64_t h0 = 0, h1; h0 < H; h0 = h1) {
@@ -537,13 +668,14 @@ int ransac_run_range(const double *x1, const double *x2, int64_t N, const int32_
             ps.draw(h0, h1, hs);
             t_draw += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
             const int64_t a = std::max(h0, r0), b = std::min(h1, r1);
-            if ((rc = launch(a, b, hs + a * M::K))) return rc;
+            if ((rc = pipe.add(a, b, hs + a * M::K))) return rc;
         }
         ps.save(st);
     } else {
         std::memcpy(hs, samples + r0 * M::K, sb);
-        if ((rc = launch(r0, r1, hs))) return rc;
+        if ((rc = pipe.add(r0, r1, hs))) return rc;
     }
+    if ((rc = pipe.flush())) return rc;
     if (tm) SFM_HIP(hipEventRecord(c->ev[3], s));
     if (nh > 0) {
         hipLaunchKernelGGL(k_ransac_select<M>, dim3(1), dim3(1024), 0, s, d1, d2, N, dF, dcnt, nh, thr, dbest, dFb,

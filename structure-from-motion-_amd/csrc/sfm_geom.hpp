@@ -339,6 +339,93 @@ __device__ __forceinline__ void f8_points(const double (&x1)[8], const double (&
     f8_finish(n, h1, h2, F_out);
 }
 
+// f8_points on a group of 8 consecutive lanes, lane i of the group holding
+// sample point i: the same operations in the same order, with one
+// design-matrix row per lane.  The compiler contracts some products into
+// FMAs differently in the two forms, so F can differ from f8_points in the
+// last bits (tools/fit_group_check.hip); every RANSAC path therefore fits F
+// with this one, and the batch entry (sfm_f8_batch) with f8_points.  The Hartley sums gather the group's
+// values by shuffles in point order; reflector k (row k's lane) and its tau
+// are broadcast to the group for the rows below and again for the
+// back-substitution, which every lane runs on its own copy of n.  ~60 VGPRs
+// against the one-thread fit's 136, so it can share a launch with the score.
+// Lane 0 of the group writes F_out.
+__device__ __forceinline__ double hartley_sum8(double v) {
+    double s = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += __shfl(v, k, 8);
+    return s;
+}
+
+__device__ __forceinline__ Hartley hartley8_group(double x, double y) {
+    const double mx = hartley_sum8(x) / 8.0, my = hartley_sum8(y) / 8.0;
+    const double ax = x - mx, ay = y - my;
+    const double d = hartley_sum8(sqrt(ax * ax + ay * ay));
+    Hartley h;
+    h.s = 1.4142135623730951 / (d / 8.0 + 1e-8);
+    h.ox = -h.s * mx;
+    h.oy = -h.s * my;
+    return h;
+}
+
+__device__ __forceinline__ void f8_points_group8(double px, double py, double qx, double qy, double *F_out) {
+    const int i = threadIdx.x & 7;
+    const Hartley h1 = hartley8_group(px, py), h2 = hartley8_group(qx, qy);
+    double A[9];
+    {
+        const double a = h1.s * px + h1.ox, b = h1.s * py + h1.oy;
+        const double c = h2.s * qx + h2.ox, d = h2.s * qy + h2.oy;
+        A[0] = a * c; A[1] = a * d; A[2] = a;
+        A[3] = b * c; A[4] = b * d; A[5] = b;
+        A[6] = c; A[7] = d; A[8] = 1.0;
+    }
+    double tau = 0;  // this lane's reflector (row i)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        if (i == k) {
+            double nrm2 = 0;
+#pragma unroll
+            for (int j = k; j < 9; ++j) nrm2 += A[j] * A[j];
+            const double nrm = sqrt(nrm2);
+            const double alpha = A[k] > 0 ? -nrm : nrm;
+            A[k] -= alpha;
+            double vtv = 0;
+#pragma unroll
+            for (int j = k; j < 9; ++j) vtv += A[j] * A[j];
+            tau = nrm2 > 0 ? 2.0 / vtv : 0.0;
+        }
+        double v[9];
+#pragma unroll
+        for (int j = k; j < 9; ++j) v[j] = __shfl(A[j], k, 8);
+        const double tk = __shfl(tau, k, 8);
+        if (i > k) {
+            double d = 0;
+#pragma unroll
+            for (int j = k; j < 9; ++j) d += A[j] * v[j];
+            d *= tk;
+#pragma unroll
+            for (int j = k; j < 9; ++j) A[j] -= d * v[j];
+        }
+    }
+    double n[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) n[j] = (j == 8) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 7; k >= 0; --k) {
+        double v[9];
+#pragma unroll
+        for (int j = k; j < 9; ++j) v[j] = __shfl(A[j], k, 8);
+        const double tk = __shfl(tau, k, 8);
+        double d = 0;
+#pragma unroll
+        for (int j = k; j < 9; ++j) d += v[j] * n[j];
+        d *= tk;
+#pragma unroll
+        for (int j = k; j < 9; ++j) n[j] -= d * v[j];
+    }
+    if (i == 0) f8_finish(n, h1, h2, F_out);
+}
+
 // ------------------------------------------------------------ homography
 // find_homography (GetHomographyInliers.py:4-85).  numpy's 3x3 @ 3xN and
 // 3x3 @ 3x3 products run through OpenBLAS dgemm, whose accumulation is an
