@@ -10,7 +10,7 @@ update) becomes one batched evaluation on the MI355X:
    while the GPU scores the chunks already drawn, and written back with
    setstate), so the stream seen by later callers (PnPRANSAC, the next image
    pair) is unchanged;
-2. libsfmcore builds every hypothesis F (one thread each), scores every
+2. libsfmcore builds every hypothesis F (8 lanes each, the next chunk's fits riding in the current chunk's score launch), scores every
    (hypothesis, correspondence) pair (one wavefront per hypothesis, LDS
    tiles, ballot popcount) and picks the first hypothesis with the strictly
    largest count -- the reference's tie rule (:85-88).
