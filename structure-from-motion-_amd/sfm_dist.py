@@ -9,7 +9,14 @@
   applied across ranks, found as the max of a packed 64-bit key.  The sample
   table is drawn whole, in the reference's order, on every rank (the global
   random stream ends where the unsharded call leaves it).
-* LinearTriangulation: contiguous point ranges, no collective.
+* LinearTriangulation: contiguous point ranges, no collective; the ranges
+  are gathered in rank order (triangulate_sharded).
+* Image pairs: the driver's pair loop (Wrapper_dev.py:67-123) spread over
+  ranks (pair_loop_spread).  Every rank replays the global random stream
+  through the whole loop -- each pair's homography RANSAC, then the draw of
+  its F sample table -- because the F table's N is the homography inlier
+  count and every draw shifts the stream for the next pair; the F-RANSACs,
+  scored from the drawn tables, are split round-robin over the ranks.
 """
 import numpy as np
 
@@ -91,3 +98,85 @@ def point_shard(n, world, rank):
     """Contiguous point range of LinearTriangulation sharding (no collective:
     every range is independent; the caller gathers)."""
     return point_range(n, world, rank)
+
+
+def allgather_torch(obj, group=None):
+    """Every rank's obj, in rank order, over a torch.distributed group (gloo
+    on the CPU tests; objects are small: point ranges, per-pair results)."""
+    import torch.distributed as dist
+    out = [None] * dist.get_world_size(group)
+    dist.all_gather_object(out, obj, group=group)
+    return out
+
+
+def triangulate_sharded(tri_fn, x1, x2, world, rank, allgather):
+    """LinearTriangulation over contiguous point ranges: this
+    rank triangulates points [lo, hi) with tri_fn(x1[lo:hi], x2[lo:hi]) ->
+    (hi - lo, 3); allgather(piece) returns every rank's piece in rank order.
+    Points are independent, so the concatenation is the unsharded result."""
+    lo, hi = point_shard(len(x1), world, rank)
+    X = np.asarray(tri_fn(x1[lo:hi], x2[lo:hi]), dtype=np.float64).reshape(hi - lo, 3)
+    return np.concatenate([np.asarray(p).reshape(-1, 3) for p in allgather(X)])
+
+
+def f_ransac_from_table(core, points1, points2, index, samples, threshold=0.06):
+    """get_inliers_ransac's result (Phase 1/GetInliersRANSAC.py:109-121) from
+    a pre-drawn sample table (the draws happened elsewhere, in the stream's
+    order).  samples is None when the reference would not draw (N < 8)."""
+    index = np.asarray(index)
+    if samples is None or len(samples) == 0:
+        return None, np.array([])
+    points1 = np.asarray(points1, dtype=np.float64).reshape(-1, 2)
+    points2 = np.asarray(points2, dtype=np.float64).reshape(-1, 2)
+    best, F, mask, _ = core.ransac_f8(points1, points2, samples, threshold)
+    if best < 0:
+        return None, np.array([])
+    return F, index[np.where(mask)[0]]
+
+
+def pair_loop_plan(pairs, f_points, homography, draw_table, n_max=1000):
+    """The replicated part of pair_loop_spread: every pair's homography
+    RANSAC and F sample table, in the driver's order, on the global stream.
+    Returns [(H, h_idx, points1, points2, table or None)]."""
+    n_iter = max(int(n_max), 0)
+    plan = []
+    for k, (x1, x2, index) in enumerate(pairs):
+        H, h_idx = homography(x1, x2, index)
+        p1, p2 = f_points(k, h_idx)
+        n = len(p1)
+        plan.append((H, h_idx, p1, p2, draw_table(n, n_iter) if (n >= 8 and n_iter > 0) else None))
+    return plan
+
+
+def pair_loop_local(plan, world, rank, f_ransac):
+    """This rank's F-RANSACs: pairs k with k % world == rank -> {k: (F, f_idx)}."""
+    return {k: f_ransac(p1, p2, h_idx, table)
+            for k, (_, h_idx, p1, p2, table) in enumerate(plan) if k % world == rank}
+
+
+def pair_loop_merge(plan, parts):
+    """[(H, h_idx, F, f_idx)] for all pairs from every rank's local dict."""
+    merged = {}
+    for part in parts:
+        merged.update(part)
+    return [(H, h_idx) + tuple(merged[k]) for k, (H, h_idx, _, _, _) in enumerate(plan)]
+
+
+def pair_loop_spread(pairs, f_points, world, rank, homography, draw_table, f_ransac, allgather, n_max=1000):
+    """The pair loop of Wrapper_dev.py:67-123 with the F-RANSACs spread over
+    ranks.
+
+    pairs[k] = (x1, x2, index): pair k's homography inputs, in the driver's
+    order.  f_points(k, h_idx) -> (points1, points2) of pair k's F-RANSAC.
+    homography(x1, x2, index) -> (H, h_idx) consumes the global random stream
+    (get_homography_inliers).  draw_table(N, n_iter) draws pair k's F table
+    from the same stream exactly as GetInliersRANSAC's loop would
+    (sample_table; nothing for N < 8 or n_iter = 0).  f_ransac(points1,
+    points2, h_idx, table) -> (F, f_idx) scores it (f_ransac_from_table).
+    Every rank runs the homography chain and draws every table -- so the
+    stream leaves the loop where the sequential driver leaves it -- and
+    scores the F-RANSACs of the pairs k with k % world == rank;
+    allgather(dict) returns every rank's dict in rank order.  Returns
+    [(H, h_idx, F, f_idx)] for all pairs."""
+    plan = pair_loop_plan(pairs, f_points, homography, draw_table, n_max)
+    return pair_loop_merge(plan, allgather(pair_loop_local(plan, world, rank, f_ransac)))

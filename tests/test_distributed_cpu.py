@@ -8,7 +8,10 @@ runs on two gloo ranks and must equal the single-process system; a full
 distributed LM loop must reproduce the single-process oracle's converged
 cost.  RANSAC hypothesis sharding runs sfm_dist.ransac_sharded with the
 packed-key combine over gloo and must give the unsharded winner, model and
-mask.
+mask.  LinearTriangulation point ranges (sfm_dist.triangulate_sharded) and
+the image-pair spread (sfm_dist.pair_loop_spread: homography chain and F
+tables replicated, F-RANSACs round-robin) are gathered over gloo and must
+equal the single-process results and random-stream state.
 """
 import os
 import random
@@ -96,6 +99,63 @@ def partial_system(R, t, X, cam, pt, obs, nc, lam):
     return dict(S=S, diagU=diagU, gc=gc, bZ=bZ, cost=cost, V=V, gp=gp, Vi=Vi, W=W, Jc=Jc, Jp=Jp)
 
 
+# stand-ins with the reference's RNG use (GetHomographyInliers.py:124-126,
+# GetInliersRANSAC.py:53-55) and the oracle as the fit/score
+N_PAIR_ITERS = 60
+
+
+def _tri_inputs():
+    _, _, _, m = syn.two_view(n=301, seed=5)
+    return m["clean1"], m["clean2"]
+
+
+def _tri_fn(a, b):
+    _, _, _, m = syn.two_view(n=301, seed=5)
+    return O.triangulate(syn.K_REF, np.zeros(3), np.eye(3), m["C2"], m["R2"], a, b)
+
+
+def _pair_inputs():
+    pairs, pts = [], []
+    for k, n in enumerate((150, 7, 120, 90)):  # pair 1 has too few matches for any draw
+        a, b, _, _ = syn.two_view(n=n, seed=20 + k)
+        pairs.append((a, b, np.arange(n, dtype=np.int64) * 3 + k))
+        pts.append((a, b))
+    return pairs, (lambda k, h_idx: (pts[k][0][(h_idx - k) // 3], pts[k][1][(h_idx - k) // 3]))
+
+
+def _homography(x1, x2, index):
+    n = len(x1)
+    if n < 4:
+        return None, np.array([])
+    table = np.array([random.sample(range(n), 4) for _ in range(N_PAIR_ITERS)], dtype=np.int32)
+    b, _, Hm, m = O.ransac_h(x1, x2, table, 30.0)
+    return (Hm, index[m]) if b >= 0 else (None, np.array([], dtype=np.int64))
+
+
+def _draw_f_table(n, n_iter):
+    return np.array([random.sample(range(n), 8) for _ in range(n_iter)], dtype=np.int32)
+
+
+def _f_ransac(p1, p2, h_idx, table):
+    if table is None:
+        return None, np.array([])
+    b, _, F, m = O.ransac(p1, p2, table, 0.06)
+    return (F, h_idx[m]) if b >= 0 else (None, np.array([]))
+
+
+def _pair_loop_sequential():
+    """The reference driver's order: homography RANSAC, then F-RANSAC, pair by pair."""
+    random.seed(11)
+    pairs, f_points = _pair_inputs()
+    out = []
+    for k, (x1, x2, index) in enumerate(pairs):
+        Hm, h_idx = _homography(x1, x2, index)
+        p1, p2 = f_points(k, h_idx)
+        table = _draw_f_table(len(p1), N_PAIR_ITERS) if len(p1) >= 8 else None
+        out.append((Hm, h_idx) + _f_ransac(p1, p2, h_idx, table))
+    return out, random.getstate()
+
+
 def _rank_main(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -125,7 +185,14 @@ def _rank_main(rank, world, port, q):
 
         it, F, mask = sfm_dist.ransac_sharded(len(x1), H_RANSAC, rank, world, shard_fn,
                                               sfm_dist.combine_keys_torch, lambda M: O.ransac_mask(x1, x2, M, 0.06))
-        q.put((rank, payload.numpy(), (it, F, mask, st_after)))
+        # LinearTriangulation over point ranges, gathered over gloo
+        Xt = sfm_dist.triangulate_sharded(_tri_fn, *_tri_inputs(), world, rank, sfm_dist.allgather_torch)
+        # image pairs: the homography chain and the F tables on every rank,
+        # the F-RANSACs round-robin, the results gathered over gloo
+        random.seed(11)
+        spread = sfm_dist.pair_loop_spread(*_pair_inputs(), world, rank, _homography, _draw_f_table, _f_ransac,
+                                           sfm_dist.allgather_torch, n_max=N_PAIR_ITERS)
+        q.put((rank, payload.numpy(), (it, F, mask, st_after), Xt, (spread, random.getstate())))
     finally:
         dist.destroy_process_group()
 
@@ -151,12 +218,23 @@ def test_sharded_reduced_system_equals_full_gloo():
     x1, x2, _, _ = syn.two_view(n=400, seed=4)
     random.seed(7)
     table = np.array([random.sample(range(400), 8) for _ in range(H_RANSAC)], dtype=np.int32)
+    st_ref = random.getstate()
     b_ref, _, F_ref, mask_ref = O.ransac(x1, x2, table, 0.06)
     assert b_ref >= 0
-    for rank, payload, (it, F, mask, st_after) in out:
+    X_ref = _tri_fn(*_tri_inputs())
+    seq, st_seq = _pair_loop_sequential()
+    assert any(r[2] is not None for r in seq) and seq[1][2] is None
+    for rank, payload, (it, F, mask, st_after), Xt, (spread, st_spread) in out:
         assert np.allclose(payload, ref, rtol=1e-10, atol=1e-9 * np.abs(ref).max())
         assert it == b_ref and np.array_equal(F, F_ref) and np.array_equal(mask, mask_ref)
-        assert st_after == random.getstate()  # every rank's stream ends where the unsharded draw leaves it
+        assert st_after == st_ref  # every rank's stream ends where the unsharded draw leaves it
+        assert np.array_equal(Xt, X_ref)
+        assert st_spread == st_seq  # every rank's stream ends where the sequential loop leaves it
+        assert len(spread) == len(seq)
+        for (H1, h1, F1, f1), (H2, h2, F2, f2) in zip(spread, seq):
+            assert (H1 is None) == (H2 is None) and (H1 is None or np.array_equal(H1, H2))
+            assert np.array_equal(h1, h2) and np.array_equal(f1, f2)
+            assert (F1 is None) == (F2 is None) and (F1 is None or np.array_equal(F1, F2))
 
 
 def distributed_lm(shards, nc, iters=30, lam=1e-4):

@@ -402,6 +402,73 @@ def test_p3data_pair_loop_homography_then_f(core, golden, seed):
         assert np.array_equal(np.asarray(f_idx, dtype=np.int64), p[key + "_inlier_idx"]), key
 
 
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_p3data_pair_loop_spread_over_ranks(core, golden, world):
+    """Image-pair spreading (sfm_dist.pair_loop_spread): every
+    rank replays the homography chain and draws every F table on the global
+    stream, then scores its round-robin share of the 10 F-RANSACs from the
+    drawn tables.  Ranks run one after another here (each from the same
+    seed, as separate processes would); every rank's stream ends where the
+    reference's sequential loop leaves it, and the merged H / F inlier sets
+    equal the reference's (Wrapper_dev.py:67-123)."""
+    import functools
+    import sfm_dist
+    from GetHomographyInliers import get_homography_inliers
+    from itertools import combinations
+    g, p = golden("homography.npz"), golden("ransac_p3data.npz")
+    fx, fy = p["feature_x"], p["feature_y"]
+    seed = 0
+    keys = [f"s{seed}_{a}_{b}" for (a, b) in combinations(range(1, 6), 2)]
+    ab = list(combinations(range(1, 6), 2))
+    pairs = [(g[k + "_x1"], g[k + "_x2"], g[k + "_index"]) for k in keys]
+
+    def f_points(k, h_idx):
+        a, b = ab[k]
+        return (np.hstack((fx[h_idx, a - 1].reshape((-1, 1)), fy[h_idx, a - 1].reshape((-1, 1)))),
+                np.hstack((fx[h_idx, b - 1].reshape((-1, 1)), fy[h_idx, b - 1].reshape((-1, 1)))))
+
+    homography = functools.partial(get_homography_inliers, threshold=30, n_max=1000)
+    f_ransac = functools.partial(sfm_dist.f_ransac_from_table, core, threshold=0.06)
+    plans, parts = [], []
+    for rank in range(world):
+        random.seed(seed)
+        plan = sfm_dist.pair_loop_plan(pairs, f_points, homography, lambda n, it: core.sample_table(n, 8, it))
+        assert np.array_equal(_state_array(), p[keys[-1] + "_state_after"])
+        plans.append(plan)
+        parts.append(sfm_dist.pair_loop_local(plan, world, rank, f_ransac))
+    assert sorted(k for part in parts for k in part) == list(range(len(pairs)))
+    for rank in range(world):
+        out = sfm_dist.pair_loop_merge(plans[rank], parts)
+        for k, (H, h_idx, F, f_idx) in zip(keys, out):
+            assert rel(H, g[k + "_H"]) < 1e-9, k
+            assert np.array_equal(h_idx, g[k + "_inlier_idx"]), k
+            assert np.array_equal(np.asarray(f_idx, dtype=np.int64), p[k + "_inlier_idx"]), k
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_triangulation_sharded_equals_whole(core, world):
+    """LinearTriangulation over contiguous point ranges (sfm_dist.
+    triangulate_sharded): the ranges gathered in rank order are bitwise the
+    single call's result (points are independent)."""
+    import sfm_dist
+    _, _, _, m = syn.two_view(n=20_001, seed=6)
+    x1, x2 = m["clean1"], m["clean2"]
+    P1 = O.projection(K, np.zeros(3), np.eye(3))
+    P2 = O.projection(K, m["C2"], m["R2"])
+    whole = core.triangulate(P1, P2, x1, x2)
+    pieces = [None] * world
+
+    def tri(a, b):
+        return core.triangulate(P1, P2, a, b)
+
+    for rank in range(world):  # the gather returns the pieces computed so far; the last rank sees all
+        lo, hi = sfm_dist.point_shard(len(x1), world, rank)
+        pieces[rank] = tri(x1[lo:hi], x2[lo:hi])
+    X = sfm_dist.triangulate_sharded(tri, x1, x2, world, world - 1,
+                                     lambda mine: [pc if r < world - 1 else mine for r, pc in enumerate(pieces)])
+    assert np.array_equal(X, whole)
+
+
 def test_homography_ransac_edge_cases(core):
     from GetHomographyInliers import get_homography_inliers
     random.seed(3)
