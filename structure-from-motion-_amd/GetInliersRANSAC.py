@@ -47,9 +47,11 @@ def GetInliersRANSAC(points1, points2, index, threshold=0.06, n_max=1000):
     F_best : numpy.ndarray
         the best fundamental matrix
     """
-    points1 = np.array(points1)
-    points2 = np.array(points2)
-    index = np.array(index)
+    # np.asarray: the reference's np.array(...) (:32-34) without the copy
+    # (the inputs are only read)
+    points1 = np.asarray(points1)
+    points2 = np.asarray(points2)
+    index = np.asarray(index)
     n_points = len(points1)
     if n_points < 8:  # :38-40
         return np.array([]), index, None
