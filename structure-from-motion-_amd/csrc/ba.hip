@@ -1127,44 +1127,47 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// One row segment of tile k's rows per lane and register: lanes [0, TB) hold
+// the diagonal tile's column (q[m] = L[k0+m][k0+lane]), lanes [TB, 2 TB) the
+// block left of it (q[m] = L[k0+m][k0-TB+lane-TB], tile k's contribution to
+// tile k-1): one 2 TB-wide load per row instead of two loads, and the pivot
+// L[k0+li][k0+li] is q[li] of lane li (no load of its own).
 template <int TB>
 struct ChainOps {
-    double c[TB];  // L[k0+m][k0+li]       (the diagonal tile, column li)
-    double p[TB];  // L[k0+m][k0-TB+li]    (tile k's block left of it: contribution to tile k-1)
-    double d;      // L[k0+li][k0+li]
+    double q[TB];
 };
 
 template <int TB>
 __device__ __forceinline__ void chain_fetch(ChainOps<TB> &o, const double *__restrict__ A, int32_t nsp, int kt,
-                                            int li) {
-    const int kb = kt >= 0 ? kt * TB : 0, pc = kb >= TB ? kb - TB + li : 0;
+                                            int lane) {
+    const int kb = kt >= 0 ? kt * TB : 0;
+    const int col = lane < TB ? kb + lane : (lane < 2 * TB && kb >= TB) ? kb - 2 * TB + lane : kb;
+    const double *row = A + (int64_t)kb * nsp + col;
 #pragma unroll
-    for (int m = 0; m < TB; ++m) {
-        const double *row = A + (int64_t)(kb + m) * nsp;
-        o.c[m] = row[kb + li];
-        o.p[m] = row[pc];
-    }
-    o.d = A[(int64_t)(kb + li) * nsp + kb + li];
+    for (int m = 0; m < TB; ++m) o.q[m] = row[(int64_t)m * nsp];
 }
 
 template <int TB>
 __device__ __forceinline__ void chain_step(ChainOps<TB> &o, const double *__restrict__ A, int32_t nsp, int kt,
                                            double *x, double &acc, int lane, int li) {
     const int k0 = kt * TB;
-    const double rinv = 1.0 / o.d;  // off the chain
+    double d = o.q[0];
+#pragma unroll
+    for (int m = 1; m < TB; ++m) d = (li == m) ? o.q[m] : d;
+    const double rinv = 1.0 / d;  // off the chain
     double v = x[k0 + li] - acc;
 #pragma unroll
     for (int j = TB - 1; j >= 0; --j) {
         const double vj = readlane_f64(v, j) * readlane_f64(rinv, j);
         if (lane == j) v = vj;
-        if (lane < j) v -= o.c[j] * vj;
+        if (lane < j) v -= o.q[j] * vj;
     }
     if (lane < TB) x[k0 + lane] = v;
-    double a = 0;
+    double a = 0;  // lanes [TB, 2 TB): L[k0+m][k0-TB+lane-TB] x[k0+m] for the row lane - TB of tile k-1
 #pragma unroll
-    for (int m = 0; m < TB; ++m) a += o.p[m] * readlane_f64(v, m);  // L[k0+m][k0-TB+li] x[k0+m]
-    acc = a;
-    chain_fetch<TB>(o, A, nsp, kt - 2, li);
+    for (int m = 0; m < TB; ++m) a += o.q[m] * readlane_f64(v, m);
+    acc = __shfl(a, (lane + TB) & 63);
+    chain_fetch<TB>(o, A, nsp, kt - 2, lane);
     lds_barrier();
 }
 
@@ -1252,11 +1255,11 @@ __global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(double *__rest
     if (t < 64) {  // chain wave
         const int lane = t, li = lane < TB ? lane : TB - 1;
         ChainOps<TB> oa, ob;
-        chain_fetch<TB>(oa, A, nsp, nT - 1, li);
+        chain_fetch<TB>(oa, A, nsp, nT - 1, lane);
+        if (lane < TB)  // the last diagonal factor is still in the step kernel's scratch
 #pragma unroll
-        for (int m = 0; m < TB; ++m) oa.c[m] = Dlast[m * TB + li];  // the last diagonal factor is
-        oa.d = Dlast[li * TB + li];                                 // still in the step kernel's scratch
-        chain_fetch<TB>(ob, A, nsp, nT - 2, li);
+            for (int m = 0; m < TB; ++m) oa.q[m] = Dlast[m * TB + lane];
+        chain_fetch<TB>(ob, A, nsp, nT - 2, lane);
         double acc = 0;
         lds_barrier();  // x staged
         int kt = nT - 1;
