@@ -46,6 +46,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <utility>
 #include <numeric>
 #include <vector>
 
@@ -959,6 +960,84 @@ __device__ __forceinline__ void chol_factor(double (&r)[TB], double (&dinv)[TB],
     }
 }
 
+// lane j of each 16-lane row of the wave, to the whole row: one
+// v_mov_b64_dpp row_newbcast (DPP64), no SGPR round trip
+template <int J>
+__device__ __forceinline__ double bcast16_c(double v) {
+    return __longlong_as_double(
+        __builtin_amdgcn_update_dpp(0ll, __double_as_longlong(v), 0x150 + J, 0xF, 0xF, true));
+}
+__device__ __forceinline__ double bcast16(double v, int j) {  // j a constant after unrolling
+    switch (j) {
+    case 0: return bcast16_c<0>(v);   case 1: return bcast16_c<1>(v);   case 2: return bcast16_c<2>(v);
+    case 3: return bcast16_c<3>(v);   case 4: return bcast16_c<4>(v);   case 5: return bcast16_c<5>(v);
+    case 6: return bcast16_c<6>(v);   case 7: return bcast16_c<7>(v);   case 8: return bcast16_c<8>(v);
+    case 9: return bcast16_c<9>(v);   case 10: return bcast16_c<10>(v); case 11: return bcast16_c<11>(v);
+    case 12: return bcast16_c<12>(v); case 13: return bcast16_c<13>(v); case 14: return bcast16_c<14>(v);
+    default: return bcast16_c<15>(v);
+    }
+}
+
+// r_j += bcast_j(rk) * nrk and p_j += bcast_j(rk) * npk, two v_fmac_f64 with
+// a row_newbcast:j source (DPP64).  Inline asm, so the panel updates stay in
+// the pivot step that produces their operand (the compiler otherwise sinks
+// them to the end and holds the 120 broadcasts in registers); NOP = 1 puts
+// the two wait states a DPP read of a just-written VGPR needs in front.
+template <int J, int NOP>
+__device__ __forceinline__ void fmac2_bc(double &rj, double &pj, double rk, double nrk, double npk) {
+    if constexpr (NOP)
+        asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %2, %3 row_newbcast:%5 row_mask:0xf bank_mask:0xf\n\t"
+                     "v_fmac_f64_dpp %1, %2, %4 row_newbcast:%5 row_mask:0xf bank_mask:0xf"
+                     : "+v"(rj), "+v"(pj) : "v"(rk), "v"(nrk), "v"(npk), "n"(J));
+    else
+        asm volatile("v_fmac_f64_dpp %0, %2, %3 row_newbcast:%5 row_mask:0xf bank_mask:0xf\n\t"
+                     "v_fmac_f64_dpp %1, %2, %4 row_newbcast:%5 row_mask:0xf bank_mask:0xf"
+                     : "+v"(rj), "+v"(pj) : "v"(rk), "v"(nrk), "v"(npk), "n"(J));
+}
+template <int J>
+__device__ __forceinline__ double bcast16_asm(double v) {  // s_nop: v may have just been written
+    double d;
+    asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+                 : "=v"(d) : "v"(v), "n"(J));
+    return d;
+}
+template <int K, int... I>
+__device__ __forceinline__ void chol16_updates(double (&r)[16], double (&p)[16], std::integer_sequence<int, I...>) {
+    const double nrk = -r[K], npk = -p[K];
+    (fmac2_bc<K + 1 + I, I == 0>(r[K + 1 + I], p[K + 1 + I], r[K], nrk, npk), ...);
+}
+
+// The same factor for TB = 16 with the broadcasts inside 16-lane DPP rows:
+// every row of the wave holds C_ss (r[j] = element (li, j), li = lane & 15)
+// and one row of the panel (p[j] = C_rs element (li, j)).  Step k scales
+// column k by 1/L_kk and subtracts L_jk (lane j's r[k], one row_newbcast)
+// times it from columns j > k, in r and p alike: the operation order of
+// chol_factor, so L_ss and L_rs = C_rs L_ss^-T are bitwise the same.
+template <int K>
+__device__ __forceinline__ void chol16_step(double (&r)[16], double (&p)[16], double (&dinv)[16], int li,
+                                            bool &nonpos) {
+    const double d = bcast16_asm<K>(r[K]);
+    nonpos |= !(d > 0.0);
+    double g = __builtin_amdgcn_rsq(d);
+    g = g * (1.5 - 0.5 * d * g * g);
+    g = g * (1.5 - 0.5 * d * g * g);
+    dinv[K] = g;
+    r[K] = (li == K) ? d * g : r[K] * g;
+    p[K] = p[K] * g;
+    if constexpr (K < 15) chol16_updates<K>(r, p, std::make_integer_sequence<int, 15 - K>{});
+}
+template <int... K>
+__device__ __forceinline__ void chol16_steps(double (&r)[16], double (&p)[16], double (&dinv)[16], int li,
+                                             bool &nonpos, std::integer_sequence<int, K...>) {
+    (chol16_step<K>(r, p, dinv, li, nonpos), ...);
+}
+__device__ __forceinline__ void chol_factor16(double (&r)[16], double (&p)[16], double (&dinv)[16], int li,
+                                              int lane, int *bad) {
+    bool nonpos = false;  // one store after the chain: no branch (and basic block) per pivot
+    chol16_steps(r, p, dinv, li, nonpos, std::make_integer_sequence<int, 16>{});
+    if (lane == 0 && nonpos) *bad = 1;
+}
+
 // element (i, j) of the damped, identity-padded system S + lambda clamp(diag U)
 // read straight from the Schur payload (launch 0 assembles as it loads)
 __device__ __forceinline__ double assembled(const double *__restrict__ payload, int32_t ns, double lambda, int i,
@@ -981,7 +1060,7 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
                                                   double *__restrict__ D, double *__restrict__ bvec,
                                                   int *__restrict__ bad, const double *__restrict__ payload,
                                                   int32_t ns, const double *__restrict__ lam,
-                                                  const int *__restrict__ gate) {
+                                                  const int *__restrict__ gate, int dpp) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
     const double lambda = s == 0 ? *lam : 0.0;
     __shared__ double Lr[TB][TB + 1], Lc[TB][TB + 1], Ct[TB][TB + 1], Cd[TB][TB + 1];
@@ -1060,8 +1139,52 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
     __syncthreads();
     if (t >= 64) return;
     const int lane = t;
-    const int li = lane < TB ? lane : TB - 1;
     double (*Cdd)[TB + 1] = (r > s) ? Cd : Ct;
+    if constexpr (TB == 16) {
+        if (dpp) {  // every 16-lane row: C_ss row li in rw, C_rs row li in pw
+            const int li = lane & 15;
+            double rw[16], pw[16], dinv[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                rw[j] = Cdd[li][j];
+                pw[j] = Ct[li][j];
+            }
+            chol_factor16(rw, pw, dinv, li, lane, bad);
+            if (r == s) {
+                double y = upd ? bvec[s0 + li] : assembled_b(payload, ns, li);
+                if (upd) {
+                    double acc = 0;
+#pragma unroll
+                    for (int m = 0; m < TB; ++m) acc += Lc[li][m] * bvec[kp + m];
+                    y -= acc;
+                }
+#pragma unroll
+                for (int j = 0; j < TB; ++j) {
+                    const double yj = bcast16(y, j) * dinv[j];
+                    if (li == j) y = yj;
+                    if (li > j) y -= rw[j] * yj;
+                }
+                if (lane < TB) {
+                    bvec[s0 + lane] = y;
+                    double *Dn = D + (s & 1) * TB * TB;
+#pragma unroll
+                    for (int j = 0; j < TB; ++j) Dn[lane * TB + j] = j <= lane ? rw[j] : 0.0;
+                }
+                return;
+            }
+            wave_sync_lds();
+            if (lane < TB)
+#pragma unroll
+                for (int j = 0; j < TB; ++j) Lr[lane][j] = pw[j];
+            wave_sync_lds();
+            for (int e = lane; e < TB * TB; e += 64)
+                A[(int64_t)(r0 + e / TB) * nsp + s0 + e % TB] = Lr[e / TB][e % TB];
+            for (int e = lane; e < TB * TB; e += 64)  // mirror into the upper triangle
+                A[(int64_t)(s0 + e / TB) * nsp + r0 + e % TB] = Lr[e % TB][e / TB];
+            return;
+        }
+    }
+    const int li = lane < TB ? lane : TB - 1;
     // lanes [0, TB) hold the rows of C_ss; in a panel block lanes [TB, 2 TB)
     // hold the rows of C_rs.  The right-looking factor step (scale column k
     // by 1/L_kk, subtract L_jk times it from column j > k) is also the
@@ -1432,6 +1555,16 @@ static int lanes_per_point(const char *env, int dflt) {
     return (g == 1 || g == 2 || g == 4 || g == 8) ? g : dflt;
 }
 
+// DPP row broadcasts in the tile factor (default); SFM_CHOL_DPP=0 selects
+// the readlane chain, for same-box A/B
+static int chol_dpp() {
+    static const int v = [] {
+        const char *e = std::getenv("SFM_CHOL_DPP");
+        return e ? std::atoi(e) != 0 : 1;
+    }();
+    return v;
+}
+
 // Factor + forward solve (nT launches of k_chol_col) and backward solve of
 // the padded reduced camera system with tiles of tb (16 or 32) columns; A, b
 // on the device, D = 2 tb^2 scratch; nsp a multiple of tb.
@@ -1442,7 +1575,7 @@ static int launch_cholesky_t(const double *payload, int32_t ns, const double *la
     for (int st = 0; st < nT; ++st) {
         const int T = nT - st;
         hipLaunchKernelGGL(k_chol_col<TB>, dim3(T * (T + 1) / 2 + (st >= 1 ? 1 : 0)), dim3(256), 0, s, A, nsp, st, D,
-                           b, bad, payload, ns, lam, gate);
+                           b, bad, payload, ns, lam, gate, chol_dpp());
         SFM_HIP(hipGetLastError());
     }
     hipLaunchKernelGGL(k_chol_backsolve<TB>, dim3(1), dim3(SOLVE_THREADS), 0, s, A, nsp, b,
