@@ -1055,12 +1055,67 @@ __device__ __forceinline__ double assembled_b(const double *__restrict__ payload
     return i < ns ? -payload[base + ns + i] + payload[base + 2 * ns + i] : 0.0;
 }
 
+// One rank, no all-reduce between the sweep and the solve: launch 0 reads the
+// system straight from the sweep's per-range slabs (k_schur_finish's sums, in
+// its order, so bitwise the same values) and one extra workgroup writes the
+// payload's vectors for the back substitution's epilogue; no finish launch.
+struct SlabSrc {
+    const double *slab, *camlin;  // slab == nullptr: read the finished payload
+    int32_t nbd, nrange;
+};
+
+__device__ __forceinline__ double slab_sum(const SlabSrc &q, int64_t blk, int item) {
+    double v = 0;
+    const int64_t stride = (int64_t)q.nbd * ITEM_W;
+    const double *src = q.slab + blk * ITEM_W + item;
+    for (int r0 = 0; r0 < q.nrange; r0 += 8) {  // 8 loads in flight, then the sum in range order
+        double x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = r0 + u < q.nrange ? src[(r0 + u) * stride] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (r0 + u < q.nrange) v += x[u];
+    }
+    return v;
+}
+
+__device__ __forceinline__ double cam_u(const double *__restrict__ camlin, int c, int r, int k) {
+    const int lo = r < k ? r : k, hi = r < k ? k : r;
+    return camlin[CAMLIN * c + lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];
+}
+
+__device__ __forceinline__ double assembled_src(const SlabSrc &q, const double *__restrict__ payload, int32_t ns,
+                                                double lambda, int i, int j) {
+    if (!q.slab) return assembled(payload, ns, lambda, i, j);
+    if (i < ns && j < ns) {
+        const int64_t idx = pay_index(ns, i, j);
+        const int item = (int)(idx % 36);
+        const double s = slab_sum(q, idx / 36, item);
+        double v = (i / 6 == j / 6) ? cam_u(q.camlin, i / 6, item / 6, item % 6) - s : -s;
+        if (i == j) v += lambda * clampd(cam_u(q.camlin, i / 6, i % 6, i % 6));
+        return v;
+    }
+    return i == j ? 1.0 : 0.0;
+}
+
+__device__ __forceinline__ double gc_src(const SlabSrc &q, int i) { return q.camlin[CAMLIN * (i / 6) + 21 + i % 6]; }
+__device__ __forceinline__ double bz_src(const SlabSrc &q, int32_t ns, int i) {
+    return slab_sum(q, pay_index(ns, i - i % 6, i - i % 6) / 36, 36 + i % 6);
+}
+
+__device__ __forceinline__ double assembled_b_src(const SlabSrc &q, const double *__restrict__ payload, int32_t ns,
+                                                  int i) {
+    if (!q.slab) return assembled_b(payload, ns, i);
+    return i < ns ? -gc_src(q, i) + bz_src(q, ns, i) : 0.0;
+}
+
 template <int TB>
 __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_t nsp, int s,
                                                   double *__restrict__ D, double *__restrict__ bvec,
                                                   int *__restrict__ bad, const double *__restrict__ payload,
                                                   int32_t ns, const double *__restrict__ lam,
-                                                  const int *__restrict__ gate, int dpp) {
+                                                  const int *__restrict__ gate, int dpp, SlabSrc src,
+                                                  double *__restrict__ payload_out) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
     const double lambda = s == 0 ? *lam : 0.0;
     __shared__ double Lr[TB][TB + 1], Lc[TB][TB + 1], Ct[TB][TB + 1], Cd[TB][TB + 1];
@@ -1069,6 +1124,16 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
     const bool upd = s >= 1;
     const int kp = (s - 1) * TB;  // previous column's first index
     int blk = blockIdx.x;
+    if (!upd && src.slab && blk == 0) {  // launch 0 from the slabs: the payload's vectors
+        const int64_t base = pay_vec_base(ns);
+        for (int i = t; i < ns; i += blockDim.x) {
+            payload_out[base + i] = cam_u(src.camlin, i / 6, i % 6, i % 6);
+            payload_out[base + ns + i] = gc_src(src, i);
+            payload_out[base + 2 * ns + i] = bz_src(src, ns, i);
+        }
+        return;
+    }
+    if (!upd && src.slab) --blk;
     if (upd && blk == 0) {
         const double *Dp = D + ((s - 1) & 1) * TB * TB;
         for (int e = t; e < TB * TB; e += blockDim.x) {
@@ -1104,8 +1169,8 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
                 arc[q] = A[(int64_t)(r0 + i) * nsp + c0 + j];
                 ass[q] = need_d ? A[(int64_t)(s0 + i) * nsp + s0 + j] : 0.0;
             } else {
-                arc[q] = assembled(payload, ns, lambda, r0 + i, c0 + j);
-                ass[q] = need_d ? assembled(payload, ns, lambda, s0 + i, s0 + j) : 0.0;
+                arc[q] = assembled_src(src, payload, ns, lambda, r0 + i, c0 + j);
+                ass[q] = need_d ? assembled_src(src, payload, ns, lambda, s0 + i, s0 + j) : 0.0;
             }
         }
         __syncthreads();
@@ -1135,7 +1200,7 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
     // column s: C_ss (Cd, or Ct in the diagonal block) is bitwise the same in
     // every column block -- same inputs, same operation order
     if (!upd && r == s)  // launch 0: the right-hand side of the rows past tile 0
-        for (int i = TB + t; i < nsp; i += blockDim.x) bvec[i] = assembled_b(payload, ns, i);
+        for (int i = TB + t; i < nsp; i += blockDim.x) bvec[i] = assembled_b_src(src, payload, ns, i);
     __syncthreads();
     if (t >= 64) return;
     const int lane = t;
@@ -1151,7 +1216,7 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
             }
             chol_factor16(rw, pw, dinv, li, lane, bad);
             if (r == s) {
-                double y = upd ? bvec[s0 + li] : assembled_b(payload, ns, li);
+                double y = upd ? bvec[s0 + li] : assembled_b_src(src, payload, ns, li);
                 if (upd) {
                     double acc = 0;
 #pragma unroll
@@ -1196,7 +1261,7 @@ __global__ void __launch_bounds__(256) k_chol_col(double *__restrict__ A, int32_
     for (int j = 0; j < TB; ++j) rw[j] = prow ? Ct[lane - TB][j] : Cdd[li][j];
     chol_factor<TB>(rw, dinv, lane, bad);
     if (r == s) {
-        double y = upd ? bvec[s0 + li] : assembled_b(payload, ns, li);
+        double y = upd ? bvec[s0 + li] : assembled_b_src(src, payload, ns, li);
         if (upd) {
             double acc = 0;
 #pragma unroll
@@ -1555,27 +1620,20 @@ static int lanes_per_point(const char *env, int dflt) {
     return (g == 1 || g == 2 || g == 4 || g == 8) ? g : dflt;
 }
 
-// DPP row broadcasts in the tile factor (default); SFM_CHOL_DPP=0 selects
-// the readlane chain, for same-box A/B
-static int chol_dpp() {
-    static const int v = [] {
-        const char *e = std::getenv("SFM_CHOL_DPP");
-        return e ? std::atoi(e) != 0 : 1;
-    }();
-    return v;
-}
-
 // Factor + forward solve (nT launches of k_chol_col) and backward solve of
 // the padded reduced camera system with tiles of tb (16 or 32) columns; A, b
 // on the device, D = 2 tb^2 scratch; nsp a multiple of tb.
 template <int TB>
 static int launch_cholesky_t(const double *payload, int32_t ns, const double *lam, double *A, int32_t nsp, double *b,
-                             double *D, int *bad, hipStream_t s, const int *gate, const CamTrialArgs &ct) {
+                             double *D, int *bad, hipStream_t s, const int *gate, const CamTrialArgs &ct,
+                             const SlabSrc &src, int dpp) {
     const int nT = nsp / TB;
     for (int st = 0; st < nT; ++st) {
         const int T = nT - st;
-        hipLaunchKernelGGL(k_chol_col<TB>, dim3(T * (T + 1) / 2 + (st >= 1 ? 1 : 0)), dim3(256), 0, s, A, nsp, st, D,
-                           b, bad, payload, ns, lam, gate, chol_dpp());
+        const int extra = st >= 1 || src.slab ? 1 : 0;  // bookkeeping / payload-vector workgroup
+        hipLaunchKernelGGL(k_chol_col<TB>, dim3(T * (T + 1) / 2 + extra), dim3(256), 0, s, A, nsp, st, D, b, bad,
+                           payload, ns, lam, gate, dpp, st == 0 ? src : SlabSrc{nullptr, nullptr, 0, 0},
+                           const_cast<double *>(payload));
         SFM_HIP(hipGetLastError());
     }
     hipLaunchKernelGGL(k_chol_backsolve<TB>, dim3(1), dim3(SOLVE_THREADS), 0, s, A, nsp, b,
@@ -1585,9 +1643,10 @@ static int launch_cholesky_t(const double *payload, int32_t ns, const double *la
 }
 
 static int launch_cholesky(const double *payload, int32_t ns, const double *lam, double *A, int32_t nsp, double *b,
-                           double *D, int *bad, hipStream_t s, int tb, const int *gate, const CamTrialArgs &ct) {
-    return tb == 32 ? launch_cholesky_t<32>(payload, ns, lam, A, nsp, b, D, bad, s, gate, ct)
-                    : launch_cholesky_t<16>(payload, ns, lam, A, nsp, b, D, bad, s, gate, ct);
+                           double *D, int *bad, hipStream_t s, int tb, const int *gate, const CamTrialArgs &ct,
+                           const SlabSrc &src, int dpp) {
+    return tb == 32 ? launch_cholesky_t<32>(payload, ns, lam, A, nsp, b, D, bad, s, gate, ct, src, dpp)
+                    : launch_cholesky_t<16>(payload, ns, lam, A, nsp, b, D, bad, s, gate, ct, src, dpp);
 }
 
 // Cholesky tile width (env SFM_CHOL_TILE = 32 for experiments).  Measured
@@ -1615,8 +1674,9 @@ static int chol_tile(int64_t) {
 // fp64 MFMA rate and its serial per-tile chains bound both.
 static int launch_reduced_solve(int32_t ns, int32_t nsp, const double *payload, const double *lam, double *A,
                                 double *b, double *D, int *bad, hipStream_t s, int tb, const int *gate,
-                                const CamTrialArgs &ct) {
-    return launch_cholesky(payload, ns, lam, A, nsp, b, D, bad, s, tb, gate, ct);
+                                const CamTrialArgs &ct, const SlabSrc &src = SlabSrc{nullptr, nullptr, 0, 0},
+                                int dpp = 1) {
+    return launch_cholesky(payload, ns, lam, A, nsp, b, D, bad, s, tb, gate, ct, src, dpp);
 }
 
 // partial[block][4] = {trial cost, model_p, |dp|^2, |X|^2}
@@ -2021,6 +2081,7 @@ struct sfm_ba_problem {
     int32_t ndiag_items = 0, ndiag_blocks = 0;  // k_camera_lin items (one per workgroup) / cameras
     int32_t cl_fused_wg = 0, cl_fused_items = 0;  // k_schur_sweep's camera workgroups / their items
     bool cl_fused = false;                         // this solve: camera blocks inside the sweep launch
+    bool chol_dpp = true, fin_fused = true;        // this solve: DPP tile factor; finish folded into the solve
     int sw_debug = 0;                              // SFM_SWEEP_DEBUG (read once per solve)
     // Schur sweep plan (k_schur_sweep): ranges, chunks, specs
     int32_t sw_nrange = 0, sw_nspec = 0, sw_nbd = 0, sw_nchunk = 0;
@@ -2571,9 +2632,13 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
                        p->d_sw_pairs, p->d_sw_hdr, p->d_Z, p->d_slab, gst, p->sw_debug, nsweep,
                        camlin_args(p, true, &p->d_lm[par].run_lin));
     SFM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_schur_finish, dim3(p->sw_nbd), dim3(64), 0, s, p->ns, p->sw_nbd, p->sw_nrange,
-                       p->d_sw_blkij, p->d_slab, p->d_camlin, p->d_payload, gst);
-    SFM_HIP(hipGetLastError());
+    // one rank: the solve's first launch sums the slabs itself (SlabSrc)
+    const bool fin_fused = !p->comm && p->fin_fused;
+    if (!fin_fused) {
+        hipLaunchKernelGGL(k_schur_finish, dim3(p->sw_nbd), dim3(64), 0, s, p->ns, p->sw_nbd, p->sw_nrange,
+                           p->d_sw_blkij, p->d_slab, p->d_camlin, p->d_payload, gst);
+        SFM_HIP(hipGetLastError());
+    }
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SCHUR + 1], s));
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_COMM], s));
     if ((rc = allreduce(p, p->d_payload, p->payload_len - 1))) return rc;
@@ -2581,8 +2646,10 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SOLVE], s));
     // the back substitution's epilogue forms the trial cameras (k_camera_trial's work)
     const CamTrialArgs ct = {p->nc, p->ns, p->d_payload, lam, p->d_Rt, p->d_Rt2, p->d_scal + 4};
+    const SlabSrc src = fin_fused ? SlabSrc{p->d_slab, p->d_camlin, p->sw_nbd, p->sw_nrange}
+                                  : SlabSrc{nullptr, nullptr, 0, 0};
     if ((rc = launch_reduced_solve(p->ns, p->nsp, p->d_payload, lam, p->d_A, p->d_b, p->d_D, bad, s, p->tb, gst,
-                                   ct)))
+                                   ct, src, p->chol_dpp)))
         return rc;
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SOLVE + 1], s));
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_TRIAL], s));
@@ -2639,6 +2706,9 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
     // camera blocks inside the sweep launch, except when gradient_tolerance
     // needs g_c right after the linearisation
     p->cl_fused = o->gradient_tolerance == 0.0 && env_int("SFM_CAMLIN_FUSED", 1) != 0;
+    // A/B switches (read per solve): DPP tile factor, finish folded into the solve
+    p->chol_dpp = env_int("SFM_CHOL_DPP", 1) != 0;
+    p->fin_fused = env_int("SFM_FINISH_FUSED", 1) != 0;
     p->sw_debug = env_int("SFM_SWEEP_DEBUG", 0);
     (void)hipGetLastError();
     const auto t0 = std::chrono::steady_clock::now();

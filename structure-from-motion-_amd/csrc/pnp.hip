@@ -27,6 +27,7 @@
 
 #include "lm_small.hpp"
 #include "sfm_common.hpp"
+#include "select.hpp"
 
 namespace sfm {
 
@@ -455,27 +456,12 @@ __global__ void __launch_bounds__(64 * PNP_WAVES) k_pnp_score(const double *__re
 __global__ void __launch_bounds__(1024) k_pnp_select(const double *__restrict__ models,
                                                      const int32_t *__restrict__ counts, int64_t H,
                                                      int64_t *__restrict__ best_out, double *__restrict__ best_model) {
-    __shared__ int32_t sc[1024];
-    __shared__ int64_t sh[1024];
-    int32_t bc = 0;
-    int64_t bh = -1;
-    for (int64_t h = threadIdx.x; h < H; h += blockDim.x) {
-        const int32_t c = counts[h];
-        if (c > bc) { bc = c; bh = h; }
-    }
-    sc[threadIdx.x] = bc;
-    sh[threadIdx.x] = bh;
-    __syncthreads();
-    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) {
-            const int32_t c2 = sc[threadIdx.x + s], c1 = sc[threadIdx.x];
-            const int64_t h2 = sh[threadIdx.x + s], h1 = sh[threadIdx.x];
-            if (c2 > c1 || (c2 == c1 && c2 > 0 && h2 < h1)) { sc[threadIdx.x] = c2; sh[threadIdx.x] = h2; }
-        }
-        __syncthreads();
-    }
-    const int64_t best = sc[0] > 0 ? sh[0] : -1;
-    if (threadIdx.x == 0) best_out[0] = best, best_out[1] = sc[0];
+    __shared__ int32_t sc[1024 / 64];
+    __shared__ int64_t sh[1024 / 64];
+    int32_t bc;
+    int64_t best;
+    wg_select_best<1024>(counts, H, sc, sh, bc, best);
+    if (threadIdx.x == 0) best_out[0] = best, best_out[1] = bc;
     if (best >= 0 && threadIdx.x < PNP_MODEL) best_model[threadIdx.x] = models[PNP_MODEL * best + threadIdx.x];
 }
 

@@ -25,6 +25,7 @@
 #include "sfm_common.hpp"
 #include "sfm_geom.hpp"
 #include "pyrandom.hpp"
+#include "select.hpp"
 
 namespace sfm {
 
@@ -251,7 +252,8 @@ static inline int64_t score_slice(int64_t nh, int64_t N, int *ny) {
     return per * SCORE_TILE;
 }
 
-// grid = 1 workgroup of 1024 threads
+// grid = 1 workgroup of 1024 threads: the winner (wg_select_best), then the
+// mask with 4 correspondence pairs per thread loaded before any is tested.
 template <class M>
 __global__ void __launch_bounds__(1024) k_ransac_select(const double2 *__restrict__ x1,
                                                         const double2 *__restrict__ x2, int64_t N,
@@ -260,44 +262,36 @@ __global__ void __launch_bounds__(1024) k_ransac_select(const double2 *__restric
                                                         double thr, int64_t *__restrict__ best_out,
                                                         double *__restrict__ F_best,
                                                         uint8_t *__restrict__ mask) {
-    __shared__ int32_t sc[1024];
-    __shared__ int64_t sh[1024];
-    int32_t bc = 0;
-    int64_t bh = -1;
-    for (int64_t h = threadIdx.x; h < H; h += blockDim.x) {
-        const int32_t c = counts[h];
-        if (c > bc) { bc = c; bh = h; }  // ascending h per thread: first max kept
-    }
-    sc[threadIdx.x] = bc;
-    sh[threadIdx.x] = bh;
-    __syncthreads();
-    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) {
-            const int32_t c2 = sc[threadIdx.x + s];
-            const int64_t h2 = sh[threadIdx.x + s];
-            const int32_t c1 = sc[threadIdx.x];
-            const int64_t h1 = sh[threadIdx.x];
-            if (c2 > c1 || (c2 == c1 && c2 > 0 && h2 < h1)) {
-                sc[threadIdx.x] = c2;
-                sh[threadIdx.x] = h2;
-            }
-        }
-        __syncthreads();
-    }
-    const int64_t best = sc[0] > 0 ? sh[0] : -1;
-    if (threadIdx.x == 0) {
+    constexpr int NT = 1024, MU = 4;
+    __shared__ int32_t sc[NT / 64];
+    __shared__ int64_t sh[NT / 64];
+    const int t = threadIdx.x;
+    int32_t bc;
+    int64_t best;
+    wg_select_best<NT>(counts, H, sc, sh, bc, best);
+    if (t == 0) {
         best_out[0] = best;
-        best_out[1] = sc[0];  // its count (the shard key's high word)
+        best_out[1] = bc;  // its count (the shard key's high word)
     }
     if (best < 0) return;
     double f[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) f[k] = F[9 * best + k];
-    if (threadIdx.x < 9) F_best[threadIdx.x] = f[threadIdx.x];
+    if (t < 9) F_best[t] = f[t];
     if (!mask) return;  // a hypothesis shard: the mask is emitted after the combine
-    for (int64_t i = threadIdx.x; i < N; i += blockDim.x) {
-        const double2 p = x1[i], q = x2[i];
-        mask[i] = M::inlier(f, p, q, thr) ? 1 : 0;
+    for (int64_t base = t; base < N; base += (int64_t)MU * NT) {
+        double2 p[MU], q[MU];
+#pragma unroll
+        for (int u = 0; u < MU; ++u) {
+            const int64_t i = base + (int64_t)u * NT;
+            p[u] = i < N ? x1[i] : make_double2(0.0, 0.0);
+            q[u] = i < N ? x2[i] : make_double2(0.0, 0.0);
+        }
+#pragma unroll
+        for (int u = 0; u < MU; ++u) {
+            const int64_t i = base + (int64_t)u * NT;
+            if (i < N) mask[i] = M::inlier(f, p[u], q[u], thr) ? 1 : 0;
+        }
     }
 }
 

@@ -922,6 +922,34 @@ def test_ba_camera_blocks_fused_equal_standalone(core, monkeypatch):
     assert abs(a["cost"] - b["cost"]) <= 1e-10 * b["cost"]
 
 
+@pytest.mark.parametrize("shape", ["cfg3", "50x6000"])
+def test_ba_solve_variants_bitwise_equal(core, monkeypatch, shape):
+    """The reduced solve's DPP tile factor (default) and the readlane chain
+    (SFM_CHOL_DPP=0), and the Schur finish folded into the solve's first
+    launch at one rank (default) or run as its own launch
+    (SFM_FINISH_FUSED=0): the same operations in the same order, so the
+    whole LM solve -- counts, status, cost, cameras and points -- is bitwise
+    the same in all four combinations.  50x6000: 19 tile columns, as cfg4."""
+    if shape == "cfg3":
+        p = syn.ba_problem_cfg("cfg3", dense=False)
+    else:
+        p = syn.ba_problem(50, 6000, 8, seed=5)
+    cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
+    args = (cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K)
+    out = {}
+    for dpp in ("1", "0"):
+        for fin in ("1", "0"):
+            monkeypatch.setenv("SFM_CHOL_DPP", dpp)
+            monkeypatch.setenv("SFM_FINISH_FUSED", fin)
+            out[dpp + fin] = core.ba_lm(*args, max_iterations=12, fixed_iterations=True)
+    c0, x0, r0 = out["11"]
+    assert r0["accepted"] > 0
+    for key, (c, x, r) in out.items():
+        assert (r["iterations"], r["accepted"], r["status"], r["cost"]) == \
+            (r0["iterations"], r0["accepted"], r0["status"], r0["cost"]), key
+        assert np.array_equal(c, c0) and np.array_equal(x, x0), key
+
+
 def test_ba_timing_and_lm_state_polling(core):
     """Per-phase kernel times are recorded only with sfm_ba_set_timing on,
     and turning them on does not change the solve; a solve that converges
