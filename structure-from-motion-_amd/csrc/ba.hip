@@ -1607,9 +1607,9 @@ __global__ void k_lm_step(const LMState *__restrict__ lm_in, LMState *__restrict
         }
     }
     if (!lm.accept_now) return;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < 3 * np_) X[i] = X2[i];
-    if (i < 12 * (int64_t)nc) Rt[i] = Rt2[i];
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = i0; i < 3 * np_; i += st) X[i] = X2[i];  // bounded grid: cheap when nothing is copied
+    for (int64_t i = i0; i < 12 * (int64_t)nc; i += st) Rt[i] = Rt2[i];
 }
 
 // Lanes per point for the grouped per-point kernels (1, 2, 4 or 8; an
@@ -2764,7 +2764,9 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
             SFM_HIP(hipGetLastError());
         }
         if ((rc = run_step(p, ev, par))) return rc;
-        hipLaunchKernelGGL(k_lm_step, dim3(ceil_div(nacc, 256)), dim3(256), 0, s, p->d_lm + par, p->d_lm + (par ^ 1),
+        // bounded grid, grid-stride copy: after a rejected step nothing is copied
+        hipLaunchKernelGGL(k_lm_step, dim3(std::min(ceil_div(nacc, 256), 512)), dim3(256), 0, s, p->d_lm + par,
+                           p->d_lm + (par ^ 1),
                            p->d_scal, p->d_bad + par, p->d_bad + (par ^ 1), o->max_iterations, o->fixed_iterations,
                            o->function_tolerance, o->parameter_tolerance, o->initial_lambda, p->np, p->nc, p->d_X,
                            p->d_X2, p->d_Rt, p->d_Rt2, p->d_ring, it + 1);
