@@ -1680,6 +1680,7 @@ static int launch_reduced_solve(int32_t ns, int32_t nsp, const double *payload, 
 }
 
 // partial[block][4] = {trial cost, model_p, |dp|^2, |X|^2}
+constexpr int BS_PRE = 6;  // observations per lane prefetched by k_backsub_trial
 template <int G>
 __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const int32_t *__restrict__ pstart,
                                                               const int32_t *__restrict__ cam,
@@ -1710,9 +1711,20 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
     // W^T dc = Jp^T (Jc dc) = R^T A^T (A (dtheta x p + dt)), summed over the point's observations
     double wt[3] = {0, 0, 0};
     const double x[3] = {live ? X[3 * p] : 0.0, live ? X[3 * p + 1] : 0.0, live ? X[3 * p + 2] : 0.0};
-    for (int32_t o = o0 + sub; o < o1; o += G) {
-        const double *d = dc + 6 * cam[o];
-        const double *R = Rt + 12 * cam[o];
+    // the lane's first BS_PRE observations (camera index and measurement)
+    // loaded up front, for both passes: their loads are in flight together
+    // instead of one round trip per observation and pass
+    int32_t cpre[BS_PRE];
+    double2 opre[BS_PRE];
+#pragma unroll
+    for (int k = 0; k < BS_PRE; ++k) {
+        const int32_t o = o0 + sub + k * G;
+        cpre[k] = o < o1 ? cam[o] : 0;
+        opre[k] = o < o1 ? obs[o] : make_double2(0.0, 0.0);
+    }
+    auto wt_add = [&](int32_t c) {
+        const double *d = dc + 6 * c;
+        const double *R = Rt + 12 * c;
         double A[2][3], q[3];
         obs_Ap(R, x, K, A, q);
         const double v0 = d[1] * q[2] - d[2] * q[1] + d[3];
@@ -1725,7 +1737,11 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
         for (int i = 0; i < 3; ++i) w[i] = A[0][i] * s0 + A[1][i] * s1;
 #pragma unroll
         for (int i = 0; i < 3; ++i) wt[i] += R[i] * w[0] + R[3 + i] * w[1] + R[6 + i] * w[2];
-    }
+    };
+#pragma unroll
+    for (int k = 0; k < BS_PRE; ++k)
+        if (o0 + sub + k * G < o1) wt_add(cpre[k]);
+    for (int32_t o = o0 + sub + BS_PRE * G; o < o1; o += G) wt_add(cam[o]);
 #pragma unroll
     for (int i = 0; i < 3; ++i) wt[i] = group_sum<G>(wt[i]);
     if (live) {
@@ -1750,7 +1766,10 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
                 acc[3] += x[i] * x[i];
             }
         }
-        for (int32_t o = o0 + sub; o < o1; o += G) acc[0] += obs_cost(Rt_new + 12 * cam[o], xn, K, obs[o]);
+#pragma unroll
+        for (int k = 0; k < BS_PRE; ++k)
+            if (o0 + sub + k * G < o1) acc[0] += obs_cost(Rt_new + 12 * cpre[k], xn, K, opre[k]);
+        for (int32_t o = o0 + sub + BS_PRE * G; o < o1; o += G) acc[0] += obs_cost(Rt_new + 12 * cam[o], xn, K, obs[o]);
     }
     }
     grid_sum_last<4>(acc, partial, counter, out);
