@@ -49,6 +49,14 @@ struct EpiModel {
     __device__ static Part fast(const double *f, double2 p, double2 q, double, double lo, double hi) {
         return epi_fast(f, p.x, p.y, q.x, q.y, lo, hi);
     }
+    static constexpr bool SPLIT = true;  // fast() as fast_b(fast_a()): the wave-level outlier skip
+    using PartA = EpiPartA;
+    __device__ static PartA fast_a(const double *f, double2 p, double2 q, double hi) {
+        return epi_fast_a(f, p.x, p.y, q.x, q.y, hi);
+    }
+    __device__ static Part fast_b(const PartA &a, const double *f, double2 q, double lo, double hi) {
+        return epi_fast_b(a, f, q.x, q.y, lo, hi);
+    }
     __device__ static bool exact(const Part &r, double2, double2, const double *, double thr) {
         return epi_exact(r, thr);
     }
@@ -74,6 +82,10 @@ struct HomModel {
         return {hom_inlier(f, p.x, p.y, q.x, q.y, thr), false};
     }
     __device__ static bool exact(const Part &r, double2, double2, const double *, double) { return r.in; }
+    static constexpr bool SPLIT = false;
+    using PartA = Part;
+    __device__ static PartA fast_a(const double *, double2, double2, double) { return {false, false}; }
+    __device__ static Part fast_b(const PartA &, const double *, double2, double, double) { return {false, false}; }
 };
 
 template <class M>
@@ -168,7 +180,7 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES, FIT ? SFM_SCORE_FIT_OCC : 1)
                                                                    int64_t N, const double *__restrict__ F,
                                                                    int64_t H, double thr,
                                                                    int32_t *__restrict__ counts, int64_t slice,
-                                                                   FitNext fn) {
+                                                                   FitNext fn, int score_split) {
     __shared__ double2 s1[SCORE_TILE];
     __shared__ double2 s2[SCORE_TILE];
     int bx = blockIdx.x;
@@ -211,9 +223,21 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES, FIT ? SFM_SCORE_FIT_OCC : 1)
             for (; j + 128 <= n; j += 128) {
                 const double2 p0 = s1[j + lane], q0 = s2[j + lane];
                 const double2 p1 = s1[j + 64 + lane], q1 = s2[j + 64 + lane];
-                // both fast decisions before either branch to the exact tail
-                const typename M::Part r0 = M::fast(f, p0, q0, thr, thr_lo, thr_hi);
-                const typename M::Part r1 = M::fast(f, p1, q1, thr, thr_lo, thr_hi);
+                typename M::Part r0, r1;
+                if constexpr (M::SPLIT) {
+                    // stage A of both pairs; a wave whose 128 pairs are all
+                    // decided outliers there counts nothing and skips stage B
+                    // (most waves: the mean cfg2 hypothesis has ~2 inliers)
+                    const typename M::PartA a0 = M::fast_a(f, p0, q0, thr_hi);
+                    const typename M::PartA a1 = M::fast_a(f, p1, q1, thr_hi);
+                    if (score_split && __ballot(!(a0.out && a1.out)) == 0) continue;
+                    r0 = M::fast_b(a0, f, q0, thr_lo, thr_hi);
+                    r1 = M::fast_b(a1, f, q1, thr_lo, thr_hi);
+                } else {
+                    // both fast decisions before either branch to the exact tail
+                    r0 = M::fast(f, p0, q0, thr, thr_lo, thr_hi);
+                    r1 = M::fast(f, p1, q1, thr, thr_lo, thr_hi);
+                }
                 bool in0 = r0.in, in1 = r1.in;
                 if (r0.unsure) in0 = M::exact(r0, p0, q0, f, thr);
                 if (r1.unsure) in1 = M::exact(r1, p1, q1, f, thr);
@@ -237,6 +261,16 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES, FIT ? SFM_SCORE_FIT_OCC : 1)
         else
             atomicAdd(counts + h, cnt);
     }
+}
+
+// the score's wave-level outlier skip (EpiModel stage A); SFM_SCORE_SPLIT=0
+// turns it off, for same-box A/B
+static inline int score_split_on() {
+    static const int v = [] {
+        const char *e = std::getenv("SFM_SCORE_SPLIT");
+        return e ? std::atoi(e) != 0 : 1;
+    }();
+    return v;
 }
 
 // Point slices for scoring nh hypotheses: enough workgroups to put ~4 on
@@ -341,7 +375,7 @@ int ransac_run(const double *x1, const double *x2, int64_t N, const int32_t *sam
     if ((rc = launch_fit<M>(d1, d2, ds, H, dF, ny > 1 ? dcnt : nullptr, s))) return rc;
     SFM_HIP(hipEventRecord(c->ev[2], s));
     hipLaunchKernelGGL((k_ransac_score<M, false>), dim3(ceil_div(H, SCORE_WAVES), ny), dim3(64 * SCORE_WAVES), 0, s,
-                       d1, d2, N, dF, H, thr, dcnt, slice, FitNext{});
+                       d1, d2, N, dF, H, thr, dcnt, slice, FitNext{}, score_split_on());
     SFM_HIP(hipGetLastError());
     SFM_HIP(hipEventRecord(c->ev[3], s));
     hipLaunchKernelGGL(k_ransac_select<M>, dim3(1), dim3(1024), 0, s, d1, d2, N, dF, dcnt, H, thr, dbest, dFb, dmask);
@@ -463,13 +497,13 @@ struct ScorePipe {
         if constexpr (M::GROUP_FIT) {
             if (fn) {
                 hipLaunchKernelGGL((k_ransac_score<M, true>), grid, dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
-                                   dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, *fn);
+                                   dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, *fn, score_split_on());
                 SFM_HIP(hipGetLastError());
                 return 0;
             }
         }
         hipLaunchKernelGGL((k_ransac_score<M, false>), grid, dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
-                           dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, FitNext{});
+                           dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, FitNext{}, score_split_on());
         SFM_HIP(hipGetLastError());
         return 0;
     }

@@ -63,6 +63,53 @@ __device__ __forceinline__ EpiPart epi_fast(const double *F, double x, double y,
     return r;
 }
 
+// epi_fast in two stages, the same operations: stage A (the first image's
+// line, e, |Fx1|^2 and its rsq) already proves "outlier" for most pairs --
+// the mean is at least half the first distance, so a first distance above the
+// band's upper edge decides it; the score kernel skips stage B for a wave
+// whose pairs are all decided that way.  epi_fast_b(epi_fast_a(...)) equals
+// epi_fast(...) in every field.
+struct EpiPartA {
+    double ae, qa, ra;
+    bool out;  // decided: outlier
+};
+
+__device__ __forceinline__ EpiPartA epi_fast_a(const double *F, double x, double y, double u, double v,
+                                               double thr_hi2) {
+    const double a0 = F[0] * x + F[1] * y + F[2];
+    const double a1 = F[3] * x + F[4] * y + F[5];
+    const double a2 = F[6] * x + F[7] * y + F[8];
+    const double e = u * a0 + v * a1 + a2;
+    EpiPartA r;
+    r.ae = fabs(e);
+    r.qa = a0 * a0 + a1 * a1;
+    r.ra = __builtin_amdgcn_rsq(r.qa);
+    // ae / (sqrt(qa) + 1e-8) to first order (an underestimate, ~1e-6 relative
+    // while ra < 1e5); ra < 1e5 also fails for NaN
+    const double d1 = r.ae * fma(-1e-8, r.ra * r.ra, r.ra);
+    r.out = d1 > thr_hi2 && r.ra < 1e5;
+    return r;
+}
+
+__device__ __forceinline__ EpiPart epi_fast_b(const EpiPartA &a, const double *F, double u, double v,
+                                              double thr_lo2, double thr_hi2) {
+    const double b0 = F[0] * u + F[3] * v + F[6];
+    const double b1 = F[1] * u + F[4] * v + F[7];
+    EpiPart r;
+    r.ae = a.ae;
+    r.qa = a.qa;
+    r.qb = b0 * b0 + b1 * b1;
+    const double ra = a.ra, rb = __builtin_amdgcn_rsq(r.qb);
+    const double srr = ra + rb;
+    const double ap2 = r.ae * fma(-1e-8, fma(ra, ra, rb * rb), srr);
+    const bool ok = srr < 1e5;
+    const bool sure_in = ap2 < thr_lo2 && ok;
+    const bool sure_out = ap2 > thr_hi2 && ok;
+    r.in = sure_in;
+    r.unsure = !(sure_in || sure_out);
+    return r;
+}
+
 // the exact tail of epi_inlier from epi_fast's terms (same operations)
 __device__ __forceinline__ bool epi_exact(const EpiPart &r, double thr) {
     const double d1 = r.ae / (sqrt(r.qa) + 1e-8);
