@@ -64,13 +64,13 @@ __device__ __forceinline__ EpiPart epi_fast(const double *F, double x, double y,
 }
 
 // epi_fast in two stages, the same operations: stage A (the first image's
-// line, e, |Fx1|^2 and its rsq) already proves "outlier" for most pairs --
+// line, e and |Fx1|^2) already proves "outlier" for most pairs --
 // the mean is at least half the first distance, so a first distance above the
 // band's upper edge decides it; the score kernel skips stage B for a wave
 // whose pairs are all decided that way.  epi_fast_b(epi_fast_a(...)) equals
 // epi_fast(...) in every field.
 struct EpiPartA {
-    double ae, qa, ra;
+    double ae, qa;
     bool out;  // decided: outlier
 };
 
@@ -83,11 +83,14 @@ __device__ __forceinline__ EpiPartA epi_fast_a(const double *F, double x, double
     EpiPartA r;
     r.ae = fabs(e);
     r.qa = a0 * a0 + a1 * a1;
-    r.ra = __builtin_amdgcn_rsq(r.qa);
-    // ae / (sqrt(qa) + 1e-8) to first order (an underestimate, ~1e-6 relative
-    // while ra < 1e5); ra < 1e5 also fails for NaN
-    const double d1 = r.ae * fma(-1e-8, r.ra * r.ra, r.ra);
-    r.out = d1 > thr_hi2 && r.ra < 1e5;
+    // d1 = ae / (sqrt(qa) + 1e-8) > thr_hi2 without a square root:
+    // (sqrt(qa) + 1e-8)^2 <= qa (1 + 1e-8) + 1e-8 + 1e-16 (sqrt(qa) <= (qa + 1) / 2),
+    // so ae^2 > thr_hi2^2 (qa (1 + 1e-8) + 1.00000001e-8) proves it; the band
+    // (thr_hi2 = 2 thr (1 + 1e-4)) absorbs the rounding of these few
+    // operations.  The magnitude guards keep ae^2 and the right side finite;
+    // NaN fails every comparison (stage B decides those pairs)
+    const double rhs = thr_hi2 * thr_hi2 * fma(r.qa, 1.0 + 1e-8, 1.00000001e-8);
+    r.out = r.ae * r.ae > rhs && r.ae < 1e150 && r.qa < 1e290 && thr_hi2 >= 0.0;
     return r;
 }
 
@@ -99,7 +102,7 @@ __device__ __forceinline__ EpiPart epi_fast_b(const EpiPartA &a, const double *F
     r.ae = a.ae;
     r.qa = a.qa;
     r.qb = b0 * b0 + b1 * b1;
-    const double ra = a.ra, rb = __builtin_amdgcn_rsq(r.qb);
+    const double ra = __builtin_amdgcn_rsq(a.qa), rb = __builtin_amdgcn_rsq(r.qb);
     const double srr = ra + rb;
     const double ap2 = r.ae * fma(-1e-8, fma(ra, ra, rb * rb), srr);
     const bool ok = srr < 1e5;
