@@ -223,24 +223,41 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES, FIT ? SFM_SCORE_FIT_OCC : 1)
             for (; j + 128 <= n; j += 128) {
                 const double2 p0 = s1[j + lane], q0 = s2[j + lane];
                 const double2 p1 = s1[j + 64 + lane], q1 = s2[j + 64 + lane];
-                typename M::Part r0, r1;
+                bool in0 = false, in1 = false;
                 if constexpr (M::SPLIT) {
-                    // stage A of both pairs; a wave whose 128 pairs are all
-                    // decided outliers there counts nothing and skips stage B
-                    // (most waves: the mean cfg2 hypothesis has ~2 inliers)
+                    // stage A of both pairs; each 64-pair set whose pairs are
+                    // all decided outliers there counts nothing and skips stage
+                    // B (most sets: the mean cfg2 hypothesis has ~2 inliers);
+                    // both sets needed: both stage Bs before either exact tail
                     const typename M::PartA a0 = M::fast_a(f, p0, q0, thr_hi);
                     const typename M::PartA a1 = M::fast_a(f, p1, q1, thr_hi);
-                    if (score_split && __ballot(!(a0.out && a1.out)) == 0) continue;
-                    r0 = M::fast_b(a0, f, q0, thr_lo, thr_hi);
-                    r1 = M::fast_b(a1, f, q1, thr_lo, thr_hi);
+                    const bool n0 = !score_split || __ballot(!a0.out) != 0;
+                    const bool n1 = !score_split || __ballot(!a1.out) != 0;
+                    if (!n0 && !n1) continue;
+                    if (n0 && n1) {
+                        const typename M::Part r0 = M::fast_b(a0, f, q0, thr_lo, thr_hi);
+                        const typename M::Part r1 = M::fast_b(a1, f, q1, thr_lo, thr_hi);
+                        in0 = r0.in;
+                        in1 = r1.in;
+                        if (r0.unsure) in0 = M::exact(r0, p0, q0, f, thr);
+                        if (r1.unsure) in1 = M::exact(r1, p1, q1, f, thr);
+                    } else {
+                        const bool first = n0;  // the one set that needs stage B
+                        const typename M::Part r = M::fast_b(first ? a0 : a1, f, first ? q0 : q1, thr_lo, thr_hi);
+                        bool in = r.in;
+                        if (r.unsure) in = M::exact(r, first ? p0 : p1, first ? q0 : q1, f, thr);
+                        in0 = first && in;
+                        in1 = !first && in;
+                    }
                 } else {
                     // both fast decisions before either branch to the exact tail
-                    r0 = M::fast(f, p0, q0, thr, thr_lo, thr_hi);
-                    r1 = M::fast(f, p1, q1, thr, thr_lo, thr_hi);
+                    const typename M::Part r0 = M::fast(f, p0, q0, thr, thr_lo, thr_hi);
+                    const typename M::Part r1 = M::fast(f, p1, q1, thr, thr_lo, thr_hi);
+                    in0 = r0.in;
+                    in1 = r1.in;
+                    if (r0.unsure) in0 = M::exact(r0, p0, q0, f, thr);
+                    if (r1.unsure) in1 = M::exact(r1, p1, q1, f, thr);
                 }
-                bool in0 = r0.in, in1 = r1.in;
-                if (r0.unsure) in0 = M::exact(r0, p0, q0, f, thr);
-                if (r1.unsure) in1 = M::exact(r1, p1, q1, f, thr);
                 cnt += __popcll(__ballot(in0)) + __popcll(__ballot(in1));
             }
             for (; j < n; j += 64) {
