@@ -75,17 +75,17 @@ struct HomModel {
     __device__ static bool inlier_fast(const double *f, double2 p, double2 q, double thr, double, double) {
         return hom_inlier(f, p.x, p.y, q.x, q.y, thr);
     }
-    struct Part {
-        bool in, unsure;
-    };
+    using Part = HomPart;
     __device__ static Part fast(const double *f, double2 p, double2 q, double thr, double, double) {
-        return {hom_inlier(f, p.x, p.y, q.x, q.y, thr), false};
+        return hom_fast(f, p.x, p.y, q.x, q.y, thr);
     }
-    __device__ static bool exact(const Part &r, double2, double2, const double *, double) { return r.in; }
+    __device__ static bool exact(const Part &r, double2, double2 q, const double *, double thr) {
+        return hom_exact(r, q.x, q.y, thr);
+    }
     static constexpr bool SPLIT = false;
     using PartA = Part;
-    __device__ static PartA fast_a(const double *, double2, double2, double) { return {false, false}; }
-    __device__ static Part fast_b(const PartA &, const double *, double2, double, double) { return {false, false}; }
+    __device__ static PartA fast_a(const double *, double2, double2, double) { return {}; }
+    __device__ static Part fast_b(const PartA &a, const double *, double2, double, double) { return a; }
 };
 
 template <class M>

@@ -573,6 +573,49 @@ __device__ __forceinline__ bool hom_inlier(const double *H, double x, double y, 
     return sqrt(d0 * d0 + d1 * d1) < thr;
 }
 
+// The same decision, cheaper: 1/w from v_rcp_f64 and two Newton steps
+// (relative error far below 1e-12), the transfer error squared without the
+// two IEEE divides and the square root, compared against the threshold
+// widened by a bound E on how far the exact expression can sit from this one
+// (|d - d_fast| <= (|t/w| + |u|) 3e-12 per coordinate, plus 1e-9 relative for
+// the exact path's own rounding).  Pairs inside that band, and any NaN, take
+// the exact expression (hom_exact on the same t0, t1, w): every decision is
+// the reference's.
+struct HomPart {
+    double t0, t1, w;
+    bool in, unsure;
+};
+
+__device__ __forceinline__ HomPart hom_fast(const double *H, double x, double y, double u, double v, double thr) {
+    HomPart r;
+    {
+#pragma clang fp contract(off)
+        r.t0 = fma(H[1], y, H[0] * x) + H[2];
+        r.t1 = fma(H[4], y, H[3] * x) + H[5];
+        const double t2 = fma(H[7], y, H[6] * x) + H[8];
+        r.w = t2 + 1e-8;
+    }
+    double iw = __builtin_amdgcn_rcp(r.w);
+    iw = fma(iw, fma(-r.w, iw, 1.0), iw);
+    iw = fma(iw, fma(-r.w, iw, 1.0), iw);
+    const double ua = r.t0 * iw, va = r.t1 * iw;
+    const double d0 = ua - u, d1 = va - v;
+    const double s2 = d0 * d0 + d1 * d1;
+    const double E = (fabs(ua) + fabs(u) + fabs(va) + fabs(v)) * 3e-12;
+    const double lo = thr * (1.0 - 1e-9) - E, hi = thr * (1.0 + 1e-9) + E;
+    const bool sure_in = lo > 0.0 && s2 < lo * lo;
+    const bool sure_out = hi > 0.0 && s2 > hi * hi;
+    r.in = sure_in;
+    r.unsure = !(sure_in || sure_out) || thr < 0.0;
+    return r;
+}
+
+__device__ __forceinline__ bool hom_exact(const HomPart &r, double u, double v, double thr) {
+#pragma clang fp contract(off)
+    const double d0 = r.t0 / r.w - u, d1 = r.t1 / r.w - v;
+    return sqrt(d0 * d0 + d1 * d1) < thr;
+}
+
 // Rodrigues (scipy Rotation.from_rotvec(...).as_matrix()), row-major.
 __device__ __forceinline__ void rotvec_to_R(double wx, double wy, double wz, double *R) {
     const double th2 = wx * wx + wy * wy + wz * wz;
