@@ -410,6 +410,44 @@ __device__ __forceinline__ bool pnp_inlier(const double *P, double X, double Y, 
     return sqrt(du * du + dv * dv) < thr;
 }
 
+// The same decision, cheaper (as hom_fast, sfm_geom.hpp): 1/w by v_rcp_f64
+// and two Newton steps, the squared reprojection error against the threshold
+// widened by E = (|h0/w| + |u| + |h1/w| + |v|) 3e-12 and 1e-9 relative; the
+// band, NaN and thr < 0 take pnp_exact, pnp_inlier's expression on the same
+// h0, h1, w.
+struct PnpPart {
+    double h0, h1, w;
+    bool in, unsure;
+};
+
+__device__ __forceinline__ PnpPart pnp_fast(const double *P, double X, double Y, double Z, double u, double v,
+                                            double thr) {
+    PnpPart r;
+    r.h0 = fma(P[3], 1.0, fma(P[2], Z, fma(P[1], Y, P[0] * X)));
+    r.h1 = fma(P[7], 1.0, fma(P[6], Z, fma(P[5], Y, P[4] * X)));
+    const double h2 = fma(P[11], 1.0, fma(P[10], Z, fma(P[9], Y, P[8] * X)));
+    r.w = h2 + 1e-8;
+    double iw = __builtin_amdgcn_rcp(r.w);
+    iw = fma(iw, fma(-r.w, iw, 1.0), iw);
+    iw = fma(iw, fma(-r.w, iw, 1.0), iw);
+    const double pu = r.h0 * iw, pv = r.h1 * iw;
+    const double du = u - pu, dv = v - pv;
+    const double s2 = du * du + dv * dv;
+    const double E = (fabs(pu) + fabs(u) + fabs(pv) + fabs(v)) * 3e-12;
+    const double lo = thr * (1.0 - 1e-9) - E, hi = thr * (1.0 + 1e-9) + E;
+    const bool sure_in = lo > 0.0 && s2 < lo * lo;
+    const bool sure_out = hi > 0.0 && s2 > hi * hi;
+    r.in = sure_in;
+    r.unsure = !(sure_in || sure_out) || thr < 0.0;
+    return r;
+}
+
+__device__ __forceinline__ bool pnp_exact(const PnpPart &r, double u, double v, double thr) {
+    const double pu = r.h0 / r.w, pv = r.h1 / r.w;
+    const double du = u - pu, dv = v - pv;
+    return sqrt(du * du + dv * dv) < thr;
+}
+
 __global__ void __launch_bounds__(64 * PNP_WAVES) k_pnp_score(const double *__restrict__ X,
                                                               const double2 *__restrict__ x, int64_t N,
                                                               const double *__restrict__ models, int64_t H,
@@ -434,8 +472,12 @@ __global__ void __launch_bounds__(64 * PNP_WAVES) k_pnp_score(const double *__re
             for (; j + 128 <= n; j += 128) {  // two points per lane per pass: independent FP64 chains
                 const int i0 = j + lane, i1 = i0 + 64;
                 const double2 q0 = sx[i0], q1 = sx[i1];
-                const bool in0 = pnp_inlier(P, sX[3 * i0], sX[3 * i0 + 1], sX[3 * i0 + 2], q0.x, q0.y, thr);
-                const bool in1 = pnp_inlier(P, sX[3 * i1], sX[3 * i1 + 1], sX[3 * i1 + 2], q1.x, q1.y, thr);
+                // both fast decisions before either branch to the exact tail
+                const PnpPart r0 = pnp_fast(P, sX[3 * i0], sX[3 * i0 + 1], sX[3 * i0 + 2], q0.x, q0.y, thr);
+                const PnpPart r1 = pnp_fast(P, sX[3 * i1], sX[3 * i1 + 1], sX[3 * i1 + 2], q1.x, q1.y, thr);
+                bool in0 = r0.in, in1 = r1.in;
+                if (r0.unsure) in0 = pnp_exact(r0, q0.x, q0.y, thr);
+                if (r1.unsure) in1 = pnp_exact(r1, q1.x, q1.y, thr);
                 cnt += __popcll(__ballot(in0)) + __popcll(__ballot(in1));
             }
             for (; j < n; j += 64) {
