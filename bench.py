@@ -323,7 +323,7 @@ def ransac_leg(args, world, rank, local_rank, comm):
         "fp64": {"bound": "fp64-valu", "score_tflops": round(score_flops / (k_score * 1e-3) / 1e12, 2),
                  "kernels_tflops": round(all_flops / (k_all * 1e-3) / 1e12, 2), "peak_tflops": FP64_PEAK_TFLOPS,
                  "score_frac": round(score_flops / (k_score * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 4),
-                 "formula": "score: H*N*50 flop; kernels: H*(N*50 + 25e3) flop (SURVEY §8(d))"}})
+                 "formula": "score: H*N*50 flop; kernels: H*(N*50 + 25e3) flop (SURVEY §8(d)); algorithmic-equivalent: the score skips the second stage of the test for waves of proven outliers, so it executes fewer flops"}})
     return out, (x1, x2, samples)
 
 
