@@ -16,8 +16,9 @@ reduced camera system per iteration.  value = LM iterations / s of the job.
 Also reported: RANSAC hypotheses/s on config 2 (5000 correspondences, 40 %
 outliers, 16384 hypotheses) on rank 0's GPU; the converged RMSE vs the
 reference's least-squares oracle; the roofline of the dominant kernel
-(HIP-event time on the library's own stream); a CPU baseline (the C oracle,
-1 thread, rank 0 at N = 1).
+(HIP-event time on the library's own stream); the CPU baselines of SURVEY
+§8(d) (rank 0, N = 1): the OpenMP Schur-LM on the host's threads, the
+1-thread C oracle, the reference's own loop extrapolated, RANSAC oracles.
 """
 import argparse
 import json
@@ -45,20 +46,20 @@ SWEEP_RANGES = 8  # k_schur_sweep's point ranges (SFM_SWEEP_RANGES default)
 
 def design_bytes(name, n_obs, n_pts, n_pairs, nblocks, ns):
     """Bytes one launch of each kernel family must move in THIS design
-    (the J cache and the Schur records it keeps), per LM
-    iteration -- reported next to the SURVEY §8(d) compulsory bytes, which
+    (DESIGN.md §4's table: no stored Jacobians, the 128-B Schur records), per
+    LM iteration -- reported next to the SURVEY §8(d) compulsory bytes, which
     are the roofline's.  n_pairs: off-diagonal co-observation pairs;
     nblocks: camera blocks i <= j."""
-    if name == "schur_blocks":  # k_schur_sweep + finish: Schur records (p, G, q) 128 B/obs staged once,
-        # staged-slot list 4 B/obs, pair list 4 B/pair, range slab written + read, payload written
+    if name == "schur_blocks":  # k_schur_sweep: Schur records (p, G, q) 128 B/obs staged once, staged-slot
+        # list 4 B/obs, pair list 4 B/pair, range slab written + read, payload written
         return 128 * n_obs + 4 * n_obs + 4 * n_pairs + 2 * 336 * SWEEP_RANGES * nblocks + 8 * (ns * ns + 3 * ns)
-    if name == "point_prep":    # J 96 B + cam 4 B read, Schur record 128 B written per obs; V,g / L,q per pt
-        return (96 + 4 + 128) * n_obs + (72 + 72 + 4) * n_pts
-    if name == "linearize":     # k_linearize: obs, cam read, J 96 B written per obs; X, V,g per pt
-        # + k_camera_lin: J 96 B + camera-major index 4 B per obs
-        return (16 + 4 + 96) * n_obs + (24 + 72 + 4) * n_pts + (96 + 4) * n_obs
-    if name == "backsub_trial": # J, obs, cam per obs; V,g, L,q, X, X' per pt
-        return (96 + 16 + 4) * n_obs + (72 + 72 + 24 + 24 + 4) * n_pts
+    if name == "point_prep":    # DESIGN §4: the 128-B Schur record written + pt, cam indices read per obs;
+        return 136 * n_obs + 148 * n_pts  # V, g read, L, q written, X read per point
+    if name == "linearize":     # k_linearize: obs + cam (24 B/obs incl. the point CSR), X in, V, g out per point;
+        # camera blocks (in the sweep launch): camera-major pt + obs (20 B) + X gather (24 B) per obs
+        return 24 * n_obs + 100 * n_pts + 44 * n_obs
+    if name == "backsub_trial": # cam + obs per obs (the Jacobians recomputed); V,g, L,q, X, X' per pt
+        return 20 * n_obs + 196 * n_pts
     if name == "cholesky":      # the damped reduced system read, factor written and re-read
         return 8 * 3 * ns * ns
     return None
