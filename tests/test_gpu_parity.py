@@ -995,3 +995,49 @@ def test_call_timing_switch(core):
     b0, M0, m0, c0 = out[0][:4]
     for b, M, m, c in (o[:4] for o in out[1:]):
         assert b == b0 and np.array_equal(c, c0) and np.array_equal(m, m0) and np.array_equal(M, M0)
+
+
+def _thresholds_at(d, n=24):
+    """thresholds sitting exactly on (and one ulp either side of) n of the
+    given distances: every one of those pairs lies in the fast test's band"""
+    d = d[np.isfinite(d) & (d > 1e-6) & (d < 1e6)]
+    pick = np.sort(d)[np.linspace(0, len(d) - 1, n).astype(int)]
+    return np.concatenate([pick, np.nextafter(pick, np.inf), np.nextafter(pick, -np.inf)])
+
+
+def test_ransac_fast_tests_exact_at_threshold(core):
+    """The score kernels' fast tests (the two-stage epipolar test with its
+    wave-level outlier skip, the homography transfer-error test) against the
+    exact reference expressions, at thresholds placed exactly on pair
+    distances: the count of one hypothesis (fast path + exact tail) equals
+    the size of the winner's mask, which the select kernel forms with the
+    exact expression, and the standalone exact mask of the same model."""
+    x1, x2, _, _ = syn.two_view(n=3000, seed=11)
+    random.seed(4)
+    sample = np.array([random.sample(range(len(x1)), 8)], dtype=np.int32)
+    b, F, _, _ = core.ransac_f8(x1, x2, sample, 1e3, want_counts=True)
+    assert b == 0
+    h1 = np.column_stack([x1, np.ones(len(x1))])
+    h2 = np.column_stack([x2, np.ones(len(x2))])
+    l2, l1 = h1 @ F.T, h2 @ F
+    e = np.abs(np.sum(h2 * l2, axis=1))
+    d = 0.5 * (e / (np.hypot(l2[:, 0], l2[:, 1]) + 1e-8) + e / (np.hypot(l1[:, 0], l1[:, 1]) + 1e-8))
+    for thr in _thresholds_at(d):
+        b, Fb, mask, counts = core.ransac_f8(x1, x2, sample, float(thr), want_counts=True)
+        exact = core.ransac_mask(x1, x2, F, float(thr), model=8)
+        assert counts[0] == exact.sum(), thr
+        if counts[0] > 0:
+            assert b == 0 and np.array_equal(Fb, F) and np.array_equal(mask, exact), thr
+    # homography: one in-call hypothesis from a fixed stream, thresholds on its transfer errors
+    random.seed(9)
+    b, Hm, _, _, _ = core.ransac_h4_pyrandom(x1, x2, 1, 1e6)
+    assert b == 0
+    p = h1 @ Hm.T
+    t = np.hypot(p[:, 0] / (p[:, 2] + 1e-8) - x2[:, 0], p[:, 1] / (p[:, 2] + 1e-8) - x2[:, 1])
+    for thr in _thresholds_at(t):
+        random.seed(9)
+        b, Hb, mask, counts, _ = core.ransac_h4_pyrandom(x1, x2, 1, float(thr), want_counts=True)
+        exact = core.ransac_mask(x1, x2, Hm, float(thr), model=4)
+        assert counts[0] == exact.sum(), thr
+        if counts[0] > 0:
+            assert np.array_equal(mask, exact), thr
