@@ -65,6 +65,11 @@ struct LocalGroup {
     std::vector<double> result;
     int refs = 0;
     bool aborted = false;  // a rank failed: the others stop waiting and return SFM_ERR_COMM
+    // In-process ranks share one GPU: their persistent solves (gj_solve.hpp)
+    // run one after another (each launch waits for the previous rank's), so
+    // two spinning grids never compete for the CUs.
+    std::mutex solve_mu;
+    hipEvent_t last_solve = nullptr;  // an event of the rank that launched last (not owned)
 };
 
 struct sfm_comm {
@@ -1430,6 +1435,8 @@ struct CamTrialArgs {  // k_chol_backsolve's epilogue (nc = 0: none)
     double *Rt_new, *cam_out;
 };
 
+#include "gj_solve.hpp"  // the persistent block Gauss-Jordan solve (one launch)
+
 template <int TB>
 __global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(double *__restrict__ A, int32_t nsp,
                                                                   double *__restrict__ xg,
@@ -1677,6 +1684,107 @@ static int launch_reduced_solve(int32_t ns, int32_t nsp, const double *payload, 
                                 const CamTrialArgs &ct, const SlabSrc &src = SlabSrc{nullptr, nullptr, 0, 0},
                                 int dpp = 1) {
     return launch_cholesky(payload, ns, lam, A, nsp, b, D, bad, s, tb, gate, ct, src, dpp);
+}
+
+// Persistent Gauss-Jordan solve (gj_solve.hpp): the workgroup layout for
+// nT tiles.  cb = 0: the grid would not fit one workgroup per CU, so the
+// multi-launch Cholesky above runs instead (SFM_SOLVE=chol forces it).
+struct GjPlan {
+    int cb = 0, nseg = 0, ncb = 0;
+    int grid() const { return cb ? ncb * nseg : 0; }
+};
+static GjPlan gj_plan(int nT, int ncu) {
+    GjPlan g;
+    if (const char *e = std::getenv("SFM_SOLVE"))
+        if (std::strcmp(e, "chol") == 0) return g;
+    if (nT > gj::NTMAX) return g;
+    const int nseg = (nT + gj::SR - 1) / gj::SR;
+    const char *fe = std::getenv("SFM_GJ_CB");  // tuning / tests: force the column-block width
+    const int force = fe ? std::atoi(fe) : 0;
+    for (int cb : {gj::SR, 2 * gj::SR}) {
+        if (force && cb != force) continue;
+        const int ncb = (nT + cb - 1) / cb;
+        if (ncb * nseg <= ncu) {
+            g.cb = cb;
+            g.nseg = nseg;
+            g.ncb = ncb;
+            break;
+        }
+    }
+    return g;
+}
+static int device_cus(int device) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n <= 0) n = 256;
+    return n;
+}
+
+// device buffers of one solver instance: panels, L / y copies, flags (zeroed
+// once; epochs only grow), abort word, arrival counter
+struct GjBufs {
+    double *G = nullptr, *L = nullptr, *Y = nullptr;
+    int *flag = nullptr, *err = nullptr;
+    unsigned *arrive = nullptr;
+    static size_t doubles(int nT, int nseg) {
+        return (size_t)nT * nT * 16 * 16 + (size_t)nT * nseg * (256 + 16);
+    }
+    static size_t ints(int nT, int nseg) { return (size_t)nT * nseg + 64; }
+    void carve(double *d, int *i, int nT, int nseg) {
+        G = d;
+        L = G + (size_t)nT * nT * 16 * 16;
+        Y = L + (size_t)nT * nseg * 256;
+        flag = i;
+        err = i + (size_t)nT * nseg;
+        arrive = reinterpret_cast<unsigned *>(i + (size_t)nT * nseg + 32);
+    }
+};
+
+// SFM_GJ_DEBUG=1: the persistent solve records s_memrealtime stamps per
+// (workgroup, panel) into a process-wide device buffer (sfm_gj_debug reads it)
+static long long *g_gj_dbg = nullptr;
+static size_t g_gj_dbg_n = 0;
+static long long *gj_dbg_ptr() {
+    static const bool on = std::getenv("SFM_GJ_DEBUG") && std::atoi(std::getenv("SFM_GJ_DEBUG")) != 0;
+    if (!on) return nullptr;
+    if (!g_gj_dbg) {
+        g_gj_dbg_n = (size_t)256 * 128 * 16;
+        if (hipMalloc(&g_gj_dbg, g_gj_dbg_n * sizeof(long long)) != hipSuccess) return g_gj_dbg = nullptr;
+        (void)hipMemset(g_gj_dbg, 0, g_gj_dbg_n * sizeof(long long));
+    }
+    return g_gj_dbg;
+}
+extern "C" int sfm_gj_debug(long long *out, int64_t n) {
+    SFM_CHECK_ARG(out, "null pointer");
+    if (!g_gj_dbg) return 0;
+    SFM_HIP(hipDeviceSynchronize());
+    SFM_HIP(hipMemcpy(out, g_gj_dbg, std::min<size_t>((size_t)n, g_gj_dbg_n) * sizeof(long long), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+static int launch_gj(const GjPlan &g, int nT, int32_t ns, const double *payload, const double *lam, const GjBufs &b, int epoch, double *x, int *bad, const int *gate,
+                     const CamTrialArgs &ct, hipStream_t s) {
+    gj::Args a;
+    a.payload = payload;
+    a.ns = ns;
+    a.nT = nT;
+    a.cb = g.cb;
+    a.nseg = g.nseg;
+    a.lam = lam;
+    a.gate = gate;
+    a.Gp = b.G;
+    a.Lp = b.L;
+    a.Yp = b.Y;
+    a.flag = b.flag;
+    a.epoch = epoch;
+    a.x = x;
+    a.bad = bad;
+    a.err = b.err;
+    a.arrive = b.arrive;
+    a.ct = ct;
+    a.dbg = gj_dbg_ptr();
+    hipLaunchKernelGGL(gj::k_gj_solve, dim3(g.grid()), dim3(gj::THREADS), 0, s, a);
+    SFM_HIP(hipGetLastError());
+    return 0;
 }
 
 // partial[block][4] = {trial cost, model_p, |dp|^2, |X|^2}
@@ -2137,6 +2245,11 @@ struct sfm_ba_problem {
     hipEvent_t ev[2 * T_NT] = {};
     hipEvent_t ev_it[2 * T_NT * kEvSlots] = {};  // per-iteration timing slots of a batch
     LMState *d_lm = nullptr;
+    // persistent Gauss-Jordan reduced solve (gj_solve.hpp)
+    GjPlan gjp;
+    GjBufs gjb;
+    int gj_epoch = 0;
+    hipEvent_t ev_solve = nullptr;
     double t_acc[T_NT] = {};
     int t_iters = 0;
     std::vector<void *> allocs;
@@ -2148,6 +2261,13 @@ struct sfm_ba_problem {
             if (e) (void)hipEventDestroy(e);
         for (auto &e : ev_it)
             if (e) (void)hipEventDestroy(e);
+        if (ev_solve) {
+            if (comm && comm->local) {
+                std::lock_guard<std::mutex> lk(comm->local->solve_mu);
+                if (comm->local->last_solve == ev_solve) comm->local->last_solve = nullptr;
+            }
+            (void)hipEventDestroy(ev_solve);
+        }
         if (stream) (void)hipStreamDestroy(stream);
     }
     template <class T> int alloc(T *&p, int64_t n) {
@@ -2356,6 +2476,17 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = p->alloc(p->d_bad, 4)) || (rc = p->alloc(p->d_count, 3 * GS_WORDS)) ||
         (rc = p->alloc(p->d_nbig, 1)) || (rc = p->alloc(p->d_gbuf, 6 * (int64_t)nc + 1)))
         return rc;
+    p->gjp = p->tb == 16 ? gj_plan(p->nT, device_cus(device)) : GjPlan{};
+    if (p->gjp.cb) {
+        double *gd = nullptr;
+        int *gi = nullptr;
+        if ((rc = p->alloc(gd, (int64_t)GjBufs::doubles(p->nT, p->gjp.nseg))) ||
+            (rc = p->alloc(gi, (int64_t)GjBufs::ints(p->nT, p->gjp.nseg))))
+            return rc;
+        p->gjb.carve(gd, gi, p->nT, p->gjp.nseg);
+        SFM_HIP(hipMemsetAsync(gi, 0, GjBufs::ints(p->nT, p->gjp.nseg) * sizeof(int), p->stream));
+        SFM_HIP(hipEventCreateWithFlags(&p->ev_solve, hipEventDisableTiming));
+    }
     SFM_HIP(hipHostMalloc((void **)&p->h_ring, kHostRing * sizeof(HostLM), hipHostMallocMapped | hipHostMallocCoherent));
     std::memset((void *)p->h_ring, 0, kHostRing * sizeof(HostLM));
     SFM_HIP(hipHostGetDevicePointer((void **)&p->d_ring, p->h_ring, 0));
@@ -2652,7 +2783,8 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
                        camlin_args(p, true, &p->d_lm[par].run_lin));
     SFM_HIP(hipGetLastError());
     // one rank: the solve's first launch sums the slabs itself (SlabSrc)
-    const bool fin_fused = !p->comm && p->fin_fused;
+    // (the persistent solve reads the finished payload: the finish runs as its own launch)
+    const bool fin_fused = !p->comm && p->fin_fused && !p->gjp.cb;
     if (!fin_fused) {
         hipLaunchKernelGGL(k_schur_finish, dim3(p->sw_nbd), dim3(64), 0, s, p->ns, p->sw_nbd, p->sw_nrange,
                            p->d_sw_blkij, p->d_slab, p->d_camlin, p->d_payload, gst);
@@ -2667,8 +2799,22 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     const CamTrialArgs ct = {p->nc, p->ns, p->d_payload, lam, p->d_Rt, p->d_Rt2, p->d_scal + 4};
     const SlabSrc src = fin_fused ? SlabSrc{p->d_slab, p->d_camlin, p->sw_nbd, p->sw_nrange}
                                   : SlabSrc{nullptr, nullptr, 0, 0};
-    if ((rc = launch_reduced_solve(p->ns, p->nsp, p->d_payload, lam, p->d_A, p->d_b, p->d_D, bad, s, p->tb, gst,
-                                   ct, src, p->chol_dpp)))
+    if (p->gjp.cb) {
+        LocalGroup *lg = p->comm ? p->comm->local : nullptr;
+        std::unique_lock<std::mutex> lk;
+        if (lg) {  // in-process ranks on one GPU: one persistent solve at a time
+            lk = std::unique_lock<std::mutex>(lg->solve_mu);
+            if (lg->last_solve) SFM_HIP(hipStreamWaitEvent(s, lg->last_solve, 0));
+        }
+        if ((rc = launch_gj(p->gjp, p->nT, p->ns, p->d_payload, lam, p->gjb, ++p->gj_epoch, p->d_b, bad, gst,
+                            ct, s)))
+            return rc;
+        if (lg) {
+            SFM_HIP(hipEventRecord(p->ev_solve, s));
+            lg->last_solve = p->ev_solve;
+        }
+    } else if ((rc = launch_reduced_solve(p->ns, p->nsp, p->d_payload, lam, p->d_A, p->d_b, p->d_D, bad, s, p->tb,
+                                          gst, ct, src, p->chol_dpp)))
         return rc;
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SOLVE + 1], s));
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_TRIAL], s));
@@ -2746,6 +2892,7 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
     for (int k = 0; k < kHostRing; ++k) __atomic_store_n(&p->h_ring[k].seq, 0, __ATOMIC_RELAXED);
     hipLaunchKernelGGL(k_lm_reset, dim3(1), dim3(1), 0, s, p->d_lm, o->initial_lambda, p->d_bad);
     SFM_HIP(hipGetLastError());
+    if (p->gjp.cb) SFM_HIP(hipMemsetAsync(p->gjb.err, 0, sizeof(int), s));
     auto account = [&](int j) {  // per-phase event times of iteration j (complete once its state is published)
         const hipEvent_t *e = p->ev_it + (size_t)(j % kEvSlots) * 2 * T_NT;
         for (int k = 0; k < T_NT; ++k) {
@@ -2793,8 +2940,14 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
     }
     // the iterations still in flight (gated off if the solve ended earlier)
     LMState h{};
+    int gj_err = 0;
     SFM_HIP(hipMemcpyAsync(&h, p->d_lm + (it & 1), sizeof h, hipMemcpyDeviceToHost, s));
+    if (p->gjp.cb) SFM_HIP(hipMemcpyAsync(&gj_err, p->gjb.err, sizeof gj_err, hipMemcpyDeviceToHost, s));
     SFM_HIP(hipStreamSynchronize(s));
+    if (gj_err) {
+        set_error("reduced camera solve: a workgroup of the persistent solve timed out waiting for a panel");
+        return SFM_ERR_HIP;
+    }
     if (timed)
         for (int j = std::max(0, it - depth); j < it && j < h.iters; ++j)
             if (p->h_ring[j % kHostRing].st.iters == j + 1) account(j);
@@ -2814,6 +2967,22 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
 
 // Diagnostic entry: solves the SPD system S x = rhs (n x n, row-major) with
 // the reduced-camera solver of sfm_ba_solve (tiled Cholesky).
+// Diagnostic: the published panels of this thread's last persistent reduced
+// solve (sfm_reduced_solve): G [nT][nsp][16], L [nT][nseg][256], y [nT][nseg][16].
+extern "C" int sfm_gj_dump(double *G, double *L, double *Y, int32_t nT, int32_t nseg, int device) {
+    SFM_CHECK_ARG(G && L && Y, "null pointer");
+    ThreadCtx *c = thread_ctx(device);
+    if (!c) return SFM_ERR_HIP;
+    SFM_CHECK_ARG(c->buf[5].bytes >= GjBufs::doubles(nT, nseg) * sizeof(double), "no such solve");
+    GjBufs b;
+    b.carve(c->buf[5].as<double>(), c->buf[6].as<int>(), nT, nseg);
+    SFM_HIP(hipStreamSynchronize(c->stream));
+    SFM_HIP(hipMemcpy(G, b.G, (size_t)nT * nT * 256 * sizeof(double), hipMemcpyDeviceToHost));
+    SFM_HIP(hipMemcpy(L, b.L, (size_t)nT * nseg * 256 * sizeof(double), hipMemcpyDeviceToHost));
+    SFM_HIP(hipMemcpy(Y, b.Y, (size_t)nT * nseg * 16 * sizeof(double), hipMemcpyDeviceToHost));
+    return 0;
+}
+
 extern "C" int sfm_reduced_solve(const double *S, const double *rhs, int32_t n, double *x, int device) {
     SFM_CHECK_ARG(S && rhs && x, "null pointer");
     SFM_CHECK_ARG(n >= 1, "n < 1");
@@ -2821,6 +2990,7 @@ extern "C" int sfm_reduced_solve(const double *S, const double *rhs, int32_t n, 
     if (!c) return SFM_ERR_HIP;
     const int tb = chol_tile(n);
     const int32_t nsp = (n + tb - 1) / tb * tb;
+    const GjPlan gjp = tb == 16 ? gj_plan(nsp / 16, device_cus(device)) : GjPlan{};
     int rc;
     const size_t pb = (size_t)pay_vec_base(n);
     if ((rc = c->buf[0].reserve((pb + 3 * (size_t)n + 1) * sizeof(double))) ||
@@ -2837,9 +3007,35 @@ extern "C" int sfm_reduced_solve(const double *S, const double *rhs, int32_t n, 
     double *d_pay = c->buf[0].as<double>();
     SFM_HIP(hipMemcpyAsync(d_pay, pay.data(), pay.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
     SFM_HIP(hipMemsetAsync(c->buf[4].p, 0, sizeof(int), c->stream));
-    if ((rc = launch_reduced_solve(n, nsp, d_pay, d_pay + pb + 3 * (size_t)n, c->buf[1].as<double>(),
-                                   c->buf[2].as<double>(), c->buf[3].as<double>(), c->buf[4].as<int>(), c->stream,
-                                   tb, nullptr, CamTrialArgs{})))
+    if (gjp.cb) {
+        const int nT = nsp / 16;
+        const size_t nint = GjBufs::ints(nT, gjp.nseg);
+        if ((rc = c->buf[5].reserve(GjBufs::doubles(nT, gjp.nseg) * sizeof(double))) ||
+            (rc = c->buf[6].reserve(nint * sizeof(int))))
+            return rc;
+        if (c->buf[6].p != c->gj_ints) {  // fresh flags: zero them once, epochs restart
+            SFM_HIP(hipMemsetAsync(c->buf[6].p, 0, c->buf[6].bytes, c->stream));
+            c->gj_ints = c->buf[6].p;
+            c->gj_epoch = 0;
+        }
+        GjBufs b;
+        b.carve(c->buf[5].as<double>(), c->buf[6].as<int>(), nT, gjp.nseg);
+        SFM_HIP(hipMemsetAsync(b.err, 0, sizeof(int), c->stream));
+        SFM_HIP(hipMemsetAsync(c->buf[2].p, 0, (size_t)nsp * sizeof(double), c->stream));
+        if ((rc = launch_gj(gjp, nT, n, d_pay, d_pay + pb + 3 * (size_t)n, b,
+                            ++c->gj_epoch, c->buf[2].as<double>(), c->buf[4].as<int>(), nullptr, CamTrialArgs{},
+                            c->stream)))
+            return rc;
+        int err = 0;
+        SFM_HIP(hipMemcpyAsync(&err, b.err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        SFM_HIP(hipStreamSynchronize(c->stream));
+        if (err) {
+            set_error("reduced solve: the persistent solve timed out");
+            return SFM_ERR_HIP;
+        }
+    } else if ((rc = launch_reduced_solve(n, nsp, d_pay, d_pay + pb + 3 * (size_t)n, c->buf[1].as<double>(),
+                                          c->buf[2].as<double>(), c->buf[3].as<double>(), c->buf[4].as<int>(),
+                                          c->stream, tb, nullptr, CamTrialArgs{})))
         return rc;
     int bad = 0;
     SFM_HIP(hipMemcpyAsync(x, c->buf[2].p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, c->stream));

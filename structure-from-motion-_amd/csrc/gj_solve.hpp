@@ -1,0 +1,705 @@
+// Persistent block Gauss-Jordan solve of the damped reduced camera system
+// (S + lambda clamp(diag U)) x = b in ONE launch (round 3).  Replaces the
+// reference's MINPACK dense QR step (Phase 1/BundleAdjustment.py:205-212, via
+// scipy lmdif) on the BA hot path; included by ba.hip after the assembly
+// helpers (SlabSrc, assembled_src) and the 16-pivot DPP tile factor.
+//
+// Why Gauss-Jordan: a tiled Cholesky needs nT = nsp / 16 dependent column
+// steps for the factor and as many again for the back substitution.  As one
+// launch per column (k_chol_col) each step costs a kernel boundary plus a
+// round of cross-XCD tile loads (~5.4 us at cfg4); the back substitution is
+// a further serial chain.  Block Gauss-Jordan with Cholesky pivots
+//   step p:  L_p = chol(A_pp);  G_i = A_ip L_p^-T (every row tile i != p);
+//            y_p = L_p^-1 b_p;  A_ij -= G_i G_j^T (j > p);  b_i -= G_i y_p
+//   end:     x_i = L_i^-T L_i^-1 b_i   (block diagonal left over)
+// has no back substitution at all (its extra flops are off the critical
+// path), and every step's dependency is only "column p+1 updated by panel
+// p".  A_pj (j > p) is never read: the trailing matrix is symmetric, so
+// L_p^-1 A_pj = G_j^T.  Rows above the pivot (already pivoted) keep being
+// updated; a tile (i, j) with p < i < j (the mirror of (j, i)) is not kept
+// and is imported when row i becomes pivoted: A_ij = L_i G_j^T.
+//
+// Work split: workgroup (cb, s) owns the column tiles [cb*CB, cb*CB + CB)
+// restricted to the row tiles [s*SR, s*SR + SR) ("segment" s), plus a
+// replica of the diagonal tile and of b for each of its columns.  Every
+// workgroup of a column block factors each diagonal tile itself (the same
+// operations on the same values, so the same bits), so the next pivot of a
+// column block waits for no other workgroup unless its tile row sits in
+// another segment; panels go between workgroups through global memory
+// (write-through stores, one flag per (panel, segment), epoch-tagged).
+//
+// Waves of a workgroup (dataflow through LDS words, no workgroup barrier in
+// the loop):
+//   W0  the pivot chain: chol_factor16 on the diagonal replica with the
+//       segment's 64 rows of the pivot column on its lanes -> L_p, G rows;
+//   W1  the same chain with b_p on one lane -> y_p (and publishes L_p, y_p);
+//   WL  loader: polls the flags of remote panels / tiles and stages them;
+//   U*  update waves: each owns up to TPW tiles in MFMA C-fragment layout
+//       (v_mfma_f64_16x16x4f64: the VALU stays free for the chains) and
+//       applies every panel; the tiles of column p+1 first (phase A, then
+//       staged for the next chain), the rest after (phase B).
+namespace gj {
+
+constexpr int TL = 16;       // tile
+constexpr int SR = 4;        // row tiles per segment (64 rows: W0's lanes)
+constexpr int CBMAX = 8;     // column tiles per workgroup
+constexpr int NUW = 8;       // update waves
+constexpr int NW = 3 + NUW;  // W0, W1, WL, U0..U7
+constexpr int THREADS = 64 * NW;
+constexpr int TPW = ((SR + 1) * CBMAX + NUW - 1) / NUW;  // tile slots per update wave
+constexpr int LDT = TL + 1;                              // padded LDS row (doubles)
+constexpr int NTMAX = 128;                               // tiles per dimension (host checks)
+constexpr long long POLL_LIMIT = 20000000;               // s_memrealtime ticks (100 MHz): 200 ms
+constexpr unsigned SPIN_CHECK = 1024;                    // polls between two reads of the clock
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+struct Args {
+    const double *payload;  // the finished (all-reduced) Schur payload
+    int32_t ns, nT, cb, nseg;
+    const double *lam;
+    const int *gate;
+    double *Gp;        // [nT][nT*16][16] published panels (G rows)
+    double *Lp;        // [nT][nseg][256] L_p, one copy per producing segment
+    double *Yp;        // [nT][nseg][16]
+    int *flag;         // [nT][nseg] epoch of the last publication
+    int epoch;
+    double *x;         // [nT*16] solution
+    int *bad;          // not positive definite (LM rejects the step)
+    int *err;          // a poll timed out (host reports an error)
+    unsigned *arrive;  // last-block arrivals (the last one runs the epilogue)
+    CamTrialArgs ct;   // trial cameras epilogue (nc = 0: none)
+    long long *dbg;    // diagnostics (nullable): [grid][nT][16] s_memrealtime stamps
+};
+
+// diagnostic stamps (sfm_gj_debug): slot per (workgroup, panel)
+enum { DBG_CST = 0, DBG_CHAIN, DBG_PUB, DBG_LOAD0, DBG_LOADED, DBG_GM, DBG_PHA, DBG_PHB,
+       DBG_W0BUF, DBG_W0GST, DBG_W0LDS, DBG_W0DRAIN, DBG_AGJ, DBG_ACST, DBG_AMMA, DBG_ABB };
+__device__ __forceinline__ void stamp(const Args &a, int p, int slot) {
+    if (a.dbg && (threadIdx.x & 63) == 0) a.dbg[((int64_t)blockIdx.x * a.nT + p) * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+}
+
+struct Smem {
+    // Gm and Gj (adjacent) double as the prologue's staging of the tiles
+    double Gm[2][SR][TL][LDT];     // panel p: G rows of the segment's row tiles
+    double Gj[2][CBMAX][TL][LDT];  // panel p: G tile of each owned column's row
+    double Cst[SR + 1][TL][LDT];   // column p+1 staged for the chain (own tiles | replica)
+    double Ls[2][TL][LDT];         // L_p (the import A_pj = L_p G_j^T)
+    double ys[2][TL];
+    double bb[CBMAX][TL];          // b replica of each owned column's row tile
+    double ob[SR * TL];            // b of the segment's rows (last column block)
+    int gm_ok[2], ly_ok[2], gj_ok[2][CBMAX];  // = p + 1 when panel p's piece is staged
+    int cst_cnt, cst_read, abort_;
+    int pub[NTMAX];    // per pivot: arrivals of the two chain waves (the second one stores the flag)
+    int udone[NTMAX];  // per panel: update waves done with it (groups progress at different rates,
+                       // so a single running count would not say which panels are done)
+    int *err, *bad;  // global: set on an abort (the host reports it, the LM rejects the step)
+};
+
+__device__ __forceinline__ double ld_ag(const double *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_ag(double *p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int lds_ld(const int *w) {
+    return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); }
+__device__ __forceinline__ void lds_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }
+__device__ __forceinline__ void lds_set(int *w, int v) {  // after lds_release()
+    __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_add(int *w, int v) {
+    __hip_atomic_fetch_add(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ long long rtc() { return __builtin_amdgcn_s_memrealtime(); }
+
+__device__ __forceinline__ void abort_solve(Smem &S) {
+    lds_set(&S.abort_, 1);
+    if ((threadIdx.x & 63) == 0) {
+        __hip_atomic_store(S.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(S.bad, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// wait (whole wave) until the LDS word reaches target; false on abort / timeout
+__device__ __forceinline__ bool lds_wait(const int *w, int target, Smem &S) {
+    if (lds_ld(w) >= target) {  // the common case: no clock read, no sleep
+        lds_acquire();
+        return true;
+    }
+    long long t0 = -1;
+    for (unsigned it = 1;; ++it) {
+        __builtin_amdgcn_s_sleep(1);
+        if (lds_ld(w) >= target) break;
+        if (lds_ld(&S.abort_)) return false;
+        if (it % SPIN_CHECK == 0) {  // bounded: a lost hand-off ends the solve, never hangs the GPU
+            const long long t = rtc();
+            if (t0 < 0) t0 = t;
+            else if (t - t0 > POLL_LIMIT) {
+                abort_solve(S);
+                return false;
+            }
+        }
+    }
+    lds_acquire();
+    return true;
+}
+
+// wait (whole wave) for a remote publication: flag >= epoch (relaxed agent
+// loads; the producer's stores are write-through and drained before the flag)
+__device__ __forceinline__ bool flag_wait(const int *f, int epoch, Smem &S) {
+    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= epoch) return true;
+    long long t0 = -1;
+    for (unsigned it = 1;; ++it) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= epoch) return true;
+        if (lds_ld(&S.abort_)) return false;
+        if (it % (SPIN_CHECK / 8) == 0) {
+            const long long t = rtc();
+            if (t0 < 0) t0 = t;
+            else if (t - t0 > POLL_LIMIT) {
+                abort_solve(S);
+                return false;
+            }
+        }
+    }
+}
+
+// acc(r, c) += sa * sum_k Ar[r][k] Br[c][k] on fp64 MFMA 16x16x4 (lane maps
+// checked by tools/mfma_map.hip: A lane l = A[l&15][4q + l>>4], B lane l =
+// B[4q + l>>4][l&15], D lane l element e = D[(l>>4) + 4e][l&15])
+__device__ __forceinline__ d4 mma16(d4 acc, const double (*Ar)[LDT], const double (*Br)[LDT], bool neg, int l) {
+    const int r = l & 15, kq = l >> 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        double av = Ar[r][4 * q + kq];
+        if (neg) av = -av;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Br[r][4 * q + kq], acc, 0, 0, 0);
+    }
+    return acc;
+}
+
+__device__ __forceinline__ double diag_u_src(const Args &a, int i) { return a.payload[pay_vec_base(a.ns) + i]; }
+__device__ __forceinline__ double g_c_src(const Args &a, int i) { return a.payload[pay_vec_base(a.ns) + a.ns + i]; }
+
+// element (I, J) of S + lambda clamp(diag U) from the payload, the lower
+// triangle mirrored (what a Cholesky of S reads), identity on the padding;
+// the loads are issued by the caller (batched)
+struct ElemRef {
+    int64_t idx, dg;  // payload index of S_IJ (-1: padding), of diag U_I (-1: off-diagonal)
+    double pad;       // value on the padding
+};
+__device__ __forceinline__ ElemRef elem_ref(int32_t ns, int I, int J) {
+    if (I < J) {
+        const int t = I;
+        I = J;
+        J = t;
+    }
+    ElemRef r;
+    if (I < ns && J < ns) {
+        r.idx = pay_index(ns, I, J);
+        r.dg = I == J ? pay_vec_base(ns) + I : -1;
+        r.pad = 0.0;
+    } else {
+        r.idx = -1;
+        r.dg = -1;
+        r.pad = I == J ? 1.0 : 0.0;
+    }
+    return r;
+}
+
+struct Geo {
+    int cb, s, j0, j1, ncol, i0, i1, nrow, nT, nseg, wpg;
+    __device__ int seg_of(int tile) const { return tile / SR; }
+    // slot k of update wave u -> owned tile (jj, ii) (ii == SR: the replica),
+    // false if none.  The owned columns are grouped by the segment of their
+    // tile row (CB / SR groups), each group served by its own waves, so a
+    // group whose G tiles come from a lagging workgroup never holds up the
+    // tiles of the pivot column.
+    __device__ __forceinline__ bool slot(int u, int k, int &jj, int &ii) const {
+        const int grp = u / wpg, t = u % wpg + wpg * k, jl = t / (SR + 1);
+        ii = t % (SR + 1);
+        jj = grp * SR + jl;
+        return jl < SR && jj < ncol && (ii == SR || ii < nrow);
+    }
+};
+
+// -------------------------------------------------------------- the chain
+// W0 / W1: pivot p from the staged column (Cst).  W0 carries the segment's
+// rows, W1 the b row; both factor the same replica (same bits).
+__device__ __forceinline__ void chain_pivot(const Args &a, const Geo &g, Smem &S, int p, int wave, int lane) {
+    const int li = lane & 15, grp = lane >> 4, buf = p & 1;
+    double rw[16], pw[16], dinv[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) rw[j] = S.Cst[SR][li][j];
+    if (wave == 0) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) pw[j] = grp < g.nrow ? S.Cst[grp][li][j] : 0.0;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) pw[j] = lane == 0 ? S.bb[p - g.j0][j] : 0.0;
+    }
+    lds_release();
+    if (lane == 0) lds_add(&S.cst_read, 1);  // Cst may be restaged (phase A of panel p)
+    if (wave == 0) stamp(a, p, DBG_CST);
+    chol_factor16(rw, pw, dinv, li, lane, a.bad);
+    if (wave == 0) stamp(a, p, DBG_CHAIN);
+    const int nsp = g.nT * TL;
+    // panel p's buffers were last read by the update waves at panel p - 2
+    if (p >= 2 && !lds_wait(&S.udone[p - 2], NUW, S)) return;
+    if (wave == 0) stamp(a, p, DBG_W0BUF);
+    // LDS first (this workgroup's own next pivot waits on it), then the
+    // global copy for the other workgroups, read back from LDS so that every
+    // store instruction writes 1 KB contiguous (16 B a lane, write-through)
+    if (wave == 0) {
+        if (grp < g.nrow) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) S.Gm[buf][grp][li][j] = pw[j];
+            const int tj = g.i0 + grp - g.j0;  // this row tile is an owned column's row: its G tile is local
+            if (tj >= 0 && tj < g.ncol && g.i0 + grp > p)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) S.Gj[buf][tj][li][j] = pw[j];
+        }
+        lds_release();
+        if (lane == 0) {
+            lds_set(&S.gm_ok[buf], p + 1);
+            for (int gg = 0; gg < g.nrow; ++gg) {
+                const int tj = g.i0 + gg - g.j0;
+                if (tj >= 0 && tj < g.ncol && g.i0 + gg > p) lds_set(&S.gj_ok[buf][tj], p + 1);
+            }
+        }
+        stamp(a, p, DBG_W0LDS);
+        double *dst = a.Gp + ((int64_t)p * nsp + g.i0 * TL) * TL;  // the segment's rows: contiguous
+        const int nel = g.nrow * TL * TL;
+#pragma unroll
+        for (int k = 0; k < SR * TL * TL / 64; ++k) {
+            const int e = lane + 64 * k, row = e >> 4;
+            if (e < nel) st_ag(dst + e, S.Gm[buf][row >> 4][row & 15][e & 15]);
+        }
+        stamp(a, p, DBG_W0GST);
+    } else {
+        if (lane < 16) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) S.Ls[buf][li][j] = j <= li ? rw[j] : 0.0;
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) S.ys[buf][j] = pw[j];
+        }
+        lds_release();
+        if (lane == 0) lds_set(&S.ly_ok[buf], p + 1);
+        double *dl = a.Lp + ((int64_t)p * g.nseg + g.s) * 256;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int e = lane + 64 * k;
+            st_ag(dl + e, S.Ls[buf][e >> 4][e & 15]);
+        }
+        if (lane < 16) st_ag(a.Yp + ((int64_t)p * g.nseg + g.s) * 16 + lane, S.ys[buf][lane]);
+    }
+    // publish: both chain waves drained, the second one to arrive stores the flag
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (wave == 0) stamp(a, p, DBG_W0DRAIN);
+    if (lane == 0) {
+        // a count per pivot: W1 of pivot p + 1 may arrive before W0 of pivot p
+        const int old = __hip_atomic_fetch_add(&S.pub[p], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (old == 1) {
+            __hip_atomic_store(a.flag + (int64_t)p * g.nseg + g.s, a.epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            stamp(a, p, DBG_PUB);
+        }
+    }
+}
+
+// ------------------------------------------------------------- the loader
+// Stages remote pieces of panel p, one producing segment at a time: the
+// segment's flag, then every load from it in one round (the segment's own
+// G rows for a remote panel: 16 doubles a lane; the G tiles of the owned
+// columns whose tile row it holds: up to SR tiles, 16 doubles a lane), then
+// the LDS words.  The segment holding column p+1's tile row goes first.
+__device__ __forceinline__ bool load_segment(const Args &a, const Geo &g, Smem &S, int p, int sg, bool rows,
+                                             unsigned tiles, int lane) {
+    const int nsp = g.nT * TL, buf = p & 1;
+    if (!flag_wait(a.flag + (int64_t)p * g.nseg + sg, a.epoch, S)) return false;
+    stamp(a, p, DBG_LOAD0);
+    // every load in flight at once, 8 B a lane, each instruction 512 B contiguous
+    const bool lrow = rows && p >= g.i0 && p < g.i1;  // row p is this segment's: the import needs L_p
+    const int nre = rows ? g.nrow * TL * TL : 0;
+    double vr[SR * TL * TL / 64], vt[SR][4], vl[4], vy = 0.0;
+    const double *gr = a.Gp + ((int64_t)p * nsp + g.i0 * TL) * TL;
+#pragma unroll
+    for (int k = 0; k < SR * TL * TL / 64; ++k) {
+        const int e = lane + 64 * k;
+        if (e < nre) vr[k] = ld_ag(gr + e);
+    }
+#pragma unroll
+    for (int t = 0; t < SR; ++t)
+        if (tiles >> t & 1) {
+            const double *src = a.Gp + ((int64_t)p * nsp + (sg * SR + t) * TL) * TL;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) vt[t][k] = ld_ag(src + lane + 64 * k);
+        }
+    if (rows) {
+        const double *ls = a.Lp + ((int64_t)p * g.nseg + g.s) * 256;
+        if (lrow)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) vl[k] = ld_ag(ls + lane + 64 * k);
+        if (lane < 16) vy = ld_ag(a.Yp + ((int64_t)p * g.nseg + g.s) * 16 + lane);
+    }
+#pragma unroll
+    for (int k = 0; k < SR * TL * TL / 64; ++k) {
+        const int e = lane + 64 * k, row = e >> 4;
+        if (e < nre) S.Gm[buf][row >> 4][row & 15][e & 15] = vr[k];
+    }
+#pragma unroll
+    for (int t = 0; t < SR; ++t)
+        if (tiles >> t & 1) {
+            const int jj = sg * SR + t - g.j0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int e = lane + 64 * k;
+                S.Gj[buf][jj][e >> 4][e & 15] = vt[t][k];
+            }
+        }
+    if (rows) {
+        if (lrow)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int e = lane + 64 * k;
+                S.Ls[buf][e >> 4][e & 15] = vl[k];
+            }
+        if (lane < 16) S.ys[buf][lane] = vy;
+    }
+    lds_release();
+    stamp(a, p, DBG_LOADED);
+    if (lane == 0) {
+        if (rows) {
+            lds_set(&S.gm_ok[buf], p + 1);
+            lds_set(&S.ly_ok[buf], p + 1);
+        }
+        for (int t = 0; t < SR; ++t)
+            if (tiles >> t & 1) lds_set(&S.gj_ok[buf][sg * SR + t - g.j0], p + 1);
+    }
+    return true;
+}
+
+__device__ __forceinline__ void loader(const Args &a, const Geo &g, Smem &S, int lane) {
+    const int sfirst = g.j0 / SR, slast = (g.j1 - 1) / SR;  // segments of the owned columns' tile rows
+    for (int p = 0; p < g.j1; ++p) {
+        if (p >= 2 && !lds_wait(&S.udone[p - 2], NUW, S)) return;  // buffers of panel p - 2 consumed
+        const bool remote = p < g.j0;
+        // remote G tiles of the owned columns j > p (our own pivot's tiles in our rows come from W0)
+        auto tiles_of = [&](int sg) {
+            unsigned m = 0;
+            for (int t = 0; t < SR; ++t) {
+                const int j = sg * SR + t;
+                if (j >= g.j0 && j < g.j1 && j > p && (remote || sg != g.s)) m |= 1u << t;
+            }
+            return m;
+        };
+        const int scrit = (p + 1 >= g.j0 && p + 1 < g.j1) ? (p + 1) / SR : -1;
+        if (scrit >= 0) {
+            const unsigned m = tiles_of(scrit);
+            const bool rows = remote && scrit == g.s;
+            if ((m || rows) && !load_segment(a, g, S, p, scrit, rows, m, lane)) return;
+        }
+        if (remote && scrit != g.s && !load_segment(a, g, S, p, g.s, true, sfirst <= g.s && g.s <= slast ? tiles_of(g.s) : 0u, lane))
+            return;
+        for (int sg = sfirst; sg <= slast; ++sg) {
+            if (sg == scrit || (remote && sg == g.s)) continue;
+            const unsigned m = tiles_of(sg);
+            if (m && !load_segment(a, g, S, p, sg, false, m, lane)) return;
+        }
+    }
+}
+
+// ------------------------------------------------------------ update waves
+__device__ __forceinline__ void store_cst(Smem &S, int ii, const d4 &acc, int l) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) S.Cst[ii][(l >> 4) + 4 * e][l & 15] = acc[e];
+}
+
+// apply panel p to tile (jj, ii) (ii == SR: the diagonal replica)
+__device__ __forceinline__ void apply_tile(d4 &acc, const Geo &g, Smem &S, int p, int jj, int ii, int l) {
+    const int buf = p & 1, j = g.j0 + jj;
+    if (ii == SR) {
+        acc = mma16(acc, S.Gj[buf][jj], S.Gj[buf][jj], true, l);
+        return;
+    }
+    const int i = g.i0 + ii;
+    if (i == p) {  // row p just pivoted: the kept tile becomes A_pj = L_p G_j^T
+        const d4 z = {0.0, 0.0, 0.0, 0.0};
+        acc = mma16(z, S.Ls[buf], S.Gj[buf][jj], false, l);
+        return;
+    }
+    if (i > p && i < j) return;  // mirror of (j, i): not kept
+    acc = mma16(acc, S.Gm[buf][ii], S.Gj[buf][jj], true, l);
+}
+
+// b replica of column jj: bb -= G_j y_p (16 lanes, a row each)
+__device__ __forceinline__ void apply_bb(Smem &S, int p, int jj, int lane) {
+    const int buf = p & 1;
+    if (lane < 16) {
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc = fma(S.Gj[buf][jj][lane][k], S.ys[buf][k], acc);
+        S.bb[jj][lane] -= acc;
+    }
+}
+
+__device__ __forceinline__ void updater(const Args &a, const Geo &g, Smem &S, int u, int lane, d4 (&acc)[TPW], bool track_ob) {
+    for (int p = 0; p < g.j1; ++p) {
+        const int buf = p & 1;
+        if (!lds_wait(&S.gm_ok[buf], p + 1, S) || !lds_wait(&S.ly_ok[buf], p + 1, S)) return;
+        if (u == 0) stamp(a, p, DBG_GM);
+        // phase A: the tiles of column p + 1, staged for its pivot
+        const int ja = p + 1 - g.j0;
+        bool ok = true;
+        if (ja >= 0 && ja < g.ncol) {
+#pragma unroll
+            for (int k = 0; k < TPW; ++k) {
+                int jj, ii;
+                if (!ok || !g.slot(u, k, jj, ii) || jj != ja) continue;
+                // Cst still holds column p for chain(p) (both chain waves read it)
+                if (!lds_wait(&S.gj_ok[buf][jj], p + 1, S)) {
+                    ok = false;
+                    continue;
+                }
+                stamp(a, p, DBG_AGJ);
+                if (p >= g.j0 && !lds_wait(&S.cst_read, 2 * (p - g.j0 + 1), S)) {
+                    ok = false;
+                    continue;
+                }
+                stamp(a, p, DBG_ACST);
+                apply_tile(acc[k], g, S, p, jj, ii, lane);
+                store_cst(S, ii, acc[k], lane);
+                stamp(a, p, DBG_AMMA);
+                if (ii == SR) apply_bb(S, p, jj, lane);
+                stamp(a, p, DBG_ABB);
+                lds_release();
+                if (lane == 0) lds_add(&S.cst_cnt, 1);
+            }
+        }
+        if (u == 0) stamp(a, p, DBG_PHA);
+        // phase B: every other owned column j > p + 1
+#pragma unroll
+        for (int k = 0; k < TPW; ++k) {
+            int jj, ii;
+            if (!ok || !g.slot(u, k, jj, ii) || g.j0 + jj <= p + 1) continue;
+            if (!lds_wait(&S.gj_ok[buf][jj], p + 1, S)) {
+                ok = false;
+                continue;
+            }
+            apply_tile(acc[k], g, S, p, jj, ii, lane);
+            if (ii == SR) apply_bb(S, p, jj, lane);
+        }
+        if (!ok) return;
+        if (track_ob && u == 0) {  // b of the segment's rows: ob_i -= G_i y_p, i != p
+            const int ti = lane >> 4;
+            if (ti < g.nrow && g.i0 + ti != p) {
+                double s = 0.0;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) s = fma(S.Gm[buf][ti][lane & 15][k], S.ys[buf][k], s);
+                S.ob[lane] -= s;
+            }
+        }
+        lds_release();
+        if (lane == 0) lds_add(&S.udone[p], 1);
+        if (u == 0) stamp(a, p, DBG_PHB);
+    }
+}
+
+// trial cameras and the camera part of the model decrease from dc (LDS),
+// as camera_trial (k_chol_backsolve's epilogue) with the system read from
+// its source; red: 3 x THREADS doubles
+__device__ void cam_trial(const Args &a, const double *dc, double *red) {
+    const CamTrialArgs &ct = a.ct;
+    const double lambda = *a.lam;
+    double m = 0, dn = 0, xn = 0;
+    for (int c = threadIdx.x; c < ct.nc; c += THREADS) {
+        const double *d = dc + 6 * c;
+        double dR[9];
+        rotvec_to_R(d[0], d[1], d[2], dR);
+        const double *R = ct.Rt + 12 * c;
+        double *Rn = ct.Rt_new + 12 * c;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) Rn[3 * i + j] = dR[3 * i] * R[j] + dR[3 * i + 1] * R[3 + j] + dR[3 * i + 2] * R[6 + j];
+        for (int i = 0; i < 3; ++i) {
+            Rn[9 + i] = R[9 + i] + d[3 + i];
+            xn += R[9 + i] * R[9 + i];
+        }
+        for (int i = 0; i < 6; ++i) {
+            m += d[i] * (lambda * clampd(diag_u_src(a, 6 * c + i)) * d[i] - g_c_src(a, 6 * c + i));
+            dn += d[i] * d[i];
+        }
+    }
+    red[threadIdx.x] = m;
+    red[THREADS + threadIdx.x] = dn;
+    red[2 * THREADS + threadIdx.x] = xn;
+    __syncthreads();
+    if (threadIdx.x < 3) {  // fixed order
+        double s = 0.0;
+        for (int t = 0; t < THREADS; ++t) s += red[threadIdx.x * THREADS + t];
+        ct.cam_out[threadIdx.x] = s;
+    }
+}
+
+// x_i = L_i^-T L_i^-1 b_i for the segment's row tiles (W0; 16 lanes a tile)
+__device__ void final_solve(const Args &a, const Geo &g, Smem &S, int lane) {
+    const int li = lane & 15, ti = lane >> 4;
+    const bool act = ti < g.nrow;
+    const int i = g.i0 + (act ? ti : 0);
+    double L[16];  // row li of L_i
+    const double *ls = a.Lp + ((int64_t)i * g.nseg + g.s) * 256 + li * 16;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) L[j] = ld_ag(ls + j);
+    double v = S.ob[lane];
+    // forward: y = L^-1 b (lane li holds y_li when done)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const double lkk = __shfl(L[k], (lane & 48) | k);
+        const double yk = __shfl(v, (lane & 48) | k) / lkk;
+        if (li == k) v = yk;
+        if (li > k) v -= L[k] * yk;
+    }
+    // backward: x = L^-T y; lane li needs L[k][li] (row k of L, column li)
+#pragma unroll
+    for (int k = 15; k >= 0; --k) {
+        const double lkk = __shfl(L[k], (lane & 48) | k);
+        const double xk = __shfl(v, (lane & 48) | k) / lkk;
+        double lki = 0.0;  // L[k][li] from lane k's row
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const double t = __shfl(L[j], (lane & 48) | k);
+            if (j == li) lki = t;
+        }
+        if (li == k) v = xk;
+        if (li < k) v -= lki * xk;
+    }
+    if (act) st_ag(a.x + i * TL + li, v);
+}
+
+__global__ void __launch_bounds__(THREADS) k_gj_solve(Args a) {
+    if (a.gate && !*a.gate) return;  // device-side LM control: iteration gated off
+    __shared__ Smem S;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    Geo g;
+    g.nT = a.nT;
+    g.nseg = a.nseg;
+    g.cb = blockIdx.x / a.nseg;
+    g.s = blockIdx.x % a.nseg;
+    g.j0 = g.cb * a.cb;
+    g.j1 = min(a.nT, g.j0 + a.cb);
+    g.ncol = g.j1 - g.j0;
+    g.i0 = g.s * SR;
+    g.i1 = min(a.nT, g.i0 + SR);
+    g.nrow = g.i1 - g.i0;
+    g.wpg = NUW / (a.cb / SR);
+    const bool last_block = g.j1 == a.nT;
+    const double lambda = *a.lam;
+    // ---- prologue
+    if (threadIdx.x < 2) S.gm_ok[threadIdx.x] = S.ly_ok[threadIdx.x] = 0;
+    if (threadIdx.x < 2 * CBMAX) S.gj_ok[threadIdx.x / CBMAX][threadIdx.x % CBMAX] = 0;
+    if (threadIdx.x < NTMAX) S.pub[threadIdx.x] = S.udone[threadIdx.x] = 0;
+    if (threadIdx.x == 0) {
+        S.cst_cnt = S.cst_read = S.abort_ = 0;
+        S.err = a.err;
+        S.bad = a.bad;
+    }
+    d4 acc[TPW];
+#pragma unroll
+    for (int k = 0; k < TPW; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
+    const int u = wave - 3;
+    // initial tiles, SR owned columns per pass: every thread gathers up to 8
+    // elements from the payload in one round into LDS, then each update wave
+    // takes its fragments (column j0's are staged for pivot j0 if j0 == 0)
+    double *stage = &S.Gm[0][0][0][0];
+    static_assert(offsetof(Smem, Gj) == sizeof(S.Gm) &&
+                      sizeof(S.Gm) + sizeof(S.Gj) >= (SR + 1) * SR * TL * LDT * sizeof(double), "staging");
+    constexpr int EPT = ((SR + 1) * SR * 256 + THREADS - 1) / THREADS;
+    for (int c0 = 0; c0 < g.ncol; c0 += SR) {
+        const int nc = min(SR, g.ncol - c0), nel = nc * (SR + 1) * 256;
+        ElemRef er[EPT];
+        double v[EPT], dg[EPT];
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            const int idx = threadIdx.x + k * THREADS, q = idx >> 8, e = idx & 255;
+            const int jl = q / (SR + 1), ii = q % (SR + 1);
+            const bool ok = idx < nel && (ii == SR || ii < g.nrow);
+            const int ti = ii == SR ? g.j0 + c0 + jl : g.i0 + ii, tj = g.j0 + c0 + jl;
+            er[k] = ok ? elem_ref(a.ns, ti * TL + (e >> 4), tj * TL + (e & 15)) : ElemRef{-1, -1, 0.0};
+        }
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            v[k] = er[k].idx >= 0 ? a.payload[er[k].idx] : er[k].pad;
+            dg[k] = er[k].dg >= 0 ? a.payload[er[k].dg] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            const int idx = threadIdx.x + k * THREADS, q = idx >> 8, e = idx & 255;
+            if (er[k].dg >= 0) v[k] += lambda * clampd(dg[k]);
+            if (idx < nel) stage[(q * TL + (e >> 4)) * LDT + (e & 15)] = v[k];
+        }
+        __syncthreads();
+        if (u >= 0) {
+#pragma unroll
+            for (int k = 0; k < TPW; ++k) {
+                int jj, ii;
+                if (!g.slot(u, k, jj, ii) || jj < c0 || jj >= c0 + nc) continue;
+                const double *tq = stage + ((jj - c0) * (SR + 1) + ii) * TL * LDT;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[k][e] = tq[((lane >> 4) + 4 * e) * LDT + (lane & 15)];
+                if (jj == 0 && g.j0 == 0) store_cst(S, ii, acc[k], lane);  // pivot 0 needs no panel
+            }
+        }
+        __syncthreads();
+    }
+    if (wave == 1) {  // b replicas of the owned columns
+        for (int e = lane; e < g.ncol * TL; e += 64) S.bb[e / TL][e % TL] = assembled_b(a.payload, a.ns, g.j0 * TL + e);
+    } else if (wave == 2 && last_block) {  // b of the segment's rows
+        S.ob[lane] = lane / TL < g.nrow ? assembled_b(a.payload, a.ns, g.i0 * TL + lane) : 0.0;
+    }
+    if (threadIdx.x == 0) S.cst_cnt = g.j0 == 0 ? g.nrow + 1 : 0;  // else staged by panel j0 - 1
+    __syncthreads();
+    // ---- the pivot loop, by role
+    if (wave <= 1) {
+        for (int p = g.j0; p < g.j1; ++p) {
+            if (!lds_wait(&S.cst_cnt, (p - g.j0 + 1) * (g.nrow + 1), S)) break;
+            chain_pivot(a, g, S, p, wave, lane);
+            if (lds_ld(&S.abort_)) break;
+        }
+    } else if (wave == 2) {
+        loader(a, g, S, lane);
+    } else {
+        updater(a, g, S, u, lane, acc, last_block);
+    }
+    // ---- the solution (last column block) and the epilogue (last arrival)
+    if (!last_block) return;
+    __shared__ int last_arrival;
+    if (wave == 0) {
+        bool ok = lds_wait(&S.udone[a.nT - 1], NUW, S);  // every wave is done with every panel
+        if (ok) final_solve(a, g, S, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
+            last_arrival = 0;
+            if (ok) {
+                const unsigned old = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (old == (unsigned)a.nseg - 1) {
+                    last_arrival = 1;
+                    __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (!last_arrival || a.ct.nc <= 0) return;
+    double *dc = &S.Gj[0][0][0][0];  // LDS reused: x, then the reductions
+    double *red = &S.Gm[0][0][0][0];
+    static_assert(sizeof(S.Gm) >= 3 * THREADS * sizeof(double), "reduction scratch");
+    for (int i = threadIdx.x; i < 6 * a.ct.nc; i += THREADS) dc[i] = ld_ag(a.x + i);
+    __syncthreads();
+    cam_trial(a, dc, red);
+}
+
+}  // namespace gj

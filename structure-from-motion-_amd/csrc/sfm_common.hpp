@@ -90,6 +90,8 @@ struct ThreadCtx {
     hipEvent_t ev[8] = {};
     DevBuf buf[12];
     HostBuf pinned;
+    void *gj_ints = nullptr;  // sfm_reduced_solve: the flag buffer its epochs refer to
+    int gj_epoch = 0;
     ~ThreadCtx() {
         if (stream) {
             (void)hipSetDevice(device);
