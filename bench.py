@@ -2,23 +2,26 @@
 "BA LM-iterations/sec + RANSAC hypotheses/sec at 1/2/4/8 MI355X; final
 reproj RMSE vs ref").
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg4|cfg5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg5|cfg4|cfg3]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
-Workload (BASELINE config 4, the one the north-star target is quoted on):
-synthetic BA, 50 cameras / 100k points / 1M observations (sfm_synthetic).
-A step is one LM iteration (damped Schur solve + trial evaluation, plus the
-re-linearisation after an accepted step) of the sparse Schur-complement LM,
-with the problem resident in HBM.  N > 1: points are sharded across ranks
-(strong scaling of the same problem) with one RCCL all-reduce of the
-reduced camera system per iteration.  value = LM iterations / s of the job.
+Headline workload (value): BASELINE config 5, the config the 1/2/4/8 scaling
+curve is quoted on -- synthetic BA, 200 cameras / 500k points / 4M
+observations (sfm_synthetic) -- at every N, so the driver's per-N values
+form that curve.  A step is one LM iteration (damped Schur solve + trial
+evaluation, plus the re-linearisation after an accepted step) of the sparse
+Schur-complement LM with the problem resident in HBM.  N > 1: points are
+sharded across ranks (strong scaling of the same problem), one RCCL
+all-reduce of the reduced camera system per iteration.  value = LM
+iterations / s of the job.
 
-Also reported: RANSAC hypotheses/s on config 2 (5000 correspondences, 40 %
-outliers, 16384 hypotheses) on rank 0's GPU; the converged RMSE vs the
-reference's least-squares oracle; the roofline of the dominant kernel
-(HIP-event time on the library's own stream); the CPU baselines of SURVEY
-§8(d) (rank 0, N = 1): the OpenMP Schur-LM on the host's threads, the
-1-thread C oracle, the reference's own loop extrapolated, RANSAC oracles.
+Also reported: the same record for BASELINE config 4 (50 cams / 100k pts /
+1M obs, the config of the north-star >= 50x target) under "cfg4"; RANSAC
+hypotheses/s on config 2 (5000 correspondences, 40 % outliers, 16384
+hypotheses); converged RMSE vs the reference's least-squares oracle; the
+roofline of the LM iteration; the CPU baselines of SURVEY §8(d) (rank 0,
+N = 1): the OpenMP Schur-LM and RANSAC on the host's threads (a thread
+sweep), the 1-thread C oracle, the reference's own loop extrapolated.
 """
 import argparse
 import json
@@ -60,23 +63,31 @@ def design_bytes(name, n_obs, n_pts, n_pairs, nblocks, ns):
         return 24 * n_obs + 100 * n_pts + 44 * n_obs
     if name == "backsub_trial": # cam + obs per obs (the Jacobians recomputed); V,g, L,q, X, X' per pt
         return 20 * n_obs + 196 * n_pts
-    if name == "cholesky":      # the damped reduced system read, factor written and re-read
-        return 8 * 3 * ns * ns
+    if name == "cholesky":      # the persistent Gauss-Jordan solve: the damped system read once, every
+        # panel (G rows of all nsp rows x 16) written once and read by the column blocks it updates
+        nt = (ns + 15) // 16
+        return 8 * (ns * ns // 2 + 2 * nt * nt * 16 * 16)
     return None
 
 
-PMC_ROUND = "round2"
+PMC_ROUND = "round3"
 
 
-def pmc_iteration():
+def pmc_iteration(workload):
     """HBM bytes per LM iteration by kernel from the committed rocprofv3 PMC
-    passes of tools/ba_once.py (cfg4, 20 fixed iterations from x0 -- the
-    timed region's mix): {kernel: bytes per iteration}, or {}."""
-    path = os.path.join(REPO, "profiles", PMC_ROUND, "pmc_iteration.json")
-    try:
-        return json.load(open(path)).get("bytes_per_iteration", {})
-    except (OSError, ValueError):
-        return {}
+    passes of tools/ba_once.py (the workload, 20 fixed iterations from x0 --
+    the timed region's mix): ({kernel: bytes per iteration}, source path), or
+    ({}, None)."""
+    for rnd, name in ((PMC_ROUND, f"pmc_iteration_{workload}.json"),
+                      ("round2", "pmc_iteration.json" if workload == "cfg4" else None)):
+        if name is None:
+            continue
+        path = os.path.join(REPO, "profiles", rnd, name)
+        try:
+            return json.load(open(path)).get("bytes_per_iteration", {}), f"profiles/{rnd}/{name}"
+        except (OSError, ValueError):
+            continue
+    return {}, None
 
 
 def n_pairs_of(pt_idx):
@@ -93,39 +104,62 @@ def ba_flops(pt_idx, n_cams):
     return float(400 * len(pt_idx) + (108 * k + 216 * k * (k + 1) / 2).sum() + (6 * n_cams) ** 3 / 3)
 
 
-def cpu_baseline_ba(prob, K):
+def _physical_cores():
+    """Physical cores behind the CPUs this process may use (sysfs core ids),
+    or None where sysfs does not say."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+        ids = set()
+        for c in cpus:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            ids.add((open(base + "physical_package_id").read().strip(), open(base + "core_id").read().strip()))
+        return {"physical": len(ids), "logical": len(cpus)}
+    except OSError:
+        return None
+
+
+def cpu_baseline_ba(prob, cams0, sweep, single=True):
     """The CPU legs of SURVEY §8(d) for the BA (rank 0, N = 1; test
     infrastructure only -- the oracle is the checker and the baseline, never
     the product):
-      * CPU-strong: the OpenMP Schur-LM (oracle/sfm_cpu_strong.c) on all
-        OMP_NUM_THREADS host threads, full problem to convergence;
-      * the 1-thread C Schur-LM (oracle/sfm_oracle.c), full problem;
+      * CPU-strong: the OpenMP Schur-LM (oracle/sfm_cpu_strong.c) at every
+        thread count of `sweep`; at cfg4 to convergence, at cfg5 a bounded 3
+        iterations per point (LM-it/s = iterations / wall time);
+      * (single) the 1-thread C Schur-LM (oracle/sfm_oracle.c) to convergence;
       * the reference's own path priced by its residual loop
         (oracle/ref_loop.py, the reference loop structure call for call) on a
         bounded sample of observations: one lmdif Jacobian = (n + 1)
         residual evaluations (extrapolated, labelled as such)."""
     import oracle as O  # test infrastructure: the CPU restatement, timed as the baseline
     import ref_loop
-    cams0 = np.column_stack([prob["rotvec0"], np.einsum("nij,nj->ni", -prob["R0"], prob["C0"])])
     args = (cams0, prob["X0"], prob["cam_idx"], prob["pt_idx"], prob["obs"], K)
-    t = time.perf_counter()
-    _, _, srep = O.ba_lm_cpu_strong(*args, max_iterations=50)
-    ts = time.perf_counter() - t
-    t = time.perf_counter()
-    _, _, orep = O.ba_lm(*args, max_iterations=50)
-    to = time.perf_counter() - t
+    iters = 50 if single else 3
+    strong = {}
+    for t in sweep:
+        O.set_threads(t)
+        t0 = time.perf_counter()
+        _, _, srep = O.ba_lm_cpu_strong(*args, max_iterations=iters)
+        ts = time.perf_counter() - t0
+        strong[t] = (srep["iterations"] / ts, srep, ts)
+    O.set_threads(max(sweep))
+    out = dict(strong=strong)
+    if single:
+        t0 = time.perf_counter()
+        _, _, orep = O.ba_lm(*args, max_iterations=50)
+        to = time.perf_counter() - t0
+        out["oracle"] = (orep["iterations"] / to, orep, to)
     # reference residual loop on a bounded sample of observations
     n_s = 20000
     nc, npt = prob["n_cams"], prob["n_pts"]
     params = np.concatenate([cams0.ravel(), prob["X0"].ravel()])
-    t = time.perf_counter()
+    t0 = time.perf_counter()
     ref_loop.residuals(params, nc, npt, prob["cam_idx"][:n_s], prob["pt_idx"][:n_s], prob["obs"][:n_s], K)
-    per_obs = (time.perf_counter() - t) / n_s
+    per_obs = (time.perf_counter() - t0) / n_s
     n_par = 6 * nc + 3 * npt
     eval_s = per_obs * len(prob["cam_idx"])
-    return dict(strong=(srep["iterations"] / ts, srep, ts), oracle=(orep["iterations"] / to, orep, to),
-                ref=dict(per_obs_us=per_obs * 1e6, eval_s=eval_s, n_params=n_par,
-                         jacobian_s=eval_s * (n_par + 1), sample_obs=n_s))
+    out["ref"] = dict(per_obs_us=per_obs * 1e6, eval_s=eval_s, n_params=n_par,
+                      jacobian_s=eval_s * (n_par + 1), sample_obs=n_s)
+    return out
 
 
 def cpu_cfg3_as_shipped():
@@ -154,12 +188,20 @@ def cpu_cfg3_as_shipped():
                     "returns x0 unchanged here (SURVEY §0.4)"}
 
 
-def cpu_baseline_ransac(x1, x2, samples, thr=0.06):
+def cpu_baseline_ransac(x1, x2, samples, sweep, thr=0.06):
+    """The OpenMP RANSAC (cs_ransac) over the thread sweep, all hypotheses;
+    returns the fastest point (hyps/s, seconds, threads)."""
     import oracle as O
-    t = time.perf_counter()
-    O.ransac(x1, x2, samples, thr)
-    dt = time.perf_counter() - t
-    return len(samples) / dt, dt
+    best = None
+    for t in sweep:
+        O.set_threads(t)
+        t0 = time.perf_counter()
+        O.ransac_cpu_strong(x1, x2, samples, thr)
+        dt = time.perf_counter() - t0
+        if best is None or dt < best[1]:
+            best = (len(samples) / dt, dt, t)
+    O.set_threads(max(sweep))
+    return best
 
 
 K = syn.K_REF
@@ -328,12 +370,108 @@ def ransac_leg(args, world, rank, local_rank, comm):
     return out, (x1, x2, samples)
 
 
+def ba_leg(workload, args, world, rank, local_rank, comm, barrier, allmax):
+    """One BA workload: the converged solve (RMSE), W warmup + K timed LM
+    iterations from x0 (barrier + synchronize around, max over ranks), and a
+    second run of the same K iterations with HIP events on for the per-phase
+    split (each event record costs the stream a few us, so the timed run has
+    none).  Every rank builds the same problem and keeps its point shard."""
+    prob = syn.ba_problem_cfg(workload, dense=False)
+    cams0 = np.column_stack([prob["rotvec0"], np.einsum("nij,nj->ni", -prob["R0"], prob["C0"])])
+    ci, pi, ob, X0, (lo, hi) = sfm_dist.shard_ba(prob["cam_idx"], prob["pt_idx"], prob["obs"], prob["X0"],
+                                                 world, rank)
+    ba = core.BAProblem(cams0, X0, ci, pi, ob, K, comm=comm, device=local_rank)
+    ba.reset()
+    conv = ba.solve(max_iterations=100)
+    ba.reset()
+    ba.solve(max_iterations=args.warmup, fixed_iterations=True)
+    ba.reset()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rep = ba.solve(max_iterations=args.steps, fixed_iterations=True)
+    torch.cuda.synchronize()
+    barrier()
+    dt = allmax(time.perf_counter() - t0)
+    ba.reset()
+    ba.set_timing(True)
+    ba.solve(max_iterations=args.steps, fixed_iterations=True)
+    ktimes = ba.kernel_times()
+    ba.set_timing(False)
+    ba.close()
+    return dict(workload=workload, prob=prob, cams0=cams0, dt=dt, rep=rep, conv=conv, ktimes=ktimes,
+                hi=hi, n_obs_local=len(ci), n_pts_local=len(X0))
+
+
+def ba_record(leg, args, world):
+    """The bench-line fields of one BA leg (value, roofline, fp64, per-kernel
+    split, step mix, RMSE)."""
+    prob, workload = leg["prob"], leg["workload"]
+    n_obs_total, n_pts_total = len(prob["cam_idx"]), prob["n_pts"]
+    n_pairs = n_pairs_of(prob["pt_idx"][prob["pt_idx"] < leg["hi"]] if world > 1 else prob["pt_idx"])
+    ns = 6 * prob["n_cams"]
+    nblocks = prob["n_cams"] * (prob["n_cams"] + 1) // 2
+    ms_per_step = leg["dt"] / args.steps * 1e3
+    # roofline of the LM iteration (SURVEY §8(d)): compulsory bytes of the
+    # minimal three-pass design, B_iter = 52 N_obs + 240 N_pts, against the
+    # measured time of an iteration (ms_per_step)
+    iter_bytes = 52 * n_obs_total + 240 * n_pts_total
+    ach = iter_bytes / (ms_per_step * 1e-3) / 1e9
+    pmc, pmc_src = pmc_iteration(workload) if world == 1 else ({}, None)
+    roof = {"kernel": "LM iteration (all kernels of one damped solve + trial evaluation)", "bound": "hbm",
+            "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
+            "traffic": int(sum(pmc.values())) if pmc else None, "algorithmic_bytes": int(iter_bytes),
+            "formula": "52*N_obs + 240*N_pts per iteration (SURVEY §8(d)), / ms_per_step",
+            "traffic_source": (f"{pmc_src} (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE passes of tools/ba_once.py "
+                               f"{workload}; (2*FETCH+WRITE) KiB summed over the kernels / iterations)")
+            if pmc else None}
+    flops = ba_flops(prob["pt_idx"], prob["n_cams"])
+    kern = {}
+    for k, v in leg["ktimes"].items():
+        e = {"ms": round(v, 4)}
+        d = design_bytes(k, leg["n_obs_local"], leg["n_pts_local"], n_pairs, nblocks, ns)
+        if d is not None:
+            e["design_bytes"] = int(d)
+            e["design_GBs"] = round(d / (v * 1e-3) / 1e9, 1) if v > 0 else None
+        if k == "cholesky":
+            e["flops"] = ns ** 3 / 3
+            e["tflops"] = round(ns ** 3 / 3 / (v * 1e-3) / 1e12, 4) if v > 0 else None
+            e["note"] = "reduced camera solve: persistent block Gauss-Jordan (one launch); flops = n^3/3 (Cholesky)"
+        kern[k] = e
+    conv, rep = leg["conv"], leg["rep"]
+    return {
+        "value": round(args.steps / leg["dt"], 3),
+        "unit": "LM-iterations/s",
+        "ms_per_step": round(ms_per_step, 4),
+        "workload": f"{workload}: BA {prob['n_cams']} cams / {n_pts_total} pts / {n_obs_total} obs, "
+                    f"Schur-complement LM, points sharded over {world} rank(s)",
+        "roofline": roof,
+        "fp64": {"flops_per_iteration": flops, "achieved_tflops": round(flops / (ms_per_step * 1e-3) / 1e12, 3),
+                 "peak_tflops": FP64_PEAK_TFLOPS,
+                 "frac": round(flops / (ms_per_step * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 5),
+                 "formula": "400 N_obs + sum_p(108 k_p + 216 k_p(k_p+1)/2) + (6 n_c)^3/3 (SURVEY §8(d))"},
+        "kernels_ms_per_iter": kern,
+        "pmc_bytes_per_iter": {k: int(v) for k, v in pmc.items()} if pmc else None,
+        "step_mix": {"timed_steps": args.steps, "accepted": rep["accepted"],
+                     "note": "fixed iterations from x0; the problem converges in ~5, later steps are rejected "
+                             "(a rejected step skips k_linearize / the camera blocks)",
+                     "converged_solve": {"iterations": conv["iterations"], "accepted": conv["accepted"],
+                                         "loop_ms": round(conv["t_loop_ms"], 3),
+                                         "ms_per_iteration": round(conv["t_loop_ms"] / max(1, conv["iterations"]), 4)}},
+        "rmse": {f"{workload}_initial": round(syn.rmse_from_cost(conv["cost0"], n_obs_total), 6),
+                 f"{workload}_gpu": round(syn.rmse_from_cost(conv["cost"], n_obs_total), 6),
+                 "lm_iterations": conv["iterations"]},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="cfg4", choices=["cfg3", "cfg4", "cfg5"])
+    ap.add_argument("--workload", default="cfg5", choices=["cfg3", "cfg4", "cfg5"],
+                    help="headline BA workload (value); cfg5 is BASELINE's scaling config")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the cfg4 (north-star) sub-record")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ransac-hyps", type=int, default=16384)
     ap.add_argument("--force-comm", action="store_true", help="use the RCCL communicator even with one rank")
@@ -361,47 +499,18 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         return float(t.item())
 
-    # ---------------- BA workload (every rank generates the same problem)
-    K = syn.K_REF
-    prob = syn.ba_problem_cfg(args.workload, dense=False)
-    cams0 = np.column_stack([prob["rotvec0"], np.einsum("nij,nj->ni", -prob["R0"], prob["C0"])])
-    ci, pi, ob, X0, (lo, hi) = sfm_dist.shard_ba(prob["cam_idx"], prob["pt_idx"], prob["obs"], prob["X0"],
-                                                 world, rank)
     comm = None
     if world > 1 or args.force_comm:
         uid = [core.Comm.unique_id() if rank == 0 else None]
         if world > 1:
             torch.distributed.broadcast_object_list(uid, src=0)
         comm = core.Comm(uid[0], world, rank, device=local_rank)
-    ba = core.BAProblem(cams0, X0, ci, pi, ob, K, comm=comm, device=local_rank)
 
-    # converged solve (RMSE vs the oracle / the reference's least-squares solution)
-    ba.reset()
-    conv = ba.solve(max_iterations=100)
-    n_obs_total = len(prob["cam_idx"])
-    rmse0 = syn.rmse_from_cost(conv["cost0"], n_obs_total)
-    rmse = syn.rmse_from_cost(conv["cost"], n_obs_total)
-
-    # warmup, then exactly K timed LM iterations from the initial state
-    ba.reset()
-    ba.solve(max_iterations=args.warmup, fixed_iterations=True)
-    ba.reset()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    rep = ba.solve(max_iterations=args.steps, fixed_iterations=True)
-    torch.cuda.synchronize()
-    barrier()
-    dt = allmax(time.perf_counter() - t0)
-    # per-phase times from a second, separate run of the same K iterations with
-    # HIP events on (each event record costs the stream a few us, so the timed
-    # run above has none)
-    ba.reset()
-    ba.set_timing(True)
-    ba.solve(max_iterations=args.steps, fixed_iterations=True)
-    ktimes = ba.kernel_times()
-    ba.set_timing(False)
-    ba.close()
+    # ---------------- BA: the headline workload, then the cfg4 sub-record
+    legs = [ba_leg(args.workload, args, world, rank, local_rank, comm, barrier, allmax)]
+    second = None if args.no_secondary else ("cfg4" if args.workload != "cfg4" else None)
+    if second:
+        legs.append(ba_leg(second, args, world, rank, local_rank, comm, barrier, allmax))
 
     # ---------------- RANSAC (config 2)
     ransac, (x1, x2, samples) = ransac_leg(args, world, rank, local_rank, comm)
@@ -413,70 +522,32 @@ def main():
             torch.distributed.destroy_process_group()
         return
 
-    n_pts_total = prob["n_pts"]
-    n_pairs = n_pairs_of(prob["pt_idx"][prob["pt_idx"] < hi] if world > 1 else prob["pt_idx"])
-    ns = 6 * prob["n_cams"]
-    nblocks = prob["n_cams"] * (prob["n_cams"] + 1) // 2
-    ms_per_step = dt / args.steps * 1e3
-    # roofline of the LM iteration: compulsory bytes of the
-    # minimal three-pass design, B_iter = 52 N_obs + 240 N_pts, against the
-    # measured time of an iteration (ms_per_step)
-    iter_bytes = 52 * n_obs_total + 240 * n_pts_total
-    ach = iter_bytes / (ms_per_step * 1e-3) / 1e9
-    single = args.workload == "cfg4" and world == 1  # the configuration the PMC passes profiled
-    pmc = pmc_iteration() if single else {}
-    roof = {"kernel": "LM iteration (all kernels of one damped solve + trial evaluation)", "bound": "hbm",
-            "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
-            "traffic": int(sum(pmc.values())) if pmc else None, "algorithmic_bytes": int(iter_bytes),
-            "formula": "52*N_obs + 240*N_pts per iteration (SURVEY §8(d)), / ms_per_step",
-            "traffic_source": f"profiles/{PMC_ROUND}/pmc_iteration.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
-                              "passes of tools/ba_once.py; (2*FETCH+WRITE) KiB summed over the kernels / iterations)"}
-    flops = ba_flops(prob["pt_idx"], prob["n_cams"])
-    n_obs_local, n_pts_local = len(ci), len(X0)
-    kern = {}
-    for k, v in ktimes.items():
-        e = {"ms": round(v, 4)}
-        d = design_bytes(k, n_obs_local, n_pts_local, n_pairs, nblocks, ns)
-        if d is not None:
-            e["design_bytes"] = int(d)
-            e["design_GBs"] = round(d / (v * 1e-3) / 1e9, 1) if v > 0 else None
-        if k == "cholesky":
-            e["flops"] = ns ** 3 / 3
-            e["tflops"] = round(ns ** 3 / 3 / (v * 1e-3) / 1e12, 4) if v > 0 else None
-        kern[k] = e
+    head = ba_record(legs[0], args, world)
     out = {
         "metric": "BA LM-iterations/sec (+ RANSAC hypotheses/sec, final reproj RMSE vs ref)",
-        "value": round(args.steps / dt, 3),
+        "value": head["value"],
         "unit": "LM-iterations/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 4),
+        "ms_per_step": head["ms_per_step"],
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (sfm_synthetic.ba_problem, seed 3)",
-        "config": {"workload": f"{args.workload}: BA {prob['n_cams']} cams / {n_pts_total} pts / "
-                               f"{n_obs_total} obs, Schur-complement LM, points sharded over {world} rank(s)",
+        "config": {"workload": head["workload"],
                    "parallelism": f"point-shard x{world} + RCCL all-reduce of the reduced camera system"},
-        "roofline": roof,
-        "fp64": {"flops_per_iteration": flops, "achieved_tflops": round(flops / (ms_per_step * 1e-3) / 1e12, 3),
-                 "peak_tflops": FP64_PEAK_TFLOPS,
-                 "frac": round(flops / (ms_per_step * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 5),
-                 "formula": "400 N_obs + sum_p(108 k_p + 216 k_p(k_p+1)/2) + (6 n_c)^3/3 (SURVEY §8(d))"},
-        "kernels_ms_per_iter": kern,
-        "pmc_bytes_per_iter": {k: int(v) for k, v in pmc.items()} if pmc else None,
-        "step_mix": {"timed_steps": args.steps, "accepted": rep["accepted"],
-                     "note": "fixed iterations from x0; the problem converges in ~5, later steps are rejected "
-                             "(a rejected step skips k_linearize / k_camera_lin)",
-                     "converged_solve": {"iterations": conv["iterations"], "accepted": conv["accepted"],
-                                         "loop_ms": round(conv["t_loop_ms"], 3),
-                                         "ms_per_iteration": round(conv["t_loop_ms"] / max(1, conv["iterations"]), 4)}},
-        "rmse": {f"{args.workload}_initial": round(rmse0, 6), f"{args.workload}_gpu": round(rmse, 6),
-                 "lm_iterations": conv["iterations"]},
+        "roofline": head["roofline"],
+        "fp64": head["fp64"],
+        "kernels_ms_per_iter": head["kernels_ms_per_iter"],
+        "pmc_bytes_per_iter": head["pmc_bytes_per_iter"],
+        "step_mix": head["step_mix"],
+        "rmse": head["rmse"],
         "ransac": ransac,
     }
+    if second:
+        out[second] = ba_record(legs[1], args, world)
     if world == 1:
         out["rmse"].update(cfg3_rmse_vs_reference())
     cpu_leg = world == 1 and not args.no_cpu_baseline
@@ -485,34 +556,51 @@ def main():
     if not args.no_next_rows:
         out["next_rows"] = next_rows(core, local_rank, cpu_leg)
     if cpu_leg:
-        legs = cpu_baseline_ba(prob, K)
-        sv, srep, sdt = legs["strong"]
-        ov, orep, odt = legs["oracle"]
-        out["rmse"][f"{args.workload}_oracle"] = round(syn.rmse_from_cost(orep["cost"], n_obs_total), 6)
-        rv, rdt = cpu_baseline_ransac(x1, x2, samples)
+        import oracle as O  # test infrastructure: the CPU restatement, timed as the baseline
+        avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+        sweep = sorted({t for t in (1, 4, 16, min(64, avail)) if t <= avail})
+        cpu = {}
+        for i, leg in enumerate(legs):
+            rec = out if i == 0 else out[leg["workload"]]
+            base = cpu_baseline_ba(leg["prob"], leg["cams0"], sweep, single=leg["workload"] != "cfg5")
+            best_t = max(base["strong"], key=lambda t: base["strong"][t][0])
+            sv, srep, sdt = base["strong"][best_t]
+            n_obs_total = len(leg["prob"]["cam_idx"])
+            if "oracle" in base:
+                rec["rmse"][f"{leg['workload']}_oracle"] = round(syn.rmse_from_cost(base["oracle"][1]["cost"], n_obs_total), 6)
+            cpu[leg["workload"]] = {
+                "value": round(sv, 4), "unit": "LM-iterations/s", "cores": best_t, "kind": "port",
+                "sample": f"CPU-strong OpenMP Schur-LM (oracle/sfm_cpu_strong.c), full {leg['workload']} problem, "
+                          f"{srep['iterations']} LM iterations to convergence in {sdt:.2f}s on {best_t} threads "
+                          f"(the fastest of the thread sweep)",
+                "speedup": round(rec["value"] / sv, 1),
+                "thread_sweep": {str(t): {"LM_it_per_s": round(v[0], 4), "s": round(v[2], 3)}
+                                 for t, v in sorted(base["strong"].items())},
+                "reference_extrapolated": base["ref"]}
+            if "oracle" in base:
+                ov, orep, odt = base["oracle"]
+                cpu[leg["workload"]]["single_thread_oracle"] = {
+                    "value": round(ov, 4), "unit": "LM-iterations/s", "cores": 1,
+                    "sample": f"C Schur-LM (oracle/sfm_oracle.c), {orep['iterations']} iterations in {odt:.2f}s"}
+        rv, rdt, rth = cpu_baseline_ransac(x1, x2, samples, sweep)
         c1 = cpu_cfg1()
-        ref = legs["ref"]
-        out["cpu_baseline"] = {
-            "value": round(sv, 4), "unit": "LM-iterations/s", "cores": srep["threads"], "kind": "port",
-            "sample": f"CPU-strong OpenMP Schur-LM (oracle/sfm_cpu_strong.c), full {args.workload} problem, "
-                      f"{srep['iterations']} LM iterations to convergence in {sdt:.2f}s on {srep['threads']} threads",
-            "speedup": round(out["value"] / sv, 1),
-            "single_thread_oracle": {"value": round(ov, 4), "unit": "LM-iterations/s", "cores": 1,
-                                     "sample": f"C Schur-LM (oracle/sfm_oracle.c), {orep['iterations']} iterations "
-                                               f"in {odt:.2f}s"},
-            "reference_extrapolated": {
-                "residual_us_per_obs": round(ref["per_obs_us"], 3), "residual_eval_s": round(ref["eval_s"], 3),
-                "lmdif_jacobian_s": round(ref["jacobian_s"], 1), "n_params": ref["n_params"],
-                "note": f"EXTRAPOLATED: the reference residual loop (oracle/ref_loop.py) timed on "
-                        f"{ref['sample_obs']} observations, x N_obs per evaluation, x (n+1) evaluations per "
-                        f"MINPACK forward-difference Jacobian (one LM iteration of the shipped path)"},
+        head_cpu = cpu[args.workload]
+        out["cpu_baseline"] = dict(head_cpu)
+        if second:
+            out[second]["cpu_baseline"] = cpu[second]
+        out["cpu_baseline"].update({
             "cfg3_as_shipped": cpu_cfg3_as_shipped(),
-            "ransac_cfg2": {"hyps_per_s": round(rv, 1), "sample": f"C oracle, all {len(samples)} cfg2 hypotheses "
-                                                                  f"in {rdt:.2f}s, 1 thread"},
+            "ransac_cfg2": {"hyps_per_s": round(rv, 1), "cores": rth,
+                            "sample": f"OpenMP RANSAC (sfm_cpu_strong.c cs_ransac: hypotheses split over {rth} "
+                                      f"threads, same counts as the oracle), all {len(samples)} cfg2 hypotheses in "
+                                      f"{rdt:.2f}s"},
             "ransac_cfg1": c1,
-            "cpu": _cpu_model(), "os_cpu_count": os.cpu_count(),
+            "cpu": _cpu_model(), "os_cpu_count": os.cpu_count(), "cpus_available_to_this_process": avail,
+            "physical_cores": _physical_cores(),
+            "threads_note": "thread counts beyond the CPUs this process may use are not run; the sweep's "
+                            "fastest point is the baseline",
             "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"),
-            "OPENBLAS_NUM_THREADS": os.environ.get("OPENBLAS_NUM_THREADS")}
+            "OPENBLAS_NUM_THREADS": os.environ.get("OPENBLAS_NUM_THREADS")})
     print(json.dumps(out))
     if world > 1:
         torch.distributed.destroy_process_group()

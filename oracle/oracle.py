@@ -54,6 +54,13 @@ def lib():
         L.orc_f8.restype = ctypes.c_int
         L.orc_ransac_score.argtypes = [_d, _d, ctypes.c_int64, _d, ctypes.c_int64, ctypes.c_double, _i32]
         L.orc_ransac_mask.argtypes = [_d, _d, ctypes.c_int64, _d, ctypes.c_double, _u8]
+        L.orc_epi_err.argtypes = [_d, _d, ctypes.c_int64, _d, _d]
+        L.cs_ransac.argtypes = [_d, _d, ctypes.c_int64, _i32, ctypes.c_int64, ctypes.c_int, ctypes.c_double, _i32]
+        L.cs_ransac.restype = ctypes.c_int64
+        L.cs_set_threads.argtypes = [ctypes.c_int]
+        L.cs_max_threads.restype = ctypes.c_int
+        L.orc_hom_err.argtypes = [_d, _d, ctypes.c_int64, _d, _d]
+        L.orc_pnp_err.argtypes = [_d, _d, ctypes.c_int64, _d, _d, _d, _d]
         L.orc_ransac.argtypes = [_d, _d, ctypes.c_int64, _i32, ctypes.c_int64, ctypes.c_int,
                                  ctypes.c_double, _i32, _d, _u8]
         L.orc_ransac.restype = ctypes.c_int64
@@ -118,6 +125,30 @@ def ransac_mask(x1, x2, F, thr=0.06):
     m = np.zeros(len(x1), dtype=np.uint8)
     lib().orc_ransac_mask(_p(x1), _p(x2), len(x1), _p(F), thr, _p(m, _u8))
     return m.astype(bool)
+
+
+def epi_err(x1, x2, F):
+    """Per-pair symmetric epipolar error (GetInliersRANSAC.py:67-78)."""
+    x1, x2, F = f64(x1), f64(x2), f64(F)
+    err = np.zeros(len(x1))
+    lib().orc_epi_err(_p(x1), _p(x2), len(x1), _p(F), _p(err))
+    return err
+
+
+def hom_err(x1, x2, H):
+    """Per-pair homography transfer error (GetHomographyInliers.py:134-146)."""
+    x1, x2, H = f64(x1), f64(x2), f64(H)
+    err = np.zeros(len(x1))
+    lib().orc_hom_err(_p(x1), _p(x2), len(x1), _p(H), _p(err))
+    return err
+
+
+def pnp_err(X, x, K, C, R):
+    """Per-point reprojection error of one pose (PnPRANSAC.py:60-68)."""
+    X, x, K, C, R = f64(X), f64(x), f64(K), f64(C), f64(R)
+    err = np.zeros(len(X))
+    lib().orc_pnp_err(_p(X), _p(x), len(X), _p(K), _p(C), _p(R), _p(err))
+    return err
 
 
 def ransac(x1, x2, samples, thr=0.06):
@@ -264,6 +295,23 @@ def ba_lm_cpu_strong(cams, pts, cam_idx, pt_idx, obs, K, max_iterations=100, fto
         raise RuntimeError(f"cs_ba_lm failed: {rc}")
     return cams, pts, dict(iterations=rep.iterations, accepted=rep.accepted, status=rep.status,
                            threads=rep.threads, cost0=rep.cost0, cost=rep.cost)
+
+
+def ransac_cpu_strong(x1, x2, samples, thr=0.06):
+    """The OpenMP RANSAC (sfm_cpu_strong.c cs_ransac): hypotheses split over
+    the threads, same counts and winner as ransac().  Returns (best, counts)."""
+    x1, x2 = f64(x1), f64(x2)
+    samples = np.ascontiguousarray(samples, dtype=np.int32)
+    H, k = samples.shape
+    counts = np.zeros(H, dtype=np.int32)
+    best = lib().cs_ransac(_p(x1), _p(x2), len(x1), _p(samples, _i32), H, k, thr, _p(counts, _i32))
+    return int(best), counts
+
+
+def set_threads(n):
+    """Thread count of the OpenMP CPU legs (cs_*); returns the count in effect."""
+    lib().cs_set_threads(int(n))
+    return int(lib().cs_max_threads())
 
 
 def rotvec_to_R(w):

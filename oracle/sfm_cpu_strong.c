@@ -326,3 +326,42 @@ int cs_ba_lm(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const int3
     free(dp); free(Xn); free(U); free(gc); free(S); free(b); free(St); free(bt); free(Ut);
     return 0;
 }
+
+/* ---------------------------------------------------------------------
+ * CPU-strong RANSAC (bench.py's cpu leg): orc_ransac's loop with the
+ * hypotheses split over the OpenMP threads (each fits its F with orc_f8 and
+ * counts with orc_ransac_score), then the reference's strict-'>' winner
+ * (GetInliersRANSAC.py:85-88: most inliers, earliest iteration) in
+ * iteration order.  Same counts as orc_ransac.
+ * --------------------------------------------------------------------- */
+int orc_f8(const double *p1, const double *p2, int64_t n, double *F_out);
+void orc_ransac_score(const double *x1, const double *x2, int64_t n, const double *F, int64_t H, double thr,
+                      int32_t *counts);
+
+int64_t cs_ransac(const double *x1, const double *x2, int64_t n, const int32_t *samples, int64_t H, int k,
+                  double thr, int32_t *counts) {
+    if (k > 64) return -2;
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t h = 0; h < H; ++h) {
+        double p1[2 * 64], p2[2 * 64], F[9];
+        for (int j = 0; j < k; ++j) {
+            const int32_t s = samples[h * k + j];
+            p1[2 * j] = x1[2 * s]; p1[2 * j + 1] = x1[2 * s + 1];
+            p2[2 * j] = x2[2 * s]; p2[2 * j + 1] = x2[2 * s + 1];
+        }
+        int32_t c = 0;
+        if (orc_f8(p1, p2, k, F) == 0) orc_ransac_score(x1, x2, n, F, 1, thr, &c);
+        counts[h] = c;
+    }
+    int64_t best = -1;
+    int32_t best_c = 0;
+    for (int64_t h = 0; h < H; ++h)
+        if (counts[h] > best_c) { best_c = counts[h]; best = h; }
+    return best;
+}
+
+/* thread count of the OpenMP legs (0: leave OMP_NUM_THREADS' choice) */
+void cs_set_threads(int n) {
+    if (n > 0) omp_set_num_threads(n);
+}
+int cs_max_threads(void) { return omp_get_max_threads(); }

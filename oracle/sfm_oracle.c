@@ -184,19 +184,32 @@ int orc_f8(const double *p1, const double *p2, int64_t n, double *F_out) {
     return 0;
 }
 
-/* GetInliersRANSAC.py:64-81: inlier test for one F over N points. */
-static inline int epi_inlier(const double *F, double x1, double y1, double x2, double y2, double thr) {
-    double a0 = F[0] * x1 + F[1] * y1 + F[2];
-    double a1 = F[3] * x1 + F[4] * y1 + F[5];
-    double a2 = F[6] * x1 + F[7] * y1 + F[8];
-    double b0 = F[0] * x2 + F[3] * y2 + F[6];
-    double b1 = F[1] * x2 + F[4] * y2 + F[7];
+/* GetInliersRANSAC.py:64-81: symmetric epipolar error of one pair and the
+ * inlier test (strict <). */
+static inline double epi_err(const double *F, double x1, double y1, double x2, double y2) {
+    /* Fx1 = (F @ x1h.T).T and FTx2 (:67, :69) are OpenBLAS dgemm products:
+     * acc = a0 b0, then fma; the row sum of x2h * Fx1 (:72) and the squares
+     * (:76-77) are plain numpy arithmetic (checked bit for bit against numpy
+     * in tests/test_oracle.py) */
+    double a0 = fma(F[1], y1, F[0] * x1) + F[2];
+    double a1 = fma(F[4], y1, F[3] * x1) + F[5];
+    double a2 = fma(F[7], y1, F[6] * x1) + F[8];
+    double b0 = fma(F[3], y2, F[0] * x2) + F[6];
+    double b1 = fma(F[4], y2, F[1] * x2) + F[7];
     double e = x2 * a0 + y2 * a1 + a2;
     double ae = fabs(e);
     double d1 = ae / (sqrt(a0 * a0 + a1 * a1) + 1e-8);
     double d2 = ae / (sqrt(b0 * b0 + b1 * b1) + 1e-8);
-    double err = (d1 + d2) / 2.0;
-    return err < thr;
+    return (d1 + d2) / 2.0;
+}
+
+/* per-pair errors (the at-threshold tests place thresholds on them) */
+void orc_epi_err(const double *x1, const double *x2, int64_t n, const double *F, double *err) {
+    for (int64_t i = 0; i < n; ++i) err[i] = epi_err(F, x1[2 * i], x1[2 * i + 1], x2[2 * i], x2[2 * i + 1]);
+}
+
+static inline int epi_inlier(const double *F, double x1, double y1, double x2, double y2, double thr) {
+    return epi_err(F, x1, y1, x2, y2) < thr;
 }
 
 /* counts[h] for every hypothesis; mask (nullable) for hypothesis h_mask */
@@ -329,14 +342,20 @@ int orc_homography(const double *p1, const double *p2, int64_t n, double *H_out)
     return 0;
 }
 
-/* GetHomographyInliers.py:134-146: transfer error test of one point */
-static inline int hom_inlier(const double *H, double x, double y, double u, double v, double thr) {
+/* GetHomographyInliers.py:134-146: transfer error of one point, and the test */
+static inline double hom_err(const double *H, double x, double y, double u, double v) {
     double t0 = fma(H[1], y, H[0] * x) + H[2];
     double t1 = fma(H[4], y, H[3] * x) + H[5];
     double t2 = fma(H[7], y, H[6] * x) + H[8];
     double w = t2 + 1e-8;
     double d0 = t0 / w - u, d1 = t1 / w - v;
-    return sqrt(d0 * d0 + d1 * d1) < thr;
+    return sqrt(d0 * d0 + d1 * d1);
+}
+static inline int hom_inlier(const double *H, double x, double y, double u, double v, double thr) {
+    return hom_err(H, x, y, u, v) < thr;
+}
+void orc_hom_err(const double *x1, const double *x2, int64_t n, const double *H, double *err) {
+    for (int64_t i = 0; i < n; ++i) err[i] = hom_err(H, x1[2 * i], x1[2 * i + 1], x2[2 * i], x2[2 * i + 1]);
 }
 
 void orc_h_score(const double *x1, const double *x2, int64_t n, const double *Hs, int64_t nh, double thr,

@@ -327,6 +327,19 @@ static inline void pnp_project(const double *P, const double *Xw, double *u, dou
     *v = h[1] / w;
 }
 
+/* PnPRANSAC.py:60-68: the reprojection error of every point for one pose */
+void orc_pnp_err(const double *X, const double *x, int64_t n, const double *K, const double *C, const double *R,
+                 double *err) {
+    double P[12];
+    pnp_projection(K, C, R, P);
+    for (int64_t i = 0; i < n; ++i) {
+        double u, v;
+        pnp_project(P, X + 3 * i, &u, &v);
+        const double du = x[2 * i] - u, dv = x[2 * i + 1] - v;
+        err[i] = sqrt(du * du + dv * dv);
+    }
+}
+
 /* PnPRANSAC.py:60-70 for one pose */
 int64_t orc_pnp_count(const double *X, const double *x, int64_t n, const double *K, const double *C,
                       const double *R, double thr) {

@@ -47,11 +47,13 @@ def GetInliersRANSAC(points1, points2, index, threshold=0.06, n_max=1000):
     F_best : numpy.ndarray
         the best fundamental matrix
     """
-    # np.asarray: the reference's np.array(...) (:32-34) without the copy
-    # (the inputs are only read)
+    # np.asarray for the points: the reference's np.array(...) (:32-34)
+    # without the copy (they are only read).  index is copied as the
+    # reference does: the early returns hand it back, and a caller that
+    # modifies the result must not modify its own input
     points1 = np.asarray(points1)
     points2 = np.asarray(points2)
-    index = np.asarray(index)
+    index = np.array(index)
     n_points = len(points1)
     if n_points < 8:  # :38-40
         return np.array([]), index, None

@@ -226,6 +226,85 @@ struct Geo {
     }
 };
 
+// ------------------------------------------------- the 16-pivot tile factor
+// Every 16-lane row of the wave holds the rows of the diagonal tile (r[j] =
+// element (li, j)) and one row of the panel (p[j]); pivot k scales column k
+// by 1/L_kk and subtracts L_jk (lane j's r[k], DPP row_newbcast) times it
+// from columns j > k, with v_fmac_f64_dpp's neg modifier (no negated copies).
+// Unlike chol_factor16 (k_chol_col) the next pivot's 1/sqrt is started as
+// soon as its column is updated and its four dependent operations (v_rsq_f64
+// and one Newton step, ~1 ulp) are interleaved with the remaining updates of
+// the current pivot, so the chain's latency hides under their issue.  Every
+// instruction is inline asm in program order; s_nop 1 gives a DPP read of a
+// just-written VGPR its two wait states.
+template <int J>
+__device__ __forceinline__ void gj_upd2(double &rj, double &pj, double rk, double pk) {
+    asm volatile("v_fmac_f64_dpp %0, %2, -%2 row_newbcast:%4 row_mask:0xf bank_mask:0xf\n\t"
+                 "v_fmac_f64_dpp %1, %2, -%3 row_newbcast:%4 row_mask:0xf bank_mask:0xf"
+                 : "+v"(rj), "+v"(pj) : "v"(rk), "v"(pk), "n"(J));
+}
+struct NewtonState {
+    double d, h, g0, a, b, c15;
+};
+template <int STEP>
+__device__ __forceinline__ void gj_newton(NewtonState &n) {  // g1 = g0 (1.5 - (d/2) g0^2)
+    if constexpr (STEP == 0) asm volatile("v_mul_f64 %0, %1, %2" : "=v"(n.a) : "v"(n.h), "v"(n.g0));
+    if constexpr (STEP == 1) asm volatile("v_fma_f64 %0, -%1, %2, %3" : "=v"(n.b) : "v"(n.a), "v"(n.g0), "v"(n.c15));
+    if constexpr (STEP == 2) asm volatile("v_mul_f64 %0, %1, %2" : "=v"(n.g0) : "v"(n.g0), "v"(n.b));
+}
+// updates of columns K+2+U.. of pivot K, the Newton steps after updates 1, 3, 5
+template <int K, int U>
+__device__ __forceinline__ void gj_rest(double (&r)[16], double (&p)[16], NewtonState &n) {
+    if constexpr (K + 2 + U <= 15) {
+        gj_upd2<K + 2 + U>(r[K + 2 + U], p[K + 2 + U], r[K], p[K]);
+        if constexpr (U == 1) gj_newton<0>(n);
+        if constexpr (U == 3) gj_newton<1>(n);
+        if constexpr (U == 5) gj_newton<2>(n);
+        gj_rest<K, U + 1>(r, p, n);
+    } else {  // fewer updates than Newton steps: the rest back to back
+        if constexpr (U <= 1) gj_newton<0>(n);
+        if constexpr (U <= 3) gj_newton<1>(n);
+        if constexpr (U <= 5) gj_newton<2>(n);
+    }
+}
+template <int K>
+__device__ __forceinline__ void gj_step(double (&r)[16], double (&p)[16], double (&dinv)[16], NewtonState &n,
+                                        bool &nonpos) {
+    const double g = n.g0;
+    asm volatile("v_mul_f64 %0, %0, %2\n\tv_mul_f64 %1, %1, %2" : "+v"(r[K]), "+v"(p[K]) : "v"(g));
+    dinv[K] = g;
+    if constexpr (K < 15) {
+        asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %2, -%2 row_newbcast:%4 row_mask:0xf bank_mask:0xf\n\t"
+                     "v_fmac_f64_dpp %1, %2, -%3 row_newbcast:%4 row_mask:0xf bank_mask:0xf"
+                     : "+v"(r[K + 1]), "+v"(p[K + 1]) : "v"(r[K]), "v"(p[K]), "n"(K + 1));
+        asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+                     : "=v"(n.d) : "v"(r[K + 1]), "n"(K + 1));
+        asm volatile("v_rsq_f64 %0, %1" : "=v"(n.g0) : "v"(n.d));
+        asm volatile("v_mul_f64 %0, %1, 0.5" : "=v"(n.h) : "v"(n.d));
+        nonpos |= !(n.d > 0.0);
+        gj_rest<K, 0>(r, p, n);
+    }
+}
+template <int... K>
+__device__ __forceinline__ void gj_steps(double (&r)[16], double (&p)[16], double (&dinv)[16], NewtonState &n,
+                                         bool &nonpos, std::integer_sequence<int, K...>) {
+    (gj_step<K>(r, p, dinv, n, nonpos), ...);
+}
+__device__ __forceinline__ void gj_factor16(double (&r)[16], double (&p)[16], double (&dinv)[16], int lane,
+                                            int *bad) {
+    NewtonState n;
+    n.c15 = 1.5;
+    asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf" : "=v"(n.d) : "v"(r[0]));
+    asm volatile("v_rsq_f64 %0, %1" : "=v"(n.g0) : "v"(n.d));
+    asm volatile("v_mul_f64 %0, %1, 0.5" : "=v"(n.h) : "v"(n.d));
+    bool nonpos = !(n.d > 0.0);
+    gj_newton<0>(n);
+    gj_newton<1>(n);
+    gj_newton<2>(n);
+    gj_steps(r, p, dinv, n, nonpos, std::make_integer_sequence<int, 16>{});
+    if (lane == 0 && nonpos) *bad = 1;
+}
+
 // -------------------------------------------------------------- the chain
 // W0 / W1: pivot p from the staged column (Cst).  W0 carries the segment's
 // rows, W1 the b row; both factor the same replica (same bits).
@@ -244,7 +323,7 @@ __device__ __forceinline__ void chain_pivot(const Args &a, const Geo &g, Smem &S
     lds_release();
     if (lane == 0) lds_add(&S.cst_read, 1);  // Cst may be restaged (phase A of panel p)
     if (wave == 0) stamp(a, p, DBG_CST);
-    chol_factor16(rw, pw, dinv, li, lane, a.bad);
+    gj_factor16(rw, pw, dinv, lane, a.bad);
     if (wave == 0) stamp(a, p, DBG_CHAIN);
     const int nsp = g.nT * TL;
     // panel p's buffers were last read by the update waves at panel p - 2

@@ -7,15 +7,22 @@ namespace sfm {
 
 // --------------------------------------------------------------------
 // Symmetric epipolar distance test of GetInliersRANSAC.py:64-81.
-// Same operation order as the reference expression; strict '<'.
+// Same operation order as the reference expression; strict '<'.  Every
+// function of the F path (the epipolar tests and the 8-point fit below) is
+// compiled with contraction off and states numpy's FMAs explicitly: Fx1 =
+// F @ x1h and FTx2 are OpenBLAS dgemm products (a0 b0, then fma), the row
+// sum of x2h * Fx1 and the squares are plain products and sums.  The C
+// oracle uses the same expression (equal to numpy's bit for bit,
+// tests/test_oracle.py), so the decisions match at the threshold itself.
 // --------------------------------------------------------------------
 __device__ __forceinline__ bool epi_inlier(const double *F, double x, double y, double u, double v,
                                            double thr) {
-    const double a0 = F[0] * x + F[1] * y + F[2];
-    const double a1 = F[3] * x + F[4] * y + F[5];
-    const double a2 = F[6] * x + F[7] * y + F[8];
-    const double b0 = F[0] * u + F[3] * v + F[6];
-    const double b1 = F[1] * u + F[4] * v + F[7];
+#pragma clang fp contract(off)
+    const double a0 = fma(F[1], y, F[0] * x) + F[2];  // F @ x1h: OpenBLAS dgemm's order
+    const double a1 = fma(F[4], y, F[3] * x) + F[5];
+    const double a2 = fma(F[7], y, F[6] * x) + F[8];
+    const double b0 = fma(F[3], v, F[0] * u) + F[6];  // F.T @ x2h
+    const double b1 = fma(F[4], v, F[1] * u) + F[7];
     const double e = u * a0 + v * a1 + a2;
     const double ae = fabs(e);
     const double d1 = ae / (sqrt(a0 * a0 + a1 * a1) + 1e-8);
@@ -36,11 +43,12 @@ struct EpiPart {
 
 __device__ __forceinline__ EpiPart epi_fast(const double *F, double x, double y, double u, double v, double thr_lo2,
                                             double thr_hi2) {
-    const double a0 = F[0] * x + F[1] * y + F[2];
-    const double a1 = F[3] * x + F[4] * y + F[5];
-    const double a2 = F[6] * x + F[7] * y + F[8];
-    const double b0 = F[0] * u + F[3] * v + F[6];
-    const double b1 = F[1] * u + F[4] * v + F[7];
+#pragma clang fp contract(off)
+    const double a0 = fma(F[1], y, F[0] * x) + F[2];  // F @ x1h: OpenBLAS dgemm's order
+    const double a1 = fma(F[4], y, F[3] * x) + F[5];
+    const double a2 = fma(F[7], y, F[6] * x) + F[8];
+    const double b0 = fma(F[3], v, F[0] * u) + F[6];  // F.T @ x2h
+    const double b1 = fma(F[4], v, F[1] * u) + F[7];
     const double e = u * a0 + v * a1 + a2;
     EpiPart r;
     r.ae = fabs(e);
@@ -76,9 +84,10 @@ struct EpiPartA {
 
 __device__ __forceinline__ EpiPartA epi_fast_a(const double *F, double x, double y, double u, double v,
                                                double thr_hi2) {
-    const double a0 = F[0] * x + F[1] * y + F[2];
-    const double a1 = F[3] * x + F[4] * y + F[5];
-    const double a2 = F[6] * x + F[7] * y + F[8];
+#pragma clang fp contract(off)
+    const double a0 = fma(F[1], y, F[0] * x) + F[2];  // F @ x1h: OpenBLAS dgemm's order
+    const double a1 = fma(F[4], y, F[3] * x) + F[5];
+    const double a2 = fma(F[7], y, F[6] * x) + F[8];
     const double e = u * a0 + v * a1 + a2;
     EpiPartA r;
     r.ae = fabs(e);
@@ -90,14 +99,17 @@ __device__ __forceinline__ EpiPartA epi_fast_a(const double *F, double x, double
     // operations.  The magnitude guards keep ae^2 and the right side finite;
     // NaN fails every comparison (stage B decides those pairs)
     const double rhs = thr_hi2 * thr_hi2 * fma(r.qa, 1.0 + 1e-8, 1.00000001e-8);
-    r.out = r.ae * r.ae > rhs && r.ae < 1e150 && r.qa < 1e290 && thr_hi2 >= 0.0;
+    // thr_hi2 > 1e-150: below it thr_hi2^2 underflows and rhs would prove
+    // pairs "out" that the exact mean keeps (stage B decides those)
+    r.out = r.ae * r.ae > rhs && r.ae < 1e150 && r.qa < 1e290 && thr_hi2 > 1e-150;
     return r;
 }
 
 __device__ __forceinline__ EpiPart epi_fast_b(const EpiPartA &a, const double *F, double u, double v,
                                               double thr_lo2, double thr_hi2) {
-    const double b0 = F[0] * u + F[3] * v + F[6];
-    const double b1 = F[1] * u + F[4] * v + F[7];
+#pragma clang fp contract(off)
+    const double b0 = fma(F[3], v, F[0] * u) + F[6];  // F.T @ x2h
+    const double b1 = fma(F[4], v, F[1] * u) + F[7];
     EpiPart r;
     r.ae = a.ae;
     r.qa = a.qa;
@@ -115,6 +127,7 @@ __device__ __forceinline__ EpiPart epi_fast_b(const EpiPartA &a, const double *F
 
 // the exact tail of epi_inlier from epi_fast's terms (same operations)
 __device__ __forceinline__ bool epi_exact(const EpiPart &r, double thr) {
+#pragma clang fp contract(off)
     const double d1 = r.ae / (sqrt(r.qa) + 1e-8);
     const double d2 = r.ae / (sqrt(r.qb) + 1e-8);
     return (d1 + d2) * 0.5 < thr;
@@ -134,6 +147,7 @@ __device__ __forceinline__ bool epi_inlier_fast(const double *F, double x, doubl
 // --------------------------------------------------------------------
 template <int M, int N, int SWEEPS>
 __device__ __forceinline__ void jacobi_onesided(double (&a)[N][M], double (&V)[N][N]) {
+#pragma clang fp contract(off)
 #pragma unroll
     for (int i = 0; i < N; ++i)
 #pragma unroll
@@ -178,6 +192,7 @@ __device__ __forceinline__ void jacobi_onesided(double (&a)[N][M], double (&V)[N
 
 template <int M, int N>
 __device__ __forceinline__ int weakest_column(const double (&a)[N][M]) {
+#pragma clang fp contract(off)
     int best = 0;
     double bn = 0;
 #pragma unroll
@@ -198,6 +213,7 @@ struct Hartley {
 };
 
 __device__ __forceinline__ Hartley hartley8(const double (&x)[8], const double (&y)[8]) {
+#pragma clang fp contract(off)
     double mx = 0, my = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) { mx += x[i]; my += y[i]; }
@@ -225,6 +241,7 @@ __device__ __forceinline__ Hartley hartley8(const double (&x)[8], const double (
 // two rows of A - lambda I.  Its error is ~eps * lambda_1 / (lambda_2 -
 // lambda_3), i.e. ~eps unless F is nearly rank 1 (false: use Jacobi).
 __device__ __forceinline__ bool smallest_right_sv(const double (&f)[9], double (&v)[3]) {
+#pragma clang fp contract(off)
     double a[3][3];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -268,6 +285,7 @@ __device__ __forceinline__ bool smallest_right_sv(const double (&f)[9], double (
 
 __device__ __forceinline__ void f8_finish(const double (&f)[9], const Hartley &h1, const Hartley &h2,
                                           double *F_out) {
+#pragma clang fp contract(off)
     // rank 2 (EstimateFundamentalMatrix.py:70-72): U diag(s1, s2, 0) V^T =
     // F - (F v3) v3^T with v3 the smallest right singular vector
     double F2[3][3];
@@ -333,6 +351,7 @@ __device__ __forceinline__ void f8_finish(const double (&f)[9], const Hartley &h
 // divide by the [2,2] entry, which removes it).  ~0.6 kflop instead of a
 // 9-column SVD.  A is destroyed.
 __device__ __forceinline__ void null_vector_8x9(double (&A)[8][9], double (&n)[9]) {
+#pragma clang fp contract(off)
     double tau[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -374,6 +393,7 @@ __device__ __forceinline__ void null_vector_8x9(double (&A)[8][9], double (&n)[9
 // matrix (:58-62), its null vector, rank 2 and denormalisation (f8_finish).
 __device__ __forceinline__ void f8_points(const double (&x1)[8], const double (&y1)[8],
                                           const double (&x2)[8], const double (&y2)[8], double *F_out) {
+#pragma clang fp contract(off)
     const Hartley h1 = hartley8(x1, y1), h2 = hartley8(x2, y2);
     double A[8][9];
 #pragma unroll
@@ -401,6 +421,7 @@ __device__ __forceinline__ void f8_points(const double (&x1)[8], const double (&
 // against the one-thread fit's 136, so it can share a launch with the score.
 // Lane 0 of the group writes F_out.
 __device__ __forceinline__ double hartley_sum8(double v) {
+#pragma clang fp contract(off)
     double s = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) s += __shfl(v, k, 8);
@@ -408,6 +429,7 @@ __device__ __forceinline__ double hartley_sum8(double v) {
 }
 
 __device__ __forceinline__ Hartley hartley8_group(double x, double y) {
+#pragma clang fp contract(off)
     const double mx = hartley_sum8(x) / 8.0, my = hartley_sum8(y) / 8.0;
     const double ax = x - mx, ay = y - my;
     const double d = hartley_sum8(sqrt(ax * ax + ay * ay));
@@ -419,6 +441,7 @@ __device__ __forceinline__ Hartley hartley8_group(double x, double y) {
 }
 
 __device__ __forceinline__ void f8_points_group8(double px, double py, double qx, double qy, double *F_out) {
+#pragma clang fp contract(off)
     const int i = threadIdx.x & 7;
     const Hartley h1 = hartley8_group(px, py), h2 = hartley8_group(qx, qy);
     double A[9];

@@ -1008,36 +1008,61 @@ def _thresholds_at(d, n=24):
 def test_ransac_fast_tests_exact_at_threshold(core):
     """The score kernels' fast tests (the two-stage epipolar test with its
     wave-level outlier skip, the homography transfer-error test) against the
-    exact reference expressions, at thresholds placed exactly on pair
-    distances: the count of one hypothesis (fast path + exact tail) equals
-    the size of the winner's mask, which the select kernel forms with the
-    exact expression, and the standalone exact mask of the same model."""
+    ORACLE's distances (the reference expressions GetInliersRANSAC.py:67-78
+    and GetHomographyInliers.py:136-142, equal to numpy's bit for bit:
+    test_oracle.py), with thresholds placed exactly on (and one ulp around)
+    those distances: the count of one hypothesis (fast path + exact tail),
+    the winner's mask (select kernel) and the standalone mask all equal the
+    oracle's strict test err < thr."""
     x1, x2, _, _ = syn.two_view(n=3000, seed=11)
     random.seed(4)
     sample = np.array([random.sample(range(len(x1)), 8)], dtype=np.int32)
     b, F, _, _ = core.ransac_f8(x1, x2, sample, 1e3, want_counts=True)
     assert b == 0
-    h1 = np.column_stack([x1, np.ones(len(x1))])
-    h2 = np.column_stack([x2, np.ones(len(x2))])
-    l2, l1 = h1 @ F.T, h2 @ F
-    e = np.abs(np.sum(h2 * l2, axis=1))
-    d = 0.5 * (e / (np.hypot(l2[:, 0], l2[:, 1]) + 1e-8) + e / (np.hypot(l1[:, 0], l1[:, 1]) + 1e-8))
-    for thr in _thresholds_at(d):
+    err = O.epi_err(x1, x2, F)
+    for thr in _thresholds_at(err):
+        ref = err < thr
+        assert np.array_equal(ref, O.ransac_mask(x1, x2, F, float(thr)))
         b, Fb, mask, counts = core.ransac_f8(x1, x2, sample, float(thr), want_counts=True)
-        exact = core.ransac_mask(x1, x2, F, float(thr), model=8)
-        assert counts[0] == exact.sum(), thr
+        assert counts[0] == ref.sum(), thr
+        assert np.array_equal(core.ransac_mask(x1, x2, F, float(thr), model=8), ref), thr
         if counts[0] > 0:
-            assert b == 0 and np.array_equal(Fb, F) and np.array_equal(mask, exact), thr
+            assert b == 0 and np.array_equal(Fb, F) and np.array_equal(mask, ref), thr
     # homography: one in-call hypothesis from a fixed stream, thresholds on its transfer errors
     random.seed(9)
     b, Hm, _, _, _ = core.ransac_h4_pyrandom(x1, x2, 1, 1e6)
     assert b == 0
-    p = h1 @ Hm.T
-    t = np.hypot(p[:, 0] / (p[:, 2] + 1e-8) - x2[:, 0], p[:, 1] / (p[:, 2] + 1e-8) - x2[:, 1])
-    for thr in _thresholds_at(t):
+    err = O.hom_err(x1, x2, Hm)
+    for thr in _thresholds_at(err):
+        ref = err < thr
         random.seed(9)
         b, Hb, mask, counts, _ = core.ransac_h4_pyrandom(x1, x2, 1, float(thr), want_counts=True)
-        exact = core.ransac_mask(x1, x2, Hm, float(thr), model=4)
-        assert counts[0] == exact.sum(), thr
+        assert counts[0] == ref.sum(), thr
+        assert np.array_equal(core.ransac_mask(x1, x2, Hm, float(thr), model=4), ref), thr
         if counts[0] > 0:
-            assert np.array_equal(mask, exact), thr
+            assert np.array_equal(mask, ref), thr
+
+
+def test_pnp_fast_test_exact_at_threshold(core):
+    """The PnP score kernel's fast reprojection test (v_rcp_f64 + Newton, a
+    widened band, the exact tail inside it; pnp.hip pnp_fast) against the
+    oracle's reprojection errors (PnPRANSAC.py:60-68, numpy's bit for bit),
+    thresholds exactly on (and one ulp around) them: the hypothesis count
+    equals the oracle's strict test on the winning pose."""
+    X, x, Ct, Rt = _pnp_scene(4000, 21, outlier_frac=0.2)
+    random.seed(21)
+    samples = core.sample_table(len(X), 4, 64)
+    best, bc, C, R, counts, branches = core.pnp_ransac(X, x, K, samples, 1e4, want_counts=True)
+    assert best >= 0
+    one = samples[best:best + 1]
+    err = O.pnp_err(X, x, K, C, R)
+    checked = 0
+    for thr in _thresholds_at(err[err < 50.0]):
+        b1, c1, C1, R1, cnt, br = core.pnp_ransac(X, x, K, one, float(thr), want_counts=True)
+        if br[0] != 0:
+            continue  # det(R) < 0 branch: parity unpinned by construction (DESIGN §3)
+        assert cnt[0] == (err < thr).sum(), thr
+        if b1 == 0:  # a winner (>= 4 inliers): its pose is the hypothesis's
+            assert np.array_equal(C1, C) and np.array_equal(R1, R)
+        checked += 1
+    assert checked > 0

@@ -251,3 +251,39 @@ def test_reference_loop_restatement_values():
     r1 = ref_loop.residuals(params, 5, 60, p["cam_idx"], p["pt_idx"], p["obs"], syn.K_REF)
     r2 = O.ba_residuals(cams, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], syn.K_REF)
     assert np.abs(r1 - r2).max() <= 1e-9 * np.abs(r2).max()
+
+
+def test_oracle_pair_errors_equal_reference_expressions():
+    """The oracle's per-pair errors are the reference's own numpy
+    expressions bit for bit (numpy here: the fixtures' machine) -- so the
+    at-threshold GPU tests (test_gpu_parity) that compare against the
+    oracle compare against the reference arithmetic:
+      F: GetInliersRANSAC.py:67-78 (Fx1 / FTx2 are dgemm FMA chains, the
+         row sum and the squares plain);
+      H: GetHomographyInliers.py:136-142;  PnP: PnPRANSAC.py:60-68."""
+    for seed in range(4):
+        x1, x2, _, m = syn.two_view(n=4000, seed=seed)
+        random.seed(seed)
+        s = random.sample(range(len(x1)), 8)
+        F = O.f8(x1[s], x2[s])
+        h1 = np.column_stack([x1, np.ones(len(x1))])
+        h2 = np.column_stack([x2, np.ones(len(x2))])
+        Fx1 = (F @ h1.T).T
+        FTx2 = (F.T @ h2.T).T
+        e = np.sum(h2 * Fx1, axis=1)
+        d1 = np.abs(e) / (np.sqrt(Fx1[:, 0] ** 2 + Fx1[:, 1] ** 2) + 1e-8)
+        d2 = np.abs(e) / (np.sqrt(FTx2[:, 0] ** 2 + FTx2[:, 1] ** 2) + 1e-8)
+        assert np.array_equal((d1 + d2) / 2, O.epi_err(x1, x2, F))
+        H = O.homography(x1[s[:4]], x2[s[:4]])
+        t = (H @ h1.T).T
+        t2 = t[:, :2] / (t[:, 2:3] + 1e-8)
+        assert np.array_equal(np.sqrt(np.sum((t2 - x2) ** 2, axis=1)), O.hom_err(x1, x2, H))
+        rng = np.random.default_rng(seed)
+        X = np.column_stack([rng.uniform(-3, 3, 3000), rng.uniform(-2, 2, 3000), rng.uniform(5, 12, 3000)])
+        C, R = m["C2"] + 0.01 * seed, m["R2"]
+        u = (K @ (R @ (X - C).T)).T
+        x = u[:, :2] / u[:, 2:3] + rng.normal(0, 0.5, (3000, 2))
+        P = K @ np.hstack([R, -R @ C.reshape(3, 1)])
+        xp = (P @ np.hstack([X, np.ones((3000, 1))]).T).T
+        xp = xp[:, :2] / (xp[:, 2:3] + 1e-8)
+        assert np.array_equal(np.sqrt(np.sum((x - xp) ** 2, axis=1)), O.pnp_err(X, x, K, C, R))
