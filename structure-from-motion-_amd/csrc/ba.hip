@@ -1747,7 +1747,7 @@ static long long *gj_dbg_ptr() {
     static const bool on = std::getenv("SFM_GJ_DEBUG") && std::atoi(std::getenv("SFM_GJ_DEBUG")) != 0;
     if (!on) return nullptr;
     if (!g_gj_dbg) {
-        g_gj_dbg_n = (size_t)256 * 128 * 16;
+        g_gj_dbg_n = (size_t)256 * (gj::NTMAX + 1) * 16;
         if (hipMalloc(&g_gj_dbg, g_gj_dbg_n * sizeof(long long)) != hipSuccess) return g_gj_dbg = nullptr;
         (void)hipMemset(g_gj_dbg, 0, g_gj_dbg_n * sizeof(long long));
     }
@@ -3013,9 +3013,14 @@ extern "C" int sfm_reduced_solve(const double *S, const double *rhs, int32_t n, 
         if ((rc = c->buf[5].reserve(GjBufs::doubles(nT, gjp.nseg) * sizeof(double))) ||
             (rc = c->buf[6].reserve(nint * sizeof(int))))
             return rc;
-        if (c->buf[6].p != c->gj_ints) {  // fresh flags: zero them once, epochs restart
+        // fresh flags: zero them once, epochs restart.  A regrown buffer can
+        // come back at the same address, and a new layout moves the flags
+        // and the arrival word: either way the old words mean nothing
+        if (c->buf[6].p != c->gj_ints || c->gj_nT != nT || c->gj_nseg != gjp.nseg) {
             SFM_HIP(hipMemsetAsync(c->buf[6].p, 0, c->buf[6].bytes, c->stream));
             c->gj_ints = c->buf[6].p;
+            c->gj_nT = nT;
+            c->gj_nseg = gjp.nseg;
             c->gj_epoch = 0;
         }
         GjBufs b;

@@ -34,6 +34,8 @@
 //       segment's 64 rows of the pivot column on its lanes -> L_p, G rows;
 //   W1  the same chain with b_p on one lane -> y_p (and publishes L_p, y_p);
 //   WL  loader: polls the flags of remote panels / tiles and stages them;
+//   WP  publisher: copies this workgroup's pivots (G rows, L_p, y_p) from LDS
+//       to global memory and raises their flags (off the chain waves' path);
 //   U*  update waves: each owns up to TPW tiles in MFMA C-fragment layout
 //       (v_mfma_f64_16x16x4f64: the VALU stays free for the chains) and
 //       applies every panel; the tiles of column p+1 first (phase A, then
@@ -44,8 +46,9 @@ constexpr int TL = 16;       // tile
 constexpr int SR = 4;        // row tiles per segment (64 rows: W0's lanes)
 constexpr int CBMAX = 8;     // column tiles per workgroup
 constexpr int NUW = 8;       // update waves
-constexpr int NW = 3 + NUW;  // W0, W1, WL, U0..U7
+constexpr int NW = 4 + NUW;  // W0, W1, WL, WP, U0..U7
 constexpr int THREADS = 64 * NW;
+constexpr int NCONS = NUW + 2;  // consumers of a panel's LDS buffers: the update waves, W1 and WP
 constexpr int TPW = ((SR + 1) * CBMAX + NUW - 1) / NUW;  // tile slots per update wave
 constexpr int LDT = TL + 1;                              // padded LDS row (doubles)
 constexpr int NTMAX = 128;                               // tiles per dimension (host checks)
@@ -73,10 +76,13 @@ struct Args {
 };
 
 // diagnostic stamps (sfm_gj_debug): slot per (workgroup, panel)
+// (row nT of a workgroup: the kernel-wide phases)
 enum { DBG_CST = 0, DBG_CHAIN, DBG_PUB, DBG_LOAD0, DBG_LOADED, DBG_GM, DBG_PHA, DBG_PHB,
        DBG_W0BUF, DBG_W0GST, DBG_W0LDS, DBG_W0DRAIN, DBG_AGJ, DBG_ACST, DBG_AMMA, DBG_ABB };
+enum { DBG_START = 0, DBG_PROLOGUE, DBG_FINWAIT, DBG_FINSOLVED, DBG_ARRIVED, DBG_EPILOGUE };
 __device__ __forceinline__ void stamp(const Args &a, int p, int slot) {
-    if (a.dbg && (threadIdx.x & 63) == 0) a.dbg[((int64_t)blockIdx.x * a.nT + p) * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+    if (a.dbg && (threadIdx.x & 63) == 0)
+        a.dbg[((int64_t)blockIdx.x * (a.nT + 1) + p) * 16 + slot] = __builtin_amdgcn_s_memrealtime();
 }
 
 struct Smem {
@@ -89,10 +95,10 @@ struct Smem {
     double bb[CBMAX][TL];          // b replica of each owned column's row tile
     double ob[SR * TL];            // b of the segment's rows (last column block)
     int gm_ok[2], ly_ok[2], gj_ok[2][CBMAX];  // = p + 1 when panel p's piece is staged
+    int bb_cnt[CBMAX];  // panels applied to each b replica (W1: column p + 1; the replica's update wave: the rest)
     int cst_cnt, cst_read, abort_;
-    int pub[NTMAX];    // per pivot: arrivals of the two chain waves (the second one stores the flag)
-    int udone[NTMAX];  // per panel: update waves done with it (groups progress at different rates,
-                       // so a single running count would not say which panels are done)
+    int udone[NTMAX];  // per panel: update waves and W1 done with it (groups progress at different
+                       // rates, so a single running count would not say which panels are done)
     int *err, *bad;  // global: set on an abort (the host reports it, the LM rejects the step)
 };
 
@@ -181,8 +187,6 @@ __device__ __forceinline__ d4 mma16(d4 acc, const double (*Ar)[LDT], const doubl
     return acc;
 }
 
-__device__ __forceinline__ double diag_u_src(const Args &a, int i) { return a.payload[pay_vec_base(a.ns) + i]; }
-__device__ __forceinline__ double g_c_src(const Args &a, int i) { return a.payload[pay_vec_base(a.ns) + a.ns + i]; }
 
 // element (I, J) of S + lambda clamp(diag U) from the payload, the lower
 // triangle mirrored (what a Cholesky of S reads), identity on the padding;
@@ -307,8 +311,10 @@ __device__ __forceinline__ void gj_factor16(double (&r)[16], double (&p)[16], do
 
 // -------------------------------------------------------------- the chain
 // W0 / W1: pivot p from the staged column (Cst).  W0 carries the segment's
-// rows, W1 the b row; both factor the same replica (same bits).
-__device__ __forceinline__ void chain_pivot(const Args &a, const Geo &g, Smem &S, int p, int wave, int lane) {
+// rows, W1 the b row; both factor the same replica (same bits).  Only LDS
+// is written here (this workgroup's next pivot waits on it); WP writes the
+// global copy for the other workgroups.
+__device__ __forceinline__ bool chain_pivot(const Args &a, const Geo &g, Smem &S, int p, int wave, int lane) {
     const int li = lane & 15, grp = lane >> 4, buf = p & 1;
     double rw[16], pw[16], dinv[16];
 #pragma unroll
@@ -325,14 +331,10 @@ __device__ __forceinline__ void chain_pivot(const Args &a, const Geo &g, Smem &S
     if (wave == 0) stamp(a, p, DBG_CST);
     gj_factor16(rw, pw, dinv, lane, a.bad);
     if (wave == 0) stamp(a, p, DBG_CHAIN);
-    const int nsp = g.nT * TL;
-    // panel p's buffers were last read by the update waves at panel p - 2
-    if (p >= 2 && !lds_wait(&S.udone[p - 2], NUW, S)) return;
-    if (wave == 0) stamp(a, p, DBG_W0BUF);
-    // LDS first (this workgroup's own next pivot waits on it), then the
-    // global copy for the other workgroups, read back from LDS so that every
-    // store instruction writes 1 KB contiguous (16 B a lane, write-through)
+    // panel p's buffers were last read by the consumers of panel p - 2
+    if (p >= 2 && !lds_wait(&S.udone[p - 2], NCONS, S)) return false;
     if (wave == 0) {
+        stamp(a, p, DBG_W0BUF);
         if (grp < g.nrow) {
 #pragma unroll
             for (int j = 0; j < 16; ++j) S.Gm[buf][grp][li][j] = pw[j];
@@ -350,14 +352,6 @@ __device__ __forceinline__ void chain_pivot(const Args &a, const Geo &g, Smem &S
             }
         }
         stamp(a, p, DBG_W0LDS);
-        double *dst = a.Gp + ((int64_t)p * nsp + g.i0 * TL) * TL;  // the segment's rows: contiguous
-        const int nel = g.nrow * TL * TL;
-#pragma unroll
-        for (int k = 0; k < SR * TL * TL / 64; ++k) {
-            const int e = lane + 64 * k, row = e >> 4;
-            if (e < nel) st_ag(dst + e, S.Gm[buf][row >> 4][row & 15][e & 15]);
-        }
-        stamp(a, p, DBG_W0GST);
     } else {
         if (lane < 16) {
 #pragma unroll
@@ -369,25 +363,79 @@ __device__ __forceinline__ void chain_pivot(const Args &a, const Geo &g, Smem &S
         }
         lds_release();
         if (lane == 0) lds_set(&S.ly_ok[buf], p + 1);
-        double *dl = a.Lp + ((int64_t)p * g.nseg + g.s) * 256;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int e = lane + 64 * k;
-            st_ag(dl + e, S.Ls[buf][e >> 4][e & 15]);
-        }
-        if (lane < 16) st_ag(a.Yp + ((int64_t)p * g.nseg + g.s) * 16 + lane, S.ys[buf][lane]);
     }
-    // publish: both chain waves drained, the second one to arrive stores the flag
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (wave == 0) stamp(a, p, DBG_W0DRAIN);
-    if (lane == 0) {
-        // a count per pivot: W1 of pivot p + 1 may arrive before W0 of pivot p
-        const int old = __hip_atomic_fetch_add(&S.pub[p], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (old == 1) {
-            __hip_atomic_store(a.flag + (int64_t)p * g.nseg + g.s, a.epoch, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            stamp(a, p, DBG_PUB);
+    return true;
+}
+
+// WP: the global copy of each own pivot's pieces (write-through stores,
+// read back from LDS so that every store instruction writes contiguous
+// bytes), drained, then the flag; remote panels: nothing to publish
+__device__ __forceinline__ void publisher(const Args &a, const Geo &g, Smem &S, int lane) {
+    for (int p = 0; p < g.j1; ++p) {
+        if (p >= g.j0) {
+            const int buf = p & 1;
+            if (!lds_wait(&S.gm_ok[buf], p + 1, S) || !lds_wait(&S.ly_ok[buf], p + 1, S)) return;
+            double *dst = a.Gp + ((int64_t)p * g.nT * TL + g.i0 * TL) * TL;  // the segment's rows: contiguous
+            const int nel = g.nrow * TL * TL;
+#pragma unroll
+            for (int k = 0; k < SR * TL * TL / 64; ++k) {
+                const int e = lane + 64 * k, row = e >> 4;
+                if (e < nel) st_ag(dst + e, S.Gm[buf][row >> 4][row & 15][e & 15]);
+            }
+            double *dl = a.Lp + ((int64_t)p * g.nseg + g.s) * 256;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int e = lane + 64 * k;
+                st_ag(dl + e, S.Ls[buf][e >> 4][e & 15]);
+            }
+            if (lane < 16) st_ag(a.Yp + ((int64_t)p * g.nseg + g.s) * 16 + lane, S.ys[buf][lane]);
+            stamp(a, p, DBG_W0GST);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) {
+                __hip_atomic_store(a.flag + (int64_t)p * g.nseg + g.s, a.epoch, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                stamp(a, p, DBG_PUB);
+            }
         }
+        if (lane == 0) lds_add(&S.udone[p], 1);
+    }
+}
+
+// b replica of owned column jj: bb -= G_j y_p (16 lanes, a row each), in
+// panel order (bb_cnt: the panels applied so far), so that every workgroup
+// of the column block holds the same bits
+__device__ __forceinline__ bool apply_bb(Smem &S, int p, int jj, int lane) {
+    const int buf = p & 1;
+    if (!lds_wait(&S.bb_cnt[jj], p, S)) return false;
+    if (lane < 16) {
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc = fma(S.Gj[buf][jj][lane][k], S.ys[buf][k], acc);
+        S.bb[jj][lane] -= acc;
+    }
+    lds_release();
+    if (lane == 0) lds_set(&S.bb_cnt[jj], p + 1);
+    return true;
+}
+
+// W1's loop: its own pivots' chain (the b row), and for every panel p the
+// b replica of column p + 1 (the next pivot reads it; the update waves keep
+// the other columns' b replicas)
+__device__ __forceinline__ void w1_loop(const Args &a, const Geo &g, Smem &S, int lane) {
+    for (int p = 0; p < g.j1; ++p) {
+        const int buf = p & 1, ja = p + 1 - g.j0;
+        if (p >= g.j0) {
+            if (!lds_wait(&S.cst_cnt, (p - g.j0 + 1) * (g.nrow + 1), S) || !chain_pivot(a, g, S, p, 1, lane))
+                return;
+        }
+        if (ja >= 0 && ja < g.ncol) {
+            if (!lds_wait(&S.ly_ok[buf], p + 1, S) || !lds_wait(&S.gj_ok[buf][ja], p + 1, S) ||
+                !apply_bb(S, p, ja, lane))
+                return;
+        }
+        lds_release();
+        if (lane == 0) lds_add(&S.udone[p], 1);
+        if (lds_ld(&S.abort_)) return;
     }
 }
 
@@ -466,7 +514,7 @@ __device__ __forceinline__ bool load_segment(const Args &a, const Geo &g, Smem &
 __device__ __forceinline__ void loader(const Args &a, const Geo &g, Smem &S, int lane) {
     const int sfirst = g.j0 / SR, slast = (g.j1 - 1) / SR;  // segments of the owned columns' tile rows
     for (int p = 0; p < g.j1; ++p) {
-        if (p >= 2 && !lds_wait(&S.udone[p - 2], NUW, S)) return;  // buffers of panel p - 2 consumed
+        if (p >= 2 && !lds_wait(&S.udone[p - 2], NCONS, S)) return;  // buffers of panel p - 2 consumed
         const bool remote = p < g.j0;
         // remote G tiles of the owned columns j > p (our own pivot's tiles in our rows come from W0)
         auto tiles_of = [&](int sg) {
@@ -516,25 +564,22 @@ __device__ __forceinline__ void apply_tile(d4 &acc, const Geo &g, Smem &S, int p
     acc = mma16(acc, S.Gm[buf][ii], S.Gj[buf][jj], true, l);
 }
 
-// b replica of column jj: bb -= G_j y_p (16 lanes, a row each)
-__device__ __forceinline__ void apply_bb(Smem &S, int p, int jj, int lane) {
-    const int buf = p & 1;
-    if (lane < 16) {
-        double acc = 0.0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) acc = fma(S.Gj[buf][jj][lane][k], S.ys[buf][k], acc);
-        S.bb[jj][lane] -= acc;
-    }
-}
-
 __device__ __forceinline__ void updater(const Args &a, const Geo &g, Smem &S, int u, int lane, d4 (&acc)[TPW], bool track_ob) {
     for (int p = 0; p < g.j1; ++p) {
         const int buf = p & 1;
-        if (!lds_wait(&S.gm_ok[buf], p + 1, S) || !lds_wait(&S.ly_ok[buf], p + 1, S)) return;
+        if (!lds_wait(&S.gm_ok[buf], p + 1, S)) return;
         if (u == 0) stamp(a, p, DBG_GM);
+        // L_p and y_p (W1 or the loader): only the import of row p and the segment's b need them
+        bool ly = false, ok = true;
+        auto need_ly = [&]() {
+            if (!ly) {
+                ok = lds_wait(&S.ly_ok[buf], p + 1, S);
+                ly = true;
+            }
+            return ok;
+        };
         // phase A: the tiles of column p + 1, staged for its pivot
         const int ja = p + 1 - g.j0;
-        bool ok = true;
         if (ja >= 0 && ja < g.ncol) {
 #pragma unroll
             for (int k = 0; k < TPW; ++k) {
@@ -550,12 +595,11 @@ __device__ __forceinline__ void updater(const Args &a, const Geo &g, Smem &S, in
                     ok = false;
                     continue;
                 }
+                if (ii < SR && g.i0 + ii == p && !need_ly()) continue;
                 stamp(a, p, DBG_ACST);
                 apply_tile(acc[k], g, S, p, jj, ii, lane);
                 store_cst(S, ii, acc[k], lane);
                 stamp(a, p, DBG_AMMA);
-                if (ii == SR) apply_bb(S, p, jj, lane);
-                stamp(a, p, DBG_ABB);
                 lds_release();
                 if (lane == 0) lds_add(&S.cst_cnt, 1);
             }
@@ -570,11 +614,11 @@ __device__ __forceinline__ void updater(const Args &a, const Geo &g, Smem &S, in
                 ok = false;
                 continue;
             }
+            if (ii < SR && g.i0 + ii == p && !need_ly()) continue;
             apply_tile(acc[k], g, S, p, jj, ii, lane);
-            if (ii == SR) apply_bb(S, p, jj, lane);
+            if (ii == SR && (!need_ly() || !apply_bb(S, p, jj, lane))) ok = false;
         }
-        if (!ok) return;
-        if (track_ob && u == 0) {  // b of the segment's rows: ob_i -= G_i y_p, i != p
+        if (track_ob && u == 0 && ok && need_ly()) {  // b of the segment's rows: ob_i -= G_i y_p, i != p
             const int ti = lane >> 4;
             if (ti < g.nrow && g.i0 + ti != p) {
                 double s = 0.0;
@@ -583,6 +627,7 @@ __device__ __forceinline__ void updater(const Args &a, const Geo &g, Smem &S, in
                 S.ob[lane] -= s;
             }
         }
+        if (!ok) return;
         lds_release();
         if (lane == 0) lds_add(&S.udone[p], 1);
         if (u == 0) stamp(a, p, DBG_PHB);
@@ -592,16 +637,19 @@ __device__ __forceinline__ void updater(const Args &a, const Geo &g, Smem &S, in
 // trial cameras and the camera part of the model decrease from dc (LDS),
 // as camera_trial (k_chol_backsolve's epilogue) with the system read from
 // its source; red: 3 x THREADS doubles
-__device__ void cam_trial(const Args &a, const double *dc, double *red) {
-    const CamTrialArgs &ct = a.ct;
-    const double lambda = *a.lam;
+// (scalar arguments: a reference to the kernel's Args would put a copy of it
+// on the stack of every lane)
+__device__ __attribute__((noinline)) void cam_trial(int nc, const double *Rt, double *Rt_new, double *cam_out,
+                                                    double lambda, const double *payload, int32_t ns,
+                                                    const double *dc, double *red) {
+    const double *du = payload + pay_vec_base(ns), *gc = du + ns;
     double m = 0, dn = 0, xn = 0;
-    for (int c = threadIdx.x; c < ct.nc; c += THREADS) {
+    for (int c = threadIdx.x; c < nc; c += THREADS) {
         const double *d = dc + 6 * c;
         double dR[9];
         rotvec_to_R(d[0], d[1], d[2], dR);
-        const double *R = ct.Rt + 12 * c;
-        double *Rn = ct.Rt_new + 12 * c;
+        const double *R = Rt + 12 * c;
+        double *Rn = Rt_new + 12 * c;
         for (int i = 0; i < 3; ++i)
             for (int j = 0; j < 3; ++j) Rn[3 * i + j] = dR[3 * i] * R[j] + dR[3 * i + 1] * R[3 + j] + dR[3 * i + 2] * R[6 + j];
         for (int i = 0; i < 3; ++i) {
@@ -609,7 +657,7 @@ __device__ void cam_trial(const Args &a, const double *dc, double *red) {
             xn += R[9 + i] * R[9 + i];
         }
         for (int i = 0; i < 6; ++i) {
-            m += d[i] * (lambda * clampd(diag_u_src(a, 6 * c + i)) * d[i] - g_c_src(a, 6 * c + i));
+            m += d[i] * (lambda * clampd(du[6 * c + i]) * d[i] - gc[6 * c + i]);
             dn += d[i] * d[i];
         }
     }
@@ -620,48 +668,65 @@ __device__ void cam_trial(const Args &a, const double *dc, double *red) {
     if (threadIdx.x < 3) {  // fixed order
         double s = 0.0;
         for (int t = 0; t < THREADS; ++t) s += red[threadIdx.x * THREADS + t];
-        ct.cam_out[threadIdx.x] = s;
+        cam_out[threadIdx.x] = s;
     }
 }
 
-// x_i = L_i^-T L_i^-1 b_i for the segment's row tiles (W0; 16 lanes a tile)
-__device__ void final_solve(const Args &a, const Geo &g, Smem &S, int lane) {
+// x_i = L_i^-T L_i^-1 b_i for the segment's row tiles (W0; a 16-lane row a
+// tile, lane li holding row li and column li of L_i): both substitutions as
+// 16 steps of a DPP broadcast within the row (row_newbcast), a multiply by
+// the pivot's reciprocal (computed up front, off the chain) and an fma
+template <int K>
+__device__ __forceinline__ double bcast16(double v) {
+    double r;
+    asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(v), "n"(K));
+    return r;
+}
+template <int K>
+__device__ __forceinline__ void fwd_step(double &v, const double (&L)[16], const double (&inv)[16], int li) {
+    const double yk = bcast16<K>(v) * inv[K];
+    v = li == K ? yk : li > K ? fma(-L[K], yk, v) : v;
+}
+template <int K>
+__device__ __forceinline__ void bwd_step(double &v, const double (&Lc)[16], const double (&inv)[16], int li) {
+    const double xk = bcast16<K>(v) * inv[K];
+    v = li == K ? xk : li < K ? fma(-Lc[K], xk, v) : v;
+}
+template <int... K>
+__device__ __forceinline__ void tri_solve16(double &v, const double (&L)[16], const double (&Lc)[16],
+                                            const double (&inv)[16], int li, std::integer_sequence<int, K...>) {
+    (fwd_step<K>(v, L, inv, li), ...);
+    (bwd_step<15 - K>(v, Lc, inv, li), ...);
+}
+template <int... K>
+__device__ __forceinline__ void bcast_all16(double d, double (&inv)[16], std::integer_sequence<int, K...>) {
+    ((inv[K] = bcast16<K>(d)), ...);
+}
+__device__ __forceinline__ void final_solve(const double *Lp, double *x, int nseg, int s, int i0, int nrow,
+                                            double v, int lane) {
     const int li = lane & 15, ti = lane >> 4;
-    const bool act = ti < g.nrow;
-    const int i = g.i0 + (act ? ti : 0);
-    double L[16];  // row li of L_i
-    const double *ls = a.Lp + ((int64_t)i * g.nseg + g.s) * 256 + li * 16;
+    const bool act = ti < nrow;
+    const int i = i0 + (act ? ti : 0);
+    double L[16], Lc[16], inv[16];  // row li and column li of L_i
+    const double *ls = Lp + ((int64_t)i * nseg + s) * 256;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) L[j] = ld_ag(ls + j);
-    double v = S.ob[lane];
-    // forward: y = L^-1 b (lane li holds y_li when done)
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const double lkk = __shfl(L[k], (lane & 48) | k);
-        const double yk = __shfl(v, (lane & 48) | k) / lkk;
-        if (li == k) v = yk;
-        if (li > k) v -= L[k] * yk;
+    for (int j = 0; j < 16; ++j) {
+        L[j] = ld_ag(ls + li * 16 + j);
+        Lc[j] = ld_ag(ls + j * 16 + li);
     }
-    // backward: x = L^-T y; lane li needs L[k][li] (row k of L, column li)
+    double d = 0.0;
 #pragma unroll
-    for (int k = 15; k >= 0; --k) {
-        const double lkk = __shfl(L[k], (lane & 48) | k);
-        const double xk = __shfl(v, (lane & 48) | k) / lkk;
-        double lki = 0.0;  // L[k][li] from lane k's row
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const double t = __shfl(L[j], (lane & 48) | k);
-            if (j == li) lki = t;
-        }
-        if (li == k) v = xk;
-        if (li < k) v -= lki * xk;
-    }
-    if (act) st_ag(a.x + i * TL + li, v);
+    for (int j = 0; j < 16; ++j) d = j == li ? L[j] : d;
+    d = act ? 1.0 / d : 1.0;
+    bcast_all16(d, inv, std::make_integer_sequence<int, 16>{});
+    tri_solve16(v, L, Lc, inv, li, std::make_integer_sequence<int, 16>{});
+    if (act) st_ag(x + i * TL + li, v);
 }
 
 __global__ void __launch_bounds__(THREADS) k_gj_solve(Args a) {
     if (a.gate && !*a.gate) return;  // device-side LM control: iteration gated off
     __shared__ Smem S;
+    stamp(a, a.nT, DBG_START);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     Geo g;
     g.nT = a.nT;
@@ -680,7 +745,8 @@ __global__ void __launch_bounds__(THREADS) k_gj_solve(Args a) {
     // ---- prologue
     if (threadIdx.x < 2) S.gm_ok[threadIdx.x] = S.ly_ok[threadIdx.x] = 0;
     if (threadIdx.x < 2 * CBMAX) S.gj_ok[threadIdx.x / CBMAX][threadIdx.x % CBMAX] = 0;
-    if (threadIdx.x < NTMAX) S.pub[threadIdx.x] = S.udone[threadIdx.x] = 0;
+    if (threadIdx.x < CBMAX) S.bb_cnt[threadIdx.x] = 0;
+    if (threadIdx.x < NTMAX) S.udone[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
         S.cst_cnt = S.cst_read = S.abort_ = 0;
         S.err = a.err;
@@ -689,7 +755,7 @@ __global__ void __launch_bounds__(THREADS) k_gj_solve(Args a) {
     d4 acc[TPW];
 #pragma unroll
     for (int k = 0; k < TPW; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
-    const int u = wave - 3;
+    const int u = wave - 4;
     // initial tiles, SR owned columns per pass: every thread gathers up to 8
     // elements from the payload in one round into LDS, then each update wave
     // takes its fragments (column j0's are staged for pivot j0 if j0 == 0)
@@ -742,14 +808,18 @@ __global__ void __launch_bounds__(THREADS) k_gj_solve(Args a) {
     if (threadIdx.x == 0) S.cst_cnt = g.j0 == 0 ? g.nrow + 1 : 0;  // else staged by panel j0 - 1
     __syncthreads();
     // ---- the pivot loop, by role
-    if (wave <= 1) {
+    stamp(a, a.nT, DBG_PROLOGUE);
+    if (wave == 0) {
         for (int p = g.j0; p < g.j1; ++p) {
-            if (!lds_wait(&S.cst_cnt, (p - g.j0 + 1) * (g.nrow + 1), S)) break;
-            chain_pivot(a, g, S, p, wave, lane);
+            if (!lds_wait(&S.cst_cnt, (p - g.j0 + 1) * (g.nrow + 1), S) || !chain_pivot(a, g, S, p, 0, lane)) break;
             if (lds_ld(&S.abort_)) break;
         }
+    } else if (wave == 1) {
+        w1_loop(a, g, S, lane);
     } else if (wave == 2) {
         loader(a, g, S, lane);
+    } else if (wave == 3) {
+        publisher(a, g, S, lane);
     } else {
         updater(a, g, S, u, lane, acc, last_block);
     }
@@ -757,9 +827,11 @@ __global__ void __launch_bounds__(THREADS) k_gj_solve(Args a) {
     if (!last_block) return;
     __shared__ int last_arrival;
     if (wave == 0) {
-        bool ok = lds_wait(&S.udone[a.nT - 1], NUW, S);  // every wave is done with every panel
-        if (ok) final_solve(a, g, S, lane);
+        bool ok = lds_wait(&S.udone[a.nT - 1], NCONS, S);  // every wave is done with every panel
+        stamp(a, a.nT, DBG_FINWAIT);
+        if (ok) final_solve(a.Lp, a.x, g.nseg, g.s, g.i0, g.nrow, S.ob[lane], lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stamp(a, a.nT, DBG_FINSOLVED);
         if (lane == 0) {
             last_arrival = 0;
             if (ok) {
@@ -772,13 +844,16 @@ __global__ void __launch_bounds__(THREADS) k_gj_solve(Args a) {
         }
     }
     __syncthreads();
+    stamp(a, a.nT, DBG_ARRIVED);
     if (!last_arrival || a.ct.nc <= 0) return;
-    double *dc = &S.Gj[0][0][0][0];  // LDS reused: x, then the reductions
-    double *red = &S.Gm[0][0][0][0];
-    static_assert(sizeof(S.Gm) >= 3 * THREADS * sizeof(double), "reduction scratch");
+    double *dc = &S.Gm[0][0][0][0];  // LDS reused: x, then the reductions
+    double *red = &S.Gj[0][0][0][0];
+    static_assert(sizeof(S.Gj) >= 3 * THREADS * sizeof(double), "reduction scratch");
+    static_assert(sizeof(S.Gm) >= 6 * (NTMAX * TL / 6) * sizeof(double), "trial step");
     for (int i = threadIdx.x; i < 6 * a.ct.nc; i += THREADS) dc[i] = ld_ag(a.x + i);
     __syncthreads();
-    cam_trial(a, dc, red);
+    cam_trial(a.ct.nc, a.ct.Rt, a.ct.Rt_new, a.ct.cam_out, *a.lam, a.payload, a.ns, dc, red);
+    stamp(a, a.nT, DBG_EPILOGUE);
 }
 
 }  // namespace gj

@@ -92,6 +92,7 @@ struct ThreadCtx {
     HostBuf pinned;
     void *gj_ints = nullptr;  // sfm_reduced_solve: the flag buffer its epochs refer to
     int gj_epoch = 0;
+    int gj_nT = 0, gj_nseg = 0;  // ... and the layout they were carved with
     ~ThreadCtx() {
         if (stream) {
             (void)hipSetDevice(device);

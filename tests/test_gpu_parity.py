@@ -1051,18 +1051,23 @@ def test_pnp_fast_test_exact_at_threshold(core):
     equals the oracle's strict test on the winning pose."""
     X, x, Ct, Rt = _pnp_scene(4000, 21, outlier_frac=0.2)
     random.seed(21)
-    samples = core.sample_table(len(X), 4, 64)
-    best, bc, C, R, counts, branches = core.pnp_ransac(X, x, K, samples, 1e4, want_counts=True)
-    assert best >= 0
-    one = samples[best:best + 1]
-    err = O.pnp_err(X, x, K, C, R)
+    samples = core.sample_table(len(X), 4, 256)
+    _, _, _, _, counts, branches = core.pnp_ransac(X, x, K, samples, 8.0, want_counts=True)
+    # hypotheses off the det(R) < 0 branch (parity unpinned by construction,
+    # DESIGN §3), the best-supported first
+    hs = [h for h in np.argsort(-counts, kind="stable") if branches[h] == 0][:3]
+    assert hs
     checked = 0
-    for thr in _thresholds_at(err[err < 50.0]):
-        b1, c1, C1, R1, cnt, br = core.pnp_ransac(X, x, K, one, float(thr), want_counts=True)
-        if br[0] != 0:
-            continue  # det(R) < 0 branch: parity unpinned by construction (DESIGN §3)
-        assert cnt[0] == (err < thr).sum(), thr
-        if b1 == 0:  # a winner (>= 4 inliers): its pose is the hypothesis's
-            assert np.array_equal(C1, C) and np.array_equal(R1, R)
-        checked += 1
+    for h in hs:
+        one = samples[h:h + 1]
+        b0, _, C, R, _, _ = core.pnp_ransac(X, x, K, one, 1e4, want_counts=True)
+        assert b0 == 0  # every point an inlier: the hypothesis's pose comes back
+        err = O.pnp_err(X, x, K, C, R)
+        for thr in _thresholds_at(err[err < 50.0]):
+            b1, c1, C1, R1, cnt, br = core.pnp_ransac(X, x, K, one, float(thr), want_counts=True)
+            assert br[0] == 0
+            assert cnt[0] == (err < thr).sum(), thr
+            if b1 == 0:  # a winner (>= 4 inliers): its pose is the hypothesis's
+                assert np.array_equal(C1, C) and np.array_equal(R1, R)
+            checked += 1
     assert checked > 0
