@@ -226,7 +226,6 @@ __device__ __forceinline__ void grid_sum_last(double (&v)[NV], double *partial, 
 //   W  = Jc^T Jp = E (A^T A R),  E = [[p]x ; I]  (6x3)
 // so (r, A, p) is all an observation needs, and it is recomputed from X and
 // the camera wherever it is used (no stored Jacobians).
-constexpr int ZS = 16;  // Schur record: p (3) | G = A^T A R L (9, row-major) | q = L^T g_p (3) | pad: one 128-B line
 
 __device__ __forceinline__ void obs_model(const double *__restrict__ Rt, const double *X, const double (&K)[9],
                                           double2 ob, double (&r)[2], double (&A)[2][3], double (&p)[3]) {
@@ -360,36 +359,21 @@ __global__ void __launch_bounds__(PT_THREADS) k_linearize(int64_t np_, const int
     if (want_cost) grid_sum_last<1>(acc, partial, counter, cost_out);  // only the initial cost is used
 }
 
-// Lq layout per point (9 doubles): L00 L01 L02 L11 L12 L22 | q0 q1 q2
-// Z_o = W_o L = E_o G_o with G_o = A^T (A R L): the Schur record is (p, G, q),
-// q = L^T g_p repeated in every record of the point (k_schur_sweep's
-// diagonal term reads it from the staged record).
-// Thread per OBSERVATION (a thread per point leaves ~1.5 waves per SIMD at
-// cfg4 walking k observations serially): each thread rebuilds its point's
-// 3x3 factor from V (72 B, shared in cache by the point's k threads -- the
-// same arithmetic, so bitwise the same L), the point's first observation
-// also stores (L, q).
+// Lq layout per point (9 doubles): L00 L01 L02 L11 L12 L22 | q0 q1 q2,
+// L = Cinv^T with C C^T = V + lambda clamp(diag V) (so Vd^-1 = L L^T) and
+// q = L^T g_p: everything the sweep and the back substitution need of a
+// point (record-free: no per-observation Schur record is written; the
+// sweep rebuilds each observation's G = A^T (A R L) from X, L and the
+// camera, k_schur_sweep).  A thread per point, 144 B of traffic per point.
 constexpr int OBS_THREADS = 256;
 
-__global__ void __launch_bounds__(OBS_THREADS) k_point_prep(int64_t no, const int32_t *__restrict__ pt,
-                                                            const int32_t *__restrict__ pstart,
-                                                            const int32_t *__restrict__ cam,
-                                                            const double *__restrict__ Rt,
-                                                            const double *__restrict__ X, Kmat Km,
-                                                            const double *__restrict__ Vg, const double *__restrict__ lam,
-                                                            double *__restrict__ Lq, double *__restrict__ Z, const int *__restrict__ gate) {
+__global__ void __launch_bounds__(OBS_THREADS) k_point_prep(int64_t np_, const double *__restrict__ Vg,
+                                                            const double *__restrict__ lam, double *__restrict__ Lq,
+                                                            const int *__restrict__ gate) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
-    // records go out through LDS so a wave's stores cover whole 128-B lines
-    // with lane-consecutive 16-B pieces (a thread's own 128 B record written
-    // directly is 8 stores at a 128-B lane stride: measured 58 -> 23 us when
-    // the stores are dropped, i.e. the strided write was the bound)
-    __shared__ double2 zs[OBS_THREADS * 8];  // 8 pieces per record, XOR-swizzled against bank conflicts
+    const int64_t p = (int64_t)blockIdx.x * OBS_THREADS + threadIdx.x;
+    if (p >= np_) return;
     const double lambda = *lam;
-    const int64_t o0 = (int64_t)blockIdx.x * OBS_THREADS;
-    const int64_t o = o0 + threadIdx.x;
-    const int nrec = (int)min<int64_t>(OBS_THREADS, no - o0);
-    if (o < no) {
-    const int64_t p = pt[o];
     const double *vg = Vg + 9 * p;
     const double v00 = vg[0] + lambda * clampd(vg[0]), v01 = vg[1], v02 = vg[2];
     const double v11 = vg[3] + lambda * clampd(vg[3]), v12 = vg[4];
@@ -404,45 +388,11 @@ __global__ void __launch_bounds__(OBS_THREADS) k_point_prep(int64_t no, const in
     // L = Cinv^T (upper): Vd^-1 = L L^T
     const double L[3][3] = {{i00, i10, i20}, {0.0, i11, i21}, {0.0, 0.0, i22}};
     const double g0 = vg[6], g1 = vg[7], g2 = vg[8];
-    const double qp[3] = {L[0][0] * g0, L[0][1] * g0 + L[1][1] * g1, L[0][2] * g0 + L[1][2] * g1 + L[2][2] * g2};
-    if (o == pstart[p]) {
-        double *lq = Lq + 9 * p;
-        lq[0] = L[0][0]; lq[1] = L[0][1]; lq[2] = L[0][2]; lq[3] = L[1][1]; lq[4] = L[1][2]; lq[5] = L[2][2];
-        lq[6] = qp[0]; lq[7] = qp[1]; lq[8] = qp[2];
-    }
-    double K[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) K[i] = Km.k[i];
-    const double *R = Rt + 12 * cam[o];
-    const double xp[3] = {X[3 * p], X[3 * p + 1], X[3 * p + 2]};
-    double A[2][3], q[3];
-    obs_Ap(R, xp, K, A, q);
-    double T[2][3];  // (A R) L
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-        double ar[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) ar[c] = A[a][0] * R[c] + A[a][1] * R[3 + c] + A[a][2] * R[6 + c];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) T[a][c] = ar[0] * L[0][c] + ar[1] * L[1][c] + ar[2] * L[2][c];
-    }
-    double z[ZS];
-    z[0] = q[0]; z[1] = q[1]; z[2] = q[2];
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) z[3 + 3 * i + c] = A[0][i] * T[0][c] + A[1][i] * T[1][c];
-    z[12] = qp[0]; z[13] = qp[1]; z[14] = qp[2]; z[15] = 0.0;
-#pragma unroll
-    for (int k = 0; k < ZS / 2; ++k) zs[threadIdx.x * 8 + (k ^ (threadIdx.x & 7))] = make_double2(z[2 * k], z[2 * k + 1]);
-    }
-    __syncthreads();
-    double2 *zout = reinterpret_cast<double2 *>(Z + (int64_t)ZS * o0);
-#pragma unroll
-    for (int u = 0; u < ZS / 2; ++u) {
-        const int k = threadIdx.x + OBS_THREADS * u, rec = k >> 3;
-        if (rec < nrec) zout[k] = zs[rec * 8 + ((k & 7) ^ (rec & 7))];
-    }
+    double *lq = Lq + 9 * p;
+    lq[0] = L[0][0]; lq[1] = L[0][1]; lq[2] = L[0][2]; lq[3] = L[1][1]; lq[4] = L[1][2]; lq[5] = L[2][2];
+    lq[6] = L[0][0] * g0;
+    lq[7] = L[0][1] * g0 + L[1][1] * g1;
+    lq[8] = L[0][2] * g0 + L[1][2] * g1 + L[2][2] * g2;
 }
 
 // Payload layout (doubles): S as its upper-triangle 6x6 camera blocks
@@ -607,55 +557,92 @@ __global__ void __launch_bounds__(THREADS) k_camera_lin(CamLinArgs a) {
 
 // ---------------------------------------------------------------------
 // Reduced camera system S_ij = [i==j] U_i - sum_{p seen by i and j} Z_pi Z_pj^T
-// as a sweep over point ranges (the Schur record of an observation is
-// (p, G, q): Z = E G with E = [[p]x; I], q = L^T g_p; pair term
-// S_ab = E_a (G_a G_b^T) E_b^T).
+// as a sweep over point ranges, record-free: an observation's Schur factor
+// is (p, G) with Z = E G, E = [[p]x; I], G = A^T (A R L) = M L, M = A^T A R,
+// p = R X, and the pair term is S_ab = E_a (G_a G_b^T) E_b^T with
+// G_a G_b^T = (G_a L^T) M_b^T = F_a M_b^T (L L^T = Vd^-1 of the shared
+// point).  Both observations of a pair see the same point, so a pair needs
+// only the a side's (p_a, F_a), the point's X and the b camera.
 //
 // The points (with their observations, point-major) are cut into NR
-// ranges of equal observation count and every range into chunks whose
-// records fit an XCD's L2.  A workgroup owns a fixed set of camera-block
-// rows (a "spec": cameras i and nc-1-i, so every spec has the same pair
-// work) and sweeps one range chunk by chunk:
-//   * the chunk's records of the spec's own cameras (the "a" side of every
-//     pair) are staged in LDS by LDS-DMA, double-buffered one chunk ahead;
+// ranges of equal observation count and every range into chunks.  A
+// workgroup owns a fixed set of camera-block rows (a "spec": cameras i and
+// nc-1-i, so every spec has the same pair work) and sweeps one range chunk
+// by chunk:
+//   * the chunk's observations of the spec's own cameras (the "a" side of
+//     every pair) are staged in LDS one chunk ahead by two staging waves,
+//     each as a slot (p_a, F_a, G_a q, X) computed from the point's X and
+//     Lq and the spec's camera;
 //   * every block (i, j) of the spec is owned by one lane group (2 lanes
 //     per pair slot, group size proportional to the block's pair count)
-//     that accumulates its 6x6 block in registers over the whole range;
-//     the "b" records are gathered from global memory -- the range's
-//     workgroups all run on one XCD (blockIdx % 8) and walk the same
-//     chunks at the same pace, so those gathers hit that XCD's L2;
+//     that accumulates its 6x6 block in registers over the whole range; the
+//     "b" side of a pair, M_b, is rebuilt from the slot's X and the group's
+//     own camera j (registers): no global memory access in the pair loop;
 //   * at the end every group reduces its slots (fixed butterfly) and writes
 //     its block to slab[range][block]; k_schur_finish sums the ranges in
 //     order.  Deterministic, no atomics.
-// Compared with one gather of both records per pair from a pair list sorted
-// by camera block, the a side comes from LDS and the b side from L2.
 constexpr int SW_THREADS = 768;
-constexpr int SW_MAX_STAGED = 512;  // records per (chunk, spec): 2 x 64 KiB of LDS
-constexpr int SW_MAX_COLS = SW_THREADS / 2 - 32;  // blocks per spec (2 lanes each, one loader wave)
+constexpr int SW_MAX_STAGED = 512;  // slots per (chunk, spec)
+constexpr int SW_MAX_COLS = SW_THREADS / 2 - 96;  // blocks per spec (2 lanes each; a loader wave, two staging waves)
 constexpr int NXCD = 8;
+constexpr int SLOT_D = 18;  // staged slot (doubles): p (3) | F = G L^T (9, row-major) | G q (3) | X (3)
+constexpr int SW_STAGE_WAVES = 2;  // waves that stage the next chunk (no lane group)
+constexpr int SW_STAGE_BATCH = 4;  // slots a staging lane has in flight
 
 struct SweepGroup {
     int32_t blk, lane_base, G, flags;  // flags: 1 = diagonal block, 2 = a side is the spec's second camera
+    int32_t cam_b;                     // the block's column camera (the b side of every pair)
 };
 
-// record piece k (16 B) of staged slot s, XOR-swizzled against bank conflicts
-__device__ __forceinline__ double2 lds_piece(const double2 *buf, int s, int k) { return buf[s * 8 + (k ^ (s & 7))]; }
-
-__device__ __forceinline__ void load_rec_lds(const double2 *buf, int s, double (&p)[3], double (&G)[3][3]) {
-    const double2 v0 = lds_piece(buf, s, 0), v1 = lds_piece(buf, s, 1), v2 = lds_piece(buf, s, 2);
-    const double2 v3 = lds_piece(buf, s, 3), v4 = lds_piece(buf, s, 4), v5 = lds_piece(buf, s, 5);
-    p[0] = v0.x; p[1] = v0.y; p[2] = v1.x;
-    G[0][0] = v1.y; G[0][1] = v2.x; G[0][2] = v2.y;
-    G[1][0] = v3.x; G[1][1] = v3.y; G[1][2] = v4.x;
-    G[2][0] = v4.y; G[2][1] = v5.x; G[2][2] = v5.y;
+// an observation's (p, G) from its camera, the point X and the point's
+// factor l = (L00 L01 L02 L11 L12 L22): p = R X, G = A^T (A R L)
+__device__ __forceinline__ void obs_pG(const double *R, const double (&x)[3], const double (&K)[9],
+                                       const double (&l)[6], double (&p)[3], double (&G)[3][3]) {
+    double A[2][3];
+    obs_Ap(R, x, K, A, p);
+    const double L[3][3] = {{l[0], l[1], l[2]}, {0.0, l[3], l[4]}, {0.0, 0.0, l[5]}};
+    double T[2][3];  // (A R) L
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        double ar[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) ar[c] = A[a][0] * R[c] + A[a][1] * R[3 + c] + A[a][2] * R[6 + c];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) T[a][c] = ar[0] * L[0][c] + ar[1] * L[1][c] + ar[2] * L[2][c];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) G[i][c] = A[0][i] * T[0][c] + A[1][i] * T[1][c];
 }
 
-__device__ __forceinline__ void load_rec_glb(const double2 *__restrict__ z, double (&p)[3], double (&G)[3][3]) {
-    const double2 v0 = z[0], v1 = z[1], v2 = z[2], v3 = z[3], v4 = z[4], v5 = z[5];
+// M = A^T (A R) of an observation and its p = R X, from the camera and X
+__device__ __forceinline__ void obs_pM(const double *R, const double (&x)[3], const double (&K)[9], double (&p)[3],
+                                       double (&M)[3][3]) {
+    double A[2][3];
+    obs_Ap(R, x, K, A, p);
+    double ar[2][3];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) ar[a][c] = A[a][0] * R[c] + A[a][1] * R[3 + c] + A[a][2] * R[6 + c];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) M[i][c] = A[0][i] * ar[0][c] + A[1][i] * ar[1][c];
+}
+
+// slot pieces (16 B): 0-5 p, F | 6 Gq0 Gq1 | 7 Gq2 X0 | 8 X1 X2
+__device__ __forceinline__ void load_slot_a(const double2 *sl, double (&p)[3], double (&F)[3][3]) {
+    const double2 v0 = sl[0], v1 = sl[1], v2 = sl[2], v3 = sl[3], v4 = sl[4], v5 = sl[5];
     p[0] = v0.x; p[1] = v0.y; p[2] = v1.x;
-    G[0][0] = v1.y; G[0][1] = v2.x; G[0][2] = v2.y;
-    G[1][0] = v3.x; G[1][1] = v3.y; G[1][2] = v4.x;
-    G[2][0] = v4.y; G[2][1] = v5.x; G[2][2] = v5.y;
+    F[0][0] = v1.y; F[0][1] = v2.x; F[0][2] = v2.y;
+    F[1][0] = v3.x; F[1][1] = v3.y; F[1][2] = v4.x;
+    F[2][0] = v4.y; F[2][1] = v5.x; F[2][2] = v5.y;
+}
+__device__ __forceinline__ void load_slot_x(const double2 *sl, double (&x)[3]) {
+    const double2 v7 = sl[7], v8 = sl[8];
+    x[0] = v7.y; x[1] = v8.x; x[2] = v8.y;
 }
 
 __device__ __forceinline__ void cross_rows(const double (&p)[3], const double (&H)[3][3], double (&X)[3][3]) {
@@ -668,14 +655,14 @@ __device__ __forceinline__ void cross_rows(const double (&p)[3], const double (&
     }
 }
 
-// rows 3h..3h+2 of S_ab = E_a (G_a G_b^T) E_b^T into acc[0..18)
-__device__ __forceinline__ void pair_block(int h, const double (&pa)[3], const double (&Ga)[3][3],
-                                           const double (&pb)[3], const double (&Gb)[3][3], double (&acc)[21]) {
-    double H[3][3];  // G_a G_b^T
+// rows 3h..3h+2 of S_ab = E_a H E_b^T, H = G_a G_b^T = F_a M_b^T, into acc[0..18)
+__device__ __forceinline__ void pair_block(int h, const double (&pa)[3], const double (&Fa)[3][3],
+                                           const double (&pb)[3], const double (&Mb)[3][3], double (&acc)[21]) {
+    double H[3][3];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) H[i][j] = Ga[i][0] * Gb[j][0] + Ga[i][1] * Gb[j][1] + Ga[i][2] * Gb[j][2];
+        for (int j = 0; j < 3; ++j) H[i][j] = Fa[i][0] * Mb[j][0] + Fa[i][1] * Mb[j][1] + Fa[i][2] * Mb[j][2];
     double X[3][3];
     if (h == 0) {
         cross_rows(pa, H, X);
@@ -696,71 +683,40 @@ __device__ __forceinline__ void pair_block(int h, const double (&pa)[3], const d
     }
 }
 
-// Staging is done by LOADER waves: the waves that hold the diagonal groups
-// (those read only LDS), or one wave of their own when a spec has no
-// diagonal block.  vmcnt is per wave and counts LDS-DMA with ordinary loads
-// in issue order, so a wave gathering b records from global memory with
-// LDS-DMA in flight would wait for the whole staging at every use of its
-// prefetched record; the off-diagonal (gathering) waves never issue any.
-//
-// LDS per buffer (4-B words): records [buf_slots][32] | pairs [pair_cap] |
-// header [hdr_cap] (group pair offsets (ngroups + 1), n0, n1, chunk obs0) |
-// list [list_cap] (absolute record index of every staged slot).  Chunk q
-// uses buffer q & 1; its list is fetched one chunk earlier.
+// LDS per buffer (4-B words): slots [buf_slots][2 * SLOT_D] | pairs
+// [pair_cap / 2] (16-bit slot indices) | header [hdr_cap] (group pair offsets (ngroups + 1), n0, n1,
+// chunk obs0); after both buffers the spec's two cameras (24 doubles).
+// Chunk q uses buffer q & 1.  The list (global, list_cap words per
+// (chunk, spec)) holds every slot's point | (row << 31).
 struct SweepLds {
     int buf_slots, pair_cap, hdr_cap, list_cap;
-    __device__ int words() const { return buf_slots * 32 + pair_cap + hdr_cap + list_cap; }
+    __device__ int words() const { return buf_slots * 2 * SLOT_D + pair_cap / 2 + hdr_cap; }
 };
 
 __device__ __forceinline__ void glds4(const void *src, void *lds) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void *)lds, 4, 0, 0);
 }
 
-// loader lanes (t < 64 nload): the list words of region qw
-__device__ __forceinline__ void sweep_fetch_list(int t, int nload, int64_t qw, const SweepLds &L,
-                                                 const int32_t *__restrict__ list, uint32_t *bufw) {
-    uint32_t *lw = bufw + L.buf_slots * 32 + L.pair_cap + L.hdr_cap;
-    for (int base = (t & ~63); base < L.list_cap; base += 64 * nload) glds4(list + qw * L.list_cap + base + (t & 63), lw + base);
-}
-
-// loader lanes: records (16-B pieces; swizzle applied on the global side,
-// LDS image linear), pairs and header of region qw; the list is in LDS
+// loader lanes (t < 64 nload): pairs and header of region qw, LDS-DMA
 __device__ __forceinline__ void sweep_fetch(int t, int nload, int64_t qw, const SweepLds &L,
-                                            const double *__restrict__ Z, const uint32_t *__restrict__ pairs,
-                                            const int32_t *__restrict__ hdr, uint32_t *bufw) {
+                                            const uint32_t *__restrict__ pairs, const int32_t *__restrict__ hdr,
+                                            uint32_t *bufw) {
     const int lane = t & 63, step = 64 * nload;
-    const int32_t *lw = reinterpret_cast<const int32_t *>(bufw + L.buf_slots * 32 + L.pair_cap + L.hdr_cap);
-    const int npc = L.buf_slots * 8;
-    for (int base = (t & ~63); base < npc; base += 8 * step) {
-        int32_t rec[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int idx = base + u * step + lane;
-            rec[u] = idx < npc ? lw[idx >> 3] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int b0 = base + u * step;
-            if (b0 < npc) {
-                const int idx = b0 + lane, s = idx >> 3, k = (idx & 7) ^ (s & 7);
-                __builtin_amdgcn_global_load_lds(Z + (int64_t)rec[u] * 16 + 2 * k,
-                                                 (__attribute__((address_space(3))) void *)(bufw + 4 * b0), 16, 0, 0);
-            }
-        }
-    }
-    uint32_t *pw = bufw + L.buf_slots * 32;
-    for (int base = (t & ~63); base < L.pair_cap; base += step) glds4(pairs + qw * L.pair_cap + base + lane, pw + base);
-    uint32_t *hw = pw + L.pair_cap;
+    uint32_t *pw = bufw + L.buf_slots * 2 * SLOT_D;
+    const int pwords = L.pair_cap / 2;
+    for (int base = (t & ~63); base < pwords; base += step) glds4(pairs + qw * pwords + base + lane, pw + base);
+    uint32_t *hw = pw + pwords;
     for (int base = (t & ~63); base < L.hdr_cap; base += step) glds4(hdr + qw * L.hdr_cap + base + lane, hw + base);
 }
 
 __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     int32_t nspec, int32_t nrange, int32_t nbd, SweepLds L, const int32_t *__restrict__ rchunk,
-    const int32_t *__restrict__ spec_nload,
-    const int32_t *__restrict__ spec_goff, const SweepGroup *__restrict__ groups, const int16_t *__restrict__ lanegrp,
-    const int32_t *__restrict__ list, const uint32_t *__restrict__ pairs, const int32_t *__restrict__ hdr,
-    const double *__restrict__ Z, double *__restrict__ slab, const int *__restrict__ gate, int dbg, int nsweep,
-    CamLinArgs cl) {
+    const int32_t *__restrict__ spec_nload, const int32_t *__restrict__ spec_goff,
+    const SweepGroup *__restrict__ groups, const int16_t *__restrict__ lanegrp,
+    const int32_t *__restrict__ spec_cam, const uint32_t *__restrict__ list, const uint32_t *__restrict__ pairs,
+    const int32_t *__restrict__ hdr, const double *__restrict__ Xg, const double *__restrict__ Lq,
+    const double *__restrict__ Rt, Kmat Km, double *__restrict__ slab, const int *__restrict__ gate, int dbg,
+    int nsweep, CamLinArgs cl) {
     extern __shared__ double2 sw_lds[];
     if ((int)blockIdx.x >= nsweep) {  // camera blocks of the normal equations on the CUs the sweep leaves idle
         if (!*cl.glin) return;
@@ -779,45 +735,119 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     const bool loader = (t >> 6) < nload;
     const int gi = lanegrp[w * SW_THREADS + t];
     const int ng = spec_goff[w + 1] - spec_goff[w];
-    SweepGroup grp = {0, 0, 2, 0};
+    SweepGroup grp = {0, 0, 2, 0, 0};
     if (gi >= 0) grp = groups[spec_goff[w] + gi];
     const int h = (t - grp.lane_base) & 1, slot = (t - grp.lane_base) >> 1, nslot = grp.G >> 1;
     const bool diag = grp.flags & 1, second = grp.flags & 2;
     const int bw = L.words();
+    double *scam = reinterpret_cast<double *>(ldsw + 2 * bw);  // the spec's cameras (rows 0 and 1)
+    if (t < 24) {
+        const int c = spec_cam[2 * w + t / 12];
+        scam[t] = c >= 0 ? Rt[12 * c + t % 12] : 0.0;
+    }
+    double K[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) K[i] = Km.k[i];
+    const int q0 = rchunk[r], q1 = rchunk[r + 1];
+    const int tst = t - (SW_THREADS - 64 * SW_STAGE_WAVES);
+    // a scalar branch: the two roles run different barrier sequences, and a
+    // barrier inside an exec-masked (divergent) region would still execute
+    if (__builtin_amdgcn_readfirstlane(t >> 6) >= SW_THREADS / 64 - SW_STAGE_WAVES) {
+        // staging waves (no lane group): chunk q + 1's slots into the other
+        // buffer while the groups work on chunk q; SW_STAGE_BATCH slots a
+        // lane per round, their list entries, then their points' X and Lq,
+        // all in flight together.  The same barriers as the groups below.
+        auto stage_chunk = [&](int qs, uint32_t *bw_dst) {
+            const uint32_t *lst = list + ((int64_t)qs * nspec + w) * L.list_cap;
+            // (the list is padded to list_cap entries; only buf_slots slots exist)
+            for (int s0 = tst; s0 < L.buf_slots; s0 += 64 * SW_STAGE_WAVES * SW_STAGE_BATCH) {
+                uint32_t e[SW_STAGE_BATCH];
+                double gx[SW_STAGE_BATCH][3], gl[SW_STAGE_BATCH][9];
+#pragma unroll
+                for (int u = 0; u < SW_STAGE_BATCH; ++u) {
+                    const int sl = s0 + u * 64 * SW_STAGE_WAVES;
+                    e[u] = sl < L.buf_slots ? lst[sl] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < SW_STAGE_BATCH; ++u) {
+                    const int64_t P = e[u] & 0x7fffffffu;
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) gx[u][i] = Xg[3 * P + i];
+#pragma unroll
+                    for (int i = 0; i < 9; ++i) gl[u][i] = Lq[9 * P + i];
+                }
+#pragma unroll
+                for (int u = 0; u < SW_STAGE_BATCH; ++u) {
+                    const int sl = s0 + u * 64 * SW_STAGE_WAVES;
+                    if (sl >= L.buf_slots) continue;
+                    const double *R = scam + 12 * (int)(e[u] >> 31);
+                    const double l[6] = {gl[u][0], gl[u][1], gl[u][2], gl[u][3], gl[u][4], gl[u][5]};
+                    const double x[3] = {gx[u][0], gx[u][1], gx[u][2]};
+                    double pa[3], G[3][3], F[3][3], gq[3];
+                    obs_pG(R, x, K, l, pa, G);
+                    // F = G L^T (L upper: L^T[k][c] = L[c][k], k >= c); G q
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) {
+                        F[i][0] = G[i][0] * l[0] + G[i][1] * l[1] + G[i][2] * l[2];
+                        F[i][1] = G[i][1] * l[3] + G[i][2] * l[4];
+                        F[i][2] = G[i][2] * l[5];
+                        gq[i] = G[i][0] * gl[u][6] + G[i][1] * gl[u][7] + G[i][2] * gl[u][8];
+                    }
+                    double2 *d = reinterpret_cast<double2 *>(bw_dst) + sl * (SLOT_D / 2);
+                    d[0] = make_double2(pa[0], pa[1]);
+                    d[1] = make_double2(pa[2], F[0][0]);
+                    d[2] = make_double2(F[0][1], F[0][2]);
+                    d[3] = make_double2(F[1][0], F[1][1]);
+                    d[4] = make_double2(F[1][2], F[2][0]);
+                    d[5] = make_double2(F[2][1], F[2][2]);
+                    d[6] = make_double2(gq[0], gq[1]);
+                    d[7] = make_double2(gq[2], x[0]);
+                    d[8] = make_double2(x[1], x[2]);
+                }
+            }
+        };
+        __syncthreads();  // the cameras are in LDS
+        if (q0 < q1) stage_chunk(q0, ldsw);
+        __syncthreads();
+        for (int q = q0; q < q1; ++q) {
+            if (q + 1 < q1) stage_chunk(q + 1, ldsw + (((q - q0) & 1) ^ 1) * bw);
+            __syncthreads();
+        }
+        for (int k0 = 0; k0 < 21; k0 += 7) {  // the reduction's barriers
+            __syncthreads();
+            __syncthreads();
+        }
+        return;
+    }
+    double Rb[12];  // the group's column camera (the b side; the a camera itself for a diagonal block)
+#pragma unroll
+    for (int k = 0; k < 12; ++k) Rb[k] = gi >= 0 ? Rt[12 * grp.cam_b + k] : 0.0;
     double acc[21];
 #pragma unroll
     for (int k = 0; k < 21; ++k) acc[k] = 0.0;
-    const int q0 = rchunk[r], q1 = rchunk[r + 1];
-    if (loader && q0 < q1) sweep_fetch_list(t, nload, (int64_t)q0 * nspec + w, L, list, ldsw);
-    __syncthreads();
-    if (loader && q0 < q1) {
-        sweep_fetch(t, nload, (int64_t)q0 * nspec + w, L, Z, pairs, hdr, ldsw);
-        if (q0 + 1 < q1) sweep_fetch_list(t, nload, (int64_t)(q0 + 1) * nspec + w, L, list, ldsw + bw);
-    }
-    __syncthreads();
+    if (q0 < q1 && loader) sweep_fetch(t, nload, (int64_t)q0 * nspec + w, L, pairs, hdr, ldsw);
+    __syncthreads();  // the cameras are in LDS
+    __syncthreads();  // chunk q0's slots are staged
     for (int q = q0; q < q1; ++q) {
         const int cur = (q - q0) & 1;
         const uint32_t *bufw = ldsw + cur * bw;
-        if (loader && q + 1 < q1 && !(dbg & 4)) {
-            sweep_fetch(t, nload, (int64_t)(q + 1) * nspec + w, L, Z, pairs, hdr, ldsw + (cur ^ 1) * bw);
-            if (q + 2 < q1) sweep_fetch_list(t, nload, (int64_t)(q + 2) * nspec + w, L, list, ldsw + cur * bw);
-        }
+        if (loader && q + 1 < q1) sweep_fetch(t, nload, (int64_t)(q + 1) * nspec + w, L, pairs, hdr, ldsw + (cur ^ 1) * bw);
         if (gi >= 0) {
             const double2 *buf = reinterpret_cast<const double2 *>(bufw);
-            const uint32_t *pl = bufw + L.buf_slots * 32;
-            const int32_t *hd = reinterpret_cast<const int32_t *>(pl + L.pair_cap);
+            const uint32_t *pl = bufw + L.buf_slots * 2 * SLOT_D;
+            const int32_t *hd = reinterpret_cast<const int32_t *>(pl + L.pair_cap / 2);
             const int n0 = hd[ng + 1], n1 = hd[ng + 2];
-            if (diag) {  // S_ii: the camera's own records, b = a; plus sum Z_a q_p
+            if (diag) {  // S_ii: the camera's own observations, b = a; plus sum Z_a q_p
                 const int a0 = second ? n0 : 0, a1 = (dbg & 2) ? a0 : second ? n0 + n1 : n0;
                 for (int a = a0 + slot; a < a1; a += nslot) {
-                    double pa[3], Ga[3][3];
-                    load_rec_lds(buf, a, pa, Ga);
-                    pair_block(h, pa, Ga, pa, Ga, acc);
-                    const double2 v6 = lds_piece(buf, a, 6), v7 = lds_piece(buf, a, 7);
-                    const double qv[3] = {v6.x, v6.y, v7.x};
-                    double gq[3];
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) gq[i] = Ga[i][0] * qv[0] + Ga[i][1] * qv[1] + Ga[i][2] * qv[2];
+                    const double2 *sl = buf + a * (SLOT_D / 2);
+                    double pa[3], Fa[3][3], x[3], pm[3], Ma[3][3];
+                    load_slot_a(sl, pa, Fa);
+                    load_slot_x(sl, x);
+                    obs_pM(Rb, x, K, pm, Ma);
+                    pair_block(h, pa, Fa, pa, Ma, acc);
+                    const double2 v6 = sl[6], v7 = sl[7];
+                    const double gq[3] = {v6.x, v6.y, v7.x};  // G_a q
                     if (h == 0) {
                         acc[18] += -pa[2] * gq[1] + pa[1] * gq[2];
                         acc[19] += pa[2] * gq[0] - pa[0] * gq[2];
@@ -828,33 +858,18 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
                 }
             } else {
                 const int k0 = hd[gi], k1 = (dbg & 1) ? k0 : hd[gi + 1];
-                const double2 *zc = reinterpret_cast<const double2 *>(Z) + (int64_t)hd[ng + 3] * 8;
-                // b records prefetched one pair ahead (L2 latency off the
-                // chain), two register sets used alternately
-                int k = k0 + slot;
-                uint32_t pr0 = k < k1 ? pl[k] : 0u, pr1 = 0u;
-                double pb0[3] = {0, 0, 0}, Gb0[3][3] = {}, pb1[3] = {0, 0, 0}, Gb1[3][3] = {};
-                if (k < k1) load_rec_glb(zc + (int64_t)(pr0 & 0xffffu) * 8, pb0, Gb0);
-                for (; k < k1; k += 2 * nslot) {
-                    const int k1n = k + nslot, k2n = k + 2 * nslot;
-                    if (k1n < k1) {
-                        pr1 = pl[k1n];
-                        load_rec_glb(zc + (int64_t)(pr1 & 0xffffu) * 8, pb1, Gb1);
-                    }
-                    double pa[3], Ga[3][3];
-                    load_rec_lds(buf, (int)(pr0 >> 16), pa, Ga);
-                    pair_block(h, pa, Ga, pb0, Gb0, acc);
-                    if (k1n >= k1) break;
-                    if (k2n < k1) {
-                        pr0 = pl[k2n];
-                        load_rec_glb(zc + (int64_t)(pr0 & 0xffffu) * 8, pb0, Gb0);
-                    }
-                    load_rec_lds(buf, (int)(pr1 >> 16), pa, Ga);
-                    pair_block(h, pa, Ga, pb1, Gb1, acc);
+                const uint16_t *pl16 = reinterpret_cast<const uint16_t *>(pl);
+                for (int k = k0 + slot; k < k1; k += nslot) {
+                    const double2 *sl = buf + (int)pl16[k] * (SLOT_D / 2);
+                    double pa[3], Fa[3][3], x[3], pb[3], Mb[3][3];
+                    load_slot_a(sl, pa, Fa);
+                    load_slot_x(sl, x);
+                    obs_pM(Rb, x, K, pb, Mb);  // the b side: camera j, the same point
+                    pair_block(h, pa, Fa, pb, Mb, acc);
                 }
             }
         }
-        __syncthreads();  // chunk q's buffer is free; chunk q+1's staging has landed
+        __syncthreads();  // chunk q's buffer is free; chunk q+1's slots, pairs and header have landed
     }
     // reduce the group's slots (lanes of equal parity) in slot order through
     // LDS (the staging buffers are free now), 7 accumulators per round;
@@ -1938,12 +1953,14 @@ using namespace sfm;
 // chunk obs0).
 struct SweepPlan {
     int32_t nrange = 0, nspec = 0, nbd = 0, buf_slots = 0, pair_cap = 0, hdr_cap = 0, list_cap = 0, nchunk = 0;
-    std::vector<int32_t> rchunk, goff, nload, list, hdr;
+    std::vector<int32_t> rchunk, goff, nload, list, hdr, spec_cam;
     std::vector<SweepGroup> groups;
     std::vector<int16_t> lanegrp;
-    std::vector<uint32_t> pairs;
+    std::vector<uint16_t> pairs;
     std::vector<int2> blkij;
-    size_t lds_bytes() const { return (size_t)2 * (buf_slots * 128 + (size_t)(pair_cap + hdr_cap + list_cap) * 4); }
+    size_t lds_bytes() const {
+        return (size_t)2 * (buf_slots * SLOT_D * 8 + (size_t)pair_cap * 2 + (size_t)hdr_cap * 4) + 24 * sizeof(double);
+    }
 };
 
 static int env_int(const char *name, int dflt) {
@@ -2004,6 +2021,10 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
             for (int j0 = i; j0 < nc; j0 += SW_MAX_COLS) specs.push_back({{i, j0, std::min(nc, j0 + SW_MAX_COLS)}});
     }
     P.nspec = (int32_t)specs.size();
+    for (auto &sp : specs) {  // the a-side cameras of every spec (rows 0 and 1)
+        P.spec_cam.push_back(sp[0].c);
+        P.spec_cam.push_back(sp.size() > 1 ? sp[1].c : -1);
+    }
     // block (i <= j) -> spec that owns it
     std::vector<int32_t> spec_of((size_t)nc * nc, -1);
     for (int w = 0; w < P.nspec; ++w)
@@ -2016,7 +2037,7 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     std::vector<std::vector<int>> gid_of(P.nspec);  // (row, j - j0) -> group index within spec
     int max_ng = 0;
     for (int w = 0; w < P.nspec; ++w) {
-        struct G0 { int blk, flags, slots; double work; int key; };
+        struct G0 { int blk, flags, slots; double work; int key, cam_b; };
         std::vector<G0> gd, g;
         double tot = 0;
         for (size_t rr = 0; rr < specs[w].size(); ++rr) {
@@ -2024,7 +2045,7 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
             for (int j = R.j0; j < R.j1; ++j) {
                 const double work = (double)cnt[(size_t)R.c * nc + j];
                 G0 x = {dense_blk(nc, R.c, j), (j == R.c ? 1 : 0) | (rr == 1 ? 2 : 0), 1, work,
-                        (int)(rr * nc + (j - R.j0))};
+                        (int)(rr * nc + (j - R.j0)), j};
                 if (j == R.c) {
                     gd.push_back(x);
                 } else {
@@ -2037,7 +2058,7 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
         int Gd = 64, nload = 1, budget = 0;
         for (; Gd >= 2; Gd /= 2) {
             nload = std::max(1, (nd * Gd + 63) / 64);
-            budget = (SW_THREADS - 64 * nload) / 2;
+            budget = (SW_THREADS - 64 * nload - 64 * SW_STAGE_WAVES) / 2;
             if (noff <= budget) break;
         }
         // slots in proportion to the block's pair work, the whole budget
@@ -2079,7 +2100,7 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
         for (size_t k = 0; k < g.size(); ++k) {
             if (k == gd.size()) lane = 64 * nload;  // off-diagonal groups after the loader waves
             const int G = 2 * g[k].slots;
-            P.groups.push_back({g[k].blk, lane, G, g[k].flags});
+            P.groups.push_back({g[k].blk, lane, G, g[k].flags, g[k].cam_b});
             for (int l = lane; l < lane + G; ++l) P.lanegrp[(size_t)w * SW_THREADS + l] = (int16_t)k;
             gid_of[w][g[k].key] = (int)k;
             lane += G;
@@ -2132,7 +2153,7 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
             P.rchunk.push_back((int32_t)cut.size());
         }
         P.buf_slots = std::max(8, (max_staged + 7) / 8 * 8);
-        P.pair_cap = std::max(64, (max_pairs + 63) / 64 * 64);
+        P.pair_cap = std::max(128, (max_pairs + 127) / 128 * 128);  // 16-bit entries, whole 64-lane DMA rows
         P.list_cap = (P.buf_slots + 63) / 64 * 64;
         if ((ok && max_staged <= SW_MAX_STAGED && P.lds_bytes() <= 160 * 1024) || chunk_obs <= 64) break;
         chunk_obs /= 2;
@@ -2140,7 +2161,7 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     P.nchunk = (int32_t)cut.size();
     const size_t nqw = (size_t)P.nchunk * P.nspec;
     P.list.assign(nqw * P.list_cap, 0);
-    P.pairs.assign(nqw * P.pair_cap, 0u);
+    P.pairs.assign(nqw * P.pair_cap, 0);
     P.hdr.assign(nqw * P.hdr_cap, 0);
     std::vector<std::vector<int32_t>> per_cam(nc);
     std::vector<int32_t> slot_of;  // chunk-local obs offset -> position in its camera's list
@@ -2160,10 +2181,11 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
             int32_t *lst = &P.list[qw * P.list_cap];
             const int32_t n0 = (int32_t)per_cam[sp[0].c].size();
             const int32_t n1 = sp.size() > 1 ? (int32_t)per_cam[sp[1].c].size() : 0;
-            int ns_ = 0;
+            int ns_ = 0;  // every slot's point | (spec row << 31)
             for (size_t rr = 0; rr < sp.size(); ++rr)
-                for (int32_t off : per_cam[sp[rr].c]) lst[ns_++] = o0 + off;
-            for (; ns_ < P.list_cap; ++ns_) lst[ns_] = o0;  // padding: any valid record
+                for (int32_t off : per_cam[sp[rr].c])
+                    lst[ns_++] = (int32_t)((uint32_t)pt[o0 + off] | (rr ? 0x80000000u : 0u));
+            for (; ns_ < P.list_cap; ++ns_) lst[ns_] = pt[o0];  // padding: any valid point
             const int ng = P.goff[w + 1] - P.goff[w];
             glist.assign(ng, {});
             for (size_t rr = 0; rr < sp.size(); ++rr) {
@@ -2175,16 +2197,16 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
                         const int cj = cam[b];
                         if (cj <= R.c || cj < R.j0 || cj >= R.j1) continue;
                         const int g = gid_of[w][rr * nc + (cj - R.j0)];
-                        glist[g].push_back(((uint32_t)(abase + slot_of[off]) << 16) | (uint32_t)(b - o0));
+                        glist[g].push_back((uint32_t)(abase + slot_of[off]));
                     }
                 }
             }
             int32_t *hd = &P.hdr[qw * P.hdr_cap];
-            uint32_t *pp = &P.pairs[qw * P.pair_cap];
+            uint16_t *pp = &P.pairs[qw * P.pair_cap];
             int32_t np2 = 0;
             for (int g = 0; g < ng; ++g) {
                 hd[g] = np2;
-                for (uint32_t v : glist[g]) pp[np2++] = v;
+                for (uint32_t v : glist[g]) pp[np2++] = (uint16_t)v;
             }
             hd[ng] = np2;
             hd[ng + 1] = n0;
@@ -2224,13 +2246,14 @@ struct sfm_ba_problem {
     int32_t *d_wg_first = nullptr, *d_fwg_first = nullptr;
     double *d_slab = nullptr, *d_slab2 = nullptr, *d_camlin = nullptr;
     int32_t *d_sw_rchunk = nullptr, *d_sw_goff = nullptr, *d_sw_nload = nullptr, *d_sw_list = nullptr, *d_sw_hdr = nullptr;
+    int32_t *d_sw_scam = nullptr;
     SweepGroup *d_sw_groups = nullptr;
     int16_t *d_sw_lanegrp = nullptr;
     uint32_t *d_sw_pairs = nullptr;
     int2 *d_sw_blkij = nullptr;
     double2 *d_obs = nullptr;
     double *d_Rt = nullptr, *d_Rt2 = nullptr, *d_X = nullptr, *d_X2 = nullptr;
-    double *d_Vg = nullptr, *d_Lq = nullptr, *d_Z = nullptr;
+    double *d_Vg = nullptr, *d_Lq = nullptr;
     double *d_payload = nullptr, *d_A = nullptr, *d_b = nullptr, *d_D = nullptr;
     double *d_partial = nullptr, *d_scal = nullptr;
     int *d_bad = nullptr;
@@ -2462,13 +2485,13 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = p->alloc(p->d_sw_nload, sw.nload.size())) ||
         (rc = p->alloc(p->d_sw_groups, sw.groups.size())) || (rc = p->alloc(p->d_sw_lanegrp, sw.lanegrp.size())) ||
         (rc = p->alloc(p->d_sw_list, sw.list.size())) || (rc = p->alloc(p->d_sw_hdr, sw.hdr.size())) ||
-        (rc = p->alloc(p->d_sw_pairs, sw.pairs.size())) || (rc = p->alloc(p->d_sw_blkij, sw.blkij.size())) ||
+        (rc = p->alloc(p->d_sw_pairs, (int64_t)(sw.pairs.size() + 1) / 2)) || (rc = p->alloc(p->d_sw_blkij, sw.blkij.size())) ||
         (rc = p->alloc(p->d_camlin, (int64_t)CAMLIN * nc)) ||
         (rc = p->alloc(p->d_slab2, (int64_t)CAMLIN * std::max<int64_t>(1, std::max(p->ndiag_items, p->cl_fused_items)))) ||
         (rc = p->alloc(p->d_Rt, 12 * (int64_t)nc)) || (rc = p->alloc(p->d_Rt2, 12 * (int64_t)nc)) ||
         (rc = p->alloc(p->d_X, 3 * np_)) || (rc = p->alloc(p->d_X2, 3 * np_)) ||
         (rc = p->alloc(p->d_Vg, 9 * np_)) || (rc = p->alloc(p->d_Lq, 9 * np_)) ||
-        (rc = p->alloc(p->d_Z, (int64_t)ZS * no)) || (rc = p->alloc(p->d_payload, p->payload_len + 8)) ||
+        (rc = p->alloc(p->d_sw_scam, sw.spec_cam.size())) || (rc = p->alloc(p->d_payload, p->payload_len + 8)) ||
         (rc = p->alloc(p->d_A, (int64_t)p->nsp * p->nsp)) || (rc = p->alloc(p->d_b, p->nsp)) ||
         (rc = p->alloc(p->d_D, 2 * 32 * 32)) ||
         (rc = p->alloc(p->d_partial, 4 * (int64_t)p->pt_blocks)) || (rc = p->alloc(p->d_scal, 16)) ||
@@ -2531,8 +2554,9 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = up(p->d_sw_groups, sw.groups.data(), sw.groups.size() * sizeof(SweepGroup))) ||
         (rc = up(p->d_sw_lanegrp, sw.lanegrp.data(), sw.lanegrp.size() * 2)) ||
         (rc = up(p->d_sw_list, sw.list.data(), sw.list.size() * 4)) ||
+        (rc = up(p->d_sw_scam, sw.spec_cam.data(), sw.spec_cam.size() * 4)) ||
         (rc = up(p->d_sw_hdr, sw.hdr.data(), sw.hdr.size() * 4)) ||
-        (rc = up(p->d_sw_pairs, sw.pairs.data(), sw.pairs.size() * 4)) ||
+        (rc = up(p->d_sw_pairs, sw.pairs.data(), sw.pairs.size() * 2)) ||
         (rc = up(p->d_sw_blkij, sw.blkij.data(), sw.blkij.size() * sizeof(int2))))
         return rc;
     SFM_HIP(hipFuncSetAttribute((const void *)k_schur_sweep, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2769,8 +2793,8 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     const double *lam = &p->d_lm[par].lambda;
     int *bad = p->d_bad + par;
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_PREP], s));
-    hipLaunchKernelGGL(k_point_prep, dim3(std::max(1, ceil_div(p->no, OBS_THREADS))), dim3(OBS_THREADS), 0, s, (int64_t)p->no,
-                       p->d_pt, p->d_pstart, p->d_cam, p->d_Rt, p->d_X, p->K, p->d_Vg, lam, p->d_Lq, p->d_Z, gst);
+    hipLaunchKernelGGL(k_point_prep, dim3(std::max(1, ceil_div(p->np, OBS_THREADS))), dim3(OBS_THREADS), 0, s, (int64_t)p->np,
+                       p->d_Vg, lam, p->d_Lq, gst);
     SFM_HIP(hipGetLastError());
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_PREP + 1], s));
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SCHUR], s));
@@ -2778,8 +2802,9 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     const bool fused = p->cl_fused && p->ndiag_items;  // + the camera blocks (after an accepted step)
     hipLaunchKernelGGL(k_schur_sweep, dim3(nsweep + (fused ? p->cl_fused_wg : 0)), dim3(SW_THREADS),
                        p->sw_lds_bytes, s, p->sw_nspec, p->sw_nrange, p->sw_nbd, p->sw_L, p->d_sw_rchunk,
-                       p->d_sw_nload, p->d_sw_goff, p->d_sw_groups, p->d_sw_lanegrp, p->d_sw_list,
-                       p->d_sw_pairs, p->d_sw_hdr, p->d_Z, p->d_slab, gst, p->sw_debug, nsweep,
+                       p->d_sw_nload, p->d_sw_goff, p->d_sw_groups, p->d_sw_lanegrp, p->d_sw_scam,
+                       reinterpret_cast<const uint32_t *>(p->d_sw_list), p->d_sw_pairs, p->d_sw_hdr, p->d_X, p->d_Lq,
+                       p->d_Rt, p->K, p->d_slab, gst, p->sw_debug, nsweep,
                        camlin_args(p, true, &p->d_lm[par].run_lin));
     SFM_HIP(hipGetLastError());
     // one rank: the solve's first launch sums the slabs itself (SlabSrc)

@@ -782,12 +782,16 @@ def _spd(n, seed, cond=1e4):
     return 0.5 * (S + S.T), rng.standard_normal(n)
 
 
-@pytest.mark.parametrize("n", [1, 6, 16, 17, 48, 150, 300, 304, 600])
-def test_reduced_solve(core, n):
-    """The reduced-camera solver (blocked Cholesky, forward substitution
-    folded in, back substitution) against LAPACK on SPD systems with
-    condition number 1e4: relative error <= 1e-11 (fp64 Cholesky is backward
-    stable; kappa * eps ~ 2e-12); deterministic."""
+@pytest.mark.parametrize("solver", ["gj", "chol"])
+@pytest.mark.parametrize("n", [1, 6, 16, 17, 48, 150, 300, 304, 600, 1200, 1800, 2100])
+def test_reduced_solve(core, monkeypatch, n, solver):
+    """The reduced-camera solvers against LAPACK on SPD systems with condition
+    number 1e4: the persistent block Gauss-Jordan solve (default; gj_solve.hpp,
+    up to 128 tile columns -- n = 2100 falls back to the tiled Cholesky) and
+    the tiled Cholesky (SFM_SOLVE=chol: k_chol_col launches, forward
+    substitution folded in, back substitution).  Relative error <= 1e-11 (both
+    backward stable; kappa * eps ~ 2e-12); deterministic."""
+    monkeypatch.setenv("SFM_SOLVE", solver)
     S, b = _spd(n, seed=n)
     x_ref = np.linalg.solve(S, b)
     x = core.reduced_solve(S, b)
@@ -795,13 +799,52 @@ def test_reduced_solve(core, n):
     assert np.array_equal(x, core.reduced_solve(S, b))
 
 
-@pytest.mark.parametrize("n", [40, 300])
-def test_reduced_solve_not_spd(core, n):
-    """A non-positive pivot is reported (n = 300: the one-workgroup factor)."""
+@pytest.mark.parametrize("solver", ["gj", "chol"])
+@pytest.mark.parametrize("n", [40, 300, 1200])
+def test_reduced_solve_not_spd(core, monkeypatch, n, solver):
+    """A non-positive pivot is reported by either solver."""
+    monkeypatch.setenv("SFM_SOLVE", solver)
     S, b = _spd(n, seed=1)
     S[7, 7] = -1.0
     with pytest.raises(RuntimeError, match="positive definite"):
         core.reduced_solve(S, b)
+
+
+@pytest.mark.parametrize("shape", ["cfg4", "cfg5"])
+def test_ba_gj_solve_matches_cholesky(core, monkeypatch, shape):
+    """The whole LM solve with the persistent Gauss-Jordan reduced solve
+    (default) and with the tiled Cholesky (SFM_SOLVE=chol): the same
+    accept/reject sequence and cost to 1e-9 relative (the two solvers round
+    differently, so the steps agree to ~1e-12, not bitwise)."""
+    p = syn.ba_problem_cfg(shape, dense=False)
+    cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
+    args = (cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K)
+    out = {}
+    for solver in ("gj", "chol"):
+        monkeypatch.setenv("SFM_SOLVE", solver)
+        out[solver] = core.ba_lm(*args, max_iterations=30)
+    (cg, xg, rg), (cc, xc, rc) = out["gj"], out["chol"]
+    assert (rg["iterations"], rg["accepted"], rg["status"]) == (rc["iterations"], rc["accepted"], rc["status"])
+    assert abs(rg["cost"] - rc["cost"]) <= 1e-9 * rc["cost"]
+    assert np.abs(cg - cc).max() < 1e-8 and np.abs(xg - xc).max() < 1e-6
+
+
+@pytest.mark.parametrize("shape,ranks", [("cfg4", 4), ("cfg5", 8)])
+def test_ba_multi_rank_baseline_sizes(core, shape, ranks):
+    """The point-sharded LM at BASELINE's sizes (cfg4 on 4, cfg5 on 8
+    in-process ranks sharing the one GPU: partial reduced camera systems
+    all-reduced every iteration, every rank running the replicated
+    persistent solve) against the single-rank solve: the same iteration and
+    accepted counts, cost within 1e-9 relative."""
+    p = syn.ba_problem_cfg(shape, dense=False)
+    cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
+    args = (cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K)
+    c1, x1, r1 = core.ba_lm(*args, max_iterations=30)
+    cN, xN, rN = core.ba_lm_multi(*args, [0] * ranks, max_iterations=30)
+    assert rN["n_ranks"] == ranks
+    assert (rN["iterations"], rN["accepted"], rN["status"]) == (r1["iterations"], r1["accepted"], r1["status"])
+    assert abs(rN["cost"] - r1["cost"]) <= 1e-9 * r1["cost"]
+    assert np.abs(cN - c1).max() < 1e-8 and np.abs(xN - x1).max() < 1e-6
 
 
 @pytest.mark.parametrize("ranks", [2, 3])
@@ -924,7 +967,7 @@ def test_ba_camera_blocks_fused_equal_standalone(core, monkeypatch):
 
 @pytest.mark.parametrize("shape", ["cfg3", "50x6000"])
 def test_ba_solve_variants_bitwise_equal(core, monkeypatch, shape):
-    """The reduced solve's DPP tile factor (default) and the readlane chain
+    """The tiled Cholesky reduced solve (SFM_SOLVE=chol): its DPP tile factor (default) and the readlane chain
     (SFM_CHOL_DPP=0), and the Schur finish folded into the solve's first
     launch at one rank (default) or run as its own launch
     (SFM_FINISH_FUSED=0): the same operations in the same order, so the
@@ -937,6 +980,7 @@ def test_ba_solve_variants_bitwise_equal(core, monkeypatch, shape):
     cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
     args = (cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K)
     out = {}
+    monkeypatch.setenv("SFM_SOLVE", "chol")  # the variants are the tiled Cholesky's
     for dpp in ("1", "0"):
         for fin in ("1", "0"):
             monkeypatch.setenv("SFM_CHOL_DPP", dpp)
