@@ -553,6 +553,10 @@ def main():
     cpu_leg = world == 1 and not args.no_cpu_baseline
     if cpu_leg:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
+        # the OpenMP legs: threads pinned to cores, packed (read at the
+        # runtime's first parallel region, i.e. after this)
+        os.environ.setdefault("OMP_PROC_BIND", "close")
+        os.environ.setdefault("OMP_PLACES", "cores")
     if not args.no_next_rows:
         out["next_rows"] = next_rows(core, local_rank, cpu_leg)
     if cpu_leg:
@@ -600,6 +604,7 @@ def main():
             "threads_note": "thread counts beyond the CPUs this process may use are not run; the sweep's "
                             "fastest point is the baseline",
             "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"),
+            "OMP_PROC_BIND": os.environ.get("OMP_PROC_BIND"), "OMP_PLACES": os.environ.get("OMP_PLACES"),
             "OPENBLAS_NUM_THREADS": os.environ.get("OPENBLAS_NUM_THREADS")})
     print(json.dumps(out))
     if world > 1:
