@@ -4,11 +4,14 @@
  * for throughput on the host's cores with OpenMP:
  *   - linearisation, elimination, back substitution and the trial cost are
  *     parallel over points (observations of a point stay on one thread);
- *   - the reduced camera system is accumulated in per-thread copies of its
- *     upper camera blocks (no atomics) and summed in thread order;
- *   - W = Jc^T Jp and Y = W V^-1 are formed once per observation, and each
- *     unordered camera pair of a point is done once;
- *   - the dense Cholesky's row updates run in parallel.
+ *   - W = Jc^T Jp and Y = W V^-1 are formed once per observation (parallel
+ *     over points); the reduced camera system is then accumulated by camera
+ *     ROW: a thread owns a block row (camera c1, dynamic schedule) and walks
+ *     c1's observations (camera-major list), adding every pair (c1 <= c2)
+ *     of their points into its own row -- no per-thread copies of S, no
+ *     reduction, no atomics, a fixed order per row;
+ *   - the dense Cholesky is blocked (64-wide panels, parallel panel solve
+ *     and trailing update).
  * Only bench.py's cpu_baseline leg and tests/ use it.  Not the reference:
  * the reference path (MINPACK lmdif with a dense forward-difference
  * Jacobian) cannot run at cfg4/cfg5.
@@ -73,22 +76,49 @@ static void inv3_sym(const double *M, double *I) {
     I[6] = C * id; I[7] = (b * c - a * e) * id; I[8] = (a * d - b * b) * id;
 }
 
-/* dense lower Cholesky of the full symmetric S (n x n, row-major) + solve */
+/* dense lower Cholesky of the full symmetric S (n x n, row-major; the lower
+ * triangle is read and overwritten by L) + the two triangular solves; blocked
+ * right-looking with NB-wide panels: the diagonal block serially, the panel
+ * rows and the trailing update in parallel over rows */
+#define CS_NB 64
 static int chol_solve_par(double *S, int n, double *b) {
     int bad = 0;
-    for (int j = 0; j < n && !bad; ++j) {
-        double d = S[(size_t)j * n + j];
-        for (int k = 0; k < j; ++k) d -= S[(size_t)j * n + k] * S[(size_t)j * n + k];
-        if (!(d > 0)) { bad = 1; break; }
-        d = sqrt(d);
-        S[(size_t)j * n + j] = d;
-        const double *Sj = S + (size_t)j * n;
-#pragma omp parallel for schedule(static) if ((n - j) * j > 20000)
-        for (int i = j + 1; i < n; ++i) {
+    for (int k0 = 0; k0 < n && !bad; k0 += CS_NB) {
+        const int k1 = k0 + CS_NB < n ? k0 + CS_NB : n;
+        for (int j = k0; j < k1; ++j) { /* diagonal block, unblocked (its columns k0..j-1 updated) */
+            double *Sj = S + (size_t)j * n;
+            double d = Sj[j];
+            for (int k = k0; k < j; ++k) d -= Sj[k] * Sj[k];
+            if (!(d > 0)) { bad = 1; break; }
+            d = sqrt(d);
+            Sj[j] = d;
+            for (int i = j + 1; i < k1; ++i) {
+                double *Si = S + (size_t)i * n;
+                double v = Si[j];
+                for (int k = k0; k < j; ++k) v -= Si[k] * Sj[k];
+                Si[j] = v / d;
+            }
+        }
+        if (bad) break;
+#pragma omp parallel for schedule(static)
+        for (int i = k1; i < n; ++i) { /* panel rows: L_ik = S_ik L_kk^-T */
             double *Si = S + (size_t)i * n;
-            double v = Si[j];
-            for (int k = 0; k < j; ++k) v -= Si[k] * Sj[k];
-            Si[j] = v / d;
+            for (int j = k0; j < k1; ++j) {
+                const double *Sj = S + (size_t)j * n;
+                double v = Si[j];
+                for (int k = k0; k < j; ++k) v -= Si[k] * Sj[k];
+                Si[j] = v / Sj[j];
+            }
+        }
+#pragma omp parallel for schedule(dynamic, 8)
+        for (int i = k1; i < n; ++i) { /* trailing update of row i: S_ij -= L_i. L_j. (j <= i) */
+            double *Si = S + (size_t)i * n;
+            for (int j = k1; j <= i; ++j) {
+                const double *Sj = S + (size_t)j * n;
+                double v = 0;
+                for (int k = k0; k < k1; ++k) v += Si[k] * Sj[k];
+                Si[j] -= v;
+            }
         }
     }
     if (bad) return -1;
@@ -123,8 +153,18 @@ int cs_ba_lm(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const int3
     double *Xn = malloc(sizeof(double) * 3 * (np_ ? np_ : 1));
     double *U = malloc(sizeof(double) * 36 * nc), *gc = malloc(sizeof(double) * ns);
     double *S = malloc(sizeof(double) * (size_t)ns * ns), *b = malloc(sizeof(double) * ns);
-    double *St = malloc(sizeof(double) * (size_t)nth * ns * ns), *bt = malloc(sizeof(double) * (size_t)nth * ns);
+    double *Vg = malloc(sizeof(double) * 3 * (np_ ? np_ : 1));
     double *Ut = malloc(sizeof(double) * (size_t)nth * (36 * nc + ns));
+    /* camera-major observation list (point order within a camera) */
+    int64_t *cstart = calloc(nc + 1, sizeof(int64_t)), *cm = malloc(sizeof(int64_t) * (no ? no : 1));
+    for (int64_t o = 0; o < no; ++o) cstart[cam[o] + 1]++;
+    for (int c = 0; c < nc; ++c) cstart[c + 1] += cstart[c];
+    {
+        int64_t *fill = malloc(sizeof(int64_t) * (nc ? nc : 1));
+        for (int c = 0; c < nc; ++c) fill[c] = cstart[c];
+        for (int64_t o = 0; o < no; ++o) cm[fill[cam[o]]++] = o;
+        free(fill);
+    }
     for (int c = 0; c < nc; ++c) {
         orc_rotvec_to_R(cams + 6 * c, R + 9 * c);
         memcpy(t + 3 * c, cams + 6 * c + 3, 3 * sizeof(double));
@@ -181,66 +221,54 @@ int cs_ba_lm(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const int3
             if (gmax < opt->gradient_tolerance) { status = 2; break; }
             need_lin = 0;
         }
-        /* elimination: per-thread upper camera blocks of S, b */
-#pragma omp parallel
-        {
-            const int th = omp_get_thread_num();
-            double *Sl = St + (size_t)th * ns * ns, *bl = bt + (size_t)th * ns;
-            memset(bl, 0, sizeof(double) * ns);
-            for (int ci = 0; ci < nc; ++ci)  /* only the upper blocks are touched */
-                for (int i = 0; i < 6; ++i) memset(Sl + (size_t)(6 * ci + i) * ns + 6 * ci, 0, sizeof(double) * (ns - 6 * ci));
-#pragma omp for schedule(dynamic, 256)
-            for (int64_t p = 0; p < np_; ++p) {
-                double Vd[9];
-                memcpy(Vd, V + 9 * p, sizeof Vd);
-                for (int i = 0; i < 3; ++i) Vd[4 * i] += lambda * clampd(V[9 * p + 4 * i]);
-                double *Vinv = Vi + 9 * p;
-                inv3_sym(Vd, Vinv);
-                const double *g = gp + 3 * p;
-                double Vg[3];
-                for (int i = 0; i < 3; ++i) Vg[i] = Vinv[3 * i] * g[0] + Vinv[3 * i + 1] * g[1] + Vinv[3 * i + 2] * g[2];
-                for (int64_t oa = pstart[p]; oa < pstart[p + 1]; ++oa) {
-                    const double *Wa = W + 18 * oa;
-                    double *Ya = Y + 18 * oa;
-                    for (int i = 0; i < 6; ++i)
-                        for (int j = 0; j < 3; ++j)
-                            Ya[3 * i + j] = Wa[3 * i] * Vinv[j] + Wa[3 * i + 1] * Vinv[3 + j] + Wa[3 * i + 2] * Vinv[6 + j];
-                    const int ca = cam[oa];
-                    for (int i = 0; i < 6; ++i)
-                        bl[6 * ca + i] += Wa[3 * i] * Vg[0] + Wa[3 * i + 1] * Vg[1] + Wa[3 * i + 2] * Vg[2];
-                }
-                for (int64_t oa = pstart[p]; oa < pstart[p + 1]; ++oa) {
-                    const double *Ya = Y + 18 * oa;
-                    for (int64_t ob = pstart[p]; ob < pstart[p + 1]; ++ob) {
-                        int c1 = cam[oa], c2 = cam[ob];
-                        if (c1 > c2) continue;  /* each unordered pair once, into the upper block */
-                        const double *Wb = W + 18 * ob;
-                        double *blk = Sl + (size_t)(6 * c1) * ns + 6 * c2;
-                        for (int i = 0; i < 6; ++i)
-                            for (int j = 0; j < 6; ++j)
-                                blk[(size_t)i * ns + j] -= Ya[3 * i] * Wb[3 * j] + Ya[3 * i + 1] * Wb[3 * j + 1] + Ya[3 * i + 2] * Wb[3 * j + 2];
-                    }
-                }
+        /* elimination, pass 1 (parallel over points): V^-1, V^-1 g, Y = W V^-1 */
+#pragma omp parallel for schedule(dynamic, 256)
+        for (int64_t p = 0; p < np_; ++p) {
+            double Vd[9];
+            memcpy(Vd, V + 9 * p, sizeof Vd);
+            for (int i = 0; i < 3; ++i) Vd[4 * i] += lambda * clampd(V[9 * p + 4 * i]);
+            double *Vinv = Vi + 9 * p;
+            inv3_sym(Vd, Vinv);
+            const double *g = gp + 3 * p;
+            for (int i = 0; i < 3; ++i) Vg[3 * p + i] = Vinv[3 * i] * g[0] + Vinv[3 * i + 1] * g[1] + Vinv[3 * i + 2] * g[2];
+            for (int64_t oa = pstart[p]; oa < pstart[p + 1]; ++oa) {
+                const double *Wa = W + 18 * oa;
+                double *Ya = Y + 18 * oa;
+                for (int i = 0; i < 6; ++i)
+                    for (int j = 0; j < 3; ++j)
+                        Ya[3 * i + j] = Wa[3 * i] * Vinv[j] + Wa[3 * i + 1] * Vinv[3 + j] + Wa[3 * i + 2] * Vinv[6 + j];
             }
         }
-        /* sum the thread copies (thread order), add U + damping, mirror */
-#pragma omp parallel for schedule(static)
-        for (int r = 0; r < ns; ++r) {
-            const int c0 = 6 * (r / 6);
-            for (int j = c0; j < ns; ++j) {
-                double v = 0;
-                for (int th = 0; th < nth; ++th) v += St[(size_t)th * ns * ns + (size_t)r * ns + j];
-                S[(size_t)r * ns + j] = v;
-            }
-        }
-        for (int c = 0; c < nc; ++c)
+        /* pass 2 (parallel over camera block rows): row c1 of the upper
+         * camera blocks and b_c1, from c1's observations and their points */
+#pragma omp parallel for schedule(dynamic, 1)
+        for (int c1 = 0; c1 < nc; ++c1) {
             for (int i = 0; i < 6; ++i) {
-                double v = -gc[6 * c + i];
-                for (int th = 0; th < nth; ++th) v += bt[(size_t)th * ns + 6 * c + i];
-                b[6 * c + i] = v;
-                for (int j = 0; j < 6; ++j) S[(size_t)(6 * c + i) * ns + 6 * c + j] += U[36 * c + 6 * i + j];
-                S[(size_t)(6 * c + i) * ns + 6 * c + i] += lambda * clampd(U[36 * c + 7 * i]);
+                memset(S + (size_t)(6 * c1 + i) * ns + 6 * c1, 0, sizeof(double) * (ns - 6 * c1));
+                b[6 * c1 + i] = -gc[6 * c1 + i];
             }
+            for (int64_t k = cstart[c1]; k < cstart[c1 + 1]; ++k) {
+                const int64_t oa = cm[k], p = pt[oa];
+                const double *Wa = W + 18 * oa, *Ya = Y + 18 * oa, *vg = Vg + 3 * p;
+                for (int i = 0; i < 6; ++i) b[6 * c1 + i] += Wa[3 * i] * vg[0] + Wa[3 * i + 1] * vg[1] + Wa[3 * i + 2] * vg[2];
+                for (int64_t ob = pstart[p]; ob < pstart[p + 1]; ++ob) {
+                    const int c2 = cam[ob];
+                    if (c2 < c1) continue;  /* the upper block (c1 <= c2) */
+                    const double *Wb = W + 18 * ob;
+                    double *blk = S + (size_t)(6 * c1) * ns + 6 * c2;
+                    for (int i = 0; i < 6; ++i)
+                        for (int j = 0; j < 6; ++j)
+                            blk[(size_t)i * ns + j] -= Ya[3 * i] * Wb[3 * j] + Ya[3 * i + 1] * Wb[3 * j + 1] + Ya[3 * i + 2] * Wb[3 * j + 2];
+                }
+            }
+            /* + U and the damping on the diagonal block */
+            for (int i = 0; i < 6; ++i) {
+                for (int j = 0; j < 6; ++j) S[(size_t)(6 * c1 + i) * ns + 6 * c1 + j] += U[36 * c1 + 6 * i + j];
+                S[(size_t)(6 * c1 + i) * ns + 6 * c1 + i] += lambda * clampd(U[36 * c1 + 7 * i]);
+            }
+        }
+        /* mirror the upper blocks into the lower triangle (read by the factor) */
+#pragma omp parallel for schedule(static)
         for (int r = 0; r < ns; ++r)
             for (int j = 0; j < r; ++j) S[(size_t)r * ns + j] = S[(size_t)j * ns + r];
         double *dc = b;
@@ -323,7 +351,7 @@ int cs_ba_lm(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const int3
         rep->cost0 = cost0; rep->cost = cost;
     }
     free(pstart); free(R); free(t); free(Rn); free(tn); free(J); free(W); free(Y); free(V); free(gp); free(Vi);
-    free(dp); free(Xn); free(U); free(gc); free(S); free(b); free(St); free(bt); free(Ut);
+    free(dp); free(Xn); free(U); free(gc); free(S); free(b); free(Vg); free(Ut); free(cstart); free(cm);
     return 0;
 }
 
