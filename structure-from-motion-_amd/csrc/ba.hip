@@ -655,14 +655,10 @@ __device__ __forceinline__ void cross_rows(const double (&p)[3], const double (&
     }
 }
 
-// rows 3h..3h+2 of S_ab = E_a H E_b^T, H = G_a G_b^T = F_a M_b^T, into acc[0..18)
-__device__ __forceinline__ void pair_block(int h, const double (&pa)[3], const double (&Fa)[3][3],
-                                           const double (&pb)[3], const double (&Mb)[3][3], double (&acc)[21]) {
-    double H[3][3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) H[i][j] = Fa[i][0] * Mb[j][0] + Fa[i][1] * Mb[j][1] + Fa[i][2] * Mb[j][2];
+// rows 3h..3h+2 of S_ab = E_a H E_b^T, H = G_a G_b^T = F_a M_b^T, into acc[o..o+18)
+template <int NA>
+__device__ __forceinline__ void pair_rows(int h, int o, const double (&pa)[3], const double (&H)[3][3],
+                                          const double (&pb)[3], double (&acc)[NA]) {
     double X[3][3];
     if (h == 0) {
         cross_rows(pa, H, X);
@@ -674,12 +670,44 @@ __device__ __forceinline__ void pair_block(int h, const double (&pa)[3], const d
     }
 #pragma unroll
     for (int r = 0; r < 3; ++r) {  // row r of X E_b^T = [X [p_b]x^T | X]
-        acc[6 * r + 0] += -pb[2] * X[r][1] + pb[1] * X[r][2];
-        acc[6 * r + 1] += pb[2] * X[r][0] - pb[0] * X[r][2];
-        acc[6 * r + 2] += -pb[1] * X[r][0] + pb[0] * X[r][1];
-        acc[6 * r + 3] += X[r][0];
-        acc[6 * r + 4] += X[r][1];
-        acc[6 * r + 5] += X[r][2];
+        acc[o + 6 * r + 0] += -pb[2] * X[r][1] + pb[1] * X[r][2];
+        acc[o + 6 * r + 1] += pb[2] * X[r][0] - pb[0] * X[r][2];
+        acc[o + 6 * r + 2] += -pb[1] * X[r][0] + pb[0] * X[r][1];
+        acc[o + 6 * r + 3] += X[r][0];
+        acc[o + 6 * r + 4] += X[r][1];
+        acc[o + 6 * r + 5] += X[r][2];
+    }
+}
+// a lane's share of one pair: LPP = 2, rows 3h..3h+2 (acc[0..18)); LPP = 1,
+// the whole 6x6 block (acc[0..36)), H formed once
+template <int LPP, int NA>
+__device__ __forceinline__ void pair_block(int h, const double (&pa)[3], const double (&Fa)[3][3],
+                                           const double (&pb)[3], const double (&Mb)[3][3], double (&acc)[NA]) {
+    double H[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) H[i][j] = Fa[i][0] * Mb[j][0] + Fa[i][1] * Mb[j][1] + Fa[i][2] * Mb[j][2];
+    if constexpr (LPP == 2) {
+        pair_rows(h, 0, pa, H, pb, acc);
+    } else {
+        pair_rows(0, 0, pa, H, pb, acc);
+        pair_rows(1, 18, pa, H, pb, acc);
+    }
+}
+// the diagonal block's E_a (G_a q) term: LPP = 2 rows 3h..3h+2 at acc[18..21);
+// LPP = 1 all six at acc[36..42)
+template <int LPP, int NA>
+__device__ __forceinline__ void diag_gq(int h, const double (&pa)[3], const double (&gq)[3], double (&acc)[NA]) {
+    constexpr int o = LPP == 2 ? 18 : 36;
+    if (LPP == 1 || h == 0) {
+        acc[o + 0] += -pa[2] * gq[1] + pa[1] * gq[2];
+        acc[o + 1] += pa[2] * gq[0] - pa[0] * gq[2];
+        acc[o + 2] += -pa[1] * gq[0] + pa[0] * gq[1];
+    }
+    if (LPP == 1 || h == 1) {
+        constexpr int o2 = LPP == 2 ? 18 : 39;
+        acc[o2 + 0] += gq[0]; acc[o2 + 1] += gq[1]; acc[o2 + 2] += gq[2];
     }
 }
 
@@ -709,6 +737,7 @@ __device__ __forceinline__ void sweep_fetch(int t, int nload, int64_t qw, const 
     for (int base = (t & ~63); base < L.hdr_cap; base += step) glds4(hdr + qw * L.hdr_cap + base + lane, hw + base);
 }
 
+template <int LPP>  // lanes per pair slot
 __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     int32_t nspec, int32_t nrange, int32_t nbd, SweepLds L, const int32_t *__restrict__ rchunk,
     const int32_t *__restrict__ spec_nload, const int32_t *__restrict__ spec_goff,
@@ -737,7 +766,8 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     const int ng = spec_goff[w + 1] - spec_goff[w];
     SweepGroup grp = {0, 0, 2, 0, 0};
     if (gi >= 0) grp = groups[spec_goff[w] + gi];
-    const int h = (t - grp.lane_base) & 1, slot = (t - grp.lane_base) >> 1, nslot = grp.G >> 1;
+    const int h = LPP == 2 ? (t - grp.lane_base) & 1 : 0, slot = (t - grp.lane_base) / LPP, nslot = grp.G / LPP;
+    constexpr int NACC = LPP == 2 ? 21 : 42;
     const bool diag = grp.flags & 1, second = grp.flags & 2;
     const int bw = L.words();
     double *scam = reinterpret_cast<double *>(ldsw + 2 * bw);  // the spec's cameras (rows 0 and 1)
@@ -813,7 +843,7 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
             if (q + 1 < q1) stage_chunk(q + 1, ldsw + (((q - q0) & 1) ^ 1) * bw);
             __syncthreads();
         }
-        for (int k0 = 0; k0 < 21; k0 += 7) {  // the reduction's barriers
+        for (int k0 = 0; k0 < NACC; k0 += 7) {  // the reduction's barriers
             __syncthreads();
             __syncthreads();
         }
@@ -822,9 +852,9 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     double Rb[12];  // the group's column camera (the b side; the a camera itself for a diagonal block)
 #pragma unroll
     for (int k = 0; k < 12; ++k) Rb[k] = gi >= 0 ? Rt[12 * grp.cam_b + k] : 0.0;
-    double acc[21];
+    double acc[NACC];
 #pragma unroll
-    for (int k = 0; k < 21; ++k) acc[k] = 0.0;
+    for (int k = 0; k < NACC; ++k) acc[k] = 0.0;
     if (q0 < q1 && loader) sweep_fetch(t, nload, (int64_t)q0 * nspec + w, L, pairs, hdr, ldsw);
     __syncthreads();  // the cameras are in LDS
     __syncthreads();  // chunk q0's slots are staged
@@ -845,16 +875,10 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
                     load_slot_a(sl, pa, Fa);
                     load_slot_x(sl, x);
                     obs_pM(Rb, x, K, pm, Ma);
-                    pair_block(h, pa, Fa, pa, Ma, acc);
+                    pair_block<LPP>(h, pa, Fa, pa, Ma, acc);
                     const double2 v6 = sl[6], v7 = sl[7];
                     const double gq[3] = {v6.x, v6.y, v7.x};  // G_a q
-                    if (h == 0) {
-                        acc[18] += -pa[2] * gq[1] + pa[1] * gq[2];
-                        acc[19] += pa[2] * gq[0] - pa[0] * gq[2];
-                        acc[20] += -pa[1] * gq[0] + pa[0] * gq[1];
-                    } else {
-                        acc[18] += gq[0]; acc[19] += gq[1]; acc[20] += gq[2];
-                    }
+                    diag_gq<LPP>(h, pa, gq, acc);
                 }
             } else {
                 const int k0 = hd[gi], k1 = (dbg & 1) ? k0 : hd[gi + 1];
@@ -865,7 +889,7 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
                     load_slot_a(sl, pa, Fa);
                     load_slot_x(sl, x);
                     obs_pM(Rb, x, K, pb, Mb);  // the b side: camera j, the same point
-                    pair_block(h, pa, Fa, pb, Mb, acc);
+                    pair_block<LPP>(h, pa, Fa, pb, Mb, acc);
                 }
             }
         }
@@ -877,7 +901,7 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     double *red = reinterpret_cast<double *>(sw_lds);
     double *out = slab + ((int64_t)r * nbd + grp.blk) * ITEM_W;
 #pragma unroll
-    for (int k0 = 0; k0 < 21; k0 += 7) {
+    for (int k0 = 0; k0 < NACC; k0 += 7) {
 #pragma unroll
         for (int k = 0; k < 7; ++k) red[k * SW_THREADS + t] = acc[k0 + k];
         __syncthreads();
@@ -885,10 +909,15 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
 #pragma unroll
             for (int k = 0; k < 7; ++k) {
                 double v = 0.0;
-                for (int sl = 0; sl < nslot; ++sl) v += red[k * SW_THREADS + grp.lane_base + 2 * sl + h];
+                for (int sl = 0; sl < nslot; ++sl) v += red[k * SW_THREADS + grp.lane_base + LPP * sl + h];
                 const int kk = k0 + k;
-                if (kk < 18) out[18 * h + kk] = v;
-                else if (diag) out[36 + 3 * h + (kk - 18)] = v;
+                if constexpr (LPP == 2) {
+                    if (kk < 18) out[18 * h + kk] = v;
+                    else if (diag) out[36 + 3 * h + (kk - 18)] = v;
+                } else {
+                    if (kk < 36) out[kk] = v;  // acc[6r + c]: row r of the 6x6 block, row-major
+                    else if (diag) out[kk] = v;
+                }
             }
         }
         __syncthreads();
@@ -2004,7 +2033,7 @@ static void plan_camera_items(int nc, const std::vector<int32_t> &cstart, const 
 static int32_t dense_blk(int nc, int i, int j) { return i * nc - i * (i - 1) / 2 + (j - i); }
 
 static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt,
-                       const std::vector<int32_t> &pstart, const std::vector<int64_t> &cnt, SweepPlan &P) {
+                       const std::vector<int32_t> &pstart, const std::vector<int64_t> &cnt, int lpp, SweepPlan &P) {
     P.nbd = nc * (nc + 1) / 2;
     P.blkij.resize(P.nbd);
     for (int i = 0; i < nc; ++i)
@@ -2058,7 +2087,7 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
         int Gd = 64, nload = 1, budget = 0;
         for (; Gd >= 2; Gd /= 2) {
             nload = std::max(1, (nd * Gd + 63) / 64);
-            budget = (SW_THREADS - 64 * nload - 64 * SW_STAGE_WAVES) / 2;
+            budget = (SW_THREADS - 64 * nload - 64 * SW_STAGE_WAVES) / lpp;  // pair slots
             if (noff <= budget) break;
         }
         // slots in proportion to the block's pair work, the whole budget
@@ -2091,7 +2120,7 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
             sum += 1;
         }
         std::stable_sort(g.begin(), g.end(), [](const G0 &a, const G0 &b) { return a.slots > b.slots; });
-        for (auto &x : gd) x.slots = Gd / 2;
+        for (auto &x : gd) x.slots = Gd / lpp;
         g.insert(g.begin(), gd.begin(), gd.end());
         P.goff.push_back((int32_t)P.groups.size());
         P.nload.push_back(nload);
@@ -2099,7 +2128,7 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
         int lane = 0;
         for (size_t k = 0; k < g.size(); ++k) {
             if (k == gd.size()) lane = 64 * nload;  // off-diagonal groups after the loader waves
-            const int G = 2 * g[k].slots;
+            const int G = lpp * g[k].slots;
             P.groups.push_back({g[k].blk, lane, G, g[k].flags, g[k].cam_b});
             for (int l = lane; l < lane + G; ++l) P.lanegrp[(size_t)w * SW_THREADS + l] = (int16_t)k;
             gid_of[w][g[k].key] = (int)k;
@@ -2235,6 +2264,7 @@ struct sfm_ba_problem {
     // Schur sweep plan (k_schur_sweep): ranges, chunks, specs
     int32_t sw_nrange = 0, sw_nspec = 0, sw_nbd = 0, sw_nchunk = 0;
     SweepLds sw_L = {};
+    int sw_lpp = 1;
     size_t sw_lds_bytes = 0;
     Kmat K;
     std::vector<double> cams0, pts0;
@@ -2440,7 +2470,10 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
             }
     p->npairs = tot;
     SweepPlan sw;
-    plan_sweep(nc, np_, no, cam, pt, pstart, cnt, sw);
+    // lanes per pair slot: 1 (default; a lane forms a pair's whole 6x6 block,
+    // H once) or 2 (SFM_SWEEP_LPP=2: half the rows each)
+    p->sw_lpp = env_int("SFM_SWEEP_LPP", 1) == 2 ? 2 : 1;
+    plan_sweep(nc, np_, no, cam, pt, pstart, cnt, p->sw_lpp, sw);
     // camera items (the camera blocks of the normal equations): for
     // k_camera_lin, chunks of <= CAM_CHUNK of each camera's observations, one
     // per workgroup; for the camera workgroups of k_schur_sweep, the
@@ -2559,7 +2592,9 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = up(p->d_sw_pairs, sw.pairs.data(), sw.pairs.size() * 2)) ||
         (rc = up(p->d_sw_blkij, sw.blkij.data(), sw.blkij.size() * sizeof(int2))))
         return rc;
-    SFM_HIP(hipFuncSetAttribute((const void *)k_schur_sweep, hipFuncAttributeMaxDynamicSharedMemorySize,
+    SFM_HIP(hipFuncSetAttribute((const void *)k_schur_sweep<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)p->sw_lds_bytes));
+    SFM_HIP(hipFuncSetAttribute((const void *)k_schur_sweep<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)p->sw_lds_bytes));
     if ((rc = upload_state(p.get()))) return rc;
     *out = p.release();
@@ -2800,7 +2835,7 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SCHUR], s));
     const int nsweep = NXCD * p->sw_nspec * ceil_div(p->sw_nrange, NXCD);
     const bool fused = p->cl_fused && p->ndiag_items;  // + the camera blocks (after an accepted step)
-    hipLaunchKernelGGL(k_schur_sweep, dim3(nsweep + (fused ? p->cl_fused_wg : 0)), dim3(SW_THREADS),
+    hipLaunchKernelGGL(p->sw_lpp == 1 ? k_schur_sweep<1> : k_schur_sweep<2>, dim3(nsweep + (fused ? p->cl_fused_wg : 0)), dim3(SW_THREADS),
                        p->sw_lds_bytes, s, p->sw_nspec, p->sw_nrange, p->sw_nbd, p->sw_L, p->d_sw_rchunk,
                        p->d_sw_nload, p->d_sw_goff, p->d_sw_groups, p->d_sw_lanegrp, p->d_sw_scam,
                        reinterpret_cast<const uint32_t *>(p->d_sw_list), p->d_sw_pairs, p->d_sw_hdr, p->d_X, p->d_Lq,
