@@ -118,7 +118,10 @@ int sfm_ransac_h4_pyrandom(const double *x1, const double *x2, int64_t N, uint32
  *   (:82-87, LinearPnP on all points when best_count < 4).
  * sfm_nonlinear_pnp: NonlinearPnP (:47-123), scipy 'lm' semantics with
  *   max_nfev on the 2N-residual loss (:5-44); info: MINPACK info, 0 for the
- *   N < 4 early return, -1 where the reference's except keeps (C0, R0).
+ *   N < 4 early return, -1 where the reference's except keeps (C0, R0); a
+ *   non-negative info carries the CholeskyQR flags in bits 8-9 (1: the
+ *   Jacobian's Gram factor needed a shift and a third pass ran; 2: a later
+ *   Gram factor failed) -- info & 0xff is MINPACK's code.
  * ------------------------------------------------------------------- */
 int sfm_linear_pnp(const double *X, const double *x, int64_t N, const double *K, double *C_out,
                    double *R_out, int32_t *branch, int device);

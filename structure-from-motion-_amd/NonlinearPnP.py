@@ -2,11 +2,18 @@
 (Phase 1/NonlinearPnP.py:5-151).
 
 The pose refinement (scipy least_squares(method='lm', max_nfev=100) on the
-2N reprojection residuals) runs as one MINPACK lmdif per workgroup on the
-MI355X: residuals, forward-difference Jacobian columns and the m-long QR
-reductions are spread over the workgroup, the 6 x 6 trust-region solve
-(lmpar) runs on one lane.  Rotation conversions follow scipy's quaternion
-formulas.
+2N reprojection residuals) runs as MINPACK lmdif in one 512-thread
+workgroup on the MI355X (pnp.hip k_nonlinear_pnp): the 2N residual rows
+stay in registers; every forward-difference Jacobian (the base and the six
+perturbed projections in one pass) is reduced to its 6 x 6 R factor and
+Q^T f by CholeskyQR2 (fixed-order block sums of J^T J, then of q^T q and
+q^T f with q = J R1^-1; a shifted third pass when J is numerically
+rank-deficient, reported in info's flags); MINPACK's qrfac with column
+pivoting, lmpar, the trust region and the stopping tests then run on the
+6 x 6 factor on one lane.  Rotation conversions follow scipy's quaternion
+formulas.  The result is the reference's minimum (cost within 1e-9, pose
+within 1e-5), not bit-exact: device sin/cos and the parallel sums round
+differently.
 """
 import numpy as np
 from scipy.spatial.transform import Rotation

@@ -397,15 +397,19 @@ def pnp_ransac(X, x, K, samples, thr, want_counts=False):
     return int(best[0]), int(bc[0]), C, R.reshape(3, 3), counts, branches
 
 
-def nonlinear_pnp(X, x, K, C0, R0, max_nfev=100):
-    """Returns (C (3,), R (3,3), info)."""
+def nonlinear_pnp(X, x, K, C0, R0, max_nfev=100, want_flags=False):
+    """Returns (C (3,), R (3,3), info) -- info MINPACK's code (-1: the
+    reference's except path) -- and with want_flags the CholeskyQR flags
+    (1: shifted pass-1 factor, a third pass ran; 2: a Gram factor failed)."""
     require_device()
     X, x, K = _f64(np.reshape(X, (-1, 3))), _f64(np.reshape(x, (-1, 2))), _f64(K)
     C0, R0 = _f64(np.reshape(C0, 3)), _f64(np.reshape(R0, (3, 3)))
     C, R, info = np.zeros(3), np.zeros(9), np.zeros(1, dtype=np.int32)
     _check(_lib.sfm_nonlinear_pnp(_p(X), _p(x), len(X), _p(K), _p(C0), _p(R0), int(max_nfev), _p(C), _p(R),
                                   _p(info, _i32), DEVICE))
-    return C, R.reshape(3, 3), int(info[0])
+    v = int(info[0])
+    code, flags = (v & 0xff, v >> 8) if v >= 0 else (v, 0)
+    return (C, R.reshape(3, 3), code, flags) if want_flags else (C, R.reshape(3, 3), code)
 
 
 def parse_matching(data_path, no_of_images, n_threads=0):

@@ -43,6 +43,7 @@
 #include <mutex>
 #include <thread>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -582,7 +583,7 @@ __global__ void __launch_bounds__(THREADS) k_camera_lin(CamLinArgs a) {
 //     its block to slab[range][block]; k_schur_finish sums the ranges in
 //     order.  Deterministic, no atomics.
 constexpr int SW_THREADS = 768;
-constexpr int SW_MAX_STAGED = 512;  // slots per (chunk, spec)
+constexpr int SW_MAX_STAGED = 1024;  // slots per (chunk, spec) (the LDS is the tighter bound)
 constexpr int SW_MAX_COLS = SW_THREADS / 2 - 96;  // blocks per spec (2 lanes each; a loader wave, two staging waves)
 constexpr int NXCD = 8;
 constexpr int SLOT_D = 18;  // staged slot (doubles): p (3) | F = G L^T (9, row-major) | G q (3) | X (3)
@@ -2145,7 +2146,10 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     // partial pass (cfg5, 100 specs: 0.969 -> 0.885 ms; cfg4 at 16: 0.145 -> 0.161 ms)
     const int nr_dflt = P.nspec * NXCD <= 256 ? 8 : 16;
     P.nrange = std::max(NXCD, env_int("SFM_SWEEP_RANGES", nr_dflt) / NXCD * NXCD);
-    int chunk_obs = std::max(64, std::min(env_int("SFM_SWEEP_CHUNK", 11264), 65535));
+    // chunks as large as the LDS allows (every chunk boundary is a barrier
+    // and an imbalance point): from the 16-bit cap down, scaled by the
+    // overshoot until the largest (chunk, spec) fits
+    int chunk_obs = std::max(64, std::min(env_int("SFM_SWEEP_CHUNK", 65535), 65535));
     std::vector<int32_t> ccount(nc), cpairs(P.nspec);
     std::vector<int64_t> cut;  // chunk first points
     for (;;) {
@@ -2185,9 +2189,13 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
         P.pair_cap = std::max(128, (max_pairs + 127) / 128 * 128);  // 16-bit entries, whole 64-lane DMA rows
         P.list_cap = (P.buf_slots + 63) / 64 * 64;
         if ((ok && max_staged <= SW_MAX_STAGED && P.lds_bytes() <= 160 * 1024) || chunk_obs <= 64) break;
-        chunk_obs /= 2;
+        const double over = std::max((double)max_staged / SW_MAX_STAGED, (double)P.lds_bytes() / (160 * 1024));
+        chunk_obs = std::max(64, (int)(chunk_obs * std::min(0.95, std::max(0.5, 0.98 / over))));
     }
     P.nchunk = (int32_t)cut.size();
+    if (env_int("SFM_SWEEP_VERBOSE", 0))
+        std::fprintf(stderr, "sweep plan: nspec %d nrange %d nchunk %d chunk_obs %d buf_slots %d pair_cap %d lds %zu B\n",
+                     P.nspec, P.nrange, P.nchunk, chunk_obs, P.buf_slots, P.pair_cap, P.lds_bytes());
     const size_t nqw = (size_t)P.nchunk * P.nspec;
     P.list.assign(nqw * P.list_cap, 0);
     P.pairs.assign(nqw * P.pair_cap, 0);
@@ -2726,35 +2734,59 @@ extern "C" int sfm_ransac_combine(sfm_comm *c, uint64_t *key, double *model) {
     // and a stream are kept on the communicator.
     SFM_HIP(hipSetDevice(c->device));
     if (!c->scratch) {
-        SFM_HIP(hipMalloc(&c->scratch, 80));
+        SFM_HIP(hipMalloc(&c->scratch, 96));
         SFM_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     }
     void *d = c->scratch;
     hipStream_t s = c->stream;
+    // Every rank enters every collective, whatever happened locally: a rank
+    // whose copies fail contributes the neutral value (key 0, owner -1) and
+    // reports its error after the collectives, so no peer is left waiting.
+    // The model travels by broadcast from the winning rank (found by a second
+    // max-reduce of the owner), so the winner's F arrives bit for bit (-0.0
+    // included), not as a sum.
     int rc = 0;
-    uint64_t gkey = 0;
-    double m[9];
-    auto fail = [&](ncclResult_t r, const char *what) {
-        set_error("%s: %s", what, ncclGetErrorString(r));
-        rc = SFM_ERR_COMM;
-    };
-    if (hipMemcpyAsync(d, key, 8, hipMemcpyHostToDevice, s) != hipSuccess) rc = SFM_ERR_HIP;
-    ncclResult_t r;
-    if (!rc && (r = ncclAllReduce(d, d, 1, ncclUint64, ncclMax, c->comm, s)) != ncclSuccess) fail(r, "ncclAllReduce(max)");
-    if (!rc && (hipMemcpyAsync(&gkey, d, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess))
-        rc = SFM_ERR_HIP;
-    if (!rc && gkey != 0) {
-        for (int k = 0; k < 9; ++k) m[k] = (*key == gkey) ? model[k] : 0.0;
-        double *dm = reinterpret_cast<double *>(static_cast<char *>(d) + 8);
-        if (hipMemcpyAsync(dm, m, 72, hipMemcpyHostToDevice, s) != hipSuccess) rc = SFM_ERR_HIP;
-        if (!rc && (r = ncclAllReduce(dm, dm, 9, ncclDouble, ncclSum, c->comm, s)) != ncclSuccess)
-            fail(r, "ncclAllReduce(sum)");
-        if (!rc && (hipMemcpyAsync(m, dm, 72, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess))
+    auto hip_ok = [&](hipError_t e) {
+        if (e != hipSuccess && !rc) {
+            set_error("ransac combine: %s", hipGetErrorString(e));
             rc = SFM_ERR_HIP;
-        if (!rc) std::memcpy(model, m, 72);
+        }
+        return e == hipSuccess;
+    };
+    auto nccl_ok = [&](ncclResult_t r, const char *what) {
+        if (r != ncclSuccess) {
+            set_error("%s: %s", what, ncclGetErrorString(r));
+            rc = SFM_ERR_COMM;
+        }
+        return r == ncclSuccess;
+    };
+    uint64_t *dkey = static_cast<uint64_t *>(d);
+    double *dm = reinterpret_cast<double *>(static_cast<char *>(d) + 8);
+    int32_t *downer = reinterpret_cast<int32_t *>(static_cast<char *>(d) + 80);
+    const uint64_t mykey = *key;
+    if (!hip_ok(hipMemcpyAsync(dkey, &mykey, 8, hipMemcpyHostToDevice, s))) (void)hipMemsetAsync(dkey, 0, 8, s);
+    if (!nccl_ok(ncclAllReduce(dkey, dkey, 1, ncclUint64, ncclMax, c->comm, s), "ncclAllReduce(max key)")) return rc;
+    uint64_t gkey = 0;
+    if (!hip_ok(hipMemcpyAsync(&gkey, dkey, 8, hipMemcpyDeviceToHost, s)) || !hip_ok(hipStreamSynchronize(s))) gkey = 0;
+    const int32_t mine = (gkey != 0 && mykey == gkey && !rc) ? c->rank : -1;
+    if (!hip_ok(hipMemcpyAsync(downer, &mine, 4, hipMemcpyHostToDevice, s))) (void)hipMemsetAsync(downer, 0xff, 4, s);
+    if (!nccl_ok(ncclAllReduce(downer, downer, 1, ncclInt32, ncclMax, c->comm, s), "ncclAllReduce(max owner)"))
+        return rc;
+    int32_t owner = -1;
+    if (!hip_ok(hipMemcpyAsync(&owner, downer, 4, hipMemcpyDeviceToHost, s)) || !hip_ok(hipStreamSynchronize(s)))
+        owner = -1;
+    // every rank read the same owner (or every rank failed the same read): the broadcast is entered uniformly
+    if (owner >= 0) {
+        if (c->rank == owner) hip_ok(hipMemcpyAsync(dm, model, 72, hipMemcpyHostToDevice, s));
+        if (!nccl_ok(ncclBroadcast(dm, dm, 9, ncclDouble, owner, c->comm, s), "ncclBroadcast(model)")) return rc;
+        double m[9];
+        if (hip_ok(hipMemcpyAsync(m, dm, 72, hipMemcpyDeviceToHost, s)) && hip_ok(hipStreamSynchronize(s)) && !rc)
+            std::memcpy(model, m, 72);
+    } else if (gkey != 0 && !rc) {
+        set_error("ransac combine: no rank owns the winning key");
+        rc = SFM_ERR_COMM;
     }
     if (!rc) *key = gkey;
-    if (rc == SFM_ERR_HIP) set_error("sfm_ransac_combine: HIP call failed");
     return rc;
 }
 

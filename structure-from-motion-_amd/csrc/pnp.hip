@@ -703,7 +703,11 @@ __device__ void nlpnp_projection(const Cam3 &K, const double *p, double *P) {
 // 6 x 6 R factor and Q^T f by CholeskyQR2 -- pass 1 sums the Gram matrix
 // J^T J (fixed-order block sums), R1 = chol; pass 2 recomputes the rows,
 // q = J R1^-1, sums q^T q and q^T f, R2 = chol, R = R2 R1, Q^T f = R2^-T q^T f
-// (orthogonal to working precision for cond(J) up to ~1e8).  MINPACK's
+// (orthogonal to working precision for cond(J) up to ~1e8).  When pass 1's
+// Gram factor needs a diagonal shift (J numerically rank-deficient), a
+// third pass runs (shifted CholeskyQR3); a shift, and a later pass whose
+// Gram factor still fails (its factor kept as the identity), are reported
+// in bits 8 and 9 of info (sfm_nonlinear_pnp).  MINPACK's
 // qrfac with column pivoting then runs on R (6 x 6, lane 0): the trailing
 // column norms it pivots on are invariant under Q, so it picks the pivots
 // qrfac would pick on J.  lmpar, the trust region and the stopping tests are
@@ -774,7 +778,7 @@ struct NlShared {
     double rdiag[6], acnorm[6], wa1[6], wa3[6], qtf[6];
     double r6[6][6];  // upper triangle of the pivoted QR factor, column-major r6[col][row]
     double par, delta, xnorm, fnorm, gnorm, ratio, temp;
-    int ipvt[6], info, nfev, iter, flag;
+    int ipvt[6], info, nfev, iter, flag, npass, qrflags;
 };
 
 // Residual rows of point i under projection P: f = (x - proj).flatten()
@@ -808,7 +812,9 @@ __global__ void __launch_bounds__(NL2_THREADS) k_nonlinear_pnp(const double *__r
         for (int k = 0; k < 3; ++k) out[k] = C0[k];
         for (int k = 0; k < 9; ++k) out[3 + k] = R0[k];
         out[12] = 0.0;
+        out[13] = 0.0;
         S.flag = 0;
+        S.qrflags = 0;
         if (n >= 4) {
             scipy_R_to_rotvec(R0, S.p);
             for (int i = 0; i < 3; ++i)
@@ -886,7 +892,10 @@ __global__ void __launch_bounds__(NL2_THREADS) k_nonlinear_pnp(const double *__r
 #pragma unroll
             for (int k = 0; k < 21; ++k) S.g[k] = gsum[k];
             double R1[6][6];
-            if (!chol6(S.g, R1)) {  // numerically rank-deficient: shifted factor, pass 2 corrects
+            S.npass = 2;
+            if (!chol6(S.g, R1)) {  // numerically rank-deficient: shifted factor, passes 2 and 3 correct
+                S.npass = 3;
+                S.qrflags |= 1;
                 double tr = 0;
                 int u = 0;
                 for (int a2 = 0; a2 < 6; ++a2)
@@ -896,7 +905,7 @@ __global__ void __launch_bounds__(NL2_THREADS) k_nonlinear_pnp(const double *__r
                 for (int a2 = 0; a2 < 6; ++a2)
                     for (int c2 = a2; c2 < 6; ++c2, ++u)
                         if (a2 == c2) S.g[u] += 1e-12 * tr + 1e-300;
-                chol6(S.g, R1);
+                if (!chol6(S.g, R1)) S.qrflags |= 2;
             }
 #pragma unroll
             for (int a2 = 0; a2 < 6; ++a2) {
@@ -906,7 +915,9 @@ __global__ void __launch_bounds__(NL2_THREADS) k_nonlinear_pnp(const double *__r
             }
         }
         __syncthreads();
-        // ---- pass 2: q = J R1^-1 rows (R1 read from LDS): q^T q and q^T f
+        const int npass = S.npass;
+        for (int pass = 2; pass <= npass; ++pass) {
+        // ---- pass 2 (3): q = J R1^-1 rows (R1 read from LDS): q^T q and q^T f
 #pragma unroll
         for (int k = 0; k < 27; ++k) gsum[k] = 0.0;
         for (int64_t i = t; i < n; i += NL2_THREADS) {
@@ -939,9 +950,33 @@ __global__ void __launch_bounds__(NL2_THREADS) k_nonlinear_pnp(const double *__r
             for (int a2 = 0; a2 < 6; ++a2) gsum[21 + a2] += q0[a2] * b0 + q1[a2] * b1;
         }
         nl2_sum<27>(gsum, red27);
+        if (t == 0 && pass < npass) {  // an intermediate pass: R1 <- R2 R1, then the next pass
+            double R2[6][6];
+            if (!chol6(gsum, R2)) {
+                S.qrflags |= 2;
+                for (int a2 = 0; a2 < 6; ++a2)
+                    for (int c2 = 0; c2 < 6; ++c2) R2[a2][c2] = a2 == c2 ? 1.0 : 0.0;
+            }
+            double Rn[6][6];
+            for (int i = 0; i < 6; ++i)
+                for (int j = 0; j < 6; ++j) {
+                    double v = 0;
+                    for (int k = i; k <= j; ++k) v += R2[i][k] * S.R1[k][j];
+                    Rn[i][j] = i <= j ? v : 0.0;
+                }
+            for (int i = 0; i < 6; ++i) {
+                for (int j = 0; j < 6; ++j) S.R1[i][j] = Rn[i][j];
+                S.g[21 + i] = 1.0 / Rn[i][i];
+            }
+        }
+        if (pass < npass) {
+            __syncthreads();
+            continue;
+        }
         if (t == 0) {
             double R2[6][6];
-            if (!chol6(gsum, R2)) {  // cannot happen for a full-rank J; keep R1
+            if (!chol6(gsum, R2)) {  // cannot happen for a full-rank J; keep R1 (reported)
+                S.qrflags |= 2;
                 for (int a2 = 0; a2 < 6; ++a2)
                     for (int c2 = 0; c2 < 6; ++c2) R2[a2][c2] = a2 == c2 ? 1.0 : 0.0;
             }
@@ -1007,6 +1042,7 @@ __global__ void __launch_bounds__(NL2_THREADS) k_nonlinear_pnp(const double *__r
             S.gnorm = gnorm;
             if (gnorm <= 1e-8) S.info = 4;
         }
+        }  // passes
         __syncthreads();
         if (S.info != 0) break;
         // ---- inner loop
@@ -1108,6 +1144,7 @@ __global__ void __launch_bounds__(NL2_THREADS) k_nonlinear_pnp(const double *__r
         for (int i = 0; i < 3; ++i) out[i] = fma(-R[6 + i], S.p[5], fma(-R[3 + i], S.p[4], (-R[i]) * S.p[3]));
         for (int k = 0; k < 9; ++k) out[3 + k] = R[k];
         out[12] = (double)S.info;
+        out[13] = (double)S.qrflags;
     }
 }
 
@@ -1259,6 +1296,7 @@ extern "C" int sfm_nonlinear_pnp(const double *X, const double *x, int64_t N, co
     std::memcpy(hp + 16, X, (size_t)N * 24);
     std::memcpy(hp + 16 + 3 * (size_t)N, x, (size_t)N * 16);
     hres[12] = -1.0;
+    hres[13] = 0.0;
     hipStream_t s = c->stream;
     const bool tm = call_timing();
     if (tm) SFM_HIP(hipEventRecord(c->ev[0], s));
@@ -1273,7 +1311,10 @@ extern "C" int sfm_nonlinear_pnp(const double *X, const double *x, int64_t N, co
     SFM_HIP(hipStreamSynchronize(s));
     std::memcpy(C_out, hres, 3 * sizeof(double));
     std::memcpy(R_out, hres + 3, 9 * sizeof(double));
-    if (info) *info = (int32_t)hres[12];
+    // info: MINPACK's code; bits 8-9 (non-negative info only): the CholeskyQR
+    // flags (1: pass 1's Gram factor needed a shift, a third pass ran; 2: a
+    // later Gram factor failed and was kept as the identity)
+    if (info) *info = (int32_t)hres[12] >= 0 ? (int32_t)hres[12] | ((int32_t)hres[13] << 8) : (int32_t)hres[12];
     double t[4] = {0, 0, 0, 0};
     if (tm) {
         float a = 0, b = 0;
