@@ -583,12 +583,14 @@ __global__ void __launch_bounds__(THREADS) k_camera_lin(CamLinArgs a) {
 //     its block to slab[range][block]; k_schur_finish sums the ranges in
 //     order.  Deterministic, no atomics.
 constexpr int SW_THREADS = 768;
-constexpr int SW_MAX_STAGED = 1024;  // slots per (chunk, spec) (the LDS is the tighter bound)
+
 constexpr int SW_MAX_COLS = SW_THREADS / 2 - 96;  // blocks per spec (2 lanes each; a loader wave, two staging waves)
 constexpr int NXCD = 8;
 constexpr int SLOT_D = 18;  // staged slot (doubles): p (3) | F = G L^T (9, row-major) | G q (3) | X (3)
 constexpr int SW_STAGE_WAVES = 2;  // waves that stage the next chunk (no lane group)
 constexpr int SW_STAGE_BATCH = 4;  // slots a staging lane has in flight
+constexpr int SW_MAX_STAGED = 64 * SW_STAGE_WAVES * SW_STAGE_BATCH;  // slots per (chunk, spec): one staging round
+constexpr int SW_STAMP_WG = 4096, SW_STAMP_EV = 68;  // SFM_SWEEP_STAMPS: workgroups, events per wave
 
 struct SweepGroup {
     int32_t blk, lane_base, G, flags;  // flags: 1 = diagonal block, 2 = a side is the spec's second camera
@@ -617,20 +619,33 @@ __device__ __forceinline__ void obs_pG(const double *R, const double (&x)[3], co
         for (int c = 0; c < 3; ++c) G[i][c] = A[0][i] * T[0][c] + A[1][i] * T[1][c];
 }
 
-// M = A^T (A R) of an observation and its p = R X, from the camera and X
-__device__ __forceinline__ void obs_pM(const double *R, const double (&x)[3], const double (&K)[9], double (&p)[3],
-                                       double (&M)[3][3]) {
-    double A[2][3];
-    obs_Ap(R, x, K, A, p);
-    double ar[2][3];
+// the b side of a pair from its camera and the point: p = R X, the
+// projection Jacobian A (2x3) and A R.  The reciprocal of the depth is
+// v_rcp_f64 refined by two Newton steps (within an ulp of the division; the
+// Schur sweep's Hessian only -- the residuals, the gradient and the trial
+// cost use the division)
+__device__ __forceinline__ void obs_pAR(const double *R, const double (&x)[3], const double (&K)[9], double (&p)[3],
+                                        double (&A)[2][3], double (&ar)[2][3]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) p[i] = R[3 * i] * x[0] + R[3 * i + 1] * x[1] + R[3 * i + 2] * x[2];
+    const double xc0 = p[0] + R[9], xc1 = p[1] + R[10], xc2 = p[2] + R[11];
+    double u[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) u[i] = K[3 * i] * xc0 + K[3 * i + 1] * xc1 + K[3 * i + 2] * xc2;
+    const double wz = u[2] + 1e-8;
+    double iw = __builtin_amdgcn_rcp(wz);
+    iw = __builtin_fma(iw, __builtin_fma(-wz, iw, 1.0), iw);
+    iw = __builtin_fma(iw, __builtin_fma(-wz, iw, 1.0), iw);
+    const double pu = u[0] * iw, pv = u[1] * iw;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        A[0][c] = -(iw * K[c] - pu * iw * K[6 + c]);
+        A[1][c] = -(iw * K[3 + c] - pv * iw * K[6 + c]);
+    }
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int c = 0; c < 3; ++c) ar[a][c] = A[a][0] * R[c] + A[a][1] * R[3 + c] + A[a][2] * R[6 + c];
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) M[i][c] = A[0][i] * ar[0][c] + A[1][i] * ar[1][c];
 }
 
 // slot pieces (16 B): 0-5 p, F | 6 Gq0 Gq1 | 7 Gq2 X0 | 8 X1 X2
@@ -656,7 +671,9 @@ __device__ __forceinline__ void cross_rows(const double (&p)[3], const double (&
     }
 }
 
-// rows 3h..3h+2 of S_ab = E_a H E_b^T, H = G_a G_b^T = F_a M_b^T, into acc[o..o+18)
+// rows 3h..3h+2 of S_ab = E_a H E_b^T into acc[o..o+18): X = [p_a]x H (h = 0)
+// or H (h = 1), row r of X E_b^T = [X [p_b]x^T | X]; the cross terms go
+// into the accumulators as two fused multiply-adds each
 template <int NA>
 __device__ __forceinline__ void pair_rows(int h, int o, const double (&pa)[3], const double (&H)[3][3],
                                           const double (&pb)[3], double (&acc)[NA]) {
@@ -670,25 +687,33 @@ __device__ __forceinline__ void pair_rows(int h, int o, const double (&pa)[3], c
             for (int j = 0; j < 3; ++j) X[i][j] = H[i][j];
     }
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {  // row r of X E_b^T = [X [p_b]x^T | X]
-        acc[o + 6 * r + 0] += -pb[2] * X[r][1] + pb[1] * X[r][2];
-        acc[o + 6 * r + 1] += pb[2] * X[r][0] - pb[0] * X[r][2];
-        acc[o + 6 * r + 2] += -pb[1] * X[r][0] + pb[0] * X[r][1];
-        acc[o + 6 * r + 3] += X[r][0];
-        acc[o + 6 * r + 4] += X[r][1];
-        acc[o + 6 * r + 5] += X[r][2];
+    for (int r = 0; r < 3; ++r) {
+        double *a = acc + o + 6 * r;
+        a[0] = __builtin_fma(pb[1], X[r][2], __builtin_fma(-pb[2], X[r][1], a[0]));
+        a[1] = __builtin_fma(-pb[0], X[r][2], __builtin_fma(pb[2], X[r][0], a[1]));
+        a[2] = __builtin_fma(pb[0], X[r][1], __builtin_fma(-pb[1], X[r][0], a[2]));
+        a[3] += X[r][0];
+        a[4] += X[r][1];
+        a[5] += X[r][2];
     }
 }
-// a lane's share of one pair: LPP = 2, rows 3h..3h+2 (acc[0..18)); LPP = 1,
-// the whole 6x6 block (acc[0..36)), H formed once
+// a lane's share of one pair: H = G_a G_b^T = F_a M_b^T with M_b = A_b^T (A_b
+// R_b), formed as (F_a (A_b R_b)^T) A_b (18 + 18 multiply-adds, not 27 + 18);
+// LPP = 2: rows 3h..3h+2 (acc[0..18)); LPP = 1: the whole 6x6 block
+// (acc[0..36)), H formed once
 template <int LPP, int NA>
 __device__ __forceinline__ void pair_block(int h, const double (&pa)[3], const double (&Fa)[3][3],
-                                           const double (&pb)[3], const double (&Mb)[3][3], double (&acc)[NA]) {
-    double H[3][3];
+                                           const double (&pb)[3], const double (&Ab)[2][3],
+                                           const double (&arb)[2][3], double (&acc)[NA]) {
+    double U[3][2], H[3][3];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) H[i][j] = Fa[i][0] * Mb[j][0] + Fa[i][1] * Mb[j][1] + Fa[i][2] * Mb[j][2];
+        for (int a = 0; a < 2; ++a) U[i][a] = Fa[i][0] * arb[a][0] + Fa[i][1] * arb[a][1] + Fa[i][2] * arb[a][2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) H[i][j] = U[i][0] * Ab[0][j] + U[i][1] * Ab[1][j];
     if constexpr (LPP == 2) {
         pair_rows(h, 0, pa, H, pb, acc);
     } else {
@@ -716,7 +741,7 @@ __device__ __forceinline__ void diag_gq(int h, const double (&pa)[3], const doub
 // [pair_cap / 2] (16-bit slot indices) | header [hdr_cap] (group pair offsets (ngroups + 1), n0, n1,
 // chunk obs0); after both buffers the spec's two cameras (24 doubles).
 // Chunk q uses buffer q & 1.  The list (global, list_cap words per
-// (chunk, spec)) holds every slot's point | (row << 31).
+// (chunk, spec)) holds the slot count, then every slot's point | (row << 31).
 struct SweepLds {
     int buf_slots, pair_cap, hdr_cap, list_cap;
     __device__ int words() const { return buf_slots * 2 * SLOT_D + pair_cap / 2 + hdr_cap; }
@@ -738,6 +763,65 @@ __device__ __forceinline__ void sweep_fetch(int t, int nload, int64_t qw, const 
     for (int base = (t & ~63); base < L.hdr_cap; base += step) glds4(hdr + qw * L.hdr_cap + base + lane, hw + base);
 }
 
+// end-of-range reduction, SW_RED_W accumulators a round: the groups' lanes
+// put their accumulators in LDS (red[k][lane]), then EVERY thread of the
+// workgroup takes output tasks (group, half, accumulator) and sums that
+// group's slots in slot order (the order of the sequential sum before, so
+// the same bits) -- independent LDS loads in flight instead of one lane per
+// group walking its slots 42 times (28 us of a 92-us cfg5 workgroup)
+constexpr int SW_RED_W = 21;
+constexpr int SW_RED_LD = SW_THREADS + 1;  // padded row: an output task's 21 accumulators sit in different banks
+// workgroup barrier ordering LDS only: outstanding global loads and stores
+// stay in flight (__syncthreads drains them)
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+template <int LPP, int NACC>
+__device__ __forceinline__ void sweep_reduce(const double (&acc)[NACC], bool has_acc, int t, int ng,
+                                             const SweepGroup *__restrict__ grps, double *__restrict__ slab_r,
+                                             double *red) {
+    constexpr int NH = LPP == 2 ? 2 : 1;  // output halves per group (LPP = 2: rows 3h..3h+2)
+    // the spec's group table in LDS after the accumulators (one global
+    // latency, not one per output task)
+    SweepGroup *gtab = reinterpret_cast<SweepGroup *>(red + SW_RED_W * SW_RED_LD);
+    for (int g = t; g < ng; g += SW_THREADS) gtab[g] = grps[g];
+#pragma unroll
+    for (int k0 = 0; k0 < NACC; k0 += SW_RED_W) {
+        if (has_acc)
+#pragma unroll
+            for (int k = 0; k < SW_RED_W; ++k) red[k * SW_RED_LD + t] = acc[k0 + k];
+        lds_barrier();
+        for (int o = t; o < ng * NH * SW_RED_W; o += SW_THREADS) {
+            const int g = o / (NH * SW_RED_W), hk = o % (NH * SW_RED_W), h = hk / SW_RED_W, k = hk % SW_RED_W;
+            const SweepGroup gr = gtab[g];
+            const int kk = k0 + k;
+            const bool dg = gr.flags & 1;
+            // LPP = 1: acc[0..36) the 6x6 block row-major, acc[36..42) the
+            // diagonal's sum Z q; LPP = 2: acc[0..18) rows 3h..3h+2, acc[18..21) the
+            // diagonal's three sum Z q entries of half h
+            const int dst = LPP == 2 ? (kk < 18 ? 18 * h + kk : 36 + 3 * h + (kk - 18)) : kk;
+            if (dst >= 36 && !dg) continue;
+            const double *src = red + k * SW_RED_LD + gr.lane_base + h;
+            double v = 0.0;
+            const int n = gr.G / LPP;
+            int sl = 0;
+            for (; sl + 4 <= n; sl += 4) {  // four loads in flight, summed in slot order
+                const double a0 = src[LPP * sl], a1 = src[LPP * (sl + 1)], a2 = src[LPP * (sl + 2)],
+                             a3 = src[LPP * (sl + 3)];
+                v += a0;
+                v += a1;
+                v += a2;
+                v += a3;
+            }
+            for (; sl < n; ++sl) v += src[LPP * sl];
+            slab_r[(int64_t)gr.blk * ITEM_W + dst] = v;
+        }
+        lds_barrier();  // the slab stores need not land before the next round
+    }
+}
+
 template <int LPP>  // lanes per pair slot
 __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     int32_t nspec, int32_t nrange, int32_t nbd, SweepLds L, const int32_t *__restrict__ rchunk,
@@ -746,7 +830,7 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     const int32_t *__restrict__ spec_cam, const uint32_t *__restrict__ list, const uint32_t *__restrict__ pairs,
     const int32_t *__restrict__ hdr, const double *__restrict__ Xg, const double *__restrict__ Lq,
     const double *__restrict__ Rt, Kmat Km, double *__restrict__ slab, const int *__restrict__ gate, int dbg,
-    int nsweep, CamLinArgs cl) {
+    int nsweep, CamLinArgs cl, long long *__restrict__ stamps) {
     extern __shared__ double2 sw_lds[];
     if ((int)blockIdx.x >= nsweep) {  // camera blocks of the normal equations on the CUs the sweep leaves idle
         if (!*cl.glin) return;
@@ -756,11 +840,20 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
         return;
     }
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
+    if (dbg & 8) return;         // timing probe: the launch without the sweep
     uint32_t *ldsw = reinterpret_cast<uint32_t *>(sw_lds);
     const int loc = blockIdx.x / NXCD;
     const int w = loc % nspec, r = (loc / nspec) * NXCD + (int)(blockIdx.x % NXCD);
     if (r >= nrange) return;  // whole workgroup
     const int t = threadIdx.x;
+    // SFM_SWEEP_STAMPS: s_memrealtime per (workgroup, event, wave), lane 0
+    long long *stw = stamps && blockIdx.x < SW_STAMP_WG && (t & 63) == 0
+                         ? stamps + (int64_t)blockIdx.x * SW_STAMP_EV * (SW_THREADS / 64) + (t >> 6)
+                         : nullptr;
+    auto stamp = [&](int ev) {
+        if (stw && ev < SW_STAMP_EV) stw[ev * (SW_THREADS / 64)] = (long long)__builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
     const int nload = spec_nload[w];
     const bool loader = (t >> 6) < nload;
     const int gi = lanegrp[w * SW_THREADS + t];
@@ -788,66 +881,101 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
         // buffer while the groups work on chunk q; SW_STAGE_BATCH slots a
         // lane per round, their list entries, then their points' X and Lq,
         // all in flight together.  The same barriers as the groups below.
-        auto stage_chunk = [&](int qs, uint32_t *bw_dst) {
+        // one round a chunk: lane l stages slots l + 128 u (u < SW_STAGE_BATCH;
+        // the planner caps a chunk's slots at SW_MAX_STAGED).  Software
+        // pipelined over the chunks: while chunk q + 1 is written from
+        // registers, the points of chunk q + 2 and the list entries of chunk
+        // q + 3 are in flight, across the barrier (an LDS-only barrier: the
+        // stagers' loads need not land).
+        constexpr int SB = SW_STAGE_BATCH, SSTEP = 64 * SW_STAGE_WAVES;
+        uint32_t e1[SB], e2[SB];
+        int n1 = 0, n2 = 0;
+        double gx[SB][3], gl[SB][9];
+        auto load_list = [&](int qs, uint32_t(&e)[SB], int &n) {
+            if (qs >= q1) {  // uniform; point 0 stands in (load_pts may still read it)
+                n = 0;
+#pragma unroll
+                for (int u = 0; u < SB; ++u) e[u] = 0u;
+                return;
+            }
+            // word 0: the (chunk, spec)'s slot count; the entries follow
+            // (padded to list_cap > buf_slots: every load is in bounds)
             const uint32_t *lst = list + ((int64_t)qs * nspec + w) * L.list_cap;
-            // (the list is padded to list_cap entries; only buf_slots slots exist)
-            for (int s0 = tst; s0 < L.buf_slots; s0 += 64 * SW_STAGE_WAVES * SW_STAGE_BATCH) {
-                uint32_t e[SW_STAGE_BATCH];
-                double gx[SW_STAGE_BATCH][3], gl[SW_STAGE_BATCH][9];
+            n = (dbg & 4) ? 0 : (int)lst[0];
 #pragma unroll
-                for (int u = 0; u < SW_STAGE_BATCH; ++u) {
-                    const int sl = s0 + u * 64 * SW_STAGE_WAVES;
-                    e[u] = sl < L.buf_slots ? lst[sl] : 0u;
-                }
-#pragma unroll
-                for (int u = 0; u < SW_STAGE_BATCH; ++u) {
-                    const int64_t P = e[u] & 0x7fffffffu;
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) gx[u][i] = Xg[3 * P + i];
-#pragma unroll
-                    for (int i = 0; i < 9; ++i) gl[u][i] = Lq[9 * P + i];
-                }
-#pragma unroll
-                for (int u = 0; u < SW_STAGE_BATCH; ++u) {
-                    const int sl = s0 + u * 64 * SW_STAGE_WAVES;
-                    if (sl >= L.buf_slots) continue;
-                    const double *R = scam + 12 * (int)(e[u] >> 31);
-                    const double l[6] = {gl[u][0], gl[u][1], gl[u][2], gl[u][3], gl[u][4], gl[u][5]};
-                    const double x[3] = {gx[u][0], gx[u][1], gx[u][2]};
-                    double pa[3], G[3][3], F[3][3], gq[3];
-                    obs_pG(R, x, K, l, pa, G);
-                    // F = G L^T (L upper: L^T[k][c] = L[c][k], k >= c); G q
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) {
-                        F[i][0] = G[i][0] * l[0] + G[i][1] * l[1] + G[i][2] * l[2];
-                        F[i][1] = G[i][1] * l[3] + G[i][2] * l[4];
-                        F[i][2] = G[i][2] * l[5];
-                        gq[i] = G[i][0] * gl[u][6] + G[i][1] * gl[u][7] + G[i][2] * gl[u][8];
-                    }
-                    double2 *d = reinterpret_cast<double2 *>(bw_dst) + sl * (SLOT_D / 2);
-                    d[0] = make_double2(pa[0], pa[1]);
-                    d[1] = make_double2(pa[2], F[0][0]);
-                    d[2] = make_double2(F[0][1], F[0][2]);
-                    d[3] = make_double2(F[1][0], F[1][1]);
-                    d[4] = make_double2(F[1][2], F[2][0]);
-                    d[5] = make_double2(F[2][1], F[2][2]);
-                    d[6] = make_double2(gq[0], gq[1]);
-                    d[7] = make_double2(gq[2], x[0]);
-                    d[8] = make_double2(x[1], x[2]);
-                }
+            for (int u = 0; u < SB; ++u) {
+                const int sl = tst + u * SSTEP;
+                e[u] = lst[1 + (sl < L.buf_slots ? sl : 0)];
             }
         };
+        auto load_pts = [&](const uint32_t(&e)[SB]) {
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int64_t P = e[u] & 0x7fffffffu;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) gx[u][i] = Xg[3 * P + i];
+#pragma unroll
+                for (int i = 0; i < 9; ++i) gl[u][i] = Lq[9 * P + i];
+            }
+        };
+        auto commit = [&](const uint32_t(&e)[SB], int n, uint32_t *bw_dst) {
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int sl = tst + u * SSTEP;
+                if (sl >= n) continue;
+                const double *R = scam + 12 * (int)(e[u] >> 31);
+                const double l[6] = {gl[u][0], gl[u][1], gl[u][2], gl[u][3], gl[u][4], gl[u][5]};
+                const double x[3] = {gx[u][0], gx[u][1], gx[u][2]};
+                double pa[3], G[3][3], F[3][3], gq[3];
+                obs_pG(R, x, K, l, pa, G);
+                // F = G L^T (L upper: L^T[k][c] = L[c][k], k >= c); G q
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    F[i][0] = G[i][0] * l[0] + G[i][1] * l[1] + G[i][2] * l[2];
+                    F[i][1] = G[i][1] * l[3] + G[i][2] * l[4];
+                    F[i][2] = G[i][2] * l[5];
+                    gq[i] = G[i][0] * gl[u][6] + G[i][1] * gl[u][7] + G[i][2] * gl[u][8];
+                }
+                double2 *d = reinterpret_cast<double2 *>(bw_dst) + sl * (SLOT_D / 2);
+                d[0] = make_double2(pa[0], pa[1]);
+                d[1] = make_double2(pa[2], F[0][0]);
+                d[2] = make_double2(F[0][1], F[0][2]);
+                d[3] = make_double2(F[1][0], F[1][1]);
+                d[4] = make_double2(F[1][2], F[2][0]);
+                d[5] = make_double2(F[2][1], F[2][2]);
+                d[6] = make_double2(gq[0], gq[1]);
+                d[7] = make_double2(gq[2], x[0]);
+                d[8] = make_double2(x[1], x[2]);
+            }
+        };
+        load_list(q0, e1, n1);
+        load_list(q0 + 1, e2, n2);
+        load_pts(e1);
         __syncthreads();  // the cameras are in LDS
-        if (q0 < q1) stage_chunk(q0, ldsw);
-        __syncthreads();
+        if (q0 < q1) commit(e1, n1, ldsw);
+        auto advance = [&]() {  // chunk q+2's points and chunk q+3's list in flight
+            load_pts(e2);
+#pragma unroll
+            for (int u = 0; u < SB; ++u) e1[u] = e2[u];
+            n1 = n2;
+        };
+        advance();
+        load_list(q0 + 2, e2, n2);
+        stamp(1);
+        lds_barrier();
         for (int q = q0; q < q1; ++q) {
-            if (q + 1 < q1) stage_chunk(q + 1, ldsw + (((q - q0) & 1) ^ 1) * bw);
-            __syncthreads();
+            if (q + 1 < q1) commit(e1, n1, ldsw + (((q - q0) & 1) ^ 1) * bw);
+            if (q + 2 < q1) {
+                advance();
+                load_list(q + 3, e2, n2);
+            }
+            stamp(2 + q - q0);
+            lds_barrier();
         }
-        for (int k0 = 0; k0 < NACC; k0 += 7) {  // the reduction's barriers
-            __syncthreads();
-            __syncthreads();
-        }
+        const double none[NACC] = {};  // no accumulators: output tasks only
+        sweep_reduce<LPP>(none, false, t, ng, groups + spec_goff[w], slab + (int64_t)r * nbd * ITEM_W,
+                          reinterpret_cast<double *>(sw_lds));
+        stamp(SW_STAMP_EV - 1);
         return;
     }
     double Rb[12];  // the group's column camera (the b side; the a camera itself for a diagonal block)
@@ -858,6 +986,7 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     for (int k = 0; k < NACC; ++k) acc[k] = 0.0;
     if (q0 < q1 && loader) sweep_fetch(t, nload, (int64_t)q0 * nspec + w, L, pairs, hdr, ldsw);
     __syncthreads();  // the cameras are in LDS
+    stamp(1);
     __syncthreads();  // chunk q0's slots are staged
     for (int q = q0; q < q1; ++q) {
         const int cur = (q - q0) & 1;
@@ -872,11 +1001,11 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
                 const int a0 = second ? n0 : 0, a1 = (dbg & 2) ? a0 : second ? n0 + n1 : n0;
                 for (int a = a0 + slot; a < a1; a += nslot) {
                     const double2 *sl = buf + a * (SLOT_D / 2);
-                    double pa[3], Fa[3][3], x[3], pm[3], Ma[3][3];
+                    double pa[3], Fa[3][3], x[3], pm[3], Aa[2][3], ara[2][3];
                     load_slot_a(sl, pa, Fa);
                     load_slot_x(sl, x);
-                    obs_pM(Rb, x, K, pm, Ma);
-                    pair_block<LPP>(h, pa, Fa, pa, Ma, acc);
+                    obs_pAR(Rb, x, K, pm, Aa, ara);
+                    pair_block<LPP>(h, pa, Fa, pa, Aa, ara, acc);
                     const double2 v6 = sl[6], v7 = sl[7];
                     const double gq[3] = {v6.x, v6.y, v7.x};  // G_a q
                     diag_gq<LPP>(h, pa, gq, acc);
@@ -886,43 +1015,22 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
                 const uint16_t *pl16 = reinterpret_cast<const uint16_t *>(pl);
                 for (int k = k0 + slot; k < k1; k += nslot) {
                     const double2 *sl = buf + (int)pl16[k] * (SLOT_D / 2);
-                    double pa[3], Fa[3][3], x[3], pb[3], Mb[3][3];
+                    double pa[3], Fa[3][3], x[3], pb[3], Ab[2][3], arb[2][3];
                     load_slot_a(sl, pa, Fa);
                     load_slot_x(sl, x);
-                    obs_pM(Rb, x, K, pb, Mb);  // the b side: camera j, the same point
-                    pair_block<LPP>(h, pa, Fa, pb, Mb, acc);
+                    obs_pAR(Rb, x, K, pb, Ab, arb);  // the b side: camera j, the same point
+                    pair_block<LPP>(h, pa, Fa, pb, Ab, arb, acc);
                 }
             }
         }
+        stamp(2 + q - q0);
         __syncthreads();  // chunk q's buffer is free; chunk q+1's slots, pairs and header have landed
     }
-    // reduce the group's slots (lanes of equal parity) in slot order through
-    // LDS (the staging buffers are free now), 7 accumulators per round;
-    // groups of any size and position
-    double *red = reinterpret_cast<double *>(sw_lds);
-    double *out = slab + ((int64_t)r * nbd + grp.blk) * ITEM_W;
-#pragma unroll
-    for (int k0 = 0; k0 < NACC; k0 += 7) {
-#pragma unroll
-        for (int k = 0; k < 7; ++k) red[k * SW_THREADS + t] = acc[k0 + k];
-        __syncthreads();
-        if (gi >= 0 && slot == 0) {
-#pragma unroll
-            for (int k = 0; k < 7; ++k) {
-                double v = 0.0;
-                for (int sl = 0; sl < nslot; ++sl) v += red[k * SW_THREADS + grp.lane_base + LPP * sl + h];
-                const int kk = k0 + k;
-                if constexpr (LPP == 2) {
-                    if (kk < 18) out[18 * h + kk] = v;
-                    else if (diag) out[36 + 3 * h + (kk - 18)] = v;
-                } else {
-                    if (kk < 36) out[kk] = v;  // acc[6r + c]: row r of the 6x6 block, row-major
-                    else if (diag) out[kk] = v;
-                }
-            }
-        }
-        __syncthreads();
-    }
+    // reduce the groups' slots in slot order through LDS (the staging
+    // buffers are free now)
+    sweep_reduce<LPP>(acc, gi >= 0, t, ng, groups + spec_goff[w], slab + (int64_t)r * nbd * ITEM_W,
+                      reinterpret_cast<double *>(sw_lds));
+    stamp(SW_STAMP_EV - 1);
 }
 
 // one 64-thread workgroup per camera block (i <= j, dense upper-triangle
@@ -1358,13 +1466,6 @@ constexpr int SOLVE_THREADS = 512;
 constexpr int SOLVE_ROWS = SOLVE_THREADS - 64;  // rows owned by the row waves per pass
 constexpr int SOLVE_MAX = 4096;
 
-// workgroup barrier ordering LDS only: outstanding global loads stay in flight
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
 // One row segment of tile k's rows per lane and register: lanes [0, TB) hold
 // the diagonal tile's column (q[m] = L[k0+m][k0+lane]), lanes [TB, 2 TB) the
 // block left of it (q[m] = L[k0+m][k0-TB+lane-TB], tile k's contribution to
@@ -1784,6 +1885,29 @@ struct GjBufs {
     }
 };
 
+// SFM_SWEEP_STAMPS=1: k_schur_sweep records s_memrealtime stamps per
+// (workgroup, event, wave) into a process-wide device buffer (sfm_sweep_debug
+// reads it): event 0 start, 1 the first chunk staged (stagers) / the
+// cameras in LDS (groups), 2 + i chunk i done, SW_STAMP_EV - 1 the end
+static long long *g_sw_dbg = nullptr;
+static const size_t g_sw_dbg_n = (size_t)SW_STAMP_WG * SW_STAMP_EV * (SW_THREADS / 64);
+static long long *sw_dbg_ptr() {
+    static const bool on = std::getenv("SFM_SWEEP_STAMPS") && std::atoi(std::getenv("SFM_SWEEP_STAMPS")) != 0;
+    if (!on) return nullptr;
+    if (!g_sw_dbg) {
+        if (hipMalloc(&g_sw_dbg, g_sw_dbg_n * sizeof(long long)) != hipSuccess) return g_sw_dbg = nullptr;
+        (void)hipMemset(g_sw_dbg, 0, g_sw_dbg_n * sizeof(long long));
+    }
+    return g_sw_dbg;
+}
+extern "C" int sfm_sweep_debug(long long *out, int64_t n) {
+    SFM_CHECK_ARG(out, "null pointer");
+    if (!g_sw_dbg) return 0;
+    SFM_HIP(hipDeviceSynchronize());
+    SFM_HIP(hipMemcpy(out, g_sw_dbg, std::min<size_t>((size_t)n, g_sw_dbg_n) * sizeof(long long), hipMemcpyDeviceToHost));
+    return 0;
+}
+
 // SFM_GJ_DEBUG=1: the persistent solve records s_memrealtime stamps per
 // (workgroup, panel) into a process-wide device buffer (sfm_gj_debug reads it)
 static long long *g_gj_dbg = nullptr;
@@ -2033,6 +2157,76 @@ static void plan_camera_items(int nc, const std::vector<int32_t> &cstart, const 
 
 static int32_t dense_blk(int nc, int i, int j) { return i * nc - i * (i - 1) / 2 + (j - i); }
 
+// trips a slot of a group makes through its chunk share: ceil(P / s)
+static inline int sweep_trips(int P, int s) { return (P + s - 1) / s; }
+
+// slots (lanes / LPP) of the spec's off-diagonal groups, `budget` in all,
+// from the exact per-chunk pair counts P[g][q] (the plan is static: the
+// same points and cameras every LM iteration).  A chunk ends at a barrier,
+// so its time is the largest trip count of any group in it (the diagonal
+// groups' dtrip[q] included); the objective is the sum over chunks.  Greedy
+// on the separable surrogate sum_g sum_q trips^6 (a soft max), one slot at a
+// time to the group whose trips drop the surrogate most; the proportional
+// split (slots ~ total pairs) is kept when it scores better on the true
+// objective.  Returns the objective of the allocation chosen.
+static int64_t sweep_alloc(const std::vector<std::vector<uint16_t>> &P, const std::vector<int> &dtrip, int budget,
+                           std::vector<int> &slots) {
+    const int ng = (int)P.size(), nq = (int)dtrip.size();
+    auto objective = [&](const std::vector<int> &sl) {
+        int64_t f = 0;
+        for (int q = 0; q < nq; ++q) {
+            int m = dtrip[q];
+            for (int g = 0; g < ng; ++g) m = std::max(m, sweep_trips(P[g][q], sl[g]));
+            f += m;
+        }
+        return f;
+    };
+    // proportional split (the round-2/3 planner): floor shares, then the
+    // remaining slots to the group with the most pairs per slot
+    std::vector<int64_t> tot(ng, 0);
+    int64_t all = 0;
+    for (int g = 0; g < ng; ++g) {
+        for (int q = 0; q < nq; ++q) tot[g] += P[g][q];
+        all += tot[g];
+    }
+    std::vector<int> prop(ng, 1);
+    int sum = 0;
+    for (int g = 0; g < ng; ++g) {
+        prop[g] = std::max(1, (int)(all > 0 ? (double)tot[g] / all * budget : 1.0));
+        sum += prop[g];
+    }
+    while (sum > budget) {
+        auto it = std::max_element(prop.begin(), prop.end());
+        *it -= 1;
+        sum -= 1;
+    }
+    while (sum < budget && ng) {
+        int best = 0;
+        for (int g = 1; g < ng; ++g)
+            if (tot[g] * prop[best] > tot[best] * prop[g]) best = g;
+        prop[best] += 1;
+        sum += 1;
+    }
+    // greedy on the soft max
+    auto pw = [](int t) { const double x = t; return x * x * x * x * x * x; };
+    auto gain = [&](int g, int s) {
+        double d = 0;
+        for (int q = 0; q < nq; ++q) d += pw(sweep_trips(P[g][q], s)) - pw(sweep_trips(P[g][q], s + 1));
+        return d;
+    };
+    std::vector<int> gr(ng, 1);
+    std::vector<double> gn(ng);
+    for (int g = 0; g < ng; ++g) gn[g] = gain(g, 1);
+    for (int used = ng; used < budget; ++used) {
+        const int g = (int)(std::max_element(gn.begin(), gn.end()) - gn.begin());
+        gr[g] += 1;
+        gn[g] = gain(g, gr[g]);
+    }
+    const int64_t fp = objective(prop), fg = ng <= budget ? objective(gr) : INT64_MAX;
+    slots = fg < fp ? gr : prop;
+    return std::min(fp, fg);
+}
+
 static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt,
                        const std::vector<int32_t> &pstart, const std::vector<int64_t> &cnt, int lpp, SweepPlan &P) {
     P.nbd = nc * (nc + 1) / 2;
@@ -2060,28 +2254,21 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     for (int w = 0; w < P.nspec; ++w)
         for (size_t rr = 0; rr < specs[w].size(); ++rr)
             for (int j = specs[w][rr].j0; j < specs[w][rr].j1; ++j) spec_of[(size_t)specs[w][rr].c * nc + j] = w;
-    P.lanegrp.assign((size_t)P.nspec * SW_THREADS, (int16_t)-1);
-    // per spec: diagonal groups first (they only read LDS, so their waves
-    // are the loader waves; power-of-two sizes), then the off-diagonal groups
-    // sorted by size
-    std::vector<std::vector<int>> gid_of(P.nspec);  // (row, j - j0) -> group index within spec
+    // per spec: the diagonal groups (their lanes are the loader waves; power
+    // of two sizes) and the off-diagonal groups with their pair budget
+    struct G0 { int blk, flags, slots; double work; int key, cam_b, row_cam; };
+    std::vector<std::vector<G0>> sgd(P.nspec), sg(P.nspec);
+    std::vector<int> sGd(P.nspec), sbudget(P.nspec);
     int max_ng = 0;
     for (int w = 0; w < P.nspec; ++w) {
-        struct G0 { int blk, flags, slots; double work; int key, cam_b; };
-        std::vector<G0> gd, g;
-        double tot = 0;
+        auto &gd = sgd[w], &g = sg[w];
         for (size_t rr = 0; rr < specs[w].size(); ++rr) {
             const Row &R = specs[w][rr];
             for (int j = R.j0; j < R.j1; ++j) {
                 const double work = (double)cnt[(size_t)R.c * nc + j];
                 G0 x = {dense_blk(nc, R.c, j), (j == R.c ? 1 : 0) | (rr == 1 ? 2 : 0), 1, work,
-                        (int)(rr * nc + (j - R.j0)), j};
-                if (j == R.c) {
-                    gd.push_back(x);
-                } else {
-                    g.push_back(x);
-                    tot += work;
-                }
+                        (int)(rr * nc + (j - R.j0)), j, R.c};
+                (j == R.c ? gd : g).push_back(x);
             }
         }
         const int nd = (int)gd.size(), noff = (int)g.size();
@@ -2091,60 +2278,19 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
             budget = (SW_THREADS - 64 * nload - 64 * SW_STAGE_WAVES) / lpp;  // pair slots
             if (noff <= budget) break;
         }
-        // slots in proportion to the block's pair work, the whole budget
-        // used: floor shares (at least one), then the remaining slots one at
-        // a time to the group with the most work per slot (any group size:
-        // the end-of-range reduction goes through LDS, so groups need not be
-        // powers of two nor stay inside one wave).  SFM_SWEEP_POW2=1 keeps
-        // the earlier power-of-two sizes (61 % of the budget at cfg4).
-        int sum = 0;
-        const bool pow2 = env_int("SFM_SWEEP_POW2", 0) != 0;
-        for (auto &x : g) {
-            x.slots = std::max(1, (int)(tot > 0 ? x.work / tot * budget : 1.0));
-            if (pow2) {
-                int sl = 1;
-                while (sl * 2 <= x.slots && sl < 32) sl *= 2;
-                x.slots = sl;
-            }
-            sum += x.slots;
-        }
-        while (sum > budget) {  // rounding up to one slot overshot: trim the largest
-            auto it = std::max_element(g.begin(), g.end(), [](const G0 &a, const G0 &b) { return a.slots < b.slots; });
-            it->slots -= 1;
-            sum -= 1;
-        }
-        while (!pow2 && sum < budget && !g.empty()) {
-            auto it = std::max_element(g.begin(), g.end(), [](const G0 &a, const G0 &b) {
-                return a.work * b.slots < b.work * a.slots;  // a.work / a.slots < b.work / b.slots
-            });
-            it->slots += 1;
-            sum += 1;
-        }
-        std::stable_sort(g.begin(), g.end(), [](const G0 &a, const G0 &b) { return a.slots > b.slots; });
-        for (auto &x : gd) x.slots = Gd / lpp;
-        g.insert(g.begin(), gd.begin(), gd.end());
-        P.goff.push_back((int32_t)P.groups.size());
+        sGd[w] = Gd;
+        sbudget[w] = budget;
         P.nload.push_back(nload);
-        gid_of[w].assign(specs[w].size() * nc, -1);
-        int lane = 0;
-        for (size_t k = 0; k < g.size(); ++k) {
-            if (k == gd.size()) lane = 64 * nload;  // off-diagonal groups after the loader waves
-            const int G = lpp * g[k].slots;
-            P.groups.push_back({g[k].blk, lane, G, g[k].flags, g[k].cam_b});
-            for (int l = lane; l < lane + G; ++l) P.lanegrp[(size_t)w * SW_THREADS + l] = (int16_t)k;
-            gid_of[w][g[k].key] = (int)k;
-            lane += G;
-        }
-        max_ng = std::max(max_ng, (int)g.size());
+        max_ng = std::max(max_ng, nd + noff);
     }
-    P.goff.push_back((int32_t)P.groups.size());
     P.hdr_cap = (max_ng + 4 + 63) / 64 * 64;
     // ranges of equal observation count; chunks small enough that two
     // (chunk, spec) buffers fit the LDS and the chunk's records an XCD's L2
-    // 8 ranges while nspec x 8 workgroups fit one pass over the 256 CUs
-    // (cfg4: 25 specs, 200 workgroups); past that 16, which halves the last
-    // partial pass (cfg5, 100 specs: 0.969 -> 0.885 ms; cfg4 at 16: 0.145 -> 0.161 ms)
-    const int nr_dflt = P.nspec * NXCD <= 256 ? 8 : 16;
+    // 8 ranges (one per XCD): every workgroup pays a prologue (the first
+    // chunk staged, ~7 us) and the end-of-range reduction, so fewer, longer
+    // workgroups win even with a partial last pass over the CUs (cfg5, 100
+    // specs: 16 ranges 0.539 ms, 8 ranges 0.505 ms; cfg4: 0.145 -> 0.161 ms at 16)
+    const int nr_dflt = 8;
     P.nrange = std::max(NXCD, env_int("SFM_SWEEP_RANGES", nr_dflt) / NXCD * NXCD);
     // chunks as large as the LDS allows (every chunk boundary is a barrier
     // and an imbalance point): from the 16-bit cap down, scaled by the
@@ -2187,15 +2333,98 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
         }
         P.buf_slots = std::max(8, (max_staged + 7) / 8 * 8);
         P.pair_cap = std::max(128, (max_pairs + 127) / 128 * 128);  // 16-bit entries, whole 64-lane DMA rows
-        P.list_cap = (P.buf_slots + 63) / 64 * 64;
+        P.list_cap = (P.buf_slots + 1 + 63) / 64 * 64;  // the count, then the entries
         if ((ok && max_staged <= SW_MAX_STAGED && P.lds_bytes() <= 160 * 1024) || chunk_obs <= 64) break;
         const double over = std::max((double)max_staged / SW_MAX_STAGED, (double)P.lds_bytes() / (160 * 1024));
         chunk_obs = std::max(64, (int)(chunk_obs * std::min(0.95, std::max(0.5, 0.98 / over))));
     }
     P.nchunk = (int32_t)cut.size();
+    // exact per-chunk counts: pairs per block, observations per camera
+    std::vector<uint16_t> bq((size_t)P.nbd * P.nchunk, 0), cq((size_t)nc * P.nchunk, 0);
+    for (int32_t q = 0; q < P.nchunk; ++q) {
+        const int64_t pe = q + 1 < P.nchunk ? cut[q + 1] : np_;
+        for (int64_t pp = cut[q]; pp < pe; ++pp)
+            for (int32_t a = pstart[pp]; a < pstart[pp + 1]; ++a) {
+                cq[(size_t)cam[a] * P.nchunk + q]++;
+                for (int32_t b = pstart[pp]; b < pstart[pp + 1]; ++b)
+                    if (cam[b] > cam[a]) bq[(size_t)dense_blk(nc, cam[a], cam[b]) * P.nchunk + q]++;
+            }
+    }
+    // slots per group, then lanes: diagonal groups first (the loader
+    // waves), then the off-diagonal groups by size.  SFM_SWEEP_ALLOC=0 keeps
+    // the proportional split, SFM_SWEEP_POW2=1 the power-of-two sizes.
+    P.lanegrp.assign((size_t)P.nspec * SW_THREADS, (int16_t)-1);
+    std::vector<std::vector<int>> gid_of(P.nspec);  // (row, j - j0) -> group index within spec
+    const bool pow2 = env_int("SFM_SWEEP_POW2", 0) != 0, exact = env_int("SFM_SWEEP_ALLOC", 1) != 0;
+    int64_t f_plan = 0, f_ideal = 0;
+    for (int w = 0; w < P.nspec; ++w) {
+        auto &gd = sgd[w], &g = sg[w];
+        const int Gd = sGd[w], budget = sbudget[w], nload = P.nload[w];
+        std::vector<int> dtrip(P.nchunk, 0);
+        for (auto &x : gd)
+            for (int32_t q = 0; q < P.nchunk; ++q)
+                dtrip[q] = std::max(dtrip[q], sweep_trips(cq[(size_t)x.row_cam * P.nchunk + q], Gd / lpp));
+        std::vector<std::vector<uint16_t>> Pg(g.size());
+        for (size_t k = 0; k < g.size(); ++k)
+            Pg[k].assign(bq.begin() + (size_t)g[k].blk * P.nchunk, bq.begin() + (size_t)(g[k].blk + 1) * P.nchunk);
+        std::vector<int> sl;
+        if (exact && !pow2 && !g.empty() && (int)g.size() <= budget) {
+            f_plan += sweep_alloc(Pg, dtrip, budget, sl);
+        } else {  // proportional (power-of-two sizes with SFM_SWEEP_POW2)
+            double tot = 0;
+            for (auto &x : g) tot += x.work;
+            sl.assign(g.size(), 1);
+            int sum = 0;
+            for (size_t k = 0; k < g.size(); ++k) {
+                sl[k] = std::max(1, (int)(tot > 0 ? g[k].work / tot * budget : 1.0));
+                if (pow2) {
+                    int v = 1;
+                    while (v * 2 <= sl[k] && v < 32) v *= 2;
+                    sl[k] = v;
+                }
+                sum += sl[k];
+            }
+            while (sum > budget) {
+                auto it = std::max_element(sl.begin(), sl.end());
+                *it -= 1;
+                sum -= 1;
+            }
+            while (!pow2 && sum < budget && !g.empty()) {
+                size_t best = 0;
+                for (size_t k = 1; k < g.size(); ++k)
+                    if (g[k].work * sl[best] > g[best].work * sl[k]) best = k;
+                sl[best] += 1;
+                sum += 1;
+            }
+        }
+        for (int32_t q = 0; q < P.nchunk; ++q) {  // the balance bound: every chunk's pairs over all slots
+            int64_t pq = 0;
+            for (auto &v : Pg) pq += v[q];
+            f_ideal += std::max<int64_t>(dtrip[q], (pq + budget - 1) / std::max(1, budget));
+        }
+        for (size_t k = 0; k < g.size(); ++k) g[k].slots = sl[k];
+        std::stable_sort(g.begin(), g.end(), [](const G0 &a, const G0 &b) { return a.slots > b.slots; });
+        for (auto &x : gd) x.slots = Gd / lpp;
+        g.insert(g.begin(), gd.begin(), gd.end());
+        P.goff.push_back((int32_t)P.groups.size());
+        gid_of[w].assign(specs[w].size() * nc, -1);
+        int lane = 0;
+        for (size_t k = 0; k < g.size(); ++k) {
+            if (k == gd.size()) lane = 64 * nload;  // off-diagonal groups after the loader waves
+            const int G = lpp * g[k].slots;
+            P.groups.push_back({g[k].blk, lane, G, g[k].flags, g[k].cam_b});
+            for (int l = lane; l < lane + G; ++l) P.lanegrp[(size_t)w * SW_THREADS + l] = (int16_t)k;
+            gid_of[w][g[k].key] = (int)k;
+            lane += G;
+        }
+    }
+    P.goff.push_back((int32_t)P.groups.size());
     if (env_int("SFM_SWEEP_VERBOSE", 0))
-        std::fprintf(stderr, "sweep plan: nspec %d nrange %d nchunk %d chunk_obs %d buf_slots %d pair_cap %d lds %zu B\n",
-                     P.nspec, P.nrange, P.nchunk, chunk_obs, P.buf_slots, P.pair_cap, P.lds_bytes());
+        std::fprintf(stderr,
+                     "sweep plan: nspec %d nrange %d nchunk %d chunk_obs %d buf_slots %d pair_cap %d lds %zu B; "
+                     "chunk trips (sum over specs, chunks) %lld, balance bound %lld\n",
+                     P.nspec, P.nrange, P.nchunk, chunk_obs, P.buf_slots, P.pair_cap, P.lds_bytes(), (long long)f_plan,
+                     (long long)f_ideal);
     const size_t nqw = (size_t)P.nchunk * P.nspec;
     P.list.assign(nqw * P.list_cap, 0);
     P.pairs.assign(nqw * P.pair_cap, 0);
@@ -2218,10 +2447,11 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
             int32_t *lst = &P.list[qw * P.list_cap];
             const int32_t n0 = (int32_t)per_cam[sp[0].c].size();
             const int32_t n1 = sp.size() > 1 ? (int32_t)per_cam[sp[1].c].size() : 0;
-            int ns_ = 0;  // every slot's point | (spec row << 31)
+            int ns_ = 1;  // the count, then every slot's point | (spec row << 31)
             for (size_t rr = 0; rr < sp.size(); ++rr)
                 for (int32_t off : per_cam[sp[rr].c])
                     lst[ns_++] = (int32_t)((uint32_t)pt[o0 + off] | (rr ? 0x80000000u : 0u));
+            lst[0] = n0 + n1;
             for (; ns_ < P.list_cap; ++ns_) lst[ns_] = pt[o0];  // padding: any valid point
             const int ng = P.goff[w + 1] - P.goff[w];
             glist.assign(ng, {});
@@ -2482,6 +2712,11 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     // H once) or 2 (SFM_SWEEP_LPP=2: half the rows each)
     p->sw_lpp = env_int("SFM_SWEEP_LPP", 1) == 2 ? 2 : 1;
     plan_sweep(nc, np_, no, cam, pt, pstart, cnt, p->sw_lpp, sw);
+    if (sw.buf_slots > SW_MAX_STAGED) {  // one point with more observations in a spec's cameras than a round holds
+        set_error("sweep plan: %d observations of one spec's cameras in a single point range (max %d)", sw.buf_slots,
+                  SW_MAX_STAGED);
+        return SFM_ERR_ARG;
+    }
     // camera items (the camera blocks of the normal equations): for
     // k_camera_lin, chunks of <= CAM_CHUNK of each camera's observations, one
     // per workgroup; for the camera workgroups of k_schur_sweep, the
@@ -2511,7 +2746,9 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     p->sw_nbd = sw.nbd;
     p->sw_L = {sw.buf_slots, sw.pair_cap, sw.hdr_cap, sw.list_cap};
     p->sw_nchunk = sw.nchunk;
-    p->sw_lds_bytes = std::max(sw.lds_bytes(), (size_t)7 * SW_THREADS * sizeof(double));  // + the end-of-range reduction
+    // + the end-of-range reduction: the accumulators and the group table
+    p->sw_lds_bytes = std::max(sw.lds_bytes(), (size_t)SW_RED_W * SW_RED_LD * sizeof(double) +
+                                                   (size_t)sw.hdr_cap * sizeof(SweepGroup));
     p->pt_blocks = std::max(1, ceil_div(np_ * PT_GROUP, PT_THREADS));
     p->payload_len = pay_vec_base(p->ns) + 3 * p->ns + 1;
     int rc;
@@ -2872,7 +3109,7 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
                        p->d_sw_nload, p->d_sw_goff, p->d_sw_groups, p->d_sw_lanegrp, p->d_sw_scam,
                        reinterpret_cast<const uint32_t *>(p->d_sw_list), p->d_sw_pairs, p->d_sw_hdr, p->d_X, p->d_Lq,
                        p->d_Rt, p->K, p->d_slab, gst, p->sw_debug, nsweep,
-                       camlin_args(p, true, &p->d_lm[par].run_lin));
+                       camlin_args(p, true, &p->d_lm[par].run_lin), sw_dbg_ptr());
     SFM_HIP(hipGetLastError());
     // one rank: the solve's first launch sums the slabs itself (SlabSrc)
     // (the persistent solve reads the finished payload: the finish runs as its own launch)
