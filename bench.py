@@ -49,15 +49,15 @@ SWEEP_RANGES = 8  # k_schur_sweep's point ranges (SFM_SWEEP_RANGES default)
 
 def design_bytes(name, n_obs, n_pts, n_pairs, nblocks, ns):
     """Bytes one launch of each kernel family must move in THIS design
-    (DESIGN.md §4's table: no stored Jacobians, the 128-B Schur records), per
-    LM iteration -- reported next to the SURVEY §8(d) compulsory bytes, which
-    are the roofline's.  n_pairs: off-diagonal co-observation pairs;
-    nblocks: camera blocks i <= j."""
-    if name == "schur_blocks":  # k_schur_sweep: Schur records (p, G, q) 128 B/obs staged once, staged-slot
-        # list 4 B/obs, pair list 4 B/pair, range slab written + read, payload written
-        return 128 * n_obs + 4 * n_obs + 4 * n_pairs + 2 * 336 * SWEEP_RANGES * nblocks + 8 * (ns * ns + 3 * ns)
-    if name == "point_prep":    # DESIGN §4: the 128-B Schur record written + pt, cam indices read per obs;
-        return 136 * n_obs + 148 * n_pts  # V, g read, L, q written, X read per point
+    (DESIGN.md §4's table: no stored Jacobians, no per-observation records
+    -- the record-free sweep), per LM iteration -- reported next to the SURVEY
+    §8(d) compulsory bytes, which are the roofline's.  n_pairs: off-diagonal
+    co-observation pairs; nblocks: camera blocks i <= j."""
+    if name == "schur_blocks":  # k_schur_sweep: X (24 B) + Lq (72 B) gathered per staged observation, the
+        # obs index read (4 B/obs), pair list 2 B/pair, range slab written + read, payload written
+        return 100 * n_obs + 2 * n_pairs + 2 * 336 * SWEEP_RANGES * nblocks + 8 * (ns * ns + 3 * ns)
+    if name == "point_prep":    # DESIGN §4: V, g read, L, q (Lq) written per point
+        return 144 * n_pts
     if name == "linearize":     # k_linearize: obs + cam (24 B/obs incl. the point CSR), X in, V, g out per point;
         # camera blocks (in the sweep launch): camera-major pt + obs (20 B) + X gather (24 B) per obs
         return 24 * n_obs + 100 * n_pts + 44 * n_obs

@@ -741,6 +741,90 @@ __device__ __forceinline__ void nl2_sum(double (&v)[NV], double (*red)[NV]) {
     }
 }
 
+// Several workgroups per problem (round 3): the rows are cut into nb
+// contiguous slices, one per workgroup, and every workgroup runs the whole
+// lmdif control flow itself on the same totals (the same operations on the
+// same values, so the same decisions and bits everywhere; only block 0
+// writes the result).  A row pass ends in a cross-workgroup all-gather of
+// the per-workgroup sums: each block stores its totals (write-through, the
+// parity-`seq` buffer), drains them, raises its flag to (epoch << 32) | seq;
+// wave 0 polls the nb flags (one lane each), and every block sums the nb
+// partials in block order.  Double buffering by the parity of seq is enough:
+// a block reaches pass seq + 2 only after every block published seq + 1,
+// i.e. after every block finished reading seq.  Polls are bounded (200 ms);
+// a timeout raises the abort word and every block returns (info -2, the host
+// reports an error) -- no wait can outlive it.
+struct NlX {
+    double *part;                // [2][NL_MAXWG][32] per-block totals by seq parity
+    unsigned long long *flag;    // [NL_MAXWG] (epoch << 32) | seq of the block's last publication
+    unsigned long long *abort_;  // = epoch once a poll has timed out
+    unsigned long long epoch;
+    int nb;
+};
+constexpr int NL_MAXWG = 64;
+constexpr long long NL_POLL_LIMIT = 20000000;  // s_memrealtime ticks (100 MHz): 200 ms
+
+__device__ __forceinline__ double nl_ldag(const double *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// nl2_sum, then (nb > 1) the all-gather over the blocks; false on an abort
+template <int NV>
+__device__ __forceinline__ bool nlx_sum(double (&v)[NV], double (*red)[NV], const NlX &X, unsigned &seq,
+                                        double *xtot, int *xok) {
+    nl2_sum<NV>(v, red);
+    if (X.nb == 1) return true;
+    ++seq;
+    const int slot = seq & 1, lane = threadIdx.x & 63;
+    const unsigned long long want = (X.epoch << 32) | seq;
+    if (threadIdx.x == 0) {
+        double *mine = X.part + ((size_t)slot * NL_MAXWG + blockIdx.x) * 32;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) __hip_atomic_store(mine + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(X.flag + blockIdx.x, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (threadIdx.x < 64) {
+        auto seen = [&]() {
+            return lane >= X.nb ||
+                   __hip_atomic_load(X.flag + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want;
+        };
+        bool done = seen(), ab = false;
+        long long t0 = -1;
+        for (unsigned it = 1; !__all(done); ++it) {  // wave-uniform loop
+            __builtin_amdgcn_s_sleep(1);
+            if (!done) done = seen();
+            if (it % 128 == 0) {
+                bool a = __hip_atomic_load(X.abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == X.epoch;
+                const long long t = __builtin_amdgcn_s_memrealtime();
+                if (t0 < 0) t0 = t;
+                else if (t - t0 > NL_POLL_LIMIT) {
+                    a = true;
+                    if (lane == 0)
+                        __hip_atomic_store(X.abort_, X.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (__any(a)) {
+                    ab = true;
+                    break;
+                }
+            }
+        }
+        if (lane == 0) *xok = !ab;
+    }
+    __syncthreads();
+    if (!*xok) return false;
+    if (threadIdx.x < NV) {
+        const double *col = X.part + (size_t)slot * NL_MAXWG * 32 + threadIdx.x;
+        double s = 0.0;
+        for (int w = 0; w < X.nb; ++w) s += nl_ldag(col + w * 32);
+        xtot[threadIdx.x] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = xtot[k];
+    return true;
+}
+
 // Cholesky of a 6 x 6 SPD matrix given as its upper triangle (21, row-major
 // packed); R upper with R^T R = G.  false on a non-positive pivot.
 __device__ __forceinline__ bool chol6(const double *G, double (&R)[6][6]) {
@@ -798,21 +882,33 @@ __device__ __forceinline__ void nl2_res(const double *P, const double *X, const 
     nl2_res(P, X[3 * i], X[3 * i + 1], X[3 * i + 2], x[i], f0, f1);
 }
 
-// One workgroup per problem.  out: C (3) | R (9) | info (as double)
+// nb = gridDim.x workgroups per problem (NlX above).  out: C (3) | R (9) |
+// info (as double) | CholeskyQR flags, written by block 0
 __global__ void __launch_bounds__(NL2_THREADS) k_nonlinear_pnp(const double *__restrict__ X,
                                                                const double2 *__restrict__ x, int64_t n, Cam3 K,
                                                                const double *__restrict__ C0,
                                                                const double *__restrict__ R0, int32_t maxfev,
-                                                               double *__restrict__ out) {
+                                                               double *__restrict__ out, NlX XG) {
     __shared__ NlShared S;
     __shared__ double red27[NL2_WAVES][27];
+    __shared__ double red2[NL2_WAVES][2];
     __shared__ double red1[NL2_WAVES][1];
+    __shared__ double xtot[32];
+    __shared__ int xok;
     const int t = threadIdx.x;
+    const bool lead = blockIdx.x == 0;
+    const int64_t lo = n * blockIdx.x / gridDim.x, hi = n * (blockIdx.x + 1) / gridDim.x;  // this block's rows
+    unsigned seq = 0;
+    auto fail = [&]() {  // a cross-block hand-off timed out
+        if (lead && t == 0) out[12] = -2.0;
+    };
     if (t == 0) {
-        for (int k = 0; k < 3; ++k) out[k] = C0[k];
-        for (int k = 0; k < 9; ++k) out[3 + k] = R0[k];
-        out[12] = 0.0;
-        out[13] = 0.0;
+        if (lead) {
+            for (int k = 0; k < 3; ++k) out[k] = C0[k];
+            for (int k = 0; k < 9; ++k) out[3 + k] = R0[k];
+            out[12] = 0.0;
+            out[13] = 0.0;
+        }
         S.flag = 0;
         S.qrflags = 0;
         if (n >= 4) {
@@ -827,24 +923,23 @@ __global__ void __launch_bounds__(NL2_THREADS) k_nonlinear_pnp(const double *__r
         }
     }
     __syncthreads();
-    if (S.flag == 2) return;                                      // n < 4: C, R unchanged
-    if (S.flag == 1) { if (t == 0) out[12] = -1.0; return; }      // except path
-    // initial residual norm and finiteness
+    if (S.flag == 2) return;                                              // n < 4: C, R unchanged
+    if (S.flag == 1) { if (lead && t == 0) out[12] = -1.0; return; }      // except path
+    // initial residual norm and finiteness (one sum: {non-finite, |f|^2})
     {
-        double v[1] = {0.0};
+        double v[2] = {0.0, 0.0};
         int fin = 1;
-        for (int64_t i = t; i < n; i += NL2_THREADS) {
+        for (int64_t i = lo + t; i < hi; i += NL2_THREADS) {
             double f0, f1;
             nl2_res(S.sP[0], X, x, i, f0, f1);
             fin &= (isfinite(f0) && isfinite(f1)) ? 1 : 0;
-            v[0] += f0 * f0 + f1 * f1;
+            v[1] += f0 * f0 + f1 * f1;
         }
-        double nf[1] = {(double)(1 - fin)};
-        nl2_sum<1>(nf, red1);
-        if (nf[0] != 0.0) { if (t == 0) out[12] = -1.0; return; }
-        nl2_sum<1>(v, red1);
+        v[0] = (double)(1 - fin);
+        if (!nlx_sum<2>(v, red2, XG, seq, xtot, &xok)) return fail();
+        if (v[0] != 0.0) { if (lead && t == 0) out[12] = -1.0; return; }
         if (t == 0) {
-            S.fnorm = sqrt(v[0]); S.par = 0.0; S.delta = 0.0; S.xnorm = 0.0; S.iter = 1; S.nfev = 1; S.info = 0;
+            S.fnorm = sqrt(v[1]); S.par = 0.0; S.delta = 0.0; S.xnorm = 0.0; S.iter = 1; S.nfev = 1; S.info = 0;
         }
     }
     __syncthreads();
@@ -869,7 +964,7 @@ __global__ void __launch_bounds__(NL2_THREADS) k_nonlinear_pnp(const double *__r
         double gsum[27];
 #pragma unroll
         for (int k = 0; k < 27; ++k) gsum[k] = 0.0;
-        for (int64_t i = t; i < n; i += NL2_THREADS) {
+        for (int64_t i = lo + t; i < hi; i += NL2_THREADS) {
             double b0, b1, J0[6], J1[6];
             const double Xi = X[3 * i], Yi = X[3 * i + 1], Zi = X[3 * i + 2];
             const double2 qi = x[i];
@@ -887,7 +982,7 @@ __global__ void __launch_bounds__(NL2_THREADS) k_nonlinear_pnp(const double *__r
 #pragma unroll
                 for (int c2 = a2; c2 < 6; ++c2) gsum[u++] += J0[a2] * J0[c2] + J1[a2] * J1[c2];
         }
-        nl2_sum<27>(gsum, red27);
+        if (!nlx_sum<27>(gsum, red27, XG, seq, xtot, &xok)) return fail();
         if (t == 0) {
 #pragma unroll
             for (int k = 0; k < 21; ++k) S.g[k] = gsum[k];
@@ -920,7 +1015,7 @@ __global__ void __launch_bounds__(NL2_THREADS) k_nonlinear_pnp(const double *__r
         // ---- pass 2 (3): q = J R1^-1 rows (R1 read from LDS): q^T q and q^T f
 #pragma unroll
         for (int k = 0; k < 27; ++k) gsum[k] = 0.0;
-        for (int64_t i = t; i < n; i += NL2_THREADS) {
+        for (int64_t i = lo + t; i < hi; i += NL2_THREADS) {
             double b0, b1, J0[6], J1[6];
             const double Xi = X[3 * i], Yi = X[3 * i + 1], Zi = X[3 * i + 2];
             const double2 qi = x[i];
@@ -949,7 +1044,7 @@ __global__ void __launch_bounds__(NL2_THREADS) k_nonlinear_pnp(const double *__r
 #pragma unroll
             for (int a2 = 0; a2 < 6; ++a2) gsum[21 + a2] += q0[a2] * b0 + q1[a2] * b1;
         }
-        nl2_sum<27>(gsum, red27);
+        if (!nlx_sum<27>(gsum, red27, XG, seq, xtot, &xok)) return fail();
         if (t == 0 && pass < npass) {  // an intermediate pass: R1 <- R2 R1, then the next pass
             double R2[6][6];
             if (!chol6(gsum, R2)) {
@@ -1071,12 +1166,12 @@ __global__ void __launch_bounds__(NL2_THREADS) k_nonlinear_pnp(const double *__r
             }
             __syncthreads();
             double v[1] = {0.0};
-            for (int64_t i = t; i < n; i += NL2_THREADS) {
+            for (int64_t i = lo + t; i < hi; i += NL2_THREADS) {
                 double f0, f1;
                 nl2_res(S.sP[0], X, x, i, f0, f1);
                 v[0] += f0 * f0 + f1 * f1;
             }
-            nl2_sum<1>(v, red1);
+            if (!nlx_sum<1>(v, red1, XG, seq, xtot, &xok)) return fail();
             const double fnorm1 = sqrt(v[0]);
             if (t == 0) {
                 S.nfev += 1;
@@ -1138,7 +1233,7 @@ __global__ void __launch_bounds__(NL2_THREADS) k_nonlinear_pnp(const double *__r
         }
         if (S.info != 0) break;
     }
-    if (t == 0) {
+    if (lead && t == 0) {
         double R[9];
         scipy_rotvec_to_R(S.p, R);
         for (int i = 0; i < 3; ++i) out[i] = fma(-R[6 + i], S.p[5], fma(-R[3 + i], S.p[4], (-R[i]) * S.p[3]));
@@ -1151,6 +1246,11 @@ __global__ void __launch_bounds__(NL2_THREADS) k_nonlinear_pnp(const double *__r
 }  // namespace sfm
 
 using namespace sfm;
+
+static int env_int(const char *name, int dflt) {
+    const char *v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
 
 static int load_cam(const double *K, Cam3 &c) {
     std::memcpy(c.k, K, sizeof c.k);
@@ -1304,11 +1404,30 @@ extern "C" int sfm_nonlinear_pnp(const double *X, const double *x, int64_t N, co
                        c->buf[0].as<double>(), c->buf[1].as<double>());
     SFM_HIP(hipGetLastError());
     if (tm) SFM_HIP(hipEventRecord(c->ev[1], s));
-    hipLaunchKernelGGL(k_nonlinear_pnp, dim3(1), dim3(NL2_THREADS), 0, s, c->buf[0].as<double>(),
-                       c->buf[1].as<double2>(), (int64_t)N, cam, dIn, dIn + 3, max_nfev, hres);
+    // workgroups: ~1024 rows each (SFM_NLPNP_WGS overrides), at most NL_MAXWG
+    const int nb = std::max(1, std::min(NL_MAXWG, env_int("SFM_NLPNP_WGS", ceil_div((int64_t)N, 1024))));
+    NlX xg{};
+    xg.nb = nb;
+    if (nb > 1) {
+        const size_t sync_bytes = (2 * NL_MAXWG * 32 + NL_MAXWG + 1) * sizeof(double);
+        if (!c->nl_sync) {
+            SFM_HIP(hipMalloc(&c->nl_sync, sync_bytes));
+            SFM_HIP(hipMemsetAsync(c->nl_sync, 0, sync_bytes, s));
+        }
+        xg.part = static_cast<double *>(c->nl_sync);
+        xg.flag = reinterpret_cast<unsigned long long *>(xg.part + 2 * NL_MAXWG * 32);
+        xg.abort_ = xg.flag + NL_MAXWG;
+        xg.epoch = ++c->nl_epoch;
+    }
+    hipLaunchKernelGGL(k_nonlinear_pnp, dim3(nb), dim3(NL2_THREADS), 0, s, c->buf[0].as<double>(),
+                       c->buf[1].as<double2>(), (int64_t)N, cam, dIn, dIn + 3, max_nfev, hres, xg);
     SFM_HIP(hipGetLastError());
     if (tm) SFM_HIP(hipEventRecord(c->ev[2], s));
     SFM_HIP(hipStreamSynchronize(s));
+    if (hres[12] == -2.0) {
+        set_error("NonlinearPnP: a cross-workgroup hand-off timed out (%d workgroups)", nb);
+        return SFM_ERR_HIP;
+    }
     std::memcpy(C_out, hres, 3 * sizeof(double));
     std::memcpy(R_out, hres + 3, 9 * sizeof(double));
     // info: MINPACK's code; bits 8-9 (non-negative info only): the CholeskyQR

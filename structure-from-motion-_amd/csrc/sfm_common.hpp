@@ -93,9 +93,12 @@ struct ThreadCtx {
     void *gj_ints = nullptr;  // sfm_reduced_solve: the flag buffer its epochs refer to
     int gj_epoch = 0;
     int gj_nT = 0, gj_nseg = 0;  // ... and the layout they were carved with
+    void *nl_sync = nullptr;     // sfm_nonlinear_pnp's cross-workgroup sums (zeroed once; epoch-tagged flags)
+    unsigned nl_epoch = 0;
     ~ThreadCtx() {
         if (stream) {
             (void)hipSetDevice(device);
+            if (nl_sync) (void)hipFree(nl_sync);
             for (auto &e : ev)
                 if (e) (void)hipEventDestroy(e);
             (void)hipStreamDestroy(stream);

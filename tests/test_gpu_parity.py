@@ -670,6 +670,26 @@ def test_nonlinear_pnp_ill_conditioned_vs_oracle(core, kind, eps, n):
         assert abs(cg - co) <= 1e-3 * co, (cg, co)
 
 
+@pytest.mark.parametrize("wgs", [1, 2, 5, 16, 64])
+@pytest.mark.parametrize("n,outl", [(5000, 0.3), (20000, 0.0), (7, 0.0)])
+def test_nonlinear_pnp_workgroups_vs_oracle(core, monkeypatch, wgs, n, outl):
+    """NonlinearPnP (NonlinearPnP.py:97-123) with the rows cut over `wgs`
+    workgroups (every workgroup runs lmdif on all-gathered sums; n = 7 with
+    64 workgroups leaves most slices empty): the same stop reason as the
+    oracle's lmdif, pose within 1e-5, cost within 1e-9 relative -- the bar of
+    the one-workgroup kernel."""
+    X, x, C, R = _pnp_scene(n, 31, outl)
+    C0 = C + 0.05
+    R0 = syn.rotvec_to_matrix([0.03, -0.13, 0.02])[0]
+    monkeypatch.setenv("SFM_NLPNP_WGS", str(wgs))
+    Cg, Rg, ig = core.nonlinear_pnp(X, x, K, C0, R0)
+    Co, Ro, io = O.nonlinear_pnp(X, x, K, C0, R0)
+    assert ig == io
+    assert np.abs(Cg - Co).max() <= 1e-5 * max(1.0, np.abs(Co).max()) and np.abs(Rg - Ro).max() <= 1e-5
+    cg, co = _pnp_cost(X, x, Cg, Rg), _pnp_cost(X, x, Co, Ro)
+    assert abs(cg - co) <= 1e-9 * co + 1e-12
+
+
 def test_nonlinear_pnp_rank_deficient_flags(core):
     """A rank-deficient Jacobian (one point repeated): the Gram factor needs
     the shift, the third CholeskyQR pass runs and the flags say so; lmdif
