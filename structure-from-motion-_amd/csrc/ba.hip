@@ -648,6 +648,39 @@ __device__ __forceinline__ void obs_pAR(const double *R, const double (&x)[3], c
         for (int c = 0; c < 3; ++c) ar[a][c] = A[a][0] * R[c] + A[a][1] * R[3 + c] + A[a][2] * R[6 + c];
 }
 
+// obs_pAR for a pinhole K = [[fx, 0, cx], [0, fy, cy], [0, 0, 1]] (the
+// reference's calibration, checked on the host): the five structural zeros
+// and the unit K[8] dropped -- 4 of the 9 products of K xc, 10 of the 12
+// entries' products of A, 6 of the 18 of A R (~15 % of a pair's VALU work)
+template <bool PH>
+__device__ __forceinline__ void obs_pAR_k(const double *R, const double (&x)[3], const double (&K)[9],
+                                          double (&p)[3], double (&A)[2][3], double (&ar)[2][3]) {
+    if constexpr (!PH) {
+        obs_pAR(R, x, K, p, A, ar);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) p[i] = R[3 * i] * x[0] + R[3 * i + 1] * x[1] + R[3 * i + 2] * x[2];
+        const double xc0 = p[0] + R[9], xc1 = p[1] + R[10], xc2 = p[2] + R[11];
+        const double u0 = K[0] * xc0 + K[2] * xc2, u1 = K[4] * xc1 + K[5] * xc2;
+        const double wz = xc2 + 1e-8;
+        double iw = __builtin_amdgcn_rcp(wz);
+        iw = __builtin_fma(iw, __builtin_fma(-wz, iw, 1.0), iw);
+        iw = __builtin_fma(iw, __builtin_fma(-wz, iw, 1.0), iw);
+        const double pu = u0 * iw, pv = u1 * iw;
+        A[0][0] = -(iw * K[0]);
+        A[0][1] = 0.0;
+        A[0][2] = -(iw * K[2] - pu * iw);
+        A[1][0] = 0.0;
+        A[1][1] = -(iw * K[4]);
+        A[1][2] = -(iw * K[5] - pv * iw);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            ar[0][c] = A[0][0] * R[c] + A[0][2] * R[6 + c];
+            ar[1][c] = A[1][1] * R[3 + c] + A[1][2] * R[6 + c];
+        }
+    }
+}
+
 // slot pieces (16 B): 0-5 p, F | 6 Gq0 Gq1 | 7 Gq2 X0 | 8 X1 X2
 __device__ __forceinline__ void load_slot_a(const double2 *sl, double (&p)[3], double (&F)[3][3]) {
     const double2 v0 = sl[0], v1 = sl[1], v2 = sl[2], v3 = sl[3], v4 = sl[4], v5 = sl[5];
@@ -701,7 +734,7 @@ __device__ __forceinline__ void pair_rows(int h, int o, const double (&pa)[3], c
 // R_b), formed as (F_a (A_b R_b)^T) A_b (18 + 18 multiply-adds, not 27 + 18);
 // LPP = 2: rows 3h..3h+2 (acc[0..18)); LPP = 1: the whole 6x6 block
 // (acc[0..36)), H formed once
-template <int LPP, int NA>
+template <int LPP, bool PH = false, int NA>
 __device__ __forceinline__ void pair_block(int h, const double (&pa)[3], const double (&Fa)[3][3],
                                            const double (&pb)[3], const double (&Ab)[2][3],
                                            const double (&arb)[2][3], double (&acc)[NA]) {
@@ -711,9 +744,16 @@ __device__ __forceinline__ void pair_block(int h, const double (&pa)[3], const d
 #pragma unroll
         for (int a = 0; a < 2; ++a) U[i][a] = Fa[i][0] * arb[a][0] + Fa[i][1] * arb[a][1] + Fa[i][2] * arb[a][2];
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+    for (int i = 0; i < 3; ++i) {
+        if constexpr (PH) {  // A_b[0][1] = A_b[1][0] = 0
+            H[i][0] = U[i][0] * Ab[0][0];
+            H[i][1] = U[i][1] * Ab[1][1];
+            H[i][2] = U[i][0] * Ab[0][2] + U[i][1] * Ab[1][2];
+        } else {
 #pragma unroll
-        for (int j = 0; j < 3; ++j) H[i][j] = U[i][0] * Ab[0][j] + U[i][1] * Ab[1][j];
+            for (int j = 0; j < 3; ++j) H[i][j] = U[i][0] * Ab[0][j] + U[i][1] * Ab[1][j];
+        }
+    }
     if constexpr (LPP == 2) {
         pair_rows(h, 0, pa, H, pb, acc);
     } else {
@@ -822,7 +862,7 @@ __device__ __forceinline__ void sweep_reduce(const double (&acc)[NACC], bool has
     }
 }
 
-template <int LPP>  // lanes per pair slot
+template <int LPP, bool PH = false>  // lanes per pair slot; pinhole K
 __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     int32_t nspec, int32_t nrange, int32_t nbd, SweepLds L, const int32_t *__restrict__ rchunk,
     const int32_t *__restrict__ spec_nload, const int32_t *__restrict__ spec_goff,
@@ -1004,8 +1044,8 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
                     double pa[3], Fa[3][3], x[3], pm[3], Aa[2][3], ara[2][3];
                     load_slot_a(sl, pa, Fa);
                     load_slot_x(sl, x);
-                    obs_pAR(Rb, x, K, pm, Aa, ara);
-                    pair_block<LPP>(h, pa, Fa, pa, Aa, ara, acc);
+                    obs_pAR_k<PH>(Rb, x, K, pm, Aa, ara);
+                    pair_block<LPP, PH>(h, pa, Fa, pa, Aa, ara, acc);
                     const double2 v6 = sl[6], v7 = sl[7];
                     const double gq[3] = {v6.x, v6.y, v7.x};  // G_a q
                     diag_gq<LPP>(h, pa, gq, acc);
@@ -1018,8 +1058,8 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
                     double pa[3], Fa[3][3], x[3], pb[3], Ab[2][3], arb[2][3];
                     load_slot_a(sl, pa, Fa);
                     load_slot_x(sl, x);
-                    obs_pAR(Rb, x, K, pb, Ab, arb);  // the b side: camera j, the same point
-                    pair_block<LPP>(h, pa, Fa, pb, Ab, arb, acc);
+                    obs_pAR_k<PH>(Rb, x, K, pb, Ab, arb);  // the b side: camera j, the same point
+                    pair_block<LPP, PH>(h, pa, Fa, pb, Ab, arb, acc);
                 }
             }
         }
@@ -2508,6 +2548,7 @@ struct sfm_ba_problem {
     int32_t sw_nrange = 0, sw_nspec = 0, sw_nbd = 0, sw_nchunk = 0;
     SweepLds sw_L = {};
     int sw_lpp = 1;
+    bool sw_pinhole = false;
     size_t sw_lds_bytes = 0;
     Kmat K;
     std::vector<double> cams0, pts0;
@@ -2679,6 +2720,9 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     p->nT = (p->ns + p->tb - 1) / p->tb;
     p->nsp = p->nT * p->tb;
     std::memcpy(p->K.k, K, sizeof p->K.k);
+    // a pinhole K (the reference's calibration): the sweep drops its structural zeros
+    p->sw_pinhole = K[1] == 0.0 && K[3] == 0.0 && K[6] == 0.0 && K[7] == 0.0 && K[8] == 1.0 &&
+                    env_int("SFM_SWEEP_PINHOLE", 1) != 0;
     p->cams0.assign(cams, cams + 6 * (size_t)nc);
     p->pts0.assign(pts, pts + 3 * (size_t)np_);
     SFM_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
@@ -2843,6 +2887,8 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = up(p->d_sw_blkij, sw.blkij.data(), sw.blkij.size() * sizeof(int2))))
         return rc;
     SFM_HIP(hipFuncSetAttribute((const void *)k_schur_sweep<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)p->sw_lds_bytes));
+    SFM_HIP(hipFuncSetAttribute((const void *)k_schur_sweep<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)p->sw_lds_bytes));
     SFM_HIP(hipFuncSetAttribute((const void *)k_schur_sweep<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)p->sw_lds_bytes));
@@ -3109,7 +3155,8 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SCHUR], s));
     const int nsweep = NXCD * p->sw_nspec * ceil_div(p->sw_nrange, NXCD);
     const bool fused = p->cl_fused && p->ndiag_items;  // + the camera blocks (after an accepted step)
-    hipLaunchKernelGGL(p->sw_lpp == 1 ? k_schur_sweep<1> : k_schur_sweep<2>, dim3(nsweep + (fused ? p->cl_fused_wg : 0)), dim3(SW_THREADS),
+auto sweep_k = p->sw_lpp == 2 ? k_schur_sweep<2> : p->sw_pinhole ? k_schur_sweep<1, true> : k_schur_sweep<1>;
+hipLaunchKernelGGL(sweep_k, dim3(nsweep + (fused ? p->cl_fused_wg : 0)), dim3(SW_THREADS),
                        p->sw_lds_bytes, s, p->sw_nspec, p->sw_nrange, p->sw_nbd, p->sw_L, p->d_sw_rchunk,
                        p->d_sw_nload, p->d_sw_goff, p->d_sw_groups, p->d_sw_lanegrp, p->d_sw_scam,
                        reinterpret_cast<const uint32_t *>(p->d_sw_list), p->d_sw_pairs, p->d_sw_hdr, p->d_X, p->d_Lq,
