@@ -1876,7 +1876,7 @@ static int launch_reduced_solve(int32_t ns, int32_t nsp, const double *payload, 
 // nT tiles.  cb = 0: the grid would not fit one workgroup per CU, so the
 // multi-launch Cholesky above runs instead (SFM_SOLVE=chol forces it).
 struct GjPlan {
-    int cb = 0, nseg = 0, ncb = 0, sr = 4;  // sr: row tiles per segment (gj_solve.hpp: SR = CB)
+    int cb = 0, nseg = 0, ncb = 0;
     int grid() const { return cb ? ncb * nseg : 0; }
 };
 static GjPlan gj_plan(int nT, int ncu) {
@@ -1884,16 +1884,14 @@ static GjPlan gj_plan(int nT, int ncu) {
     if (const char *e = std::getenv("SFM_SOLVE"))
         if (std::strcmp(e, "chol") == 0) return g;
     if (nT > gj::NTMAX) return g;
+    const int nseg = (nT + gj::SR - 1) / gj::SR;
     const char *fe = std::getenv("SFM_GJ_CB");  // tuning / tests: force the column-block width
     const int force = fe ? std::atoi(fe) : 0;
-    const char *fs = std::getenv("SFM_GJ_SR");  // experiment: 8 row tiles per segment at CB = 8
-    const int want_sr = fs ? std::atoi(fs) : 4;
-    for (int cb : {4, 8}) {
+    for (int cb : {gj::SR, 2 * gj::SR}) {
         if (force && cb != force) continue;
-        const int sr = want_sr == 8 && cb == 8 ? 8 : 4, nseg = (nT + sr - 1) / sr, ncb = (nT + cb - 1) / cb;
+        const int ncb = (nT + cb - 1) / cb;
         if (ncb * nseg <= ncu) {
             g.cb = cb;
-            g.sr = sr;
             g.nseg = nseg;
             g.ncb = ncb;
             break;
@@ -1993,10 +1991,7 @@ static int launch_gj(const GjPlan &g, int nT, int32_t ns, const double *payload,
     a.arrive = b.arrive;
     a.ct = ct;
     a.dbg = gj_dbg_ptr();
-    if (g.sr == 8)
-        hipLaunchKernelGGL(gj::k_gj_solve<8>, dim3(g.grid()), dim3(gj::THREADS), 0, s, a);
-    else
-        hipLaunchKernelGGL(gj::k_gj_solve<4>, dim3(g.grid()), dim3(gj::THREADS), 0, s, a);
+    hipLaunchKernelGGL(gj::k_gj_solve, dim3(g.grid()), dim3(gj::THREADS), 0, s, a);
     SFM_HIP(hipGetLastError());
     return 0;
 }

@@ -27,24 +27,15 @@
 // column block waits for no other workgroup unless its tile row sits in
 // another segment; panels go between workgroups through global memory
 // (write-through stores, one flag per (panel, segment), epoch-tagged).
-// SR = 4 (W0's lanes); SR = 8 (SFM_GJ_SR=8 at CB = 8, a second chain wave)
-// makes the segment of a column block's own rows hold all of its pivots, so
-// the critical path changes workgroup only at a column-block boundary (at
-// SR = 4 < CB = 8 it also moves, one global hop behind, at every segment
-// boundary) -- at the price of 72 tiles per workgroup (TPW = 9 accumulators
-// per update wave: register spills at the 3-waves-per-SIMD budget).
 //
 // Waves of a workgroup (dataflow through LDS words, no workgroup barrier in
 // the loop):
-//   W0  the pivot chain: the DPP tile factor on the diagonal replica with the
-//       segment's row tiles 0..3 of the pivot column on its lanes -> L_p,
-//       1/L_kk, G rows;
-//   W1  (SR = 8) the same chain with row tiles 4..7 (same replica, same bits);
+//   W0  the pivot chain: chol_factor16 on the diagonal replica with the
+//       segment's 64 rows of the pivot column on its lanes -> L_p, G rows;
+//   W1  the same chain with b_p on one lane -> y_p (and publishes L_p, y_p);
 //   WL  loader: polls the flags of remote panels / tiles and stages them;
-//   WP  y_p = L_p^-1 b_p for its own pivots (the forward substitution the
-//       chain used to carry as an extra panel row, same operations), the b
-//       replica of column p+1, and the global copy of its pivots (G rows,
-//       L_p, y_p) with their flags (off the chain waves' path);
+//   WP  publisher: copies this workgroup's pivots (G rows, L_p, y_p) from LDS
+//       to global memory and raises their flags (off the chain waves' path);
 //   U*  update waves: each owns up to TPW tiles in MFMA C-fragment layout
 //       (v_mfma_f64_16x16x4f64: the VALU stays free for the chains) and
 //       applies every panel; the tiles of column p+1 first (phase A, then
@@ -52,12 +43,12 @@
 namespace gj {
 
 constexpr int TL = 16;       // tile
+constexpr int SR = 4;        // row tiles per segment (64 rows: W0's lanes)
 constexpr int CBMAX = 8;     // column tiles per workgroup
 constexpr int NUW = 8;       // update waves
 constexpr int NW = 4 + NUW;  // W0, W1, WL, WP, U0..U7
 constexpr int THREADS = 64 * NW;
-constexpr int NCONS = NUW + 1;  // consumers of a panel's LDS buffers: the update waves and WP
-template <int SR>
+constexpr int NCONS = NUW + 2;  // consumers of a panel's LDS buffers: the update waves, W1 and WP
 constexpr int TPW = ((SR + 1) * CBMAX + NUW - 1) / NUW;  // tile slots per update wave
 constexpr int LDT = TL + 1;                              // padded LDS row (doubles)
 constexpr int NTMAX = 128;                               // tiles per dimension (host checks)
@@ -94,23 +85,19 @@ __device__ __forceinline__ void stamp(const Args &a, int p, int slot) {
         a.dbg[((int64_t)blockIdx.x * (a.nT + 1) + p) * 16 + slot] = __builtin_amdgcn_s_memrealtime();
 }
 
-template <int SR>
 struct Smem {
     // Gm and Gj (adjacent) double as the prologue's staging of the tiles
     double Gm[2][SR][TL][LDT];     // panel p: G rows of the segment's row tiles
     double Gj[2][CBMAX][TL][LDT];  // panel p: G tile of each owned column's row
     double Cst[SR + 1][TL][LDT];   // column p+1 staged for the chain (own tiles | replica)
-    double Ls[2][TL][LDT];         // L_p (the import A_pj = L_p G_j^T, y_p)
-    double dv[2][TL];              // the chain's 1/L_kk of panel p (y_p's scaling)
+    double Ls[2][TL][LDT];         // L_p (the import A_pj = L_p G_j^T)
     double ys[2][TL];
     double bb[CBMAX][TL];          // b replica of each owned column's row tile
     double ob[SR * TL];            // b of the segment's rows (last column block)
-    // = p + 1 when panel p's piece is staged: gm_ok per half of the segment's
-    // rows (W0: tiles 0..3, W1: 4..7), ls_ok L_p and dv, y_ok y_p
-    int gm_ok[2][2], ls_ok[2], y_ok[2], gj_ok[2][CBMAX];
-    int bb_cnt[CBMAX];  // panels applied to each b replica (WP: column p + 1; the replica's update wave: the rest)
+    int gm_ok[2], ly_ok[2], gj_ok[2][CBMAX];  // = p + 1 when panel p's piece is staged
+    int bb_cnt[CBMAX];  // panels applied to each b replica (W1: column p + 1; the replica's update wave: the rest)
     int cst_cnt, cst_read, abort_;
-    int udone[NTMAX];  // per panel: update waves and WP done with it (groups progress at different
+    int udone[NTMAX];  // per panel: update waves and W1 done with it (groups progress at different
                        // rates, so a single running count would not say which panels are done)
     int *err, *bad;  // global: set on an abort (the host reports it, the LM rejects the step)
 };
@@ -134,8 +121,7 @@ __device__ __forceinline__ void lds_add(int *w, int v) {
 }
 __device__ __forceinline__ long long rtc() { return __builtin_amdgcn_s_memrealtime(); }
 
-template <class SM>
-__device__ __forceinline__ void abort_solve(SM &S) {
+__device__ __forceinline__ void abort_solve(Smem &S) {
     lds_set(&S.abort_, 1);
     if ((threadIdx.x & 63) == 0) {
         __hip_atomic_store(S.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -144,8 +130,7 @@ __device__ __forceinline__ void abort_solve(SM &S) {
 }
 
 // wait (whole wave) until the LDS word reaches target; false on abort / timeout
-template <class SM>
-__device__ __forceinline__ bool lds_wait(const int *w, int target, SM &S) {
+__device__ __forceinline__ bool lds_wait(const int *w, int target, Smem &S) {
     if (lds_ld(w) >= target) {  // the common case: no clock read, no sleep
         lds_acquire();
         return true;
@@ -170,8 +155,7 @@ __device__ __forceinline__ bool lds_wait(const int *w, int target, SM &S) {
 
 // wait (whole wave) for a remote publication: flag >= epoch (relaxed agent
 // loads; the producer's stores are write-through and drained before the flag)
-template <class SM>
-__device__ __forceinline__ bool flag_wait(const int *f, int epoch, SM &S) {
+__device__ __forceinline__ bool flag_wait(const int *f, int epoch, Smem &S) {
     if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= epoch) return true;
     long long t0 = -1;
     for (unsigned it = 1;; ++it) {
@@ -230,9 +214,9 @@ __device__ __forceinline__ ElemRef elem_ref(int32_t ns, int I, int J) {
     return r;
 }
 
-template <int SR>
 struct Geo {
     int cb, s, j0, j1, ncol, i0, i1, nrow, nT, nseg, wpg;
+    __device__ int seg_of(int tile) const { return tile / SR; }
     // slot k of update wave u -> owned tile (jj, ii) (ii == SR: the replica),
     // false if none.  The owned columns are grouped by the segment of their
     // tile row (CB / SR groups), each group served by its own waves, so a
@@ -327,112 +311,70 @@ __device__ __forceinline__ void gj_factor16(double (&r)[16], double (&p)[16], do
 
 // -------------------------------------------------------------- the chain
 // W0 / W1: pivot p from the staged column (Cst).  W0 carries the segment's
-// row tiles 0..3, W1 (SR = 8) tiles 4..7; both factor the same replica (same
-// bits).  Only LDS is written here (this workgroup's next pivot waits on
-// it); WP writes the global copy for the other workgroups.
-template <int SR>
-__device__ __forceinline__ bool chain_pivot(const Args &a, const Geo<SR> &g, Smem<SR> &S, int p, int half,
-                                            int lane) {
-    const int li = lane & 15, grp = lane >> 4, buf = p & 1, tr = 4 * half + grp;  // tr: this lane's row tile
+// rows, W1 the b row; both factor the same replica (same bits).  Only LDS
+// is written here (this workgroup's next pivot waits on it); WP writes the
+// global copy for the other workgroups.
+__device__ __forceinline__ bool chain_pivot(const Args &a, const Geo &g, Smem &S, int p, int wave, int lane) {
+    const int li = lane & 15, grp = lane >> 4, buf = p & 1;
     double rw[16], pw[16], dinv[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) rw[j] = S.Cst[SR][li][j];
+    if (wave == 0) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) pw[j] = tr < g.nrow ? S.Cst[tr][li][j] : 0.0;
+        for (int j = 0; j < 16; ++j) pw[j] = grp < g.nrow ? S.Cst[grp][li][j] : 0.0;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) pw[j] = lane == 0 ? S.bb[p - g.j0][j] : 0.0;
+    }
     lds_release();
     if (lane == 0) lds_add(&S.cst_read, 1);  // Cst may be restaged (phase A of panel p)
-    if (half == 0) stamp(a, p, DBG_CST);
+    if (wave == 0) stamp(a, p, DBG_CST);
     gj_factor16(rw, pw, dinv, lane, a.bad);
-    if (half == 0) stamp(a, p, DBG_CHAIN);
+    if (wave == 0) stamp(a, p, DBG_CHAIN);
     // panel p's buffers were last read by the consumers of panel p - 2
     if (p >= 2 && !lds_wait(&S.udone[p - 2], NCONS, S)) return false;
-    if (half == 0) stamp(a, p, DBG_W0BUF);
-    if (tr < g.nrow) {
+    if (wave == 0) {
+        stamp(a, p, DBG_W0BUF);
+        if (grp < g.nrow) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j) S.Gm[buf][tr][li][j] = pw[j];
-        const int tj = g.i0 + tr - g.j0;  // this row tile is an owned column's row: its G tile is local
-        if (tj >= 0 && tj < g.ncol && g.i0 + tr > p)
+            for (int j = 0; j < 16; ++j) S.Gm[buf][grp][li][j] = pw[j];
+            const int tj = g.i0 + grp - g.j0;  // this row tile is an owned column's row: its G tile is local
+            if (tj >= 0 && tj < g.ncol && g.i0 + grp > p)
 #pragma unroll
-            for (int j = 0; j < 16; ++j) S.Gj[buf][tj][li][j] = pw[j];
-    }
-    if (half == 0) {  // L_p (row li of the factored replica) and the pivots' reciprocals
-        if (lane < 16)
+                for (int j = 0; j < 16; ++j) S.Gj[buf][tj][li][j] = pw[j];
+        }
+        lds_release();
+        if (lane == 0) {
+            lds_set(&S.gm_ok[buf], p + 1);
+            for (int gg = 0; gg < g.nrow; ++gg) {
+                const int tj = g.i0 + gg - g.j0;
+                if (tj >= 0 && tj < g.ncol && g.i0 + gg > p) lds_set(&S.gj_ok[buf][tj], p + 1);
+            }
+        }
+        stamp(a, p, DBG_W0LDS);
+    } else {
+        if (lane < 16) {
 #pragma unroll
             for (int j = 0; j < 16; ++j) S.Ls[buf][li][j] = j <= li ? rw[j] : 0.0;
-        if (lane == 0)
-#pragma unroll
-            for (int j = 0; j < 16; ++j) S.dv[buf][j] = dinv[j];
-    }
-    lds_release();
-    if (lane == 0) {
-        lds_set(&S.gm_ok[buf][half], p + 1);
-        if (half == 0) lds_set(&S.ls_ok[buf], p + 1);
-        for (int gg = 4 * half; gg < min(g.nrow, 4 * half + 4); ++gg) {
-            const int tj = g.i0 + gg - g.j0;
-            if (tj >= 0 && tj < g.ncol && g.i0 + gg > p) lds_set(&S.gj_ok[buf][tj], p + 1);
         }
-    }
-    if (half == 0) stamp(a, p, DBG_W0LDS);
-    return true;
-}
-
-template <int SR>
-__device__ __forceinline__ bool rows_staged(Smem<SR> &S, int buf, int p) {
-    return lds_wait(&S.gm_ok[buf][0], p + 1, S) && (SR <= 4 || lds_wait(&S.gm_ok[buf][1], p + 1, S));
-}
-
-// b replica of owned column jj: bb -= G_j y_p (16 lanes, a row each), in
-// panel order (bb_cnt: the panels applied so far), so that every workgroup
-// of the column block holds the same bits
-template <int SR>
-__device__ __forceinline__ bool apply_bb(Smem<SR> &S, int p, int jj, int lane) {
-    const int buf = p & 1;
-    if (!lds_wait(&S.bb_cnt[jj], p, S)) return false;
-    if (lane < 16) {
-        double acc = 0.0;
+        if (lane == 0) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) acc = fma(S.Gj[buf][jj][lane][k], S.ys[buf][k], acc);
-        S.bb[jj][lane] -= acc;
+            for (int j = 0; j < 16; ++j) S.ys[buf][j] = pw[j];
+        }
+        lds_release();
+        if (lane == 0) lds_set(&S.ly_ok[buf], p + 1);
     }
-    lds_release();
-    if (lane == 0) lds_set(&S.bb_cnt[jj], p + 1);
     return true;
 }
 
-__device__ __forceinline__ double readlane_d(double v, int k) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)b, k), hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
-// WP's y_p = L_p^-1 b_p on lanes 0..15 (lane j: row j) is the operations
-// the chain applied to the b row when it rode there as a panel row: y_k =
-// b_k * (1/L_kk from the chain), then b_j = fma(L_jk, -y_k, b_j) for j > k in
-// k order -- the same bits.
-// WP's loop: for its own pivots y_p, then the global copy of the pivot's
-// pieces (write-through stores, read back from LDS so that every store
-// instruction writes contiguous bytes), drained, then the flag; for every
-// panel the b replica of column p + 1 (the next y reads it; the update waves
-// keep the other columns' b replicas)
-template <int SR>
-__device__ __forceinline__ void publisher(const Args &a, const Geo<SR> &g, Smem<SR> &S, int lane) {
-    const int li = lane & 15;
+// WP: the global copy of each own pivot's pieces (write-through stores,
+// read back from LDS so that every store instruction writes contiguous
+// bytes), drained, then the flag; remote panels: nothing to publish
+__device__ __forceinline__ void publisher(const Args &a, const Geo &g, Smem &S, int lane) {
     for (int p = 0; p < g.j1; ++p) {
-        const int buf = p & 1, ja = p + 1 - g.j0;
         if (p >= g.j0) {
-            if (!lds_wait(&S.ls_ok[buf], p + 1, S) || !lds_wait(&S.bb_cnt[p - g.j0], p, S)) return;
-            double v = S.bb[p - g.j0][li], L[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) L[k] = S.Ls[buf][li][k];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const double yk = readlane_d(v, k) * S.dv[buf][k];
-                v = li == k ? yk : li > k ? fma(L[k], -yk, v) : v;
-            }
-            if (lane < 16) S.ys[buf][lane] = v;
-            lds_release();
-            if (lane == 0) lds_set(&S.y_ok[buf], p + 1);
-            if (!rows_staged(S, buf, p)) return;
+            const int buf = p & 1;
+            if (!lds_wait(&S.gm_ok[buf], p + 1, S) || !lds_wait(&S.ly_ok[buf], p + 1, S)) return;
             double *dst = a.Gp + ((int64_t)p * g.nT * TL + g.i0 * TL) * TL;  // the segment's rows: contiguous
             const int nel = g.nrow * TL * TL;
 #pragma unroll
@@ -446,7 +388,7 @@ __device__ __forceinline__ void publisher(const Args &a, const Geo<SR> &g, Smem<
                 const int e = lane + 64 * k;
                 st_ag(dl + e, S.Ls[buf][e >> 4][e & 15]);
             }
-            if (lane < 16) st_ag(a.Yp + ((int64_t)p * g.nseg + g.s) * 16 + lane, v);
+            if (lane < 16) st_ag(a.Yp + ((int64_t)p * g.nseg + g.s) * 16 + lane, S.ys[buf][lane]);
             stamp(a, p, DBG_W0GST);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0) {
@@ -455,8 +397,39 @@ __device__ __forceinline__ void publisher(const Args &a, const Geo<SR> &g, Smem<
                 stamp(a, p, DBG_PUB);
             }
         }
+        if (lane == 0) lds_add(&S.udone[p], 1);
+    }
+}
+
+// b replica of owned column jj: bb -= G_j y_p (16 lanes, a row each), in
+// panel order (bb_cnt: the panels applied so far), so that every workgroup
+// of the column block holds the same bits
+__device__ __forceinline__ bool apply_bb(Smem &S, int p, int jj, int lane) {
+    const int buf = p & 1;
+    if (!lds_wait(&S.bb_cnt[jj], p, S)) return false;
+    if (lane < 16) {
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc = fma(S.Gj[buf][jj][lane][k], S.ys[buf][k], acc);
+        S.bb[jj][lane] -= acc;
+    }
+    lds_release();
+    if (lane == 0) lds_set(&S.bb_cnt[jj], p + 1);
+    return true;
+}
+
+// W1's loop: its own pivots' chain (the b row), and for every panel p the
+// b replica of column p + 1 (the next pivot reads it; the update waves keep
+// the other columns' b replicas)
+__device__ __forceinline__ void w1_loop(const Args &a, const Geo &g, Smem &S, int lane) {
+    for (int p = 0; p < g.j1; ++p) {
+        const int buf = p & 1, ja = p + 1 - g.j0;
+        if (p >= g.j0) {
+            if (!lds_wait(&S.cst_cnt, (p - g.j0 + 1) * (g.nrow + 1), S) || !chain_pivot(a, g, S, p, 1, lane))
+                return;
+        }
         if (ja >= 0 && ja < g.ncol) {
-            if (!lds_wait(&S.y_ok[buf], p + 1, S) || !lds_wait(&S.gj_ok[buf][ja], p + 1, S) ||
+            if (!lds_wait(&S.ly_ok[buf], p + 1, S) || !lds_wait(&S.gj_ok[buf][ja], p + 1, S) ||
                 !apply_bb(S, p, ja, lane))
                 return;
         }
@@ -469,13 +442,11 @@ __device__ __forceinline__ void publisher(const Args &a, const Geo<SR> &g, Smem<
 // ------------------------------------------------------------- the loader
 // Stages remote pieces of panel p, one producing segment at a time: the
 // segment's flag, then every load from it in one round (the segment's own
-// G rows for a remote panel: SR/4 x 16 doubles a lane; the G tiles of the
-// owned columns whose tile row it holds: up to SR tiles, 4 doubles a lane
-// each), then the LDS words.  The segment holding column p+1's tile row goes
-// first.
-template <int SR>
-__device__ __forceinline__ bool load_segment(const Args &a, const Geo<SR> &g, Smem<SR> &S, int p, int sg,
-                                             bool rows, unsigned tiles, int lane) {
+// G rows for a remote panel: 16 doubles a lane; the G tiles of the owned
+// columns whose tile row it holds: up to SR tiles, 16 doubles a lane), then
+// the LDS words.  The segment holding column p+1's tile row goes first.
+__device__ __forceinline__ bool load_segment(const Args &a, const Geo &g, Smem &S, int p, int sg, bool rows,
+                                             unsigned tiles, int lane) {
     const int nsp = g.nT * TL, buf = p & 1;
     if (!flag_wait(a.flag + (int64_t)p * g.nseg + sg, a.epoch, S)) return false;
     stamp(a, p, DBG_LOAD0);
@@ -531,10 +502,8 @@ __device__ __forceinline__ bool load_segment(const Args &a, const Geo<SR> &g, Sm
     stamp(a, p, DBG_LOADED);
     if (lane == 0) {
         if (rows) {
-            lds_set(&S.gm_ok[buf][0], p + 1);
-            lds_set(&S.gm_ok[buf][1], p + 1);
-            lds_set(&S.ls_ok[buf], p + 1);
-            lds_set(&S.y_ok[buf], p + 1);
+            lds_set(&S.gm_ok[buf], p + 1);
+            lds_set(&S.ly_ok[buf], p + 1);
         }
         for (int t = 0; t < SR; ++t)
             if (tiles >> t & 1) lds_set(&S.gj_ok[buf][sg * SR + t - g.j0], p + 1);
@@ -542,13 +511,12 @@ __device__ __forceinline__ bool load_segment(const Args &a, const Geo<SR> &g, Sm
     return true;
 }
 
-template <int SR>
-__device__ __forceinline__ void loader(const Args &a, const Geo<SR> &g, Smem<SR> &S, int lane) {
+__device__ __forceinline__ void loader(const Args &a, const Geo &g, Smem &S, int lane) {
     const int sfirst = g.j0 / SR, slast = (g.j1 - 1) / SR;  // segments of the owned columns' tile rows
     for (int p = 0; p < g.j1; ++p) {
         if (p >= 2 && !lds_wait(&S.udone[p - 2], NCONS, S)) return;  // buffers of panel p - 2 consumed
         const bool remote = p < g.j0;
-        // remote G tiles of the owned columns j > p (our own pivot's tiles in our rows come from W0 / W1)
+        // remote G tiles of the owned columns j > p (our own pivot's tiles in our rows come from W0)
         auto tiles_of = [&](int sg) {
             unsigned m = 0;
             for (int t = 0; t < SR; ++t) {
@@ -563,8 +531,7 @@ __device__ __forceinline__ void loader(const Args &a, const Geo<SR> &g, Smem<SR>
             const bool rows = remote && scrit == g.s;
             if ((m || rows) && !load_segment(a, g, S, p, scrit, rows, m, lane)) return;
         }
-        if (remote && scrit != g.s &&
-            !load_segment(a, g, S, p, g.s, true, sfirst <= g.s && g.s <= slast ? tiles_of(g.s) : 0u, lane))
+        if (remote && scrit != g.s && !load_segment(a, g, S, p, g.s, true, sfirst <= g.s && g.s <= slast ? tiles_of(g.s) : 0u, lane))
             return;
         for (int sg = sfirst; sg <= slast; ++sg) {
             if (sg == scrit || (remote && sg == g.s)) continue;
@@ -575,15 +542,13 @@ __device__ __forceinline__ void loader(const Args &a, const Geo<SR> &g, Smem<SR>
 }
 
 // ------------------------------------------------------------ update waves
-template <int SR>
-__device__ __forceinline__ void store_cst(Smem<SR> &S, int ii, const d4 &acc, int l) {
+__device__ __forceinline__ void store_cst(Smem &S, int ii, const d4 &acc, int l) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) S.Cst[ii][(l >> 4) + 4 * e][l & 15] = acc[e];
 }
 
 // apply panel p to tile (jj, ii) (ii == SR: the diagonal replica)
-template <int SR>
-__device__ __forceinline__ void apply_tile(d4 &acc, const Geo<SR> &g, Smem<SR> &S, int p, int jj, int ii, int l) {
+__device__ __forceinline__ void apply_tile(d4 &acc, const Geo &g, Smem &S, int p, int jj, int ii, int l) {
     const int buf = p & 1, j = g.j0 + jj;
     if (ii == SR) {
         acc = mma16(acc, S.Gj[buf][jj], S.Gj[buf][jj], true, l);
@@ -599,32 +564,17 @@ __device__ __forceinline__ void apply_tile(d4 &acc, const Geo<SR> &g, Smem<SR> &
     acc = mma16(acc, S.Gm[buf][ii], S.Gj[buf][jj], true, l);
 }
 
-template <int SR>
-__device__ __forceinline__ void updater(const Args &a, const Geo<SR> &g, Smem<SR> &S, int u, int lane,
-                                        d4 (&acc)[TPW<SR>], bool track_ob) {
-    const int u0 = u;
+__device__ __forceinline__ void updater(const Args &a, const Geo &g, Smem &S, int u, int lane, d4 (&acc)[TPW], bool track_ob) {
     for (int p = 0; p < g.j1; ++p) {
         const int buf = p & 1;
-        if (!rows_staged(S, buf, p)) return;
-        // the slot maps are recomputed per panel (opaque copy of u): hoisted
-        // out of the loop they would hold TPW tile coordinates in registers
-        int u = u0;
-        asm volatile("" : "+v"(u));
+        if (!lds_wait(&S.gm_ok[buf], p + 1, S)) return;
         if (u == 0) stamp(a, p, DBG_GM);
-        // L_p (a chain wave or the loader): only the import of row p needs it;
-        // y_p (WP or the loader): the b replicas and the segment's b
-        bool ls = false, ys = false, ok = true;
-        auto need_ls = [&]() {
-            if (!ls) {
-                ok = ok && lds_wait(&S.ls_ok[buf], p + 1, S);
-                ls = true;
-            }
-            return ok;
-        };
-        auto need_y = [&]() {
-            if (!ys) {
-                ok = ok && lds_wait(&S.y_ok[buf], p + 1, S);
-                ys = true;
+        // L_p and y_p (W1 or the loader): only the import of row p and the segment's b need them
+        bool ly = false, ok = true;
+        auto need_ly = [&]() {
+            if (!ly) {
+                ok = lds_wait(&S.ly_ok[buf], p + 1, S);
+                ly = true;
             }
             return ok;
         };
@@ -632,20 +582,20 @@ __device__ __forceinline__ void updater(const Args &a, const Geo<SR> &g, Smem<SR
         const int ja = p + 1 - g.j0;
         if (ja >= 0 && ja < g.ncol) {
 #pragma unroll
-            for (int k = 0; k < TPW<SR>; ++k) {
+            for (int k = 0; k < TPW; ++k) {
                 int jj, ii;
                 if (!ok || !g.slot(u, k, jj, ii) || jj != ja) continue;
-                // Cst still holds column p for chain(p) (every chain wave reads it)
+                // Cst still holds column p for chain(p) (both chain waves read it)
                 if (!lds_wait(&S.gj_ok[buf][jj], p + 1, S)) {
                     ok = false;
                     continue;
                 }
                 stamp(a, p, DBG_AGJ);
-                if (p >= g.j0 && !lds_wait(&S.cst_read, (SR / 4) * (p - g.j0 + 1), S)) {
+                if (p >= g.j0 && !lds_wait(&S.cst_read, 2 * (p - g.j0 + 1), S)) {
                     ok = false;
                     continue;
                 }
-                if (ii < SR && g.i0 + ii == p && !need_ls()) continue;
+                if (ii < SR && g.i0 + ii == p && !need_ly()) continue;
                 stamp(a, p, DBG_ACST);
                 apply_tile(acc[k], g, S, p, jj, ii, lane);
                 store_cst(S, ii, acc[k], lane);
@@ -657,27 +607,24 @@ __device__ __forceinline__ void updater(const Args &a, const Geo<SR> &g, Smem<SR
         if (u == 0) stamp(a, p, DBG_PHA);
         // phase B: every other owned column j > p + 1
 #pragma unroll
-        for (int k = 0; k < TPW<SR>; ++k) {
+        for (int k = 0; k < TPW; ++k) {
             int jj, ii;
             if (!ok || !g.slot(u, k, jj, ii) || g.j0 + jj <= p + 1) continue;
             if (!lds_wait(&S.gj_ok[buf][jj], p + 1, S)) {
                 ok = false;
                 continue;
             }
-            if (ii < SR && g.i0 + ii == p && !need_ls()) continue;
+            if (ii < SR && g.i0 + ii == p && !need_ly()) continue;
             apply_tile(acc[k], g, S, p, jj, ii, lane);
-            if (ii == SR && (!need_y() || !apply_bb(S, p, jj, lane))) ok = false;
+            if (ii == SR && (!need_ly() || !apply_bb(S, p, jj, lane))) ok = false;
         }
-        if (track_ob && u == 0 && ok && need_y()) {  // b of the segment's rows: ob_i -= G_i y_p, i != p
+        if (track_ob && u == 0 && ok && need_ly()) {  // b of the segment's rows: ob_i -= G_i y_p, i != p
+            const int ti = lane >> 4;
+            if (ti < g.nrow && g.i0 + ti != p) {
+                double s = 0.0;
 #pragma unroll
-            for (int h = 0; h < SR / 4; ++h) {
-                const int ti = (lane >> 4) + 4 * h;
-                if (ti < g.nrow && g.i0 + ti != p) {
-                    double s = 0.0;
-#pragma unroll
-                    for (int k = 0; k < 16; ++k) s = fma(S.Gm[buf][ti][lane & 15][k], S.ys[buf][k], s);
-                    S.ob[lane + 64 * h] -= s;
-                }
+                for (int k = 0; k < 16; ++k) s = fma(S.Gm[buf][ti][lane & 15][k], S.ys[buf][k], s);
+                S.ob[lane] -= s;
             }
         }
         if (!ok) return;
@@ -786,13 +733,12 @@ __device__ __forceinline__ void final_solve(const double *Lp, double *x, int nse
     if (act) st_ag(x + i * TL + li, v);
 }
 
-template <int SR>
 __global__ void __launch_bounds__(THREADS) k_gj_solve(Args a) {
     if (a.gate && !*a.gate) return;  // device-side LM control: iteration gated off
-    __shared__ Smem<SR> S;
+    __shared__ Smem S;
     stamp(a, a.nT, DBG_START);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    Geo<SR> g;
+    Geo g;
     g.nT = a.nT;
     g.nseg = a.nseg;
     g.cb = blockIdx.x / a.nseg;
@@ -807,8 +753,7 @@ __global__ void __launch_bounds__(THREADS) k_gj_solve(Args a) {
     const bool last_block = g.j1 == a.nT;
     const double lambda = *a.lam;
     // ---- prologue
-    if (threadIdx.x < 4) S.gm_ok[threadIdx.x >> 1][threadIdx.x & 1] = 0;
-    if (threadIdx.x < 2) S.ls_ok[threadIdx.x] = S.y_ok[threadIdx.x] = 0;
+    if (threadIdx.x < 2) S.gm_ok[threadIdx.x] = S.ly_ok[threadIdx.x] = 0;
     if (threadIdx.x < 2 * CBMAX) S.gj_ok[threadIdx.x / CBMAX][threadIdx.x % CBMAX] = 0;
     if (threadIdx.x < CBMAX) S.bb_cnt[threadIdx.x] = 0;
     if (threadIdx.x < NTMAX) S.udone[threadIdx.x] = 0;
@@ -817,20 +762,19 @@ __global__ void __launch_bounds__(THREADS) k_gj_solve(Args a) {
         S.err = a.err;
         S.bad = a.bad;
     }
-    d4 acc[TPW<SR>];
+    d4 acc[TPW];
 #pragma unroll
-    for (int k = 0; k < TPW<SR>; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int k = 0; k < TPW; ++k) acc[k] = d4{0.0, 0.0, 0.0, 0.0};
     const int u = wave - 4;
-    // initial tiles, PC owned columns per pass: every thread gathers up to 7
+    // initial tiles, SR owned columns per pass: every thread gathers up to 8
     // elements from the payload in one round into LDS, then each update wave
     // takes its fragments (column j0's are staged for pivot j0 if j0 == 0)
-    constexpr int PC = 16 / SR;  // columns per pass (4 at SR = 4, 2 at SR = 8)
     double *stage = &S.Gm[0][0][0][0];
-    static_assert(offsetof(Smem<SR>, Gj) == sizeof(S.Gm) &&
-                      sizeof(S.Gm) + sizeof(S.Gj) >= (SR + 1) * PC * TL * LDT * sizeof(double), "staging");
-    constexpr int EPT = ((SR + 1) * PC * 256 + THREADS - 1) / THREADS;
-    for (int c0 = 0; c0 < g.ncol; c0 += PC) {
-        const int nc = min(PC, g.ncol - c0), nel = nc * (SR + 1) * 256;
+    static_assert(offsetof(Smem, Gj) == sizeof(S.Gm) &&
+                      sizeof(S.Gm) + sizeof(S.Gj) >= (SR + 1) * SR * TL * LDT * sizeof(double), "staging");
+    constexpr int EPT = ((SR + 1) * SR * 256 + THREADS - 1) / THREADS;
+    for (int c0 = 0; c0 < g.ncol; c0 += SR) {
+        const int nc = min(SR, g.ncol - c0), nel = nc * (SR + 1) * 256;
         ElemRef er[EPT];
         double v[EPT], dg[EPT];
 #pragma unroll
@@ -855,7 +799,7 @@ __global__ void __launch_bounds__(THREADS) k_gj_solve(Args a) {
         __syncthreads();
         if (u >= 0) {
 #pragma unroll
-            for (int k = 0; k < TPW<SR>; ++k) {
+            for (int k = 0; k < TPW; ++k) {
                 int jj, ii;
                 if (!g.slot(u, k, jj, ii) || jj < c0 || jj >= c0 + nc) continue;
                 const double *tq = stage + ((jj - c0) * (SR + 1) + ii) * TL * LDT;
@@ -866,49 +810,46 @@ __global__ void __launch_bounds__(THREADS) k_gj_solve(Args a) {
         }
         __syncthreads();
     }
-    if (wave == 3) {  // b replicas of the owned columns
+    if (wave == 1) {  // b replicas of the owned columns
         for (int e = lane; e < g.ncol * TL; e += 64) S.bb[e / TL][e % TL] = assembled_b(a.payload, a.ns, g.j0 * TL + e);
     } else if (wave == 2 && last_block) {  // b of the segment's rows
-        for (int e = lane; e < SR * TL; e += 64)
-            S.ob[e] = e / TL < g.nrow ? assembled_b(a.payload, a.ns, g.i0 * TL + e) : 0.0;
+        S.ob[lane] = lane / TL < g.nrow ? assembled_b(a.payload, a.ns, g.i0 * TL + lane) : 0.0;
     }
     if (threadIdx.x == 0) S.cst_cnt = g.j0 == 0 ? g.nrow + 1 : 0;  // else staged by panel j0 - 1
     __syncthreads();
     // ---- the pivot loop, by role
     stamp(a, a.nT, DBG_PROLOGUE);
-    if (wave < SR / 4) {  // W0, and W1 at SR = 8
+    if (wave == 0) {
         for (int p = g.j0; p < g.j1; ++p) {
-            if (!lds_wait(&S.cst_cnt, (p - g.j0 + 1) * (g.nrow + 1), S) || !chain_pivot(a, g, S, p, wave, lane))
-                break;
+            if (!lds_wait(&S.cst_cnt, (p - g.j0 + 1) * (g.nrow + 1), S) || !chain_pivot(a, g, S, p, 0, lane)) break;
             if (lds_ld(&S.abort_)) break;
         }
+    } else if (wave == 1) {
+        w1_loop(a, g, S, lane);
     } else if (wave == 2) {
         loader(a, g, S, lane);
     } else if (wave == 3) {
         publisher(a, g, S, lane);
-    } else if (u >= 0) {
+    } else {
         updater(a, g, S, u, lane, acc, last_block);
     }
     // ---- the solution (last column block) and the epilogue (last arrival)
     if (!last_block) return;
-    __shared__ int last_arrival, fin_ok;
-    if (wave < SR / 4) {  // x of the row tiles 4 * wave .. 4 * wave + 3
-        const bool ok = lds_wait(&S.udone[a.nT - 1], NCONS, S);  // every wave is done with every panel
-        if (wave == 0) stamp(a, a.nT, DBG_FINWAIT);
-        if (ok && g.nrow > 4 * wave)
-            final_solve(a.Lp, a.x, g.nseg, g.s, g.i0 + 4 * wave, g.nrow - 4 * wave, S.ob[lane + 64 * wave], lane);
+    __shared__ int last_arrival;
+    if (wave == 0) {
+        bool ok = lds_wait(&S.udone[a.nT - 1], NCONS, S);  // every wave is done with every panel
+        stamp(a, a.nT, DBG_FINWAIT);
+        if (ok) final_solve(a.Lp, a.x, g.nseg, g.s, g.i0, g.nrow, S.ob[lane], lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (wave == 0) stamp(a, a.nT, DBG_FINSOLVED);
-        if (wave == 0 && lane == 0) fin_ok = ok;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        last_arrival = 0;
-        if (fin_ok && !lds_ld(&S.abort_)) {
-            const unsigned old = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (old == (unsigned)a.nseg - 1) {
-                last_arrival = 1;
-                __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        stamp(a, a.nT, DBG_FINSOLVED);
+        if (lane == 0) {
+            last_arrival = 0;
+            if (ok) {
+                const unsigned old = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (old == (unsigned)a.nseg - 1) {
+                    last_arrival = 1;
+                    __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
         }
     }
@@ -917,7 +858,7 @@ __global__ void __launch_bounds__(THREADS) k_gj_solve(Args a) {
     if (!last_arrival || a.ct.nc <= 0) return;
     double *dc = &S.Gm[0][0][0][0];  // LDS reused: x, then the reductions
     double *red = &S.Gj[0][0][0][0];
-    static_assert(sizeof(S.Gj) >= 3 * NW * sizeof(double), "reduction scratch");
+    static_assert(sizeof(S.Gj) >= 3 * THREADS * sizeof(double), "reduction scratch");
     static_assert(sizeof(S.Gm) >= 6 * (NTMAX * TL / 6) * sizeof(double), "trial step");
     for (int i = threadIdx.x; i < 6 * a.ct.nc; i += THREADS) dc[i] = ld_ag(a.x + i);
     __syncthreads();

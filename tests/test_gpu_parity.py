@@ -877,23 +877,6 @@ def test_reduced_solve(core, monkeypatch, n, solver):
     assert np.array_equal(x, core.reduced_solve(S, b))
 
 
-@pytest.mark.parametrize("n", [300, 600, 1200, 1800])
-def test_reduced_solve_segment_height_bitwise(core, monkeypatch, n):
-    """The persistent Gauss-Jordan solve with 8 row tiles per segment
-    (SFM_GJ_SR=8, column blocks of 8: the critical path changes workgroup
-    only at column-block boundaries) against the default 4-tile segments:
-    every tile sees the same panels in the same order, so x is bitwise the
-    same; both within 1e-11 of LAPACK."""
-    S, b = _spd(n, seed=n + 1)
-    x_ref = np.linalg.solve(S, b)
-    monkeypatch.setenv("SFM_GJ_CB", "8")
-    x4 = core.reduced_solve(S, b)
-    monkeypatch.setenv("SFM_GJ_SR", "8")
-    x8 = core.reduced_solve(S, b)
-    assert np.abs(x8 - x_ref).max() <= 1e-11 * np.abs(x_ref).max()
-    assert np.array_equal(x4, x8)
-
-
 @pytest.mark.parametrize("solver", ["gj", "chol"])
 @pytest.mark.parametrize("n", [40, 300, 1200])
 def test_reduced_solve_not_spd(core, monkeypatch, n, solver):
@@ -937,19 +920,6 @@ def test_ba_sweep_pinhole_matches_general_k(core, monkeypatch):
     c0, x0, r0 = core.ba_lm(*args, max_iterations=30)
     assert (r1["iterations"], r1["accepted"], r1["status"]) == (r0["iterations"], r0["accepted"], r0["status"])
     assert abs(r1["cost"] - r0["cost"]) <= 1e-9 * r0["cost"]
-
-
-def test_ba_gj_segment_height_bitwise_cfg5(core, monkeypatch):
-    """cfg5's LM solve (fixed 6 iterations) with 8-tile GJ segments
-    (SFM_GJ_SR=8) is bitwise the default 4-tile one."""
-    p = syn.ba_problem_cfg("cfg5", dense=False)
-    cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
-    args = (cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K)
-    c4, x4, r4 = core.ba_lm(*args, max_iterations=6, fixed_iterations=True)
-    monkeypatch.setenv("SFM_GJ_SR", "8")
-    c8, x8, r8 = core.ba_lm(*args, max_iterations=6, fixed_iterations=True)
-    assert r4["accepted"] > 0 and (r4["accepted"], r4["cost"]) == (r8["accepted"], r8["cost"])
-    assert np.array_equal(c4, c8) and np.array_equal(x4, x8)
 
 
 @pytest.mark.parametrize("shape,ranks", [("cfg4", 4), ("cfg5", 8)])
