@@ -588,6 +588,7 @@ constexpr int SW_MAX_COLS = SW_THREADS / 2 - 96;  // blocks per spec (2 lanes ea
 constexpr int NXCD = 8;
 constexpr int SLOT_D = 18;  // staged slot (doubles): p (3) | F = G L^T (9, row-major) | G q (3) | X (3)
 constexpr int SW_STAGE_WAVES = 2;  // waves that stage the next chunk (no lane group)
+constexpr int SW_PAIR_WAVES = SW_THREADS / 64 - SW_STAGE_WAVES;  // the lane groups' waves (loaders among them)
 constexpr int SW_STAGE_BATCH = 4;  // slots a staging lane has in flight
 constexpr int SW_MAX_STAGED = 64 * SW_STAGE_WAVES * SW_STAGE_BATCH;  // slots per (chunk, spec): one staging round
 constexpr int SW_STAMP_WG = 4096, SW_STAMP_EV = 68;  // SFM_SWEEP_STAMPS: workgroups, events per wave
@@ -818,6 +819,39 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
+// k_schur_sweep's chunk hand-off: wait (whole wave) until the LDS counter
+// reaches target.  Bounded (200 ms of s_memrealtime): a lost hand-off raises
+// the workgroup's abort word and the global error word (the host reports it)
+// instead of hanging the GPU
+__device__ __forceinline__ bool sw_wait(const int *c, int target, int *abort_w, int *err) {
+    if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        return true;
+    }
+    long long t0 = -1;
+    for (unsigned it = 1;; ++it) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+        if (__hip_atomic_load(abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+        if (it % 1024 == 0) {
+            const long long tn = __builtin_amdgcn_s_memrealtime();
+            if (t0 < 0) t0 = tn;
+            else if (tn - t0 > 20000000) {
+                __hip_atomic_store(abort_w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (err && (threadIdx.x & 63) == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return false;
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    return true;
+}
+// after the wave's LDS writes (and, for a loader, its LDS-DMA: vmcnt first)
+__device__ __forceinline__ void sw_signal(int *c) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 template <int LPP, int NACC>
 __device__ __forceinline__ void sweep_reduce(const double (&acc)[NACC], bool has_acc, int t, int ng,
                                              const SweepGroup *__restrict__ grps, double *__restrict__ slab_r,
@@ -870,7 +904,7 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     const int32_t *__restrict__ spec_cam, const uint32_t *__restrict__ list, const uint32_t *__restrict__ pairs,
     const int32_t *__restrict__ hdr, const double *__restrict__ Xg, const double *__restrict__ Lq,
     const double *__restrict__ Rt, Kmat Km, double *__restrict__ slab, const int *__restrict__ gate, int dbg,
-    int nsweep, CamLinArgs cl, long long *__restrict__ stamps) {
+    int nsweep, CamLinArgs cl, long long *__restrict__ stamps, int *__restrict__ sw_err) {
     extern __shared__ double2 sw_lds[];
     if ((int)blockIdx.x >= nsweep) {  // camera blocks of the normal equations on the CUs the sweep leaves idle
         if (!*cl.glin) return;
@@ -905,6 +939,16 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     const bool diag = grp.flags & 1, second = grp.flags & 2;
     const int bw = L.words();
     double *scam = reinterpret_cast<double *>(ldsw + 2 * bw);  // the spec's cameras (rows 0 and 1)
+    // chunk hand-off counters (dbg bit 16 clear): filled[b] += 1 per producer
+    // wave (two stagers, nload loaders) once its part of a chunk is in buffer
+    // b; freed[b] += 1 per pair wave once it is done with the chunk in b.
+    // Instead of a workgroup barrier per chunk, a pair wave waits only for
+    // its next chunk to be filled and a producer only for its buffer to be
+    // freed, so the per-chunk spread between the lane groups (Poisson pair
+    // counts) averages out over the chunks instead of adding up chunk by chunk
+    int *cnt = reinterpret_cast<int *>(scam + 24);  // filled[2] | freed[2] | abort
+    const bool csync = !(dbg & 16);
+    if (t < 5) cnt[t] = 0;
     if (t < 24) {
         const int c = spec_cam[2 * w + t / 12];
         scam[t] = c >= 0 ? Rt[12 * c + t % 12] : 0.0;
@@ -993,6 +1037,7 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
         load_pts(e1);
         __syncthreads();  // the cameras are in LDS
         if (q0 < q1) commit(e1, n1, ldsw);
+        if (csync) sw_signal(&cnt[0]);
         auto advance = [&]() {  // chunk q+2's points and chunk q+3's list in flight
             load_pts(e2);
 #pragma unroll
@@ -1002,16 +1047,24 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
         advance();
         load_list(q0 + 2, e2, n2);
         stamp(1);
-        lds_barrier();
+        if (!csync) lds_barrier();
         for (int q = q0; q < q1; ++q) {
-            if (q + 1 < q1) commit(e1, n1, ldsw + (((q - q0) & 1) ^ 1) * bw);
+            if (q + 1 < q1) {
+                const int b1 = ((q - q0) & 1) ^ 1;
+                // buffer b1 held chunk q - 1: every pair wave done with it
+                if (!csync || sw_wait(&cnt[2 + b1], ((q + 1 - q0) >> 1) * SW_PAIR_WAVES, &cnt[4], sw_err)) {
+                    commit(e1, n1, ldsw + b1 * bw);
+                    if (csync) sw_signal(&cnt[b1]);
+                }
+            }
             if (q + 2 < q1) {
                 advance();
                 load_list(q + 3, e2, n2);
             }
             stamp(2 + q - q0);
-            lds_barrier();
+            if (!csync) lds_barrier();
         }
+        if (csync) lds_barrier();  // every pair wave is done with the buffers sweep_reduce reuses
         const double none[NACC] = {};  // no accumulators: output tasks only
         sweep_reduce<LPP>(none, false, t, ng, groups + spec_goff[w], slab + (int64_t)r * nbd * ITEM_W,
                           reinterpret_cast<double *>(sw_lds));
@@ -1027,12 +1080,25 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     if (q0 < q1 && loader) sweep_fetch(t, nload, (int64_t)q0 * nspec + w, L, pairs, hdr, ldsw);
     __syncthreads();  // the cameras are in LDS
     stamp(1);
-    __syncthreads();  // chunk q0's slots are staged
+    const int nprod = SW_STAGE_WAVES + nload;  // producer waves of a chunk
+    if (csync) {
+        if (loader && q0 < q1) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA of chunk q0's pairs and header
+            sw_signal(&cnt[0]);
+        }
+    } else {
+        __syncthreads();  // chunk q0's slots are staged
+    }
     for (int q = q0; q < q1; ++q) {
         const int cur = (q - q0) & 1;
         const uint32_t *bufw = ldsw + cur * bw;
-        if (loader && q + 1 < q1) sweep_fetch(t, nload, (int64_t)(q + 1) * nspec + w, L, pairs, hdr, ldsw + (cur ^ 1) * bw);
-        if (gi >= 0) {
+        if (loader && q + 1 < q1) {
+            // buffer cur ^ 1 held chunk q - 1: every pair wave done with it
+            if (!csync || sw_wait(&cnt[2 + (cur ^ 1)], ((q + 1 - q0) >> 1) * SW_PAIR_WAVES, &cnt[4], sw_err))
+                sweep_fetch(t, nload, (int64_t)(q + 1) * nspec + w, L, pairs, hdr, ldsw + (cur ^ 1) * bw);
+        }
+        const bool have = !csync || sw_wait(&cnt[cur], (((q - q0) >> 1) + 1) * nprod, &cnt[4], sw_err);
+        if (gi >= 0 && have) {
             const double2 *buf = reinterpret_cast<const double2 *>(bufw);
             const uint32_t *pl = bufw + L.buf_slots * 2 * SLOT_D;
             const int32_t *hd = reinterpret_cast<const int32_t *>(pl + L.pair_cap / 2);
@@ -1063,11 +1129,19 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
                 }
             }
         }
+        if (csync) {
+            if (loader && q + 1 < q1) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk q + 1's DMA, overlapped with chunk q
+                sw_signal(&cnt[cur ^ 1]);
+            }
+            sw_signal(&cnt[2 + cur]);
+        }
         stamp(2 + q - q0);
-        __syncthreads();  // chunk q's buffer is free; chunk q+1's slots, pairs and header have landed
+        if (!csync) __syncthreads();  // chunk q's buffer is free; chunk q+1's slots, pairs and header have landed
     }
     // reduce the groups' slots in slot order through LDS (the staging
     // buffers are free now)
+    if (csync) lds_barrier();
     sweep_reduce<LPP>(acc, gi >= 0, t, ng, groups + spec_goff[w], slab + (int64_t)r * nbd * ITEM_W,
                       reinterpret_cast<double *>(sw_lds));
     stamp(SW_STAMP_EV - 1);
@@ -2153,7 +2227,8 @@ struct SweepPlan {
     std::vector<uint16_t> pairs;
     std::vector<int2> blkij;
     size_t lds_bytes() const {
-        return (size_t)2 * (buf_slots * SLOT_D * 8 + (size_t)pair_cap * 2 + (size_t)hdr_cap * 4) + 24 * sizeof(double);
+        return (size_t)2 * (buf_slots * SLOT_D * 8 + (size_t)pair_cap * 2 + (size_t)hdr_cap * 4) + 24 * sizeof(double) +
+               16 * sizeof(int);  // + the chunk hand-off counters (SW_SYNC)
     }
 };
 
@@ -2566,6 +2641,7 @@ struct sfm_ba_problem {
     double *d_payload = nullptr, *d_A = nullptr, *d_b = nullptr, *d_D = nullptr;
     double *d_partial = nullptr, *d_scal = nullptr;
     int *d_bad = nullptr;
+    int *d_sw_err = nullptr;  // k_schur_sweep: a chunk hand-off timed out
     unsigned *d_count = nullptr;  // grid_sum_last arrival counters
     unsigned *d_nbig = nullptr;   // gradient_tolerance: point-gradient entries >= gtol
     double *d_gbuf = nullptr;     // gradient_tolerance: [count, g_c (6 nc)]
@@ -2818,7 +2894,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = p->alloc(p->d_D, 2 * 32 * 32)) ||
         (rc = p->alloc(p->d_partial, 4 * (int64_t)p->pt_blocks)) || (rc = p->alloc(p->d_scal, 16)) ||
         (rc = p->alloc(p->d_lm, 2)) ||
-        (rc = p->alloc(p->d_bad, 4)) || (rc = p->alloc(p->d_count, 3 * GS_WORDS)) ||
+        (rc = p->alloc(p->d_bad, 4)) || (rc = p->alloc(p->d_sw_err, 1)) || (rc = p->alloc(p->d_count, 3 * GS_WORDS)) ||
         (rc = p->alloc(p->d_nbig, 1)) || (rc = p->alloc(p->d_gbuf, 6 * (int64_t)nc + 1)))
         return rc;
     p->gjp = p->tb == 16 ? gj_plan(p->nT, device_cus(device)) : GjPlan{};
@@ -3150,13 +3226,13 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SCHUR], s));
     const int nsweep = NXCD * p->sw_nspec * ceil_div(p->sw_nrange, NXCD);
     const bool fused = p->cl_fused && p->ndiag_items;  // + the camera blocks (after an accepted step)
-auto sweep_k = p->sw_lpp == 2 ? k_schur_sweep<2> : p->sw_pinhole ? k_schur_sweep<1, true> : k_schur_sweep<1>;
-hipLaunchKernelGGL(sweep_k, dim3(nsweep + (fused ? p->cl_fused_wg : 0)), dim3(SW_THREADS),
+    auto sweep_k = p->sw_lpp == 2 ? k_schur_sweep<2> : p->sw_pinhole ? k_schur_sweep<1, true> : k_schur_sweep<1>;
+    hipLaunchKernelGGL(sweep_k, dim3(nsweep + (fused ? p->cl_fused_wg : 0)), dim3(SW_THREADS),
                        p->sw_lds_bytes, s, p->sw_nspec, p->sw_nrange, p->sw_nbd, p->sw_L, p->d_sw_rchunk,
                        p->d_sw_nload, p->d_sw_goff, p->d_sw_groups, p->d_sw_lanegrp, p->d_sw_scam,
                        reinterpret_cast<const uint32_t *>(p->d_sw_list), p->d_sw_pairs, p->d_sw_hdr, p->d_X, p->d_Lq,
                        p->d_Rt, p->K, p->d_slab, gst, p->sw_debug, nsweep,
-                       camlin_args(p, true, &p->d_lm[par].run_lin), sw_dbg_ptr());
+                       camlin_args(p, true, &p->d_lm[par].run_lin), sw_dbg_ptr(), p->d_sw_err);
     SFM_HIP(hipGetLastError());
     // one rank: the solve's first launch sums the slabs itself (SlabSrc)
     // (the persistent solve reads the finished payload: the finish runs as its own launch)
@@ -3250,7 +3326,7 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
     // A/B switches (read per solve): DPP tile factor, finish folded into the solve
     p->chol_dpp = env_int("SFM_CHOL_DPP", 1) != 0;
     p->fin_fused = env_int("SFM_FINISH_FUSED", 1) != 0;
-    p->sw_debug = env_int("SFM_SWEEP_DEBUG", 0);
+    p->sw_debug = env_int("SFM_SWEEP_DEBUG", 0) | (env_int("SFM_SWEEP_SYNC", 1) ? 0 : 16);
     (void)hipGetLastError();
     const auto t0 = std::chrono::steady_clock::now();
     for (double &t : p->t_acc) t = 0;
@@ -3269,6 +3345,7 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
     hipLaunchKernelGGL(k_lm_reset, dim3(1), dim3(1), 0, s, p->d_lm, o->initial_lambda, p->d_bad);
     SFM_HIP(hipGetLastError());
     if (p->gjp.cb) SFM_HIP(hipMemsetAsync(p->gjb.err, 0, sizeof(int), s));
+    SFM_HIP(hipMemsetAsync(p->d_sw_err, 0, sizeof(int), s));
     auto account = [&](int j) {  // per-phase event times of iteration j (complete once its state is published)
         const hipEvent_t *e = p->ev_it + (size_t)(j % kEvSlots) * 2 * T_NT;
         for (int k = 0; k < T_NT; ++k) {
@@ -3319,7 +3396,13 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
     int gj_err = 0;
     SFM_HIP(hipMemcpyAsync(&h, p->d_lm + (it & 1), sizeof h, hipMemcpyDeviceToHost, s));
     if (p->gjp.cb) SFM_HIP(hipMemcpyAsync(&gj_err, p->gjb.err, sizeof gj_err, hipMemcpyDeviceToHost, s));
+    int sw_err = 0;
+    SFM_HIP(hipMemcpyAsync(&sw_err, p->d_sw_err, sizeof sw_err, hipMemcpyDeviceToHost, s));
     SFM_HIP(hipStreamSynchronize(s));
+    if (sw_err) {
+        set_error("Schur sweep: a workgroup timed out waiting for a chunk hand-off");
+        return SFM_ERR_HIP;
+    }
     if (gj_err) {
         set_error("reduced camera solve: a workgroup of the persistent solve timed out waiting for a panel");
         return SFM_ERR_HIP;
