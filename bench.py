@@ -295,6 +295,104 @@ def next_rows(core, local_rank, cpu):
     return out
 
 
+def end_to_end_ba(workload):
+    """The drop-in itself, perform_bundle_adjustment (Phase 1/BundleAdjustment.py:113-242),
+    on the reference's dense interface: feature_x / feature_y / flag matrices
+    (n_pts x n_cams) and R / C lists in, optimised R / C lists and points out,
+    run to convergence.  The call is timed whole (host buffers in and out:
+    PCIe and host prep included) and split into its phases
+    (BundleAdjustment.last_timings).  Second of two calls (the first warms the
+    library's thread context)."""
+    import contextlib
+    import io
+    import BundleAdjustment as BA
+    p = syn.ba_problem_cfg(workload, dense=False)
+    n_pts, n_cams = p["n_pts"], p["n_cams"]
+    fx = np.zeros((n_pts, n_cams))
+    fy = np.zeros((n_pts, n_cams))
+    fl = np.zeros((n_pts, n_cams), dtype=np.int64)
+    fx[p["pt_idx"], p["cam_idx"]] = p["obs"][:, 0]
+    fy[p["pt_idx"], p["cam_idx"]] = p["obs"][:, 1]
+    fl[p["pt_idx"], p["cam_idx"]] = 1
+    fwc = np.ones((n_pts, 1), dtype=np.int64)
+    R_set, C_set = list(p["R0"]), list(p["C0"])
+    runs = []
+    for _ in range(2):
+        with contextlib.redirect_stdout(io.StringIO()):
+            t0 = time.perf_counter()
+            BA.perform_bundle_adjustment(p["X0"], fwc, fx, fy, fl, R_set, C_set, K, 0)
+            dt = time.perf_counter() - t0
+        runs.append((dt, dict(BA.last_timings)))
+    del fx, fy, fl
+    dt, tm = runs[-1]
+    its = int(tm.get("iterations", 0))
+    phases = {k: round(v, 3) for k, v in tm.items() if k not in ("iterations", "total")}
+    lib = tm.get("ba_lm", 0.0)
+    phases["ba_lm_wrapper"] = round(lib - tm.get("ba_lm_create", 0) - tm.get("ba_lm_loop", 0)
+                                    - tm.get("ba_lm_download", 0), 3)
+    total = dt * 1e3
+    return {"workload": f"{workload}: perform_bundle_adjustment, dense {n_pts} x {n_cams} feature/flag matrices, "
+                        f"to convergence",
+            "total_ms": round(total, 3), "LM_iterations": its,
+            "LM_it_per_s_end_to_end": round(its / dt, 2) if its else None,
+            "LM_it_per_s_loop_only": round(its / (tm["ba_lm_loop"] * 1e-3), 2) if its and tm.get("ba_lm_loop") else None,
+            "phases_ms": phases,
+            "phase_frac": {k: round(v / total, 4) for k, v in phases.items() if not k.startswith("ba_lm_")
+                           or k == "ba_lm_create"},
+            "note": "phases: observations = dense flags -> COO (np.nonzero over n_pts x n_cams), cams0 = Rotation "
+                    "-> rotvec, r0 = initial residual check on the GPU (scipy's non-finite-x0 error), ba_lm = the "
+                    "C-ABI call (create: host prep + sweep plan + uploads; loop; download), post = rotvec -> R, C"}
+
+
+def shard_local(workload, steps, warmup):
+    """Rank 0's point shard of the workload for N = 2, 4, 8 ranks, run alone
+    on this one GPU through a one-rank RCCL communicator (the multi-rank code
+    path: the Schur finish launch and the all-reduce call are in, the
+    replicated reduced solve too), W warmup + K fixed LM iterations from x0,
+    then the per-kernel split with HIP events on.  Bounds the N-GPU step from
+    below (no xGMI traffic); the all-reduce over xGMI is given as an estimate
+    beside it, labelled so.  The shard's own LM sees a different cost than the
+    full problem, so its accept/reject mix is reported too."""
+    prob = syn.ba_problem_cfg(workload, dense=False)
+    cams0 = np.column_stack([prob["rotvec0"], np.einsum("nij,nj->ni", -prob["R0"], prob["C0"])])
+    comm = core.Comm(core.Comm.unique_id(), 1, 0, device=0)
+    nc = prob["n_cams"]
+    ns = 6 * nc
+    payload_bytes = 8 * (36 * nc * (nc + 1) // 2 + 3 * ns)
+    out = {"workload": workload, "payload_bytes": payload_bytes}
+    try:
+        for n in (1, 2, 4, 8):
+            ci, pi, ob, X0, (lo, hi) = sfm_dist.shard_ba(prob["cam_idx"], prob["pt_idx"], prob["obs"],
+                                                         prob["X0"], n, 0)
+            ba = core.BAProblem(cams0, X0, ci, pi, ob, K, comm=comm)
+            ba.solve(max_iterations=warmup, fixed_iterations=True)
+            ba.reset()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            rep = ba.solve(max_iterations=steps, fixed_iterations=True)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            ba.reset()
+            ba.set_timing(True)
+            ba.solve(max_iterations=steps, fixed_iterations=True)
+            kt = ba.kernel_times()
+            ba.close()
+            # ring all-reduce estimate over xGMI (NOT measured): 2 (N-1)/N of the
+            # payload at an assumed 300 GB/s bus bandwidth + 15 us latency
+            est = (15e-3 + 2 * (n - 1) / n * payload_bytes / 300e9 * 1e3) if n > 1 else 0.0
+            ms = dt / steps * 1e3
+            out[str(n)] = {"ms_per_step": round(ms, 4), "accepted": rep["accepted"], "n_pts_local": len(X0),
+                           "n_obs_local": len(ci), "kernels_ms": {k: round(v, 4) for k, v in kt.items()},
+                           "allreduce_ms_estimate": round(est, 4),
+                           "ms_per_step_bound": round(ms + est, 4),
+                           "LM_it_per_s_bound": round(1e3 / (ms + est), 2)}
+    finally:
+        comm.close()
+    out["note"] = ("rank-0 shard alone on one GPU (1-rank RCCL communicator); ms_per_step_bound = measured + "
+                   "all-reduce ESTIMATE (2(N-1)/N x payload / 300 GB/s + 15 us, not measured)")
+    return out
+
+
 def ransac_leg(args, world, rank, local_rank, comm):
     """RANSAC on config 2 (5000 correspondences, 40 % outliers, H = 16384).
     Without a communicator: the drop-in's whole call (in-call sampling from
@@ -458,6 +556,7 @@ def ba_record(leg, args, world):
                      "converged_solve": {"iterations": conv["iterations"], "accepted": conv["accepted"],
                                          "loop_ms": round(conv["t_loop_ms"], 3),
                                          "ms_per_iteration": round(conv["t_loop_ms"] / max(1, conv["iterations"]), 4)}},
+        "converged_LM_it_per_s": round(conv["iterations"] / (conv["t_loop_ms"] * 1e-3), 2) if conv["t_loop_ms"] else None,
         "rmse": {f"{workload}_initial": round(syn.rmse_from_cost(conv["cost0"], n_obs_total), 6),
                  f"{workload}_gpu": round(syn.rmse_from_cost(conv["cost"], n_obs_total), 6),
                  "lm_iterations": conv["iterations"]},
@@ -476,6 +575,8 @@ def main():
     ap.add_argument("--ransac-hyps", type=int, default=16384)
     ap.add_argument("--force-comm", action="store_true", help="use the RCCL communicator even with one rank")
     ap.add_argument("--no-next-rows", action="store_true", help="skip the SURVEY §8(f) row measurements")
+    ap.add_argument("--no-end-to-end", action="store_true", help="skip the dense perform_bundle_adjustment call")
+    ap.add_argument("--no-shard-local", action="store_true", help="skip the per-rank shard bound")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -512,6 +613,14 @@ def main():
     if second:
         legs.append(ba_leg(second, args, world, rank, local_rank, comm, barrier, allmax))
 
+    # ---------------- the drop-in end to end, and the per-rank shard bound (N = 1 only)
+    e2e, shards = {}, None
+    if world == 1 and not args.no_end_to_end:
+        for wl in [args.workload] + ([second] if second else []):
+            e2e[wl] = end_to_end_ba(wl)
+    if world == 1 and not args.no_shard_local:
+        shards = shard_local(args.workload, args.steps, args.warmup)
+
     # ---------------- RANSAC (config 2)
     ransac, (x1, x2, samples) = ransac_leg(args, world, rank, local_rank, comm)
     if comm is not None:
@@ -543,11 +652,18 @@ def main():
         "kernels_ms_per_iter": head["kernels_ms_per_iter"],
         "pmc_bytes_per_iter": head["pmc_bytes_per_iter"],
         "step_mix": head["step_mix"],
+        "converged_LM_it_per_s": head["converged_LM_it_per_s"],
         "rmse": head["rmse"],
         "ransac": ransac,
     }
     if second:
         out[second] = ba_record(legs[1], args, world)
+    if args.workload in e2e:
+        out["end_to_end"] = e2e[args.workload]
+    if second in e2e:
+        out[second]["end_to_end"] = e2e[second]
+    if shards:
+        out["shard_local"] = shards
     if world == 1:
         out["rmse"].update(cfg3_rmse_vs_reference())
     cpu_leg = world == 1 and not args.no_cpu_baseline

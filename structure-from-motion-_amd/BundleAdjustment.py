@@ -13,6 +13,8 @@ The reference's scipy call stops at max_nfev=100 and, for any problem with
 the drop-in's result is never worse than that and matches the converged
 least-squares solution (tests/test_gpu_parity.py).
 """
+import time
+
 import numpy as np
 from scipy.spatial.transform import Rotation
 
@@ -58,6 +60,15 @@ def bundle_adjustment_residuals(params, n_cameras, n_points, camera_indices, poi
     points_3d = params[n_cameras * n_cam_params:].reshape(n_points, 3)
     return _core.ba_residuals(camera_params, points_3d, camera_indices, point_indices,
                               np.asarray(points_2d).reshape(-1, 2), K)
+
+
+# Wall-time split of the last perform_bundle_adjustment(_coo) call, in ms
+# (measurement only; bench.py reports it as the drop-in's end-to-end time):
+# observations (dense flags -> COO), cams0 (Rotation -> rotvec), r0 (the
+# initial residual check on the GPU), ba_lm (the library call: create = host
+# prep + plan + upload, loop, download, and the wrapper's copies), post
+# (rotvec -> R, C and the point copy), total.
+last_timings = {}
 
 
 def _observations(filtered_world_coords, feature_x, feature_y, filtered_feature_flags, n_cameras):
@@ -110,12 +121,17 @@ def perform_bundle_adjustment(all_world_coords, filtered_world_coords, feature_x
     all_world_coords_opt : numpy.ndarray
         Optimized 3D points
     """
+    t0 = time.perf_counter()
     valid_point_indices = np.where(np.asarray(filtered_world_coords).flatten() == 1)[0]
     if len(valid_point_indices) == 0:  # :152-153
         return R_set, C_set, all_world_coords
     obs = _observations(filtered_world_coords, feature_x, feature_y, filtered_feature_flags, len(R_set))
-    return _adjust(all_world_coords, obs, R_set, C_set, K, max_iterations, function_tolerance,
-                   parameter_tolerance, initial_lambda)
+    t_obs = (time.perf_counter() - t0) * 1e3
+    out = _adjust(all_world_coords, obs, R_set, C_set, K, max_iterations, function_tolerance,
+                  parameter_tolerance, initial_lambda)
+    last_timings["observations"] = t_obs
+    last_timings["total"] = (time.perf_counter() - t0) * 1e3
+    return out
 
 
 def perform_bundle_adjustment_coo(all_world_coords, filtered_world_coords, store, R_set, C_set, K, *,
@@ -125,12 +141,17 @@ def perform_bundle_adjustment_coo(all_world_coords, filtered_world_coords, store
     plays filtered_feature_flags) instead of dense n_features x n_images
     matrices; same observations, order, solver, prints and failure
     behaviour."""
+    t0 = time.perf_counter()
     valid_point_indices = np.where(np.asarray(filtered_world_coords).flatten() == 1)[0]
     if len(valid_point_indices) == 0:
         return R_set, C_set, all_world_coords
     obs = store.observations(filtered_world_coords, len(R_set))
-    return _adjust(all_world_coords, obs, R_set, C_set, K, max_iterations, function_tolerance,
-                   parameter_tolerance, initial_lambda)
+    t_obs = (time.perf_counter() - t0) * 1e3
+    out = _adjust(all_world_coords, obs, R_set, C_set, K, max_iterations, function_tolerance,
+                  parameter_tolerance, initial_lambda)
+    last_timings["observations"] = t_obs
+    last_timings["total"] = (time.perf_counter() - t0) * 1e3
+    return out
 
 
 def _adjust(all_world_coords, obs, R_set, C_set, K, max_iterations, function_tolerance, parameter_tolerance,
@@ -139,8 +160,10 @@ def _adjust(all_world_coords, obs, R_set, C_set, K, max_iterations, function_tol
     valid_point_indices, camera_indices, point_indices, points_2d = obs
     n_cameras = len(R_set)
     n_points = len(valid_point_indices)
+    last_timings.clear()
     if len(camera_indices) == 0:  # :171-172
         return R_set, C_set, all_world_coords
+    t0 = time.perf_counter()
     cams0 = np.zeros((n_cameras, 6))
     for i in range(n_cameras):  # :183-193
         R = np.array(R_set[i])
@@ -148,18 +171,26 @@ def _adjust(all_world_coords, obs, R_set, C_set, K, max_iterations, function_tol
         cams0[i, :3] = Rotation.from_matrix(R).as_rotvec()
         cams0[i, 3:] = -R @ C
     pts0 = np.asarray(all_world_coords, dtype=np.float64)[valid_point_indices]
+    t1 = time.perf_counter()
+    last_timings["cams0"] = (t1 - t0) * 1e3
     print(f"  Bundle adjustment: {n_cameras} cameras, {n_points} points, {len(camera_indices)} observations")
     _core.require_device()  # a missing GPU is an error, never a silent "failed"
     try:
         if 2 * len(camera_indices) < 6 * n_cameras + 3 * n_points:  # scipy least_squares.py:850-852
             raise ValueError("Method 'lm' doesn't work when the number of residuals is less than the "
                              "number of variables.")
+        t2 = time.perf_counter()
         r0 = _core.ba_residuals(cams0, pts0, camera_indices, point_indices, points_2d, K)
         if not np.all(np.isfinite(r0)):  # least_squares.py:843-845
             raise ValueError("Residuals are not finite in the initial point.")
+        t3 = time.perf_counter()
         cams, pts, rep = _core.ba_lm(cams0, pts0, camera_indices, point_indices, points_2d, K,
                                      max_iterations=max_iterations, function_tolerance=function_tolerance,
                                      parameter_tolerance=parameter_tolerance, initial_lambda=initial_lambda)
+        t4 = time.perf_counter()
+        last_timings.update(r0=(t3 - t2) * 1e3, ba_lm=(t4 - t3) * 1e3, ba_lm_create=rep["t_setup_ms"],
+                            ba_lm_loop=rep["t_loop_ms"], ba_lm_download=rep["t_download_ms"],
+                            iterations=rep["iterations"])
         R_set_opt = []
         C_set_opt = []
         for i in range(n_cameras):  # :220-228
@@ -169,6 +200,7 @@ def _adjust(all_world_coords, obs, R_set, C_set, K, max_iterations, function_tol
             C_set_opt.append(C_opt)
         all_world_coords_opt = all_world_coords.copy()  # :231-234
         all_world_coords_opt[valid_point_indices] = pts
+        last_timings["post"] = (time.perf_counter() - t4) * 1e3
         print(f"  Bundle adjustment completed. Final cost: {rep['cost']:.6f}")
         return R_set_opt, C_set_opt, all_world_coords_opt
     except Exception as e:

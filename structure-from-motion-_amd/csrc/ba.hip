@@ -1695,7 +1695,8 @@ struct CamTrialArgs {  // k_chol_backsolve's epilogue (nc = 0: none)
     double *Rt_new, *cam_out;
 };
 
-#include "gj_solve.hpp"  // the persistent block Gauss-Jordan solve (one launch)
+#include "gj_solve.hpp"   // the persistent block Gauss-Jordan solve (one launch), segment layout
+#include "gjr_solve.hpp"  // ... and its row-distributed form (default since round 4)
 
 template <int TB>
 __global__ void __launch_bounds__(SOLVE_THREADS) k_chol_backsolve(double *__restrict__ A, int32_t nsp,
@@ -2066,6 +2067,81 @@ static int launch_gj(const GjPlan &g, int nT, int32_t ns, const double *payload,
     a.ct = ct;
     a.dbg = gj_dbg_ptr();
     hipLaunchKernelGGL(gj::k_gj_solve, dim3(g.grid()), dim3(gj::THREADS), 0, s, a);
+    SFM_HIP(hipGetLastError());
+    return 0;
+}
+
+// Row-distributed persistent solve (gjr_solve.hpp): one workgroup per tile
+// row, all resident at once (every wait is bounded, and the host checks the
+// occupancy against the grid).  tpw = 0: not applicable, the segment layout
+// above (or the Cholesky) runs instead; SFM_SOLVE=gjseg / chol force those.
+struct GjrPlan {
+    int nT = 0, tpw = 0;
+    bool ok() const { return tpw > 0; }
+};
+template <int TPW>
+static bool gjr_resident(int nT, int ncu) {
+    static int nb = -1;  // resident workgroups per CU (queried once per instantiation)
+    if (nb < 0) {
+        nb = 0;
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&gjr::k_gjr_solve<TPW>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, gjr::DYN_LDS) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gjr::k_gjr_solve<TPW>, gjr::THREADS, gjr::DYN_LDS) !=
+                hipSuccess)
+            nb = 0;
+        (void)hipGetLastError();
+    }
+    return nb >= 1 && nT <= nb * ncu;
+}
+static GjrPlan gjr_plan(int nT, int ncu) {
+    GjrPlan g;
+    if (const char *e = std::getenv("SFM_SOLVE"))
+        if (std::strcmp(e, "chol") == 0 || std::strcmp(e, "gjseg") == 0) return g;
+    // tile slots per U wave (a compile-time register array): up to 28 / 77 tile
+    // rows (more would spill: the segment layout takes those)
+    if (nT < 1 || nT > 11 * gjr::NUW || nT > ncu) return g;
+    const int tpw = nT <= 4 * gjr::NUW ? 4 : 11;
+    const bool res = tpw == 4 ? gjr_resident<4>(nT, ncu) : gjr_resident<11>(nT, ncu);
+    if (!res) return g;
+    g.nT = nT;
+    g.tpw = tpw;
+    return g;
+}
+// granule records (zeroed once; tags only grow) and the err / arrival words
+struct GjrBufs {
+    gjr::u64 *P = nullptr, *G = nullptr;
+    int *err = nullptr;
+    unsigned *arrive = nullptr;
+    static size_t words(int nT) { return ((size_t)nT * gjr::PBYTES + (size_t)nT * nT * gjr::GBYTES) / 8; }
+    static constexpr size_t ints = 64;
+    void carve(gjr::u64 *w, int *i, int nT) {
+        P = w;
+        G = w + (size_t)nT * gjr::PBYTES / 8;
+        err = i;
+        arrive = reinterpret_cast<unsigned *>(i + 32);
+    }
+};
+static int launch_gjr(const GjrPlan &g, int32_t ns, const double *payload, const double *lam, const GjrBufs &b,
+                      unsigned tag, double *x, int *bad, const int *gate, const CamTrialArgs &ct, hipStream_t s) {
+    gjr::Args a;
+    a.payload = payload;
+    a.ns = ns;
+    a.nT = g.nT;
+    a.lam = lam;
+    a.gate = gate;
+    a.P = b.P;
+    a.G = b.G;
+    a.tag = tag;
+    a.x = x;
+    a.bad = bad;
+    a.err = b.err;
+    a.arrive = b.arrive;
+    a.ct = ct;
+    a.dbg = gj_dbg_ptr();
+    switch (g.tpw) {
+    case 4: hipLaunchKernelGGL(gjr::k_gjr_solve<4>, dim3(g.nT), dim3(gjr::THREADS), gjr::DYN_LDS, s, a); break;
+    default: hipLaunchKernelGGL(gjr::k_gjr_solve<11>, dim3(g.nT), dim3(gjr::THREADS), gjr::DYN_LDS, s, a); break;
+    }
     SFM_HIP(hipGetLastError());
     return 0;
 }
@@ -2657,6 +2733,9 @@ struct sfm_ba_problem {
     GjPlan gjp;
     GjBufs gjb;
     int gj_epoch = 0;
+    GjrPlan gjrp;  // the row-distributed solve (default; gjp is then unused)
+    GjrBufs gjrb;
+    unsigned gjr_tag = 0;
     hipEvent_t ev_solve = nullptr;
     double t_acc[T_NT] = {};
     int t_iters = 0;
@@ -2897,7 +2976,18 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = p->alloc(p->d_bad, 4)) || (rc = p->alloc(p->d_sw_err, 1)) || (rc = p->alloc(p->d_count, 3 * GS_WORDS)) ||
         (rc = p->alloc(p->d_nbig, 1)) || (rc = p->alloc(p->d_gbuf, 6 * (int64_t)nc + 1)))
         return rc;
-    p->gjp = p->tb == 16 ? gj_plan(p->nT, device_cus(device)) : GjPlan{};
+    p->gjrp = p->tb == 16 ? gjr_plan(p->nT, device_cus(device)) : GjrPlan{};
+    p->gjp = p->tb == 16 && !p->gjrp.ok() ? gj_plan(p->nT, device_cus(device)) : GjPlan{};
+    if (p->gjrp.ok()) {
+        gjr::u64 *gw = nullptr;
+        int *gi = nullptr;
+        if ((rc = p->alloc(gw, (int64_t)GjrBufs::words(p->nT))) || (rc = p->alloc(gi, (int64_t)GjrBufs::ints)))
+            return rc;
+        p->gjrb.carve(gw, gi, p->nT);
+        SFM_HIP(hipMemsetAsync(gw, 0, GjrBufs::words(p->nT) * sizeof(gjr::u64), p->stream));
+        SFM_HIP(hipMemsetAsync(gi, 0, GjrBufs::ints * sizeof(int), p->stream));
+        SFM_HIP(hipEventCreateWithFlags(&p->ev_solve, hipEventDisableTiming));
+    }
     if (p->gjp.cb) {
         double *gd = nullptr;
         int *gi = nullptr;
@@ -3088,22 +3178,24 @@ extern "C" int sfm_ransac_combine(sfm_comm *c, uint64_t *key, double *model) {
         }
         return 0;
     }
-    // RCCL: also with a single rank (in-place no-ops), so one-GPU runs
-    // exercise the transport.  Device scratch [key (u64) | model (9 f64)]
-    // and a stream are kept on the communicator.
+    // RCCL: also with a single rank, so one-GPU runs exercise the transport.
+    // ONE all-gather of every rank's [key (u64 bits) | model (9 f64)] record,
+    // entered by every rank whatever happened locally (a rank whose upload
+    // fails contributes the neutral key 0 and reports its error after it):
+    // no collective depends on a value read back on one rank only, so no
+    // rank can skip one its peers are in.  Each rank then picks the largest
+    // key (the reference's strict-> winner: max count, earliest iteration;
+    // the ranges are disjoint, so keys of different ranks never tie unless
+    // 0) and takes that rank's model bit for bit (-0.0 included): a copy,
+    // not a sum.
     SFM_HIP(hipSetDevice(c->device));
+    constexpr int REC = 10;
     if (!c->scratch) {
-        SFM_HIP(hipMalloc(&c->scratch, 96));
+        SFM_HIP(hipMalloc(&c->scratch, sizeof(double) * REC * (c->nranks + 1)));
         SFM_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     }
-    void *d = c->scratch;
+    double *dmine = static_cast<double *>(c->scratch), *dall = dmine + REC;
     hipStream_t s = c->stream;
-    // Every rank enters every collective, whatever happened locally: a rank
-    // whose copies fail contributes the neutral value (key 0, owner -1) and
-    // reports its error after the collectives, so no peer is left waiting.
-    // The model travels by broadcast from the winning rank (found by a second
-    // max-reduce of the owner), so the winner's F arrives bit for bit (-0.0
-    // included), not as a sum.
     int rc = 0;
     auto hip_ok = [&](hipError_t e) {
         if (e != hipSuccess && !rc) {
@@ -3112,41 +3204,34 @@ extern "C" int sfm_ransac_combine(sfm_comm *c, uint64_t *key, double *model) {
         }
         return e == hipSuccess;
     };
-    auto nccl_ok = [&](ncclResult_t r, const char *what) {
-        if (r != ncclSuccess) {
-            set_error("%s: %s", what, ncclGetErrorString(r));
-            rc = SFM_ERR_COMM;
-        }
-        return r == ncclSuccess;
-    };
-    uint64_t *dkey = static_cast<uint64_t *>(d);
-    double *dm = reinterpret_cast<double *>(static_cast<char *>(d) + 8);
-    int32_t *downer = reinterpret_cast<int32_t *>(static_cast<char *>(d) + 80);
-    const uint64_t mykey = *key;
-    if (!hip_ok(hipMemcpyAsync(dkey, &mykey, 8, hipMemcpyHostToDevice, s))) (void)hipMemsetAsync(dkey, 0, 8, s);
-    if (!nccl_ok(ncclAllReduce(dkey, dkey, 1, ncclUint64, ncclMax, c->comm, s), "ncclAllReduce(max key)")) return rc;
-    uint64_t gkey = 0;
-    if (!hip_ok(hipMemcpyAsync(&gkey, dkey, 8, hipMemcpyDeviceToHost, s)) || !hip_ok(hipStreamSynchronize(s))) gkey = 0;
-    const int32_t mine = (gkey != 0 && mykey == gkey && !rc) ? c->rank : -1;
-    if (!hip_ok(hipMemcpyAsync(downer, &mine, 4, hipMemcpyHostToDevice, s))) (void)hipMemsetAsync(downer, 0xff, 4, s);
-    if (!nccl_ok(ncclAllReduce(downer, downer, 1, ncclInt32, ncclMax, c->comm, s), "ncclAllReduce(max owner)"))
-        return rc;
-    int32_t owner = -1;
-    if (!hip_ok(hipMemcpyAsync(&owner, downer, 4, hipMemcpyDeviceToHost, s)) || !hip_ok(hipStreamSynchronize(s)))
-        owner = -1;
-    // every rank read the same owner (or every rank failed the same read): the broadcast is entered uniformly
-    if (owner >= 0) {
-        if (c->rank == owner) hip_ok(hipMemcpyAsync(dm, model, 72, hipMemcpyHostToDevice, s));
-        if (!nccl_ok(ncclBroadcast(dm, dm, 9, ncclDouble, owner, c->comm, s), "ncclBroadcast(model)")) return rc;
-        double m[9];
-        if (hip_ok(hipMemcpyAsync(m, dm, 72, hipMemcpyDeviceToHost, s)) && hip_ok(hipStreamSynchronize(s)) && !rc)
-            std::memcpy(model, m, 72);
-    } else if (gkey != 0 && !rc) {
-        set_error("ransac combine: no rank owns the winning key");
-        rc = SFM_ERR_COMM;
+    double h[REC];
+    std::memcpy(&h[0], key, 8);
+    std::memcpy(&h[1], model, 72);
+    if (!hip_ok(hipMemcpyAsync(dmine, h, sizeof h, hipMemcpyHostToDevice, s)) || !hip_ok(hipStreamSynchronize(s)))
+        (void)hipMemsetAsync(dmine, 0, sizeof h, s);
+    const ncclResult_t nr = ncclAllGather(dmine, dall, REC, ncclDouble, c->comm, s);
+    if (nr != ncclSuccess) {
+        set_error("ncclAllGather(ransac keys): %s", ncclGetErrorString(nr));
+        return SFM_ERR_COMM;
     }
-    if (!rc) *key = gkey;
-    return rc;
+    std::vector<double> all((size_t)REC * c->nranks);
+    if (!hip_ok(hipMemcpyAsync(all.data(), dall, all.size() * sizeof(double), hipMemcpyDeviceToHost, s)) ||
+        !hip_ok(hipStreamSynchronize(s)))
+        return rc;
+    uint64_t best = 0;
+    int owner = -1;
+    for (int r = 0; r < c->nranks; ++r) {
+        uint64_t k;
+        std::memcpy(&k, &all[(size_t)REC * r], 8);
+        if (k > best) {
+            best = k;
+            owner = r;
+        }
+    }
+    if (rc) return rc;
+    if (owner >= 0) std::memcpy(model, &all[(size_t)REC * owner + 1], 72);
+    *key = best;
+    return 0;
 }
 
 static int allreduce(sfm_ba_problem *p, double *buf, int64_t n) {
@@ -3236,7 +3321,7 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     SFM_HIP(hipGetLastError());
     // one rank: the solve's first launch sums the slabs itself (SlabSrc)
     // (the persistent solve reads the finished payload: the finish runs as its own launch)
-    const bool fin_fused = !p->comm && p->fin_fused && !p->gjp.cb;
+    const bool fin_fused = !p->comm && p->fin_fused && !p->gjp.cb && !p->gjrp.ok();
     if (!fin_fused) {
         hipLaunchKernelGGL(k_schur_finish, dim3(p->sw_nbd), dim3(64), 0, s, p->ns, p->sw_nbd, p->sw_nrange,
                            p->d_sw_blkij, p->d_slab, p->d_camlin, p->d_payload, gst);
@@ -3251,15 +3336,18 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     const CamTrialArgs ct = {p->nc, p->ns, p->d_payload, lam, p->d_Rt, p->d_Rt2, p->d_scal + 4};
     const SlabSrc src = fin_fused ? SlabSrc{p->d_slab, p->d_camlin, p->sw_nbd, p->sw_nrange}
                                   : SlabSrc{nullptr, nullptr, 0, 0};
-    if (p->gjp.cb) {
+    if (p->gjp.cb || p->gjrp.ok()) {
         LocalGroup *lg = p->comm ? p->comm->local : nullptr;
         std::unique_lock<std::mutex> lk;
         if (lg) {  // in-process ranks on one GPU: one persistent solve at a time
             lk = std::unique_lock<std::mutex>(lg->solve_mu);
             if (lg->last_solve) SFM_HIP(hipStreamWaitEvent(s, lg->last_solve, 0));
         }
-        if ((rc = launch_gj(p->gjp, p->nT, p->ns, p->d_payload, lam, p->gjb, ++p->gj_epoch, p->d_b, bad, gst,
-                            ct, s)))
+        if (p->gjrp.ok()) {
+            if ((rc = launch_gjr(p->gjrp, p->ns, p->d_payload, lam, p->gjrb, ++p->gjr_tag, p->d_b, bad, gst, ct, s)))
+                return rc;
+        } else if ((rc = launch_gj(p->gjp, p->nT, p->ns, p->d_payload, lam, p->gjb, ++p->gj_epoch, p->d_b, bad,
+                                   gst, ct, s)))
             return rc;
         if (lg) {
             SFM_HIP(hipEventRecord(p->ev_solve, s));
@@ -3344,7 +3432,13 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
     for (int k = 0; k < kHostRing; ++k) __atomic_store_n(&p->h_ring[k].seq, 0, __ATOMIC_RELAXED);
     hipLaunchKernelGGL(k_lm_reset, dim3(1), dim3(1), 0, s, p->d_lm, o->initial_lambda, p->d_bad);
     SFM_HIP(hipGetLastError());
-    if (p->gjp.cb) SFM_HIP(hipMemsetAsync(p->gjb.err, 0, sizeof(int), s));
+    // the persistent solves' error and arrival words start clean every solve
+    // (an aborted launch may have left an arrival count behind)
+    if (p->gjp.cb) {
+        SFM_HIP(hipMemsetAsync(p->gjb.err, 0, sizeof(int), s));
+        SFM_HIP(hipMemsetAsync(p->gjb.arrive, 0, sizeof(unsigned), s));
+    }
+    if (p->gjrp.ok()) SFM_HIP(hipMemsetAsync(p->gjrb.err, 0, GjrBufs::ints * sizeof(int), s));
     SFM_HIP(hipMemsetAsync(p->d_sw_err, 0, sizeof(int), s));
     auto account = [&](int j) {  // per-phase event times of iteration j (complete once its state is published)
         const hipEvent_t *e = p->ev_it + (size_t)(j % kEvSlots) * 2 * T_NT;
@@ -3396,6 +3490,7 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
     int gj_err = 0;
     SFM_HIP(hipMemcpyAsync(&h, p->d_lm + (it & 1), sizeof h, hipMemcpyDeviceToHost, s));
     if (p->gjp.cb) SFM_HIP(hipMemcpyAsync(&gj_err, p->gjb.err, sizeof gj_err, hipMemcpyDeviceToHost, s));
+    if (p->gjrp.ok()) SFM_HIP(hipMemcpyAsync(&gj_err, p->gjrb.err, sizeof gj_err, hipMemcpyDeviceToHost, s));
     int sw_err = 0;
     SFM_HIP(hipMemcpyAsync(&sw_err, p->d_sw_err, sizeof sw_err, hipMemcpyDeviceToHost, s));
     SFM_HIP(hipStreamSynchronize(s));
@@ -3449,7 +3544,8 @@ extern "C" int sfm_reduced_solve(const double *S, const double *rhs, int32_t n, 
     if (!c) return SFM_ERR_HIP;
     const int tb = chol_tile(n);
     const int32_t nsp = (n + tb - 1) / tb * tb;
-    const GjPlan gjp = tb == 16 ? gj_plan(nsp / 16, device_cus(device)) : GjPlan{};
+    const GjrPlan gjrp = tb == 16 ? gjr_plan(nsp / 16, device_cus(device)) : GjrPlan{};
+    const GjPlan gjp = tb == 16 && !gjrp.ok() ? gj_plan(nsp / 16, device_cus(device)) : GjPlan{};
     int rc;
     const size_t pb = (size_t)pay_vec_base(n);
     if ((rc = c->buf[0].reserve((pb + 3 * (size_t)n + 1) * sizeof(double))) ||
@@ -3466,7 +3562,33 @@ extern "C" int sfm_reduced_solve(const double *S, const double *rhs, int32_t n, 
     double *d_pay = c->buf[0].as<double>();
     SFM_HIP(hipMemcpyAsync(d_pay, pay.data(), pay.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
     SFM_HIP(hipMemsetAsync(c->buf[4].p, 0, sizeof(int), c->stream));
-    if (gjp.cb) {
+    if (gjrp.ok()) {
+        const int nT = nsp / 16;
+        if ((rc = c->buf[7].reserve(GjrBufs::words(nT) * sizeof(gjr::u64))) ||
+            (rc = c->buf[8].reserve(GjrBufs::ints * sizeof(int))))
+            return rc;
+        // records zeroed whenever the buffer or the layout changes: tags restart
+        if (c->buf[7].p != c->gjr_words || c->gjr_nT != nT) {
+            SFM_HIP(hipMemsetAsync(c->buf[7].p, 0, c->buf[7].bytes, c->stream));
+            c->gjr_words = c->buf[7].p;
+            c->gjr_nT = nT;
+            c->gjr_tag = 0;
+        }
+        GjrBufs b;
+        b.carve(c->buf[7].as<gjr::u64>(), c->buf[8].as<int>(), nT);
+        SFM_HIP(hipMemsetAsync(b.err, 0, GjrBufs::ints * sizeof(int), c->stream));
+        SFM_HIP(hipMemsetAsync(c->buf[2].p, 0, (size_t)nsp * sizeof(double), c->stream));
+        if ((rc = launch_gjr(gjrp, n, d_pay, d_pay + pb + 3 * (size_t)n, b, ++c->gjr_tag, c->buf[2].as<double>(),
+                             c->buf[4].as<int>(), nullptr, CamTrialArgs{}, c->stream)))
+            return rc;
+        int err = 0;
+        SFM_HIP(hipMemcpyAsync(&err, b.err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        SFM_HIP(hipStreamSynchronize(c->stream));
+        if (err) {
+            set_error("reduced solve: the persistent solve timed out");
+            return SFM_ERR_HIP;
+        }
+    } else if (gjp.cb) {
         const int nT = nsp / 16;
         const size_t nint = GjBufs::ints(nT, gjp.nseg);
         if ((rc = c->buf[5].reserve(GjBufs::doubles(nT, gjp.nseg) * sizeof(double))) ||
@@ -3485,6 +3607,7 @@ extern "C" int sfm_reduced_solve(const double *S, const double *rhs, int32_t n, 
         GjBufs b;
         b.carve(c->buf[5].as<double>(), c->buf[6].as<int>(), nT, gjp.nseg);
         SFM_HIP(hipMemsetAsync(b.err, 0, sizeof(int), c->stream));
+        SFM_HIP(hipMemsetAsync(b.arrive, 0, sizeof(unsigned), c->stream));  // an aborted launch may have left a count
         SFM_HIP(hipMemsetAsync(c->buf[2].p, 0, (size_t)nsp * sizeof(double), c->stream));
         if ((rc = launch_gj(gjp, nT, n, d_pay, d_pay + pb + 3 * (size_t)n, b,
                             ++c->gj_epoch, c->buf[2].as<double>(), c->buf[4].as<int>(), nullptr, CamTrialArgs{},

@@ -636,15 +636,17 @@ __device__ __forceinline__ void updater(const Args &a, const Geo &g, Smem &S, in
 
 // trial cameras and the camera part of the model decrease from dc (LDS),
 // as camera_trial (k_chol_backsolve's epilogue) with the system read from
-// its source; red: 3 x THREADS doubles
+// its source; red: 3 x NTH / 64 doubles
 // (scalar arguments: a reference to the kernel's Args would put a copy of it
 // on the stack of every lane)
+template <int NTH>
 __device__ __attribute__((noinline)) void cam_trial(int nc, const double *Rt, double *Rt_new, double *cam_out,
                                                     double lambda, const double *payload, int32_t ns,
                                                     const double *dc, double *red) {
     const double *du = payload + pay_vec_base(ns), *gc = du + ns;
     double m = 0, dn = 0, xn = 0;
-    for (int c = threadIdx.x; c < nc; c += THREADS) {
+    constexpr int NWT = NTH / 64;
+    for (int c = threadIdx.x; c < nc; c += NTH) {
         const double *d = dc + 6 * c;
         double dR[9];
         rotvec_to_R(d[0], d[1], d[2], dR);
@@ -672,12 +674,12 @@ __device__ __attribute__((noinline)) void cam_trial(int nc, const double *Rt, do
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) red[k * NW + w] = v[k];
+        for (int k = 0; k < 3; ++k) red[k * NWT + w] = v[k];
     __syncthreads();
     if (threadIdx.x < 3) {
         double s = 0.0;
 #pragma unroll
-        for (int t = 0; t < NW; ++t) s += red[threadIdx.x * NW + t];
+        for (int t = 0; t < NWT; ++t) s += red[threadIdx.x * NWT + t];
         cam_out[threadIdx.x] = s;
     }
 }
@@ -862,7 +864,7 @@ __global__ void __launch_bounds__(THREADS) k_gj_solve(Args a) {
     static_assert(sizeof(S.Gm) >= 6 * (NTMAX * TL / 6) * sizeof(double), "trial step");
     for (int i = threadIdx.x; i < 6 * a.ct.nc; i += THREADS) dc[i] = ld_ag(a.x + i);
     __syncthreads();
-    cam_trial(a.ct.nc, a.ct.Rt, a.ct.Rt_new, a.ct.cam_out, *a.lam, a.payload, a.ns, dc, red);
+    cam_trial<THREADS>(a.ct.nc, a.ct.Rt, a.ct.Rt_new, a.ct.cam_out, *a.lam, a.payload, a.ns, dc, red);
     stamp(a, a.nT, DBG_EPILOGUE);
 }
 

@@ -1,0 +1,493 @@
+// Row-distributed persistent block Gauss-Jordan solve of the damped reduced
+// camera system (S + lambda clamp(diag U)) x = b in ONE launch (round 4).
+// Replaces the reference's MINPACK dense QR step on the BA hot path
+// (Phase 1/BundleAdjustment.py:205-212, via scipy lmdif); included by ba.hip
+// after gj_solve.hpp (the 16-pivot DPP tile factor, elem_ref, cam_trial).
+//
+// The algorithm is gj_solve.hpp's block Gauss-Jordan with Cholesky pivots
+// (step p: L_p = chol(A_pp), G_i = A_ip L_p^-T for every row tile i != p,
+// A_ij -= G_i G_j^T for j > p, b_i -= G_i y_p; at the end x_i = L_i^-T L_i^-1
+// b_i), laid out so that the critical path crosses ONE workgroup boundary per
+// pivot and nothing else:
+//
+//  * workgroup r owns row tile r ("owner r"): the tiles A_rj of its row that
+//    are still live (j <= r before its pivot: the lower triangle; j > p after
+//    it: the rows above the pivot keep being eliminated), and b_r;
+//  * at pivot p owner p publishes ONE record P_p = {L_p^-1, y_p} (the tile
+//    factor also inverts: the identity rides as a second panel row set, so
+//    L_p^-T costs no extra chain steps).  Every owner forms its own
+//    G_r = A_rp L_p^-T as an MFMA product (no triangular solve), and the
+//    unpivoted owners r > p publish G_r for the others' updates;
+//  * owner r's wave W0 holds A_r,r-1 and A_rr: when P_{r-1} arrives it forms
+//    G_r, publishes it, updates A_rr, and runs the chain for pivot r -- the
+//    whole critical step inside one wave, with no LDS hand-off; the one
+//    cross-workgroup hop per pivot is P_{r-1} -> owner r;
+//  * G_r is only ever needed by others while r is unpivoted; the G of a
+//    pivoted row updates that row alone (and its b), off every critical path.
+//
+// Hand-offs are data-tagged granules (MI355X_MICROARCH.md handoff-1to1,
+// cdna_hip_programming.md Guideline 16 R2): every 8-byte word {tag, 32 data
+// bits} is written by ONE agent-scope store and re-read by agent-scope loads
+// until every tag equals this launch's tag -- no flag, no fence.  A double
+// travels as two granules.  Tags grow by one every launch (host epoch), so
+// no word needs re-zeroing between launches.
+//
+// Layout.  Tiles live in MFMA accumulators (v_mfma_f64_16x16x4f64: lane l
+// element e = D[(l >> 4) + 4e][l & 15]).  A tile of owner r is held as the
+// accumulator of A_rj^T: element e of lane l is A_rj(l & 15, (l >> 4) + 4e),
+// which is exactly the k-block-e operand fragment of A_rj.  So:
+//   G_r^T = L_p^-1 A_rp^T          A = L_p^-1 fragment, B = held A_rp
+//   A_rj^T -= G_j G_r^T            A = -G_j fragment,  B = G_r fragment
+//   A_rj^T  = G_j L_r^T (import)   A = G_j fragment,   B = L_r fragment
+// and the product G_r^T comes out as the fragment of G_r: nothing is ever
+// transposed through LDS except the diagonal tile into the chain's rows.
+namespace gjr {
+
+constexpr int TL = 16;
+constexpr int NUW = 7;           // tile-holding waves U0..U6 (tile j -> U[j % NUW]); with W0 two waves a SIMD
+constexpr int NW = NUW + 1;      // + W0
+constexpr int THREADS = 64 * NW;
+constexpr int NTMAX = 128;       // tile rows (host checks; larger systems take the Cholesky path)
+constexpr int RING = 4;          // LDS ring depth of the per-step pieces
+constexpr int PPAIRS = 5;        // granule pairs a lane of a pivot record: L^-1 fragment (4), y (1)
+constexpr int GPAIRS = 4;        // granule pairs a lane of a published G tile
+constexpr int PBYTES = PPAIRS * 64 * 16;
+constexpr int GBYTES = GPAIRS * 64 * 16;
+constexpr long long POLL_LIMIT = 20000000;  // s_memrealtime ticks (100 MHz): 200 ms
+constexpr int DYN_LDS = 64 * 1024;          // dynamic LDS: the epilogue's scratch, and one workgroup per CU
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef unsigned long long u64;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+struct Args {
+    const double *payload;  // the finished (all-reduced) Schur payload
+    int32_t ns, nT;
+    const double *lam;
+    const int *gate;
+    u64 *P;         // [nT] pivot records of PBYTES
+    u64 *G;         // [nT][nT] G_r of step p at (p, r), GBYTES each
+    unsigned tag;   // this launch's granule tag (>= 1)
+    double *x;      // [nT * 16] solution
+    int *bad;       // not positive definite (the LM rejects the step)
+    int *err;       // a wait timed out (the host reports an error)
+    unsigned *arrive;
+    CamTrialArgs ct;  // trial cameras epilogue (nc = 0: none)
+    long long *dbg;   // diagnostics (nullable): [grid][nT + 1][16] s_memrealtime stamps
+};
+
+enum { DBG_PIN = 0, DBG_GCRIT, DBG_CHAIN0, DBG_CHAIN1, DBG_PPUB, DBG_GHOLD, DBG_UDONE, DBG_GREM };
+enum { DBG_START = 0, DBG_PROLOGUE, DBG_W0END, DBG_ARRIVED };
+__device__ __forceinline__ void stamp(const Args &a, int p, int slot) {
+    if (a.dbg && (threadIdx.x & 63) == 0)
+        a.dbg[((int64_t)blockIdx.x * (a.nT + 1) + p) * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+}
+
+struct Smem {
+    double PL[RING][4][64];  // L_p^-1 fragments for the holder of A_rp
+    double GL[RING][4][64];  // G_r of step p for every wave's updates
+    double Lf[4][64];        // L_r fragment (the imports A_rj = L_r G_j^T)
+    double Dm[TL][TL + 1];   // the diagonal tile into the chain's rows; L_r rows after it
+    double Li[TL][TL + 1];   // L_r^-1 (row-major)
+    double bv[TL], yv[TL];
+    int pready[RING], pdone[RING], gready[RING], gdone[RING];
+    int lready, abort_, last;
+    int *err, *bad;
+};
+
+__device__ __forceinline__ int lds_ld(const int *w) {
+    return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_set(int *w, int v) {
+    __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_add(int *w, int v) {
+    __hip_atomic_fetch_add(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); }
+__device__ __forceinline__ void lds_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }
+__device__ __forceinline__ void wave_lds() { asm volatile("" ::: "memory"); }  // one wave's LDS accesses stay in order
+__device__ __forceinline__ long long rtc() { return __builtin_amdgcn_s_memrealtime(); }
+
+__device__ __forceinline__ void abort_solve(Smem &S) {
+    lds_set(&S.abort_, 1);
+    if ((threadIdx.x & 63) == 0) {
+        __hip_atomic_store(S.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(S.bad, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+// bounded waits: a lost hand-off (or another workgroup's abort) ends the
+// solve with an error, it never hangs the GPU
+__device__ __forceinline__ bool give_up(Smem &S, unsigned it, long long &t0) {
+    if (lds_ld(&S.abort_)) return true;
+    if (__hip_atomic_load(S.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        lds_set(&S.abort_, 1);
+        return true;
+    }
+    const long long t = rtc();
+    if (t0 < 0) t0 = t;
+    else if (t - t0 > POLL_LIMIT) {
+        abort_solve(S);
+        return true;
+    }
+    return false;
+}
+__device__ __forceinline__ bool lds_wait(const int *w, int target, Smem &S) {
+    if (lds_ld(w) >= target) {
+        lds_acquire();
+        return true;
+    }
+    long long t0 = -1;
+    for (unsigned it = 1;; ++it) {
+        __builtin_amdgcn_s_sleep(1);
+        if (lds_ld(w) >= target) break;
+        if (it % 256 == 0 && give_up(S, it, t0)) return false;
+    }
+    lds_acquire();
+    return true;
+}
+
+// ------------------------------------------------------------- granules
+// A double travels as ONE 16-byte pair of granules {lo, tag, hi, tag},
+// written by one sc1 buffer store (each 8-byte half is an untorn granule) and
+// polled by sc1 buffer loads; a record is PAIRS rows of 64 lanes x 16 bytes,
+// so every instruction moves 1 KB contiguous.  The descriptors are built from
+// kernel arguments (wave-uniform: no waterfall loops), offsets are 32-bit.
+struct Rs {
+    __amdgpu_buffer_rsrc_t P, G;
+};
+constexpr int SC1 = 16;  // buffer op aux: sc1 (write-through stores, L2-served loads)
+__device__ __forceinline__ void put_pair(__amdgpu_buffer_rsrc_t rs, int soff, int e, unsigned tag, double v,
+                                         int lane) {
+    const u64 b = (u64)__double_as_longlong(v);
+    const u32x4 w = {(unsigned)b, tag, (unsigned)(b >> 32), tag};
+    __builtin_amdgcn_raw_buffer_store_b128(w, rs, e * 1024 + lane * 16, soff, SC1);
+}
+__device__ __forceinline__ void put4(__amdgpu_buffer_rsrc_t rs, int soff, unsigned tag, const d4 &v, int lane) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) put_pair(rs, soff, e, tag, v[e], lane);
+}
+__device__ __forceinline__ double dec(const u32x4 &x) {
+    return __longlong_as_double((long long)(((u64)x.z << 32) | x.x));
+}
+// ONE wave re-reads the N pairs of NR records (all loads in flight) until
+// every tag of every lane matches; false on abort / timeout
+template <int NR, int N>
+__device__ __forceinline__ bool sweep(__amdgpu_buffer_rsrc_t rs, const int (&soff)[NR], const bool (&need)[NR],
+                                      unsigned tag, u32x4 (&x)[NR][N], int lane, Smem &S) {
+    long long t0 = -1;
+    for (unsigned it = 1;; ++it) {
+        asm volatile("" ::: "memory");  // every pass reloads
+#pragma unroll
+        for (int q = 0; q < NR; ++q)
+#pragma unroll
+            for (int k = 0; k < N; ++k)
+                x[q][k] = need[q] ? __builtin_amdgcn_raw_buffer_load_b128(rs, k * 1024 + lane * 16, soff[q], SC1)
+                                  : u32x4{0u, tag, 0u, tag};
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < NR; ++q)
+#pragma unroll
+            for (int k = 0; k < N; ++k) ok &= x[q][k].y == tag && x[q][k].w == tag;
+        if (__all(ok)) return true;
+        __builtin_amdgcn_s_sleep(1);
+        if (it % 64 == 0 && give_up(S, it, t0)) return false;
+    }
+}
+template <int N>
+__device__ __forceinline__ d4 dec4(const u32x4 (&v)[N]) {
+    return d4{dec(v[0]), dec(v[1]), dec(v[2]), dec(v[3])};
+}
+__device__ __forceinline__ int gsoff(const Args &a, int p, int r) { return (p * a.nT + r) * GBYTES; }
+
+// acc += sum_q A_q B_q (fp64 MFMA 16x16x4; fragment element q = k-block q)
+__device__ __forceinline__ d4 mfma4(d4 acc, const d4 &a, const d4 &b) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], b[q], acc, 0, 0, 0);
+    return acc;
+}
+__device__ __forceinline__ d4 zero4() { return d4{0.0, 0.0, 0.0, 0.0}; }
+
+// (G y)(l & 15) on every lane, from the G fragment and y(l & 15): fixed order
+__device__ __forceinline__ double gy(const d4 &g, double yl, int lane) {
+    double s = 0.0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s = fma(g[e], __shfl(yl, 4 * e + (lane >> 4)), s);
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    return s;
+}
+
+// tile A_rj of the damped, identity-padded system, held as the accumulator
+// of A_rj^T: element e of lane l = A(16 r + (l & 15), 16 j + (l >> 4) + 4e)
+__device__ __forceinline__ d4 load_tile(const Args &a, double lambda, int r, int j, int lane) {
+    gj::ElemRef er[4];
+    double v[4], dg[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) er[e] = gj::elem_ref(a.ns, TL * r + (lane & 15), TL * j + (lane >> 4) + 4 * e);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        v[e] = er[e].idx >= 0 ? a.payload[er[e].idx] : er[e].pad;
+        dg[e] = er[e].dg >= 0 ? a.payload[er[e].dg] : 0.0;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        if (er[e].dg >= 0) v[e] += lambda * clampd(dg[e]);
+    return d4{v[0], v[1], v[2], v[3]};
+}
+
+// uses of ring slot p % RING before step p: by the G pieces (every step but
+// r) and by the L^-1 pieces for a holder (every step but r - 1 and r)
+__device__ __forceinline__ int g_uses(int p, int r) {
+    return p / RING - (r < p && (r & (RING - 1)) == (p & (RING - 1)) ? 1 : 0);
+}
+__device__ __forceinline__ int p_uses(int p, int r) {
+    int u = g_uses(p, r);
+    if (r >= 1 && r - 1 < p && ((r - 1) & (RING - 1)) == (p & (RING - 1))) --u;
+    return u;
+}
+
+// ------------------------------------------------------------------- W0
+// The pivot: the chain on the diagonal tile with the b row (lane 0) and the
+// identity (lanes 16..31) as panel rows -> L_r (rows), y_r, L_r^-T rows.
+// Publishes P_r; leaves L_r^-1 in S.Li and the L_r fragment in S.Lf.
+__device__ __forceinline__ void pivot(const Args &a, const Rs &rs, Smem &S, int r, int lane, const d4 &Td, double b) {
+    const int li = lane & 15, grp = lane >> 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) S.Dm[li][grp + 4 * e] = Td[e];  // symmetric: column li = row li
+    if (lane < 16) S.bv[lane] = b;
+    wave_lds();
+    double rw[16], pw[16], dinv[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) rw[j] = S.Dm[li][j];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) pw[j] = grp == 0 ? (lane == 0 ? S.bv[j] : 0.0) : (grp == 1 && j == li ? 1.0 : 0.0);
+    stamp(a, r, DBG_CHAIN0);
+    gj::gj_factor16(rw, pw, dinv, lane, a.bad);
+    stamp(a, r, DBG_CHAIN1);
+    if (grp == 1)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) S.Li[j][li] = pw[j];  // row li of L^-T = column li of L^-1
+    if (lane == 0)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) S.yv[j] = pw[j];
+    if (grp == 0)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) S.Dm[li][j] = j <= li ? rw[j] : 0.0;
+    wave_lds();
+    d4 lv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lv[e] = S.Li[li][4 * e + grp];  // L^-1(l & 15, 4e + (l >> 4))
+    put4(rs.P, r * PBYTES, a.tag, lv, lane);
+    put_pair(rs.P, r * PBYTES, 4, a.tag, S.yv[li], lane);
+    stamp(a, r, DBG_PPUB);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) S.Lf[e][lane] = S.Dm[li][4 * e + grp];
+    lds_release();
+    lds_set(&S.lready, 1);
+}
+
+// W0 of owner r: A_r,r-1 (Tm), A_rr (Td), b_r; the pivot records of every
+// step (L^-1 into the ring for the holder of A_rp, y_p for b_r)
+__device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, int r, int lane, double lambda) {
+    const int nT = a.nT, li = lane & 15;
+    d4 Tm = r > 0 ? load_tile(a, lambda, r, r - 1, lane) : zero4();
+    d4 Td = load_tile(a, lambda, r, r, lane);
+    double b = assembled_b(a.payload, a.ns, TL * r + li);
+    stamp(a, nT, DBG_PROLOGUE);
+    for (int p = 0; p < nT; ++p) {
+        const int s = p & (RING - 1);
+        double yl = 0.0;
+        d4 lv = zero4();
+        if (p != r) {
+            const int soff[1] = {p * PBYTES};
+            const bool need[1] = {true};
+            u32x4 v[1][PPAIRS];
+            if (!sweep<1, PPAIRS>(rs.P, soff, need, a.tag, v, lane, S)) return false;
+            stamp(a, p, DBG_PIN);
+            lv = dec4(v[0]);
+            yl = dec(v[0][4]);
+            if (p != r - 1) {  // the holder of A_rp forms G_r from L_p^-1
+                if (!lds_wait(&S.pdone[s], p_uses(p, r), S)) return false;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) S.PL[s][e][lane] = lv[e];
+                lds_release();
+                lds_set(&S.pready[s], p + 1);
+            }
+        }
+        if (p == r - 1) {  // the critical step: G_r, its publication, A_rr, then the pivot
+            const d4 g = mfma4(zero4(), lv, Tm);
+            put4(rs.G, gsoff(a, p, r), a.tag, g, lane);  // owner r + 1 waits for it first
+            stamp(a, p, DBG_GCRIT);
+            Td = mfma4(Td, -g, g);
+            b -= gy(g, yl, lane);
+            if (!lds_wait(&S.gdone[s], NW * g_uses(p, r), S)) return false;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) S.GL[s][e][lane] = g[e];
+            lds_release();
+            lds_set(&S.gready[s], p + 1);
+            lds_add(&S.gdone[s], 1);
+        } else if (p == r) {
+            pivot(a, rs, S, r, lane, Td, b);
+        } else {
+            if (!lds_wait(&S.gready[s], p + 1, S)) return false;
+            d4 g;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) g[e] = S.GL[s][e][lane];
+            lds_release();
+            lds_add(&S.gdone[s], 1);
+            b -= gy(g, yl, lane);
+            if (p < r) {  // A_rr and A_r,r-1 (G_r-1 from owner r - 1)
+                Td = mfma4(Td, -g, g);
+                const int soff[1] = {gsoff(a, p, r - 1)};
+                const bool need[1] = {true};
+                u32x4 v[1][GPAIRS];
+                if (!sweep<1, GPAIRS>(rs.G, soff, need, a.tag, v, lane, S)) return false;
+                stamp(a, p, DBG_GREM);
+                const d4 gm = dec4(v[0]);
+                Tm = mfma4(Tm, -gm, g);
+            }
+        }
+    }
+    // x_r = L_r^-T (L_r^-1 b_r)
+    if (lane < 16) S.bv[lane] = b;
+    wave_lds();
+    double u = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) u = fma(S.Li[li][k], S.bv[k], u);
+    if (lane < 16) S.yv[lane] = u;
+    wave_lds();
+    double x = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x = fma(S.Li[i][li], S.yv[i], x);
+    if (lane < 16) __hip_atomic_store(a.x + TL * r + lane, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    stamp(a, nT, DBG_W0END);
+    return true;
+}
+
+// ------------------------------------------------------------- U waves
+// U_w of owner r holds the tiles j = w + NUW k (k < TPW) other than r - 1
+// and r: the lower ones from the start, the ones right of the diagonal from
+// the import at its pivot.  Per step: the holder of A_rp forms G_r (and
+// publishes it while r is unpivoted); every U wave applies it to its live
+// tiles j in (p, hi), two tiles' remote G loads in flight at a time.
+template <int TPW>
+__device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int r, int w, int lane, double lambda) {
+    const int nT = a.nT;
+    d4 T[TPW];
+#pragma unroll
+    for (int k = 0; k < TPW; ++k) {  // a tile at a time (the loads of all of them at once would spill)
+        const int j = w + NUW * k;
+        T[k] = j <= r - 2 ? load_tile(a, lambda, r, j, lane) : zero4();
+        asm volatile("" ::: "memory");
+    }
+    for (int p = 0; p < nT; ++p) {
+        const int s = p & (RING - 1);
+        if (p == r) {  // the import: A_rj^T = G_j L_r^T for j > r (G_j of step r from owner j)
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < TPW; ++k) any |= w + NUW * k > r && w + NUW * k < nT;
+            if (!any) continue;
+            if (!lds_wait(&S.lready, 1, S)) return false;
+            d4 lf;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) lf[e] = S.Lf[e][lane];
+#pragma unroll
+            for (int k = 0; k < TPW; k += 2) {
+                const int j0 = w + NUW * k, j1 = j0 + NUW;
+                const bool need[2] = {j0 > r && j0 < nT, k + 1 < TPW && j1 > r && j1 < nT};
+                if (!need[0] && !need[1]) continue;
+                const int soff[2] = {gsoff(a, p, need[0] ? j0 : 0), gsoff(a, p, need[1] ? j1 : 0)};
+                u32x4 v[2][GPAIRS];
+                if (!sweep<2, GPAIRS>(rs.G, soff, need, a.tag, v, lane, S)) return false;
+                if (need[0]) T[k] = mfma4(zero4(), dec4(v[0]), lf);
+                if (k + 1 < TPW && need[1]) T[k + 1] = mfma4(zero4(), dec4(v[1]), lf);
+            }
+            continue;
+        }
+        if (p % NUW == w && p != r - 1) {  // holder of A_rp: G_r = A_rp L_p^-T
+            if (!lds_wait(&S.pready[s], p + 1, S)) return false;
+            d4 lv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) lv[e] = S.PL[s][e][lane];
+            lds_release();
+            lds_add(&S.pdone[s], 1);
+            d4 tp = zero4();
+#pragma unroll
+            for (int k = 0; k < TPW; ++k)
+                if (k == p / NUW) tp = T[k];
+            const d4 g = mfma4(zero4(), lv, tp);
+            if (r > p) put4(rs.G, gsoff(a, p, r), a.tag, g, lane);
+            if (!lds_wait(&S.gdone[s], NW * g_uses(p, r), S)) return false;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) S.GL[s][e][lane] = g[e];
+            lds_release();
+            lds_set(&S.gready[s], p + 1);
+            stamp(a, p, DBG_GHOLD);
+        }
+        const int hi = r > p ? r - 1 : nT;  // live tiles j in (p, hi); W0 holds r - 1 and r
+        if (!lds_wait(&S.gready[s], p + 1, S)) return false;
+        d4 g;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) g[e] = S.GL[s][e][lane];
+        lds_release();
+        lds_add(&S.gdone[s], 1);
+#pragma unroll
+        for (int k = 0; k < TPW; k += 2) {
+            const int j0 = w + NUW * k, j1 = j0 + NUW;
+            const bool need[2] = {j0 > p && j0 < hi, k + 1 < TPW && j1 > p && j1 < hi};
+            if (!need[0] && !need[1]) continue;
+            const int soff[2] = {gsoff(a, p, need[0] ? j0 : 0), gsoff(a, p, need[1] ? j1 : 0)};
+            u32x4 v[2][GPAIRS];
+            if (!sweep<2, GPAIRS>(rs.G, soff, need, a.tag, v, lane, S)) return false;
+            if (need[0]) T[k] = mfma4(T[k], -dec4(v[0]), g);
+            if (k + 1 < TPW && need[1]) T[k + 1] = mfma4(T[k + 1], -dec4(v[1]), g);
+        }
+        if (w == 0) stamp(a, p, DBG_UDONE);
+    }
+    return true;
+}
+
+template <int TPW>
+__global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
+    if (a.gate && !*a.gate) return;  // device-side LM control: iteration gated off
+    __shared__ Smem S;
+    extern __shared__ __attribute__((aligned(16))) double dyn[];  // epilogue scratch (DYN_LDS bytes)
+    stamp(a, a.nT, DBG_START);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = blockIdx.x;
+    const double lambda = *a.lam;
+    if (threadIdx.x < RING) S.pready[threadIdx.x] = S.pdone[threadIdx.x] = S.gready[threadIdx.x] = S.gdone[threadIdx.x] = 0;
+    if (threadIdx.x == 0) {
+        S.lready = S.abort_ = S.last = 0;
+        S.err = a.err;
+        S.bad = a.bad;
+    }
+    Rs rs;
+    rs.P = __builtin_amdgcn_make_buffer_rsrc(a.P, (short)0, a.nT * PBYTES, 0x00020000);
+    rs.G = __builtin_amdgcn_make_buffer_rsrc(a.G, (short)0, a.nT * a.nT * GBYTES, 0x00020000);
+    __syncthreads();
+    if (wave == 0) w0_loop(a, rs, S, r, lane, lambda);
+    else u_loop<TPW>(a, rs, S, r, wave - 1, lane, lambda);
+    // every owner arrives (an aborted one too, so the count stays whole); the
+    // last one forms the trial cameras unless the solve failed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // W0's x stores drained before the barrier
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == (unsigned)a.nT - 1) {
+            __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            S.last = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+        }
+    }
+    __syncthreads();
+    stamp(a, a.nT, DBG_ARRIVED);
+    if (!S.last || a.ct.nc <= 0) return;
+    double *dc = dyn, *red = dyn + NTMAX * TL;
+    static_assert((NTMAX * TL + 3 * THREADS) * sizeof(double) <= DYN_LDS, "epilogue scratch");
+    for (int i = threadIdx.x; i < 6 * a.ct.nc; i += THREADS)
+        dc[i] = __hip_atomic_load(a.x + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    gj::cam_trial<THREADS>(a.ct.nc, a.ct.Rt, a.ct.Rt_new, a.ct.cam_out, *a.lam, a.payload, a.ns, dc, red);
+}
+
+}  // namespace gjr

@@ -1404,8 +1404,23 @@ extern "C" int sfm_nonlinear_pnp(const double *X, const double *x, int64_t N, co
                        c->buf[0].as<double>(), c->buf[1].as<double>());
     SFM_HIP(hipGetLastError());
     if (tm) SFM_HIP(hipEventRecord(c->ev[1], s));
-    // workgroups: ~1024 rows each (SFM_NLPNP_WGS overrides), at most NL_MAXWG
-    const int nb = std::max(1, std::min(NL_MAXWG, env_int("SFM_NLPNP_WGS", ceil_div((int64_t)N, 1024))));
+    // workgroups: ~1024 rows each (SFM_NLPNP_WGS overrides), at most NL_MAXWG,
+    // and never more than can be resident at once (the workgroups wait on
+    // each other's sums)
+    int nb = std::max(1, std::min(NL_MAXWG, env_int("SFM_NLPNP_WGS", ceil_div((int64_t)N, 1024))));
+    {
+        static int resident = -1;
+        if (resident < 0) {
+            int per_cu = 0, ncu = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_nonlinear_pnp, NL2_THREADS, 0) != hipSuccess ||
+                hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
+                per_cu = ncu = 0;
+            (void)hipGetLastError();
+            resident = std::max(1, per_cu * ncu);
+        }
+        nb = std::min(nb, resident);
+    }
+    for (int attempt = 0;; ++attempt) {
     NlX xg{};
     xg.nb = nb;
     if (nb > 1) {
@@ -1425,8 +1440,18 @@ extern "C" int sfm_nonlinear_pnp(const double *X, const double *x, int64_t N, co
     if (tm) SFM_HIP(hipEventRecord(c->ev[2], s));
     SFM_HIP(hipStreamSynchronize(s));
     if (hres[12] == -2.0) {
+        // a hand-off timed out (other work held the CUs the workgroups wait
+        // on): the same solve again on one workgroup, which waits on nobody
+        if (nb > 1 && attempt == 0) {
+            nb = 1;
+            hres[12] = -1.0;
+            hres[13] = 0.0;
+            continue;
+        }
         set_error("NonlinearPnP: a cross-workgroup hand-off timed out (%d workgroups)", nb);
         return SFM_ERR_HIP;
+    }
+    break;
     }
     std::memcpy(C_out, hres, 3 * sizeof(double));
     std::memcpy(R_out, hres + 3, 9 * sizeof(double));

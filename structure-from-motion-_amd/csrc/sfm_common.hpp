@@ -93,6 +93,9 @@ struct ThreadCtx {
     void *gj_ints = nullptr;  // sfm_reduced_solve: the flag buffer its epochs refer to
     int gj_epoch = 0;
     int gj_nT = 0, gj_nseg = 0;  // ... and the layout they were carved with
+    void *gjr_words = nullptr;   // ... the row-distributed solve's granule records (buf[7])
+    unsigned gjr_tag = 0;
+    int gjr_nT = 0;
     void *nl_sync = nullptr;     // sfm_nonlinear_pnp's cross-workgroup sums (zeroed once; epoch-tagged flags)
     unsigned nl_epoch = 0;
     ~ThreadCtx() {
