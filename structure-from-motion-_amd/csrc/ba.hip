@@ -852,10 +852,23 @@ __device__ __forceinline__ void sw_signal(int *c) {
     if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// The dispatch tail (round 4): nspec x nrange (spec, range) items run as
+// rounds of one workgroup per CU; when the last round would be a sliver
+// (cfg5: 800 items on 256 CUs, the fourth round 32 workgroups for a
+// quarter of the span), the specs [w0, nspec) that would form it are cut
+// per range into S chunk sub-ranges instead, S x as many short workgroups
+// filling the last round.  A sub-range's partial goes to slabx, indexed by
+// (range, sub-range, spec - w0, group); k_schur_finish adds those partials
+// in (range, sub-range) order for the split specs' blocks.
+struct SweepSplit {
+    int32_t nfull, S, w0, nsplit, gmax;  // S = 0: no split (every workgroup a whole item)
+    double *slabx;
+};
+
 template <int LPP, int NACC>
 __device__ __forceinline__ void sweep_reduce(const double (&acc)[NACC], bool has_acc, int t, int ng,
                                              const SweepGroup *__restrict__ grps, double *__restrict__ slab_r,
-                                             double *red) {
+                                             double *red, bool by_group = false) {
     constexpr int NH = LPP == 2 ? 2 : 1;  // output halves per group (LPP = 2: rows 3h..3h+2)
     // the spec's group table in LDS after the accumulators (one global
     // latency, not one per output task)
@@ -890,7 +903,7 @@ __device__ __forceinline__ void sweep_reduce(const double (&acc)[NACC], bool has
                 v += a3;
             }
             for (; sl < n; ++sl) v += src[LPP * sl];
-            slab_r[(int64_t)gr.blk * ITEM_W + dst] = v;
+            slab_r[(int64_t)(by_group ? g : gr.blk) * ITEM_W + dst] = v;
         }
         lds_barrier();  // the slab stores need not land before the next round
     }
@@ -904,7 +917,7 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     const int32_t *__restrict__ spec_cam, const uint32_t *__restrict__ list, const uint32_t *__restrict__ pairs,
     const int32_t *__restrict__ hdr, const double *__restrict__ Xg, const double *__restrict__ Lq,
     const double *__restrict__ Rt, Kmat Km, double *__restrict__ slab, const int *__restrict__ gate, int dbg,
-    int nsweep, CamLinArgs cl, long long *__restrict__ stamps, int *__restrict__ sw_err) {
+    int nsweep, CamLinArgs cl, long long *__restrict__ stamps, int *__restrict__ sw_err, SweepSplit sp) {
     extern __shared__ double2 sw_lds[];
     if ((int)blockIdx.x >= nsweep) {  // camera blocks of the normal equations on the CUs the sweep leaves idle
         if (!*cl.glin) return;
@@ -916,9 +929,27 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
     if (dbg & 8) return;         // timing probe: the launch without the sweep
     uint32_t *ldsw = reinterpret_cast<uint32_t *>(sw_lds);
-    const int loc = blockIdx.x / NXCD;
-    const int w = loc % nspec, r = (loc / nspec) * NXCD + (int)(blockIdx.x % NXCD);
-    if (r >= nrange) return;  // whole workgroup
+    // the work item: a whole (spec, range), or a chunk sub-range of a split one
+    int w, r, q0, q1;
+    double *slab_out;
+    const bool sub = sp.S > 0 && (int)blockIdx.x >= sp.nfull;
+    if (!sub) {
+        const int loc = blockIdx.x / NXCD;
+        w = loc % nspec;
+        r = (loc / nspec) * NXCD + (int)(blockIdx.x % NXCD);
+        if (r >= nrange) return;  // whole workgroup
+        q0 = rchunk[r];
+        q1 = rchunk[r + 1];
+        slab_out = slab + (int64_t)r * nbd * ITEM_W;
+    } else {
+        const int u = blockIdx.x - sp.nfull, v = u / NXCD, s = v % sp.S;
+        r = u % NXCD;
+        w = sp.w0 + v / sp.S;
+        const int Q0 = rchunk[r], Q1 = rchunk[r + 1];
+        q0 = Q0 + (Q1 - Q0) * s / sp.S;
+        q1 = Q0 + (Q1 - Q0) * (s + 1) / sp.S;
+        slab_out = sp.slabx + ((int64_t)((r * sp.S + s) * sp.nsplit + (w - sp.w0)) * sp.gmax) * ITEM_W;
+    }
     const int t = threadIdx.x;
     // SFM_SWEEP_STAMPS: s_memrealtime per (workgroup, event, wave), lane 0
     long long *stw = stamps && blockIdx.x < SW_STAMP_WG && (t & 63) == 0
@@ -956,7 +987,6 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     double K[9];
 #pragma unroll
     for (int i = 0; i < 9; ++i) K[i] = Km.k[i];
-    const int q0 = rchunk[r], q1 = rchunk[r + 1];
     const int tst = t - (SW_THREADS - 64 * SW_STAGE_WAVES);
     // a scalar branch: the two roles run different barrier sequences, and a
     // barrier inside an exec-masked (divergent) region would still execute
@@ -1066,8 +1096,8 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
         }
         if (csync) lds_barrier();  // every pair wave is done with the buffers sweep_reduce reuses
         const double none[NACC] = {};  // no accumulators: output tasks only
-        sweep_reduce<LPP>(none, false, t, ng, groups + spec_goff[w], slab + (int64_t)r * nbd * ITEM_W,
-                          reinterpret_cast<double *>(sw_lds));
+        sweep_reduce<LPP>(none, false, t, ng, groups + spec_goff[w], slab_out, reinterpret_cast<double *>(sw_lds),
+                          sub);
         stamp(SW_STAMP_EV - 1);
         return;
     }
@@ -1142,8 +1172,7 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     // reduce the groups' slots in slot order through LDS (the staging
     // buffers are free now)
     if (csync) lds_barrier();
-    sweep_reduce<LPP>(acc, gi >= 0, t, ng, groups + spec_goff[w], slab + (int64_t)r * nbd * ITEM_W,
-                      reinterpret_cast<double *>(sw_lds));
+    sweep_reduce<LPP>(acc, gi >= 0, t, ng, groups + spec_goff[w], slab_out, reinterpret_cast<double *>(sw_lds), sub);
     stamp(SW_STAMP_EV - 1);
 }
 
@@ -1153,14 +1182,21 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
 __global__ void __launch_bounds__(64) k_schur_finish(int32_t ns, int32_t nbd, int32_t nrange,
                                                      const int2 *__restrict__ blkij, const double *__restrict__ slab,
                                                      const double *__restrict__ camlin,
-                                                     double *__restrict__ payload, const int *__restrict__ gate) {
+                                                     double *__restrict__ payload, const int *__restrict__ gate,
+                                                     const int32_t *__restrict__ split_of, SweepSplit sp) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
     const int2 ij = blkij[blockIdx.x];
     const int t = threadIdx.x;
     const bool diag = ij.x == ij.y;
     if (t >= (diag ? ITEM_W : 36)) return;
     double v = 0;
-    for (int r = 0; r < nrange; ++r) v += slab[((int64_t)r * nbd + blockIdx.x) * ITEM_W + t];
+    const int si = sp.S > 0 ? split_of[blockIdx.x] : -1;  // (spec - w0) * gmax + group, split specs only
+    if (si < 0) {
+        for (int r = 0; r < nrange; ++r) v += slab[((int64_t)r * nbd + blockIdx.x) * ITEM_W + t];
+    } else {
+        const int64_t row = (int64_t)sp.nsplit * sp.gmax;
+        for (int rs = 0; rs < nrange * sp.S; ++rs) v += sp.slabx[(rs * row + si) * ITEM_W + t];
+    }
     const int64_t base = pay_vec_base(ns);
     if (t < 36) {
         const int r = t / 6, c = t % 6;
@@ -2168,16 +2204,41 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
     for (int i = 0; i < 9; ++i) K[i] = Km.k[i];
     double acc[4] = {0, 0, 0, 0};
     // grid-stride over points (a bounded grid keeps the per-block partial
-    // store + arrival count, and the last block's sum, small)
-    for (int64_t gt = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x; gt / G < np_;
-         gt += (int64_t)gridDim.x * PT_THREADS) {
+    // store + arrival count, and the last block's sum, small), software
+    // pipelined: the next point's pstart, X, V / g and L are loaded while this
+    // point is worked on, so an iteration waits for one round of loads (its
+    // observations') instead of three in a row (pstart, then the
+    // observations, then V / g and L)
+    struct Pre {
+        int32_t o0, o1;
+        double x[3], g[3], dg[3], l[6];
+    };
+    auto fetch = [&](int64_t gtn, Pre &P) {
+        const int64_t p = gtn / G;
+        const bool live = p < np_;
+        P.o0 = live ? pstart[p] : 0;
+        P.o1 = live ? pstart[p + 1] : 0;
+        const double *vg = Vg + 9 * (live ? p : 0);
+        const double *l = Lq + 9 * (live ? p : 0);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            P.x[i] = live ? X[3 * p + i] : 0.0;
+            P.g[i] = vg[6 + i];
+        }
+        P.dg[0] = vg[0];
+        P.dg[1] = vg[3];
+        P.dg[2] = vg[5];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) P.l[i] = l[i];
+    };
+    const int64_t stride = (int64_t)gridDim.x * PT_THREADS;
+    Pre cur;
+    fetch((int64_t)blockIdx.x * PT_THREADS + threadIdx.x, cur);
+    for (int64_t gt = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x; gt / G < np_; gt += stride) {
     const int64_t p = gt / G;  // G lanes per point, striding over its observations
     const int sub = (int)(gt % G);
     const bool live = p < np_;
-    const int32_t o0 = live ? pstart[p] : 0, o1 = live ? pstart[p + 1] : 0;
-    // W^T dc = Jp^T (Jc dc) = R^T A^T (A (dtheta x p + dt)), summed over the point's observations
-    double wt[3] = {0, 0, 0};
-    const double x[3] = {live ? X[3 * p] : 0.0, live ? X[3 * p + 1] : 0.0, live ? X[3 * p + 2] : 0.0};
+    const int32_t o0 = cur.o0, o1 = cur.o1;
     // the lane's first BS_PRE observations (camera index and measurement)
     // loaded up front, for both passes: their loads are in flight together
     // instead of one round trip per observation and pass
@@ -2189,6 +2250,11 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
         cpre[k] = o < o1 ? cam[o] : 0;
         opre[k] = o < o1 ? obs[o] : make_double2(0.0, 0.0);
     }
+    Pre nxt;
+    fetch(gt + stride, nxt);
+    // W^T dc = Jp^T (Jc dc) = R^T A^T (A (dtheta x p + dt)), summed over the point's observations
+    double wt[3] = {0, 0, 0};
+    const double x[3] = {cur.x[0], cur.x[1], cur.x[2]};
     auto wt_add = [&](int32_t c) {
         const double *d = dc + 6 * c;
         const double *R = Rt + 12 * c;
@@ -2212,23 +2278,21 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
 #pragma unroll
     for (int i = 0; i < 3; ++i) wt[i] = group_sum<G>(wt[i]);
     if (live) {
-        const double *vg = Vg + 9 * p;
-        const double rhs[3] = {-vg[6] - wt[0], -vg[7] - wt[1], -vg[8] - wt[2]};
-        const double *l = Lq + 9 * p;  // L upper: 00 01 02 11 12 22
+        const double rhs[3] = {-cur.g[0] - wt[0], -cur.g[1] - wt[1], -cur.g[2] - wt[2]};
+        const double *l = cur.l;  // L upper: 00 01 02 11 12 22
         // y = L^T rhs ; dp = L y  (every lane of the group, identically)
         const double y0 = l[0] * rhs[0];
         const double y1 = l[1] * rhs[0] + l[3] * rhs[1];
         const double y2 = l[2] * rhs[0] + l[4] * rhs[1] + l[5] * rhs[2];
         const double dp[3] = {l[0] * y0 + l[1] * y1 + l[2] * y2, l[3] * y1 + l[4] * y2, l[5] * y2};
         double xn[3];
-        const double dg[3] = {vg[0], vg[3], vg[5]};
 #pragma unroll
         for (int i = 0; i < 3; ++i) xn[i] = x[i] + dp[i];
         if (sub == 0) {
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
                 X_new[3 * p + i] = xn[i];
-                acc[1] += dp[i] * (lambda * clampd(dg[i]) * dp[i] - vg[6 + i]);
+                acc[1] += dp[i] * (lambda * clampd(cur.dg[i]) * dp[i] - cur.g[i]);
                 acc[2] += dp[i] * dp[i];
                 acc[3] += x[i] * x[i];
             }
@@ -2238,6 +2302,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
             if (o0 + sub + k * G < o1) acc[0] += obs_cost(Rt_new + 12 * cpre[k], xn, K, opre[k]);
         for (int32_t o = o0 + sub + BS_PRE * G; o < o1; o += G) acc[0] += obs_cost(Rt_new + 12 * cam[o], xn, K, obs[o]);
     }
+    cur = nxt;
     }
     grid_sum_last<4>(acc, partial, counter, out);
 }
@@ -2297,7 +2362,8 @@ using namespace sfm;
 // chunk obs0).
 struct SweepPlan {
     int32_t nrange = 0, nspec = 0, nbd = 0, buf_slots = 0, pair_cap = 0, hdr_cap = 0, list_cap = 0, nchunk = 0;
-    std::vector<int32_t> rchunk, goff, nload, list, hdr, spec_cam;
+    int32_t split_S = 0, split_w0 = 0, split_n = 0, split_gmax = 0;  // the dispatch tail's split (SweepSplit)
+    std::vector<int32_t> rchunk, goff, nload, list, hdr, spec_cam, split_of;
     std::vector<SweepGroup> groups;
     std::vector<int16_t> lanegrp;
     std::vector<uint16_t> pairs;
@@ -2419,7 +2485,8 @@ static int64_t sweep_alloc(const std::vector<std::vector<uint16_t>> &P, const st
 }
 
 static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt,
-                       const std::vector<int32_t> &pstart, const std::vector<int64_t> &cnt, int lpp, SweepPlan &P) {
+                       const std::vector<int32_t> &pstart, const std::vector<int64_t> &cnt, int lpp, int ncu,
+                       bool allow_split, SweepPlan &P) {
     P.nbd = nc * (nc + 1) / 2;
     P.blkij.resize(P.nbd);
     for (int i = 0; i < nc; ++i)
@@ -2610,6 +2677,31 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
         }
     }
     P.goff.push_back((int32_t)P.groups.size());
+    // the dispatch tail: one workgroup per CU (SW_THREADS, 168 VGPRs), so
+    // items run in rounds of ncu; a short last round's specs are split per
+    // range into S chunk sub-ranges (SFM_SWEEP_SPLIT=0: off).  Not with the
+    // Cholesky solve, whose first launch reads the slabs itself (SlabSrc).
+    P.split_of.assign(P.nbd, -1);
+    {
+        const int per_round = ncu / NXCD;  // specs of one range group per round
+        const int want = env_int("SFM_SWEEP_SPLIT", 8);
+        int min_chunks = INT32_MAX;
+        for (int r = 0; r < P.nrange; ++r) min_chunks = std::min(min_chunks, P.rchunk[r + 1] - P.rchunk[r]);
+        const int nsplit = P.nspec % std::max(1, per_round);
+        if (allow_split && want >= 2 && P.nrange == NXCD && per_round >= 1 && P.nspec > per_round && nsplit > 0) {
+            const int S = std::min({want, per_round / nsplit, min_chunks});
+            if (S >= 2) {
+                P.split_S = S;
+                P.split_n = nsplit;
+                P.split_w0 = P.nspec - nsplit;
+                for (int w = P.split_w0; w < P.nspec; ++w)
+                    P.split_gmax = std::max(P.split_gmax, P.goff[w + 1] - P.goff[w]);
+                for (int w = P.split_w0; w < P.nspec; ++w)
+                    for (int g = P.goff[w]; g < P.goff[w + 1]; ++g)
+                        P.split_of[P.groups[g].blk] = (w - P.split_w0) * P.split_gmax + (g - P.goff[w]);
+            }
+        }
+    }
     if (env_int("SFM_SWEEP_VERBOSE", 0))
         std::fprintf(stderr,
                      "sweep plan: nspec %d nrange %d nchunk %d chunk_obs %d buf_slots %d pair_cap %d lds %zu B; "
@@ -2692,6 +2784,8 @@ struct sfm_ba_problem {
     int sw_debug = 0;                              // SFM_SWEEP_DEBUG (read once per solve)
     // Schur sweep plan (k_schur_sweep): ranges, chunks, specs
     int32_t sw_nrange = 0, sw_nspec = 0, sw_nbd = 0, sw_nchunk = 0;
+    SweepSplit sw_split = {};
+    int32_t *d_sw_split_of = nullptr;
     SweepLds sw_L = {};
     int sw_lpp = 1;
     bool sw_pinhole = false;
@@ -2910,7 +3004,12 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     // lanes per pair slot: 1 (default; a lane forms a pair's whole 6x6 block,
     // H once) or 2 (SFM_SWEEP_LPP=2: half the rows each)
     p->sw_lpp = env_int("SFM_SWEEP_LPP", 1) == 2 ? 2 : 1;
-    plan_sweep(nc, np_, no, cam, pt, pstart, cnt, p->sw_lpp, sw);
+    // the persistent reduced solves read the finished payload (finish runs
+    // as its own launch): the sweep's dispatch tail may be split
+    const char *solve_env = std::getenv("SFM_SOLVE");
+    const bool split_ok = p->tb == 16 && !(solve_env && std::strcmp(solve_env, "chol") == 0) &&
+                          p->nT <= gj::NTMAX;
+    plan_sweep(nc, np_, no, cam, pt, pstart, cnt, p->sw_lpp, device_cus(device), split_ok, sw);
     if (sw.buf_slots > SW_MAX_STAGED) {  // one point with more observations in a spec's cameras than a round holds
         set_error("sweep plan: %d observations of one spec's cameras in a single point range (max %d)", sw.buf_slots,
                   SW_MAX_STAGED);
@@ -2923,7 +3022,8 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     // as many as the CUs the sweep leaves idle), each cut again at camera
     // boundaries
     const int cam_chunk = std::max(64, env_int("SFM_CAM_CHUNK", CAM_CHUNK));
-    const int busy = sw.nspec * sw.nrange, idle = (256 - busy % 256) % 256;
+    const int busy = sw.split_S ? NXCD * (sw.split_w0 + sw.split_n * sw.split_S) : sw.nspec * sw.nrange,
+              idle = (256 - busy % 256) % 256;
     p->cl_fused_wg = (int32_t)std::min<int64_t>(std::max<int64_t>(1, ceil_div(no, SW_THREADS)),
                                                 env_int("SFM_CAMLIN_WG", idle >= 32 ? idle : 64));
     CamPlan csa, cfu;
@@ -2945,6 +3045,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     p->sw_nbd = sw.nbd;
     p->sw_L = {sw.buf_slots, sw.pair_cap, sw.hdr_cap, sw.list_cap};
     p->sw_nchunk = sw.nchunk;
+    p->sw_split = {NXCD * sw.split_w0, sw.split_S, sw.split_w0, sw.split_n, sw.split_gmax, nullptr};
     // + the end-of-range reduction: the accumulators and the group table
     p->sw_lds_bytes = std::max(sw.lds_bytes(), (size_t)SW_RED_W * SW_RED_LD * sizeof(double) +
                                                    (size_t)sw.hdr_cap * sizeof(SweepGroup));
@@ -2958,6 +3059,9 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = p->alloc(p->d_wg_first, csa.wg_first.size())) || (rc = p->alloc(p->d_fitems, cfu.items.size())) ||
         (rc = p->alloc(p->d_fblocks, cfu.blocks.size())) || (rc = p->alloc(p->d_fwg_first, cfu.wg_first.size())) ||
         (rc = p->alloc(p->d_slab, (int64_t)ITEM_W * sw.nrange * sw.nbd)) ||
+        (rc = p->alloc(p->sw_split.slabx, std::max<int64_t>(1, (int64_t)ITEM_W * sw.nrange * sw.split_S * sw.split_n *
+                                                                   sw.split_gmax))) ||
+        (rc = p->alloc(p->d_sw_split_of, sw.split_of.size())) ||
         (rc = p->alloc(p->d_sw_rchunk, sw.rchunk.size())) || (rc = p->alloc(p->d_sw_goff, sw.goff.size())) ||
         (rc = p->alloc(p->d_sw_nload, sw.nload.size())) ||
         (rc = p->alloc(p->d_sw_groups, sw.groups.size())) || (rc = p->alloc(p->d_sw_lanegrp, sw.lanegrp.size())) ||
@@ -3045,7 +3149,8 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = up(p->d_sw_scam, sw.spec_cam.data(), sw.spec_cam.size() * 4)) ||
         (rc = up(p->d_sw_hdr, sw.hdr.data(), sw.hdr.size() * 4)) ||
         (rc = up(p->d_sw_pairs, sw.pairs.data(), sw.pairs.size() * 2)) ||
-        (rc = up(p->d_sw_blkij, sw.blkij.data(), sw.blkij.size() * sizeof(int2))))
+        (rc = up(p->d_sw_blkij, sw.blkij.data(), sw.blkij.size() * sizeof(int2))) ||
+        (rc = up(p->d_sw_split_of, sw.split_of.data(), sw.split_of.size() * 4)))
         return rc;
     SFM_HIP(hipFuncSetAttribute((const void *)k_schur_sweep<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)p->sw_lds_bytes));
@@ -3309,7 +3414,8 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     SFM_HIP(hipGetLastError());
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_PREP + 1], s));
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SCHUR], s));
-    const int nsweep = NXCD * p->sw_nspec * ceil_div(p->sw_nrange, NXCD);
+    const int nsweep = p->sw_split.S ? p->sw_split.nfull + NXCD * p->sw_split.nsplit * p->sw_split.S
+                                     : NXCD * p->sw_nspec * ceil_div(p->sw_nrange, NXCD);
     const bool fused = p->cl_fused && p->ndiag_items;  // + the camera blocks (after an accepted step)
     auto sweep_k = p->sw_lpp == 2 ? k_schur_sweep<2> : p->sw_pinhole ? k_schur_sweep<1, true> : k_schur_sweep<1>;
     hipLaunchKernelGGL(sweep_k, dim3(nsweep + (fused ? p->cl_fused_wg : 0)), dim3(SW_THREADS),
@@ -3317,14 +3423,14 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
                        p->d_sw_nload, p->d_sw_goff, p->d_sw_groups, p->d_sw_lanegrp, p->d_sw_scam,
                        reinterpret_cast<const uint32_t *>(p->d_sw_list), p->d_sw_pairs, p->d_sw_hdr, p->d_X, p->d_Lq,
                        p->d_Rt, p->K, p->d_slab, gst, p->sw_debug, nsweep,
-                       camlin_args(p, true, &p->d_lm[par].run_lin), sw_dbg_ptr(), p->d_sw_err);
+                       camlin_args(p, true, &p->d_lm[par].run_lin), sw_dbg_ptr(), p->d_sw_err, p->sw_split);
     SFM_HIP(hipGetLastError());
     // one rank: the solve's first launch sums the slabs itself (SlabSrc)
     // (the persistent solve reads the finished payload: the finish runs as its own launch)
-    const bool fin_fused = !p->comm && p->fin_fused && !p->gjp.cb && !p->gjrp.ok();
+    const bool fin_fused = !p->comm && p->fin_fused && !p->gjp.cb && !p->gjrp.ok() && !p->sw_split.S;
     if (!fin_fused) {
         hipLaunchKernelGGL(k_schur_finish, dim3(p->sw_nbd), dim3(64), 0, s, p->ns, p->sw_nbd, p->sw_nrange,
-                           p->d_sw_blkij, p->d_slab, p->d_camlin, p->d_payload, gst);
+                           p->d_sw_blkij, p->d_slab, p->d_camlin, p->d_payload, gst, p->d_sw_split_of, p->sw_split);
         SFM_HIP(hipGetLastError());
     }
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SCHUR + 1], s));

@@ -215,6 +215,7 @@ struct PySampler {
         const __m512i vnn = _mm512_set1_epi32((int)(uint32_t)n);
         const __m512i iota = _mm512_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
         const __m128i vsh = _mm_cvtsi32_si128(sh);
+        static const bool cstore = std::getenv("SFM_PYRANDOM_CSTORE") && std::atoi(std::getenv("SFM_PYRANDOM_CSTORE"));
         int32_t *res = out + h0 * K;
         int32_t *const end = out + h1 * K;
         if (res >= end) return;
@@ -237,14 +238,28 @@ struct PySampler {
             }
             uint32_t *v = vals.data();
             int32_t *a = pos.data();  // index within the current block
-            for (int i = i0; i < 624; i += 16) {
-                const __mmask16 lm = 624 - i >= 16 ? (__mmask16)0xFFFF : (__mmask16)((1u << (624 - i)) - 1);
-                const __m512i u = _mm512_srl_epi32(_mm512_maskz_loadu_epi32(lm, m.tmp + i), vsh);
-                const __mmask16 kin = _mm512_mask_cmplt_epu32_mask(lm, u, vnn);
-                _mm512_mask_compressstoreu_epi32(v + c, kin, u);
-                _mm512_mask_compressstoreu_epi32(a + c, kin, _mm512_add_epi32(_mm512_set1_epi32(i), iota));
-                c += _mm_popcnt_u32((unsigned)kin);
-            }
+            // compress into a register, then one full 64-byte store (the
+            // buffers carry 16 words of slack): the memory form of
+            // vpcompressd is microcoded on AMD Zen cores (SFM_PYRANDOM_CSTORE=1
+            // keeps it, for comparison)
+            if (cstore)
+                for (int i = i0; i < 624; i += 16) {
+                    const __mmask16 lm = 624 - i >= 16 ? (__mmask16)0xFFFF : (__mmask16)((1u << (624 - i)) - 1);
+                    const __m512i u = _mm512_srl_epi32(_mm512_maskz_loadu_epi32(lm, m.tmp + i), vsh);
+                    const __mmask16 kin = _mm512_mask_cmplt_epu32_mask(lm, u, vnn);
+                    _mm512_mask_compressstoreu_epi32(v + c, kin, u);
+                    _mm512_mask_compressstoreu_epi32(a + c, kin, _mm512_add_epi32(_mm512_set1_epi32(i), iota));
+                    c += _mm_popcnt_u32((unsigned)kin);
+                }
+            else
+                for (int i = i0; i < 624; i += 16) {
+                    const __mmask16 lm = 624 - i >= 16 ? (__mmask16)0xFFFF : (__mmask16)((1u << (624 - i)) - 1);
+                    const __m512i u = _mm512_srl_epi32(_mm512_maskz_loadu_epi32(lm, m.tmp + i), vsh);
+                    const __mmask16 kin = _mm512_mask_cmplt_epu32_mask(lm, u, vnn);
+                    _mm512_storeu_si512(v + c, _mm512_maskz_compress_epi32(kin, u));
+                    _mm512_storeu_si512(a + c, _mm512_maskz_compress_epi32(kin, _mm512_add_epi32(_mm512_set1_epi32(i), iota)));
+                    c += _mm_popcnt_u32((unsigned)kin);
+                }
             i0 = 624;
             while (res < end && c - p >= K) {
                 const uint32_t *g = v + p;
