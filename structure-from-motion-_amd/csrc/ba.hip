@@ -2115,14 +2115,14 @@ struct GjrPlan {
     int nT = 0, tpw = 0;
     bool ok() const { return tpw > 0; }
 };
-template <int TPW>
+template <int TR, int TLS>
 static bool gjr_resident(int nT, int ncu) {
     static int nb = -1;  // resident workgroups per CU (queried once per instantiation)
     if (nb < 0) {
         nb = 0;
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&gjr::k_gjr_solve<TPW>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&gjr::k_gjr_solve<TR, TLS>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, gjr::DYN_LDS) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gjr::k_gjr_solve<TPW>, gjr::THREADS, gjr::DYN_LDS) !=
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gjr::k_gjr_solve<TR, TLS>, gjr::THREADS, gjr::DYN_LDS) !=
                 hipSuccess)
             nb = 0;
         (void)hipGetLastError();
@@ -2133,11 +2133,13 @@ static GjrPlan gjr_plan(int nT, int ncu) {
     GjrPlan g;
     if (const char *e = std::getenv("SFM_SOLVE"))
         if (std::strcmp(e, "chol") == 0 || std::strcmp(e, "gjseg") == 0) return g;
-    // tile slots per U wave (a compile-time register array): up to 28 / 77 tile
-    // rows (more would spill: the segment layout takes those)
-    if (nT < 1 || nT > 11 * gjr::NUW || nT > ncu) return g;
-    const int tpw = nT <= 4 * gjr::NUW ? 4 : 11;
-    const bool res = tpw == 4 ? gjr_resident<4>(nT, ncu) : gjr_resident<11>(nT, ncu);
+    // tile slots per U wave: 4 or TREG in registers (up to 28 / 77 tile
+    // rows), past that TREG_L + TLDS_L (the latter in LDS: up to 133)
+    if (nT < 1 || nT > gjr::NTMAX || nT > ncu) return g;
+    const int tpw = nT <= 4 * gjr::NUW ? 4 : nT <= gjr::TREG * gjr::NUW ? gjr::TREG : gjr::TREG_L + gjr::TLDS_L;
+    const bool res = tpw == 4 ? gjr_resident<4, 0>(nT, ncu)
+                   : tpw == gjr::TREG ? gjr_resident<gjr::TREG, 0>(nT, ncu)
+                                      : gjr_resident<gjr::TREG_L, gjr::TLDS_L>(nT, ncu);
     if (!res) return g;
     g.nT = nT;
     g.tpw = tpw;
@@ -2175,8 +2177,14 @@ static int launch_gjr(const GjrPlan &g, int32_t ns, const double *payload, const
     a.ct = ct;
     a.dbg = gj_dbg_ptr();
     switch (g.tpw) {
-    case 4: hipLaunchKernelGGL(gjr::k_gjr_solve<4>, dim3(g.nT), dim3(gjr::THREADS), gjr::DYN_LDS, s, a); break;
-    default: hipLaunchKernelGGL(gjr::k_gjr_solve<11>, dim3(g.nT), dim3(gjr::THREADS), gjr::DYN_LDS, s, a); break;
+    case 4: hipLaunchKernelGGL((gjr::k_gjr_solve<4, 0>), dim3(g.nT), dim3(gjr::THREADS), gjr::DYN_LDS, s, a); break;
+    case gjr::TREG:
+        hipLaunchKernelGGL((gjr::k_gjr_solve<gjr::TREG, 0>), dim3(g.nT), dim3(gjr::THREADS), gjr::DYN_LDS, s, a);
+        break;
+    default:
+        hipLaunchKernelGGL((gjr::k_gjr_solve<gjr::TREG_L, gjr::TLDS_L>), dim3(g.nT), dim3(gjr::THREADS), gjr::DYN_LDS,
+                           s, a);
+        break;
     }
     SFM_HIP(hipGetLastError());
     return 0;
@@ -3001,9 +3009,9 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
             }
     p->npairs = tot;
     SweepPlan sw;
-    // lanes per pair slot: 1 (default; a lane forms a pair's whole 6x6 block,
-    // H once) or 2 (SFM_SWEEP_LPP=2: half the rows each)
-    p->sw_lpp = env_int("SFM_SWEEP_LPP", 1) == 2 ? 2 : 1;
+    // lanes per pair slot: 1 (a lane forms a pair's whole 6x6 block, H once;
+    // two lanes with half the rows each: cfg4 0.155 against 0.134 ms, round 3; retired)
+    p->sw_lpp = 1;
     // the persistent reduced solves read the finished payload (finish runs
     // as its own launch): the sweep's dispatch tail may be split
     const char *solve_env = std::getenv("SFM_SOLVE");
@@ -3417,7 +3425,7 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     const int nsweep = p->sw_split.S ? p->sw_split.nfull + NXCD * p->sw_split.nsplit * p->sw_split.S
                                      : NXCD * p->sw_nspec * ceil_div(p->sw_nrange, NXCD);
     const bool fused = p->cl_fused && p->ndiag_items;  // + the camera blocks (after an accepted step)
-    auto sweep_k = p->sw_lpp == 2 ? k_schur_sweep<2> : p->sw_pinhole ? k_schur_sweep<1, true> : k_schur_sweep<1>;
+    auto sweep_k = p->sw_pinhole ? k_schur_sweep<1, true> : k_schur_sweep<1>;
     hipLaunchKernelGGL(sweep_k, dim3(nsweep + (fused ? p->cl_fused_wg : 0)), dim3(SW_THREADS),
                        p->sw_lds_bytes, s, p->sw_nspec, p->sw_nrange, p->sw_nbd, p->sw_L, p->d_sw_rchunk,
                        p->d_sw_nload, p->d_sw_goff, p->d_sw_groups, p->d_sw_lanegrp, p->d_sw_scam,

@@ -54,7 +54,10 @@ constexpr int GPAIRS = 4;        // granule pairs a lane of a published G tile
 constexpr int PBYTES = PPAIRS * 64 * 16;
 constexpr int GBYTES = GPAIRS * 64 * 16;
 constexpr long long POLL_LIMIT = 20000000;  // s_memrealtime ticks (100 MHz): 200 ms
-constexpr int DYN_LDS = 64 * 1024;          // dynamic LDS: the epilogue's scratch, and one workgroup per CU
+constexpr int TREG = 11;                    // tile slots a U wave holds in registers (more would spill)
+constexpr int TREG_L = 10, TLDS_L = 9;      // large systems (77 < nT <= 133): 10 slots in registers, 9 in LDS
+constexpr int DYN_LDS = NUW * TLDS_L * 256 * 8;  // dynamic LDS: those slots, the epilogue's scratch, and
+                                                 // one workgroup per CU
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef unsigned long long u64;
@@ -371,14 +374,34 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
 // the import at its pivot.  Per step: the holder of A_rp forms G_r (and
 // publishes it while r is unpivoted); every U wave applies it to its live
 // tiles j in (p, hi), two tiles' remote G loads in flight at a time.
-template <int TPW>
-__device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int r, int w, int lane, double lambda) {
+// Slots: TR in registers, TLS more in LDS (tl: this wave's [TLS][4][64]
+// doubles; large systems only, the register file holds 11 a wave).
+template <int TR, int TLS>
+__device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int r, int w, int lane, double lambda,
+                                       double *tl) {
+    constexpr int TPW = TR + TLS;
     const int nT = a.nT;
-    d4 T[TPW];
+    d4 T[TR];
+    auto tget = [&](int k) -> d4 {  // k is a constant after unrolling: the branch folds
+        if (k < TR) return T[k < TR ? k : 0];
+        const double *q = tl + (k - TR) * 256 + lane;
+        return d4{q[0], q[64], q[128], q[192]};
+    };
+    auto tset = [&](int k, const d4 &v) {
+        if (k < TR) {
+            T[k < TR ? k : 0] = v;
+            return;
+        }
+        double *q = tl + (k - TR) * 256 + lane;
+        q[0] = v[0];
+        q[64] = v[1];
+        q[128] = v[2];
+        q[192] = v[3];
+    };
 #pragma unroll
     for (int k = 0; k < TPW; ++k) {  // a tile at a time (the loads of all of them at once would spill)
         const int j = w + NUW * k;
-        T[k] = j <= r - 2 ? load_tile(a, lambda, r, j, lane) : zero4();
+        tset(k, j <= r - 2 ? load_tile(a, lambda, r, j, lane) : zero4());
         asm volatile("" ::: "memory");
     }
     for (int p = 0; p < nT; ++p) {
@@ -400,8 +423,8 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
                 const int soff[2] = {gsoff(a, p, need[0] ? j0 : 0), gsoff(a, p, need[1] ? j1 : 0)};
                 u32x4 v[2][GPAIRS];
                 if (!sweep<2, GPAIRS>(rs.G, soff, need, a.tag, v, lane, S)) return false;
-                if (need[0]) T[k] = mfma4(zero4(), dec4(v[0]), lf);
-                if (k + 1 < TPW && need[1]) T[k + 1] = mfma4(zero4(), dec4(v[1]), lf);
+                if (need[0]) tset(k, mfma4(zero4(), dec4(v[0]), lf));
+                if (k + 1 < TPW && need[1]) tset(k + 1, mfma4(zero4(), dec4(v[1]), lf));
             }
             continue;
         }
@@ -415,7 +438,7 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
             d4 tp = zero4();
 #pragma unroll
             for (int k = 0; k < TPW; ++k)
-                if (k == p / NUW) tp = T[k];
+                if (k == p / NUW) tp = tget(k);
             const d4 g = mfma4(zero4(), lv, tp);
             if (r > p) put4(rs.G, gsoff(a, p, r), a.tag, g, lane);
             if (!lds_wait(&S.gdone[s], NW * g_uses(p, r), S)) return false;
@@ -440,19 +463,20 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
             const int soff[2] = {gsoff(a, p, need[0] ? j0 : 0), gsoff(a, p, need[1] ? j1 : 0)};
             u32x4 v[2][GPAIRS];
             if (!sweep<2, GPAIRS>(rs.G, soff, need, a.tag, v, lane, S)) return false;
-            if (need[0]) T[k] = mfma4(T[k], -dec4(v[0]), g);
-            if (k + 1 < TPW && need[1]) T[k + 1] = mfma4(T[k + 1], -dec4(v[1]), g);
+            if (need[0]) tset(k, mfma4(tget(k), -dec4(v[0]), g));
+            if (k + 1 < TPW && need[1]) tset(k + 1, mfma4(tget(k + 1), -dec4(v[1]), g));
         }
         if (w == 0) stamp(a, p, DBG_UDONE);
     }
     return true;
 }
 
-template <int TPW>
+template <int TR, int TLS>
 __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
     if (a.gate && !*a.gate) return;  // device-side LM control: iteration gated off
     __shared__ Smem S;
-    extern __shared__ __attribute__((aligned(16))) double dyn[];  // epilogue scratch (DYN_LDS bytes)
+    extern __shared__ __attribute__((aligned(16))) double dyn[];  // LDS tile slots, then the epilogue's scratch
+    static_assert(NUW * TLS * 256 * sizeof(double) <= DYN_LDS, "LDS tile slots");
     stamp(a, a.nT, DBG_START);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = blockIdx.x;
     const double lambda = *a.lam;
@@ -467,7 +491,7 @@ __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
     rs.G = __builtin_amdgcn_make_buffer_rsrc(a.G, (short)0, a.nT * a.nT * GBYTES, 0x00020000);
     __syncthreads();
     if (wave == 0) w0_loop(a, rs, S, r, lane, lambda);
-    else u_loop<TPW>(a, rs, S, r, wave - 1, lane, lambda);
+    else u_loop<TR, TLS>(a, rs, S, r, wave - 1, lane, lambda, dyn + (wave - 1) * TLS * 256);
     // every owner arrives (an aborted one too, so the count stays whole); the
     // last one forms the trial cameras unless the solve failed
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // W0's x stores drained before the barrier

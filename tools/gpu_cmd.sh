@@ -9,8 +9,10 @@ step() {  # step NAME SECONDS CMD...
     echo "[$name] rc=$rc"; tail -4 "gpurun_out/$name.txt"
     if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
-step t1 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "reduced_solve or gj_solve_matches or cfg4_matches or cfg5_matches"
+step t1 400 python -u -m pytest -v --timeout 120 --timeout-method thread tests -m gpu
 step tl300 120 python -u tools/gjr_timeline.py 300
 step tl1200 120 python -u tools/gjr_timeline.py 1200
 step ab1 300 python -u tools/gj_ab.py SFM_SOLVE gjr,gjseg 2
 step ab2 300 python -u tools/gj_ab.py SFM_SWEEP_SPLIT 8,0 2
+step draw 120 python -u tools/draw_bench.py
+step bench 600 python -u bench.py --no-cpu-baseline --no-next-rows
