@@ -1370,10 +1370,27 @@ __device__ __forceinline__ double assembled_b(const double *__restrict__ payload
 struct SlabSrc {
     const double *slab, *camlin;  // slab == nullptr: read the finished payload
     int32_t nbd, nrange;
+    SweepSplit sp;                // the dispatch tail's split (sp.S = 0: none)
+    const int32_t *split_of;
 };
 
 __device__ __forceinline__ double slab_sum(const SlabSrc &q, int64_t blk, int item) {
     double v = 0;
+    const int si = q.sp.S > 0 ? q.split_of[blk] : -1;
+    if (si >= 0) {  // a split spec's block: every (range, sub-range) partial, in order (k_schur_finish's)
+        const int64_t row = (int64_t)q.sp.nsplit * q.sp.gmax * ITEM_W;
+        const double *src = q.sp.slabx + (int64_t)si * ITEM_W + item;
+        const int n = q.nrange * q.sp.S;
+        for (int r0 = 0; r0 < n; r0 += 8) {
+            double x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = r0 + u < n ? src[(r0 + u) * row] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (r0 + u < n) v += x[u];
+        }
+        return v;
+    }
     const int64_t stride = (int64_t)q.nbd * ITEM_W;
     const double *src = q.slab + blk * ITEM_W + item;
     for (int r0 = 0; r0 < q.nrange; r0 += 8) {  // 8 loads in flight, then the sum in range order
@@ -2160,8 +2177,10 @@ struct GjrBufs {
     }
 };
 static int launch_gjr(const GjrPlan &g, int32_t ns, const double *payload, const double *lam, const GjrBufs &b,
-                      unsigned tag, double *x, int *bad, const int *gate, const CamTrialArgs &ct, hipStream_t s) {
+                      unsigned tag, double *x, int *bad, const int *gate, const CamTrialArgs &ct, hipStream_t s,
+                      const SlabSrc &src = SlabSrc{nullptr, nullptr, 0, 0, {}, nullptr}) {
     gjr::Args a;
+    a.src = src;
     a.payload = payload;
     a.ns = ns;
     a.nT = g.nT;
@@ -2688,7 +2707,7 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     // the dispatch tail: one workgroup per CU (SW_THREADS, 168 VGPRs), so
     // items run in rounds of ncu; a short last round's specs are split per
     // range into S chunk sub-ranges (SFM_SWEEP_SPLIT=0: off).  Not with the
-    // Cholesky solve, whose first launch reads the slabs itself (SlabSrc).
+    // SlabSrc reads the partials in the finish's order when it is folded in.
     P.split_of.assign(P.nbd, -1);
     {
         const int per_round = ncu / NXCD;  // specs of one range group per round
@@ -3012,11 +3031,9 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     // lanes per pair slot: 1 (a lane forms a pair's whole 6x6 block, H once;
     // two lanes with half the rows each: cfg4 0.155 against 0.134 ms, round 3; retired)
     p->sw_lpp = 1;
-    // the persistent reduced solves read the finished payload (finish runs
-    // as its own launch): the sweep's dispatch tail may be split
-    const char *solve_env = std::getenv("SFM_SOLVE");
-    const bool split_ok = p->tb == 16 && !(solve_env && std::strcmp(solve_env, "chol") == 0) &&
-                          p->nT <= gj::NTMAX;
+    // the solves read the split partials in k_schur_finish's order (SlabSrc
+    // when the finish is folded in): the sweep's dispatch tail may be split
+    const bool split_ok = true;
     plan_sweep(nc, np_, no, cam, pt, pstart, cnt, p->sw_lpp, device_cus(device), split_ok, sw);
     if (sw.buf_slots > SW_MAX_STAGED) {  // one point with more observations in a spec's cameras than a round holds
         set_error("sweep plan: %d observations of one spec's cameras in a single point range (max %d)", sw.buf_slots,
@@ -3435,7 +3452,7 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     SFM_HIP(hipGetLastError());
     // one rank: the solve's first launch sums the slabs itself (SlabSrc)
     // (the persistent solve reads the finished payload: the finish runs as its own launch)
-    const bool fin_fused = !p->comm && p->fin_fused && !p->gjp.cb && !p->gjrp.ok() && !p->sw_split.S;
+    const bool fin_fused = !p->comm && p->fin_fused && !p->gjp.cb;
     if (!fin_fused) {
         hipLaunchKernelGGL(k_schur_finish, dim3(p->sw_nbd), dim3(64), 0, s, p->ns, p->sw_nbd, p->sw_nrange,
                            p->d_sw_blkij, p->d_slab, p->d_camlin, p->d_payload, gst, p->d_sw_split_of, p->sw_split);
@@ -3448,8 +3465,8 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SOLVE], s));
     // the back substitution's epilogue forms the trial cameras (k_camera_trial's work)
     const CamTrialArgs ct = {p->nc, p->ns, p->d_payload, lam, p->d_Rt, p->d_Rt2, p->d_scal + 4};
-    const SlabSrc src = fin_fused ? SlabSrc{p->d_slab, p->d_camlin, p->sw_nbd, p->sw_nrange}
-                                  : SlabSrc{nullptr, nullptr, 0, 0};
+    const SlabSrc src = fin_fused ? SlabSrc{p->d_slab, p->d_camlin, p->sw_nbd, p->sw_nrange, p->sw_split, p->d_sw_split_of}
+                                  : SlabSrc{nullptr, nullptr, 0, 0, {}, nullptr};
     if (p->gjp.cb || p->gjrp.ok()) {
         LocalGroup *lg = p->comm ? p->comm->local : nullptr;
         std::unique_lock<std::mutex> lk;
@@ -3458,7 +3475,8 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
             if (lg->last_solve) SFM_HIP(hipStreamWaitEvent(s, lg->last_solve, 0));
         }
         if (p->gjrp.ok()) {
-            if ((rc = launch_gjr(p->gjrp, p->ns, p->d_payload, lam, p->gjrb, ++p->gjr_tag, p->d_b, bad, gst, ct, s)))
+            if ((rc = launch_gjr(p->gjrp, p->ns, p->d_payload, lam, p->gjrb, ++p->gjr_tag, p->d_b, bad, gst, ct, s,
+                                 src)))
                 return rc;
         } else if ((rc = launch_gj(p->gjp, p->nT, p->ns, p->d_payload, lam, p->gjb, ++p->gj_epoch, p->d_b, bad,
                                    gst, ct, s)))

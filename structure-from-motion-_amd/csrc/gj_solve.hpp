@@ -642,7 +642,8 @@ __device__ __forceinline__ void updater(const Args &a, const Geo &g, Smem &S, in
 template <int NTH>
 __device__ __attribute__((noinline)) void cam_trial(int nc, const double *Rt, double *Rt_new, double *cam_out,
                                                     double lambda, const double *payload, int32_t ns,
-                                                    const double *dc, double *red) {
+                                                    const double *dc, double *red, const double *camlin = nullptr) {
+    // diag U and g_c: the payload's vectors, or (finish folded into the solve) the camera blocks themselves
     const double *du = payload + pay_vec_base(ns), *gc = du + ns;
     double m = 0, dn = 0, xn = 0;
     constexpr int NWT = NTH / 64;
@@ -659,7 +660,9 @@ __device__ __attribute__((noinline)) void cam_trial(int nc, const double *Rt, do
             xn += R[9 + i] * R[9 + i];
         }
         for (int i = 0; i < 6; ++i) {
-            m += d[i] * (lambda * clampd(du[6 * c + i]) * d[i] - gc[6 * c + i]);
+            const double u = camlin ? cam_u(camlin, c, i, i) : du[6 * c + i];
+            const double g = camlin ? camlin[CAMLIN * c + 21 + i] : gc[6 * c + i];
+            m += d[i] * (lambda * clampd(u) * d[i] - g);
             dn += d[i] * d[i];
         }
     }

@@ -65,6 +65,7 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 struct Args {
     const double *payload;  // the finished (all-reduced) Schur payload
+    SlabSrc src;            // one rank: the sweep's slabs read directly (k_schur_finish folded in), or none
     int32_t ns, nT;
     const double *lam;
     const int *gate;
@@ -223,7 +224,18 @@ __device__ __forceinline__ double gy(const d4 &g, double yl, int lane) {
 
 // tile A_rj of the damped, identity-padded system, held as the accumulator
 // of A_rj^T: element e of lane l = A(16 r + (l & 15), 16 j + (l >> 4) + 4e)
+// from the slabs: the finish's sums, in its order (the same bits); out of
+// line, so that the callers' unrolled slot loops stay small
+__device__ __attribute__((noinline)) d4 load_tile_src(const SlabSrc &q, const double *payload, int32_t ns,
+                                                      double lambda, int r, int j, int lane) {
+    d4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        v[e] = assembled_src(q, payload, ns, lambda, TL * r + (lane & 15), TL * j + (lane >> 4) + 4 * e);
+    return v;
+}
 __device__ __forceinline__ d4 load_tile(const Args &a, double lambda, int r, int j, int lane) {
+    if (a.src.slab) return load_tile_src(a.src, a.payload, a.ns, lambda, r, j, lane);
     gj::ElemRef er[4];
     double v[4], dg[4];
 #pragma unroll
@@ -296,7 +308,7 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
     const int nT = a.nT, li = lane & 15;
     d4 Tm = r > 0 ? load_tile(a, lambda, r, r - 1, lane) : zero4();
     d4 Td = load_tile(a, lambda, r, r, lane);
-    double b = assembled_b(a.payload, a.ns, TL * r + li);
+    double b = assembled_b_src(a.src, a.payload, a.ns, TL * r + li);
     stamp(a, nT, DBG_PROLOGUE);
     for (int p = 0; p < nT; ++p) {
         const int s = p & (RING - 1);
@@ -402,7 +414,6 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
     for (int k = 0; k < TPW; ++k) {  // a tile at a time (the loads of all of them at once would spill)
         const int j = w + NUW * k;
         tset(k, j <= r - 2 ? load_tile(a, lambda, r, j, lane) : zero4());
-        asm volatile("" ::: "memory");
     }
     for (int p = 0; p < nT; ++p) {
         const int s = p & (RING - 1);
@@ -511,7 +522,8 @@ __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
     for (int i = threadIdx.x; i < 6 * a.ct.nc; i += THREADS)
         dc[i] = __hip_atomic_load(a.x + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    gj::cam_trial<THREADS>(a.ct.nc, a.ct.Rt, a.ct.Rt_new, a.ct.cam_out, *a.lam, a.payload, a.ns, dc, red);
+    gj::cam_trial<THREADS>(a.ct.nc, a.ct.Rt, a.ct.Rt_new, a.ct.cam_out, *a.lam, a.payload, a.ns, dc, red,
+                           a.src.slab ? a.src.camlin : nullptr);
 }
 
 }  // namespace gjr
