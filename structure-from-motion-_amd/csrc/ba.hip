@@ -2711,7 +2711,7 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     P.split_of.assign(P.nbd, -1);
     {
         const int per_round = ncu / NXCD;  // specs of one range group per round
-        const int want = env_int("SFM_SWEEP_SPLIT", 8);
+        const int want = env_int("SFM_SWEEP_SPLIT", 0);  // off: cfg5 0.341 (none) vs 0.362 ms (S = 8), round 4
         int min_chunks = INT32_MAX;
         for (int r = 0; r < P.nrange; ++r) min_chunks = std::min(min_chunks, P.rchunk[r + 1] - P.rchunk[r]);
         const int nsplit = P.nspec % std::max(1, per_round);
@@ -2857,6 +2857,7 @@ struct sfm_ba_problem {
     GjrPlan gjrp;  // the row-distributed solve (default; gjp is then unused)
     GjrBufs gjrb;
     unsigned gjr_tag = 0;
+    bool gjr_fold = false;  // fold k_schur_finish into the row-distributed solve (SFM_GJR_FOLD)
     hipEvent_t ev_solve = nullptr;
     double t_acc[T_NT] = {};
     int t_iters = 0;
@@ -3452,7 +3453,10 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     SFM_HIP(hipGetLastError());
     // one rank: the solve's first launch sums the slabs itself (SlabSrc)
     // (the persistent solve reads the finished payload: the finish runs as its own launch)
-    const bool fin_fused = !p->comm && p->fin_fused && !p->gjp.cb;
+    // (the row-distributed solve only with SFM_GJR_FOLD=1: its prologue then
+    // reads 8 range slabs per element while the chain runs, cfg5 solve 0.457
+    // -> 0.523 ms against the finish's 0.028 ms, round 4)
+    const bool fin_fused = !p->comm && p->fin_fused && !p->gjp.cb && (!p->gjrp.ok() || p->gjr_fold);
     if (!fin_fused) {
         hipLaunchKernelGGL(k_schur_finish, dim3(p->sw_nbd), dim3(64), 0, s, p->ns, p->sw_nbd, p->sw_nrange,
                            p->d_sw_blkij, p->d_slab, p->d_camlin, p->d_payload, gst, p->d_sw_split_of, p->sw_split);
@@ -3546,6 +3550,7 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
     // A/B switches (read per solve): DPP tile factor, finish folded into the solve
     p->chol_dpp = env_int("SFM_CHOL_DPP", 1) != 0;
     p->fin_fused = env_int("SFM_FINISH_FUSED", 1) != 0;
+    p->gjr_fold = env_int("SFM_GJR_FOLD", 0) != 0;
     p->sw_debug = env_int("SFM_SWEEP_DEBUG", 0) | (env_int("SFM_SWEEP_SYNC", 1) ? 0 : 16);
     (void)hipGetLastError();
     const auto t0 = std::chrono::steady_clock::now();

@@ -157,17 +157,31 @@ __device__ __forceinline__ bool lds_wait(const int *w, int target, Smem &S) {
 // polled by sc1 buffer loads; a record is PAIRS rows of 64 lanes x 16 bytes,
 // so every instruction moves 1 KB contiguous.  The descriptors are built from
 // kernel arguments (wave-uniform: no waterfall loops), offsets are 32-bit.
-struct Rs {
-    __amdgpu_buffer_rsrc_t P, G;
+// The descriptor is rebuilt at every use from readfirstlane'd words and the
+// record offset is readfirstlane'd too: a descriptor or soffset the compiler
+// cannot prove wave-uniform wraps every buffer op in a waterfall loop
+// (cdna_hip_programming.md T20), which serialised this solve's hand-offs.
+struct Buf {
+    const void *base;
+    int bytes;
 };
+struct Rs {
+    Buf P, G;
+};
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const Buf &b) {
+    const u64 a = (u64)b.base;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(((u64)hi << 32) | lo), (short)0,
+                                             __builtin_amdgcn_readfirstlane(b.bytes), 0x00020000);
+}
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 constexpr int SC1 = 16;  // buffer op aux: sc1 (write-through stores, L2-served loads)
-__device__ __forceinline__ void put_pair(__amdgpu_buffer_rsrc_t rs, int soff, int e, unsigned tag, double v,
-                                         int lane) {
+__device__ __forceinline__ void put_pair(const Buf &bf, int soff, int e, unsigned tag, double v, int lane) {
     const u64 b = (u64)__double_as_longlong(v);
     const u32x4 w = {(unsigned)b, tag, (unsigned)(b >> 32), tag};
-    __builtin_amdgcn_raw_buffer_store_b128(w, rs, e * 1024 + lane * 16, soff, SC1);
+    __builtin_amdgcn_raw_buffer_store_b128(w, rsrc(bf), e * 1024 + lane * 16, uni(soff), SC1);
 }
-__device__ __forceinline__ void put4(__amdgpu_buffer_rsrc_t rs, int soff, unsigned tag, const d4 &v, int lane) {
+__device__ __forceinline__ void put4(const Buf &rs, int soff, unsigned tag, const d4 &v, int lane) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) put_pair(rs, soff, e, tag, v[e], lane);
 }
@@ -177,17 +191,29 @@ __device__ __forceinline__ double dec(const u32x4 &x) {
 // ONE wave re-reads the N pairs of NR records (all loads in flight) until
 // every tag of every lane matches; false on abort / timeout
 template <int NR, int N>
-__device__ __forceinline__ bool sweep(__amdgpu_buffer_rsrc_t rs, const int (&soff)[NR], const bool (&need)[NR],
+__device__ __forceinline__ bool sweep(const Buf &bf, const int (&soff)[NR], const bool (&need)[NR],
                                       unsigned tag, u32x4 (&x)[NR][N], int lane, Smem &S) {
     long long t0 = -1;
+    int so[NR], nd[NR];  // both through readfirstlane: scalar branches around the loads
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+        so[q] = uni(soff[q]);
+        nd[q] = uni((int)need[q]);
+    }
     for (unsigned it = 1;; ++it) {
         asm volatile("" ::: "memory");  // every pass reloads
+        const __amdgpu_buffer_rsrc_t rs = rsrc(bf);
 #pragma unroll
-        for (int q = 0; q < NR; ++q)
+        for (int q = 0; q < NR; ++q) {
+            if (nd[q]) {
 #pragma unroll
-            for (int k = 0; k < N; ++k)
-                x[q][k] = need[q] ? __builtin_amdgcn_raw_buffer_load_b128(rs, k * 1024 + lane * 16, soff[q], SC1)
-                                  : u32x4{0u, tag, 0u, tag};
+                for (int k = 0; k < N; ++k)
+                    x[q][k] = __builtin_amdgcn_raw_buffer_load_b128(rs, k * 1024 + lane * 16, so[q], SC1);
+            } else {
+#pragma unroll
+                for (int k = 0; k < N; ++k) x[q][k] = u32x4{0u, tag, 0u, tag};
+            }
+        }
         bool ok = true;
 #pragma unroll
         for (int q = 0; q < NR; ++q)
@@ -224,18 +250,14 @@ __device__ __forceinline__ double gy(const d4 &g, double yl, int lane) {
 
 // tile A_rj of the damped, identity-padded system, held as the accumulator
 // of A_rj^T: element e of lane l = A(16 r + (l & 15), 16 j + (l >> 4) + 4e)
-// from the slabs: the finish's sums, in its order (the same bits); out of
-// line, so that the callers' unrolled slot loops stay small
-__device__ __attribute__((noinline)) d4 load_tile_src(const SlabSrc &q, const double *payload, int32_t ns,
-                                                      double lambda, int r, int j, int lane) {
-    d4 v;
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-        v[e] = assembled_src(q, payload, ns, lambda, TL * r + (lane & 15), TL * j + (lane >> 4) + 4 * e);
-    return v;
-}
 __device__ __forceinline__ d4 load_tile(const Args &a, double lambda, int r, int j, int lane) {
-    if (a.src.slab) return load_tile_src(a.src, a.payload, a.ns, lambda, r, j, lane);
+    if (a.src.slab) {  // from the slabs: the finish's sums, in its order (the same bits)
+        d4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            v[e] = assembled_src(a.src, a.payload, a.ns, lambda, TL * r + (lane & 15), TL * j + (lane >> 4) + 4 * e);
+        return v;
+    }
     gj::ElemRef er[4];
     double v[4], dg[4];
 #pragma unroll
@@ -410,10 +432,17 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
         q[128] = v[2];
         q[192] = v[3];
     };
-#pragma unroll
-    for (int k = 0; k < TPW; ++k) {  // a tile at a time (the loads of all of them at once would spill)
+    // a tile at a time, in a loop that is not unrolled (the loads of all of
+    // them at once would spill; unrolled, the slab loads make it too large to
+    // keep the slots in registers): the slot is chosen by selects
+#pragma unroll 1
+    for (int k = 0; k < TPW; ++k) {
         const int j = w + NUW * k;
-        tset(k, j <= r - 2 ? load_tile(a, lambda, r, j, lane) : zero4());
+        const d4 v = j <= r - 2 ? load_tile(a, lambda, r, j, lane) : zero4();
+#pragma unroll
+        for (int kk = 0; kk < TR; ++kk)
+            if (kk == k) T[kk] = v;
+        if (k >= TR) tset(k, v);
     }
     for (int p = 0; p < nT; ++p) {
         const int s = p & (RING - 1);
@@ -498,11 +527,14 @@ __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
         S.bad = a.bad;
     }
     Rs rs;
-    rs.P = __builtin_amdgcn_make_buffer_rsrc(a.P, (short)0, a.nT * PBYTES, 0x00020000);
-    rs.G = __builtin_amdgcn_make_buffer_rsrc(a.G, (short)0, a.nT * a.nT * GBYTES, 0x00020000);
+    rs.P = Buf{a.P, a.nT * PBYTES};
+    rs.G = Buf{a.G, a.nT * a.nT * GBYTES};
     __syncthreads();
-    if (wave == 0) w0_loop(a, rs, S, r, lane, lambda);
-    else u_loop<TR, TLS>(a, rs, S, r, wave - 1, lane, lambda, dyn + (wave - 1) * TLS * 256);
+    // the wave index through readfirstlane: provably uniform, so the slot
+    // tests are scalar branches, not exec-masked ones around every load
+    const int wu = uni(wave);
+    if (wu == 0) w0_loop(a, rs, S, r, lane, lambda);
+    else u_loop<TR, TLS>(a, rs, S, r, wu - 1, lane, lambda, dyn + (wu - 1) * TLS * 256);
     // every owner arrives (an aborted one too, so the count stays whole); the
     // last one forms the trial cameras unless the solve failed
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // W0's x stores drained before the barrier

@@ -9,10 +9,11 @@ step() {  # step NAME SECONDS CMD...
     echo "[$name] rc=$rc"; tail -4 "gpurun_out/$name.txt"
     if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
-step t1 400 python -u -m pytest -v --timeout 120 --timeout-method thread tests -m gpu
+step t1 400 python -u -m pytest -q --timeout 120 --timeout-method thread tests -m gpu
 step tl300 120 python -u tools/gjr_timeline.py 300
 step tl1200 120 python -u tools/gjr_timeline.py 1200
-step ab1 300 python -u tools/gj_ab.py SFM_SOLVE gjr,gjseg 2
-step ab2 300 python -u tools/gj_ab.py SFM_SWEEP_SPLIT 8,0 2
-step draw 120 python -u tools/draw_bench.py
-step bench 600 python -u bench.py --no-cpu-baseline --no-next-rows
+step ab1 300 python -u tools/gj_ab.py SFM_SOLVE gjr,gjseg 3
+step swt0 120 env SFM_SWEEP_SPLIT=0 python -u tools/sweep_timeline.py cfg5
+step swt8 120 env SFM_SWEEP_SPLIT=8 python -u tools/sweep_timeline.py cfg5
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+step kt5 200 rocprofv3 --kernel-trace --stats -d gpurun_out/kt5 -o run --output-format csv -- python tools/ba_once.py cfg5 20

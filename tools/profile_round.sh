@@ -25,4 +25,18 @@ for W in cfg4 cfg5; do
     fi
   done
 done
+# RANSAC (cfg2 drop-in calls): kernel trace and the FP64 / VALU counters of
+# k_fit_samples and k_ransac_score (the executed-flop count behind bench's
+# algorithmic-equivalent score rate)
+W=ransac
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $OUT/$W/kernel_trace -o run --output-format csv -- python tools/ransac_once.py > $OUT/kt_$W.log 2>&1 || exit 1
+for C in "SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64" \
+         "SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES" FETCH_SIZE; do
+  tag=$(echo $C | tr ' ' '_')
+  if timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/$W/$tag -o run -- python tools/ransac_once.py > $OUT/pmc_${W}_$tag.log 2>&1; then
+    echo "$W $tag ok" >> $OUT/passes.log
+  else
+    echo "$W $tag FAILED $?" >> $OUT/passes.log
+  fi
+done
 echo DONE
