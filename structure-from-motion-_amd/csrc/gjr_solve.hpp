@@ -105,8 +105,10 @@ __device__ __forceinline__ int lds_ld(const int *w) {
 __device__ __forceinline__ void lds_set(int *w, int v) {
     __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// a wave's count: ONE lane adds (called by every lane, the atomic optimiser
+// would fold the wave's adds into one add of 64)
 __device__ __forceinline__ void lds_add(int *w, int v) {
-    __hip_atomic_fetch_add(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); }
 __device__ __forceinline__ void lds_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }

@@ -6,14 +6,11 @@ step() {  # step NAME SECONDS CMD...
     local name=$1 t=$2; shift 2
     timeout -k 10 "$t" "$@" > "gpurun_out/$name.txt" 2>&1
     local rc=$?
-    echo "[$name] rc=$rc"; tail -4 "gpurun_out/$name.txt"
+    echo "[$name] rc=$rc"; grep -v amdgpu.ids "gpurun_out/$name.txt" | tail -${TAILN:-6}
     if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
+TAILN=8 step acc 120 python -u tools/gjr_accuracy.py
 step t1 400 python -u -m pytest -q --timeout 120 --timeout-method thread tests -m gpu
 step tl300 120 python -u tools/gjr_timeline.py 300
 step tl1200 120 python -u tools/gjr_timeline.py 1200
 step ab1 300 python -u tools/gj_ab.py SFM_SOLVE gjr,gjseg 3
-step swt0 120 env SFM_SWEEP_SPLIT=0 python -u tools/sweep_timeline.py cfg5
-step swt8 120 env SFM_SWEEP_SPLIT=8 python -u tools/sweep_timeline.py cfg5
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-step kt5 200 rocprofv3 --kernel-trace --stats -d gpurun_out/kt5 -o run --output-format csv -- python tools/ba_once.py cfg5 20
