@@ -159,10 +159,15 @@ __device__ __forceinline__ bool lds_wait(const int *w, int target, Smem &S) {
 // polled by sc1 buffer loads; a record is PAIRS rows of 64 lanes x 16 bytes,
 // so every instruction moves 1 KB contiguous.  The descriptors are built from
 // kernel arguments (wave-uniform: no waterfall loops), offsets are 32-bit.
-// The descriptor is rebuilt at every use from readfirstlane'd words and the
-// record offset is readfirstlane'd too: a descriptor or soffset the compiler
-// cannot prove wave-uniform wraps every buffer op in a waterfall loop
-// (cdna_hip_programming.md T20), which serialised this solve's hand-offs.
+// The descriptor is rebuilt at every use from readfirstlane'd words: one the
+// compiler cannot prove wave-uniform wraps every buffer op in a waterfall
+// loop (cdna_hip_programming.md T20), which serialised this solve's
+// hand-offs.  A store's record offset rides in the per-lane voffset
+// (soffset 0): the same offset handed to the soffset through readfirstlane
+// gave wrong, nondeterministic (~1e-6) solves on gfx950 although every lane
+// holds the same value (cause not isolated; the voffset form is exact and
+// as fast -- DESIGN.md section 6).  The polls' offsets stay readfirstlane'd
+// soffsets (exact; a voffset there costs VGPRs and spills the tile slots).
 struct Buf {
     const void *base;
     int bytes;
@@ -176,12 +181,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const Buf &b) {
     return __builtin_amdgcn_make_buffer_rsrc((void *)(((u64)hi << 32) | lo), (short)0,
                                              __builtin_amdgcn_readfirstlane(b.bytes), 0x00020000);
 }
-__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 constexpr int SC1 = 16;  // buffer op aux: sc1 (write-through stores, L2-served loads)
 __device__ __forceinline__ void put_pair(const Buf &bf, int soff, int e, unsigned tag, double v, int lane) {
     const u64 b = (u64)__double_as_longlong(v);
     const u32x4 w = {(unsigned)b, tag, (unsigned)(b >> 32), tag};
-    __builtin_amdgcn_raw_buffer_store_b128(w, rsrc(bf), e * 1024 + lane * 16, uni(soff), SC1);
+    __builtin_amdgcn_raw_buffer_store_b128(w, rsrc(bf), soff + e * 1024 + lane * 16, 0, SC1);
 }
 __device__ __forceinline__ void put4(const Buf &rs, int soff, unsigned tag, const d4 &v, int lane) {
 #pragma unroll
@@ -196,21 +200,15 @@ template <int NR, int N>
 __device__ __forceinline__ bool sweep(const Buf &bf, const int (&soff)[NR], const bool (&need)[NR],
                                       unsigned tag, u32x4 (&x)[NR][N], int lane, Smem &S) {
     long long t0 = -1;
-    int so[NR], nd[NR];  // both through readfirstlane: scalar branches around the loads
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-        so[q] = uni(soff[q]);
-        nd[q] = uni((int)need[q]);
-    }
     for (unsigned it = 1;; ++it) {
         asm volatile("" ::: "memory");  // every pass reloads
         const __amdgpu_buffer_rsrc_t rs = rsrc(bf);
 #pragma unroll
         for (int q = 0; q < NR; ++q) {
-            if (nd[q]) {
+            if (need[q]) {
 #pragma unroll
                 for (int k = 0; k < N; ++k)
-                    x[q][k] = __builtin_amdgcn_raw_buffer_load_b128(rs, k * 1024 + lane * 16, so[q], SC1);
+                    x[q][k] = __builtin_amdgcn_raw_buffer_load_b128(rs, k * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(soff[q]), SC1);
             } else {
 #pragma unroll
                 for (int k = 0; k < N; ++k) x[q][k] = u32x4{0u, tag, 0u, tag};
@@ -532,9 +530,7 @@ __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
     rs.P = Buf{a.P, a.nT * PBYTES};
     rs.G = Buf{a.G, a.nT * a.nT * GBYTES};
     __syncthreads();
-    // the wave index through readfirstlane: provably uniform, so the slot
-    // tests are scalar branches, not exec-masked ones around every load
-    const int wu = uni(wave);
+    const int wu = __builtin_amdgcn_readfirstlane(wave);  // provably uniform: scalar record offsets
     if (wu == 0) w0_loop(a, rs, S, r, lane, lambda);
     else u_loop<TR, TLS>(a, rs, S, r, wu - 1, lane, lambda, dyn + (wu - 1) * TLS * 256);
     // every owner arrives (an aborted one too, so the count stays whole); the

@@ -1,10 +1,10 @@
 """Dev probe (round 3): A/B of a BA setting (SFM_* variable) on one box -- the BA
 solve at cfg4 / cfg5 (20 fixed LM iterations, HIP-event kernel split),
 alternating the environment variable given on the command line between its
-values, several rounds.  Usage: gj_ab.py VAR v1,v2 [rounds]"""
+values, several rounds.  Usage: gj_ab.py VAR v1,v2 [rounds [pkgdir]]"""
 import os, sys
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, R + '/structure-from-motion-_amd')
+sys.path.insert(0, sys.argv[4] if len(sys.argv) > 4 else R + '/structure-from-motion-_amd')
 import numpy as np, _sfmcore as c, sfm_synthetic as syn
 var, vals = sys.argv[1], sys.argv[2].split(",")
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3

@@ -6,11 +6,10 @@ step() {  # step NAME SECONDS CMD...
     local name=$1 t=$2; shift 2
     timeout -k 10 "$t" "$@" > "gpurun_out/$name.txt" 2>&1
     local rc=$?
-    echo "[$name] rc=$rc"; grep -v amdgpu.ids "gpurun_out/$name.txt" | tail -${TAILN:-6}
+    echo "[$name] rc=$rc"; grep -v amdgpu.ids "gpurun_out/$name.txt" | tail -${TAILN:-8}
     if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
-TAILN=8 step acc 120 python -u tools/gjr_accuracy.py
-step t1 400 python -u -m pytest -q --timeout 120 --timeout-method thread tests -m gpu
+step acc 120 python -u tools/gjr_accuracy.py
+step t1 500 python -u -m pytest -q --timeout 120 --timeout-method thread tests -m gpu
 step tl300 120 python -u tools/gjr_timeline.py 300
 step tl1200 120 python -u tools/gjr_timeline.py 1200
-step ab1 300 python -u tools/gj_ab.py SFM_SOLVE gjr,gjseg 3
