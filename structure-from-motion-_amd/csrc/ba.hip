@@ -2165,13 +2165,21 @@ static GjrPlan gjr_plan(int nT, int ncu) {
 // granule records (zeroed once; tags only grow) and the err / arrival words
 struct GjrBufs {
     gjr::u64 *P = nullptr, *G = nullptr;
+    double *Gd = nullptr;
+    unsigned *Gf = nullptr;
     int *err = nullptr;
     unsigned *arrive = nullptr;
-    static size_t words(int nT) { return ((size_t)nT * gjr::PBYTES + (size_t)nT * nT * gjr::GBYTES) / 8; }
+    static size_t words(int nT) {
+        const size_t t = (size_t)nT * nT;
+        return ((size_t)nT * gjr::PBYTES + t * gjr::GBYTES + t * gjr::GDBYTES) / 8 + (t + 1) / 2;
+    }
     static constexpr size_t ints = 64;
     void carve(gjr::u64 *w, int *i, int nT) {
+        const size_t t = (size_t)nT * nT;
         P = w;
-        G = w + (size_t)nT * gjr::PBYTES / 8;
+        G = P + (size_t)nT * gjr::PBYTES / 8;
+        Gd = reinterpret_cast<double *>(G + t * gjr::GBYTES / 8);
+        Gf = reinterpret_cast<unsigned *>(Gd + t * gjr::GDBYTES / 8);
         err = i;
         arrive = reinterpret_cast<unsigned *>(i + 32);
     }
@@ -2188,6 +2196,8 @@ static int launch_gjr(const GjrPlan &g, int32_t ns, const double *payload, const
     a.gate = gate;
     a.P = b.P;
     a.G = b.G;
+    a.Gd = b.Gd;
+    a.Gf = b.Gf;
     a.tag = tag;
     a.x = x;
     a.bad = bad;

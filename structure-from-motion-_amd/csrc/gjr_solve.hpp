@@ -53,6 +53,8 @@ constexpr int PPAIRS = 5;        // granule pairs a lane of a pivot record: L^-1
 constexpr int GPAIRS = 4;        // granule pairs a lane of a published G tile
 constexpr int PBYTES = PPAIRS * 64 * 16;
 constexpr int GBYTES = GPAIRS * 64 * 16;
+constexpr int GDBYTES = 2 * 64 * 16;  // a G tile untagged: two 16-byte rows of 64 lanes (the bulk copy)
+constexpr int NB = 4;                 // bulk G tiles a U wave has in flight
 constexpr long long POLL_LIMIT = 20000000;  // s_memrealtime ticks (100 MHz): 200 ms
 constexpr int TREG = 11;                    // tile slots a U wave holds in registers (more would spill)
 constexpr int TREG_L = 10, TLDS_L = 9;      // large systems (77 < nT <= 133): 10 slots in registers, 9 in LDS
@@ -70,7 +72,9 @@ struct Args {
     const double *lam;
     const int *gate;
     u64 *P;         // [nT] pivot records of PBYTES
-    u64 *G;         // [nT][nT] G_r of step p at (p, r), GBYTES each
+    u64 *G;         // [nT][nT] G_r of step p at (p, r), GBYTES each (granules: W0 of owner r + 1)
+    double *Gd;     // [nT][nT] the same untagged, GDBYTES each (the U waves' bulk updates) ...
+    unsigned *Gf;   // [nT][nT] ... published by a flag (= tag) behind the drained stores
     unsigned tag;   // this launch's granule tag (>= 1)
     double *x;      // [nT * 16] solution
     int *bad;       // not positive definite (the LM rejects the step)
@@ -80,7 +84,7 @@ struct Args {
     long long *dbg;   // diagnostics (nullable): [grid][nT + 1][16] s_memrealtime stamps
 };
 
-enum { DBG_PIN = 0, DBG_GCRIT, DBG_CHAIN0, DBG_CHAIN1, DBG_PPUB, DBG_GHOLD, DBG_UDONE, DBG_GREM };
+enum { DBG_PIN = 0, DBG_GCRIT, DBG_CHAIN0, DBG_CHAIN1, DBG_PPUB, DBG_GHOLD, DBG_UDONE, DBG_GREM, DBG_PLW, DBG_GRDY, DBG_HPRDY };
 enum { DBG_START = 0, DBG_PROLOGUE, DBG_W0END, DBG_ARRIVED };
 __device__ __forceinline__ void stamp(const Args &a, int p, int slot) {
     if (a.dbg && (threadIdx.x & 63) == 0)
@@ -173,7 +177,7 @@ struct Buf {
     int bytes;
 };
 struct Rs {
-    Buf P, G;
+    Buf P, G, Gd;
 };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const Buf &b) {
     const u64 a = (u64)b.base;
@@ -230,6 +234,49 @@ __device__ __forceinline__ d4 dec4(const u32x4 (&v)[N]) {
 }
 __device__ __forceinline__ int gsoff(const Args &a, int p, int r) { return (p * a.nT + r) * GBYTES; }
 
+// The bulk copy of G_r (step p): the U waves of every other owner read it,
+// (nT - p) tiles an owner a step, so it travels untagged -- half the bytes of
+// the granules, whose reads set the pace of the late owners' U waves (the
+// per-CU rate of handed-off reads, MI355X_MICROARCH.md handoff-payload).
+// R1 form (cdna_hip_programming.md Guideline 16): sc1 payload stores, the
+// storing wave's vmcnt(0), then ONE lane's sc1 flag store; the reading wave
+// polls the flags of all the tiles it needs at a step in one load and reads
+// the payloads with sc1 loads after they matched.
+__device__ __forceinline__ int gdoff(const Args &a, int p, int r) { return (p * a.nT + r) * GDBYTES; }
+__device__ __forceinline__ void put_bulk(const Buf &bf, int off, const d4 &v, int lane) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const u64 b0 = (u64)__double_as_longlong(v[2 * h]), b1 = (u64)__double_as_longlong(v[2 * h + 1]);
+        const u32x4 w = {(unsigned)b0, (unsigned)(b0 >> 32), (unsigned)b1, (unsigned)(b1 >> 32)};
+        __builtin_amdgcn_raw_buffer_store_b128(w, rsrc(bf), off + h * 1024 + lane * 16, 0, SC1);
+    }
+}
+__device__ __forceinline__ void flag_bulk(const Args &a, int p, int r) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's payload stores have completed
+    if ((threadIdx.x & 63) == 0) __hip_atomic_store(a.Gf + p * a.nT + r, a.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ d4 dec_bulk(const u32x4 (&x)[2]) {
+    return d4{__longlong_as_double((long long)(((u64)x[0].y << 32) | x[0].x)),
+              __longlong_as_double((long long)(((u64)x[0].w << 32) | x[0].z)),
+              __longlong_as_double((long long)(((u64)x[1].y << 32) | x[1].x)),
+              __longlong_as_double((long long)(((u64)x[1].w << 32) | x[1].z))};
+}
+// until the bulk copies of step p of this wave's tiles j = w + NUW k,
+// lo < j < hi, are all published (lane k polls tile k's flag); false on abort
+template <int TPW>
+__device__ __forceinline__ bool wait_bulk(const Args &a, int p, int w, int lo, int hi, int lane, Smem &S) {
+    static_assert(TPW <= 64, "one flag a lane");
+    const int j = w + NUW * lane;
+    const bool need = lane < TPW && j > lo && j < hi;
+    const unsigned *f = a.Gf + p * a.nT + (need ? j : 0);
+    long long t0 = -1;
+    for (unsigned it = 1;; ++it) {
+        const unsigned v = need ? __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : a.tag;
+        if (__all(v == a.tag)) return true;
+        __builtin_amdgcn_s_sleep(1);
+        if (it % 64 == 0 && give_up(S, it, t0)) return false;
+    }
+}
 // acc += sum_q A_q B_q (fp64 MFMA 16x16x4; fragment element q = k-block q)
 __device__ __forceinline__ d4 mfma4(d4 acc, const d4 &a, const d4 &b) {
 #pragma unroll
@@ -237,6 +284,40 @@ __device__ __forceinline__ d4 mfma4(d4 acc, const d4 &a, const d4 &b) {
     return acc;
 }
 __device__ __forceinline__ d4 zero4() { return d4{0.0, 0.0, 0.0, 0.0}; }
+
+// this wave's tiles j in (lo, hi): T_k = import ? G_j L^T : T_k - G_j G_r^T,
+// NB payloads in flight (after wait_bulk)
+template <int TPW, bool IMPORT, class Get, class Set>
+__device__ __forceinline__ void bulk_update(const Args &a, const Rs &rs, int p, int w, int lo, int hi, const d4 &m,
+                                            int lane, Get &&tget, Set &&tset) {
+    const __amdgpu_buffer_rsrc_t rd = rsrc(rs.Gd);
+#pragma unroll
+    for (int k0 = 0; k0 < TPW; k0 += NB) {
+        bool nd[NB], any = false;
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            const int j = w + NUW * (k0 + q);
+            nd[q] = k0 + q < TPW && j > lo && j < hi;
+            any |= nd[q];
+        }
+        if (!any) continue;
+        u32x4 x[NB][2];
+#pragma unroll
+        for (int q = 0; q < NB; ++q)
+            if (nd[q]) {
+                const int so = __builtin_amdgcn_readfirstlane(gdoff(a, p, w + NUW * (k0 + q)));
+#pragma unroll
+                for (int h = 0; h < 2; ++h) x[q][h] = __builtin_amdgcn_raw_buffer_load_b128(rd, h * 1024 + lane * 16, so, SC1);
+            }
+#pragma unroll
+        for (int q = 0; q < NB; ++q)
+            if (nd[q]) {
+                const int k = k0 + q < TPW ? k0 + q : 0;
+                if (IMPORT) tset(k, mfma4(zero4(), dec_bulk(x[q]), m));
+                else tset(k, mfma4(tget(k), -dec_bulk(x[q]), m));
+            }
+    }
+}
 
 // (G y)(l & 15) on every lane, from the G fragment and y(l & 15): fixed order
 __device__ __forceinline__ double gy(const d4 &g, double yl, int lane) {
@@ -332,6 +413,7 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
     d4 Td = load_tile(a, lambda, r, r, lane);
     double b = assembled_b_src(a.src, a.payload, a.ns, TL * r + li);
     stamp(a, nT, DBG_PROLOGUE);
+    d4 gc = zero4();  // G_r of the critical step: its bulk copy goes out after the pivot
     for (int p = 0; p < nT; ++p) {
         const int s = p & (RING - 1);
         double yl = 0.0;
@@ -346,6 +428,7 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
             yl = dec(v[0][4]);
             if (p != r - 1) {  // the holder of A_rp forms G_r from L_p^-1
                 if (!lds_wait(&S.pdone[s], p_uses(p, r), S)) return false;
+                stamp(a, p, DBG_PLW);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) S.PL[s][e][lane] = lv[e];
                 lds_release();
@@ -355,6 +438,7 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
         if (p == r - 1) {  // the critical step: G_r, its publication, A_rr, then the pivot
             const d4 g = mfma4(zero4(), lv, Tm);
             put4(rs.G, gsoff(a, p, r), a.tag, g, lane);  // owner r + 1 waits for it first
+            gc = g;
             stamp(a, p, DBG_GCRIT);
             Td = mfma4(Td, -g, g);
             b -= gy(g, yl, lane);
@@ -366,8 +450,13 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
             lds_add(&S.gdone[s], 1);
         } else if (p == r) {
             pivot(a, rs, S, r, lane, Td, b);
+            if (r > 0) {
+                put_bulk(rs.Gd, gdoff(a, r - 1, r), gc, lane);
+                flag_bulk(a, r - 1, r);
+            }
         } else {
             if (!lds_wait(&S.gready[s], p + 1, S)) return false;
+            stamp(a, p, DBG_GRDY);
             d4 g;
 #pragma unroll
             for (int e = 0; e < 4; ++e) g[e] = S.GL[s][e][lane];
@@ -455,21 +544,13 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
             d4 lf;
 #pragma unroll
             for (int e = 0; e < 4; ++e) lf[e] = S.Lf[e][lane];
-#pragma unroll
-            for (int k = 0; k < TPW; k += 2) {
-                const int j0 = w + NUW * k, j1 = j0 + NUW;
-                const bool need[2] = {j0 > r && j0 < nT, k + 1 < TPW && j1 > r && j1 < nT};
-                if (!need[0] && !need[1]) continue;
-                const int soff[2] = {gsoff(a, p, need[0] ? j0 : 0), gsoff(a, p, need[1] ? j1 : 0)};
-                u32x4 v[2][GPAIRS];
-                if (!sweep<2, GPAIRS>(rs.G, soff, need, a.tag, v, lane, S)) return false;
-                if (need[0]) tset(k, mfma4(zero4(), dec4(v[0]), lf));
-                if (k + 1 < TPW && need[1]) tset(k + 1, mfma4(zero4(), dec4(v[1]), lf));
-            }
+            if (!wait_bulk<TPW>(a, p, w, r, nT, lane, S)) return false;
+            bulk_update<TPW, true>(a, rs, p, w, r, nT, lf, lane, tget, tset);
             continue;
         }
         if (p % NUW == w && p != r - 1) {  // holder of A_rp: G_r = A_rp L_p^-T
             if (!lds_wait(&S.pready[s], p + 1, S)) return false;
+            stamp(a, p, DBG_HPRDY);
             d4 lv;
 #pragma unroll
             for (int e = 0; e < 4; ++e) lv[e] = S.PL[s][e][lane];
@@ -480,13 +561,17 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
             for (int k = 0; k < TPW; ++k)
                 if (k == p / NUW) tp = tget(k);
             const d4 g = mfma4(zero4(), lv, tp);
-            if (r > p) put4(rs.G, gsoff(a, p, r), a.tag, g, lane);
             if (!lds_wait(&S.gdone[s], NW * g_uses(p, r), S)) return false;
 #pragma unroll
             for (int e = 0; e < 4; ++e) S.GL[s][e][lane] = g[e];
             lds_release();
             lds_set(&S.gready[s], p + 1);
             stamp(a, p, DBG_GHOLD);
+            if (r > p) {  // for W0 of owner r + 1 (granules) and every other owner's U waves (bulk)
+                put4(rs.G, gsoff(a, p, r), a.tag, g, lane);
+                put_bulk(rs.Gd, gdoff(a, p, r), g, lane);
+                flag_bulk(a, p, r);
+            }
         }
         const int hi = r > p ? r - 1 : nT;  // live tiles j in (p, hi); W0 holds r - 1 and r
         if (!lds_wait(&S.gready[s], p + 1, S)) return false;
@@ -495,17 +580,8 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
         for (int e = 0; e < 4; ++e) g[e] = S.GL[s][e][lane];
         lds_release();
         lds_add(&S.gdone[s], 1);
-#pragma unroll
-        for (int k = 0; k < TPW; k += 2) {
-            const int j0 = w + NUW * k, j1 = j0 + NUW;
-            const bool need[2] = {j0 > p && j0 < hi, k + 1 < TPW && j1 > p && j1 < hi};
-            if (!need[0] && !need[1]) continue;
-            const int soff[2] = {gsoff(a, p, need[0] ? j0 : 0), gsoff(a, p, need[1] ? j1 : 0)};
-            u32x4 v[2][GPAIRS];
-            if (!sweep<2, GPAIRS>(rs.G, soff, need, a.tag, v, lane, S)) return false;
-            if (need[0]) tset(k, mfma4(tget(k), -dec4(v[0]), g));
-            if (k + 1 < TPW && need[1]) tset(k + 1, mfma4(tget(k + 1), -dec4(v[1]), g));
-        }
+        if (!wait_bulk<TPW>(a, p, w, p, hi, lane, S)) return false;
+        bulk_update<TPW, false>(a, rs, p, w, p, hi, g, lane, tget, tset);
         if (w == 0) stamp(a, p, DBG_UDONE);
     }
     return true;
@@ -529,6 +605,7 @@ __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
     Rs rs;
     rs.P = Buf{a.P, a.nT * PBYTES};
     rs.G = Buf{a.G, a.nT * a.nT * GBYTES};
+    rs.Gd = Buf{a.Gd, a.nT * a.nT * GDBYTES};
     __syncthreads();
     const int wu = __builtin_amdgcn_readfirstlane(wave);  // provably uniform: scalar record offsets
     if (wu == 0) w0_loop(a, rs, S, r, lane, lambda);

@@ -1,7 +1,9 @@
 """Dev probe (round 4): SFM_GJ_DEBUG stamps of one row-distributed persistent
 reduced solve (gjr_solve.hpp) on a dense SPD n x n system, printed as the
 critical path per pivot: P_{p-1} arriving at owner p, G_p published, the
-chain, P_p published, and the hop to owner p + 1.  Usage: gjr_timeline.py [n]"""
+chain, P_p published, and the hop to owner p + 1; with owners listed, each
+one's own stamps over the steps before its pivot.
+Usage: gjr_timeline.py [n [owner,owner,...]]"""
 import os, sys, ctypes
 os.environ["SFM_GJ_DEBUG"] = "1"
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -22,7 +24,7 @@ c._lib.sfm_gj_debug(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), ctype
 d = buf[:nT * (nT + 1) * 16].reshape(nT, nT + 1, 16).astype(np.float64)
 t0 = d[d > 0].min()
 d = np.where(d > 0, (d - t0) * 0.01, np.nan)  # us (100 MHz)
-PIN, GCRIT, CH0, CH1, PPUB, GHOLD, UDONE, GREM = range(8)
+PIN, GCRIT, CH0, CH1, PPUB, GHOLD, UDONE, GREM, PLW, GRDY, HPRDY = range(11)
 print(f"n={n} nT={nT}   (us from the first stamp)")
 print("   p  P_{p-1}@p   G_p pub   chain0   chain1   P_p pub | hop->p+1   step")
 prev = None
@@ -40,3 +42,8 @@ for w in range(nT):
         print(f"owner {w:3d}: " + " ".join(f"{fin[k]}={d[w, nT, k]:8.2f}" for k in range(4)))
 steps = np.diff(d[np.arange(nT), np.arange(nT), PPUB])
 print(f"mean step {np.nanmean(steps):.3f} us, median {np.nanmedian(steps):.3f}")
+if len(sys.argv) > 2:
+    for r in map(int, sys.argv[2].split(",")):
+        print(f"owner {r}: step  Ppub@p   P_p@W0  pdoneOK  Hpready   G_hold  greadyW0   G_rem   U0done")
+        for p in range(0 if os.environ.get("GJR_ALL") else max(0, r - 8), r):
+            print(f"   {p:4d} " + " ".join(f"{d[i, p, k]:8.2f}" for i, k in ((p, PPUB), (r, PIN), (r, PLW), (r, HPRDY), (r, GHOLD), (r, GRDY), (r, GREM), (r, UDONE))))
