@@ -72,8 +72,15 @@ last_timings = {}
 
 
 def _observations(filtered_world_coords, feature_x, feature_y, filtered_feature_flags, n_cameras):
-    """Dense flags -> COO observations in the reference's order (:164-169)."""
+    """Dense flags -> COO observations in the reference's order (:164-169):
+    the library's threaded scan of the valid rows (point-major, camera
+    ascending, as np.where), or the numpy expression for layouts it does not
+    read (a non-contiguous row, a flag dtype other than float/int/bool)."""
     valid_point_indices = np.where(np.asarray(filtered_world_coords).flatten() == 1)[0]
+    got = _core.dense_observations(filtered_feature_flags, feature_x, feature_y, valid_point_indices, n_cameras)
+    if got is not None:
+        camera_indices, point_indices, points_2d = got
+        return valid_point_indices, camera_indices, point_indices, points_2d
     flags = np.asarray(filtered_feature_flags)[valid_point_indices][:, :n_cameras] == 1
     point_indices, camera_indices = np.nonzero(flags)  # row-major = point-major, camera ascending
     rows = valid_point_indices[point_indices]

@@ -85,6 +85,10 @@ SIGNATURES = [
                                 _i64, _i64]),
     ("sfm_matching_read", _c, [ctypes.c_void_p, _i32, _i32, _d, _d]),
     ("sfm_matching_free", _c, [ctypes.c_void_p]),
+    ("sfm_dense_obs_scan", _c, [ctypes.c_void_p, ctypes.c_int32, _i, _i64, _i, ctypes.c_int32, _d, _d, _i,
+                                ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p), _i64]),
+    ("sfm_dense_obs_read", _c, [ctypes.c_void_p, _i32, _i32, _d]),
+    ("sfm_dense_obs_free", _c, [ctypes.c_void_p]),
     ("sfm_triangulate_dlt", _c, [_d, _d, _d, _d, _i, _d, _c]),
     ("sfm_triangulate_nonlinear", _c, [_d, _d, _d, _d, _d, _i, ctypes.c_int32, _d, _i32, _c]),
     ("sfm_project_points", _c, [_d, _d, _i, _d, _c]),
@@ -427,6 +431,37 @@ def parse_matching(data_path, no_of_images, n_threads=0):
     finally:
         _lib.sfm_matching_free(h)
     return int(nf[0]), feat, img, x, y
+
+
+_DENSE_DTYPES = {np.dtype(np.float64): 0, np.dtype(np.float32): 1, np.dtype(np.int64): 2, np.dtype(np.int32): 3,
+                 np.dtype(np.uint8): 4, np.dtype(np.bool_): 4}
+
+
+def dense_observations(flags, feature_x, feature_y, rows, n_cams, n_threads=0):
+    """Native dense -> COO scan (host threads, no device needed): the
+    observations np.where(flags[rows][:, :n_cams] == 1) gives, in its order,
+    with feature_x / feature_y at the hits.  Returns (camera_indices,
+    point_indices, points_2d), or None when the matrices' layout or dtype is
+    not one the scanner reads (the caller then takes the numpy expression)."""
+    f, fx, fy = np.asarray(flags), np.asarray(feature_x), np.asarray(feature_y)
+    if (f.ndim != 2 or fx.ndim != 2 or fx.shape != fy.shape or f.shape[0] != fx.shape[0]
+            or f.dtype not in _DENSE_DTYPES or fx.dtype != np.float64 or fy.dtype != np.float64
+            or f.strides[1] != f.itemsize or fx.strides != fy.strides or fx.strides[1] != 8
+            or min(f.shape[1], fx.shape[1]) < n_cams):
+        return None
+    rows = np.ascontiguousarray(rows, dtype=np.int64)
+    h = ctypes.c_void_p()
+    no = np.zeros(1, dtype=np.int64)
+    _check(_lib.sfm_dense_obs_scan(f.ctypes.data, _DENSE_DTYPES[f.dtype], f.strides[0], _p(rows, _i64), len(rows),
+                                   int(n_cams), fx.ctypes.data_as(_d), fy.ctypes.data_as(_d), fx.strides[0],
+                                   int(n_threads), ctypes.byref(h), _p(no, _i64)))
+    try:
+        n = int(no[0])
+        cam, pt, obs = np.empty(n, dtype=np.int32), np.empty(n, dtype=np.int32), np.empty((n, 2))
+        _check(_lib.sfm_dense_obs_read(h, _p(cam, _i32), _p(pt, _i32), _p(obs)))
+    finally:
+        _lib.sfm_dense_obs_free(h)
+    return cam, pt, obs
 
 
 def triangulate(P1, P2, x1, x2):

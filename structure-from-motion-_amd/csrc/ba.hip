@@ -1819,6 +1819,20 @@ struct HostLM {
 };
 constexpr int kHostRing = 4;
 
+// create: the camera-major copies of (point, observation) gathered on the
+// device from the uploaded point-major arrays; cm_pt holds the permutation
+// (camera-major position -> observation) on entry, each thread reads its own
+// entry before overwriting it
+__global__ void __launch_bounds__(256) k_gather_cam_major(int64_t no, const int32_t *__restrict__ pt,
+                                                         const double2 *__restrict__ obs, int32_t *cm_pt,
+                                                         double2 *__restrict__ cm_obs) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= no) return;
+    const int32_t o = cm_pt[k];
+    cm_pt[k] = pt[o];
+    cm_obs[k] = obs[o];
+}
+
 __global__ void k_lm_reset(LMState *lm, double lambda0, int *bad) {
     lm->lambda = lambda0; lm->nu = 2.0; lm->cost = 0.0; lm->cost0 = 0.0;
     lm->status = 4; lm->accepted = 0; lm->iters = 0; lm->done = 0;
@@ -2521,9 +2535,43 @@ static int64_t sweep_alloc(const std::vector<std::vector<uint16_t>> &P, const st
     return std::min(fp, fg);
 }
 
+// the planner's independent loops (per chunk, per spec) on host threads:
+// f(i) for i in [0, n), contiguous blocks, up to 16 threads (SFM_PLAN_THREADS)
+template <class F>
+static void par_for(int64_t n, F &&f) {
+    static const int nt0 = [] {
+        const int e = env_int("SFM_PLAN_THREADS", 0);
+        return e > 0 ? e : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    }();
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt0, n));
+    if (nt == 1) {
+        for (int64_t i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            for (int64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) f(i);
+        });
+    for (auto &x : th) x.join();
+}
+
+// SFM_CREATE_TIMING=1: host phase times of sfm_ba_create on stderr
+struct PhaseTimer {
+    bool on = env_int("SFM_CREATE_TIMING", 0) != 0;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    void tick(const char *what) {
+        if (!on) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[create] %-14s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
+        t0 = t;
+    }
+};
+
 static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt,
                        const std::vector<int32_t> &pstart, const std::vector<int64_t> &cnt, int lpp, int ncu,
                        bool allow_split, SweepPlan &P) {
+    PhaseTimer pt_;
     P.nbd = nc * (nc + 1) / 2;
     P.blkij.resize(P.nbd);
     for (int i = 0; i < nc; ++i)
@@ -2591,40 +2639,50 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     // and an imbalance point): from the 16-bit cap down, scaled by the
     // overshoot until the largest (chunk, spec) fits
     int chunk_obs = std::max(64, std::min(env_int("SFM_SWEEP_CHUNK", 65535), 65535));
-    std::vector<int32_t> ccount(nc), cpairs(P.nspec);
     std::vector<int64_t> cut;  // chunk first points
     for (;;) {
+        // the cuts follow from the observation counts alone; the chunks'
+        // staged slots and pair counts (the LDS bound) are then counted per
+        // chunk on host threads
         P.rchunk.assign(1, 0);
         cut.clear();
-        int max_staged = 0, max_pairs = 0;
+        std::vector<int64_t> cend;  // chunk end points
         bool ok = true;
         int64_t pcur = 0;
         for (int r = 0; r < P.nrange && ok; ++r) {
             const int64_t oend = no * (r + 1) / P.nrange;
             while (pcur < np_ && pstart[pcur] < oend) {  // one chunk
                 const int32_t o0 = pstart[pcur];
-                std::fill(ccount.begin(), ccount.end(), 0);
-                std::fill(cpairs.begin(), cpairs.end(), 0);
                 int64_t pe = pcur;
-                while (pe < np_ && pstart[pe] < oend && (pe == pcur || pstart[pe + 1] - o0 <= chunk_obs)) {
+                while (pe < np_ && pstart[pe] < oend && (pe == pcur || pstart[pe + 1] - o0 <= chunk_obs)) ++pe;
+                if (pstart[pe] - o0 > 65535) { ok = false; break; }
+                cut.push_back(pcur);
+                cend.push_back(pe);
+                pcur = pe;
+            }
+            P.rchunk.push_back((int32_t)cut.size());
+        }
+        std::vector<int> cstaged(cut.size(), 0), cpmax(cut.size(), 0);
+        if (ok)
+            par_for((int64_t)cut.size(), [&](int64_t k) {
+                std::vector<int32_t> ccount(nc, 0), cpairs(P.nspec, 0);
+                for (int64_t pe = cut[k]; pe < cend[k]; ++pe)
                     for (int32_t a = pstart[pe]; a < pstart[pe + 1]; ++a) {
                         ccount[cam[a]]++;
                         for (int32_t b = pstart[pe]; b < pstart[pe + 1]; ++b)
                             if (cam[b] > cam[a]) cpairs[spec_of[(size_t)cam[a] * nc + cam[b]]]++;
                     }
-                    ++pe;
-                }
-                if (pstart[pe] - o0 > 65535) { ok = false; break; }
                 for (int w = 0; w < P.nspec; ++w) {
                     int st = 0;
                     for (auto &R : specs[w]) st += ccount[R.c];
-                    max_staged = std::max(max_staged, st);
-                    max_pairs = std::max(max_pairs, cpairs[w]);
+                    cstaged[k] = std::max(cstaged[k], st);
+                    cpmax[k] = std::max(cpmax[k], cpairs[w]);
                 }
-                cut.push_back(pcur);
-                pcur = pe;
-            }
-            P.rchunk.push_back((int32_t)cut.size());
+            });
+        int max_staged = 0, max_pairs = 0;
+        for (size_t k = 0; k < cut.size(); ++k) {
+            max_staged = std::max(max_staged, cstaged[k]);
+            max_pairs = std::max(max_pairs, cpmax[k]);
         }
         P.buf_slots = std::max(8, (max_staged + 7) / 8 * 8);
         P.pair_cap = std::max(128, (max_pairs + 127) / 128 * 128);  // 16-bit entries, whole 64-lane DMA rows
@@ -2634,9 +2692,10 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
         chunk_obs = std::max(64, (int)(chunk_obs * std::min(0.95, std::max(0.5, 0.98 / over))));
     }
     P.nchunk = (int32_t)cut.size();
+    pt_.tick("plan:chunks");
     // exact per-chunk counts: pairs per block, observations per camera
     std::vector<uint16_t> bq((size_t)P.nbd * P.nchunk, 0), cq((size_t)nc * P.nchunk, 0);
-    for (int32_t q = 0; q < P.nchunk; ++q) {
+    par_for(P.nchunk, [&](int64_t q) {  // chunk q writes column q only
         const int64_t pe = q + 1 < P.nchunk ? cut[q + 1] : np_;
         for (int64_t pp = cut[q]; pp < pe; ++pp)
             for (int32_t a = pstart[pp]; a < pstart[pp + 1]; ++a) {
@@ -2644,7 +2703,8 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
                 for (int32_t b = pstart[pp]; b < pstart[pp + 1]; ++b)
                     if (cam[b] > cam[a]) bq[(size_t)dense_blk(nc, cam[a], cam[b]) * P.nchunk + q]++;
             }
-    }
+    });
+    pt_.tick("plan:counts");
     // slots per group, then lanes: diagonal groups first (the loader
     // waves), then the off-diagonal groups by size.  SFM_SWEEP_ALLOC=0 keeps
     // the proportional split, SFM_SWEEP_POW2=1 the power-of-two sizes.
@@ -2652,9 +2712,13 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     std::vector<std::vector<int>> gid_of(P.nspec);  // (row, j - j0) -> group index within spec
     const bool pow2 = env_int("SFM_SWEEP_POW2", 0) != 0, exact = env_int("SFM_SWEEP_ALLOC", 1) != 0;
     int64_t f_plan = 0, f_ideal = 0;
-    for (int w = 0; w < P.nspec; ++w) {
-        auto &gd = sgd[w], &g = sg[w];
-        const int Gd = sGd[w], budget = sbudget[w], nload = P.nload[w];
+    // the slot allocation of every spec (independent: host threads), then the
+    // lane layout in spec order
+    std::vector<std::vector<int>> sl_of(P.nspec);
+    std::vector<int64_t> fplan_w(P.nspec, 0), fideal_w(P.nspec, 0);
+    par_for(P.nspec, [&](int64_t w) {
+        const auto &gd = sgd[w], &g = sg[w];
+        const int Gd = sGd[w], budget = sbudget[w];
         std::vector<int> dtrip(P.nchunk, 0);
         for (auto &x : gd)
             for (int32_t q = 0; q < P.nchunk; ++q)
@@ -2662,9 +2726,9 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
         std::vector<std::vector<uint16_t>> Pg(g.size());
         for (size_t k = 0; k < g.size(); ++k)
             Pg[k].assign(bq.begin() + (size_t)g[k].blk * P.nchunk, bq.begin() + (size_t)(g[k].blk + 1) * P.nchunk);
-        std::vector<int> sl;
+        std::vector<int> &sl = sl_of[w];
         if (exact && !pow2 && !g.empty() && (int)g.size() <= budget) {
-            f_plan += sweep_alloc(Pg, dtrip, budget, sl);
+            fplan_w[w] = sweep_alloc(Pg, dtrip, budget, sl);
         } else {  // proportional (power-of-two sizes with SFM_SWEEP_POW2)
             double tot = 0;
             for (auto &x : g) tot += x.work;
@@ -2695,8 +2759,15 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
         for (int32_t q = 0; q < P.nchunk; ++q) {  // the balance bound: every chunk's pairs over all slots
             int64_t pq = 0;
             for (auto &v : Pg) pq += v[q];
-            f_ideal += std::max<int64_t>(dtrip[q], (pq + budget - 1) / std::max(1, budget));
+            fideal_w[w] += std::max<int64_t>(dtrip[q], (pq + budget - 1) / std::max(1, budget));
         }
+    });
+    for (int w = 0; w < P.nspec; ++w) {
+        f_plan += fplan_w[w];
+        f_ideal += fideal_w[w];
+        auto &gd = sgd[w], &g = sg[w];
+        const int Gd = sGd[w], nload = P.nload[w];
+        const std::vector<int> &sl = sl_of[w];
         for (size_t k = 0; k < g.size(); ++k) g[k].slots = sl[k];
         std::stable_sort(g.begin(), g.end(), [](const G0 &a, const G0 &b) { return a.slots > b.slots; });
         for (auto &x : gd) x.slots = Gd / lpp;
@@ -2714,6 +2785,7 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
         }
     }
     P.goff.push_back((int32_t)P.groups.size());
+    pt_.tick("plan:alloc");
     // the dispatch tail: one workgroup per CU (SW_THREADS, 168 VGPRs), so
     // items run in rounds of ncu; a short last round's specs are split per
     // range into S chunk sub-ranges (SFM_SWEEP_SPLIT=0: off).  Not with the
@@ -2721,7 +2793,10 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     P.split_of.assign(P.nbd, -1);
     {
         const int per_round = ncu / NXCD;  // specs of one range group per round
-        const int want = env_int("SFM_SWEEP_SPLIT", 0);  // off: cfg5 0.341 (none) vs 0.362 ms (S = 8), round 4
+        // S = 8 (SFM_SWEEP_SPLIT=0: off): cfg5 0.361 -> 0.343 ms with a full
+        // round of camera workgroups (below); the first try (0.341 -> 0.362)
+        // left 64 camera workgroups behind the split round, a tail of their own
+        const int want = env_int("SFM_SWEEP_SPLIT", 8);
         int min_chunks = INT32_MAX;
         for (int r = 0; r < P.nrange; ++r) min_chunks = std::min(min_chunks, P.rchunk[r + 1] - P.rchunk[r]);
         const int nsplit = P.nspec % std::max(1, per_round);
@@ -2749,10 +2824,10 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     P.list.assign(nqw * P.list_cap, 0);
     P.pairs.assign(nqw * P.pair_cap, 0);
     P.hdr.assign(nqw * P.hdr_cap, 0);
-    std::vector<std::vector<int32_t>> per_cam(nc);
-    std::vector<int32_t> slot_of;  // chunk-local obs offset -> position in its camera's list
-    std::vector<std::vector<uint32_t>> glist;
-    for (int32_t q = 0; q < P.nchunk; ++q) {
+    par_for(P.nchunk, [&](int64_t q) {  // chunk q writes its (chunk, spec) regions only
+        std::vector<std::vector<int32_t>> per_cam(nc);
+        std::vector<int32_t> slot_of;  // chunk-local obs offset -> position in its camera's list
+        std::vector<std::vector<uint32_t>> glist;
         const int32_t o0 = pstart[cut[q]];
         const int32_t o1 = q + 1 < P.nchunk ? pstart[cut[q + 1]] : (int32_t)no;
         for (auto &v : per_cam) v.clear();
@@ -2800,7 +2875,8 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
             hd[ng + 2] = n1;
             hd[ng + 3] = o0;
         }
-    }
+    });
+    pt_.tick("plan:lists");
 }
 
 // ------------------------------------------------------------ problem
@@ -2985,10 +3061,15 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     SFM_CHECK_ARG(nc >= 1 && np_ >= 0 && no >= 0, "bad sizes");
     SFM_CHECK_ARG(no < ((int64_t)1 << 31), "problem too large for int32 indexing");
     SFM_CHECK_ARG(6 * nc <= SOLVE_MAX, "at most 682 cameras (dense reduced camera system)");
+    // SFM_CREATE_TIMING=1: the host phases of create on stderr (measurement)
+    PhaseTimer ctm_;
+    auto ctick = [&](const char *what) { ctm_.tick(what); };
+    const bool ctm = ctm_.on;
     for (int64_t o = 0; o < no; ++o) {
         SFM_CHECK_ARG(cam[o] >= 0 && cam[o] < nc && pt[o] >= 0 && pt[o] < np_, "observation index out of range");
         SFM_CHECK_ARG(o == 0 || pt[o] >= pt[o - 1], "observations must be point-major (sorted by point)");
     }
+    ctick("validate");
     SFM_HIP(hipSetDevice(device));
     (void)hipGetLastError();  // launches below are checked with hipGetLastError: start clean
     auto p = std::make_unique<sfm_ba_problem>();
@@ -3010,6 +3091,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     SFM_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
     for (auto &e : p->ev) SFM_HIP(hipEventCreate(&e));
     for (auto &e : p->ev_it) SFM_HIP(hipEventCreate(&e));
+    ctick("stream");
     // point CSR
     std::vector<int32_t> pstart(np_ + 1, 0);
     for (int64_t o = 0; o < no; ++o) pstart[pt[o] + 1]++;
@@ -3022,22 +3104,41 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         std::vector<int32_t> fill(cstart.begin(), cstart.end() - 1);
         for (int64_t o = 0; o < no; ++o) cam_obs[fill[cam[o]]++] = (int32_t)o;
     }
+    ctick("csr");
     for (int64_t i = 0; i < np_; ++i)
         for (int32_t a = pstart[i]; a < pstart[i + 1]; ++a)
             for (int32_t b = a + 1; b < pstart[i + 1]; ++b)
                 SFM_CHECK_ARG(cam[a] != cam[b], "a point is observed twice by the same camera");
+    ctick("dupcheck");
     // co-observation counts per camera block (static sparsity of the reduced camera system)
+    // (host threads over point blocks, integer sums)
     std::vector<int64_t> cnt((size_t)nc * nc, 0);
     int64_t tot = 0;
-    for (int64_t i = 0; i < np_; ++i)
-        for (int32_t a = pstart[i]; a < pstart[i + 1]; ++a)
-            for (int32_t b = a; b < pstart[i + 1]; ++b) {
-                int ci = cam[a], cj = cam[b];
-                if (ci > cj) std::swap(ci, cj);
-                cnt[(size_t)ci * nc + cj]++;
-                ++tot;
-            }
+    {
+        constexpr int NB = 16;
+        std::vector<std::vector<int64_t>> part(NB);
+        std::vector<int64_t> tpart(NB, 0);
+        par_for(NB, [&](int64_t t) {
+            auto &c = part[t];
+            c.assign((size_t)nc * nc, 0);
+            int64_t n = 0;
+            for (int64_t i = np_ * t / NB; i < np_ * (t + 1) / NB; ++i)
+                for (int32_t a = pstart[i]; a < pstart[i + 1]; ++a)
+                    for (int32_t b = a; b < pstart[i + 1]; ++b) {
+                        int ci = cam[a], cj = cam[b];
+                        if (ci > cj) std::swap(ci, cj);
+                        c[(size_t)ci * nc + cj]++;
+                        ++n;
+                    }
+            tpart[t] = n;
+        });
+        for (int t = 0; t < NB; ++t) {
+            tot += tpart[t];
+            for (size_t k = 0; k < cnt.size(); ++k) cnt[k] += part[t][k];
+        }
+    }
     p->npairs = tot;
+    ctick("blockcounts");
     SweepPlan sw;
     // lanes per pair slot: 1 (a lane forms a pair's whole 6x6 block, H once;
     // two lanes with half the rows each: cfg4 0.155 against 0.134 ms, round 3; retired)
@@ -3046,6 +3147,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     // when the finish is folded in): the sweep's dispatch tail may be split
     const bool split_ok = true;
     plan_sweep(nc, np_, no, cam, pt, pstart, cnt, p->sw_lpp, device_cus(device), split_ok, sw);
+    ctick("plan_sweep");
     if (sw.buf_slots > SW_MAX_STAGED) {  // one point with more observations in a spec's cameras than a round holds
         set_error("sweep plan: %d observations of one spec's cameras in a single point range (max %d)", sw.buf_slots,
                   SW_MAX_STAGED);
@@ -3060,8 +3162,11 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     const int cam_chunk = std::max(64, env_int("SFM_CAM_CHUNK", CAM_CHUNK));
     const int busy = sw.split_S ? NXCD * (sw.split_w0 + sw.split_n * sw.split_S) : sw.nspec * sw.nrange,
               idle = (256 - busy % 256) % 256;
+    // the camera workgroups take the CUs the sweep's last round leaves idle;
+    // when the dispatch tail is split there are none, and a full round of
+    // them (256) beats a short one behind the split round
     p->cl_fused_wg = (int32_t)std::min<int64_t>(std::max<int64_t>(1, ceil_div(no, SW_THREADS)),
-                                                env_int("SFM_CAMLIN_WG", idle >= 32 ? idle : 64));
+                                                env_int("SFM_CAMLIN_WG", sw.split_S ? 256 : idle >= 32 ? idle : 64));
     CamPlan csa, cfu;
     {
         std::vector<int32_t> cuts;
@@ -3087,6 +3192,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
                                                    (size_t)sw.hdr_cap * sizeof(SweepGroup));
     p->pt_blocks = std::max(1, ceil_div(np_ * PT_GROUP, PT_THREADS));
     p->payload_len = pay_vec_base(p->ns) + 3 * p->ns + 1;
+    ctick("cam_items");
     int rc;
     if ((rc = p->alloc(p->d_cam, no)) || (rc = p->alloc(p->d_pt, no)) || (rc = p->alloc(p->d_pstart, np_ + 1)) ||
         (rc = p->alloc(p->d_obs, no)) || (rc = p->alloc(p->d_cm_pt, no)) ||
@@ -3138,6 +3244,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         SFM_HIP(hipMemsetAsync(gi, 0, GjBufs::ints(p->nT, p->gjp.nseg) * sizeof(int), p->stream));
         SFM_HIP(hipEventCreateWithFlags(&p->ev_solve, hipEventDisableTiming));
     }
+    ctick("alloc");
     SFM_HIP(hipHostMalloc((void **)&p->h_ring, kHostRing * sizeof(HostLM), hipHostMallocMapped | hipHostMallocCoherent));
     std::memset((void *)p->h_ring, 0, kHostRing * sizeof(HostLM));
     SFM_HIP(hipHostGetDevicePointer((void **)&p->d_ring, p->h_ring, 0));
@@ -3148,19 +3255,15 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         SFM_HIP(hipMemcpyAsync(p->d_obs, obs, no * 16, hipMemcpyHostToDevice, s));
     }
     SFM_HIP(hipMemcpyAsync(p->d_pstart, pstart.data(), pstart.size() * 4, hipMemcpyHostToDevice, s));
-    std::vector<int32_t> cm_pt(no);
-    std::vector<double> cm_obs(2 * (size_t)no);
-    for (int64_t k = 0; k < no; ++k) {
-        const int32_t o = cam_obs[k];
-        cm_pt[k] = pt[o];
-        cm_obs[2 * k] = obs[2 * (size_t)o];
-        cm_obs[2 * k + 1] = obs[2 * (size_t)o + 1];
-    }
-    if (no) {
-        SFM_HIP(hipMemcpyAsync(p->d_cm_pt, cm_pt.data(), no * 4, hipMemcpyHostToDevice, s));
-        SFM_HIP(hipMemcpyAsync(p->d_cm_obs, cm_obs.data(), no * 16, hipMemcpyHostToDevice, s));
+    ctick("up:obs");
+    if (no) {  // the permutation up, the camera-major copies gathered on the device
+        SFM_HIP(hipMemcpyAsync(p->d_cm_pt, cam_obs.data(), no * 4, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_gather_cam_major, dim3((unsigned)ceil_div(no, 256)), dim3(256), 0, s, no, p->d_pt,
+                           p->d_obs, p->d_cm_pt, p->d_cm_obs);
+        SFM_HIP(hipGetLastError());
     }
     SFM_HIP(hipMemcpyAsync(p->d_cstart, cstart.data(), cstart.size() * 4, hipMemcpyHostToDevice, s));
+    ctick("up:cammajor");
     SFM_HIP(hipMemsetAsync(p->d_camlin, 0, (size_t)CAMLIN * nc * sizeof(double), s));
     SFM_HIP(hipMemsetAsync(p->d_count, 0, 3 * GS_WORDS * sizeof(unsigned), s));
     SFM_HIP(hipMemsetAsync(p->d_nbig, 0, sizeof(unsigned), s));
@@ -3188,6 +3291,10 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = up(p->d_sw_blkij, sw.blkij.data(), sw.blkij.size() * sizeof(int2))) ||
         (rc = up(p->d_sw_split_of, sw.split_of.data(), sw.split_of.size() * 4)))
         return rc;
+    ctick("up:sweep");
+    if (ctm)
+        std::fprintf(stderr, "[create] sweep arrays: list %.1f MB pairs %.1f MB hdr %.1f MB\n", sw.list.size() * 4e-6,
+                     sw.pairs.size() * 2e-6, sw.hdr.size() * 4e-6);
     SFM_HIP(hipFuncSetAttribute((const void *)k_schur_sweep<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)p->sw_lds_bytes));
     SFM_HIP(hipFuncSetAttribute((const void *)k_schur_sweep<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3195,6 +3302,11 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     SFM_HIP(hipFuncSetAttribute((const void *)k_schur_sweep<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)p->sw_lds_bytes));
     if ((rc = upload_state(p.get()))) return rc;
+    ctick("upload");
+    if (ctm) {
+        SFM_HIP(hipStreamSynchronize(s));
+        ctick("sync");
+    }
     *out = p.release();
     return 0;
 }

@@ -1,0 +1,68 @@
+"""The BA drop-in's dense -> COO step (BundleAdjustment.py:164-169): the
+library's threaded scan (csrc/dense_obs.cpp) against the reference's numpy
+expression, on the flag dtypes the reference's drivers build (int, float,
+bool), with invalid rows, flags other than 0/1, a camera count below the
+matrices' width and a row-strided view.  Host only (no device)."""
+import numpy as np
+import pytest
+
+import _sfmcore as core
+import BundleAdjustment as BA
+
+
+def reference_observations(fwc, fx, fy, flags, n_cams):
+    valid = np.where(np.asarray(fwc).flatten() == 1)[0]
+    f = np.asarray(flags)[valid][:, :n_cams] == 1
+    pi, ci = np.nonzero(f)
+    rows = valid[pi]
+    return valid, ci, pi, np.column_stack([np.asarray(fx)[rows, ci], np.asarray(fy)[rows, ci]])
+
+
+def problem(n, m, dtype, seed):
+    rng = np.random.default_rng(seed)
+    flags = (rng.random((n, m)) < 0.2).astype(dtype)
+    if np.dtype(dtype).kind in "fi":
+        flags[rng.random((n, m)) < 0.02] = 2  # not == 1: no observation
+    fx, fy = rng.standard_normal((n, m)), rng.standard_normal((n, m))
+    fwc = (rng.random((n, 1)) < 0.8).astype(np.int64)
+    return fwc, fx, fy, flags
+
+
+@pytest.mark.parametrize("dtype", [np.int64, np.float64, np.int32, np.float32, np.bool_, np.uint8])
+@pytest.mark.parametrize("n_threads", [0, 1, 3])
+def test_dense_observations_match_numpy(dtype, n_threads):
+    fwc, fx, fy, flags = problem(20011, 37, dtype, 7)
+    n_cams = 33  # the reference slices [:, :n_cameras]
+    valid, ci, pi, obs = reference_observations(fwc, fx, fy, flags, n_cams)
+    got = core.dense_observations(flags, fx, fy, valid, n_cams, n_threads=n_threads)
+    assert got is not None
+    cam, pt, xy = got
+    assert np.array_equal(cam, ci) and np.array_equal(pt, pi)
+    assert np.array_equal(xy, obs)  # gathered, not computed: bit for bit
+
+
+def test_drop_in_observations_equal_reference_and_fallback():
+    fwc, fx, fy, flags = problem(5003, 20, np.int64, 11)
+    ref = reference_observations(fwc, fx, fy, flags, 20)
+    got = BA._observations(fwc, fx, fy, flags, 20)
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)
+    # a view the scanner does not read (column-strided): numpy's expression
+    fx2 = np.asfortranarray(fx)
+    assert core.dense_observations(flags, fx2, fy, ref[0], 20) is None
+    for a, b in zip(BA._observations(fwc, fx2, fy, flags, 20), ref):
+        assert np.array_equal(a, b)
+    # a row-strided view (every other row of bigger matrices) is read in place
+    big = [np.repeat(a, 2, axis=0) for a in (fx, fy, flags)]
+    views = [a[::2] for a in big]
+    for a, b in zip(BA._observations(fwc, *views, 20), ref):
+        assert np.array_equal(a, b)
+
+
+def test_dense_observations_empty():
+    fwc, fx, fy, flags = problem(100, 5, np.int64, 3)
+    cam, pt, xy = core.dense_observations(flags, fx, fy, np.zeros(0, dtype=np.int64), 5)
+    assert len(cam) == len(pt) == len(xy) == 0
+    flags[:] = 0
+    cam, pt, xy = core.dense_observations(flags, fx, fy, np.arange(100), 5)
+    assert len(cam) == 0 and xy.shape == (0, 2)
