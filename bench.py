@@ -124,7 +124,9 @@ def cpu_baseline_ba(prob, cams0, sweep, single=True):
     the product):
       * CPU-strong: the OpenMP Schur-LM (oracle/sfm_cpu_strong.c) at every
         thread count of `sweep`; at cfg4 to convergence, at cfg5 a bounded 3
-        iterations per point (LM-it/s = iterations / wall time);
+        iterations per point (LM-it/s = iterations / wall time; the 1-thread
+        point alone would take minutes to converge), then the sweep's fastest
+        thread count again to convergence;
       * (single) the 1-thread C Schur-LM (oracle/sfm_oracle.c) to convergence;
       * the reference's own path priced by its residual loop
         (oracle/ref_loop.py, the reference loop structure call for call) on a
@@ -141,8 +143,15 @@ def cpu_baseline_ba(prob, cams0, sweep, single=True):
         _, _, srep = O.ba_lm_cpu_strong(*args, max_iterations=iters)
         ts = time.perf_counter() - t0
         strong[t] = (srep["iterations"] / ts, srep, ts)
-    O.set_threads(max(sweep))
     out = dict(strong=strong)
+    if not single:  # cfg5: the fastest thread count to convergence
+        best_t = max(strong, key=lambda t: strong[t][0])
+        O.set_threads(best_t)
+        t0 = time.perf_counter()
+        _, _, crep = O.ba_lm_cpu_strong(*args, max_iterations=50)
+        ts = time.perf_counter() - t0
+        out["converged"] = (crep["iterations"] / ts, crep, ts, best_t)
+    O.set_threads(max(sweep))
     if single:
         t0 = time.perf_counter()
         _, _, orep = O.ba_lm(*args, max_iterations=50)
@@ -678,7 +687,7 @@ def main():
     if cpu_leg:
         import oracle as O  # test infrastructure: the CPU restatement, timed as the baseline
         avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-        sweep = sorted({t for t in (1, 4, 16, min(64, avail)) if t <= avail})
+        sweep = sorted({t for t in (1, 4, 16, 64, 128) if t <= avail} | {min(128, avail)})
         cpu = {}
         for i, leg in enumerate(legs):
             rec = out if i == 0 else out[leg["workload"]]
@@ -697,6 +706,11 @@ def main():
                 "thread_sweep": {str(t): {"LM_it_per_s": round(v[0], 4), "s": round(v[2], 3)}
                                  for t, v in sorted(base["strong"].items())},
                 "reference_extrapolated": base["ref"]}
+            if "converged" in base:
+                cv, crep, cdt, ct = base["converged"]
+                cpu[leg["workload"]]["converged_at_fastest_threads"] = {
+                    "LM_it_per_s": round(cv, 4), "threads": ct, "iterations": crep["iterations"],
+                    "s": round(cdt, 3), "status": crep.get("status")}
             if "oracle" in base:
                 ov, orep, odt = base["oracle"]
                 cpu[leg["workload"]]["single_thread_oracle"] = {

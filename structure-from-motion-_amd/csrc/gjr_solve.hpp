@@ -355,7 +355,10 @@ __device__ __forceinline__ d4 load_tile(const Args &a, double lambda, int r, int
 }
 
 // uses of ring slot p % RING before step p: by the G pieces (every step but
-// r) and by the L^-1 pieces for a holder (every step but r - 1 and r)
+// r) and by the L^-1 pieces for a holder (every step but r - 1 and r).
+// Measured and not kept (round 4): the critical step's G kept out of the
+// ring (the U waves skip step r - 1, where they have no live tile): cfg4
+// 0.0848 -> 0.0834 ms but cfg5 0.301 -> 0.346 ms
 __device__ __forceinline__ int g_uses(int p, int r) {
     return p / RING - (r < p && (r & (RING - 1)) == (p & (RING - 1)) ? 1 : 0);
 }
@@ -389,9 +392,6 @@ __device__ __forceinline__ void pivot(const Args &a, const Rs &rs, Smem &S, int 
     if (lane == 0)
 #pragma unroll
         for (int j = 0; j < 16; ++j) S.yv[j] = pw[j];
-    if (grp == 0)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) S.Dm[li][j] = j <= li ? rw[j] : 0.0;
     wave_lds();
     d4 lv;
 #pragma unroll
@@ -399,6 +399,11 @@ __device__ __forceinline__ void pivot(const Args &a, const Rs &rs, Smem &S, int 
     put4(rs.P, r * PBYTES, a.tag, lv, lane);
     put_pair(rs.P, r * PBYTES, 4, a.tag, S.yv[li], lane);
     stamp(a, r, DBG_PPUB);
+    // the L_r rows (for the import's fragment) after the publication
+    if (grp == 0)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) S.Dm[li][j] = j <= li ? rw[j] : 0.0;
+    wave_lds();
 #pragma unroll
     for (int e = 0; e < 4; ++e) S.Lf[e][lane] = S.Dm[li][4 * e + grp];
     lds_release();
@@ -455,6 +460,19 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
                 flag_bulk(a, r - 1, r);
             }
         } else {
+            // G_{r-1} of this step (for A_r,r-1) first: owner r - 1 publishes
+            // it as soon as it has P_p, so its round trip overlaps the holder's
+            // work on G_r instead of following it (this wave reaches the next
+            // step's poll, the critical one at p = r - 2, one round trip sooner)
+            d4 gm = zero4();
+            if (p < r) {
+                const int soff[1] = {gsoff(a, p, r - 1)};
+                const bool need[1] = {true};
+                u32x4 v[1][GPAIRS];
+                if (!sweep<1, GPAIRS>(rs.G, soff, need, a.tag, v, lane, S)) return false;
+                stamp(a, p, DBG_GREM);
+                gm = dec4(v[0]);
+            }
             if (!lds_wait(&S.gready[s], p + 1, S)) return false;
             stamp(a, p, DBG_GRDY);
             d4 g;
@@ -463,14 +481,8 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
             lds_release();
             lds_add(&S.gdone[s], 1);
             b -= gy(g, yl, lane);
-            if (p < r) {  // A_rr and A_r,r-1 (G_r-1 from owner r - 1)
+            if (p < r) {  // A_rr and A_r,r-1
                 Td = mfma4(Td, -g, g);
-                const int soff[1] = {gsoff(a, p, r - 1)};
-                const bool need[1] = {true};
-                u32x4 v[1][GPAIRS];
-                if (!sweep<1, GPAIRS>(rs.G, soff, need, a.tag, v, lane, S)) return false;
-                stamp(a, p, DBG_GREM);
-                const d4 gm = dec4(v[0]);
                 Tm = mfma4(Tm, -gm, g);
             }
         }
