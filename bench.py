@@ -70,7 +70,7 @@ def design_bytes(name, n_obs, n_pts, n_pairs, nblocks, ns):
     return None
 
 
-PMC_ROUND = "round3"
+PMC_ROUND = "round4"
 
 
 def pmc_iteration(workload):
