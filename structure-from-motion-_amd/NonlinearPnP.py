@@ -2,15 +2,19 @@
 (Phase 1/NonlinearPnP.py:5-151).
 
 The pose refinement (scipy least_squares(method='lm', max_nfev=100) on the
-2N reprojection residuals) runs as MINPACK lmdif in one 512-thread
-workgroup on the MI355X (pnp.hip k_nonlinear_pnp): the 2N residual rows
-stay in registers; every forward-difference Jacobian (the base and the six
-perturbed projections in one pass) is reduced to its 6 x 6 R factor and
-Q^T f by CholeskyQR2 (fixed-order block sums of J^T J, then of q^T q and
-q^T f with q = J R1^-1; a shifted third pass when J is numerically
-rank-deficient, reported in info's flags); MINPACK's qrfac with column
-pivoting, lmpar, the trust region and the stopping tests then run on the
-6 x 6 factor on one lane.  Rotation conversions follow scipy's quaternion
+2N reprojection residuals) runs as MINPACK lmdif on the MI355X (pnp.hip
+k_nonlinear_pnp) over ceil(2N / 1024) workgroups (at most 64, clamped to
+the resident count; a timed-out hand-off retries on one workgroup): each
+workgroup keeps its ~1,024 residual rows in registers and forms its partial
+block sums, the partials are all-gathered and every workgroup adds them in
+the same fixed order, so each runs the same replicated lmdif control.  Every
+forward-difference Jacobian (the base and the six perturbed projections in
+one pass) is reduced to its 6 x 6 R factor and Q^T f by CholeskyQR2
+(fixed-order block sums of J^T J, then of q^T q and q^T f with
+q = J R1^-1; a shifted third pass when J is numerically rank-deficient,
+reported in info's flags); MINPACK's qrfac with column pivoting, lmpar, the
+trust region and the stopping tests then run on the 6 x 6 factor on one
+lane.  Rotation conversions follow scipy's quaternion
 formulas.  The result is the reference's minimum (cost within 1e-9, pose
 within 1e-5), not bit-exact: device sin/cos and the parallel sums round
 differently.

@@ -1,5 +1,6 @@
 """The oracle (oracle/sfm_oracle.c) pinned against vectors captured from the
 reference itself (tests/golden/make_golden.py).  CPU only."""
+import os
 import random
 
 import numpy as np
@@ -253,6 +254,14 @@ def test_reference_loop_restatement_values():
     assert np.abs(r1 - r2).max() <= 1e-9 * np.abs(r2).max()
 
 
+def blas_config():
+    """numpy's BLAS build (library, version, micro-kernel architecture)"""
+    import threadpoolctl
+    return [{k: d.get(k) for k in ("internal_api", "version", "architecture", "user_api")}
+            for d in threadpoolctl.threadpool_info()
+            if d.get("user_api") == "blas" and "numpy" in str(d.get("filepath", ""))]
+
+
 def test_oracle_pair_errors_equal_reference_expressions():
     """The oracle's per-pair errors are the reference's own numpy
     expressions bit for bit (numpy here: the fixtures' machine) -- so the
@@ -260,7 +269,14 @@ def test_oracle_pair_errors_equal_reference_expressions():
     oracle compare against the reference arithmetic:
       F: GetInliersRANSAC.py:67-78 (Fx1 / FTx2 are dgemm FMA chains, the
          row sum and the squares plain);
-      H: GetHomographyInliers.py:136-142;  PnP: PnPRANSAC.py:60-68."""
+      H: GetHomographyInliers.py:136-142;  PnP: PnPRANSAC.py:60-68.
+    The dgemm FMA order is the BLAS micro-kernel's: the equality is pinned on
+    the build recorded in tests/golden/blas_config.json and skipped on
+    another (a different BLAS orders Fx1's products differently)."""
+    import json
+    pinned = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "blas_config.json")))["numpy_blas"]
+    if blas_config() != pinned:
+        pytest.skip(f"numpy BLAS {blas_config()} differs from the pinned {pinned}")
     for seed in range(4):
         x1, x2, _, m = syn.two_view(n=4000, seed=seed)
         random.seed(seed)
