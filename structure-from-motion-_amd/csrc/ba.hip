@@ -2185,13 +2185,13 @@ struct GjrBufs {
     unsigned *arrive = nullptr;
     static size_t words(int nT) {
         const size_t t = (size_t)nT * nT;
-        return ((size_t)nT * gjr::PBYTES + t * gjr::GBYTES + t * gjr::GDBYTES) / 8 + (t + 1) / 2;
+        return ((size_t)2 * nT * gjr::PBYTES + t * gjr::GBYTES + t * gjr::GDBYTES) / 8 + (t + 1) / 2;
     }
     static constexpr size_t ints = 64;
     void carve(gjr::u64 *w, int *i, int nT) {
         const size_t t = (size_t)nT * nT;
         P = w;
-        G = P + (size_t)nT * gjr::PBYTES / 8;
+        G = P + (size_t)2 * nT * gjr::PBYTES / 8;
         Gd = reinterpret_cast<double *>(G + t * gjr::GBYTES / 8);
         Gf = reinterpret_cast<unsigned *>(Gd + t * gjr::GDBYTES / 8);
         err = i;

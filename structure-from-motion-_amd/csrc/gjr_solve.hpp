@@ -71,7 +71,7 @@ struct Args {
     int32_t ns, nT;
     const double *lam;
     const int *gate;
-    u64 *P;         // [nT] pivot records of PBYTES
+    u64 *P;         // [2][nT] pivot records of PBYTES: write-through copy, then the L2-local copy
     u64 *G;         // [nT][nT] G_r of step p at (p, r), GBYTES each (granules: W0 of owner r + 1)
     double *Gd;     // [nT][nT] the same untagged, GDBYTES each (the U waves' bulk updates) ...
     unsigned *Gf;   // [nT][nT] ... published by a flag (= tag) behind the drained stores
@@ -86,9 +86,21 @@ struct Args {
 
 enum { DBG_PIN = 0, DBG_GCRIT, DBG_CHAIN0, DBG_CHAIN1, DBG_PPUB, DBG_GHOLD, DBG_UDONE, DBG_GREM, DBG_PLW, DBG_GRDY, DBG_HPRDY };
 enum { DBG_START = 0, DBG_PROLOGUE, DBG_W0END, DBG_ARRIVED };
+// row tile of workgroup b: consecutive rows on one XCD (workgroups are
+// dealt round-robin over the 8 XCDs, b % 8), so the critical hop P_{r-1} ->
+// owner r mostly stays inside one L2
+constexpr int NXCD_ = 8;
+__device__ __forceinline__ int row_of(int b, int nT) {
+    const int x = b % NXCD_;
+    return x * (nT / NXCD_) + min(x, nT % NXCD_) + b / NXCD_;
+}
+__device__ __forceinline__ int xcd_of_row(int r, int nT) {
+    const int q = nT / NXCD_, m = nT % NXCD_;
+    return r < m * (q + 1) ? r / (q + 1) : m + (r - m * (q + 1)) / max(q, 1);
+}
 __device__ __forceinline__ void stamp(const Args &a, int p, int slot) {
     if (a.dbg && (threadIdx.x & 63) == 0)
-        a.dbg[((int64_t)blockIdx.x * (a.nT + 1) + p) * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+        a.dbg[((int64_t)row_of(blockIdx.x, a.nT) * (a.nT + 1) + p) * 16 + slot] = __builtin_amdgcn_s_memrealtime();
 }
 
 struct Smem {
@@ -186,14 +198,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const Buf &b) {
                                              __builtin_amdgcn_readfirstlane(b.bytes), 0x00020000);
 }
 constexpr int SC1 = 16;  // buffer op aux: sc1 (write-through stores, L2-served loads)
+template <int AUX = SC1>
 __device__ __forceinline__ void put_pair(const Buf &bf, int soff, int e, unsigned tag, double v, int lane) {
     const u64 b = (u64)__double_as_longlong(v);
     const u32x4 w = {(unsigned)b, tag, (unsigned)(b >> 32), tag};
-    __builtin_amdgcn_raw_buffer_store_b128(w, rsrc(bf), soff + e * 1024 + lane * 16, 0, SC1);
+    __builtin_amdgcn_raw_buffer_store_b128(w, rsrc(bf), soff + e * 1024 + lane * 16, 0, AUX);
 }
+template <int AUX = SC1>
 __device__ __forceinline__ void put4(const Buf &rs, int soff, unsigned tag, const d4 &v, int lane) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) put_pair(rs, soff, e, tag, v[e], lane);
+    for (int e = 0; e < 4; ++e) put_pair<AUX>(rs, soff, e, tag, v[e], lane);
 }
 __device__ __forceinline__ double dec(const u32x4 &x) {
     return __longlong_as_double((long long)(((u64)x.z << 32) | x.x));
@@ -224,6 +238,40 @@ __device__ __forceinline__ bool sweep(const Buf &bf, const int (&soff)[NR], cons
 #pragma unroll
             for (int k = 0; k < N; ++k) ok &= x[q][k].y == tag && x[q][k].w == tag;
         if (__all(ok)) return true;
+        __builtin_amdgcn_s_sleep(1);
+        if (it % 64 == 0 && give_up(S, it, t0)) return false;
+    }
+}
+// the critical poll (owner r - 1 on this XCD): P_{r-1} from its L2-local
+// copy (plain stores: the line stays in the shared L2, an sc1 load is served
+// there) or from the write-through copy, per lane whichever is complete --
+// the same values, so a lane may take either; the write-through copy also
+// covers a workgroup placement other than round-robin
+__device__ __forceinline__ bool poll_p2(const Buf &bf, int soff_wt, int soff_l2, unsigned tag, u32x4 (&x)[PPAIRS],
+                                        int lane, Smem &S) {
+    long long t0 = -1;
+    for (unsigned it = 1;; ++it) {
+        asm volatile("" ::: "memory");  // every pass reloads
+        const __amdgpu_buffer_rsrc_t rs = rsrc(bf);
+        u32x4 y[PPAIRS];
+#pragma unroll
+        for (int k = 0; k < PPAIRS; ++k)
+            x[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, k * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(soff_l2), SC1);
+#pragma unroll
+        for (int k = 0; k < PPAIRS; ++k)
+            y[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, k * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(soff_wt), SC1);
+        bool ok = true, okw = true;
+#pragma unroll
+        for (int k = 0; k < PPAIRS; ++k) {
+            ok &= x[k].y == tag && x[k].w == tag;
+            okw &= y[k].y == tag && y[k].w == tag;
+        }
+        if (__all(ok || okw)) {
+            if (!ok)
+#pragma unroll
+                for (int k = 0; k < PPAIRS; ++k) x[k] = y[k];
+            return true;
+        }
         __builtin_amdgcn_s_sleep(1);
         if (it % 64 == 0 && give_up(S, it, t0)) return false;
     }
@@ -396,8 +444,11 @@ __device__ __forceinline__ void pivot(const Args &a, const Rs &rs, Smem &S, int 
     d4 lv;
 #pragma unroll
     for (int e = 0; e < 4; ++e) lv[e] = S.Li[li][4 * e + grp];  // L^-1(l & 15, 4e + (l >> 4))
+    const double yr = S.yv[li];
+    put4<0>(rs.P, (a.nT + r) * PBYTES, a.tag, lv, lane);  // the L2-local copy first (the next owner)
+    put_pair<0>(rs.P, (a.nT + r) * PBYTES, 4, a.tag, yr, lane);
     put4(rs.P, r * PBYTES, a.tag, lv, lane);
-    put_pair(rs.P, r * PBYTES, 4, a.tag, S.yv[li], lane);
+    put_pair(rs.P, r * PBYTES, 4, a.tag, yr, lane);
     stamp(a, r, DBG_PPUB);
     // the L_r rows (for the import's fragment) after the publication
     if (grp == 0)
@@ -427,7 +478,11 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
             const int soff[1] = {p * PBYTES};
             const bool need[1] = {true};
             u32x4 v[1][PPAIRS];
-            if (!sweep<1, PPAIRS>(rs.P, soff, need, a.tag, v, lane, S)) return false;
+            if (p == r - 1 && xcd_of_row(p, nT) == xcd_of_row(r, nT)) {
+                if (!poll_p2(rs.P, p * PBYTES, (nT + p) * PBYTES, a.tag, v[0], lane, S)) return false;
+            } else if (!sweep<1, PPAIRS>(rs.P, soff, need, a.tag, v, lane, S)) {
+                return false;
+            }
             stamp(a, p, DBG_PIN);
             lv = dec4(v[0]);
             yl = dec(v[0][4]);
@@ -606,7 +661,7 @@ __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
     extern __shared__ __attribute__((aligned(16))) double dyn[];  // LDS tile slots, then the epilogue's scratch
     static_assert(NUW * TLS * 256 * sizeof(double) <= DYN_LDS, "LDS tile slots");
     stamp(a, a.nT, DBG_START);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = blockIdx.x;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = row_of(blockIdx.x, a.nT);
     const double lambda = *a.lam;
     if (threadIdx.x < RING) S.pready[threadIdx.x] = S.pdone[threadIdx.x] = S.gready[threadIdx.x] = S.gdone[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
@@ -615,7 +670,7 @@ __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
         S.bad = a.bad;
     }
     Rs rs;
-    rs.P = Buf{a.P, a.nT * PBYTES};
+    rs.P = Buf{a.P, 2 * a.nT * PBYTES};
     rs.G = Buf{a.G, a.nT * a.nT * GBYTES};
     rs.Gd = Buf{a.Gd, a.nT * a.nT * GDBYTES};
     __syncthreads();
