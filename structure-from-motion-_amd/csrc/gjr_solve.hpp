@@ -54,7 +54,7 @@ constexpr int GPAIRS = 4;        // granule pairs a lane of a published G tile
 constexpr int PBYTES = PPAIRS * 64 * 16;
 constexpr int GBYTES = GPAIRS * 64 * 16;
 constexpr int GDBYTES = 2 * 64 * 16;  // a G tile untagged: two 16-byte rows of 64 lanes (the bulk copy)
-constexpr int NB = 4;                 // bulk G tiles a U wave has in flight
+constexpr int NB = 6;                 // bulk G tiles a U wave has in flight
 constexpr long long POLL_LIMIT = 20000000;  // s_memrealtime ticks (100 MHz): 200 ms
 constexpr int TREG = 11;                    // tile slots a U wave holds in registers (more would spill)
 constexpr int TREG_L = 10, TLDS_L = 9;      // large systems (77 < nT <= 133): 10 slots in registers, 9 in LDS
