@@ -379,6 +379,31 @@ __device__ __forceinline__ double gy(const d4 &g, double yl, int lane) {
 
 // tile A_rj of the damped, identity-padded system, held as the accumulator
 // of A_rj^T: element e of lane l = A(16 r + (l & 15), 16 j + (l >> 4) + 4e)
+// a strictly lower tile (j <= r - 2: no diagonal element, no damping) of the
+// U waves' prologue from the payload: pay_index in 32-bit arithmetic with the
+// lane's row terms hoisted, zero unless live, every load unconditional (in
+// bounds) so that a group of tiles has its loads in flight together
+__device__ __forceinline__ d4 load_lower(const Args &a, int r, int j, int lane) {
+    const int I = TL * r + (lane & 15), nc = (a.ns + 5) / 6;
+    const int ib = I / 6, ir = I - 6 * ib;
+    const bool live = j <= r - 2 && I < a.ns;
+    int idx[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int J = TL * j + (lane >> 4) + 4 * e, jb = J / 6, jr = J - 6 * jb;
+        // J < I: block (jb, ib) of the upper block triangle; inside one
+        // camera block the element (ir, jr), as the 64-bit pay_index takes it
+        const int blk = 36 * (jb * nc - jb * (jb - 1) / 2 + ib - jb);
+        idx[e] = live ? blk + (ib == jb ? ir * 6 + jr : jr * 6 + ir) : 0;
+    }
+    d4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = a.payload[idx[e]];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        if (!live) v[e] = 0.0;
+    return v;
+}
 __device__ __forceinline__ d4 load_tile(const Args &a, double lambda, int r, int j, int lane) {
     if (a.src.slab) {  // from the slabs: the finish's sums, in its order (the same bits)
         d4 v;
@@ -588,17 +613,41 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
         q[128] = v[2];
         q[192] = v[3];
     };
-    // a tile at a time, in a loop that is not unrolled (the loads of all of
-    // them at once would spill; unrolled, the slab loads make it too large to
-    // keep the slots in registers): the slot is chosen by selects
-#pragma unroll 1
-    for (int k = 0; k < TPW; ++k) {
-        const int j = w + NUW * k;
-        const d4 v = j <= r - 2 ? load_tile(a, lambda, r, j, lane) : zero4();
+    // PG tiles at a time from the payload (their loads in flight together:
+    // the late owners' U waves start their first step sooner, cfg5 0.296 ->
+    // 0.290 ms) when a wave holds more than 4 tiles (with 4, cfg4, the same
+    // change cost 0.081 -> 0.085 ms), else a tile at a time (and always from
+    // the slabs, SlabSrc); loops that are not unrolled (all the loads at once
+    // would spill), the slot chosen by selects
+    if (TPW > 4 && !a.src.slab) {
 #pragma unroll
-        for (int kk = 0; kk < TR; ++kk)
-            if (kk == k) T[kk] = v;
-        if (k >= TR) tset(k, v);
+        for (int kk = 0; kk < TR; ++kk) T[kk] = zero4();  // tiles right of r - 2: set by the import
+        constexpr int PG = 4;
+#pragma unroll 1
+        for (int k0 = 0; k0 < TPW; k0 += PG) {
+            if (w + NUW * k0 > r - 2) break;  // nothing live from here on
+            d4 v[PG];
+#pragma unroll
+            for (int q = 0; q < PG; ++q) v[q] = load_lower(a, r, w + NUW * (k0 + q), lane);
+#pragma unroll
+            for (int q = 0; q < PG; ++q) {
+                const int k = k0 + q;
+#pragma unroll
+                for (int kk = 0; kk < TR; ++kk)
+                    if (kk == k) T[kk] = v[q];
+                if (k >= TR && k < TPW) tset(k, v[q]);
+            }
+        }
+    } else {
+#pragma unroll 1
+        for (int k = 0; k < TPW; ++k) {
+            const int j = w + NUW * k;
+            const d4 v = j <= r - 2 ? load_tile(a, lambda, r, j, lane) : zero4();
+#pragma unroll
+            for (int kk = 0; kk < TR; ++kk)
+                if (kk == k) T[kk] = v;
+            if (k >= TR) tset(k, v);
+        }
     }
     for (int p = 0; p < nT; ++p) {
         const int s = p & (RING - 1);

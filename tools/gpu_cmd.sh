@@ -9,8 +9,7 @@ step() {  # step NAME SECONDS CMD...
     echo "[$name] rc=$rc"; grep -v amdgpu.ids "gpurun_out/$name.txt" | tail -${TAILN:-8}
     if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
-step acc 120 python -u tools/gjr_accuracy.py
-TAILN=3 step ab 300 python -u tools/gj_ab.py SFM_SOLVE gjr 3
-TAILN=3 step tl300 120 python -u tools/gjr_timeline.py 300
-TAILN=3 step tl1200 120 python -u tools/gjr_timeline.py 1200
-step t1 500 python -u -m pytest -q --timeout 120 --timeout-method thread tests -m gpu
+for v in HD cur HD cur; do
+  d=tools/_ab$v; [ $v = cur ] && d=structure-from-motion-_amd
+  TAILN=2 step ab$v 300 python -u tools/gj_ab.py SFM_SOLVE gjr 2 $d
+done
