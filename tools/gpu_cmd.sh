@@ -9,7 +9,7 @@ step() {  # step NAME SECONDS CMD...
     echo "[$name] rc=$rc"; grep -v amdgpu.ids "gpurun_out/$name.txt" | tail -${TAILN:-8}
     if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
-for v in cur lb4 lb3 lb4p4 cur lb4 lb3 lb4p4; do
-  d=tools/_ab$v; [ $v = cur ] && d=structure-from-motion-_amd
-  TAILN=2 step ab$v 300 python -u tools/gj_ab.py SFM_SOLVE gjr 1 $d
+step acc 120 python -u tools/gjr_accuracy.py tools/_abG3
+for v in HD G3 HD G3; do
+  TAILN=2 step ab$v 300 python -u tools/gj_ab.py SFM_SOLVE gjr 2 tools/_ab$v
 done
