@@ -527,17 +527,21 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
             stamp(a, p, DBG_GCRIT);
             Td = mfma4(Td, -g, g);
             b -= gy(g, yl, lane);
-            if (!lds_wait(&S.gdone[s], NW * g_uses(p, r), S)) return false;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) S.GL[s][e][lane] = g[e];
-            lds_release();
-            lds_set(&S.gready[s], p + 1);
-            lds_add(&S.gdone[s], 1);
         } else if (p == r) {
             pivot(a, rs, S, r, lane, Td, b);
             if (r > 0) {
                 put_bulk(rs.Gd, gdoff(a, r - 1, r), gc, lane);
                 flag_bulk(a, r - 1, r);
+                // the ring piece of the critical step r - 1, after the pivot
+                // record is out: no U wave has a live tile at step r - 1, they
+                // only count the slot, so it leaves the critical path
+                const int sc = (r - 1) & (RING - 1);
+                if (!lds_wait(&S.gdone[sc], NW * g_uses(r - 1, r), S)) return false;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) S.GL[sc][e][lane] = gc[e];
+                lds_release();
+                lds_set(&S.gready[sc], r);
+                lds_add(&S.gdone[sc], 1);
             }
         } else {
             // G_{r-1} of this step (for A_r,r-1) first: owner r - 1 publishes

@@ -9,7 +9,6 @@ step() {  # step NAME SECONDS CMD...
     echo "[$name] rc=$rc"; grep -v amdgpu.ids "gpurun_out/$name.txt" | tail -${TAILN:-8}
     if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
-step acc 120 python -u tools/gjr_accuracy.py tools/_abG3
-for v in HD G3 HD G3; do
-  TAILN=2 step ab$v 300 python -u tools/gj_ab.py SFM_SOLVE gjr 2 tools/_ab$v
-done
+step t1 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu
+TAILN=3 step tl300 120 python -u tools/gjr_timeline.py 300
+TAILN=3 step tl1200 120 python -u tools/gjr_timeline.py 1200
