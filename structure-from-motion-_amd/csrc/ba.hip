@@ -2235,8 +2235,13 @@ static int launch_gjr(const GjrPlan &g, int32_t ns, const double *payload, const
 
 // partial[block][4] = {trial cost, model_p, |dp|^2, |X|^2}
 constexpr int BS_PRE = 6;  // observations per lane prefetched by k_backsub_trial
-template <int G>
-__global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const int32_t *__restrict__ pstart,
+// CL: the cameras (Rt 12 | Rt_new 12 | dc 6 doubles, 240 B each) staged in
+// LDS once per workgroup, so the per-observation camera reads (30 doubles,
+// 240 B) are LDS reads instead of L1/L2 gathers
+constexpr int BS_CAM = 30;
+constexpr int BS_CAM_LDS_MAX = 64 * 1024;
+template <int G, bool CL>
+__global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, int32_t nc, const int32_t *__restrict__ pstart,
                                                               const int32_t *__restrict__ cam,
                                                               const double2 *__restrict__ obs, Kmat Km,
                                                               const double *__restrict__ Vg,
@@ -2285,6 +2290,24 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
     const int64_t stride = (int64_t)gridDim.x * PT_THREADS;
     Pre cur;
     fetch((int64_t)blockIdx.x * PT_THREADS + threadIdx.x, cur);
+    extern __shared__ __attribute__((aligned(16))) double bs_cam[];
+    if constexpr (CL) {
+        auto stage = [&](const double *__restrict__ src, int w, int off) {
+            const int n = w * nc;
+#pragma unroll 4
+            for (int i = threadIdx.x; i < n; i += PT_THREADS) {
+                const int c = i / w;
+                bs_cam[BS_CAM * c + off + (i - w * c)] = src[i];
+            }
+        };
+        stage(Rt, 12, 0);
+        stage(Rt_new, 12, 12);
+        stage(dc, 6, 24);
+        __syncthreads();
+    }
+    const double *const cRt = CL ? bs_cam : Rt, *const cRn = CL ? bs_cam + 12 : Rt_new,
+                        *const cdc = CL ? bs_cam + 24 : dc;
+    constexpr int RS = CL ? BS_CAM : 12, DS = CL ? BS_CAM : 6;
     for (int64_t gt = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x; gt / G < np_; gt += stride) {
     const int64_t p = gt / G;  // G lanes per point, striding over its observations
     const int sub = (int)(gt % G);
@@ -2307,8 +2330,8 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
     double wt[3] = {0, 0, 0};
     const double x[3] = {cur.x[0], cur.x[1], cur.x[2]};
     auto wt_add = [&](int32_t c) {
-        const double *d = dc + 6 * c;
-        const double *R = Rt + 12 * c;
+        const double *d = cdc + DS * c;
+        const double *R = cRt + RS * c;
         double A[2][3], q[3];
         obs_Ap(R, x, K, A, q);
         const double v0 = d[1] * q[2] - d[2] * q[1] + d[3];
@@ -2350,8 +2373,8 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, const
         }
 #pragma unroll
         for (int k = 0; k < BS_PRE; ++k)
-            if (o0 + sub + k * G < o1) acc[0] += obs_cost(Rt_new + 12 * cpre[k], xn, K, opre[k]);
-        for (int32_t o = o0 + sub + BS_PRE * G; o < o1; o += G) acc[0] += obs_cost(Rt_new + 12 * cam[o], xn, K, obs[o]);
+            if (o0 + sub + k * G < o1) acc[0] += obs_cost(cRn + RS * cpre[k], xn, K, opre[k]);
+        for (int32_t o = o0 + sub + BS_PRE * G; o < o1; o += G) acc[0] += obs_cost(cRn + RS * cam[o], xn, K, obs[o]);
     }
     cur = nxt;
     }
@@ -2428,6 +2451,31 @@ struct SweepPlan {
 static int env_int(const char *name, int dflt) {
     const char *v = std::getenv(name);
     return v ? std::atoi(v) : dflt;
+}
+
+// k_backsub_trial's grid when the cameras fit its LDS stage: the resident
+// workgroup count for that LDS size (every workgroup starts at once), at most
+// the partial-sum slots; 0 selects the global-camera kernel
+static int backsub_cl_blocks(int32_t nc, int ncu, int max_blocks) {
+    if (env_int("SFM_BACKSUB_CAM_LDS", 1) == 0) return 0;
+    const size_t lds = (size_t)8 * BS_CAM * nc;
+    if (nc < 1 || lds > (size_t)BS_CAM_LDS_MAX) return 0;
+    int nb = 0;
+    auto occ = [&](auto kern) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, PT_THREADS, lds) != hipSuccess)
+            nb = 0;
+    };
+    switch (lanes_per_point("SFM_BACKSUB_LANES", 2)) {  // the instantiation the launch picks
+    case 1: occ(k_backsub_trial<1, true>); break;
+    case 2: occ(k_backsub_trial<2, true>); break;
+    case 4: occ(k_backsub_trial<4, true>); break;
+    default: occ(k_backsub_trial<8, true>); break;
+    }
+    (void)hipGetLastError();
+    if (nb < 1) return 0;
+    return std::max(1, std::min(nb * ncu, max_blocks));
 }
 
 // camera items for camera_lin_wg from workgroup cuts (camera-major
@@ -2933,6 +2981,7 @@ struct sfm_ba_problem {
     bool timing = false;                         // per-phase HIP events (sfm_ba_set_timing)
     int64_t payload_len = 0;
     int pt_blocks = 0;
+    int bs_cl_blocks = 0;  // k_backsub_trial with the cameras in LDS: its grid (0: cameras from global)
     hipEvent_t ev[2 * T_NT] = {};
     hipEvent_t ev_it[2 * T_NT * kEvSlots] = {};  // per-iteration timing slots of a batch
     LMState *d_lm = nullptr;
@@ -3224,6 +3273,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         return rc;
     p->gjrp = p->tb == 16 ? gjr_plan(p->nT, device_cus(device)) : GjrPlan{};
     p->gjp = p->tb == 16 && !p->gjrp.ok() ? gj_plan(p->nT, device_cus(device)) : GjPlan{};
+    p->bs_cl_blocks = backsub_cl_blocks(nc, device_cus(device), p->pt_blocks);
     if (p->gjrp.ok()) {
         gjr::u64 *gw = nullptr;
         int *gi = nullptr;
@@ -3619,11 +3669,16 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     const int gb = lanes_per_point("SFM_BACKSUB_LANES", 2);
     // grid-stride: 1024 workgroups (4 per CU); measured at cfg4 (1563 needed
     // without the stride): 512 -> 49 us, 896..1152 -> 43 us, 2048+ -> 51 us
-    const int nbb = std::max(1, std::min(ceil_div(p->np * gb, PT_THREADS), env_int("SFM_BACKSUB_BLOCKS", 1024)));
+    // with the cameras in LDS: as many workgroups as are resident at once
+    // (a grid-stride kernel whose last workgroups start late ends late)
+    const bool cl = p->bs_cl_blocks > 0;
+    const int nbb = std::max(1, std::min(ceil_div(p->np * gb, PT_THREADS),
+                                         env_int("SFM_BACKSUB_BLOCKS", cl ? p->bs_cl_blocks : 1024)));
+    const size_t cl_lds = cl ? (size_t)8 * BS_CAM * p->nc : 0;
 #define SFM_BS(G)                                                                                                  \
-    hipLaunchKernelGGL(k_backsub_trial<G>, dim3(nbb), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam,        \
-                       p->d_obs, p->K, p->d_Vg, p->d_Lq, p->d_b, lam, p->d_Rt, p->d_Rt2, p->d_X, p->d_X2, \
-                       p->d_partial, p->d_count + GS_WORDS, p->d_scal, gst)
+    hipLaunchKernelGGL((cl ? k_backsub_trial<G, true> : k_backsub_trial<G, false>), dim3(nbb), dim3(PT_THREADS),   \
+                       cl_lds, s, p->np, p->nc, p->d_pstart, p->d_cam, p->d_obs, p->K, p->d_Vg, p->d_Lq, p->d_b,  \
+                       lam, p->d_Rt, p->d_Rt2, p->d_X, p->d_X2, p->d_partial, p->d_count + GS_WORDS, p->d_scal, gst)
     switch (gb) { case 1: SFM_BS(1); break; case 2: SFM_BS(2); break; case 4: SFM_BS(4); break; default: SFM_BS(8); }
 #undef SFM_BS
     SFM_HIP(hipGetLastError());

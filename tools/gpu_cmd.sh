@@ -9,6 +9,14 @@ step() {  # step NAME SECONDS CMD...
     echo "[$name] rc=$rc"; grep -v amdgpu.ids "gpurun_out/$name.txt" | tail -${TAILN:-8}
     if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
-step t1 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu
-TAILN=3 step tl300 120 python -u tools/gjr_timeline.py 300
-TAILN=3 step tl1200 120 python -u tools/gjr_timeline.py 1200
+B="python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-next-rows --no-end-to-end --no-shard-local"
+TAILN=30 step t1 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu -k "ba_cfg or multi_rank or backsub or perform_bundle"
+for v in 0 1 0 1; do
+  SFM_BACKSUB_CAM_LDS=$v TAILN=1 step b$v 200 $B
+  python - "$v" <<'PY'
+import json,sys
+d=json.loads(open(f"gpurun_out/b{sys.argv[1]}.txt").read().strip().splitlines()[-1])
+k=d.get("kernels_ms_per_iter",{}); s=d.get("secondary",{}) or {}
+print("LDS", sys.argv[1], d["value"], d["ms_per_step"], {a: k[a] for a in k if "trial" in a or "back" in a})
+PY
+done
