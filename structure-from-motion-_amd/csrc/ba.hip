@@ -138,9 +138,9 @@ __device__ __forceinline__ void block_sum_store(double (&v)[NV], double *out) {
 constexpr int GS_STRIDE = 32;
 constexpr int GS_WORDS = 9 * GS_STRIDE;
 
-template <int NV>
+template <int NV, int NT = PT_THREADS>
 __device__ __forceinline__ void grid_sum_last(double (&v)[NV], double *partial, unsigned *counter, double *out) {
-    __shared__ double red[PT_THREADS / 64][NV];
+    __shared__ double red[NT / 64][NV];
     __shared__ int last;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const unsigned nblk = gridDim.x;
@@ -154,7 +154,7 @@ __device__ __forceinline__ void grid_sum_last(double (&v)[NV], double *partial, 
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
             double s = 0;
-            for (int i = 0; i < PT_THREADS / 64; ++i) s += red[i][k];
+            for (int i = 0; i < NT / 64; ++i) s += red[i][k];
             __hip_atomic_store(partial + (int64_t)NV * blockIdx.x + k, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         // Release side.  The partials are agent-scope atomic stores (sc1,
@@ -185,16 +185,16 @@ __device__ __forceinline__ void grid_sum_last(double (&v)[NV], double *partial, 
     // would add ~1.7 us to the tail of every launch.
     // all NV sums at once: NV x GS_BATCH independent sc1 loads in flight
     // per thread, one tree -- per value the same order as summing them one by one
-    __shared__ double tot[NV][PT_THREADS];
+    __shared__ double tot[NV][NT];
     double s[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) s[k] = 0;
     constexpr int GS_BATCH = NV > 1 ? 8 : 16;  // bounded so the tail does not set the kernel's VGPR count
-    for (unsigned b0 = threadIdx.x; b0 < nblk; b0 += GS_BATCH * PT_THREADS) {
+    for (unsigned b0 = threadIdx.x; b0 < nblk; b0 += GS_BATCH * NT) {
         double v16[NV][GS_BATCH];
 #pragma unroll
         for (int u = 0; u < GS_BATCH; ++u) {
-            const unsigned b = b0 + u * PT_THREADS;
+            const unsigned b = b0 + u * NT;
 #pragma unroll
             for (int k = 0; k < NV; ++k)
                 v16[k][u] = b < nblk ? __hip_atomic_load(partial + (int64_t)NV * b + k, __ATOMIC_RELAXED,
@@ -209,7 +209,7 @@ __device__ __forceinline__ void grid_sum_last(double (&v)[NV], double *partial, 
 #pragma unroll
     for (int k = 0; k < NV; ++k) tot[k][threadIdx.x] = s[k];
     __syncthreads();
-    for (int st = PT_THREADS / 2; st > 0; st >>= 1) {
+    for (int st = NT / 2; st > 0; st >>= 1) {
         if ((int)threadIdx.x < st)
 #pragma unroll
             for (int k = 0; k < NV; ++k) tot[k][threadIdx.x] += tot[k][threadIdx.x + st];
@@ -2240,8 +2240,8 @@ constexpr int BS_PRE = 6;  // observations per lane prefetched by k_backsub_tria
 // 240 B) are LDS reads instead of L1/L2 gathers
 constexpr int BS_CAM = 30;
 constexpr int BS_CAM_LDS_MAX = 64 * 1024;
-template <int G, bool CL>
-__global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, int32_t nc, const int32_t *__restrict__ pstart,
+template <int G, bool CL, int NT = PT_THREADS>
+__global__ void __launch_bounds__(NT) k_backsub_trial(int64_t np_, int32_t nc, const int32_t *__restrict__ pstart,
                                                               const int32_t *__restrict__ cam,
                                                               const double2 *__restrict__ obs, Kmat Km,
                                                               const double *__restrict__ Vg,
@@ -2287,15 +2287,15 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, int32
 #pragma unroll
         for (int i = 0; i < 6; ++i) P.l[i] = l[i];
     };
-    const int64_t stride = (int64_t)gridDim.x * PT_THREADS;
+    const int64_t stride = (int64_t)gridDim.x * NT;
     Pre cur;
-    fetch((int64_t)blockIdx.x * PT_THREADS + threadIdx.x, cur);
+    fetch((int64_t)blockIdx.x * NT + threadIdx.x, cur);
     extern __shared__ __attribute__((aligned(16))) double bs_cam[];
     if constexpr (CL) {
         auto stage = [&](const double *__restrict__ src, int w, int off) {
             const int n = w * nc;
 #pragma unroll 4
-            for (int i = threadIdx.x; i < n; i += PT_THREADS) {
+            for (int i = threadIdx.x; i < n; i += NT) {
                 const int c = i / w;
                 bs_cam[BS_CAM * c + off + (i - w * c)] = src[i];
             }
@@ -2308,7 +2308,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, int32
     const double *const cRt = CL ? bs_cam : Rt, *const cRn = CL ? bs_cam + 12 : Rt_new,
                         *const cdc = CL ? bs_cam + 24 : dc;
     constexpr int RS = CL ? BS_CAM : 12, DS = CL ? BS_CAM : 6;
-    for (int64_t gt = (int64_t)blockIdx.x * PT_THREADS + threadIdx.x; gt / G < np_; gt += stride) {
+    for (int64_t gt = (int64_t)blockIdx.x * NT + threadIdx.x; gt / G < np_; gt += stride) {
     const int64_t p = gt / G;  // G lanes per point, striding over its observations
     const int sub = (int)(gt % G);
     const bool live = p < np_;
@@ -2378,7 +2378,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_backsub_trial(int64_t np_, int32
     }
     cur = nxt;
     }
-    grid_sum_last<4>(acc, partial, counter, out);
+    grid_sum_last<4, NT>(acc, partial, counter, out);
 }
 
 // ---------------------------------------------------------------- host math
@@ -2456,7 +2456,7 @@ static int env_int(const char *name, int dflt) {
 // k_backsub_trial's grid when the cameras fit its LDS stage: the resident
 // workgroup count for that LDS size (every workgroup starts at once), at most
 // the partial-sum slots; 0 selects the global-camera kernel
-static int backsub_cl_blocks(int32_t nc, int ncu, int max_blocks) {
+static int backsub_cl_blocks(int32_t nc, int ncu, int max_blocks, int nt) {
     if (env_int("SFM_BACKSUB_CAM_LDS", 1) == 0) return 0;
     const size_t lds = (size_t)8 * BS_CAM * nc;
     if (nc < 1 || lds > (size_t)BS_CAM_LDS_MAX) return 0;
@@ -2464,14 +2464,25 @@ static int backsub_cl_blocks(int32_t nc, int ncu, int max_blocks) {
     auto occ = [&](auto kern) {
         if (hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, PT_THREADS, lds) != hipSuccess)
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, nt, lds) != hipSuccess)
             nb = 0;
     };
-    switch (lanes_per_point("SFM_BACKSUB_LANES", 2)) {  // the instantiation the launch picks
-    case 1: occ(k_backsub_trial<1, true>); break;
-    case 2: occ(k_backsub_trial<2, true>); break;
-    case 4: occ(k_backsub_trial<4, true>); break;
-    default: occ(k_backsub_trial<8, true>); break;
+    // the instantiation the launch picks
+    const int g = lanes_per_point("SFM_BACKSUB_LANES", 2);
+    if (nt == 256) {
+        switch (g) {
+        case 1: occ(k_backsub_trial<1, true, 256>); break;
+        case 2: occ(k_backsub_trial<2, true, 256>); break;
+        case 4: occ(k_backsub_trial<4, true, 256>); break;
+        default: occ(k_backsub_trial<8, true, 256>); break;
+        }
+    } else {
+        switch (g) {
+        case 1: occ(k_backsub_trial<1, true>); break;
+        case 2: occ(k_backsub_trial<2, true>); break;
+        case 4: occ(k_backsub_trial<4, true>); break;
+        default: occ(k_backsub_trial<8, true>); break;
+        }
     }
     (void)hipGetLastError();
     if (nb < 1) return 0;
@@ -2982,6 +2993,7 @@ struct sfm_ba_problem {
     int64_t payload_len = 0;
     int pt_blocks = 0;
     int bs_cl_blocks = 0;  // k_backsub_trial with the cameras in LDS: its grid (0: cameras from global)
+    int bs_threads = PT_THREADS;  // and its workgroup size
     hipEvent_t ev[2 * T_NT] = {};
     hipEvent_t ev_it[2 * T_NT * kEvSlots] = {};  // per-iteration timing slots of a batch
     LMState *d_lm = nullptr;
@@ -3273,7 +3285,8 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         return rc;
     p->gjrp = p->tb == 16 ? gjr_plan(p->nT, device_cus(device)) : GjrPlan{};
     p->gjp = p->tb == 16 && !p->gjrp.ok() ? gj_plan(p->nT, device_cus(device)) : GjPlan{};
-    p->bs_cl_blocks = backsub_cl_blocks(nc, device_cus(device), p->pt_blocks);
+    p->bs_threads = env_int("SFM_BACKSUB_THREADS", 256) == 256 ? 256 : PT_THREADS;
+    p->bs_cl_blocks = backsub_cl_blocks(nc, device_cus(device), p->pt_blocks, p->bs_threads);
     if (p->gjrp.ok()) {
         gjr::u64 *gw = nullptr;
         int *gi = nullptr;
@@ -3672,12 +3685,13 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     // with the cameras in LDS: as many workgroups as are resident at once
     // (a grid-stride kernel whose last workgroups start late ends late)
     const bool cl = p->bs_cl_blocks > 0;
-    const int nbb = std::max(1, std::min(ceil_div(p->np * gb, PT_THREADS),
+    const int nbb = std::max(1, std::min(ceil_div(p->np * gb, cl ? p->bs_threads : PT_THREADS),
                                          env_int("SFM_BACKSUB_BLOCKS", cl ? p->bs_cl_blocks : 1024)));
     const size_t cl_lds = cl ? (size_t)8 * BS_CAM * p->nc : 0;
 #define SFM_BS(G)                                                                                                  \
-    hipLaunchKernelGGL((cl ? k_backsub_trial<G, true> : k_backsub_trial<G, false>), dim3(nbb), dim3(PT_THREADS),   \
-                       cl_lds, s, p->np, p->nc, p->d_pstart, p->d_cam, p->d_obs, p->K, p->d_Vg, p->d_Lq, p->d_b,  \
+    hipLaunchKernelGGL((!cl ? k_backsub_trial<G, false> : p->bs_threads == 256 ? k_backsub_trial<G, true, 256>      \
+                                                                              : k_backsub_trial<G, true>),        \
+                       dim3(nbb), dim3(cl ? p->bs_threads : PT_THREADS), cl_lds, s, p->np, p->nc, p->d_pstart, p->d_cam, p->d_obs, p->K, p->d_Vg, p->d_Lq, p->d_b,  \
                        lam, p->d_Rt, p->d_Rt2, p->d_X, p->d_X2, p->d_partial, p->d_count + GS_WORDS, p->d_scal, gst)
     switch (gb) { case 1: SFM_BS(1); break; case 2: SFM_BS(2); break; case 4: SFM_BS(4); break; default: SFM_BS(8); }
 #undef SFM_BS

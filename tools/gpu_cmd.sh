@@ -10,13 +10,14 @@ step() {  # step NAME SECONDS CMD...
     if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
 B="python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-next-rows --no-end-to-end --no-shard-local"
-TAILN=30 step t1 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu -k "ba_cfg or multi_rank or backsub or perform_bundle"
-for v in 0 1 0 1; do
-  SFM_BACKSUB_CAM_LDS=$v TAILN=1 step b$v 200 $B
-  python - "$v" <<'PY'
+for r in 1 2; do
+for tg in 128:2 256:2 128:1 256:1 128:4; do
+  T=${tg%:*}; G=${tg#*:}
+  SFM_BACKSUB_THREADS=$T SFM_BACKSUB_LANES=$G TAILN=0 step b${T}_$G 200 $B
+  python - "b${T}_$G" <<'PY'
 import json,sys
-d=json.loads(open(f"gpurun_out/b{sys.argv[1]}.txt").read().strip().splitlines()[-1])
-k=d.get("kernels_ms_per_iter",{}); s=d.get("secondary",{}) or {}
-print("LDS", sys.argv[1], d["value"], d["ms_per_step"], {a: k[a] for a in k if "trial" in a or "back" in a})
+d=json.loads(open(f"gpurun_out/{sys.argv[1]}.txt").read().strip().splitlines()[-1])
+print(sys.argv[1], "cfg5", d["value"], d["kernels_ms_per_iter"]["backsub_trial"]["ms"], "cfg4", d["cfg4"]["value"], d["cfg4"]["kernels_ms_per_iter"]["backsub_trial"]["ms"])
 PY
+done
 done
