@@ -1176,27 +1176,41 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     stamp(SW_STAMP_EV - 1);
 }
 
-// one 64-thread workgroup per camera block (i <= j, dense upper-triangle
-// index): fixed-order sum over the ranges, then U_i - S (diagonal) / -S
-// (off-diagonal, mirrored), g_c and sum Z q into the payload
-__global__ void __launch_bounds__(64) k_schur_finish(int32_t ns, int32_t nbd, int32_t nrange,
-                                                     const int2 *__restrict__ blkij, const double *__restrict__ slab,
-                                                     const double *__restrict__ camlin,
-                                                     double *__restrict__ payload, const int *__restrict__ gate,
-                                                     const int32_t *__restrict__ split_of, SweepSplit sp) {
+// one thread per (camera block, entry) over the dense upper-triangle block
+// index (blocks of ITEM_W entries, coalesced across the workgroup): fixed-
+// order sum over the ranges, then U_i - S (diagonal) / -S (off-diagonal,
+// mirrored), g_c and sum Z q into the payload.  (Round 4: it was one
+// 64-thread workgroup per block, 42 lanes busy, one range load at a time:
+// 20,100 workgroups at cfg5, 28 us.)
+constexpr int FIN_THREADS = 256;
+__global__ void __launch_bounds__(FIN_THREADS) k_schur_finish(int32_t ns, int32_t nbd, int32_t nrange,
+                                                              const int2 *__restrict__ blkij,
+                                                              const double *__restrict__ slab,
+                                                              const double *__restrict__ camlin,
+                                                              double *__restrict__ payload, const int *__restrict__ gate,
+                                                              const int32_t *__restrict__ split_of, SweepSplit sp) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
-    const int2 ij = blkij[blockIdx.x];
-    const int t = threadIdx.x;
+    const int64_t e = (int64_t)blockIdx.x * FIN_THREADS + threadIdx.x;
+    if (e >= (int64_t)nbd * ITEM_W) return;
+    const int b = (int)(e / ITEM_W), t = (int)(e - (int64_t)b * ITEM_W);
+    const int2 ij = blkij[b];
     const bool diag = ij.x == ij.y;
     if (t >= (diag ? ITEM_W : 36)) return;
+    const int si = sp.S > 0 ? split_of[b] : -1;  // (spec - w0) * gmax + group, split specs only
+    // the partials in range order, eight loads in flight, summed one by one
+    const double *src = si < 0 ? slab + (int64_t)b * ITEM_W + t : sp.slabx + (int64_t)si * ITEM_W + t;
+    const int64_t rstr = si < 0 ? (int64_t)nbd * ITEM_W : (int64_t)sp.nsplit * sp.gmax * ITEM_W;
+    const int n = si < 0 ? nrange : nrange * sp.S;
     double v = 0;
-    const int si = sp.S > 0 ? split_of[blockIdx.x] : -1;  // (spec - w0) * gmax + group, split specs only
-    if (si < 0) {
-        for (int r = 0; r < nrange; ++r) v += slab[((int64_t)r * nbd + blockIdx.x) * ITEM_W + t];
-    } else {
-        const int64_t row = (int64_t)sp.nsplit * sp.gmax;
-        for (int rs = 0; rs < nrange * sp.S; ++rs) v += sp.slabx[(rs * row + si) * ITEM_W + t];
+    int q = 0;
+    for (; q + 8 <= n; q += 8) {
+        double a8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a8[u] = src[(q + u) * rstr];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v += a8[u];
     }
+    for (; q < n; ++q) v += src[q * rstr];
     const int64_t base = pay_vec_base(ns);
     if (t < 36) {
         const int r = t / 6, c = t % 6;
@@ -3643,7 +3657,7 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     // -> 0.523 ms against the finish's 0.028 ms, round 4)
     const bool fin_fused = !p->comm && p->fin_fused && !p->gjp.cb && (!p->gjrp.ok() || p->gjr_fold);
     if (!fin_fused) {
-        hipLaunchKernelGGL(k_schur_finish, dim3(p->sw_nbd), dim3(64), 0, s, p->ns, p->sw_nbd, p->sw_nrange,
+        hipLaunchKernelGGL(k_schur_finish, dim3(ceil_div(p->sw_nbd * ITEM_W, FIN_THREADS)), dim3(FIN_THREADS), 0, s, p->ns, p->sw_nbd, p->sw_nrange,
                            p->d_sw_blkij, p->d_slab, p->d_camlin, p->d_payload, gst, p->d_sw_split_of, p->sw_split);
         SFM_HIP(hipGetLastError());
     }

@@ -2,6 +2,7 @@
 # a signal, a time limit or an abort (rc >= 124) ends the session there.
 set -o pipefail
 mkdir -p gpurun_out
+export TMPDIR=/tmp
 step() {  # step NAME SECONDS CMD...
     local name=$1 t=$2; shift 2
     timeout -k 10 "$t" "$@" > "gpurun_out/$name.txt" 2>&1
@@ -10,14 +11,17 @@ step() {  # step NAME SECONDS CMD...
     if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
 B="python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-next-rows --no-end-to-end --no-shard-local"
-for r in 1 2; do
-for tg in 128:2 256:2 128:1 256:1 128:4; do
-  T=${tg%:*}; G=${tg#*:}
-  SFM_BACKSUB_THREADS=$T SFM_BACKSUB_LANES=$G TAILN=0 step b${T}_$G 200 $B
-  python - "b${T}_$G" <<'PY'
-import json,sys
-d=json.loads(open(f"gpurun_out/{sys.argv[1]}.txt").read().strip().splitlines()[-1])
-print(sys.argv[1], "cfg5", d["value"], d["kernels_ms_per_iter"]["backsub_trial"]["ms"], "cfg4", d["cfg4"]["value"], d["cfg4"]["kernels_ms_per_iter"]["backsub_trial"]["ms"])
+TAILN=4 step t1 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu -k "ba or reduced or schur or gj or perform_bundle"
+TAILN=2 step ks 200 rocprofv3 --kernel-trace --stats -d gpurun_out/ks -o ks -- python3 tools/ba_once.py cfg5
+f=$(find gpurun_out/ks -name "*kernel_stats.csv" | head -1); python3 - "$f" <<'PY'
+import csv,sys
+for r in csv.DictReader(open(sys.argv[1])):
+    print(r["Name"][:40], r["Calls"], round(float(r["AverageNs"])/1000,2))
 PY
-done
-done
+TAILN=0 step b1 200 $B
+python - <<'PY'
+import json
+d=json.loads(open("gpurun_out/b1.txt").read().strip().splitlines()[-1])
+print("cfg5", d["value"], d["ms_per_step"], d["converged_LM_it_per_s"], {k: v["ms"] for k, v in d["kernels_ms_per_iter"].items()})
+c=d["cfg4"]; print("cfg4", c["value"], c["ms_per_step"], c["converged_LM_it_per_s"], {k: v["ms"] for k, v in c["kernels_ms_per_iter"].items()})
+PY
