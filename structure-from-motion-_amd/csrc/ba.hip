@@ -372,28 +372,43 @@ __global__ void __launch_bounds__(OBS_THREADS) k_point_prep(int64_t np_, const d
                                                             const double *__restrict__ lam, double *__restrict__ Lq,
                                                             const int *__restrict__ gate) {
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
-    const int64_t p = (int64_t)blockIdx.x * OBS_THREADS + threadIdx.x;
-    if (p >= np_) return;
-    const double lambda = *lam;
-    const double *vg = Vg + 9 * p;
-    const double v00 = vg[0] + lambda * clampd(vg[0]), v01 = vg[1], v02 = vg[2];
-    const double v11 = vg[3] + lambda * clampd(vg[3]), v12 = vg[4];
-    const double v22 = vg[5] + lambda * clampd(vg[5]);
-    const double c00 = sqrt(v00), c10 = v01 / c00, c20 = v02 / c00;
-    const double c11 = sqrt(v11 - c10 * c10), c21 = (v12 - c20 * c10) / c11;
-    const double c22 = sqrt(v22 - c20 * c20 - c21 * c21);
-    const double i00 = 1.0 / c00, i11 = 1.0 / c11, i22 = 1.0 / c22;
-    const double i10 = -c10 * i00 * i11;
-    const double i21 = -c21 * i11 * i22;
-    const double i20 = -(c20 * i00 + c21 * i10) * i22;
-    // L = Cinv^T (upper): Vd^-1 = L L^T
-    const double L[3][3] = {{i00, i10, i20}, {0.0, i11, i21}, {0.0, 0.0, i22}};
-    const double g0 = vg[6], g1 = vg[7], g2 = vg[8];
-    double *lq = Lq + 9 * p;
-    lq[0] = L[0][0]; lq[1] = L[0][1]; lq[2] = L[0][2]; lq[3] = L[1][1]; lq[4] = L[1][2]; lq[5] = L[2][2];
-    lq[6] = L[0][0] * g0;
-    lq[7] = L[0][1] * g0 + L[1][1] * g1;
-    lq[8] = L[0][2] * g0 + L[1][2] * g1 + L[2][2] * g2;
+    // the workgroup's 9-double records go through LDS both ways: coalesced
+    // global loads and stores (a thread's own 72-B record, strided across
+    // the wave, touched 36 lines per load instruction)
+    __shared__ double buf[9 * OBS_THREADS];
+    const int64_t p0 = (int64_t)blockIdx.x * OBS_THREADS;
+    const int n9 = 9 * (int)(np_ - p0 < OBS_THREADS ? np_ - p0 : OBS_THREADS);
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+        if (t + k * OBS_THREADS < n9) buf[t + k * OBS_THREADS] = Vg[9 * p0 + t + k * OBS_THREADS];
+    __syncthreads();
+    if (9 * t < n9) {
+        const double lambda = *lam;
+        double *vg = buf + 9 * t;
+        const double v00 = vg[0] + lambda * clampd(vg[0]), v01 = vg[1], v02 = vg[2];
+        const double v11 = vg[3] + lambda * clampd(vg[3]), v12 = vg[4];
+        const double v22 = vg[5] + lambda * clampd(vg[5]);
+        const double c00 = sqrt(v00), c10 = v01 / c00, c20 = v02 / c00;
+        const double c11 = sqrt(v11 - c10 * c10), c21 = (v12 - c20 * c10) / c11;
+        const double c22 = sqrt(v22 - c20 * c20 - c21 * c21);
+        const double i00 = 1.0 / c00, i11 = 1.0 / c11, i22 = 1.0 / c22;
+        const double i10 = -c10 * i00 * i11;
+        const double i21 = -c21 * i11 * i22;
+        const double i20 = -(c20 * i00 + c21 * i10) * i22;
+        // L = Cinv^T (upper): Vd^-1 = L L^T
+        const double L[3][3] = {{i00, i10, i20}, {0.0, i11, i21}, {0.0, 0.0, i22}};
+        const double g0 = vg[6], g1 = vg[7], g2 = vg[8];
+        double *lq = vg;  // in place: the thread's own record
+        lq[0] = L[0][0]; lq[1] = L[0][1]; lq[2] = L[0][2]; lq[3] = L[1][1]; lq[4] = L[1][2]; lq[5] = L[2][2];
+        lq[6] = L[0][0] * g0;
+        lq[7] = L[0][1] * g0 + L[1][1] * g1;
+        lq[8] = L[0][2] * g0 + L[1][2] * g1 + L[2][2] * g2;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+        if (t + k * OBS_THREADS < n9) Lq[9 * p0 + t + k * OBS_THREADS] = buf[t + k * OBS_THREADS];
 }
 
 // Payload layout (doubles): S as its upper-triangle 6x6 camera blocks
