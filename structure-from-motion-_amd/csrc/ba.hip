@@ -360,6 +360,112 @@ __global__ void __launch_bounds__(PT_THREADS) k_linearize(int64_t np_, const int
     if (want_cost) grid_sum_last<1>(acc, partial, counter, cost_out);  // only the initial cost is used
 }
 
+// k_linearize with the cameras' Rt (96 B each) staged in LDS once per
+// workgroup instead of gathered per observation (as k_backsub_trial): a
+// resident grid striding over points, the next point's pstart and X loaded
+// while this one is worked on, a lane's first LIN_PRE observations loaded
+// together.  The per-point values are the same bits; the cost's block
+// partials are summed over a different grid.
+constexpr int LIN_PRE = 4;
+constexpr int LIN_CL_THREADS = 256;
+template <int G, int NT = LIN_CL_THREADS>
+__global__ void __launch_bounds__(NT) k_linearize_cl(int64_t np_, int32_t nc, const int32_t *__restrict__ pstart,
+                                                     const int32_t *__restrict__ cam, const double2 *__restrict__ obs,
+                                                     Kmat Km, const double *__restrict__ Rt,
+                                                     const double *__restrict__ X, double *__restrict__ Vg,
+                                                     double *__restrict__ partial, unsigned *__restrict__ counter,
+                                                     double *__restrict__ cost_out, int want_cost,
+                                                     const int *__restrict__ gate, double gtol,
+                                                     unsigned *__restrict__ nbig) {
+    if (gate && !*gate) return;  // device-side LM control: iteration gated off
+    struct Pre {
+        int32_t o0, o1;
+        double x[3];
+    };
+    auto fetch = [&](int64_t g, Pre &P) {
+        const int64_t p = g / G;
+        const bool live = p < np_;
+        P.o0 = live ? pstart[p] : 0;
+        P.o1 = live ? pstart[p + 1] : 0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) P.x[i] = live ? X[3 * p + i] : 0.0;
+    };
+    const int64_t stride = (int64_t)gridDim.x * NT;
+    Pre cur;
+    fetch((int64_t)blockIdx.x * NT + threadIdx.x, cur);
+    extern __shared__ __attribute__((aligned(16))) double lin_cam[];
+#pragma unroll 4
+    for (int i = threadIdx.x; i < 12 * nc; i += NT) lin_cam[i] = Rt[i];
+    __syncthreads();
+    double K[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) K[i] = Km.k[i];
+    double acc[1] = {0.0};
+    int big = 0;
+    for (int64_t gt = (int64_t)blockIdx.x * NT + threadIdx.x; gt / G < np_; gt += stride) {
+        const int64_t p = gt / G;
+        const int sub = (int)(gt % G);
+        const int32_t o0 = cur.o0, o1 = cur.o1;
+        int32_t cpre[LIN_PRE];
+        double2 opre[LIN_PRE];
+#pragma unroll
+        for (int k = 0; k < LIN_PRE; ++k) {
+            const int32_t o = o0 + sub + k * G;
+            cpre[k] = o < o1 ? cam[o] : 0;
+            opre[k] = o < o1 ? obs[o] : make_double2(0.0, 0.0);
+        }
+        Pre nxt;
+        fetch(gt + stride, nxt);
+        const double x[3] = {cur.x[0], cur.x[1], cur.x[2]};
+        double V[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+        auto add = [&](int32_t c, double2 ob) {
+            const double *Rt_c = lin_cam + 12 * c;
+            double r[2], A[2][3], q[3];
+            obs_model(Rt_c, x, K, ob, r, A, q);
+            double Jp[2][3];
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int c2 = 0; c2 < 3; ++c2)
+                    Jp[a][c2] = A[a][0] * Rt_c[c2] + A[a][1] * Rt_c[3 + c2] + A[a][2] * Rt_c[6 + c2];
+            acc[0] += 0.5 * (r[0] * r[0] + r[1] * r[1]);
+            V[0] += Jp[0][0] * Jp[0][0] + Jp[1][0] * Jp[1][0];
+            V[1] += Jp[0][0] * Jp[0][1] + Jp[1][0] * Jp[1][1];
+            V[2] += Jp[0][0] * Jp[0][2] + Jp[1][0] * Jp[1][2];
+            V[3] += Jp[0][1] * Jp[0][1] + Jp[1][1] * Jp[1][1];
+            V[4] += Jp[0][1] * Jp[0][2] + Jp[1][1] * Jp[1][2];
+            V[5] += Jp[0][2] * Jp[0][2] + Jp[1][2] * Jp[1][2];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) g[i] += Jp[0][i] * r[0] + Jp[1][i] * r[1];
+        };
+#pragma unroll
+        for (int k = 0; k < LIN_PRE; ++k)
+            if (o0 + sub + k * G < o1) add(cpre[k], opre[k]);
+        for (int32_t o = o0 + sub + LIN_PRE * G; o < o1; o += G) add(cam[o], obs[o]);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) V[i] = group_sum<G>(V[i]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) g[i] = group_sum<G>(g[i]);
+        if (sub == 0) {
+            double *vg = Vg + 9 * p;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) vg[i] = V[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) vg[6 + i] = g[i];
+            if (gtol > 0.0)
+#pragma unroll
+                for (int i = 0; i < 3; ++i) big += fabs(g[i]) >= gtol;
+        }
+        cur = nxt;
+    }
+    if (gtol > 0.0) {  // gradient_tolerance: count point-gradient entries >= gtol (an exact integer sum)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) big += __shfl_xor(big, o);
+        if ((threadIdx.x & 63) == 0 && big) atomicAdd(nbig, (unsigned)big);
+    }
+    if (want_cost) grid_sum_last<1, NT>(acc, partial, counter, cost_out);
+}
+
 // Lq layout per point (9 doubles): L00 L01 L02 L11 L12 L22 | q0 q1 q2,
 // L = Cinv^T with C C^T = V + lambda clamp(diag V) (so Vd^-1 = L L^T) and
 // q = L^T g_p: everything the sweep and the back substitution need of a
@@ -2518,6 +2624,30 @@ static int backsub_cl_blocks(int32_t nc, int ncu, int max_blocks, int nt) {
     return std::max(1, std::min(nb * ncu, max_blocks));
 }
 
+// k_linearize_cl's grid: the resident workgroups for the cameras' LDS size
+// (0: more than 64 KB of cameras, or SFM_LINEARIZE_CAM_LDS=0)
+static int linearize_cl_blocks(int32_t nc, int ncu, int max_blocks) {
+    if (env_int("SFM_LINEARIZE_CAM_LDS", 1) == 0) return 0;
+    const size_t lds = (size_t)96 * nc;
+    if (nc < 1 || lds > (size_t)BS_CAM_LDS_MAX) return 0;
+    int nb = 0;
+    auto occ = [&](auto kern) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, LIN_CL_THREADS, lds) != hipSuccess)
+            nb = 0;
+    };
+    switch (lanes_per_point("SFM_LINEARIZE_LANES", 2)) {
+    case 1: occ(k_linearize_cl<1>); break;
+    case 2: occ(k_linearize_cl<2>); break;
+    case 4: occ(k_linearize_cl<4>); break;
+    default: occ(k_linearize_cl<8>); break;
+    }
+    (void)hipGetLastError();
+    if (nb < 1) return 0;
+    return std::max(1, std::min(nb * ncu, max_blocks));
+}
+
 // camera items for camera_lin_wg from workgroup cuts (camera-major
 // observation offsets, ascending, first 0, last n_obs): every item is the
 // part of one camera inside one workgroup's range.  by_wg: workgroup g takes
@@ -3023,6 +3153,7 @@ struct sfm_ba_problem {
     int pt_blocks = 0;
     int bs_cl_blocks = 0;  // k_backsub_trial with the cameras in LDS: its grid (0: cameras from global)
     int bs_threads = PT_THREADS;  // and its workgroup size
+    int lin_cl_blocks = 0;        // k_linearize_cl's grid (0: k_linearize, cameras from global)
     hipEvent_t ev[2 * T_NT] = {};
     hipEvent_t ev_it[2 * T_NT * kEvSlots] = {};  // per-iteration timing slots of a batch
     LMState *d_lm = nullptr;
@@ -3316,6 +3447,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     p->gjp = p->tb == 16 && !p->gjrp.ok() ? gj_plan(p->nT, device_cus(device)) : GjPlan{};
     p->bs_threads = env_int("SFM_BACKSUB_THREADS", 256) == 256 ? 256 : PT_THREADS;
     p->bs_cl_blocks = backsub_cl_blocks(nc, device_cus(device), p->pt_blocks, p->bs_threads);
+    p->lin_cl_blocks = linearize_cl_blocks(nc, device_cus(device), p->pt_blocks);
     if (p->gjrp.ok()) {
         gjr::u64 *gw = nullptr;
         int *gi = nullptr;
@@ -3621,6 +3753,23 @@ static int run_linearize(sfm_ba_problem *p, int par, int want_cost) {
     hipStream_t s = p->stream;
     const int *glin = &p->d_lm[par].run_lin;
 
+    if (p->lin_cl_blocks > 0) {  // the cameras in LDS
+        const int gc = lanes_per_point("SFM_LINEARIZE_LANES", 2);
+        const int nb = std::max(1, std::min(ceil_div(p->np * gc, LIN_CL_THREADS), p->lin_cl_blocks));
+#define SFM_LINC(G)                                                                                               \
+    hipLaunchKernelGGL(k_linearize_cl<G>, dim3(nb), dim3(LIN_CL_THREADS), (size_t)96 * p->nc, s, p->np, p->nc,     \
+                       p->d_pstart, p->d_cam, p->d_obs, p->K, p->d_Rt, p->d_X, p->d_Vg, p->d_partial, p->d_count,  \
+                       p->d_scal + 8, want_cost, glin, p->gtol, p->d_nbig)
+        switch (gc) { case 1: SFM_LINC(1); break; case 2: SFM_LINC(2); break; case 4: SFM_LINC(4); break; default: SFM_LINC(8); }
+#undef SFM_LINC
+        SFM_HIP(hipGetLastError());
+        if (p->ndiag_items && !p->cl_fused) {
+            const CamLinArgs cl = camlin_args(p, false, glin);
+            hipLaunchKernelGGL(k_camera_lin<256>, dim3(p->ndiag_items), dim3(256), 0, s, cl);
+            SFM_HIP(hipGetLastError());
+        }
+        return want_cost ? allreduce(p, p->d_scal + 8, 1) : 0;
+    }
     const int gl = lanes_per_point("SFM_LINEARIZE_LANES", 4);
     const int nbl = std::max(1, ceil_div(p->np * gl, PT_THREADS));
 #define SFM_LIN(G)                                                                                                \
