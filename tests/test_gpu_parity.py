@@ -1208,3 +1208,30 @@ def test_pnp_fast_test_exact_at_threshold(core):
                 assert np.array_equal(C1, C) and np.array_equal(R1, R)
             checked += 1
     assert checked > 0
+
+
+@pytest.mark.parametrize("shape", ["cfg3", "300x6000"])
+def test_ba_camera_lds_paths_match_global(core, monkeypatch, shape):
+    """k_backsub_trial and k_linearize with the cameras staged in LDS
+    (default) against the per-observation camera gathers
+    (SFM_BACKSUB_CAM_LDS=0, SFM_LINEARIZE_CAM_LDS=0): the per-point values
+    are the same bits, only the block partials of the costs are summed over
+    a different grid, so the LM trajectory (counts, status) is the same and
+    the cost, cameras and points agree to rounding.  300x6000: 300 cameras
+    are 72 KB of back-substitution cameras, past the 64-KB LDS stage, so
+    that kernel falls back to the gathers while k_linearize (29 KB) stages."""
+    if shape == "cfg3":
+        p = syn.ba_problem_cfg("cfg3", dense=False)
+    else:
+        p = syn.ba_problem(300, 6000, 8, seed=7)
+    cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
+    args = (cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K)
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("SFM_BACKSUB_CAM_LDS", v)
+        monkeypatch.setenv("SFM_LINEARIZE_CAM_LDS", v)
+        out[v] = core.ba_lm(*args, max_iterations=20)
+    (ca, Xa, a), (cb, Xb, b) = out["1"], out["0"]
+    assert (a["iterations"], a["accepted"], a["status"]) == (b["iterations"], b["accepted"], b["status"])
+    assert abs(a["cost"] - b["cost"]) <= 1e-10 * b["cost"]
+    assert np.allclose(ca, cb, rtol=0, atol=1e-8) and np.allclose(Xa, Xb, rtol=0, atol=1e-8)

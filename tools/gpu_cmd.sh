@@ -9,6 +9,12 @@ step() {  # step NAME SECONDS CMD...
     echo "[$name] rc=$rc"; grep -v amdgpu.ids "gpurun_out/$name.txt" | tail -${TAILN:-8}
     if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
-TAILN=3 step t1 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu
-TAILN=3 step sm 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
-bash tools/profile_round.sh r4d && tail -3 gpurun_out/r4d/passes.log
+TAILN=4 step t1 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu
+TAILN=2 step sm 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+TAILN=0 step bench 600 python bench.py
+python - <<'PY'
+import json
+d=json.loads(open("gpurun_out/bench.txt").read().strip().splitlines()[-1])
+print("cfg5", d["value"], d["ms_per_step"], d["converged_LM_it_per_s"], d["roofline"]["frac"])
+c=d["cfg4"]; print("cfg4", c["value"], c["ms_per_step"], c["converged_LM_it_per_s"])
+PY
