@@ -36,15 +36,12 @@ for p in range(nT):
     step = pp - prev if prev is not None else float("nan")
     prev = pp
     print(f"{p:4d} {pin:9.2f} {gcr:9.2f} {c0:8.2f} {c1:8.2f} {pp:9.2f} | {hop:8.2f} {step:7.2f}")
-fin = ["start", "prologue", "w0end", "arrived", "u0prologue"]
+fin = ["start", "prologue", "w0end", "arrived"]
 for w in range(nT):
     if w < 2 or w >= nT - 2:
-        print(f"owner {w:3d}: " + " ".join(f"{fin[k]}={d[w, nT, k]:8.2f}" for k in range(5)))
+        print(f"owner {w:3d}: " + " ".join(f"{fin[k]}={d[w, nT, k]:8.2f}" for k in range(len(fin))))
 steps = np.diff(d[np.arange(nT), np.arange(nT), PPUB])
 print(f"mean step {np.nanmean(steps):.3f} us, median {np.nanmedian(steps):.3f}")
-print("U0 prologue groups (owner: stamps)")
-for w in (0, 1, nT // 2, nT - 2, nT - 1):
-    print(f"  {w:3d}: " + " ".join(f"{d[w, g, 12]:7.2f}" for g in range(4)))
 if len(sys.argv) > 2:
     for r in map(int, sys.argv[2].split(",")):
         print(f"owner {r}: step  Ppub@p   P_p@W0  pdoneOK  Hpready   G_hold  greadyW0   U0done")

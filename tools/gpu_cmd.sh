@@ -9,16 +9,6 @@ step() {  # step NAME SECONDS CMD...
     echo "[$name] rc=$rc"; grep -v amdgpu.ids "gpurun_out/$name.txt" | tail -${TAILN:-8}
     if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
-L=structure-from-motion-_amd/libsfmcore.so
-B="python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-next-rows --no-end-to-end --no-shard-local"
-TAILN=2 step t1 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu -k "ba_cfg or camera_lds or multi_rank"
-for v in a b a b; do
-  cp abso/$v.so $L
-  TAILN=0 step v$v 200 $B
-  python - "$v" <<'PY'
-import json,sys
-d=json.loads(open(f"gpurun_out/v{sys.argv[1]}.txt").read().strip().splitlines()[-1])
-k=d["kernels_ms_per_iter"]; c=d["cfg4"]; k4=c["kernels_ms_per_iter"]
-print(sys.argv[1], "cfg5", d["value"], k["backsub_trial"]["ms"], "cfg4", c["value"], k4["backsub_trial"]["ms"])
-PY
-done
+TAILN=3 step t1 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu
+TAILN=2 step sm 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+TAILN=1 step bench 300 python bench.py --no-cpu-baseline --no-next-rows --no-end-to-end --no-shard-local
