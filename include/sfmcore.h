@@ -150,16 +150,17 @@ int sfm_matching_free(void *handle);
  * Dense visibility -> COO observations (BundleAdjustment.py:164-169, the
  * drop-in's np.where over filtered_feature_flags[valid_point_indices]
  * [:, :n_cameras] == 1 and the feature_x / feature_y gathers at the hits).
- * sfm_dense_obs_scan: rows[i] (i < n_rows) are the valid feature rows; a
- *   row r of the flag matrix starts at flags + r * flag_row_bytes (dtype
+ * sfm_dense_obs_scan: rows[i] (i < n_rows) are the valid feature rows, each
+ *   in [0, n_matrix_rows) (SFM_ERR_ARG otherwise: the matrices' row count,
+ *   where the reference's indexing raises IndexError); a row r of the flag matrix starts at flags + r * flag_row_bytes (dtype
  *   0 f64, 1 f32, 2 i64, 3 i32, 4 u8/bool; "== 1" in that dtype), of the
  *   coordinate matrices at fx / fy + r * xy_row_bytes (f64); n_threads
  *   host threads (0 = up to 16).  Returns a store of n_obs observations in
  *   np.where's order (point-major, camera ascending).
  * sfm_dense_obs_read: copies (camera, point i, (x, y)).
  * ------------------------------------------------------------------- */
-int sfm_dense_obs_scan(const void *flags, int32_t dtype, int64_t flag_row_bytes, const int64_t *rows,
-                       int64_t n_rows, int32_t n_cams, const double *fx, const double *fy,
+int sfm_dense_obs_scan(const void *flags, int32_t dtype, int64_t flag_row_bytes, int64_t n_matrix_rows,
+                       const int64_t *rows, int64_t n_rows, int32_t n_cams, const double *fx, const double *fy,
                        int64_t xy_row_bytes, int32_t n_threads, void **handle, int64_t *n_obs);
 int sfm_dense_obs_read(void *handle, int32_t *cam, int32_t *pt, double *obs);
 int sfm_dense_obs_free(void *handle);

@@ -77,6 +77,16 @@ def _observations(filtered_world_coords, feature_x, feature_y, filtered_feature_
     ascending, as np.where), or the numpy expression for layouts it does not
     read (a non-contiguous row, a flag dtype other than float/int/bool)."""
     valid_point_indices = np.where(np.asarray(filtered_world_coords).flatten() == 1)[0]
+    # the reference's loop indexes filtered_feature_flags[pt_idx, cam_idx] for
+    # every valid point and camera (:164-166), outside its try: IndexError
+    # escapes when the flag matrix is too short or too narrow
+    flag_shape = np.shape(filtered_feature_flags)
+    if len(flag_shape) != 2:
+        raise IndexError(f"too many indices for array: array is {len(flag_shape)}-dimensional, but 2 were indexed")
+    if valid_point_indices[-1] >= flag_shape[0]:
+        raise IndexError(f"index {valid_point_indices[-1]} is out of bounds for axis 0 with size {flag_shape[0]}")
+    if n_cameras > flag_shape[1]:
+        raise IndexError(f"index {flag_shape[1]} is out of bounds for axis 1 with size {flag_shape[1]}")
     got = _core.dense_observations(filtered_feature_flags, feature_x, feature_y, valid_point_indices, n_cameras)
     if got is not None:
         camera_indices, point_indices, points_2d = got
@@ -128,6 +138,7 @@ def perform_bundle_adjustment(all_world_coords, filtered_world_coords, feature_x
     all_world_coords_opt : numpy.ndarray
         Optimized 3D points
     """
+    last_timings.clear()  # a call that returns early leaves no stale split behind
     t0 = time.perf_counter()
     valid_point_indices = np.where(np.asarray(filtered_world_coords).flatten() == 1)[0]
     if len(valid_point_indices) == 0:  # :152-153
@@ -148,6 +159,7 @@ def perform_bundle_adjustment_coo(all_world_coords, filtered_world_coords, store
     plays filtered_feature_flags) instead of dense n_features x n_images
     matrices; same observations, order, solver, prints and failure
     behaviour."""
+    last_timings.clear()  # a call that returns early leaves no stale split behind
     t0 = time.perf_counter()
     valid_point_indices = np.where(np.asarray(filtered_world_coords).flatten() == 1)[0]
     if len(valid_point_indices) == 0:

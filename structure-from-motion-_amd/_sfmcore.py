@@ -85,7 +85,7 @@ SIGNATURES = [
                                 _i64, _i64]),
     ("sfm_matching_read", _c, [ctypes.c_void_p, _i32, _i32, _d, _d]),
     ("sfm_matching_free", _c, [ctypes.c_void_p]),
-    ("sfm_dense_obs_scan", _c, [ctypes.c_void_p, ctypes.c_int32, _i, _i64, _i, ctypes.c_int32, _d, _d, _i,
+    ("sfm_dense_obs_scan", _c, [ctypes.c_void_p, ctypes.c_int32, _i, _i, _i64, _i, ctypes.c_int32, _d, _d, _i,
                                 ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p), _i64]),
     ("sfm_dense_obs_read", _c, [ctypes.c_void_p, _i32, _i32, _d]),
     ("sfm_dense_obs_free", _c, [ctypes.c_void_p]),
@@ -452,7 +452,8 @@ def dense_observations(flags, feature_x, feature_y, rows, n_cams, n_threads=0):
     rows = np.ascontiguousarray(rows, dtype=np.int64)
     h = ctypes.c_void_p()
     no = np.zeros(1, dtype=np.int64)
-    _check(_lib.sfm_dense_obs_scan(f.ctypes.data, _DENSE_DTYPES[f.dtype], f.strides[0], _p(rows, _i64), len(rows),
+    _check(_lib.sfm_dense_obs_scan(f.ctypes.data, _DENSE_DTYPES[f.dtype], f.strides[0], f.shape[0],
+                                   _p(rows, _i64), len(rows),
                                    int(n_cams), fx.ctypes.data_as(_d), fy.ctypes.data_as(_d), fx.strides[0],
                                    int(n_threads), ctypes.byref(h), _p(no, _i64)))
     try:

@@ -66,11 +66,16 @@ void scan_rows(const char *flags, int64_t flag_row_bytes, const int64_t *rows, i
 
 }  // namespace
 
-extern "C" int sfm_dense_obs_scan(const void *flags, int32_t dtype, int64_t flag_row_bytes, const int64_t *rows,
-                                  int64_t n_rows, int32_t n_cams, const double *fx, const double *fy,
-                                  int64_t xy_row_bytes, int32_t n_threads, void **handle, int64_t *n_obs) {
+extern "C" int sfm_dense_obs_scan(const void *flags, int32_t dtype, int64_t flag_row_bytes, int64_t n_matrix_rows,
+                                  const int64_t *rows, int64_t n_rows, int32_t n_cams, const double *fx,
+                                  const double *fy, int64_t xy_row_bytes, int32_t n_threads, void **handle,
+                                  int64_t *n_obs) {
     SFM_CHECK_ARG(handle && n_obs && (n_rows == 0 || (flags && rows && fx && fy)), "null pointer");
-    SFM_CHECK_ARG(n_rows >= 0 && n_cams >= 0 && n_rows < ((int64_t)1 << 31), "bad sizes");
+    SFM_CHECK_ARG(n_rows >= 0 && n_cams >= 0 && n_rows < ((int64_t)1 << 31) && n_matrix_rows >= 0, "bad sizes");
+    // every row index inside the matrices (the reference's fancy index raises
+    // IndexError there, BundleAdjustment.py:166; the binding raises it first)
+    for (int64_t i = 0; i < n_rows; ++i)
+        SFM_CHECK_ARG(rows[i] >= 0 && rows[i] < n_matrix_rows, "row index out of bounds of the flag matrix");
     SFM_CHECK_ARG(dtype >= 0 && dtype <= 4, "flag dtype: 0 f64, 1 f32, 2 i64, 3 i32, 4 u8/bool");
     int nt = n_threads > 0 ? n_threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, (n_rows + 4095) / 4096));

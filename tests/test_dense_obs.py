@@ -66,3 +66,20 @@ def test_dense_observations_empty():
     flags[:] = 0
     cam, pt, xy = core.dense_observations(flags, fx, fy, np.arange(100), 5)
     assert len(cam) == 0 and xy.shape == (0, 2)
+
+
+def test_dense_observations_row_out_of_bounds():
+    """a valid row past the matrices is refused by the scan (no
+    out-of-bounds host read), and the drop-in raises IndexError from the
+    observation loop as the reference does (its loop is outside the try,
+    BundleAdjustment.py:164-169)."""
+    fwc, fx, fy, flags = problem(100, 5, np.int64, 3)
+    with pytest.raises(core.SfmCoreError, match="out of bounds"):
+        core.dense_observations(flags, fx, fy, np.array([3, 100]), 5)
+    big = np.ones((120, 1), dtype=np.int64)  # 20 more valid rows than the matrices have
+    R = [np.eye(3)] * 5
+    C = [np.zeros(3)] * 5
+    with pytest.raises(IndexError, match="out of bounds for axis 0 with size 100"):
+        BA.perform_bundle_adjustment(np.zeros((120, 3)), big, fx, fy, flags, R, C, np.eye(3), 4)
+    with pytest.raises(IndexError, match="axis 1"):  # more cameras than flag columns
+        BA.perform_bundle_adjustment(np.zeros((100, 3)), fwc, fx, fy, flags, R + R, C + C, np.eye(3), 4)

@@ -860,15 +860,17 @@ def _spd(n, seed, cond=1e4):
     return 0.5 * (S + S.T), rng.standard_normal(n)
 
 
-@pytest.mark.parametrize("solver", ["gj", "chol"])
+@pytest.mark.parametrize("solver", ["gj", "gjseg", "chol"])
 @pytest.mark.parametrize("n", [1, 6, 16, 17, 48, 150, 300, 304, 600, 1200, 1800, 2100])
 def test_reduced_solve(core, monkeypatch, n, solver):
     """The reduced-camera solvers against LAPACK on SPD systems with condition
-    number 1e4: the persistent block Gauss-Jordan solve (default; gj_solve.hpp,
-    up to 128 tile columns -- n = 2100 falls back to the tiled Cholesky) and
-    the tiled Cholesky (SFM_SOLVE=chol: k_chol_col launches, forward
-    substitution folded in, back substitution).  Relative error <= 1e-11 (both
-    backward stable; kappa * eps ~ 2e-12); deterministic."""
+    number 1e4: the row-distributed persistent block Gauss-Jordan solve
+    (default; gjr_solve.hpp, up to 128 tile rows -- n = 2100 falls back to
+    the tiled Cholesky), the column-block segment Gauss-Jordan solve
+    (SFM_SOLVE=gjseg, gj_solve.hpp: the live fallback when the row layout
+    declines) and the tiled Cholesky (SFM_SOLVE=chol: k_chol_col launches,
+    forward substitution folded in, back substitution).  Relative error
+    <= 1e-11 (all backward stable; kappa * eps ~ 2e-12); deterministic."""
     monkeypatch.setenv("SFM_SOLVE", solver)
     S, b = _spd(n, seed=n)
     x_ref = np.linalg.solve(S, b)
@@ -877,7 +879,7 @@ def test_reduced_solve(core, monkeypatch, n, solver):
     assert np.array_equal(x, core.reduced_solve(S, b))
 
 
-@pytest.mark.parametrize("solver", ["gj", "chol"])
+@pytest.mark.parametrize("solver", ["gj", "gjseg", "chol"])
 @pytest.mark.parametrize("n", [40, 300, 1200])
 def test_reduced_solve_not_spd(core, monkeypatch, n, solver):
     """A non-positive pivot is reported by either solver."""
@@ -920,6 +922,32 @@ def test_ba_sweep_pinhole_matches_general_k(core, monkeypatch):
     c0, x0, r0 = core.ba_lm(*args, max_iterations=30)
     assert (r1["iterations"], r1["accepted"], r1["status"]) == (r0["iterations"], r0["accepted"], r0["status"])
     assert abs(r1["cost"] - r0["cost"]) <= 1e-9 * r0["cost"]
+
+
+def test_ba_sweep_split_and_gjr_fold_paths(core, monkeypatch):
+    """cfg5, where the Schur sweep's last dispatch round is cut into chunk
+    sub-ranges (SweepSplit, split_S = 8 by default): the split plan against
+    the unsplit one (SFM_SWEEP_SPLIT=0: the same blocks summed in another
+    order, so the LM agrees to rounding), and k_schur_finish folded into the
+    row solve's prologue (SFM_GJR_FOLD=1: the slabs read in the finish's
+    order, camera U / g from the camera-block partials) against the finish
+    launch: the same sums in the same order, so bitwise the same solve."""
+    p = syn.ba_problem_cfg("cfg5", dense=False)
+    cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
+    args = (cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K)
+    out = {}
+    for split, fold in (("8", "0"), ("0", "0"), ("8", "1"), ("0", "1")):
+        monkeypatch.setenv("SFM_SWEEP_SPLIT", split)
+        monkeypatch.setenv("SFM_GJR_FOLD", fold)
+        out[split, fold] = core.ba_lm(*args, max_iterations=12)
+    c8, x8, r8 = out["8", "0"]
+    for key, (c, x, r) in out.items():
+        assert (r["iterations"], r["accepted"], r["status"]) == (r8["iterations"], r8["accepted"], r8["status"]), key
+        assert abs(r["cost"] - r8["cost"]) <= 1e-9 * r8["cost"], key
+        assert np.abs(c - c8).max() < 1e-8 and np.abs(x - x8).max() < 1e-6, key
+    for split in ("8", "0"):  # the fold is the finish's arithmetic
+        (ca, xa, ra), (cb, xb, rb) = out[split, "0"], out[split, "1"]
+        assert ra["cost"] == rb["cost"] and np.array_equal(ca, cb) and np.array_equal(xa, xb), split
 
 
 @pytest.mark.parametrize("shape,ranks", [("cfg4", 4), ("cfg5", 8)])
