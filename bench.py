@@ -349,7 +349,7 @@ def end_to_end_ba(workload):
             "phase_frac": {k: round(v / total, 4) for k, v in phases.items() if not k.startswith("ba_lm_")
                            or k == "ba_lm_create"},
             "note": "phases: observations = dense flags -> COO (np.nonzero over n_pts x n_cams), cams0 = Rotation "
-                    "-> rotvec, r0 = initial residual check on the GPU (scipy's non-finite-x0 error), ba_lm = the "
+                    "-> rotvec (stacked), the non-finite-x0 check = the device's initial cost (status 6), ba_lm = the "
                     "C-ABI call (create: host prep + sweep plan + uploads; loop; download), post = rotvec -> R, C"}
 
 

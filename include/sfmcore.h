@@ -212,7 +212,8 @@ typedef struct {
 typedef struct {
     int32_t iterations;  /* LM iterations performed                             */
     int32_t accepted;    /* accepted steps (re-linearisations)                  */
-    int32_t status;      /* 1 ftol, 2 gtol, 3 xtol, 4 max_iterations, 5 lambda */
+    int32_t status;      /* 1 ftol, 2 gtol, 3 xtol, 4 max_iterations, 5 lambda,
+                            6 cost at x0 not finite (no step taken)             */
     int32_t n_ranks;
     double cost0, cost;  /* 0.5 sum r^2 before / after                          */
     double t_setup_ms;   /* host prep + uploads                                 */
@@ -279,6 +280,10 @@ int sfm_ba_create(int32_t n_cams, int64_t n_pts, int64_t n_obs, const int32_t *c
                   const double *cam_params, const double *points, int device, sfm_comm *comm,
                   sfm_ba_problem **out);
 int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *opts, sfm_ba_report *report);
+/* digest of the Schur sweep plan built at create (set only when the
+ * environment has SFM_PLAN_DIGEST=1, else 0): the device planner and the
+ * host planner (SFM_PLAN_HOST=1) must produce the same plan */
+int sfm_ba_plan_digest(sfm_ba_problem *p, uint64_t *out);
 /* reset the device state to the initial parameters given at create time */
 int sfm_ba_reset(sfm_ba_problem *p);
 int sfm_ba_download(sfm_ba_problem *p, double *cam_params, double *points);

@@ -183,12 +183,13 @@ def _adjust(all_world_coords, obs, R_set, C_set, K, max_iterations, function_tol
     if len(camera_indices) == 0:  # :171-172
         return R_set, C_set, all_world_coords
     t0 = time.perf_counter()
-    cams0 = np.zeros((n_cameras, 6))
-    for i in range(n_cameras):  # :183-193
-        R = np.array(R_set[i])
-        C = np.array(C_set[i])
-        cams0[i, :3] = Rotation.from_matrix(R).as_rotvec()
-        cams0[i, 3:] = -R @ C
+    # :183-193 for all cameras at once (the stacked conversions and products
+    # give the per-camera loop's bits: the same routine per matrix)
+    Rs = np.array([np.array(R) for R in R_set], dtype=np.float64).reshape(n_cameras, 3, 3)
+    Cs = np.array([np.array(C) for C in C_set], dtype=np.float64).reshape(n_cameras, 3)
+    cams0 = np.empty((n_cameras, 6))
+    cams0[:, :3] = Rotation.from_matrix(Rs).as_rotvec()
+    cams0[:, 3:] = (-Rs @ Cs[:, :, None])[:, :, 0]
     pts0 = np.asarray(all_world_coords, dtype=np.float64)[valid_point_indices]
     t1 = time.perf_counter()
     last_timings["cams0"] = (t1 - t0) * 1e3
@@ -198,25 +199,21 @@ def _adjust(all_world_coords, obs, R_set, C_set, K, max_iterations, function_tol
         if 2 * len(camera_indices) < 6 * n_cameras + 3 * n_points:  # scipy least_squares.py:850-852
             raise ValueError("Method 'lm' doesn't work when the number of residuals is less than the "
                              "number of variables.")
-        t2 = time.perf_counter()
-        r0 = _core.ba_residuals(cams0, pts0, camera_indices, point_indices, points_2d, K)
-        if not np.all(np.isfinite(r0)):  # least_squares.py:843-845
-            raise ValueError("Residuals are not finite in the initial point.")
         t3 = time.perf_counter()
         cams, pts, rep = _core.ba_lm(cams0, pts0, camera_indices, point_indices, points_2d, K,
                                      max_iterations=max_iterations, function_tolerance=function_tolerance,
                                      parameter_tolerance=parameter_tolerance, initial_lambda=initial_lambda)
         t4 = time.perf_counter()
-        last_timings.update(r0=(t3 - t2) * 1e3, ba_lm=(t4 - t3) * 1e3, ba_lm_create=rep["t_setup_ms"],
+        if rep["status"] == 6:  # the cost at x0 is not finite: least_squares.py:843-845, nothing solved
+            raise ValueError("Residuals are not finite in the initial point.")
+        last_timings.update(ba_lm=(t4 - t3) * 1e3, ba_lm_create=rep["t_setup_ms"],
                             ba_lm_loop=rep["t_loop_ms"], ba_lm_download=rep["t_download_ms"],
                             iterations=rep["iterations"])
-        R_set_opt = []
-        C_set_opt = []
-        for i in range(n_cameras):  # :220-228
-            R_opt = Rotation.from_rotvec(cams[i, :3]).as_matrix()
-            C_opt = -R_opt.T @ cams[i, 3:]
-            R_set_opt.append(R_opt)
-            C_set_opt.append(C_opt)
+        # :220-228 for all cameras at once (bitwise the per-camera loop)
+        R_all = Rotation.from_rotvec(cams[:, :3]).as_matrix()
+        C_all = (-np.transpose(R_all, (0, 2, 1)) @ cams[:, 3:, None])[:, :, 0]
+        R_set_opt = [R_all[i] for i in range(n_cameras)]
+        C_set_opt = [C_all[i] for i in range(n_cameras)]
         all_world_coords_opt = all_world_coords.copy()  # :231-234
         all_world_coords_opt[valid_point_indices] = pts
         last_timings["post"] = (time.perf_counter() - t4) * 1e3

@@ -104,6 +104,7 @@ SIGNATURES = [
                            ctypes.POINTER(ctypes.c_void_p)]),
     ("sfm_ba_solve", _c, [ctypes.c_void_p, ctypes.POINTER(BAOpts), ctypes.POINTER(BAReport)]),
     ("sfm_ba_reset", _c, [ctypes.c_void_p]),
+    ("sfm_ba_plan_digest", _c, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     ("sfm_ba_download", _c, [ctypes.c_void_p, _d, _d]),
     ("sfm_ba_kernel_times", _c, [ctypes.c_void_p, _d, _c, ctypes.c_char_p, _c]),
     ("sfm_ba_set_timing", _c, [ctypes.c_void_p, _c]),
@@ -596,6 +597,12 @@ class BAProblem:
 
     def reset(self):
         _check(_lib.sfm_ba_reset(self.h))
+
+    def plan_digest(self):
+        """Digest of the Schur sweep plan (create with SFM_PLAN_DIGEST=1; else 0)."""
+        d = ctypes.c_uint64()
+        _check(_lib.sfm_ba_plan_digest(self.h, ctypes.byref(d)))
+        return d.value
 
     def download(self):
         cams = np.zeros((self.n_cams, 6))

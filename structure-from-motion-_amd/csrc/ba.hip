@@ -1975,7 +1975,19 @@ __global__ void k_lm_reset(LMState *lm, double lambda0, int *bad) {
     bad[0] = 0;
 }
 
-__global__ void k_lm_init(LMState *lm, const double *lin_cost) { lm->cost = lm->cost0 = *lin_cost; }
+// the cost at x0; a non-finite one (a residual is NaN / inf: scipy's
+// "Residuals are not finite in the initial point", least_squares.py:843-845)
+// ends the solve before its first step with status 6
+__global__ void k_lm_init(LMState *lm, const double *lin_cost) {
+    const double c0 = *lin_cost;
+    lm->cost = lm->cost0 = c0;
+    if (!isfinite(c0)) {
+        lm->status = 6;
+        lm->done = 1;
+        lm->run_step = 0;
+        lm->run_lin = 0;
+    }
+}
 
 // sfm_ba_solve's host logic, verbatim: Nielsen's lambda update on the gain
 // ratio of the trial step; scal = [cost_trial, model_p, dn_p, xn_p, model_c,
@@ -2300,7 +2312,7 @@ static GjrPlan gjr_plan(int nT, int ncu) {
     if (const char *e = std::getenv("SFM_SOLVE"))
         if (std::strcmp(e, "chol") == 0 || std::strcmp(e, "gjseg") == 0) return g;
     // tile slots per U wave: 4 or TREG in registers (up to 28 / 77 tile
-    // rows), past that TREG_L + TLDS_L (the latter in LDS: up to 133)
+    // rows), past that TREG_L + TLDS_L (the latter in LDS: up to gjr::NTMAX = 128)
     if (nT < 1 || nT > gjr::NTMAX || nT > ncu) return g;
     const int tpw = nT <= 4 * gjr::NUW ? 4 : nT <= gjr::TREG * gjr::NUW ? gjr::TREG : gjr::TREG_L + gjr::TLDS_L;
     const bool res = tpw == 4 ? gjr_resident<4, 0>(nT, ncu)
@@ -2313,14 +2325,15 @@ static GjrPlan gjr_plan(int nT, int ncu) {
 }
 // granule records (zeroed once; tags only grow) and the err / arrival words
 struct GjrBufs {
-    gjr::u64 *P = nullptr, *G = nullptr;
+    gjr::u64 *P = nullptr, *G = nullptr, *R = nullptr;
     double *Gd = nullptr;
     unsigned *Gf = nullptr;
     int *err = nullptr;
     unsigned *arrive = nullptr;
     static size_t words(int nT) {
         const size_t t = (size_t)nT * nT;
-        return ((size_t)2 * nT * gjr::PBYTES + t * gjr::GBYTES + t * gjr::GDBYTES) / 8 + (t + 1) / 2;
+        return ((size_t)2 * nT * gjr::PBYTES + t * gjr::GBYTES + t * gjr::GDBYTES + (size_t)nT * gjr::RBYTES) / 8 +
+               (t + 1) / 2;
     }
     static constexpr size_t ints = 64;
     void carve(gjr::u64 *w, int *i, int nT) {
@@ -2328,7 +2341,8 @@ struct GjrBufs {
         P = w;
         G = P + (size_t)2 * nT * gjr::PBYTES / 8;
         Gd = reinterpret_cast<double *>(G + t * gjr::GBYTES / 8);
-        Gf = reinterpret_cast<unsigned *>(Gd + t * gjr::GDBYTES / 8);
+        R = reinterpret_cast<gjr::u64 *>(Gd + t * gjr::GDBYTES / 8);
+        Gf = reinterpret_cast<unsigned *>(R + (size_t)nT * gjr::RBYTES / 8);
         err = i;
         arrive = reinterpret_cast<unsigned *>(i + 32);
     }
@@ -2346,6 +2360,7 @@ static int launch_gjr(const GjrPlan &g, int32_t ns, const double *payload, const
     a.P = b.P;
     a.G = b.G;
     a.Gd = b.Gd;
+    a.R = b.R;
     a.Gf = b.Gf;
     a.tag = tag;
     a.x = x;
@@ -2573,6 +2588,9 @@ struct SweepPlan {
     int32_t nrange = 0, nspec = 0, nbd = 0, buf_slots = 0, pair_cap = 0, hdr_cap = 0, list_cap = 0, nchunk = 0;
     int32_t split_S = 0, split_w0 = 0, split_n = 0, split_gmax = 0;  // the dispatch tail's split (SweepSplit)
     std::vector<int32_t> rchunk, goff, nload, list, hdr, spec_cam, split_of;
+    std::vector<int32_t> spec_row;  // per spec: (camera, j0, j1) of rows 0 and 1 (camera -1: none)
+    std::vector<int32_t> cut;       // chunk first points, then np
+    bool dev_lists = false;         // list / pairs / hdr are generated on the device (k_plan_lists)
     std::vector<SweepGroup> groups;
     std::vector<int16_t> lanegrp;
     std::vector<uint16_t> pairs;
@@ -2683,6 +2701,189 @@ static void plan_camera_items(int nc, const std::vector<int32_t> &cstart, const 
 
 static int32_t dense_blk(int nc, int i, int j) { return i * nc - i * (i - 1) / 2 + (j - i); }
 
+// ------------------------------------------------- the sweep plan on the device (round 5)
+// plan_sweep's passes over every point's observation pairs (the chunk
+// statistics that size the LDS, the per-chunk pair counts, and the (chunk,
+// spec) slot and pair lists) run as kernels over the uploaded point-major
+// COO and the camera-major points, producing the host planner's arrays
+// exactly (same traversal orders; SFM_PLAN_HOST=1 keeps the host passes and
+// the plan digest test compares the two).  The allocation of lanes to the
+// groups (a greedy over the chunk counts) stays on the host.
+__device__ __forceinline__ int32_t dense_blk_d(int nc, int i, int j) { return i * nc - i * (i - 1) / 2 + (j - i); }
+__device__ __forceinline__ int32_t lower_bound_d(const int32_t *__restrict__ a, int32_t lo, int32_t hi, int32_t v) {
+    while (lo < hi) {
+        const int32_t m = lo + ((hi - lo) >> 1);
+        if (a[m] < v) lo = m + 1;
+        else hi = m;
+    }
+    return lo;
+}
+
+// chunk q of a trial cut: the observations of points [cut[q], cend[q]); its
+// largest staged-slot count (the observations of one spec's cameras) and
+// pair count (off-diagonal pairs of one spec's blocks) -> out[2q], out[2q+1]
+__global__ void __launch_bounds__(256) k_plan_chunkmax(int32_t nc, int32_t nspec, const int32_t *__restrict__ pstart,
+                                                       const int32_t *__restrict__ pt, const int32_t *__restrict__ cam,
+                                                       const int32_t *__restrict__ cut, const int32_t *__restrict__ cend,
+                                                       const int32_t *__restrict__ spec_of,
+                                                       const int32_t *__restrict__ spec_cam, int32_t *__restrict__ out) {
+    extern __shared__ int32_t plan_sh[];
+    int32_t *cc = plan_sh, *cp = plan_sh + nc, *mx = plan_sh + nc + nspec;
+    const int q = blockIdx.x;
+    for (int i = threadIdx.x; i < nc + nspec + 2; i += blockDim.x) plan_sh[i] = 0;
+    __syncthreads();
+    const int32_t o0 = pstart[cut[q]], o1 = pstart[cend[q]];
+    for (int32_t a = o0 + (int32_t)threadIdx.x; a < o1; a += blockDim.x) {
+        const int ca = cam[a], pnt = pt[a];
+        atomicAdd(&cc[ca], 1);
+        for (int32_t b = pstart[pnt]; b < pstart[pnt + 1]; ++b) {
+            const int cb = cam[b];
+            if (cb > ca) atomicAdd(&cp[spec_of[ca * nc + cb]], 1);
+        }
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < nspec; w += blockDim.x) {
+        const int c0 = spec_cam[2 * w], c1 = spec_cam[2 * w + 1];
+        atomicMax(&mx[0], cc[c0] + (c1 >= 0 ? cc[c1] : 0));
+        atomicMax(&mx[1], cp[w]);
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) out[2 * q + threadIdx.x] = mx[threadIdx.x];
+}
+
+// per chunk (cut: the chunks' first points, nchunk + 1 entries, the last
+// np_): pairs per camera block, bq[blk][q], and observations per camera,
+// cq[c][q] (32-bit counters; k_plan_narrow makes the host planner's uint16)
+__global__ void __launch_bounds__(256) k_plan_counts(int64_t no, int32_t nc, int32_t nchunk,
+                                                     const int32_t *__restrict__ pstart, const int32_t *__restrict__ pt,
+                                                     const int32_t *__restrict__ cam, const int32_t *__restrict__ cut,
+                                                     uint32_t *__restrict__ bq, uint32_t *__restrict__ cq) {
+    const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (a >= no) return;
+    const int32_t pnt = pt[a], ca = cam[a];
+    const int q = (int)lower_bound_d(cut, 0, nchunk + 1, pnt + 1) - 1;  // last chunk starting at or before pnt
+    atomicAdd(&cq[(size_t)ca * nchunk + q], 1u);
+    for (int32_t b = pstart[pnt]; b < pstart[pnt + 1]; ++b) {
+        const int cb = cam[b];
+        if (cb > ca) atomicAdd(&bq[(size_t)dense_blk_d(nc, ca, cb) * nchunk + q], 1u);
+    }
+}
+__global__ void __launch_bounds__(256) k_plan_narrow(int64_t n, const uint32_t *__restrict__ in, uint16_t *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = (uint16_t)in[i];
+}
+
+// one workgroup per (chunk q, spec w), qw = q * nspec + w: the slot list
+// (count, then every slot's point | row << 31, padded with the chunk's first
+// observed point), the group header (pair offsets from bq, total, n0, n1,
+// first observation) and the pairs, every group's in slot order (the host's
+// traversal: spec row, the camera's observations in point order, at most one
+// pair per point and block).  Slots' column hits go through an LDS bit mask
+// (slot x the row's block columns); one thread per group then walks the
+// slots in order.
+constexpr int PLAN_THREADS = 256;
+__global__ void __launch_bounds__(PLAN_THREADS) k_plan_lists(
+    int32_t nchunk, int32_t nspec, int32_t np_, int32_t mw, const int32_t *__restrict__ cut,
+    const int32_t *__restrict__ pstart, const int32_t *__restrict__ pt, const int32_t *__restrict__ cam,
+    const int32_t *__restrict__ cstart, const int32_t *__restrict__ cm_pt, const int32_t *__restrict__ spec_row,
+    const int32_t *__restrict__ goff, const SweepGroup *__restrict__ groups, const uint16_t *__restrict__ bq,
+    int32_t list_cap, int32_t pair_cap, int32_t hdr_cap, int32_t *__restrict__ list, uint16_t *__restrict__ pairs,
+    int32_t *__restrict__ hdr) {
+    extern __shared__ int32_t plan_sh[];
+    int32_t *off = plan_sh;                                             // hdr_cap group offsets
+    uint32_t *mask = reinterpret_cast<uint32_t *>(plan_sh + hdr_cap);   // [slot][mw] column hits
+    __shared__ int32_t lo[2], nr[2], tot;
+    const int q = blockIdx.x / nspec, w = blockIdx.x % nspec;
+    const size_t qw = (size_t)q * nspec + w;
+    const int32_t P0 = cut[q], P1 = cut[q + 1];
+    const int32_t *sr = spec_row + 6 * w;  // rows: (camera, j0, j1) x 2, camera -1 = none
+    if (threadIdx.x < 2) {
+        const int c = sr[3 * threadIdx.x];
+        int32_t l = 0, h = 0;
+        if (c >= 0) {
+            l = lower_bound_d(cm_pt, cstart[c], cstart[c + 1], P0);
+            h = lower_bound_d(cm_pt, l, cstart[c + 1], P1);
+        }
+        lo[threadIdx.x] = l;
+        nr[threadIdx.x] = h - l;
+    }
+    __syncthreads();
+    const int32_t n0 = nr[0], n1 = nr[1], ns = n0 + n1;
+    const int32_t o0 = pstart[P0];
+    // the slot list
+    int32_t *lst = list + qw * list_cap;
+    const int32_t pad = pt[o0];
+    for (int i = threadIdx.x; i < list_cap; i += PLAN_THREADS) {
+        int32_t v = pad;
+        if (i == 0) v = ns;
+        else if (i - 1 < n0) v = cm_pt[lo[0] + i - 1];
+        else if (i - 1 < ns) v = (int32_t)((uint32_t)cm_pt[lo[1] + i - 1 - n0] | 0x80000000u);
+        lst[i] = v;
+    }
+    // every slot's block-column hits (the point's cameras cj > c, j0 <= cj < j1)
+    for (int s = threadIdx.x; s < ns; s += PLAN_THREADS) {
+        const int rr = s < n0 ? 0 : 1;
+        const int c = sr[3 * rr], j0 = sr[3 * rr + 1], j1 = sr[3 * rr + 2];
+        const int32_t pnt = cm_pt[lo[rr] + (rr ? s - n0 : s)];
+        uint32_t *m = mask + (size_t)s * mw;
+        for (int k = 0; k < mw; ++k) m[k] = 0u;
+        for (int32_t b = pstart[pnt]; b < pstart[pnt + 1]; ++b) {
+            const int cj = cam[b];
+            if (cj <= c || cj < j0 || cj >= j1) continue;
+            m[(cj - j0) >> 5] |= 1u << ((cj - j0) & 31);
+        }
+    }
+    // the group offsets: one wave, 64 groups a step (inclusive scan by shuffles)
+    const int g0 = goff[w], ng = goff[w + 1] - g0;
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x < 64) {
+        int32_t run = 0;
+        for (int base = 0; base < ng; base += 64) {
+            const int g = base + lane;
+            int32_t v = 0;
+            if (g < ng) {
+                const SweepGroup G = groups[g0 + g];
+                v = (G.flags & 1) ? 0 : (int32_t)bq[(size_t)G.blk * nchunk + q];
+            }
+            int32_t x = v;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int32_t y = __shfl_up(x, d);
+                if (lane >= d) x += y;
+            }
+            if (g < ng) off[g] = run + x - v;
+            run += __shfl(x, 63);
+        }
+        if (lane == 0) tot = run;
+    }
+    __syncthreads();
+    int32_t *hd = hdr + qw * hdr_cap;
+    for (int i = threadIdx.x; i < hdr_cap; i += PLAN_THREADS) {
+        int32_t v = 0;
+        if (i < ng) v = off[i];
+        else if (i == ng) v = tot;
+        else if (i == ng + 1) v = n0;
+        else if (i == ng + 2) v = n1;
+        else if (i == ng + 3) v = o0;
+        hd[i] = v;
+    }
+    // the pairs: a thread per group walks the slots of its row in order
+    uint16_t *pp = pairs + qw * pair_cap;
+    for (int i = tot + (int)threadIdx.x; i < pair_cap; i += PLAN_THREADS) pp[i] = 0;
+    for (int g = threadIdx.x; g < ng; g += PLAN_THREADS) {
+        const SweepGroup G = groups[g0 + g];
+        if (G.flags & 1) continue;
+        const int rr = (G.flags & 2) ? 1 : 0;
+        const int col = G.cam_b - sr[3 * rr + 1], wd = col >> 5;
+        const uint32_t bit = 1u << (col & 31);
+        const int s0 = rr ? n0 : 0, s1 = rr ? ns : n0;
+        int32_t k = off[g];
+        for (int s = s0; s < s1; ++s)
+            if (mask[(size_t)s * mw + wd] & bit) pp[k++] = (uint16_t)s;
+    }
+}
+
+
 // trips a slot of a group makes through its chunk share: ceil(P / s)
 static inline int sweep_trips(int P, int s) { return (P + s - 1) / s; }
 
@@ -2786,9 +2987,38 @@ struct PhaseTimer {
     }
 };
 
+// the device side of the planner: the uploaded COO and a stream; scratch
+// buffers live until the object goes (freed on every return path)
+struct DevPlan {
+    hipStream_t s = nullptr;
+    const int32_t *pstart = nullptr, *pt = nullptr, *cam = nullptr;
+    int64_t no = 0;
+    std::vector<void *> bufs;
+    int err = 0;
+    ~DevPlan() {
+        for (void *b : bufs) (void)hipFree(b);
+    }
+    template <class T>
+    T *scratch(size_t n) {
+        void *q = nullptr;
+        if (hipMalloc(&q, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) {
+            err = SFM_ERR_NOMEM;
+            return nullptr;
+        }
+        bufs.push_back(q);
+        return static_cast<T *>(q);
+    }
+    bool ok(hipError_t e) {
+        if (e != hipSuccess && !err) err = SFM_ERR_HIP;
+        return !err;
+    }
+    uint16_t *d_bq = nullptr;   // bq [blk][q] (uint16), kept for k_plan_lists
+    int32_t *d_cut = nullptr;   // the final cut (nchunk + 1)
+};
+
 static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt,
                        const std::vector<int32_t> &pstart, const std::vector<int64_t> &cnt, int lpp, int ncu,
-                       bool allow_split, SweepPlan &P) {
+                       bool allow_split, SweepPlan &P, DevPlan *dev = nullptr) {
     PhaseTimer pt_;
     P.nbd = nc * (nc + 1) / 2;
     P.blkij.resize(P.nbd);
@@ -2809,6 +3039,12 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     for (auto &sp : specs) {  // the a-side cameras of every spec (rows 0 and 1)
         P.spec_cam.push_back(sp[0].c);
         P.spec_cam.push_back(sp.size() > 1 ? sp[1].c : -1);
+        for (size_t rr = 0; rr < 2; ++rr) {
+            const bool has = rr < sp.size();
+            P.spec_row.push_back(has ? sp[rr].c : -1);
+            P.spec_row.push_back(has ? sp[rr].j0 : 0);
+            P.spec_row.push_back(has ? sp[rr].j1 : 0);
+        }
     }
     // block (i <= j) -> spec that owns it
     std::vector<int32_t> spec_of((size_t)nc * nc, -1);
@@ -2858,6 +3094,7 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     // overshoot until the largest (chunk, spec) fits
     int chunk_obs = std::max(64, std::min(env_int("SFM_SWEEP_CHUNK", 65535), 65535));
     std::vector<int64_t> cut;  // chunk first points
+    int32_t *d_spec_of = nullptr, *d_scam = nullptr;  // device planner: the spec tables
     for (;;) {
         // the cuts follow from the observation counts alone; the chunks'
         // staged slots and pair counts (the LDS bound) are then counted per
@@ -2881,7 +3118,35 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
             P.rchunk.push_back((int32_t)cut.size());
         }
         std::vector<int> cstaged(cut.size(), 0), cpmax(cut.size(), 0);
-        if (ok)
+        if (ok && dev && !cut.empty()) {  // the same statistics from k_plan_chunkmax
+            const size_t nk = cut.size();
+            if (!d_spec_of) {
+                d_spec_of = dev->scratch<int32_t>(spec_of.size());
+                d_scam = dev->scratch<int32_t>(P.spec_cam.size());
+                if (dev->err) return;
+                dev->ok(hipMemcpyAsync(d_spec_of, spec_of.data(), spec_of.size() * 4, hipMemcpyHostToDevice, dev->s));
+                dev->ok(hipMemcpyAsync(d_scam, P.spec_cam.data(), P.spec_cam.size() * 4, hipMemcpyHostToDevice, dev->s));
+            }
+            std::vector<int32_t> cc(2 * nk), out(2 * nk);
+            for (size_t k = 0; k < nk; ++k) {
+                cc[k] = (int32_t)cut[k];
+                cc[nk + k] = (int32_t)cend[k];
+            }
+            int32_t *d_cc = dev->scratch<int32_t>(2 * nk), *d_out = dev->scratch<int32_t>(2 * nk);
+            if (dev->err) return;
+            dev->ok(hipMemcpyAsync(d_cc, cc.data(), 2 * nk * 4, hipMemcpyHostToDevice, dev->s));
+            hipLaunchKernelGGL(k_plan_chunkmax, dim3((unsigned)nk), dim3(256), (nc + P.nspec + 2) * sizeof(int32_t),
+                               dev->s, nc, P.nspec, dev->pstart, dev->pt, dev->cam, d_cc, d_cc + nk, d_spec_of, d_scam,
+                               d_out);
+            dev->ok(hipGetLastError());
+            dev->ok(hipMemcpyAsync(out.data(), d_out, 2 * nk * 4, hipMemcpyDeviceToHost, dev->s));
+            dev->ok(hipStreamSynchronize(dev->s));
+            if (dev->err) return;
+            for (size_t k = 0; k < nk; ++k) {
+                cstaged[k] = out[2 * k];
+                cpmax[k] = out[2 * k + 1];
+            }
+        } else if (ok)
             par_for((int64_t)cut.size(), [&](int64_t k) {
                 std::vector<int32_t> ccount(nc, 0), cpairs(P.nspec, 0);
                 for (int64_t pe = cut[k]; pe < cend[k]; ++pe)
@@ -2911,8 +3176,32 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     }
     P.nchunk = (int32_t)cut.size();
     pt_.tick("plan:chunks");
+    P.cut.assign(cut.begin(), cut.end());
+    P.cut.push_back((int32_t)np_);
     // exact per-chunk counts: pairs per block, observations per camera
     std::vector<uint16_t> bq((size_t)P.nbd * P.nchunk, 0), cq((size_t)nc * P.nchunk, 0);
+    if (dev) {  // k_plan_counts (32-bit atomics), narrowed to the planner's uint16 on the device
+        const size_t nb = (size_t)P.nbd * P.nchunk, ncq = (size_t)nc * P.nchunk;
+        uint32_t *b32 = dev->scratch<uint32_t>(nb + ncq);
+        uint16_t *b16 = dev->scratch<uint16_t>(nb + ncq);
+        dev->d_cut = dev->scratch<int32_t>(P.cut.size());
+        if (dev->err) return;
+        dev->ok(hipMemcpyAsync(dev->d_cut, P.cut.data(), P.cut.size() * 4, hipMemcpyHostToDevice, dev->s));
+        dev->ok(hipMemsetAsync(b32, 0, (nb + ncq) * 4, dev->s));
+        if (no) {
+            hipLaunchKernelGGL(k_plan_counts, dim3((unsigned)ceil_div(no, 256)), dim3(256), 0, dev->s, no, nc, P.nchunk,
+                               dev->pstart, dev->pt, dev->cam, dev->d_cut, b32, b32 + nb);
+            dev->ok(hipGetLastError());
+        }
+        hipLaunchKernelGGL(k_plan_narrow, dim3((unsigned)ceil_div((int64_t)(nb + ncq), 256)), dim3(256), 0, dev->s,
+                           (int64_t)(nb + ncq), b32, b16);
+        dev->ok(hipGetLastError());
+        dev->ok(hipMemcpyAsync(bq.data(), b16, nb * 2, hipMemcpyDeviceToHost, dev->s));
+        dev->ok(hipMemcpyAsync(cq.data(), b16 + nb, ncq * 2, hipMemcpyDeviceToHost, dev->s));
+        dev->ok(hipStreamSynchronize(dev->s));
+        if (dev->err) return;
+        dev->d_bq = b16;
+    } else
     par_for(P.nchunk, [&](int64_t q) {  // chunk q writes column q only
         const int64_t pe = q + 1 < P.nchunk ? cut[q + 1] : np_;
         for (int64_t pp = cut[q]; pp < pe; ++pp)
@@ -3039,13 +3328,18 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
                      P.nspec, P.nrange, P.nchunk, chunk_obs, P.buf_slots, P.pair_cap, P.lds_bytes(), (long long)f_plan,
                      (long long)f_ideal);
     const size_t nqw = (size_t)P.nchunk * P.nspec;
+    if (dev && P.hdr_cap <= 1024) {  // k_plan_lists writes them into the problem's buffers
+        P.dev_lists = true;
+        pt_.tick("plan:lists");
+        return;
+    }
     P.list.assign(nqw * P.list_cap, 0);
     P.pairs.assign(nqw * P.pair_cap, 0);
     P.hdr.assign(nqw * P.hdr_cap, 0);
     par_for(P.nchunk, [&](int64_t q) {  // chunk q writes its (chunk, spec) regions only
         std::vector<std::vector<int32_t>> per_cam(nc);
         std::vector<int32_t> slot_of;  // chunk-local obs offset -> position in its camera's list
-        std::vector<std::vector<uint32_t>> glist;
+        std::vector<int32_t> gpos;     // each group's next pair position
         const int32_t o0 = pstart[cut[q]];
         const int32_t o1 = q + 1 < P.nchunk ? pstart[cut[q + 1]] : (int32_t)no;
         for (auto &v : per_cam) v.clear();
@@ -3067,28 +3361,35 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
             lst[0] = n0 + n1;
             for (; ns_ < P.list_cap; ++ns_) lst[ns_] = pt[o0];  // padding: any valid point
             const int ng = P.goff[w + 1] - P.goff[w];
-            glist.assign(ng, {});
-            for (size_t rr = 0; rr < sp.size(); ++rr) {
-                const Row &R = sp[rr];
-                const int32_t abase = rr == 0 ? 0 : n0;
-                for (int32_t off : per_cam[R.c]) {
-                    const int32_t a = o0 + off, pnt = pt[a];
-                    for (int32_t b = pstart[pnt]; b < pstart[pnt + 1]; ++b) {
-                        const int cj = cam[b];
-                        if (cj <= R.c || cj < R.j0 || cj >= R.j1) continue;
-                        const int g = gid_of[w][rr * nc + (cj - R.j0)];
-                        glist[g].push_back((uint32_t)(abase + slot_of[off]));
-                    }
-                }
-            }
+            // every group's pairs in this chunk are counted already (bq: a
+            // block belongs to one group of one spec), so the group offsets
+            // come first and the pairs go straight to their place, in the
+            // traversal order (spec row, the camera's observations, the
+            // point's observations)
             int32_t *hd = &P.hdr[qw * P.hdr_cap];
             uint16_t *pp = &P.pairs[qw * P.pair_cap];
             int32_t np2 = 0;
             for (int g = 0; g < ng; ++g) {
                 hd[g] = np2;
-                for (uint32_t v : glist[g]) pp[np2++] = (uint16_t)v;
+                const SweepGroup &G = P.groups[P.goff[w] + g];
+                if (!(G.flags & 1)) np2 += bq[(size_t)G.blk * P.nchunk + q];
             }
             hd[ng] = np2;
+            gpos.assign(hd, hd + ng);
+            for (size_t rr = 0; rr < sp.size(); ++rr) {
+                const Row &R = sp[rr];
+                const int32_t abase = rr == 0 ? 0 : n0;
+                const int *gid = gid_of[w].data() + rr * nc - R.j0;
+                for (int32_t off : per_cam[R.c]) {
+                    const int32_t a = o0 + off, pnt = pt[a];
+                    const uint16_t v = (uint16_t)(abase + slot_of[off]);
+                    for (int32_t b = pstart[pnt]; b < pstart[pnt + 1]; ++b) {
+                        const int cj = cam[b];
+                        if (cj <= R.c || cj < R.j0 || cj >= R.j1) continue;
+                        pp[gpos[gid[cj]]++] = v;
+                    }
+                }
+            }
             hd[ng + 1] = n0;
             hd[ng + 2] = n1;
             hd[ng + 3] = o0;
@@ -3108,6 +3409,7 @@ struct sfm_ba_problem {
     sfm_comm *comm = nullptr;
     int32_t nc = 0, ns = 0, nsp = 0, nT = 0, tb = 16;
     int64_t np = 0, no = 0, npairs = 0;
+    uint64_t plan_digest = 0;  // SFM_PLAN_DIGEST=1: the digest of the sweep plan (sfm_ba_plan_digest)
     int32_t ndiag_items = 0, ndiag_blocks = 0;  // k_camera_lin items (one per workgroup) / cameras
     int32_t cl_fused_wg = 0, cl_fused_items = 0;  // k_schur_sweep's camera workgroups / their items
     bool cl_fused = false;                         // this solve: camera blocks inside the sweep launch
@@ -3291,8 +3593,6 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         SFM_CHECK_ARG(o == 0 || pt[o] >= pt[o - 1], "observations must be point-major (sorted by point)");
     }
     ctick("validate");
-    SFM_HIP(hipSetDevice(device));
-    (void)hipGetLastError();  // launches below are checked with hipGetLastError: start clean
     auto p = std::make_unique<sfm_ba_problem>();
     p->device = device;
     p->comm = comm;
@@ -3309,10 +3609,6 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
                     env_int("SFM_SWEEP_PINHOLE", 1) != 0;
     p->cams0.assign(cams, cams + 6 * (size_t)nc);
     p->pts0.assign(pts, pts + 3 * (size_t)np_);
-    SFM_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
-    for (auto &e : p->ev) SFM_HIP(hipEventCreate(&e));
-    for (auto &e : p->ev_it) SFM_HIP(hipEventCreate(&e));
-    ctick("stream");
     // point CSR
     std::vector<int32_t> pstart(np_ + 1, 0);
     for (int64_t o = 0; o < no; ++o) pstart[pt[o] + 1]++;
@@ -3360,6 +3656,38 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     }
     p->npairs = tot;
     ctick("blockcounts");
+    // SFM_CREATE_PLAN_ONLY=1 (measurement, tools/create_probe.py): the host
+    // planner alone, without a device; returns 1 and no problem
+    const bool plan_only = env_int("SFM_CREATE_PLAN_ONLY", 0) != 0;
+    int rc;
+    if (!plan_only) {
+        SFM_HIP(hipSetDevice(device));
+        (void)hipGetLastError();  // launches below are checked with hipGetLastError: start clean
+        SFM_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+        for (auto &e : p->ev) SFM_HIP(hipEventCreate(&e));
+        for (auto &e : p->ev_it) SFM_HIP(hipEventCreate(&e));
+        ctick("stream");
+        // the COO up first: the device planner reads it
+        if ((rc = p->alloc(p->d_cam, no)) || (rc = p->alloc(p->d_pt, no)) || (rc = p->alloc(p->d_pstart, np_ + 1)) ||
+            (rc = p->alloc(p->d_obs, no)) || (rc = p->alloc(p->d_cm_pt, no)) || (rc = p->alloc(p->d_cm_obs, no)) ||
+            (rc = p->alloc(p->d_cstart, nc + 1)))
+            return rc;
+        hipStream_t s = p->stream;
+        if (no) {
+            SFM_HIP(hipMemcpyAsync(p->d_cam, cam, no * 4, hipMemcpyHostToDevice, s));
+            SFM_HIP(hipMemcpyAsync(p->d_pt, pt, no * 4, hipMemcpyHostToDevice, s));
+            SFM_HIP(hipMemcpyAsync(p->d_obs, obs, no * 16, hipMemcpyHostToDevice, s));
+        }
+        SFM_HIP(hipMemcpyAsync(p->d_pstart, pstart.data(), pstart.size() * 4, hipMemcpyHostToDevice, s));
+        if (no) {  // the permutation up, the camera-major copies gathered on the device
+            SFM_HIP(hipMemcpyAsync(p->d_cm_pt, cam_obs.data(), no * 4, hipMemcpyHostToDevice, s));
+            hipLaunchKernelGGL(k_gather_cam_major, dim3((unsigned)ceil_div(no, 256)), dim3(256), 0, s, no, p->d_pt,
+                               p->d_obs, p->d_cm_pt, p->d_cm_obs);
+            SFM_HIP(hipGetLastError());
+        }
+        SFM_HIP(hipMemcpyAsync(p->d_cstart, cstart.data(), cstart.size() * 4, hipMemcpyHostToDevice, s));
+        ctick("up:obs");
+    }
     SweepPlan sw;
     // lanes per pair slot: 1 (a lane forms a pair's whole 6x6 block, H once;
     // two lanes with half the rows each: cfg4 0.155 against 0.134 ms, round 3; retired)
@@ -3367,7 +3695,23 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     // the solves read the split partials in k_schur_finish's order (SlabSrc
     // when the finish is folded in): the sweep's dispatch tail may be split
     const bool split_ok = true;
-    plan_sweep(nc, np_, no, cam, pt, pstart, cnt, p->sw_lpp, device_cus(device), split_ok, sw);
+    // the plan's passes over the observation pairs on the device
+    // (SFM_PLAN_HOST=1: the host planner's threads, the same plan)
+    DevPlan dev;
+    const bool dev_plan = !plan_only && env_int("SFM_PLAN_HOST", 0) == 0;
+    if (dev_plan) {
+        dev.s = p->stream;
+        dev.pstart = p->d_pstart;
+        dev.pt = p->d_pt;
+        dev.cam = p->d_cam;
+        dev.no = no;
+    }
+    plan_sweep(nc, np_, no, cam, pt, pstart, cnt, p->sw_lpp, plan_only ? 256 : device_cus(device), split_ok, sw,
+               dev_plan ? &dev : nullptr);
+    if (dev.err) {
+        set_error("sweep plan on the device: %s", dev.err == SFM_ERR_NOMEM ? "hipMalloc failed" : "HIP error");
+        return dev.err;
+    }
     ctick("plan_sweep");
     if (sw.buf_slots > SW_MAX_STAGED) {  // one point with more observations in a spec's cameras than a round holds
         set_error("sweep plan: %d observations of one spec's cameras in a single point range (max %d)", sw.buf_slots,
@@ -3414,11 +3758,35 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     p->pt_blocks = std::max(1, ceil_div(np_ * PT_GROUP, PT_THREADS));
     p->payload_len = pay_vec_base(p->ns) + 3 * p->ns + 1;
     ctick("cam_items");
-    int rc;
-    if ((rc = p->alloc(p->d_cam, no)) || (rc = p->alloc(p->d_pt, no)) || (rc = p->alloc(p->d_pstart, np_ + 1)) ||
-        (rc = p->alloc(p->d_obs, no)) || (rc = p->alloc(p->d_cm_pt, no)) ||
-        (rc = p->alloc(p->d_cm_obs, no)) || (rc = p->alloc(p->d_cstart, nc + 1)) ||
-        (rc = p->alloc(p->d_items, p->ndiag_items)) || (rc = p->alloc(p->d_blocks, p->ndiag_blocks)) ||
+    // a digest of everything the planning produced, the (chunk, spec) lists
+    // read back from the device (SFM_PLAN_DIGEST=1 or SFM_CREATE_TIMING=1;
+    // the host and device planners must agree: tests/test_gpu_parity.py)
+    const size_t nqw = (size_t)sw.nchunk * sw.nspec;
+    auto plan_digest = [&](const int32_t *list, const uint16_t *pairs, const int32_t *hdr) {
+        uint64_t h = 1469598103934665603ull;
+        auto mix = [&](const void *d, size_t n) {
+            const unsigned char *b = static_cast<const unsigned char *>(d);
+            for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+        };
+        auto mixv = [&](const auto &v) { mix(v.data(), v.size() * sizeof(v[0])); };
+        mixv(pstart), mixv(cstart), mixv(cam_obs), mixv(cnt);
+        mixv(sw.rchunk), mixv(sw.goff), mixv(sw.nload), mix(list, nqw * sw.list_cap * 4), mix(hdr, nqw * sw.hdr_cap * 4);
+        mixv(sw.spec_cam), mixv(sw.split_of), mixv(sw.groups), mixv(sw.lanegrp), mix(pairs, nqw * sw.pair_cap * 2);
+        mixv(sw.blkij);
+        const int32_t sc[] = {sw.nrange, sw.nspec, sw.nbd, sw.buf_slots, sw.pair_cap, sw.hdr_cap, sw.list_cap,
+                              sw.nchunk, sw.split_S, sw.split_w0, sw.split_n, sw.split_gmax, p->cl_fused_wg};
+        mix(sc, sizeof sc);
+        mixv(csa.items), mixv(csa.blocks), mixv(csa.wg_first), mixv(cfu.items), mixv(cfu.blocks), mixv(cfu.wg_first);
+        return h;
+    };
+    const bool want_digest = ctm || env_int("SFM_PLAN_DIGEST", 0) != 0;
+    if (plan_only) {
+        if (want_digest)
+            std::fprintf(stderr, "[create] plan digest %016llx\n",
+                         (unsigned long long)plan_digest(sw.list.data(), sw.pairs.data(), sw.hdr.data()));
+        return 1;
+    }
+    if ((rc = p->alloc(p->d_items, p->ndiag_items)) || (rc = p->alloc(p->d_blocks, p->ndiag_blocks)) ||
         (rc = p->alloc(p->d_wg_first, csa.wg_first.size())) || (rc = p->alloc(p->d_fitems, cfu.items.size())) ||
         (rc = p->alloc(p->d_fblocks, cfu.blocks.size())) || (rc = p->alloc(p->d_fwg_first, cfu.wg_first.size())) ||
         (rc = p->alloc(p->d_slab, (int64_t)ITEM_W * sw.nrange * sw.nbd)) ||
@@ -3428,8 +3796,10 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = p->alloc(p->d_sw_rchunk, sw.rchunk.size())) || (rc = p->alloc(p->d_sw_goff, sw.goff.size())) ||
         (rc = p->alloc(p->d_sw_nload, sw.nload.size())) ||
         (rc = p->alloc(p->d_sw_groups, sw.groups.size())) || (rc = p->alloc(p->d_sw_lanegrp, sw.lanegrp.size())) ||
-        (rc = p->alloc(p->d_sw_list, sw.list.size())) || (rc = p->alloc(p->d_sw_hdr, sw.hdr.size())) ||
-        (rc = p->alloc(p->d_sw_pairs, (int64_t)(sw.pairs.size() + 1) / 2)) || (rc = p->alloc(p->d_sw_blkij, sw.blkij.size())) ||
+        (rc = p->alloc(p->d_sw_list, (int64_t)(nqw * sw.list_cap))) ||
+        (rc = p->alloc(p->d_sw_hdr, (int64_t)(nqw * sw.hdr_cap))) ||
+        (rc = p->alloc(p->d_sw_pairs, (int64_t)(nqw * sw.pair_cap + 1) / 2)) ||
+        (rc = p->alloc(p->d_sw_blkij, sw.blkij.size())) ||
         (rc = p->alloc(p->d_camlin, (int64_t)CAMLIN * nc)) ||
         (rc = p->alloc(p->d_slab2, (int64_t)CAMLIN * std::max<int64_t>(1, std::max(p->ndiag_items, p->cl_fused_items)))) ||
         (rc = p->alloc(p->d_Rt, 12 * (int64_t)nc)) || (rc = p->alloc(p->d_Rt2, 12 * (int64_t)nc)) ||
@@ -3473,21 +3843,6 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     std::memset((void *)p->h_ring, 0, kHostRing * sizeof(HostLM));
     SFM_HIP(hipHostGetDevicePointer((void **)&p->d_ring, p->h_ring, 0));
     hipStream_t s = p->stream;
-    if (no) {
-        SFM_HIP(hipMemcpyAsync(p->d_cam, cam, no * 4, hipMemcpyHostToDevice, s));
-        SFM_HIP(hipMemcpyAsync(p->d_pt, pt, no * 4, hipMemcpyHostToDevice, s));
-        SFM_HIP(hipMemcpyAsync(p->d_obs, obs, no * 16, hipMemcpyHostToDevice, s));
-    }
-    SFM_HIP(hipMemcpyAsync(p->d_pstart, pstart.data(), pstart.size() * 4, hipMemcpyHostToDevice, s));
-    ctick("up:obs");
-    if (no) {  // the permutation up, the camera-major copies gathered on the device
-        SFM_HIP(hipMemcpyAsync(p->d_cm_pt, cam_obs.data(), no * 4, hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_gather_cam_major, dim3((unsigned)ceil_div(no, 256)), dim3(256), 0, s, no, p->d_pt,
-                           p->d_obs, p->d_cm_pt, p->d_cm_obs);
-        SFM_HIP(hipGetLastError());
-    }
-    SFM_HIP(hipMemcpyAsync(p->d_cstart, cstart.data(), cstart.size() * 4, hipMemcpyHostToDevice, s));
-    ctick("up:cammajor");
     SFM_HIP(hipMemsetAsync(p->d_camlin, 0, (size_t)CAMLIN * nc * sizeof(double), s));
     SFM_HIP(hipMemsetAsync(p->d_count, 0, 3 * GS_WORDS * sizeof(unsigned), s));
     SFM_HIP(hipMemsetAsync(p->d_nbig, 0, sizeof(unsigned), s));
@@ -3508,17 +3863,48 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         (rc = up(p->d_sw_nload, sw.nload.data(), sw.nload.size() * 4)) ||
         (rc = up(p->d_sw_groups, sw.groups.data(), sw.groups.size() * sizeof(SweepGroup))) ||
         (rc = up(p->d_sw_lanegrp, sw.lanegrp.data(), sw.lanegrp.size() * 2)) ||
-        (rc = up(p->d_sw_list, sw.list.data(), sw.list.size() * 4)) ||
         (rc = up(p->d_sw_scam, sw.spec_cam.data(), sw.spec_cam.size() * 4)) ||
-        (rc = up(p->d_sw_hdr, sw.hdr.data(), sw.hdr.size() * 4)) ||
-        (rc = up(p->d_sw_pairs, sw.pairs.data(), sw.pairs.size() * 2)) ||
         (rc = up(p->d_sw_blkij, sw.blkij.data(), sw.blkij.size() * sizeof(int2))) ||
         (rc = up(p->d_sw_split_of, sw.split_of.data(), sw.split_of.size() * 4)))
         return rc;
+    if (sw.dev_lists) {  // the (chunk, spec) lists built on the device from the camera-major points
+        int32_t *d_row = dev.scratch<int32_t>(sw.spec_row.size());
+        if (dev.err) return dev.err;
+        if ((rc = up(d_row, sw.spec_row.data(), sw.spec_row.size() * 4))) return rc;
+        int mcols = 1;
+        for (size_t w = 0; w < sw.spec_row.size() / 6; ++w)
+            for (int rr = 0; rr < 2; ++rr) mcols = std::max(mcols, sw.spec_row[6 * w + 3 * rr + 2] - sw.spec_row[6 * w + 3 * rr + 1]);
+        const int mw = (mcols + 31) / 32;
+        const size_t lds = (size_t)sw.hdr_cap * 4 + (size_t)sw.buf_slots * mw * 4;
+        SFM_HIP(hipFuncSetAttribute((const void *)k_plan_lists, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        if (nqw) {
+            hipLaunchKernelGGL(k_plan_lists, dim3((unsigned)nqw), dim3(PLAN_THREADS), lds, s, sw.nchunk, sw.nspec,
+                               (int32_t)np_, mw, dev.d_cut, p->d_pstart, p->d_pt, p->d_cam, p->d_cstart, p->d_cm_pt,
+                               d_row, p->d_sw_goff, p->d_sw_groups, dev.d_bq, sw.list_cap, sw.pair_cap, sw.hdr_cap,
+                               p->d_sw_list, reinterpret_cast<uint16_t *>(p->d_sw_pairs), p->d_sw_hdr);
+            SFM_HIP(hipGetLastError());
+        }
+    } else if ((rc = up(p->d_sw_list, sw.list.data(), sw.list.size() * 4)) ||
+               (rc = up(p->d_sw_hdr, sw.hdr.data(), sw.hdr.size() * 4)) ||
+               (rc = up(p->d_sw_pairs, sw.pairs.data(), sw.pairs.size() * 2))) {
+        return rc;
+    }
     ctick("up:sweep");
+    if (want_digest) {  // everything planned, the lists as the device holds them
+        std::vector<int32_t> hl(nqw * sw.list_cap), hh(nqw * sw.hdr_cap);
+        std::vector<uint16_t> hp(nqw * sw.pair_cap);
+        SFM_HIP(hipMemcpyAsync(hl.data(), p->d_sw_list, hl.size() * 4, hipMemcpyDeviceToHost, s));
+        SFM_HIP(hipMemcpyAsync(hh.data(), p->d_sw_hdr, hh.size() * 4, hipMemcpyDeviceToHost, s));
+        SFM_HIP(hipMemcpyAsync(hp.data(), p->d_sw_pairs, hp.size() * 2, hipMemcpyDeviceToHost, s));
+        SFM_HIP(hipStreamSynchronize(s));
+        p->plan_digest = plan_digest(hl.data(), hp.data(), hh.data());
+        if (ctm) std::fprintf(stderr, "[create] plan digest %016llx (%s lists)\n", (unsigned long long)p->plan_digest,
+                              sw.dev_lists ? "device" : "host");
+        ctick("digest");
+    }
     if (ctm)
-        std::fprintf(stderr, "[create] sweep arrays: list %.1f MB pairs %.1f MB hdr %.1f MB\n", sw.list.size() * 4e-6,
-                     sw.pairs.size() * 2e-6, sw.hdr.size() * 4e-6);
+        std::fprintf(stderr, "[create] sweep arrays: list %.1f MB pairs %.1f MB hdr %.1f MB\n",
+                     nqw * sw.list_cap * 4e-6, nqw * sw.pair_cap * 2e-6, nqw * sw.hdr_cap * 4e-6);
     SFM_HIP(hipFuncSetAttribute((const void *)k_schur_sweep<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)p->sw_lds_bytes));
     SFM_HIP(hipFuncSetAttribute((const void *)k_schur_sweep<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3532,6 +3918,14 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         ctick("sync");
     }
     *out = p.release();
+    return 0;
+}
+
+// the sweep plan's digest, computed at create with SFM_PLAN_DIGEST=1 (0
+// otherwise): the device planner's lists against SFM_PLAN_HOST=1's
+extern "C" int sfm_ba_plan_digest(sfm_ba_problem *p, uint64_t *out) {
+    SFM_CHECK_ARG(p && out, "null pointer");
+    *out = p->plan_digest;
     return 0;
 }
 

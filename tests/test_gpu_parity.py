@@ -850,6 +850,17 @@ def test_ba_failure_contract(core, capsys):
     R1, C1, X1 = perform_bundle_adjustment(Xw, 0 * p["filtered_world_coords"], p["feature_x"], p["feature_y"],
                                            p["flags"], R0, C0, K, 2)
     assert X1 is Xw and capsys.readouterr().out == ""
+    # a non-finite residual at x0 (scipy least_squares.py:843-845): the
+    # device's initial cost ends the solve (status 6) and the drop-in fails
+    Xn = p["X0"].copy()
+    Xn[3, 1] = np.nan
+    R1, C1, X1 = perform_bundle_adjustment(Xn, p["filtered_world_coords"], p["feature_x"], p["feature_y"],
+                                           p["flags"], R0, C0, K, 2)
+    assert R1 is R0 and C1 is C0 and X1 is Xn
+    assert "Bundle adjustment failed: Residuals are not finite in the initial point." in capsys.readouterr().out
+    cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
+    _, _, rep = core.ba_lm(cams0, Xn, p["cam_idx"], p["pt_idx"], p["obs"], K, max_iterations=20)
+    assert rep["status"] == 6 and rep["iterations"] == 0 and not np.isfinite(rep["cost0"])
 
 
 def _spd(n, seed, cond=1e4):
@@ -922,6 +933,27 @@ def test_ba_sweep_pinhole_matches_general_k(core, monkeypatch):
     c0, x0, r0 = core.ba_lm(*args, max_iterations=30)
     assert (r1["iterations"], r1["accepted"], r1["status"]) == (r0["iterations"], r0["accepted"], r0["status"])
     assert abs(r1["cost"] - r0["cost"]) <= 1e-9 * r0["cost"]
+
+
+@pytest.mark.parametrize("shape", ["cfg4", "cfg5", "many"])
+def test_ba_device_plan_equals_host_plan(core, monkeypatch, shape):
+    """The Schur sweep plan built on the device at create (the chunk
+    statistics, the per-chunk pair counts and the (chunk, spec) slot / pair
+    lists from the uploaded COO) is the host planner's plan (SFM_PLAN_HOST=1)
+    byte for byte: the same digest over every plan array, the lists read back
+    from the device in both cases.  "many": 356 cameras, long rows split over
+    several specs."""
+    p = syn.ba_problem_cfg(shape, dense=False) if shape != "many" else syn.ba_problem(356, 2000, 3, seed=11,
+                                                                                     dense=False)
+    cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
+    monkeypatch.setenv("SFM_PLAN_DIGEST", "1")
+    dig = {}
+    for host in ("0", "1"):
+        monkeypatch.setenv("SFM_PLAN_HOST", host)
+        prob = core.BAProblem(cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K)
+        dig[host] = prob.plan_digest()
+        prob.close()
+    assert dig["0"] != 0 and dig["0"] == dig["1"], dig
 
 
 def test_ba_sweep_split_and_gjr_fold_paths(core, monkeypatch):
