@@ -1055,9 +1055,16 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     double *slab_out;
     const bool sub = sp.S > 0 && (int)blockIdx.x >= sp.nfull;
     if (!sub) {
-        const int loc = blockIdx.x / NXCD;
-        w = loc % nspec;
-        r = (loc / nspec) * NXCD + (int)(blockIdx.x % NXCD);
+        if (nrange >= NXCD) {  // range r on XCD r % 8 (round-robin dispatch)
+            const int loc = blockIdx.x / NXCD;
+            w = loc % nspec;
+            r = (loc / nspec) * NXCD + (int)(blockIdx.x % NXCD);
+        } else {  // 1, 2 or 4 ranges: range r on the XCDs x with x % nrange == r
+            const int x = blockIdx.x % NXCD;
+            w = (int)(blockIdx.x / NXCD) * (NXCD / nrange) + x / nrange;
+            r = x % nrange;
+            if (w >= nspec) return;  // whole workgroup
+        }
         if (r >= nrange) return;  // whole workgroup
         q0 = rchunk[r];
         q1 = rchunk[r + 1];
@@ -3087,8 +3094,31 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     // chunk staged, ~7 us) and the end-of-range reduction, so fewer, longer
     // workgroups win even with a partial last pass over the CUs (cfg5, 100
     // specs: 16 ranges 0.539 ms, 8 ranges 0.505 ms; cfg4: 0.145 -> 0.161 ms at 16)
-    const int nr_dflt = 8;
-    P.nrange = std::max(NXCD, env_int("SFM_SWEEP_RANGES", nr_dflt) / NXCD * NXCD);
+    // Round 5: a rank's shard (1/N of the points) keeps 8 ranges only while
+    // its work fills the dispatch rounds; a small shard takes 4, 2 or 1 range
+    // (every range then spans 8 / nrange XCDs): fewer, longer workgroups in
+    // one round instead of four short rounds of mostly prologue and
+    // reduction.  Model per candidate: rounds x (13.3 us fixed + 4.7 ns per
+    // pair / workgroups), calibrated on cfg5's measured sweep (800
+    // workgroups, 95 us each); rounds fractional for 8 (the dispatch tail is
+    // split) and whole below.  cfg4 / cfg5 whole: 8; cfg5 points over 4 or 8
+    // ranks: 2.  SFM_SWEEP_RANGES overrides (a multiple of 8, or 1, 2, 4).
+    {
+        const double pairs = (double)std::accumulate(cnt.begin(), cnt.end(), int64_t(0)) - (double)no;
+        int best = NXCD;
+        double tbest = 1e300;
+        for (int nr : {8, 4, 2, 1}) {
+            const double wgs = (double)P.nspec * nr;
+            const double rounds = nr >= NXCD ? std::max(1.0, wgs / ncu) : std::ceil(wgs / ncu);
+            const double t = rounds * (13.3 + pairs * 4.7e-3 / wgs);
+            if (t < tbest * 0.97) {  // a smaller count only for a clear win
+                tbest = t;
+                best = nr;
+            }
+        }
+        const int e = env_int("SFM_SWEEP_RANGES", 0);
+        P.nrange = e >= NXCD ? e / NXCD * NXCD : (e == 1 || e == 2 || e == 4) ? e : best;
+    }
     // chunks as large as the LDS allows (every chunk boundary is a barrier
     // and an imbalance point): from the 16-bit cap down, scaled by the
     // overshoot until the largest (chunk, spec) fits
@@ -4197,8 +4227,9 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
     SFM_HIP(hipGetLastError());
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_PREP + 1], s));
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SCHUR], s));
-    const int nsweep = p->sw_split.S ? p->sw_split.nfull + NXCD * p->sw_split.nsplit * p->sw_split.S
-                                     : NXCD * p->sw_nspec * ceil_div(p->sw_nrange, NXCD);
+    const int nsweep = p->sw_split.S       ? p->sw_split.nfull + NXCD * p->sw_split.nsplit * p->sw_split.S
+                       : p->sw_nrange < NXCD ? NXCD * ceil_div(p->sw_nspec, NXCD / p->sw_nrange)
+                                             : NXCD * p->sw_nspec * ceil_div(p->sw_nrange, NXCD);
     const bool fused = p->cl_fused && p->ndiag_items;  // + the camera blocks (after an accepted step)
     auto sweep_k = p->sw_pinhole ? k_schur_sweep<1, true> : k_schur_sweep<1>;
     hipLaunchKernelGGL(sweep_k, dim3(nsweep + (fused ? p->cl_fused_wg : 0)), dim3(SW_THREADS),
