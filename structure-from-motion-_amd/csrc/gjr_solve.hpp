@@ -121,7 +121,7 @@ struct Smem {
     double Dm[TL][TL + 1];   // the diagonal tile into the chain's rows; L_r rows after it
     double Li[TL][TL + 1];   // L_r^-1 (row-major)
     double bv[TL], yv[TL];
-    double T2[4][64];        // A_r,r-2 after step r - 3, handed from its U wave to W0
+    double T2[4][64];        // A_r,r-2 after step r - 4, handed from its U wave to W0
     int pready[RING], pdone[RING], gready[RING], gdone[RING];
     int lready, t2ready, abort_, last;
     int *err, *bad;
@@ -532,8 +532,12 @@ __device__ __forceinline__ bool w0_ring_g(Smem &S, int p, int r, const d4 &g, in
 // pivots (P_{r-2} -> owner r), and pivot r - 1's record (published by owner
 // r - 1 for everyone else) is never waited for here.  Owner r publishes R_r
 // (for owner r + 1) right after its step-(r-2) updates, long before owner
-// r + 1's own critical step.  A_r,r-2 (for G_r of step r - 2) comes from its
-// U wave after step r - 3 (S.T2), so the step's G pieces need no holder.
+// r + 1's own critical step.  A_r,r-2 comes from its U wave after step
+// r - 4 (S.T2) and W0 applies step r - 3 to it itself (with owner r - 2's
+// G granules, published between that owner's two chains), so G_r of step
+// r - 2 is formed the moment P_{r-2} arrives and no U wave, bulk flag or
+// LDS ring sits on the critical path; the G pieces of steps r - 2 and r - 1
+// (for the U waves) go out behind P_r.
 __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, int r, int lane, double lambda) {
     const int nT = a.nT, li = lane & 15;
     d4 Tm = r > 0 ? load_tile(a, lambda, r, r - 1, lane) : zero4();
@@ -551,26 +555,24 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
     // the critical record P_{r-2} is polled in both copies when owner r - 2
     // shares this XCD's L2 (scalar: decided once)
     const bool crit_l2 = __builtin_amdgcn_readfirstlane(r >= 2 && xcd_of_row(r - 2, nT) == xcd_of_row(r, nT)) != 0;
-    d4 gc = zero4();  // G_r of step r - 1: its bulk copy goes out after the pivot
+    d4 gc = zero4();  // G_r of step r - 1
     if (r == 1) {     // no step before: pivot 0 recomputed from the system, then pivot 1
         double rw[16], y0;
         d4 l0;
         chain_tile(a, S, 0, lane, Rd, bm, rw, l0, y0);
         gc = mfma4(zero4(), l0, Tm);
+        put4(rs.G, gsoff(a, 0, 1), a.tag, gc, lane);  // W0 of owner 3 (its A_3,1 at step 0)
+        put_bulk(rs.Gd, gdoff(a, 0, 1), gc, lane);
         Td = mfma4(Td, -gc, gc);
         b -= gy(gc, y0, lane);
         pivot(a, rs, S, r, lane, Td, b);
+        flag_bulk(a, 0, 1);
+        if (!w0_ring_g(S, 0, 1, gc, lane)) return false;
     }
+    d4 T2 = zero4();  // A_r,r-2: from its U wave after step r - 4, updated here at step r - 3
     for (int p = 0; p < nT; ++p) {
         const int s = p & (RING - 1);
-        if (p == r - 1 || (p == r && r > 0)) {
-            if (p == r) {  // G_r of step r - 1: the bulk copy and the ring piece, off the critical path
-                put_bulk(rs.Gd, gdoff(a, r - 1, r), gc, lane);
-                flag_bulk(a, r - 1, r);
-                if (!w0_ring_g(S, r - 1, r, gc, lane)) return false;
-            }
-            continue;
-        }
+        if (p == r - 1 || (p == r && r > 0)) continue;  // done at the critical step
         if (p == r) {  // owner 0
             pivot(a, rs, S, r, lane, Td, b);
             continue;
@@ -584,11 +586,11 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
                 Rm = d4{dec(v[0][0]), dec(v[0][1]), dec(v[0][2]), dec(v[0][3])};
                 Rd = d4{dec(v[0][4]), dec(v[0][5]), dec(v[0][6]), dec(v[0][7])};
                 bm = dec(v[0][8]);
-            }
-            if (!lds_wait(&S.t2ready, 1, S)) return false;
-            d4 T2;
+            } else {  // owner 2: A_2,0 straight from its U wave's prologue
+                if (!lds_wait(&S.t2ready, 1, S)) return false;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) T2[e] = S.T2[e][lane];
+                for (int e = 0; e < 4; ++e) T2[e] = S.T2[e][lane];
+            }
             u32x4 v[1][PPAIRS];
             if (crit_l2) {
                 if (!poll_p2(rs.P, p * PBYTES, (nT + p) * PBYTES, a.tag, v[0], lane, S)) return false;
@@ -617,16 +619,21 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
                 put_pair(rs.R, ro, 8, a.tag, b, lane);
             }
             put_bulk(rs.Gd, gdoff(a, p, r), g0, lane);  // flagged after the chain (its stores have drained)
-            if (!w0_ring_g(S, p, r, g0, lane)) return false;
             // pivot r - 1, as owner r - 1 runs it
             double rw[16], y1;
             d4 l1;
             chain_tile(a, S, r - 1, lane, Rd, bm, rw, l1, y1);
             flag_bulk(a, p, r);
             gc = mfma4(zero4(), l1, Tm);  // G_r of step r - 1
+            put4(rs.G, gsoff(a, r - 1, r), a.tag, gc, lane);  // W0 of owner r + 2 (its A_r+2,r at step r - 1)
+            put_bulk(rs.Gd, gdoff(a, r - 1, r), gc, lane);
             Td = mfma4(Td, -gc, gc);
             b -= gy(gc, y1, lane);
             pivot(a, rs, S, r, lane, Td, b);
+            flag_bulk(a, r - 1, r);  // behind P_r's stores: off the critical path
+            // the ring pieces of steps r - 2 and r - 1 (the U waves only count
+            // them: no tile of theirs is live there)
+            if (!w0_ring_g(S, r - 2, r, g0, lane) || !w0_ring_g(S, r - 1, r, gc, lane)) return false;
             continue;
         }
         // an ordinary step: P_p, and for the rows of the lower triangle the
@@ -647,14 +654,21 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
         for (int e = 0; e < 4; ++e) S.PL[s][e][lane] = lv[e];
         lds_release();
         lds_set(&S.pready[s], p + 1);
-        d4 gm = zero4();
-        if (p < r) {
-            const int soff[1] = {gsoff(a, p, r - 1)};
-            const bool need[1] = {true};
-            u32x4 w[1][GPAIRS];
-            if (!sweep<1, GPAIRS>(rs.G, soff, need, a.tag, w, lane, S)) return false;
+        d4 gm = zero4(), gmm = zero4();
+        if (p < r) {  // G_{r-1} of the step; at step r - 3 also G_{r-2} (for A_r,r-2)
+            const bool t2 = p == r - 3;
+            const int soff[2] = {gsoff(a, p, r - 1), t2 ? gsoff(a, p, r - 2) : 0};
+            const bool need[2] = {true, t2};
+            u32x4 w[2][GPAIRS];
+            if (!sweep<2, GPAIRS>(rs.G, soff, need, a.tag, w, lane, S)) return false;
             stamp(a, p, DBG_GREM);
             gm = dec4(w[0]);
+            gmm = dec4(w[1]);
+            if (t2) {
+                if (!lds_wait(&S.t2ready, 1, S)) return false;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) T2[e] = S.T2[e][lane];
+            }
         }
         if (!lds_wait(&S.gready[s], p + 1, S)) return false;
         stamp(a, p, DBG_GRDY);
@@ -664,9 +678,10 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
         lds_release();
         lds_add(&S.gdone[s], 1);
         b -= gy(g, yl, lane);
-        if (p < r) {  // A_rr and A_r,r-1
+        if (p < r) {  // A_rr and A_r,r-1 (and A_r,r-2 at step r - 3)
             Td = mfma4(Td, -g, g);
             Tm = mfma4(Tm, -gm, g);
+            if (p == r - 3) T2 = mfma4(T2, -gmm, g);
         }
     }
     // x_r = L_r^-T (L_r^-1 b_r)
@@ -751,8 +766,10 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
             if (k >= TR) tset(k, v);
         }
     }
-    // A_r,r-2 after step r - 3 goes to W0 (its pivots' critical step r - 2
-    // forms G_r from it): from its wave, after that step's update
+    // A_r,r-2 after step r - 4 goes to W0 (it applies step r - 3 itself with
+    // owner r - 2's granules, and forms G_r of step r - 2 the moment P_{r-2}
+    // arrives): from its wave, after that step's update (owners 2 and 3:
+    // after the prologue)
     const int k2 = (r - 2) / NUW;
     const bool hand2 = r >= 2 && (r - 2) % NUW == w;
     auto hand_t2 = [&]() {
@@ -765,7 +782,7 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
         lds_release();
         lds_set(&S.t2ready, 1);
     };
-    if (hand2 && r == 2) hand_t2();  // no step before
+    if (hand2 && r <= 3) hand_t2();  // no step r - 4
     for (int p = 0; p < nT; ++p) {
         const int s = p & (RING - 1);
         if (p == r) {  // the import: A_rj^T = G_j L_r^T for j > r (G_j of step r from owner j)
@@ -806,7 +823,8 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
                 flag_bulk(a, p, r);
             }
         }
-        const int hi = r > p ? r - 1 : nT;  // live tiles j in (p, hi); W0 holds r - 1 and r
+        // live tiles j in (p, hi): W0 holds r - 1 and r, and r - 2 from step r - 3 on
+        const int hi = r > p ? (p == r - 3 ? r - 2 : r - 1) : nT;
         if (!lds_wait(&S.gready[s], p + 1, S)) return false;
         d4 g;
 #pragma unroll
@@ -815,7 +833,7 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
         lds_add(&S.gdone[s], 1);
         if (!wait_bulk<TPW>(a, p, w, p, hi, lane, S)) return false;
         bulk_update<TPW, false>(a, rs, p, w, p, hi, g, lane, tget, tset);
-        if (hand2 && p == r - 3) hand_t2();
+        if (hand2 && p == r - 4) hand_t2();
         if (w == 0) stamp(a, p, DBG_UDONE);
     }
     return true;
