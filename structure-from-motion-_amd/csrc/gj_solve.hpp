@@ -294,8 +294,15 @@ __device__ __forceinline__ void gj_steps(double (&r)[16], double (&p)[16], doubl
                                          bool &nonpos, std::integer_sequence<int, K...>) {
     (gj_step<K>(r, p, dinv, n, nonpos), ...);
 }
+struct NoHook {
+    __device__ void operator()() const {}
+};
+// hook() runs between pivots 7 and 8 (behind a compiler memory barrier, so
+// its stores stay there): work whose operands are still in the MFMA pipe
+// when the chain starts (gjr's step-(r-2) publications) goes out mid-chain
+template <class Hook = NoHook>
 __device__ __forceinline__ void gj_factor16(double (&r)[16], double (&p)[16], double (&dinv)[16], int lane,
-                                            int *bad) {
+                                            int *bad, Hook &&hook = Hook{}) {
     NewtonState n;
     n.c15 = 1.5;
     asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf" : "=v"(n.d) : "v"(r[0]));
@@ -305,7 +312,11 @@ __device__ __forceinline__ void gj_factor16(double (&r)[16], double (&p)[16], do
     gj_newton<0>(n);
     gj_newton<1>(n);
     gj_newton<2>(n);
-    gj_steps(r, p, dinv, n, nonpos, std::make_integer_sequence<int, 16>{});
+    gj_steps(r, p, dinv, n, nonpos, std::integer_sequence<int, 0, 1, 2, 3, 4, 5, 6, 7>{});
+    asm volatile("" ::: "memory");
+    hook();
+    asm volatile("" ::: "memory");
+    gj_steps(r, p, dinv, n, nonpos, std::integer_sequence<int, 8, 9, 10, 11, 12, 13, 14, 15>{});
     if (lane == 0 && nonpos) *bad = 1;
 }
 

@@ -460,8 +460,9 @@ __device__ __forceinline__ int p_uses(int p, int r) {
 // L^-1 fragment (lv) and y(l & 15) (yr) on every lane; L^-1 also in S.Li.
 // The same code for an owner's own pivot and for the pivot of the row above
 // it that the owner recomputes (same inputs, same bits).
+template <class Hook = gj::NoHook>
 __device__ __forceinline__ void chain_tile(const Args &a, Smem &S, int p, int lane, const d4 &Td, double b,
-                                           double (&rw)[16], d4 &lv, double &yr) {
+                                           double (&rw)[16], d4 &lv, double &yr, Hook &&hook = Hook{}) {
     const int li = lane & 15, grp = lane >> 4;
 #pragma unroll
     for (int e = 0; e < 4; ++e) S.Dm[li][grp + 4 * e] = Td[e];  // symmetric: column li = row li
@@ -473,7 +474,7 @@ __device__ __forceinline__ void chain_tile(const Args &a, Smem &S, int p, int la
 #pragma unroll
     for (int j = 0; j < 16; ++j) pw[j] = grp == 0 ? (lane == 0 ? S.bv[j] : 0.0) : (grp == 1 && j == li ? 1.0 : 0.0);
     stamp(a, p, DBG_CHAIN0);
-    gj::gj_factor16(rw, pw, dinv, lane, a.bad);
+    gj::gj_factor16(rw, pw, dinv, lane, a.bad, hook);
     stamp(a, p, DBG_CHAIN1);
     if (grp == 1)
 #pragma unroll
@@ -602,27 +603,36 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
             stamp(a, p, DBG_PIN);
             const d4 lv = dec4(v[0]);
             const double yl = dec(v[0][4]);
-            const d4 g1 = mfma4(zero4(), lv, Rm);  // G_{r-1} of step r - 2 (owner r - 1 forms the same)
-            const d4 g0 = mfma4(zero4(), lv, T2);  // G_r of step r - 2
+            // the critical MFMAs first (the pipe takes one wave's MFMAs in
+            // order, 64 cycles each): G_{r-1} of step r - 2 (owner r - 1 forms
+            // the same) and A_r-1,r-1 for pivot r - 1's chain
+            const d4 g1 = mfma4(zero4(), lv, Rm);
             Rd = mfma4(Rd, -g1, g1);
-            bm -= gy(g1, yl, lane);
-            put4(rs.G, gsoff(a, p, r), a.tag, g0, lane);  // W0 of owner r + 1 (its step r - 2)
-            stamp(a, p, DBG_GCRIT);
+            // then G_r of step r - 2 and this row's updates: they run in the
+            // MFMA pipe under the chain's VALU work, and their publications
+            // (owner r + 1's G granule and row state R_r, the U waves' bulk
+            // G) go out mid-chain, when the products are long done
+            const d4 g0 = mfma4(zero4(), lv, T2);
             Tm = mfma4(Tm, -g1, g0);
             Td = mfma4(Td, -g0, g0);
-            b -= gy(g0, yl, lane);
-            if (r + 1 < nT) {  // R_r for owner r + 1
-                const int ro = r * RBYTES;
-                put4(rs.R, ro, a.tag, Tm, lane);
+            bm -= gy(g1, yl, lane);
+            stamp(a, p, DBG_GCRIT);
+            auto publish = [&]() {
+                put4(rs.G, gsoff(a, p, r), a.tag, g0, lane);  // W0 of owner r + 1 (its step r - 2)
+                b -= gy(g0, yl, lane);
+                if (r + 1 < nT) {  // R_r for owner r + 1
+                    const int ro = r * RBYTES;
+                    put4(rs.R, ro, a.tag, Tm, lane);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) put_pair(rs.R, ro, 4 + e, a.tag, Td[e], lane);
-                put_pair(rs.R, ro, 8, a.tag, b, lane);
-            }
-            put_bulk(rs.Gd, gdoff(a, p, r), g0, lane);  // flagged after the chain (its stores have drained)
+                    for (int e = 0; e < 4; ++e) put_pair(rs.R, ro, 4 + e, a.tag, Td[e], lane);
+                    put_pair(rs.R, ro, 8, a.tag, b, lane);
+                }
+                put_bulk(rs.Gd, gdoff(a, p, r), g0, lane);  // flagged after the chain (its stores have drained)
+            };
             // pivot r - 1, as owner r - 1 runs it
             double rw[16], y1;
             d4 l1;
-            chain_tile(a, S, r - 1, lane, Rd, bm, rw, l1, y1);
+            chain_tile(a, S, r - 1, lane, Rd, bm, rw, l1, y1, publish);
             flag_bulk(a, p, r);
             gc = mfma4(zero4(), l1, Tm);  // G_r of step r - 1
             put4(rs.G, gsoff(a, r - 1, r), a.tag, gc, lane);  // W0 of owner r + 2 (its A_r+2,r at step r - 1)
