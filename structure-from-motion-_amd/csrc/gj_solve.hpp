@@ -271,9 +271,13 @@ __device__ __forceinline__ void gj_rest(double (&r)[16], double (&p)[16], Newton
         if constexpr (U <= 5) gj_newton<2>(n);
     }
 }
-template <int K>
+struct NoHook {
+    template <class KC>
+    __device__ void operator()(KC) const {}
+};
+template <int K, class Hook = NoHook>
 __device__ __forceinline__ void gj_step(double (&r)[16], double (&p)[16], double (&dinv)[16], NewtonState &n,
-                                        bool &nonpos) {
+                                        bool &nonpos, Hook &hook) {
     const double g = n.g0;
     asm volatile("v_mul_f64 %0, %0, %2\n\tv_mul_f64 %1, %1, %2" : "+v"(r[K]), "+v"(p[K]) : "v"(g));
     dinv[K] = g;
@@ -288,18 +292,17 @@ __device__ __forceinline__ void gj_step(double (&r)[16], double (&p)[16], double
         nonpos |= !(n.d > 0.0);
         gj_rest<K, 0>(r, p, n);
     }
+    hook(std::integral_constant<int, K>{});
 }
-template <int... K>
+template <class Hook, int... K>
 __device__ __forceinline__ void gj_steps(double (&r)[16], double (&p)[16], double (&dinv)[16], NewtonState &n,
-                                         bool &nonpos, std::integer_sequence<int, K...>) {
-    (gj_step<K>(r, p, dinv, n, nonpos), ...);
+                                         bool &nonpos, Hook &hook, std::integer_sequence<int, K...>) {
+    (gj_step<K>(r, p, dinv, n, nonpos, hook), ...);
 }
-struct NoHook {
-    __device__ void operator()() const {}
-};
-// hook() runs between pivots 7 and 8 (behind a compiler memory barrier, so
-// its stores stay there): work whose operands are still in the MFMA pipe
-// when the chain starts (gjr's step-(r-2) publications) goes out mid-chain
+// hook(integral_constant<K>) runs after pivot K: gjr's critical step spreads
+// its own-row MFMAs over the chain (one wave's MFMAs enter the pipe one per
+// 64 cycles, so issued together they stalled the chain's start) and
+// publishes their results mid-chain
 template <class Hook = NoHook>
 __device__ __forceinline__ void gj_factor16(double (&r)[16], double (&p)[16], double (&dinv)[16], int lane,
                                             int *bad, Hook &&hook = Hook{}) {
@@ -312,11 +315,7 @@ __device__ __forceinline__ void gj_factor16(double (&r)[16], double (&p)[16], do
     gj_newton<0>(n);
     gj_newton<1>(n);
     gj_newton<2>(n);
-    gj_steps(r, p, dinv, n, nonpos, std::integer_sequence<int, 0, 1, 2, 3, 4, 5, 6, 7>{});
-    asm volatile("" ::: "memory");
-    hook();
-    asm volatile("" ::: "memory");
-    gj_steps(r, p, dinv, n, nonpos, std::integer_sequence<int, 8, 9, 10, 11, 12, 13, 14, 15>{});
+    gj_steps(r, p, dinv, n, nonpos, hook, std::make_integer_sequence<int, 16>{});
     if (lane == 0 && nonpos) *bad = 1;
 }
 

@@ -608,31 +608,45 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
             // the same) and A_r-1,r-1 for pivot r - 1's chain
             const d4 g1 = mfma4(zero4(), lv, Rm);
             Rd = mfma4(Rd, -g1, g1);
-            // then G_r of step r - 2 and this row's updates: they run in the
-            // MFMA pipe under the chain's VALU work, and their publications
-            // (owner r + 1's G granule and row state R_r, the U waves' bulk
-            // G) go out mid-chain, when the products are long done
-            const d4 g0 = mfma4(zero4(), lv, T2);
-            Tm = mfma4(Tm, -g1, g0);
-            Td = mfma4(Td, -g0, g0);
             bm -= gy(g1, yl, lane);
             stamp(a, p, DBG_GCRIT);
-            auto publish = [&]() {
-                put4(rs.G, gsoff(a, p, r), a.tag, g0, lane);  // W0 of owner r + 1 (its step r - 2)
-                b -= gy(g0, yl, lane);
-                if (r + 1 < nT) {  // R_r for owner r + 1
-                    const int ro = r * RBYTES;
-                    put4(rs.R, ro, a.tag, Tm, lane);
+            // then G_r of step r - 2 and this row's updates, two MFMAs after
+            // each of the chain's first six pivots (the pipe takes one of this
+            // wave's MFMAs per 64 cycles: issued together they held the
+            // chain's start ~0.3 us), the same accumulation order as mfma4;
+            // their publications (owner r + 1's G granule and row state R_r,
+            // the U waves' bulk G) go out after pivot 7
+            d4 g0 = zero4();
+            auto step_work = [&](auto kc) {
+                constexpr int K = decltype(kc)::value;
+                if constexpr (K < 6) {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) put_pair(rs.R, ro, 4 + e, a.tag, Td[e], lane);
-                    put_pair(rs.R, ro, 8, a.tag, b, lane);
+                    for (int u = 2 * K; u < 2 * K + 2; ++u) {
+                        const int q = u & 3;
+                        if (u < 4) g0 = __builtin_amdgcn_mfma_f64_16x16x4f64(lv[q], T2[q], g0, 0, 0, 0);
+                        else if (u < 8) Tm = __builtin_amdgcn_mfma_f64_16x16x4f64(-g1[q], g0[q], Tm, 0, 0, 0);
+                        else Td = __builtin_amdgcn_mfma_f64_16x16x4f64(-g0[q], g0[q], Td, 0, 0, 0);
+                    }
                 }
-                put_bulk(rs.Gd, gdoff(a, p, r), g0, lane);  // flagged after the chain (its stores have drained)
+                if constexpr (K == 7) {
+                    asm volatile("" ::: "memory");
+                    put4(rs.G, gsoff(a, p, r), a.tag, g0, lane);  // W0 of owner r + 1 (its step r - 2)
+                    b -= gy(g0, yl, lane);
+                    if (r + 1 < nT) {  // R_r for owner r + 1
+                        const int ro = r * RBYTES;
+                        put4(rs.R, ro, a.tag, Tm, lane);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) put_pair(rs.R, ro, 4 + e, a.tag, Td[e], lane);
+                        put_pair(rs.R, ro, 8, a.tag, b, lane);
+                    }
+                    put_bulk(rs.Gd, gdoff(a, p, r), g0, lane);  // flagged after the chain (its stores have drained)
+                    asm volatile("" ::: "memory");
+                }
             };
             // pivot r - 1, as owner r - 1 runs it
             double rw[16], y1;
             d4 l1;
-            chain_tile(a, S, r - 1, lane, Rd, bm, rw, l1, y1, publish);
+            chain_tile(a, S, r - 1, lane, Rd, bm, rw, l1, y1, step_work);
             flag_bulk(a, p, r);
             gc = mfma4(zero4(), l1, Tm);  // G_r of step r - 1
             put4(rs.G, gsoff(a, r - 1, r), a.tag, gc, lane);  // W0 of owner r + 2 (its A_r+2,r at step r - 1)
