@@ -40,6 +40,7 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <cmath>
@@ -2726,6 +2727,65 @@ __device__ __forceinline__ int32_t lower_bound_d(const int32_t *__restrict__ a, 
     return lo;
 }
 
+// create's CSR on the device (round 5; SFM_PLAN_HOST=1 keeps the host's):
+// pstart from the point-sorted observations, cstart from the camera-sorted
+// keys of the stable radix sort (csr_sort.hip: the permutation, in point
+// order within a camera), the co-observation block counts (a <= b within a
+// point, the diagonal included) with the duplicate-camera check
+namespace sfm {
+int cam_major_sort(void *temp, size_t &temp_bytes, const int32_t *cam, uint32_t *keys_out, int32_t *perm_out,
+                   int64_t no, int32_t nc, hipStream_t s);
+}
+__global__ void __launch_bounds__(256) k_csr_pstart(int64_t no, int64_t np_, const int32_t *__restrict__ pt,
+                                                    int32_t *__restrict__ pstart) {
+    const int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (o > no) return;
+    if (o == no) {  // the points after the last observed one
+        for (int64_t i = no ? (int64_t)pt[no - 1] + 1 : 0; i <= np_; ++i) pstart[i] = (int32_t)no;
+        return;
+    }
+    const int64_t lo = o == 0 ? 0 : (int64_t)pt[o - 1] + 1;
+    for (int64_t i = lo; i <= pt[o]; ++i) pstart[i] = (int32_t)o;
+}
+__global__ void __launch_bounds__(256) k_csr_cstart(int64_t no, int32_t nc, const uint32_t *__restrict__ keys,
+                                                    int32_t *__restrict__ cstart) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c > nc) return;
+    int64_t lo = 0, hi = no;
+    while (lo < hi) {
+        const int64_t m = lo + ((hi - lo) >> 1);
+        if (keys[m] < (uint32_t)c) lo = m + 1;
+        else hi = m;
+    }
+    cstart[c] = (int32_t)lo;
+}
+__global__ void __launch_bounds__(256) k_csr_cnt(int64_t no, int32_t nc, const int32_t *__restrict__ pstart,
+                                                 const int32_t *__restrict__ pt, const int32_t *__restrict__ cam,
+                                                 uint32_t *__restrict__ cnt, uint32_t *__restrict__ dup) {
+    const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (a >= no) return;
+    const int ca = cam[a];
+    const int32_t e = pstart[pt[a] + 1];
+    atomicAdd(&cnt[(size_t)ca * nc + ca], 1u);
+    for (int32_t b = (int32_t)a + 1; b < e; ++b) {
+        const int cb = cam[b];
+        if (cb == ca) atomicOr(dup, 1u);
+        atomicAdd(&cnt[ca < cb ? (size_t)ca * nc + cb : (size_t)cb * nc + ca], 1u);
+    }
+}
+
+// the pinned staging buffer of create's uploads (grown, never shrunk; one
+// user at a time)
+struct PinnedStage {
+    std::mutex mu;
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+static PinnedStage &pinned_stage() {
+    static PinnedStage *st = new PinnedStage();
+    return *st;
+}
+
 // chunk q of a trial cut: the observations of points [cut[q], cend[q]); its
 // largest staged-slot count (the observations of one spec's cameras) and
 // pair count (off-diagonal pairs of one spec's blocks) -> out[2q], out[2q+1]
@@ -2961,6 +3021,68 @@ static int64_t sweep_alloc(const std::vector<std::vector<uint16_t>> &P, const st
     return std::min(fp, fg);
 }
 
+// Host threads kept across calls (round 5): create fans out ~15 times (the
+// validation, the CSR, the counts, the planner's passes), and spawning and
+// joining 16 threads cost ~0.3-0.5 ms each time.  Workers park on a
+// condition variable; one job at a time -- a concurrent caller (in-process
+// ranks creating their problems together) spawns its own threads instead.
+class HostPool {
+  public:
+    static HostPool &get() {
+        static HostPool *p = new HostPool();  // never destroyed: workers may outlive static teardown
+        return *p;
+    }
+    // f(t) for t in [0, nt), the caller taking t = nt - 1; false if busy
+    template <class F>
+    bool try_run(int nt, F &&f) {
+        std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
+        if (!busy.owns_lock()) return false;
+        const int nw = nt - 1;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            while ((int)workers_.size() < nw) {
+                const int id = (int)workers_.size();
+                workers_.emplace_back([this, id] { loop(id); });
+                workers_.back().detach();
+            }
+            job_ = [&f](int t) { f(t); };
+            njob_ = nw;
+            remaining_ = nw;
+            ++gen_;
+        }
+        cv_.notify_all();
+        f(nt - 1);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [this] { return remaining_ == 0; });
+        job_ = nullptr;
+        return true;
+    }
+
+  private:
+    void loop(int id) {
+        uint64_t seen = 0;
+        for (;;) {
+            std::function<void(int)> job;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (id >= njob_) continue;
+                job = job_;
+            }
+            job(id);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--remaining_ == 0) done_cv_.notify_all();
+        }
+    }
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_, done_cv_;
+    std::vector<std::thread> workers_;
+    std::function<void(int)> job_;
+    uint64_t gen_ = 0;
+    int njob_ = 0, remaining_ = 0;
+};
+
 // the planner's independent loops (per chunk, per spec) on host threads:
 // f(i) for i in [0, n), contiguous blocks, up to 16 threads (SFM_PLAN_THREADS)
 template <class F>
@@ -2974,11 +3096,12 @@ static void par_for(int64_t n, F &&f) {
         for (int64_t i = 0; i < n; ++i) f(i);
         return;
     }
+    auto block = [&](int t) {
+        for (int64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) f(i);
+    };
+    if (HostPool::get().try_run(nt, block)) return;
     std::vector<std::thread> th;
-    for (int t = 0; t < nt; ++t)
-        th.emplace_back([&, t] {
-            for (int64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) f(i);
-        });
+    for (int t = 0; t < nt; ++t) th.emplace_back(block, t);
     for (auto &x : th) x.join();
 }
 
@@ -3618,9 +3741,19 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     PhaseTimer ctm_;
     auto ctick = [&](const char *what) { ctm_.tick(what); };
     const bool ctm = ctm_.on;
-    for (int64_t o = 0; o < no; ++o) {
-        SFM_CHECK_ARG(cam[o] >= 0 && cam[o] < nc && pt[o] >= 0 && pt[o] < np_, "observation index out of range");
-        SFM_CHECK_ARG(o == 0 || pt[o] >= pt[o - 1], "observations must be point-major (sorted by point)");
+    {  // host threads over contiguous observation ranges
+        constexpr int NB = 16;
+        int bad[NB] = {0};
+        par_for(NB, [&](int64_t t) {
+            for (int64_t o = no * t / NB; o < no * (t + 1) / NB; ++o) {
+                if (!(cam[o] >= 0 && cam[o] < nc && pt[o] >= 0 && pt[o] < np_)) bad[t] |= 1;
+                if (!(o == 0 || pt[o] >= pt[o - 1])) bad[t] |= 2;
+            }
+        });
+        int any = 0;
+        for (int t = 0; t < NB; ++t) any |= bad[t];
+        SFM_CHECK_ARG(!(any & 1), "observation index out of range");
+        SFM_CHECK_ARG(!(any & 2), "observations must be point-major (sorted by point)");
     }
     ctick("validate");
     auto p = std::make_unique<sfm_ba_problem>();
@@ -3639,57 +3772,20 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
                     env_int("SFM_SWEEP_PINHOLE", 1) != 0;
     p->cams0.assign(cams, cams + 6 * (size_t)nc);
     p->pts0.assign(pts, pts + 3 * (size_t)np_);
-    // point CSR
-    std::vector<int32_t> pstart(np_ + 1, 0);
-    for (int64_t o = 0; o < no; ++o) pstart[pt[o] + 1]++;
-    for (int64_t i = 0; i < np_; ++i) pstart[i + 1] += pstart[i];
-    // camera-major observation list (stable: point order within a camera)
-    std::vector<int32_t> cstart(nc + 1, 0), cam_obs(no);
-    for (int64_t o = 0; o < no; ++o) cstart[cam[o] + 1]++;
-    for (int c = 0; c < nc; ++c) cstart[c + 1] += cstart[c];
-    {
-        std::vector<int32_t> fill(cstart.begin(), cstart.end() - 1);
-        for (int64_t o = 0; o < no; ++o) cam_obs[fill[cam[o]]++] = (int32_t)o;
-    }
-    ctick("csr");
-    for (int64_t i = 0; i < np_; ++i)
-        for (int32_t a = pstart[i]; a < pstart[i + 1]; ++a)
-            for (int32_t b = a + 1; b < pstart[i + 1]; ++b)
-                SFM_CHECK_ARG(cam[a] != cam[b], "a point is observed twice by the same camera");
-    ctick("dupcheck");
-    // co-observation counts per camera block (static sparsity of the reduced camera system)
-    // (host threads over point blocks, integer sums)
+    // SFM_CREATE_PLAN_ONLY=1 (measurement, tools/create_probe.py): the host
+    // planner alone, without a device; returns 1 and no problem.
+    // SFM_PLAN_HOST=1: the host's CSR, counts and planner passes (the device
+    // ones must produce the same plan: the digest test)
+    const bool plan_only = env_int("SFM_CREATE_PLAN_ONLY", 0) != 0;
+    const bool host_plan = plan_only || env_int("SFM_PLAN_HOST", 0) != 0;
+    const bool want_digest = ctm || env_int("SFM_PLAN_DIGEST", 0) != 0;
+    int rc;
+    // point CSR (pstart), camera-major permutation (cam_obs, stable: point
+    // order within a camera) and its offsets (cstart), co-observation counts
+    // per camera block (cnt, the static sparsity of the reduced camera system)
+    std::vector<int32_t> pstart(np_ + 1), cstart(nc + 1, 0), cam_obs;
     std::vector<int64_t> cnt((size_t)nc * nc, 0);
     int64_t tot = 0;
-    {
-        constexpr int NB = 16;
-        std::vector<std::vector<int64_t>> part(NB);
-        std::vector<int64_t> tpart(NB, 0);
-        par_for(NB, [&](int64_t t) {
-            auto &c = part[t];
-            c.assign((size_t)nc * nc, 0);
-            int64_t n = 0;
-            for (int64_t i = np_ * t / NB; i < np_ * (t + 1) / NB; ++i)
-                for (int32_t a = pstart[i]; a < pstart[i + 1]; ++a)
-                    for (int32_t b = a; b < pstart[i + 1]; ++b) {
-                        int ci = cam[a], cj = cam[b];
-                        if (ci > cj) std::swap(ci, cj);
-                        c[(size_t)ci * nc + cj]++;
-                        ++n;
-                    }
-            tpart[t] = n;
-        });
-        for (int t = 0; t < NB; ++t) {
-            tot += tpart[t];
-            for (size_t k = 0; k < cnt.size(); ++k) cnt[k] += part[t][k];
-        }
-    }
-    p->npairs = tot;
-    ctick("blockcounts");
-    // SFM_CREATE_PLAN_ONLY=1 (measurement, tools/create_probe.py): the host
-    // planner alone, without a device; returns 1 and no problem
-    const bool plan_only = env_int("SFM_CREATE_PLAN_ONLY", 0) != 0;
-    int rc;
     if (!plan_only) {
         SFM_HIP(hipSetDevice(device));
         (void)hipGetLastError();  // launches below are checked with hipGetLastError: start clean
@@ -3697,26 +3793,167 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         for (auto &e : p->ev) SFM_HIP(hipEventCreate(&e));
         for (auto &e : p->ev_it) SFM_HIP(hipEventCreate(&e));
         ctick("stream");
-        // the COO up first: the device planner reads it
         if ((rc = p->alloc(p->d_cam, no)) || (rc = p->alloc(p->d_pt, no)) || (rc = p->alloc(p->d_pstart, np_ + 1)) ||
             (rc = p->alloc(p->d_obs, no)) || (rc = p->alloc(p->d_cm_pt, no)) || (rc = p->alloc(p->d_cm_obs, no)) ||
             (rc = p->alloc(p->d_cstart, nc + 1)))
             return rc;
-        hipStream_t s = p->stream;
-        if (no) {
-            SFM_HIP(hipMemcpyAsync(p->d_cam, cam, no * 4, hipMemcpyHostToDevice, s));
-            SFM_HIP(hipMemcpyAsync(p->d_pt, pt, no * 4, hipMemcpyHostToDevice, s));
-            SFM_HIP(hipMemcpyAsync(p->d_obs, obs, no * 16, hipMemcpyHostToDevice, s));
+    }
+    // the COO up through a pinned staging buffer kept across calls (host
+    // threads copy into it, the copy engine takes it from there: a pageable
+    // hipMemcpy of the 96 MB at cfg5 ran ~10 GB/s); a concurrent create
+    // finding it busy uploads from pageable memory
+    std::unique_lock<std::mutex> stage_lk;
+    if (!plan_only && no) {
+        PinnedStage &st = pinned_stage();
+        stage_lk = std::unique_lock<std::mutex>(st.mu, std::try_to_lock);
+        const size_t need = (size_t)no * 24;
+        bool staged = false;
+        if (stage_lk.owns_lock()) {
+            if (st.bytes < need) {
+                if (st.p) (void)hipHostFree(st.p);
+                st.p = nullptr;
+                st.bytes = 0;
+                if (hipHostMalloc(&st.p, need, hipHostMallocDefault) == hipSuccess) st.bytes = need;
+                else (void)hipGetLastError();
+            }
+            if (st.bytes >= need) {
+                char *h = static_cast<char *>(st.p);
+                constexpr int NB = 16;
+                par_for(3 * NB, [&](int64_t k) {
+                    const int a = (int)(k / NB), t = (int)(k % NB);
+                    const size_t w = a == 2 ? 16 : 4, n0 = no * t / NB, n1 = no * (t + 1) / NB;
+                    const char *src = a == 0 ? (const char *)cam : a == 1 ? (const char *)pt : (const char *)obs;
+                    char *dst = h + (a == 0 ? 0 : a == 1 ? (size_t)no * 4 : (size_t)no * 8);
+                    std::memcpy(dst + n0 * w, src + n0 * w, (n1 - n0) * w);
+                });
+                SFM_HIP(hipMemcpyAsync(p->d_cam, h, no * 4, hipMemcpyHostToDevice, p->stream));
+                SFM_HIP(hipMemcpyAsync(p->d_pt, h + (size_t)no * 4, no * 4, hipMemcpyHostToDevice, p->stream));
+                SFM_HIP(hipMemcpyAsync(p->d_obs, h + (size_t)no * 8, no * 16, hipMemcpyHostToDevice, p->stream));
+                staged = true;
+            }
         }
-        SFM_HIP(hipMemcpyAsync(p->d_pstart, pstart.data(), pstart.size() * 4, hipMemcpyHostToDevice, s));
-        if (no) {  // the permutation up, the camera-major copies gathered on the device
-            SFM_HIP(hipMemcpyAsync(p->d_cm_pt, cam_obs.data(), no * 4, hipMemcpyHostToDevice, s));
-            hipLaunchKernelGGL(k_gather_cam_major, dim3((unsigned)ceil_div(no, 256)), dim3(256), 0, s, no, p->d_pt,
-                               p->d_obs, p->d_cm_pt, p->d_cm_obs);
+        if (!staged) {
+            if (stage_lk.owns_lock()) stage_lk.unlock();
+            SFM_HIP(hipMemcpyAsync(p->d_cam, cam, no * 4, hipMemcpyHostToDevice, p->stream));
+            SFM_HIP(hipMemcpyAsync(p->d_pt, pt, no * 4, hipMemcpyHostToDevice, p->stream));
+            SFM_HIP(hipMemcpyAsync(p->d_obs, obs, no * 16, hipMemcpyHostToDevice, p->stream));
+        }
+        ctick("up:obs");
+    }
+    if (host_plan) {  // host threads
+        constexpr int NBC = 16;
+        par_for(NBC, [&](int64_t t) {  // the observations are sorted by point
+            const int64_t o0 = no * t / NBC, o1 = no * (t + 1) / NBC;
+            for (int64_t o = o0; o < o1; ++o) {
+                const int64_t lo = o == 0 ? 0 : (int64_t)pt[o - 1] + 1;
+                for (int64_t i = lo; i <= pt[o]; ++i) pstart[i] = (int32_t)o;
+            }
+            if (t == NBC - 1)
+                for (int64_t i = no ? (int64_t)pt[no - 1] + 1 : 0; i <= np_; ++i) pstart[i] = (int32_t)no;
+        });
+        // a counting sort: per-range camera counts, offsets in (camera, range)
+        // order, every range scatters its own observations in order
+        cam_obs.resize(no);
+        std::vector<int32_t> rc_cnt((size_t)NBC * nc, 0);
+        par_for(NBC, [&](int64_t t) {
+            int32_t *hh = rc_cnt.data() + (size_t)t * nc;
+            for (int64_t o = no * t / NBC; o < no * (t + 1) / NBC; ++o) hh[cam[o]]++;
+        });
+        int32_t run = 0;
+        for (int c = 0; c < nc; ++c) {
+            cstart[c] = run;
+            for (int t = 0; t < NBC; ++t) {
+                const int32_t v = rc_cnt[(size_t)t * nc + c];
+                rc_cnt[(size_t)t * nc + c] = run;
+                run += v;
+            }
+        }
+        cstart[nc] = run;
+        par_for(NBC, [&](int64_t t) {
+            int32_t *f = rc_cnt.data() + (size_t)t * nc;
+            for (int64_t o = no * t / NBC; o < no * (t + 1) / NBC; ++o) cam_obs[f[cam[o]]++] = (int32_t)o;
+        });
+        ctick("csr");
+        int dup[NBC] = {0};
+        std::vector<std::vector<int64_t>> part(NBC);
+        std::vector<int64_t> tpart(NBC, 0);
+        par_for(NBC, [&](int64_t t) {
+            auto &c = part[t];
+            c.assign((size_t)nc * nc, 0);
+            int64_t n = 0;
+            for (int64_t i = np_ * t / NBC; i < np_ * (t + 1) / NBC; ++i)
+                for (int32_t a = pstart[i]; a < pstart[i + 1]; ++a)
+                    for (int32_t b = a; b < pstart[i + 1]; ++b) {
+                        int ci = cam[a], cj = cam[b];
+                        if (b > a && ci == cj) dup[t] = 1;
+                        if (ci > cj) std::swap(ci, cj);
+                        c[(size_t)ci * nc + cj]++;
+                        ++n;
+                    }
+            tpart[t] = n;
+        });
+        int any = 0;
+        for (int t = 0; t < NBC; ++t) {
+            any |= dup[t];
+            tot += tpart[t];
+            for (size_t k = 0; k < cnt.size(); ++k) cnt[k] += part[t][k];
+        }
+        SFM_CHECK_ARG(!any, "a point is observed twice by the same camera");
+        ctick("blockcounts");
+        if (!plan_only) {
+            hipStream_t s = p->stream;
+            SFM_HIP(hipMemcpyAsync(p->d_pstart, pstart.data(), pstart.size() * 4, hipMemcpyHostToDevice, s));
+            if (no) SFM_HIP(hipMemcpyAsync(p->d_cm_pt, cam_obs.data(), no * 4, hipMemcpyHostToDevice, s));
+            SFM_HIP(hipMemcpyAsync(p->d_cstart, cstart.data(), cstart.size() * 4, hipMemcpyHostToDevice, s));
+        }
+    } else {  // on the device: the point CSR from the sorted point indices, a
+              // stable radix sort of the camera indices for the permutation,
+              // and the block counts with the duplicate check in one pass
+        hipStream_t s = p->stream;
+        DevPlan tmp;
+        uint32_t *keys = tmp.scratch<uint32_t>(no), *cnt32 = tmp.scratch<uint32_t>((size_t)nc * nc + 1);
+        size_t tb = 0;
+        if ((rc = sfm::cam_major_sort(nullptr, tb, p->d_cam, keys, p->d_cm_pt, no, nc, s))) return rc;
+        void *temp = tmp.scratch<char>(tb);
+        if (tmp.err) return tmp.err;
+        SFM_HIP(hipMemsetAsync(cnt32, 0, ((size_t)nc * nc + 1) * 4, s));
+        hipLaunchKernelGGL(k_csr_pstart, dim3((unsigned)ceil_div(no + 1, 256)), dim3(256), 0, s, no, np_, p->d_pt,
+                           p->d_pstart);
+        SFM_HIP(hipGetLastError());
+        if (no && (rc = sfm::cam_major_sort(temp, tb, p->d_cam, keys, p->d_cm_pt, no, nc, s))) return rc;
+        hipLaunchKernelGGL(k_csr_cstart, dim3((unsigned)ceil_div(nc + 1, 256)), dim3(256), 0, s, no, nc, keys,
+                           p->d_cstart);
+        SFM_HIP(hipGetLastError());
+        if (no) {
+            hipLaunchKernelGGL(k_csr_cnt, dim3((unsigned)ceil_div(no, 256)), dim3(256), 0, s, no, nc, p->d_pstart,
+                               p->d_pt, p->d_cam, cnt32, cnt32 + (size_t)nc * nc);
             SFM_HIP(hipGetLastError());
         }
-        SFM_HIP(hipMemcpyAsync(p->d_cstart, cstart.data(), cstart.size() * 4, hipMemcpyHostToDevice, s));
-        ctick("up:obs");
+        std::vector<uint32_t> c32((size_t)nc * nc + 1);
+        SFM_HIP(hipMemcpyAsync(pstart.data(), p->d_pstart, pstart.size() * 4, hipMemcpyDeviceToHost, s));
+        SFM_HIP(hipMemcpyAsync(cstart.data(), p->d_cstart, cstart.size() * 4, hipMemcpyDeviceToHost, s));
+        SFM_HIP(hipMemcpyAsync(c32.data(), cnt32, c32.size() * 4, hipMemcpyDeviceToHost, s));
+        if (want_digest) {
+            cam_obs.resize(no);
+            if (no) SFM_HIP(hipMemcpyAsync(cam_obs.data(), p->d_cm_pt, no * 4, hipMemcpyDeviceToHost, s));
+        }
+        SFM_HIP(hipStreamSynchronize(s));
+        SFM_CHECK_ARG(c32[(size_t)nc * nc] == 0, "a point is observed twice by the same camera");
+        for (size_t k = 0; k + 1 < c32.size(); ++k) {
+            cnt[k] = c32[k];
+            tot += c32[k];
+        }
+        ctick("csr+blockcounts (device)");
+    }
+    if (stage_lk.owns_lock()) {  // the staged copies are done once the stream has passed them
+        SFM_HIP(hipStreamSynchronize(p->stream));
+        stage_lk.unlock();
+    }
+    p->npairs = tot;
+    if (!plan_only && no) {  // the camera-major copies gathered on the device (cm_pt: permutation -> points)
+        hipLaunchKernelGGL(k_gather_cam_major, dim3((unsigned)ceil_div(no, 256)), dim3(256), 0, p->stream, no,
+                           p->d_pt, p->d_obs, p->d_cm_pt, p->d_cm_obs);
+        SFM_HIP(hipGetLastError());
     }
     SweepPlan sw;
     // lanes per pair slot: 1 (a lane forms a pair's whole 6x6 block, H once;
@@ -3728,7 +3965,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     // the plan's passes over the observation pairs on the device
     // (SFM_PLAN_HOST=1: the host planner's threads, the same plan)
     DevPlan dev;
-    const bool dev_plan = !plan_only && env_int("SFM_PLAN_HOST", 0) == 0;
+    const bool dev_plan = !host_plan;
     if (dev_plan) {
         dev.s = p->stream;
         dev.pstart = p->d_pstart;
@@ -3809,7 +4046,6 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         mixv(csa.items), mixv(csa.blocks), mixv(csa.wg_first), mixv(cfu.items), mixv(cfu.blocks), mixv(cfu.wg_first);
         return h;
     };
-    const bool want_digest = ctm || env_int("SFM_PLAN_DIGEST", 0) != 0;
     if (plan_only) {
         if (want_digest)
             std::fprintf(stderr, "[create] plan digest %016llx\n",

@@ -87,7 +87,8 @@ struct Args {
     long long *dbg;   // diagnostics (nullable): [grid][nT + 1][16] s_memrealtime stamps
 };
 
-enum { DBG_PIN = 0, DBG_GCRIT, DBG_CHAIN0, DBG_CHAIN1, DBG_PPUB, DBG_GHOLD, DBG_UDONE, DBG_GREM, DBG_PLW, DBG_GRDY, DBG_HPRDY };
+enum { DBG_PIN = 0, DBG_GCRIT, DBG_CHAIN0, DBG_CHAIN1, DBG_PPUB, DBG_GHOLD, DBG_UDONE, DBG_GREM, DBG_PLW, DBG_GRDY, DBG_HPRDY,
+       DBG_RIN, DBG_T2, DBG_READY, DBG_GC };
 enum { DBG_START = 0, DBG_PROLOGUE, DBG_W0END, DBG_ARRIVED };
 // row tile of workgroup b: consecutive rows on one XCD (workgroups are
 // dealt round-robin over the 8 XCDs, b % 8), so the critical hop P_{r-1} ->
@@ -579,6 +580,7 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
             continue;
         }
         if (p == r - 2) {  // the critical step: pivots r - 1 and r
+            stamp(a, p, DBG_READY);
             if (r >= 3) {  // R_{r-1}: A_r-1,r-2, A_r-1,r-1, b_r-1 after step r - 3
                 const int soff[1] = {(r - 1) * RBYTES};
                 const bool need[1] = {true};
@@ -587,6 +589,7 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
                 Rm = d4{dec(v[0][0]), dec(v[0][1]), dec(v[0][2]), dec(v[0][3])};
                 Rd = d4{dec(v[0][4]), dec(v[0][5]), dec(v[0][6]), dec(v[0][7])};
                 bm = dec(v[0][8]);
+                stamp(a, p, DBG_RIN);
             } else {  // owner 2: A_2,0 straight from its U wave's prologue
                 if (!lds_wait(&S.t2ready, 1, S)) return false;
 #pragma unroll
@@ -649,6 +652,7 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
             chain_tile(a, S, r - 1, lane, Rd, bm, rw, l1, y1, step_work);
             flag_bulk(a, p, r);
             gc = mfma4(zero4(), l1, Tm);  // G_r of step r - 1
+            stamp(a, r - 1, DBG_GC);
             put4(rs.G, gsoff(a, r - 1, r), a.tag, gc, lane);  // W0 of owner r + 2 (its A_r+2,r at step r - 1)
             put_bulk(rs.Gd, gdoff(a, r - 1, r), gc, lane);
             Td = mfma4(Td, -gc, gc);
@@ -692,6 +696,7 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
                 if (!lds_wait(&S.t2ready, 1, S)) return false;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) T2[e] = S.T2[e][lane];
+                stamp(a, p, DBG_T2);
             }
         }
         if (!lds_wait(&S.gready[s], p + 1, S)) return false;
