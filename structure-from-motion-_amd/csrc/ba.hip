@@ -2333,15 +2333,14 @@ static GjrPlan gjr_plan(int nT, int ncu) {
 }
 // granule records (zeroed once; tags only grow) and the err / arrival words
 struct GjrBufs {
-    gjr::u64 *P = nullptr, *G = nullptr, *R = nullptr;
+    gjr::u64 *P = nullptr, *G = nullptr;
     double *Gd = nullptr;
     unsigned *Gf = nullptr;
     int *err = nullptr;
     unsigned *arrive = nullptr;
     static size_t words(int nT) {
         const size_t t = (size_t)nT * nT;
-        return ((size_t)2 * nT * gjr::PBYTES + t * gjr::GBYTES + t * gjr::GDBYTES + (size_t)nT * gjr::RBYTES) / 8 +
-               (t + 1) / 2;
+        return ((size_t)2 * nT * gjr::PBYTES + t * gjr::GBYTES + t * gjr::GDBYTES) / 8 + (t + 1) / 2;
     }
     static constexpr size_t ints = 64;
     void carve(gjr::u64 *w, int *i, int nT) {
@@ -2349,8 +2348,7 @@ struct GjrBufs {
         P = w;
         G = P + (size_t)2 * nT * gjr::PBYTES / 8;
         Gd = reinterpret_cast<double *>(G + t * gjr::GBYTES / 8);
-        R = reinterpret_cast<gjr::u64 *>(Gd + t * gjr::GDBYTES / 8);
-        Gf = reinterpret_cast<unsigned *>(R + (size_t)nT * gjr::RBYTES / 8);
+        Gf = reinterpret_cast<unsigned *>(Gd + t * gjr::GDBYTES / 8);
         err = i;
         arrive = reinterpret_cast<unsigned *>(i + 32);
     }
@@ -2368,7 +2366,6 @@ static int launch_gjr(const GjrPlan &g, int32_t ns, const double *payload, const
     a.P = b.P;
     a.G = b.G;
     a.Gd = b.Gd;
-    a.R = b.R;
     a.Gf = b.Gf;
     a.tag = tag;
     a.x = x;

@@ -271,13 +271,9 @@ __device__ __forceinline__ void gj_rest(double (&r)[16], double (&p)[16], Newton
         if constexpr (U <= 5) gj_newton<2>(n);
     }
 }
-struct NoHook {
-    template <class KC>
-    __device__ void operator()(KC) const {}
-};
-template <int K, class Hook = NoHook>
+template <int K>
 __device__ __forceinline__ void gj_step(double (&r)[16], double (&p)[16], double (&dinv)[16], NewtonState &n,
-                                        bool &nonpos, Hook &hook) {
+                                        bool &nonpos) {
     const double g = n.g0;
     asm volatile("v_mul_f64 %0, %0, %2\n\tv_mul_f64 %1, %1, %2" : "+v"(r[K]), "+v"(p[K]) : "v"(g));
     dinv[K] = g;
@@ -292,20 +288,14 @@ __device__ __forceinline__ void gj_step(double (&r)[16], double (&p)[16], double
         nonpos |= !(n.d > 0.0);
         gj_rest<K, 0>(r, p, n);
     }
-    hook(std::integral_constant<int, K>{});
 }
-template <class Hook, int... K>
+template <int... K>
 __device__ __forceinline__ void gj_steps(double (&r)[16], double (&p)[16], double (&dinv)[16], NewtonState &n,
-                                         bool &nonpos, Hook &hook, std::integer_sequence<int, K...>) {
-    (gj_step<K>(r, p, dinv, n, nonpos, hook), ...);
+                                         bool &nonpos, std::integer_sequence<int, K...>) {
+    (gj_step<K>(r, p, dinv, n, nonpos), ...);
 }
-// hook(integral_constant<K>) runs after pivot K: gjr's critical step spreads
-// its own-row MFMAs over the chain (one wave's MFMAs enter the pipe one per
-// 64 cycles, so issued together they stalled the chain's start) and
-// publishes their results mid-chain
-template <class Hook = NoHook>
 __device__ __forceinline__ void gj_factor16(double (&r)[16], double (&p)[16], double (&dinv)[16], int lane,
-                                            int *bad, Hook &&hook = Hook{}) {
+                                            int *bad) {
     NewtonState n;
     n.c15 = 1.5;
     asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf" : "=v"(n.d) : "v"(r[0]));
@@ -315,7 +305,7 @@ __device__ __forceinline__ void gj_factor16(double (&r)[16], double (&p)[16], do
     gj_newton<0>(n);
     gj_newton<1>(n);
     gj_newton<2>(n);
-    gj_steps(r, p, dinv, n, nonpos, hook, std::make_integer_sequence<int, 16>{});
+    gj_steps(r, p, dinv, n, nonpos, std::make_integer_sequence<int, 16>{});
     if (lane == 0 && nonpos) *bad = 1;
 }
 

@@ -51,9 +51,7 @@ constexpr int NTMAX = 128;       // tile rows (host checks; larger systems take 
 constexpr int RING = 4;          // LDS ring depth of the per-step pieces
 constexpr int PPAIRS = 5;        // granule pairs a lane of a pivot record: L^-1 fragment (4), y (1)
 constexpr int GPAIRS = 4;        // granule pairs a lane of a published G tile
-constexpr int RPAIRS = 9;        // granule pairs a lane of a row-state record: A_r,r-1 (4), A_rr (4), b_r (1)
 constexpr int PBYTES = PPAIRS * 64 * 16;
-constexpr int RBYTES = RPAIRS * 64 * 16;
 constexpr int GBYTES = GPAIRS * 64 * 16;
 constexpr int GDBYTES = 2 * 64 * 16;  // a G tile untagged: two 16-byte rows of 64 lanes (the bulk copy)
 constexpr int NB = 6;                 // bulk G tiles a U wave has in flight
@@ -74,7 +72,6 @@ struct Args {
     const double *lam;
     const int *gate;
     u64 *P;         // [2][nT] pivot records of PBYTES: write-through copy, then the L2-local copy
-    u64 *R;         // [nT] row-state records of RBYTES: owner r's A_r,r-1, A_rr, b_r after step r - 2
     u64 *G;         // [nT][nT] G_r of step p at (p, r), GBYTES each (granules: W0 of owner r + 1)
     double *Gd;     // [nT][nT] the same untagged, GDBYTES each (the U waves' bulk updates) ...
     unsigned *Gf;   // [nT][nT] ... published by a flag (= tag) behind the drained stores
@@ -87,8 +84,7 @@ struct Args {
     long long *dbg;   // diagnostics (nullable): [grid][nT + 1][16] s_memrealtime stamps
 };
 
-enum { DBG_PIN = 0, DBG_GCRIT, DBG_CHAIN0, DBG_CHAIN1, DBG_PPUB, DBG_GHOLD, DBG_UDONE, DBG_GREM, DBG_PLW, DBG_GRDY, DBG_HPRDY,
-       DBG_RIN, DBG_T2, DBG_READY, DBG_GC };
+enum { DBG_PIN = 0, DBG_GCRIT, DBG_CHAIN0, DBG_CHAIN1, DBG_PPUB, DBG_GHOLD, DBG_UDONE, DBG_GREM, DBG_PLW, DBG_GRDY, DBG_HPRDY };
 enum { DBG_START = 0, DBG_PROLOGUE, DBG_W0END, DBG_ARRIVED };
 // row tile of workgroup b: consecutive rows on one XCD (workgroups are
 // dealt round-robin over the 8 XCDs, b % 8), so the critical hop P_{r-1} ->
@@ -102,17 +98,9 @@ __device__ __forceinline__ int xcd_of_row(int r, int nT) {
     const int q = nT / NXCD_, m = nT % NXCD_;
     return r < m * (q + 1) ? r / (q + 1) : m + (r - m * (q + 1)) / max(q, 1);
 }
-// s_memrealtime stamps (tools/gjr_timeline.py) exist only in a build with
-// -DGJR_STAMPS=1: their address arithmetic, hoisted out of the loops, pushed
-// the kernel past its 256 VGPRs
-#ifndef GJR_STAMPS
-#define GJR_STAMPS 0
-#endif
 __device__ __forceinline__ void stamp(const Args &a, int p, int slot) {
-    if constexpr (GJR_STAMPS) {
-        if (a.dbg && (threadIdx.x & 63) == 0)
-            a.dbg[((int64_t)row_of(blockIdx.x, a.nT) * (a.nT + 1) + p) * 16 + slot] = __builtin_amdgcn_s_memrealtime();
-    }
+    if (a.dbg && (threadIdx.x & 63) == 0)
+        a.dbg[((int64_t)row_of(blockIdx.x, a.nT) * (a.nT + 1) + p) * 16 + slot] = __builtin_amdgcn_s_memrealtime();
 }
 
 struct Smem {
@@ -122,9 +110,8 @@ struct Smem {
     double Dm[TL][TL + 1];   // the diagonal tile into the chain's rows; L_r rows after it
     double Li[TL][TL + 1];   // L_r^-1 (row-major)
     double bv[TL], yv[TL];
-    double T2[4][64];        // A_r,r-2 after step r - 4, handed from its U wave to W0
     int pready[RING], pdone[RING], gready[RING], gdone[RING];
-    int lready, t2ready, abort_, last;
+    int lready, abort_, last;
     int *err, *bad;
 };
 
@@ -202,7 +189,7 @@ struct Buf {
     int bytes;
 };
 struct Rs {
-    Buf P, G, Gd, R;
+    Buf P, G, Gd;
 };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const Buf &b) {
     const u64 a = (u64)b.base;
@@ -451,32 +438,27 @@ __device__ __forceinline__ int g_uses(int p, int r) {
 __device__ __forceinline__ int p_uses(int p, int r) {
     int u = g_uses(p, r);
     if (r >= 1 && r - 1 < p && ((r - 1) & (RING - 1)) == (p & (RING - 1))) --u;
-    if (r >= 2 && r - 2 < p && ((r - 2) & (RING - 1)) == (p & (RING - 1))) --u;
     return u;
 }
 
 // ------------------------------------------------------------------- W0
-// The chain on a diagonal tile with the b row (lane 0) and the identity
-// (lanes 16..31) as panel rows -> L (rows, left in rw), y, L^-T rows: the
-// L^-1 fragment (lv) and y(l & 15) (yr) on every lane; L^-1 also in S.Li.
-// The same code for an owner's own pivot and for the pivot of the row above
-// it that the owner recomputes (same inputs, same bits).
-template <class Hook = gj::NoHook>
-__device__ __forceinline__ void chain_tile(const Args &a, Smem &S, int p, int lane, const d4 &Td, double b,
-                                           double (&rw)[16], d4 &lv, double &yr, Hook &&hook = Hook{}) {
+// The pivot: the chain on the diagonal tile with the b row (lane 0) and the
+// identity (lanes 16..31) as panel rows -> L_r (rows), y_r, L_r^-T rows.
+// Publishes P_r; leaves L_r^-1 in S.Li and the L_r fragment in S.Lf.
+__device__ __forceinline__ void pivot(const Args &a, const Rs &rs, Smem &S, int r, int lane, const d4 &Td, double b) {
     const int li = lane & 15, grp = lane >> 4;
 #pragma unroll
     for (int e = 0; e < 4; ++e) S.Dm[li][grp + 4 * e] = Td[e];  // symmetric: column li = row li
     if (lane < 16) S.bv[lane] = b;
     wave_lds();
-    double pw[16], dinv[16];
+    double rw[16], pw[16], dinv[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) rw[j] = S.Dm[li][j];
 #pragma unroll
     for (int j = 0; j < 16; ++j) pw[j] = grp == 0 ? (lane == 0 ? S.bv[j] : 0.0) : (grp == 1 && j == li ? 1.0 : 0.0);
-    stamp(a, p, DBG_CHAIN0);
-    gj::gj_factor16(rw, pw, dinv, lane, a.bad, hook);
-    stamp(a, p, DBG_CHAIN1);
+    stamp(a, r, DBG_CHAIN0);
+    gj::gj_factor16(rw, pw, dinv, lane, a.bad);
+    stamp(a, r, DBG_CHAIN1);
     if (grp == 1)
 #pragma unroll
         for (int j = 0; j < 16; ++j) S.Li[j][li] = pw[j];  // row li of L^-T = column li of L^-1
@@ -484,20 +466,11 @@ __device__ __forceinline__ void chain_tile(const Args &a, Smem &S, int p, int la
 #pragma unroll
         for (int j = 0; j < 16; ++j) S.yv[j] = pw[j];
     wave_lds();
+    d4 lv;
 #pragma unroll
     for (int e = 0; e < 4; ++e) lv[e] = S.Li[li][4 * e + grp];  // L^-1(l & 15, 4e + (l >> 4))
-    yr = S.yv[li];
-}
-
-// The owner's pivot: the chain, then P_r published; leaves L_r^-1 in S.Li
-// and the L_r fragment in S.Lf (the U waves' imports)
-__device__ __forceinline__ void pivot(const Args &a, const Rs &rs, Smem &S, int r, int lane, const d4 &Td, double b) {
-    const int li = lane & 15, grp = lane >> 4;
-    double rw[16];
-    d4 lv;
-    double yr;
-    chain_tile(a, S, r, lane, Td, b, rw, lv, yr);
-    put4<0>(rs.P, (a.nT + r) * PBYTES, a.tag, lv, lane);  // the L2-local copy first (the critical reader)
+    const double yr = S.yv[li];
+    put4<0>(rs.P, (a.nT + r) * PBYTES, a.tag, lv, lane);  // the L2-local copy first (the next owner)
     put_pair<0>(rs.P, (a.nT + r) * PBYTES, 4, a.tag, yr, lane);
     put4(rs.P, r * PBYTES, a.tag, lv, lane);
     put_pair(rs.P, r * PBYTES, 4, a.tag, yr, lane);
@@ -513,204 +486,89 @@ __device__ __forceinline__ void pivot(const Args &a, const Rs &rs, Smem &S, int 
     lds_set(&S.lready, 1);
 }
 
-// a GL ring piece written by W0 (steps r - 2 and r - 1, which have no U-wave
-// holder): every wave counts it, W0 included
-__device__ __forceinline__ bool w0_ring_g(Smem &S, int p, int r, const d4 &g, int lane) {
-    const int sc = p & (RING - 1);
-    if (!lds_wait(&S.gdone[sc], NW * g_uses(p, r), S)) return false;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) S.GL[sc][e][lane] = g[e];
-    lds_release();
-    lds_set(&S.gready[sc], p + 1);
-    lds_add(&S.gdone[sc], 1);
-    return true;
-}
-
-// W0 of owner r holds A_r,r-1 (Tm), A_rr (Td) and b_r, and runs the critical
-// path two pivots at a time: when P_{r-2} arrives it recomputes pivot r - 1
-// itself from the row-state record R_{r-1} that owner r - 1 published (its
-// A_r-1,r-2, A_r-1,r-1 and b_r-1 after step r - 3) and then runs its own
-// pivot r -- so the critical path crosses one workgroup boundary per TWO
-// pivots (P_{r-2} -> owner r), and pivot r - 1's record (published by owner
-// r - 1 for everyone else) is never waited for here.  Owner r publishes R_r
-// (for owner r + 1) right after its step-(r-2) updates, long before owner
-// r + 1's own critical step.  A_r,r-2 comes from its U wave after step
-// r - 4 (S.T2) and W0 applies step r - 3 to it itself (with owner r - 2's
-// G granules, published between that owner's two chains), so G_r of step
-// r - 2 is formed the moment P_{r-2} arrives and no U wave, bulk flag or
-// LDS ring sits on the critical path; the G pieces of steps r - 2 and r - 1
-// (for the U waves) go out behind P_r.
+// W0 of owner r: A_r,r-1 (Tm), A_rr (Td), b_r; the pivot records of every
+// step (L^-1 into the ring for the holder of A_rp, y_p for b_r)
 __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, int r, int lane, double lambda) {
     const int nT = a.nT, li = lane & 15;
     d4 Tm = r > 0 ? load_tile(a, lambda, r, r - 1, lane) : zero4();
     d4 Td = load_tile(a, lambda, r, r, lane);
     double b = assembled_b_src(a.src, a.payload, a.ns, TL * r + li);
-    // the row above before any step (owners 1 and 2 take it from the system)
-    d4 Rm = zero4(), Rd = zero4();
-    double bm = 0.0;
-    if (r == 1 || r == 2) {
-        Rm = r == 2 ? load_tile(a, lambda, r - 1, r - 2, lane) : zero4();
-        Rd = load_tile(a, lambda, r - 1, r - 1, lane);
-        bm = assembled_b_src(a.src, a.payload, a.ns, TL * (r - 1) + li);
-    }
     stamp(a, nT, DBG_PROLOGUE);
-    // the critical record P_{r-2} is polled in both copies when owner r - 2
-    // shares this XCD's L2 (scalar: decided once)
-    const bool crit_l2 = __builtin_amdgcn_readfirstlane(r >= 2 && xcd_of_row(r - 2, nT) == xcd_of_row(r, nT)) != 0;
-    d4 gc = zero4();  // G_r of step r - 1
-    if (r == 1) {     // no step before: pivot 0 recomputed from the system, then pivot 1
-        double rw[16], y0;
-        d4 l0;
-        chain_tile(a, S, 0, lane, Rd, bm, rw, l0, y0);
-        gc = mfma4(zero4(), l0, Tm);
-        put4(rs.G, gsoff(a, 0, 1), a.tag, gc, lane);  // W0 of owner 3 (its A_3,1 at step 0)
-        put_bulk(rs.Gd, gdoff(a, 0, 1), gc, lane);
-        Td = mfma4(Td, -gc, gc);
-        b -= gy(gc, y0, lane);
-        pivot(a, rs, S, r, lane, Td, b);
-        flag_bulk(a, 0, 1);
-        if (!w0_ring_g(S, 0, 1, gc, lane)) return false;
-    }
-    d4 T2 = zero4();  // A_r,r-2: from its U wave after step r - 4, updated here at step r - 3
+    d4 gc = zero4();  // G_r of the critical step: its bulk copy goes out after the pivot
     for (int p = 0; p < nT; ++p) {
         const int s = p & (RING - 1);
-        if (p == r - 1 || (p == r && r > 0)) continue;  // done at the critical step
-        if (p == r) {  // owner 0
-            pivot(a, rs, S, r, lane, Td, b);
-            continue;
-        }
-        if (p == r - 2) {  // the critical step: pivots r - 1 and r
-            stamp(a, p, DBG_READY);
-            if (r >= 3) {  // R_{r-1}: A_r-1,r-2, A_r-1,r-1, b_r-1 after step r - 3
-                const int soff[1] = {(r - 1) * RBYTES};
-                const bool need[1] = {true};
-                u32x4 v[1][RPAIRS];
-                if (!sweep<1, RPAIRS>(rs.R, soff, need, a.tag, v, lane, S)) return false;
-                Rm = d4{dec(v[0][0]), dec(v[0][1]), dec(v[0][2]), dec(v[0][3])};
-                Rd = d4{dec(v[0][4]), dec(v[0][5]), dec(v[0][6]), dec(v[0][7])};
-                bm = dec(v[0][8]);
-                stamp(a, p, DBG_RIN);
-            } else {  // owner 2: A_2,0 straight from its U wave's prologue
-                if (!lds_wait(&S.t2ready, 1, S)) return false;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) T2[e] = S.T2[e][lane];
-            }
-            u32x4 v[1][PPAIRS];
-            if (crit_l2) {
-                if (!poll_p2(rs.P, p * PBYTES, (nT + p) * PBYTES, a.tag, v[0], lane, S)) return false;
-            } else {
-                const int soff[1] = {p * PBYTES};
-                const bool need[1] = {true};
-                if (!sweep<1, PPAIRS>(rs.P, soff, need, a.tag, v, lane, S)) return false;
-            }
-            stamp(a, p, DBG_PIN);
-            const d4 lv = dec4(v[0]);
-            const double yl = dec(v[0][4]);
-            // the critical MFMAs first (the pipe takes one wave's MFMAs in
-            // order, 64 cycles each): G_{r-1} of step r - 2 (owner r - 1 forms
-            // the same) and A_r-1,r-1 for pivot r - 1's chain
-            const d4 g1 = mfma4(zero4(), lv, Rm);
-            Rd = mfma4(Rd, -g1, g1);
-            bm -= gy(g1, yl, lane);
-            stamp(a, p, DBG_GCRIT);
-            // then G_r of step r - 2 and this row's updates, two MFMAs after
-            // each of the chain's first six pivots (the pipe takes one of this
-            // wave's MFMAs per 64 cycles: issued together they held the
-            // chain's start ~0.3 us), the same accumulation order as mfma4;
-            // their publications (owner r + 1's G granule and row state R_r,
-            // the U waves' bulk G) go out after pivot 7
-            d4 g0 = zero4();
-            auto step_work = [&](auto kc) {
-                constexpr int K = decltype(kc)::value;
-                if constexpr (K < 6) {
-#pragma unroll
-                    for (int u = 2 * K; u < 2 * K + 2; ++u) {
-                        const int q = u & 3;
-                        if (u < 4) g0 = __builtin_amdgcn_mfma_f64_16x16x4f64(lv[q], T2[q], g0, 0, 0, 0);
-                        else if (u < 8) Tm = __builtin_amdgcn_mfma_f64_16x16x4f64(-g1[q], g0[q], Tm, 0, 0, 0);
-                        else Td = __builtin_amdgcn_mfma_f64_16x16x4f64(-g0[q], g0[q], Td, 0, 0, 0);
-                    }
-                }
-                if constexpr (K == 7) {
-                    asm volatile("" ::: "memory");
-                    put4(rs.G, gsoff(a, p, r), a.tag, g0, lane);  // W0 of owner r + 1 (its step r - 2)
-                    b -= gy(g0, yl, lane);
-                    if (r + 1 < nT) {  // R_r for owner r + 1
-                        const int ro = r * RBYTES;
-                        put4(rs.R, ro, a.tag, Tm, lane);
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) put_pair(rs.R, ro, 4 + e, a.tag, Td[e], lane);
-                        put_pair(rs.R, ro, 8, a.tag, b, lane);
-                    }
-                    put_bulk(rs.Gd, gdoff(a, p, r), g0, lane);  // flagged after the chain (its stores have drained)
-                    asm volatile("" ::: "memory");
-                }
-            };
-            // pivot r - 1, as owner r - 1 runs it
-            double rw[16], y1;
-            d4 l1;
-            chain_tile(a, S, r - 1, lane, Rd, bm, rw, l1, y1, step_work);
-            flag_bulk(a, p, r);
-            gc = mfma4(zero4(), l1, Tm);  // G_r of step r - 1
-            stamp(a, r - 1, DBG_GC);
-            put4(rs.G, gsoff(a, r - 1, r), a.tag, gc, lane);  // W0 of owner r + 2 (its A_r+2,r at step r - 1)
-            put_bulk(rs.Gd, gdoff(a, r - 1, r), gc, lane);
-            Td = mfma4(Td, -gc, gc);
-            b -= gy(gc, y1, lane);
-            pivot(a, rs, S, r, lane, Td, b);
-            flag_bulk(a, r - 1, r);  // behind P_r's stores: off the critical path
-            // the ring pieces of steps r - 2 and r - 1 (the U waves only count
-            // them: no tile of theirs is live there)
-            if (!w0_ring_g(S, r - 2, r, g0, lane) || !w0_ring_g(S, r - 1, r, gc, lane)) return false;
-            continue;
-        }
-        // an ordinary step: P_p, and for the rows of the lower triangle the
-        // G_{r-1} of the step (for A_r,r-1) before the holder's G_r
-        u32x4 v[1][PPAIRS];
-        {
+        double yl = 0.0;
+        d4 lv = zero4();
+        if (p != r) {
             const int soff[1] = {p * PBYTES};
             const bool need[1] = {true};
-            if (!sweep<1, PPAIRS>(rs.P, soff, need, a.tag, v, lane, S)) return false;
-        }
-        stamp(a, p, DBG_PIN);
-        const d4 lv = dec4(v[0]);
-        const double yl = dec(v[0][4]);
-        // the holder of A_rp forms G_r from L_p^-1
-        if (!lds_wait(&S.pdone[s], p_uses(p, r), S)) return false;
-        stamp(a, p, DBG_PLW);
+            u32x4 v[1][PPAIRS];
+            if (p == r - 1 && xcd_of_row(p, nT) == xcd_of_row(r, nT)) {
+                if (!poll_p2(rs.P, p * PBYTES, (nT + p) * PBYTES, a.tag, v[0], lane, S)) return false;
+            } else if (!sweep<1, PPAIRS>(rs.P, soff, need, a.tag, v, lane, S)) {
+                return false;
+            }
+            stamp(a, p, DBG_PIN);
+            lv = dec4(v[0]);
+            yl = dec(v[0][4]);
+            if (p != r - 1) {  // the holder of A_rp forms G_r from L_p^-1
+                if (!lds_wait(&S.pdone[s], p_uses(p, r), S)) return false;
+                stamp(a, p, DBG_PLW);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) S.PL[s][e][lane] = lv[e];
-        lds_release();
-        lds_set(&S.pready[s], p + 1);
-        d4 gm = zero4(), gmm = zero4();
-        if (p < r) {  // G_{r-1} of the step; at step r - 3 also G_{r-2} (for A_r,r-2)
-            const bool t2 = p == r - 3;
-            const int soff[2] = {gsoff(a, p, r - 1), t2 ? gsoff(a, p, r - 2) : 0};
-            const bool need[2] = {true, t2};
-            u32x4 w[2][GPAIRS];
-            if (!sweep<2, GPAIRS>(rs.G, soff, need, a.tag, w, lane, S)) return false;
-            stamp(a, p, DBG_GREM);
-            gm = dec4(w[0]);
-            gmm = dec4(w[1]);
-            if (t2) {
-                if (!lds_wait(&S.t2ready, 1, S)) return false;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) T2[e] = S.T2[e][lane];
-                stamp(a, p, DBG_T2);
+                for (int e = 0; e < 4; ++e) S.PL[s][e][lane] = lv[e];
+                lds_release();
+                lds_set(&S.pready[s], p + 1);
             }
         }
-        if (!lds_wait(&S.gready[s], p + 1, S)) return false;
-        stamp(a, p, DBG_GRDY);
-        d4 g;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) g[e] = S.GL[s][e][lane];
-        lds_release();
-        lds_add(&S.gdone[s], 1);
-        b -= gy(g, yl, lane);
-        if (p < r) {  // A_rr and A_r,r-1 (and A_r,r-2 at step r - 3)
+        if (p == r - 1) {  // the critical step: G_r, its publication, A_rr, then the pivot
+            const d4 g = mfma4(zero4(), lv, Tm);
+            put4(rs.G, gsoff(a, p, r), a.tag, g, lane);  // owner r + 1 waits for it first
+            gc = g;
+            stamp(a, p, DBG_GCRIT);
             Td = mfma4(Td, -g, g);
-            Tm = mfma4(Tm, -gm, g);
-            if (p == r - 3) T2 = mfma4(T2, -gmm, g);
+            b -= gy(g, yl, lane);
+        } else if (p == r) {
+            pivot(a, rs, S, r, lane, Td, b);
+            if (r > 0) {
+                put_bulk(rs.Gd, gdoff(a, r - 1, r), gc, lane);
+                flag_bulk(a, r - 1, r);
+                // the ring piece of the critical step r - 1, after the pivot
+                // record is out: no U wave has a live tile at step r - 1, they
+                // only count the slot, so it leaves the critical path
+                const int sc = (r - 1) & (RING - 1);
+                if (!lds_wait(&S.gdone[sc], NW * g_uses(r - 1, r), S)) return false;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) S.GL[sc][e][lane] = gc[e];
+                lds_release();
+                lds_set(&S.gready[sc], r);
+                lds_add(&S.gdone[sc], 1);
+            }
+        } else {
+            // G_{r-1} of this step (for A_r,r-1) first: owner r - 1 publishes
+            // it as soon as it has P_p, so its round trip overlaps the holder's
+            // work on G_r instead of following it (this wave reaches the next
+            // step's poll, the critical one at p = r - 2, one round trip sooner)
+            d4 gm = zero4();
+            if (p < r) {
+                const int soff[1] = {gsoff(a, p, r - 1)};
+                const bool need[1] = {true};
+                u32x4 v[1][GPAIRS];
+                if (!sweep<1, GPAIRS>(rs.G, soff, need, a.tag, v, lane, S)) return false;
+                stamp(a, p, DBG_GREM);
+                gm = dec4(v[0]);
+            }
+            if (!lds_wait(&S.gready[s], p + 1, S)) return false;
+            stamp(a, p, DBG_GRDY);
+            d4 g;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) g[e] = S.GL[s][e][lane];
+            lds_release();
+            lds_add(&S.gdone[s], 1);
+            b -= gy(g, yl, lane);
+            if (p < r) {  // A_rr and A_r,r-1
+                Td = mfma4(Td, -g, g);
+                Tm = mfma4(Tm, -gm, g);
+            }
         }
     }
     // x_r = L_r^-T (L_r^-1 b_r)
@@ -795,23 +653,6 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
             if (k >= TR) tset(k, v);
         }
     }
-    // A_r,r-2 after step r - 4 goes to W0 (it applies step r - 3 itself with
-    // owner r - 2's granules, and forms G_r of step r - 2 the moment P_{r-2}
-    // arrives): from its wave, after that step's update (owners 2 and 3:
-    // after the prologue)
-    const int k2 = (r - 2) / NUW;
-    const bool hand2 = r >= 2 && (r - 2) % NUW == w;
-    auto hand_t2 = [&]() {
-        d4 t = zero4();
-#pragma unroll
-        for (int k = 0; k < TPW; ++k)
-            if (k == k2) t = tget(k);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) S.T2[e][lane] = t[e];
-        lds_release();
-        lds_set(&S.t2ready, 1);
-    };
-    if (hand2 && r <= 3) hand_t2();  // no step r - 4
     for (int p = 0; p < nT; ++p) {
         const int s = p & (RING - 1);
         if (p == r) {  // the import: A_rj^T = G_j L_r^T for j > r (G_j of step r from owner j)
@@ -827,7 +668,7 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
             bulk_update<TPW, true>(a, rs, p, w, r, nT, lf, lane, tget, tset);
             continue;
         }
-        if (p % NUW == w && p != r - 1 && p != r - 2) {  // holder of A_rp: G_r = A_rp L_p^-T
+        if (p % NUW == w && p != r - 1) {  // holder of A_rp: G_r = A_rp L_p^-T
             if (!lds_wait(&S.pready[s], p + 1, S)) return false;
             stamp(a, p, DBG_HPRDY);
             d4 lv;
@@ -852,8 +693,7 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
                 flag_bulk(a, p, r);
             }
         }
-        // live tiles j in (p, hi): W0 holds r - 1 and r, and r - 2 from step r - 3 on
-        const int hi = r > p ? (p == r - 3 ? r - 2 : r - 1) : nT;
+        const int hi = r > p ? r - 1 : nT;  // live tiles j in (p, hi); W0 holds r - 1 and r
         if (!lds_wait(&S.gready[s], p + 1, S)) return false;
         d4 g;
 #pragma unroll
@@ -862,7 +702,6 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
         lds_add(&S.gdone[s], 1);
         if (!wait_bulk<TPW>(a, p, w, p, hi, lane, S)) return false;
         bulk_update<TPW, false>(a, rs, p, w, p, hi, g, lane, tget, tset);
-        if (hand2 && p == r - 4) hand_t2();
         if (w == 0) stamp(a, p, DBG_UDONE);
     }
     return true;
@@ -879,7 +718,7 @@ __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
     const double lambda = *a.lam;
     if (threadIdx.x < RING) S.pready[threadIdx.x] = S.pdone[threadIdx.x] = S.gready[threadIdx.x] = S.gdone[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
-        S.lready = S.t2ready = S.abort_ = S.last = 0;
+        S.lready = S.abort_ = S.last = 0;
         S.err = a.err;
         S.bad = a.bad;
     }
@@ -887,7 +726,6 @@ __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
     rs.P = Buf{a.P, 2 * a.nT * PBYTES};
     rs.G = Buf{a.G, a.nT * a.nT * GBYTES};
     rs.Gd = Buf{a.Gd, a.nT * a.nT * GDBYTES};
-    rs.R = Buf{a.R, a.nT * RBYTES};
     __syncthreads();
     const int wu = __builtin_amdgcn_readfirstlane(wave);  // provably uniform: scalar record offsets
     if (wu == 0) w0_loop(a, rs, S, r, lane, lambda);
