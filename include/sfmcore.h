@@ -84,6 +84,13 @@ int sfm_ransac_f8(const double *x1, const double *x2, int64_t N, const int32_t *
 int sfm_ransac_f8_pyrandom(const double *x1, const double *x2, int64_t N, uint32_t *st, int64_t H,
                            double thr, int32_t *counts_out, int64_t *best_iter, double *F_best,
                            uint8_t *best_mask, int32_t *samples_out, int device);
+/* GetInliersRANSAC's whole call (GetInliersRANSAC.py:53-106) as the drop-in
+ * needs it: sfm_ransac_f8_pyrandom with the winner's inlier positions
+ * (ascending) in split[0, *n_inliers) and the outliers' positions in
+ * split[*n_inliers, N) (split: N entries) in place of the mask;
+ * *n_inliers = 0 when *best_iter is -1. */
+int sfm_ransac_f8_dropin(const double *x1, const double *x2, int64_t N, uint32_t *st, int64_t H, double thr,
+                         int64_t *best_iter, double *F_best, int64_t *split, int64_t *n_inliers, int device);
 
 /* ---------------------------------------------------------------------
  * Homography (GetHomographyInliers.py)
@@ -155,9 +162,11 @@ int sfm_matching_free(void *handle);
  *   where the reference's indexing raises IndexError); a row r of the flag matrix starts at flags + r * flag_row_bytes (dtype
  *   0 f64, 1 f32, 2 i64, 3 i32, 4 u8/bool; "== 1" in that dtype), of the
  *   coordinate matrices at fx / fy + r * xy_row_bytes (f64); n_threads
- *   host threads (0 = up to 16).  Returns a store of n_obs observations in
- *   np.where's order (point-major, camera ascending).
+ *   row jobs on the library's host threads (0 = its default).  Returns a
+ *   store of n_obs observations in np.where's order (point-major, camera
+ *   ascending), kept by the library for the next scan once freed.
  * sfm_dense_obs_read: copies (camera, point i, (x, y)).
+ * sfm_ba_lm_dense (below) solves from the store without these copies.
  * ------------------------------------------------------------------- */
 int sfm_dense_obs_scan(const void *flags, int32_t dtype, int64_t flag_row_bytes, int64_t n_matrix_rows,
                        const int64_t *rows, int64_t n_rows, int32_t n_cams, const double *fx, const double *fy,
@@ -228,6 +237,14 @@ typedef struct {
 int sfm_ba_lm(int32_t n_cams, int64_t n_pts, int64_t n_obs, const int32_t *cam_idx,
               const int32_t *pt_idx, const double *obs, const double *K, double *cam_params,
               double *points, const sfm_ba_opts *opts, sfm_ba_report *report, int device);
+
+/* sfm_ba_lm with the observations of a dense scan (sfm_dense_obs_scan's
+ * handle, not freed here; its rows are the n_pts points, its cameras at
+ * most n_cams): perform_bundle_adjustment's whole path
+ * (BundleAdjustment.py:156-242) from the dense matrices, the observations
+ * copied from the scan straight into the pinned upload buffer. */
+int sfm_ba_lm_dense(void *obs_handle, int32_t n_cams, int64_t n_pts, const double *K, double *cam_params,
+                    double *points, const sfm_ba_opts *opts, sfm_ba_report *report, int device);
 
 /* ---- device-resident BA session (bench / multi-GPU) -------------------
  * A problem is uploaded once and iterated many times.  With a communicator

@@ -64,19 +64,24 @@ def bundle_adjustment_residuals(params, n_cameras, n_points, camera_indices, poi
 
 # Wall-time split of the last perform_bundle_adjustment(_coo) call, in ms
 # (measurement only; bench.py reports it as the drop-in's end-to-end time):
-# observations (dense flags -> COO), cams0 (Rotation -> rotvec), r0 (the
-# initial residual check on the GPU), ba_lm (the library call: create = host
-# prep + plan + upload, loop, download, and the wrapper's copies), post
-# (rotvec -> R, C and the point copy), total.
+# observations (the dense scan of the flag matrix), cams0 (Rotation ->
+# rotvec), ba_lm (the library call: create = host prep + plan + upload,
+# loop, download, and the wrapper's copies), post (rotvec -> R, C and the
+# points out), total.
 last_timings = {}
 
 
-def _observations(filtered_world_coords, feature_x, feature_y, filtered_feature_flags, n_cameras):
+def _observation_source(filtered_world_coords, feature_x, feature_y, filtered_feature_flags, n_cameras,
+                        valid_point_indices=None):
     """Dense flags -> COO observations in the reference's order (:164-169):
-    the library's threaded scan of the valid rows (point-major, camera
-    ascending, as np.where), or the numpy expression for layouts it does not
-    read (a non-contiguous row, a flag dtype other than float/int/bool)."""
-    valid_point_indices = np.where(np.asarray(filtered_world_coords).flatten() == 1)[0]
+    (valid_point_indices, source), the source the library's threaded scan of
+    the valid rows (point-major, camera ascending, as np.where; a
+    _core.DenseScan the solve reads without COO arrays), or the numpy
+    expression's (camera_indices, point_indices, points_2d) for layouts the
+    scanner does not read (a non-contiguous row, a flag dtype other than
+    float/int/bool)."""
+    if valid_point_indices is None:
+        valid_point_indices = np.where(np.asarray(filtered_world_coords).flatten() == 1)[0]
     # the reference's loop indexes filtered_feature_flags[pt_idx, cam_idx] for
     # every valid point and camera (:164-166), outside its try: IndexError
     # escapes when the flag matrix is too short or too narrow
@@ -87,16 +92,26 @@ def _observations(filtered_world_coords, feature_x, feature_y, filtered_feature_
         raise IndexError(f"index {valid_point_indices[-1]} is out of bounds for axis 0 with size {flag_shape[0]}")
     if n_cameras > flag_shape[1]:
         raise IndexError(f"index {flag_shape[1]} is out of bounds for axis 1 with size {flag_shape[1]}")
-    got = _core.dense_observations(filtered_feature_flags, feature_x, feature_y, valid_point_indices, n_cameras)
-    if got is not None:
-        camera_indices, point_indices, points_2d = got
-        return valid_point_indices, camera_indices, point_indices, points_2d
+    scan = _core.dense_scan(filtered_feature_flags, feature_x, feature_y, valid_point_indices, n_cameras)
+    if scan is not None:
+        return valid_point_indices, scan
     flags = np.asarray(filtered_feature_flags)[valid_point_indices][:, :n_cameras] == 1
     point_indices, camera_indices = np.nonzero(flags)  # row-major = point-major, camera ascending
     rows = valid_point_indices[point_indices]
     points_2d = np.column_stack([np.asarray(feature_x)[rows, camera_indices],
                                  np.asarray(feature_y)[rows, camera_indices]])
-    return valid_point_indices, camera_indices, point_indices, points_2d
+    return valid_point_indices, (camera_indices, point_indices, points_2d)
+
+
+def _observations(filtered_world_coords, feature_x, feature_y, filtered_feature_flags, n_cameras):
+    """(valid_point_indices, camera_indices, point_indices, points_2d) as the
+    reference assembles them (:164-169)."""
+    valid_point_indices, src = _observation_source(filtered_world_coords, feature_x, feature_y,
+                                                   filtered_feature_flags, n_cameras)
+    if isinstance(src, _core.DenseScan):
+        with src:
+            src = src.arrays()
+    return (valid_point_indices,) + tuple(src)
 
 
 def perform_bundle_adjustment(all_world_coords, filtered_world_coords, feature_x, feature_y,
@@ -143,10 +158,15 @@ def perform_bundle_adjustment(all_world_coords, filtered_world_coords, feature_x
     valid_point_indices = np.where(np.asarray(filtered_world_coords).flatten() == 1)[0]
     if len(valid_point_indices) == 0:  # :152-153
         return R_set, C_set, all_world_coords
-    obs = _observations(filtered_world_coords, feature_x, feature_y, filtered_feature_flags, len(R_set))
+    vpi, src = _observation_source(filtered_world_coords, feature_x, feature_y, filtered_feature_flags, len(R_set),
+                                   valid_point_indices)
     t_obs = (time.perf_counter() - t0) * 1e3
-    out = _adjust(all_world_coords, obs, R_set, C_set, K, max_iterations, function_tolerance,
-                  parameter_tolerance, initial_lambda)
+    try:
+        out = _adjust(all_world_coords, vpi, src, R_set, C_set, K, max_iterations, function_tolerance,
+                      parameter_tolerance, initial_lambda)
+    finally:
+        if isinstance(src, _core.DenseScan):
+            src.close()
     last_timings["observations"] = t_obs
     last_timings["total"] = (time.perf_counter() - t0) * 1e3
     return out
@@ -166,21 +186,23 @@ def perform_bundle_adjustment_coo(all_world_coords, filtered_world_coords, store
         return R_set, C_set, all_world_coords
     obs = store.observations(filtered_world_coords, len(R_set))
     t_obs = (time.perf_counter() - t0) * 1e3
-    out = _adjust(all_world_coords, obs, R_set, C_set, K, max_iterations, function_tolerance,
+    out = _adjust(all_world_coords, obs[0], obs[1:], R_set, C_set, K, max_iterations, function_tolerance,
                   parameter_tolerance, initial_lambda)
     last_timings["observations"] = t_obs
     last_timings["total"] = (time.perf_counter() - t0) * 1e3
     return out
 
 
-def _adjust(all_world_coords, obs, R_set, C_set, K, max_iterations, function_tolerance, parameter_tolerance,
-            initial_lambda):
-    """BundleAdjustment.py:156-242 from COO observations."""
-    valid_point_indices, camera_indices, point_indices, points_2d = obs
+def _adjust(all_world_coords, valid_point_indices, src, R_set, C_set, K, max_iterations, function_tolerance,
+            parameter_tolerance, initial_lambda):
+    """BundleAdjustment.py:156-242 from the observations: src a DenseScan or
+    (camera_indices, point_indices, points_2d)."""
+    dense = isinstance(src, _core.DenseScan)
+    n_obs = len(src) if dense else len(src[0])
     n_cameras = len(R_set)
     n_points = len(valid_point_indices)
     last_timings.clear()
-    if len(camera_indices) == 0:  # :171-172
+    if n_obs == 0:  # :171-172
         return R_set, C_set, all_world_coords
     t0 = time.perf_counter()
     # :183-193 for all cameras at once (the stacked conversions and products
@@ -193,16 +215,21 @@ def _adjust(all_world_coords, obs, R_set, C_set, K, max_iterations, function_tol
     pts0 = np.asarray(all_world_coords, dtype=np.float64)[valid_point_indices]
     t1 = time.perf_counter()
     last_timings["cams0"] = (t1 - t0) * 1e3
-    print(f"  Bundle adjustment: {n_cameras} cameras, {n_points} points, {len(camera_indices)} observations")
+    print(f"  Bundle adjustment: {n_cameras} cameras, {n_points} points, {n_obs} observations")
     _core.require_device()  # a missing GPU is an error, never a silent "failed"
     try:
-        if 2 * len(camera_indices) < 6 * n_cameras + 3 * n_points:  # scipy least_squares.py:850-852
+        if 2 * n_obs < 6 * n_cameras + 3 * n_points:  # scipy least_squares.py:850-852
             raise ValueError("Method 'lm' doesn't work when the number of residuals is less than the "
                              "number of variables.")
         t3 = time.perf_counter()
-        cams, pts, rep = _core.ba_lm(cams0, pts0, camera_indices, point_indices, points_2d, K,
-                                     max_iterations=max_iterations, function_tolerance=function_tolerance,
-                                     parameter_tolerance=parameter_tolerance, initial_lambda=initial_lambda)
+        opts = dict(max_iterations=max_iterations, function_tolerance=function_tolerance,
+                    parameter_tolerance=parameter_tolerance, initial_lambda=initial_lambda)
+        # cams0 / pts0 are this call's own arrays: solved in place (own=True)
+        if dense:
+            cams, pts, rep = _core.ba_lm_dense(cams0, pts0, src, K, own=True, **opts)
+        else:
+            camera_indices, point_indices, points_2d = src
+            cams, pts, rep = _core.ba_lm(cams0, pts0, camera_indices, point_indices, points_2d, K, own=True, **opts)
         t4 = time.perf_counter()
         if rep["status"] == 6:  # the cost at x0 is not finite: least_squares.py:843-845, nothing solved
             raise ValueError("Residuals are not finite in the initial point.")
@@ -214,8 +241,14 @@ def _adjust(all_world_coords, obs, R_set, C_set, K, max_iterations, function_tol
         C_all = (-np.transpose(R_all, (0, 2, 1)) @ cams[:, 3:, None])[:, :, 0]
         R_set_opt = [R_all[i] for i in range(n_cameras)]
         C_set_opt = [C_all[i] for i in range(n_cameras)]
-        all_world_coords_opt = all_world_coords.copy()  # :231-234
-        all_world_coords_opt[valid_point_indices] = pts
+        if (type(all_world_coords) is np.ndarray and all_world_coords.dtype == np.float64
+                and all_world_coords.shape == pts.shape):
+            # every row valid (valid_point_indices = arange): the copy with
+            # every row replaced is pts itself, a fresh C-order array
+            all_world_coords_opt = pts
+        else:
+            all_world_coords_opt = all_world_coords.copy()  # :231-234
+            all_world_coords_opt[valid_point_indices] = pts
         last_timings["post"] = (time.perf_counter() - t4) * 1e3
         print(f"  Bundle adjustment completed. Final cost: {rep['cost']:.6f}")
         return R_set_opt, C_set_opt, all_world_coords_opt

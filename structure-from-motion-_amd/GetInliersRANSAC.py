@@ -60,12 +60,19 @@ def GetInliersRANSAC(points1, points2, index, threshold=0.06, n_max=1000):
     n_iter = max(int(n_max), 0)
     # n_iter draws of random.sample(range(N), 8) from the global stream,
     # replayed inside the call while the GPU scores the drawn chunks
-    best, F_best, mask, _, _ = _core.ransac_f8_pyrandom(points1.reshape(n_points, 2), points2.reshape(n_points, 2),
-                                                        n_iter, threshold)
+    best, F_best, split, n_in = _core.ransac_f8_dropin(points1.reshape(n_points, 2), points2.reshape(n_points, 2),
+                                                       n_iter, threshold)
     if best < 0:  # :95-96 (no hypothesis with a positive count)
         return np.array([]), index, None
-    inlier_index = np.where(mask)[0]
-    outlier_indices = index[~mask]
+    # :99-106 from the library's positions: split[:n_in] is np.where(inlier_mask)[0],
+    # split[n_in:] the outlier positions, ascending
+    inlier_index = split[:n_in]
+    if index.ndim >= 1 and len(index) == n_points:
+        outlier_indices = index[split[n_in:]]
+    else:  # the reference's boolean index, with its IndexError
+        outlier_mask = np.ones(n_points, dtype=bool)
+        outlier_mask[inlier_index] = False
+        outlier_indices = index[outlier_mask]
     return inlier_index, outlier_indices, F_best
 
 

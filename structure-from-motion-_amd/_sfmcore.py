@@ -68,6 +68,7 @@ SIGNATURES = [
     # the in-call-sampling entries take raw addresses (c_void_p): the drop-in
     # calls them once per image pair and .ctypes.data_as costs ~4 us a pointer
     ("sfm_ransac_f8_pyrandom", _c, [_v, _v, _i, _v, _i, ctypes.c_double, _v, _v, _v, _v, _v, _c]),
+    ("sfm_ransac_f8_dropin", _c, [_v, _v, _i, _v, _i, ctypes.c_double, _v, _v, _v, _v, _c]),
     ("sfm_ransac_f8_range", _c, [_d, _d, _i, _i32, _i, _i, _i, ctypes.c_double, _i32, _u64, _d, _c]),
     ("sfm_ransac_f8_pyrandom_range", _c, [_d, _d, _i, _u32, _i, _i, _i, ctypes.c_double, _i32, _u64, _d, _c]),
     ("sfm_ransac_f8_mask", _c, [_d, _d, _i, _d, ctypes.c_double, _u8, _c]),
@@ -96,6 +97,8 @@ SIGNATURES = [
     ("sfm_ba_residuals", _c, [ctypes.c_int32, _i, _i, _i32, _i32, _d, _d, _d, _d, _d, _c]),
     ("sfm_ba_lm", _c, [ctypes.c_int32, _i, _i, _i32, _i32, _d, _d, _d, _d, ctypes.POINTER(BAOpts),
                        ctypes.POINTER(BAReport), _c]),
+    ("sfm_ba_lm_dense", _c, [ctypes.c_void_p, ctypes.c_int32, _i, _d, _d, _d, ctypes.POINTER(BAOpts),
+                             ctypes.POINTER(BAReport), _c]),
     ("sfm_comm_unique_id", _c, [ctypes.c_char_p]),
     ("sfm_comm_init", _c, [ctypes.c_char_p, _c, _c, _c, ctypes.POINTER(ctypes.c_void_p)]),
     ("sfm_comm_init_local", _c, [_c, ctypes.POINTER(ctypes.c_void_p)]),
@@ -163,11 +166,59 @@ def last_timings():
 # ------------------------------------------------------------------ random
 assert array.array("I").itemsize == 4
 
+# The global generator's MT19937 state crosses the C-ABI as uint32[625] (624
+# key words + position).  CPython keeps it inside the _random.Random object
+# as {PyObject_HEAD; int index; uint32_t state[624]}; when import verifies
+# that layout against random.getstate() (at three positions, one across a
+# twist, and a write-back), the state is copied out of and back into the
+# object with two memmoves -- random.getstate / setstate build and parse a
+# 625-int tuple, ~25 us of every RANSAC drop-in call.  Otherwise (another
+# interpreter, another layout) getstate / setstate.
+_MT_INDEX = ctypes.sizeof(ctypes.c_ssize_t) + ctypes.sizeof(ctypes.c_void_p)  # after PyObject_HEAD
+_MT_KEY = _MT_INDEX + 4
+_MT_ZERO = bytes(625 * 4)
+
+
+def _mt_layout_ok():
+    import sys
+    try:
+        import _random
+        inst = random.sample.__self__
+        if (sys.implementation.name != "cpython" or not isinstance(inst, _random.Random)
+                or _random.Random.__basicsize__ < _MT_KEY + 624 * 4):
+            return False
+    except (AttributeError, ImportError):
+        return False
+    saved = random.getstate()
+    try:
+        v, st, g = saved
+        random.setstate((v, st[:624] + (623,), g))
+        base = id(inst)
+        for _ in range(3):  # positions 623, 624, then 1 after the twist
+            _, cur, _ = random.getstate()
+            raw = (ctypes.c_uint32 * 624).from_address(base + _MT_KEY)
+            if tuple(raw) != cur[:624] or ctypes.c_int.from_address(base + _MT_INDEX).value != cur[624]:
+                return False
+            random.getrandbits(32)
+        ctypes.c_int.from_address(base + _MT_INDEX).value = 5  # write-back
+        return random.getstate()[1][624] == 5
+    finally:
+        random.setstate(saved)
+
+
+_MT_DIRECT = _mt_layout_ok()
+
 
 def _mt_state():
-    """The global MT19937 state as a C uint32[625] (key + position) plus the
-    parts random.setstate needs back (array.array: ~3x cheaper than numpy
-    for the 625-int round trip, which sits inside every RANSAC call)."""
+    """The global MT19937 state as a C uint32[625] (key + position) plus what
+    _mt_restore needs to put it back (array.array: ~3x cheaper than numpy
+    for the 625-int round trip of the getstate path)."""
+    if _MT_DIRECT:
+        base = id(random.sample.__self__)
+        st = array.array("I", _MT_ZERO)
+        ctypes.memmove(st.buffer_info()[0], base + _MT_KEY, 624 * 4)
+        st[624] = ctypes.c_int.from_address(base + _MT_INDEX).value
+        return base, st, None
     version_, internal, gauss = random.getstate()
     return version_, array.array("I", internal), gauss
 
@@ -176,8 +227,12 @@ def _mt_ptr(st):
     return ctypes.cast(st.buffer_info()[0], _u32)
 
 
-def _mt_restore(version_, st, gauss):
-    random.setstate((version_, tuple(st), gauss))
+def _mt_restore(h, st, gauss):
+    if _MT_DIRECT:
+        ctypes.memmove(h + _MT_KEY, st.buffer_info()[0], 624 * 4)
+        ctypes.c_int.from_address(h + _MT_INDEX).value = st[624]
+        return
+    random.setstate((h, tuple(st), gauss))
 
 
 def sample_table(n, k, H):
@@ -256,6 +311,27 @@ def ransac_f8_pyrandom(x1, x2, H, thr, want_counts=False, want_samples=False, de
     the call from the global random stream (sfm_ransac_f8_pyrandom).
     Returns (best_iter or -1, F_best or None, mask, counts or None, samples or None)."""
     return _ransac_pyrandom((_lib.sfm_ransac_f8_pyrandom, 8), x1, x2, H, thr, want_counts, want_samples, device)
+
+
+def ransac_f8_dropin(x1, x2, H, thr, device=None):
+    """GetInliersRANSAC's loop as its drop-in needs it (sfm_ransac_f8_dropin):
+    (best_iter or -1, F_best or None, split, n_inliers) -- split[:n_inliers]
+    the winner's inlier positions, split[n_inliers:] the outliers'."""
+    require_device()
+    x1, x2 = _f64(x1), _f64(x2)
+    N = len(x1)
+    h, st, gauss = _mt_state()
+    out = np.zeros(2, dtype=np.int64)  # best_iter, n_inliers
+    M = np.empty(9)
+    split = np.empty(N, dtype=np.int64)
+    oa = out.ctypes.data
+    _check(_lib.sfm_ransac_f8_dropin(x1.ctypes.data, x2.ctypes.data, N, st.buffer_info()[0], int(H), float(thr), oa,
+                                     M.ctypes.data, split.ctypes.data, oa + 8, DEVICE if device is None else device))
+    _mt_restore(h, st, gauss)
+    b = int(out[0])
+    if b < 0:
+        return -1, None, split[:0], 0
+    return b, M.reshape(3, 3), split, int(out[1])
 
 
 def ransac_h4_pyrandom(x1, x2, H, thr, want_counts=False, want_samples=False, device=None):
@@ -438,12 +514,44 @@ _DENSE_DTYPES = {np.dtype(np.float64): 0, np.dtype(np.float32): 1, np.dtype(np.i
                  np.dtype(np.uint8): 4, np.dtype(np.bool_): 4}
 
 
-def dense_observations(flags, feature_x, feature_y, rows, n_cams, n_threads=0):
-    """Native dense -> COO scan (host threads, no device needed): the
-    observations np.where(flags[rows][:, :n_cams] == 1) gives, in its order,
-    with feature_x / feature_y at the hits.  Returns (camera_indices,
-    point_indices, points_2d), or None when the matrices' layout or dtype is
-    not one the scanner reads (the caller then takes the numpy expression)."""
+class DenseScan:
+    """The native dense -> COO scan kept in the library (sfm_dense_obs_scan):
+    len() observations, .arrays() copies them out as (camera_indices,
+    point_indices, points_2d), ba_lm_dense() solves from it without the
+    arrays.  close() (or the context manager) hands the pieces back."""
+
+    def __init__(self, handle, n):
+        self.h, self.n = handle, n
+
+    def __len__(self):
+        return self.n
+
+    def arrays(self):
+        n = self.n
+        cam, pt, obs = np.empty(n, dtype=np.int32), np.empty(n, dtype=np.int32), np.empty((n, 2))
+        _check(_lib.sfm_dense_obs_read(self.h, _p(cam, _i32), _p(pt, _i32), _p(obs)))
+        return cam, pt, obs
+
+    def close(self):
+        if self.h:
+            _lib.sfm_dense_obs_free(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        self.close()
+
+
+def dense_scan(flags, feature_x, feature_y, rows, n_cams, n_threads=0):
+    """np.where(flags[rows][:, :n_cams] == 1) and the coordinates at the hits,
+    scanned natively (host threads, no device): a DenseScan, or None when the
+    matrices' layout or dtype is not one the scanner reads (the caller then
+    takes the numpy expression).  n_threads: row jobs (0: the library's)."""
     f, fx, fy = np.asarray(flags), np.asarray(feature_x), np.asarray(feature_y)
     if (f.ndim != 2 or fx.ndim != 2 or fx.shape != fy.shape or f.shape[0] != fx.shape[0]
             or f.dtype not in _DENSE_DTYPES or fx.dtype != np.float64 or fy.dtype != np.float64
@@ -457,13 +565,20 @@ def dense_observations(flags, feature_x, feature_y, rows, n_cams, n_threads=0):
                                    _p(rows, _i64), len(rows),
                                    int(n_cams), fx.ctypes.data_as(_d), fy.ctypes.data_as(_d), fx.strides[0],
                                    int(n_threads), ctypes.byref(h), _p(no, _i64)))
-    try:
-        n = int(no[0])
-        cam, pt, obs = np.empty(n, dtype=np.int32), np.empty(n, dtype=np.int32), np.empty((n, 2))
-        _check(_lib.sfm_dense_obs_read(h, _p(cam, _i32), _p(pt, _i32), _p(obs)))
-    finally:
-        _lib.sfm_dense_obs_free(h)
-    return cam, pt, obs
+    return DenseScan(h, int(no[0]))
+
+
+def dense_observations(flags, feature_x, feature_y, rows, n_cams, n_threads=0):
+    """Native dense -> COO scan (host threads, no device needed): the
+    observations np.where(flags[rows][:, :n_cams] == 1) gives, in its order,
+    with feature_x / feature_y at the hits.  Returns (camera_indices,
+    point_indices, points_2d), or None when the matrices' layout or dtype is
+    not one the scanner reads (the caller then takes the numpy expression)."""
+    scan = dense_scan(flags, feature_x, feature_y, rows, n_cams, n_threads)
+    if scan is None:
+        return None
+    with scan:
+        return scan.arrays()
 
 
 def triangulate(P1, P2, x1, x2):
@@ -526,16 +641,35 @@ def ba_opts(max_iterations=100, fixed_iterations=False, function_tolerance=1e-10
                   parameter_tolerance, initial_lambda)
 
 
-def ba_lm(cams, pts, cam_idx, pt_idx, obs, K, **opts):
-    """Schur-complement LM on the GPU. Returns (cams, pts, report dict)."""
+def _own(a, own):
+    """a as a C-order float64 array the solve may overwrite: a itself when
+    the caller hands it over (own=True and already that layout), else a copy."""
+    b = _f64(a)
+    return b if own and b is a else b.copy()
+
+
+def ba_lm(cams, pts, cam_idx, pt_idx, obs, K, own=False, **opts):
+    """Schur-complement LM on the GPU. Returns (cams, pts, report dict);
+    own=True: cams / pts are the caller's to overwrite (no copies)."""
     require_device()
-    cams, pts = _f64(cams).copy(), _f64(pts).copy()
+    cams, pts = _own(cams, own), _own(pts, own)
     obs, K = _f64(obs), _f64(K)
     ci = np.ascontiguousarray(cam_idx, dtype=np.int32)
     pi = np.ascontiguousarray(pt_idx, dtype=np.int32)
     o, rep = ba_opts(**opts), BAReport()
     _check(_lib.sfm_ba_lm(len(cams), len(pts), len(ci), _p(ci, _i32), _p(pi, _i32), _p(obs), _p(K), _p(cams),
                           _p(pts), ctypes.byref(o), ctypes.byref(rep), DEVICE))
+    return cams, pts, rep.as_dict()
+
+
+def ba_lm_dense(cams, pts, scan, K, own=False, **opts):
+    """ba_lm with the observations of a DenseScan (sfm_ba_lm_dense): they go
+    from the scan's pieces into the upload buffer, no COO arrays."""
+    require_device()
+    cams, pts = _own(cams, own), _own(pts, own)
+    o, rep = ba_opts(**opts), BAReport()
+    _check(_lib.sfm_ba_lm_dense(scan.h, len(cams), len(pts), _p(_f64(K)), _p(cams), _p(pts), ctypes.byref(o),
+                                ctypes.byref(rep), DEVICE))
     return cams, pts, rep.as_dict()
 
 

@@ -40,6 +40,7 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -54,6 +55,7 @@
 
 #include "sfm_common.hpp"
 #include "sfm_geom.hpp"
+#include "host_pool.hpp"
 
 // In-process rank group (N host threads, one per rank): the all-reduce is
 // staged through host memory and summed in rank order (deterministic).
@@ -3018,90 +3020,6 @@ static int64_t sweep_alloc(const std::vector<std::vector<uint16_t>> &P, const st
     return std::min(fp, fg);
 }
 
-// Host threads kept across calls (round 5): create fans out ~15 times (the
-// validation, the CSR, the counts, the planner's passes), and spawning and
-// joining 16 threads cost ~0.3-0.5 ms each time.  Workers park on a
-// condition variable; one job at a time -- a concurrent caller (in-process
-// ranks creating their problems together) spawns its own threads instead.
-class HostPool {
-  public:
-    static HostPool &get() {
-        static HostPool *p = new HostPool();  // never destroyed: workers may outlive static teardown
-        return *p;
-    }
-    // f(t) for t in [0, nt), the caller taking t = nt - 1; false if busy
-    template <class F>
-    bool try_run(int nt, F &&f) {
-        std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
-        if (!busy.owns_lock()) return false;
-        const int nw = nt - 1;
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            while ((int)workers_.size() < nw) {
-                const int id = (int)workers_.size();
-                workers_.emplace_back([this, id] { loop(id); });
-                workers_.back().detach();
-            }
-            job_ = [&f](int t) { f(t); };
-            njob_ = nw;
-            remaining_ = nw;
-            ++gen_;
-        }
-        cv_.notify_all();
-        f(nt - 1);
-        std::unique_lock<std::mutex> lk(mu_);
-        done_cv_.wait(lk, [this] { return remaining_ == 0; });
-        job_ = nullptr;
-        return true;
-    }
-
-  private:
-    void loop(int id) {
-        uint64_t seen = 0;
-        for (;;) {
-            std::function<void(int)> job;
-            {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return gen_ != seen; });
-                seen = gen_;
-                if (id >= njob_) continue;
-                job = job_;
-            }
-            job(id);
-            std::lock_guard<std::mutex> lk(mu_);
-            if (--remaining_ == 0) done_cv_.notify_all();
-        }
-    }
-    std::mutex run_mu_, mu_;
-    std::condition_variable cv_, done_cv_;
-    std::vector<std::thread> workers_;
-    std::function<void(int)> job_;
-    uint64_t gen_ = 0;
-    int njob_ = 0, remaining_ = 0;
-};
-
-// the planner's independent loops (per chunk, per spec) on host threads:
-// f(i) for i in [0, n), contiguous blocks, up to 16 threads (SFM_PLAN_THREADS)
-template <class F>
-static void par_for(int64_t n, F &&f) {
-    static const int nt0 = [] {
-        const int e = env_int("SFM_PLAN_THREADS", 0);
-        return e > 0 ? e : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-    }();
-    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt0, n));
-    if (nt == 1) {
-        for (int64_t i = 0; i < n; ++i) f(i);
-        return;
-    }
-    auto block = [&](int t) {
-        for (int64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) f(i);
-    };
-    if (HostPool::get().try_run(nt, block)) return;
-    std::vector<std::thread> th;
-    for (int t = 0; t < nt; ++t) th.emplace_back(block, t);
-    for (auto &x : th) x.join();
-}
-
 // SFM_CREATE_TIMING=1: host phase times of sfm_ba_create on stderr
 struct PhaseTimer {
     bool on = env_int("SFM_CREATE_TIMING", 0) != 0;
@@ -3114,25 +3032,120 @@ struct PhaseTimer {
     }
 };
 
+// Device blocks of destroyed problems (and of the planner's scratch), kept
+// for the next create on the same device.  The drop-in creates and destroys
+// a problem per call; hipMalloc, and hipFree (which synchronises the
+// device), cost ~6 ms of every cfg5 call.  A block is reused for a request
+// of up to 1.5x less; the cache holds at most 16 GiB (oldest blocks go
+// first) and is emptied for a device whose hipMalloc fails.  Every buffer a
+// kernel reads before writing is memset or uploaded in create, so a reused
+// block's old contents are never read: SFM_POOL_POISON=1 fills reused blocks
+// with 0xFF (the tests' check of that claim), SFM_POOL=0 turns the cache off.
+struct DevBlockCache {
+    struct Blk {
+        int dev;
+        size_t bytes;
+        void *p;
+    };
+    std::mutex mu;
+    std::deque<Blk> blks;  // oldest first
+    size_t held = 0;
+    static constexpr size_t kCap = (size_t)16 << 30;
+};
+static DevBlockCache &dev_cache() {
+    static auto *c = new DevBlockCache();
+    return *c;
+}
+static bool pool_on() {
+    static const bool v = env_int("SFM_POOL", 1) != 0;
+    return v;
+}
+static void pool_trim(int dev) {  // every cached block of dev back to the driver
+    DevBlockCache &c = dev_cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    for (auto it = c.blks.begin(); it != c.blks.end();) {
+        if (it->dev == dev) {
+            (void)hipFree(it->p);
+            c.held -= it->bytes;
+            it = c.blks.erase(it);
+        } else {
+            ++it;
+        }
+    }
+}
+// a block of at least `bytes` on the current device dev; *got = its size
+static hipError_t pool_malloc(void **out, size_t bytes, int dev, size_t *got) {
+    *got = bytes;
+    if (pool_on()) {
+        DevBlockCache &c = dev_cache();
+        std::unique_lock<std::mutex> lk(c.mu);
+        auto best = c.blks.end();
+        for (auto it = c.blks.begin(); it != c.blks.end(); ++it)
+            if (it->dev == dev && it->bytes >= bytes && it->bytes <= bytes + bytes / 2 &&
+                (best == c.blks.end() || it->bytes < best->bytes))
+                best = it;
+        if (best != c.blks.end()) {
+            *out = best->p;
+            *got = best->bytes;
+            c.held -= best->bytes;
+            c.blks.erase(best);
+            lk.unlock();
+            if (env_int("SFM_POOL_POISON", 0)) {
+                (void)hipMemset(*out, 0xFF, *got);
+                (void)hipDeviceSynchronize();
+            }
+            return hipSuccess;
+        }
+    }
+    hipError_t e = hipMalloc(out, bytes);
+    if (e != hipSuccess && pool_on()) {
+        (void)hipGetLastError();
+        pool_trim(dev);
+        e = hipMalloc(out, bytes);
+    }
+    return e;
+}
+// back to the cache; the caller has synchronised every stream that used it
+static void pool_free(void *p, size_t bytes, int dev) {
+    if (!p) return;
+    if (!pool_on()) {
+        (void)hipFree(p);
+        return;
+    }
+    DevBlockCache &c = dev_cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    c.blks.push_back({dev, bytes, p});
+    c.held += bytes;
+    while (c.held > DevBlockCache::kCap && !c.blks.empty()) {
+        (void)hipFree(c.blks.front().p);
+        c.held -= c.blks.front().bytes;
+        c.blks.pop_front();
+    }
+}
+
 // the device side of the planner: the uploaded COO and a stream; scratch
-// buffers live until the object goes (freed on every return path)
+// buffers live until the object goes (released on every return path, once
+// the stream has drained)
 struct DevPlan {
     hipStream_t s = nullptr;
+    int dev = 0;
     const int32_t *pstart = nullptr, *pt = nullptr, *cam = nullptr;
     int64_t no = 0;
-    std::vector<void *> bufs;
+    std::vector<std::pair<void *, size_t>> bufs;
     int err = 0;
     ~DevPlan() {
-        for (void *b : bufs) (void)hipFree(b);
+        if (!bufs.empty() && s) (void)hipStreamSynchronize(s);
+        for (auto &b : bufs) pool_free(b.first, b.second, dev);
     }
     template <class T>
     T *scratch(size_t n) {
         void *q = nullptr;
-        if (hipMalloc(&q, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) {
+        size_t got;
+        if (pool_malloc(&q, std::max<size_t>(n, 1) * sizeof(T), dev, &got) != hipSuccess) {
             err = SFM_ERR_NOMEM;
             return nullptr;
         }
-        bufs.push_back(q);
+        bufs.push_back({q, got});
         return static_cast<T *>(q);
     }
     bool ok(hipError_t e) {
@@ -3620,36 +3633,96 @@ struct sfm_ba_problem {
     hipEvent_t ev_solve = nullptr;
     double t_acc[T_NT] = {};
     int t_iters = 0;
-    std::vector<void *> allocs;
+    std::vector<std::pair<void *, size_t>> allocs;
     ~sfm_ba_problem() {
         (void)hipSetDevice(device);
-        for (void *p : allocs) (void)hipFree(p);
+        if (ev_solve && comm && comm->local) {
+            std::lock_guard<std::mutex> lk(comm->local->solve_mu);
+            if (comm->local->last_solve == ev_solve) comm->local->last_solve = nullptr;
+        }
+        // the stream drains before its blocks and events go back to the caches
+        const bool idle = stream && hipStreamSynchronize(stream) == hipSuccess;
+        for (auto &a : allocs) {
+            if (idle) pool_free(a.first, a.second, device);
+            else (void)hipFree(a.first);
+        }
+        if (stream && idle) {
+            kit_release(*this);
+            return;
+        }
+        (void)hipGetLastError();
         if (h_ring) (void)hipHostFree(h_ring);
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
         for (auto &e : ev_it)
             if (e) (void)hipEventDestroy(e);
-        if (ev_solve) {
-            if (comm && comm->local) {
-                std::lock_guard<std::mutex> lk(comm->local->solve_mu);
-                if (comm->local->last_solve == ev_solve) comm->local->last_solve = nullptr;
-            }
-            (void)hipEventDestroy(ev_solve);
-        }
+        if (ev_solve) (void)hipEventDestroy(ev_solve);
         if (stream) (void)hipStreamDestroy(stream);
     }
     template <class T> int alloc(T *&p, int64_t n) {
         void *q = nullptr;
-        size_t bytes = (size_t)std::max<int64_t>(n, 1) * sizeof(T);
-        if (hipMalloc(&q, bytes) != hipSuccess) {
+        size_t bytes = (size_t)std::max<int64_t>(n, 1) * sizeof(T), got;
+        if (pool_malloc(&q, bytes, device, &got) != hipSuccess) {
             set_error("hipMalloc(%zu) failed", bytes);
             return SFM_ERR_NOMEM;
         }
-        allocs.push_back(q);
+        allocs.push_back({q, got});
         p = reinterpret_cast<T *>(q);
         return 0;
     }
+    static void kit_release(sfm_ba_problem &p);
+    bool kit_acquire();
 };
+
+// A destroyed problem's stream, its 200 timing events, the solve event and
+// the pinned LM ring, kept for the next create on the same device (creating
+// them cost ~2-3 ms per create).
+struct StreamKit {
+    int dev;
+    hipStream_t stream;
+    hipEvent_t ev[2 * T_NT];
+    hipEvent_t ev_it[2 * T_NT * kEvSlots];
+    hipEvent_t ev_solve;
+    HostLM *h_ring, *d_ring;
+};
+static std::mutex &kit_mu() {
+    static auto *m = new std::mutex();
+    return *m;
+}
+static std::vector<StreamKit> &kits() {
+    static auto *v = new std::vector<StreamKit>();
+    return *v;
+}
+void sfm_ba_problem::kit_release(sfm_ba_problem &p) {
+    StreamKit k;
+    k.dev = p.device;
+    k.stream = p.stream;
+    std::memcpy(k.ev, p.ev, sizeof k.ev);
+    std::memcpy(k.ev_it, p.ev_it, sizeof k.ev_it);
+    k.ev_solve = p.ev_solve;
+    k.h_ring = p.h_ring;
+    k.d_ring = p.d_ring;
+    std::lock_guard<std::mutex> lk(kit_mu());
+    kits().push_back(k);
+}
+bool sfm_ba_problem::kit_acquire() {
+    if (!pool_on()) return false;
+    std::lock_guard<std::mutex> lk(kit_mu());
+    auto &v = kits();
+    for (size_t i = v.size(); i-- > 0;)
+        if (v[i].dev == device) {
+            const StreamKit &k = v[i];
+            stream = k.stream;
+            std::memcpy(ev, k.ev, sizeof ev);
+            std::memcpy(ev_it, k.ev_it, sizeof ev_it);
+            ev_solve = k.ev_solve;
+            h_ring = k.h_ring;
+            d_ring = k.d_ring;
+            v.erase(v.begin() + i);
+            return true;
+        }
+    return false;
+}
 
 static int upload_state(sfm_ba_problem *p) {
     std::vector<double> Rt(12 * (size_t)p->nc);
@@ -3727,10 +3800,18 @@ extern "C" int sfm_comm_destroy(sfm_comm *c) {
     return 0;
 }
 
-extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt,
-                             const double *obs, const double *K, const double *cams, const double *pts, int device,
-                             sfm_comm *comm, sfm_ba_problem **out) {
-    SFM_CHECK_ARG(out && K && cams && (pts || np_ == 0) && (no == 0 || (cam && pt && obs)), "null pointer");
+namespace sfm {
+bool dense_obs_info(void *handle, int64_t *n, int64_t *n_rows, int32_t *n_cams);  // dense_obs.cpp
+void dense_obs_copy(void *handle, int32_t *cam, int32_t *pt, double *obs);
+}  // namespace sfm
+
+// sfm_ba_create; with `dense` (a sfm_dense_obs_scan handle) the
+// observations come from the scan's pieces, copied straight into the pinned
+// upload buffer (cam / pt / obs are then null): no COO arrays in between
+static int ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt, const double *obs,
+                     void *dense, const double *K, const double *cams, const double *pts, int device, sfm_comm *comm,
+                     sfm_ba_problem **out) {
+    SFM_CHECK_ARG(out && K && cams && (pts || np_ == 0) && (no == 0 || dense || (cam && pt && obs)), "null pointer");
     SFM_CHECK_ARG(nc >= 1 && np_ >= 0 && no >= 0, "bad sizes");
     SFM_CHECK_ARG(no < ((int64_t)1 << 31), "problem too large for int32 indexing");
     SFM_CHECK_ARG(6 * nc <= SOLVE_MAX, "at most 682 cameras (dense reduced camera system)");
@@ -3738,7 +3819,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     PhaseTimer ctm_;
     auto ctick = [&](const char *what) { ctm_.tick(what); };
     const bool ctm = ctm_.on;
-    {  // host threads over contiguous observation ranges
+    if (!dense) {  // host threads over contiguous observation ranges (the scan's output is valid by construction)
         constexpr int NB = 16;
         int bad[NB] = {0};
         par_for(NB, [&](int64_t t) {
@@ -3775,7 +3856,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     // ones must produce the same plan: the digest test)
     const bool plan_only = env_int("SFM_CREATE_PLAN_ONLY", 0) != 0;
     const bool host_plan = plan_only || env_int("SFM_PLAN_HOST", 0) != 0;
-    const bool want_digest = ctm || env_int("SFM_PLAN_DIGEST", 0) != 0;
+    const bool want_digest = env_int("SFM_PLAN_DIGEST", 0) != 0;
     int rc;
     // point CSR (pstart), camera-major permutation (cam_obs, stable: point
     // order within a camera) and its offsets (cstart), co-observation counts
@@ -3786,9 +3867,11 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     if (!plan_only) {
         SFM_HIP(hipSetDevice(device));
         (void)hipGetLastError();  // launches below are checked with hipGetLastError: start clean
-        SFM_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
-        for (auto &e : p->ev) SFM_HIP(hipEventCreate(&e));
-        for (auto &e : p->ev_it) SFM_HIP(hipEventCreate(&e));
+        if (!p->kit_acquire()) {
+            SFM_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+            for (auto &e : p->ev) SFM_HIP(hipEventCreate(&e));
+            for (auto &e : p->ev_it) SFM_HIP(hipEventCreate(&e));
+        }
         ctick("stream");
         if ((rc = p->alloc(p->d_cam, no)) || (rc = p->alloc(p->d_pt, no)) || (rc = p->alloc(p->d_pstart, np_ + 1)) ||
             (rc = p->alloc(p->d_obs, no)) || (rc = p->alloc(p->d_cm_pt, no)) || (rc = p->alloc(p->d_cm_obs, no)) ||
@@ -3800,6 +3883,17 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     // hipMemcpy of the 96 MB at cfg5 ran ~10 GB/s); a concurrent create
     // finding it busy uploads from pageable memory
     std::unique_lock<std::mutex> stage_lk;
+    std::vector<int32_t> dense_cam, dense_pt;
+    std::vector<double> dense_xy;
+    if (dense && (plan_only || !no)) {  // no upload: the host arrays alone
+        dense_cam.resize(no);
+        dense_pt.resize(no);
+        dense_xy.resize(2 * (size_t)no);
+        if (no) dense_obs_copy(dense, dense_cam.data(), dense_pt.data(), dense_xy.data());
+        cam = dense_cam.data();
+        pt = dense_pt.data();
+        obs = dense_xy.data();
+    }
     if (!plan_only && no) {
         PinnedStage &st = pinned_stage();
         stage_lk = std::unique_lock<std::mutex>(st.mu, std::try_to_lock);
@@ -3815,14 +3909,22 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
             }
             if (st.bytes >= need) {
                 char *h = static_cast<char *>(st.p);
-                constexpr int NB = 16;
-                par_for(3 * NB, [&](int64_t k) {
-                    const int a = (int)(k / NB), t = (int)(k % NB);
-                    const size_t w = a == 2 ? 16 : 4, n0 = no * t / NB, n1 = no * (t + 1) / NB;
-                    const char *src = a == 0 ? (const char *)cam : a == 1 ? (const char *)pt : (const char *)obs;
-                    char *dst = h + (a == 0 ? 0 : a == 1 ? (size_t)no * 4 : (size_t)no * 8);
-                    std::memcpy(dst + n0 * w, src + n0 * w, (n1 - n0) * w);
-                });
+                if (dense) {
+                    dense_obs_copy(dense, reinterpret_cast<int32_t *>(h), reinterpret_cast<int32_t *>(h + (size_t)no * 4),
+                                   reinterpret_cast<double *>(h + (size_t)no * 8));
+                    cam = reinterpret_cast<const int32_t *>(h);
+                    pt = reinterpret_cast<const int32_t *>(h + (size_t)no * 4);
+                    obs = reinterpret_cast<const double *>(h + (size_t)no * 8);
+                } else {
+                    constexpr int NB = 16;
+                    par_for(3 * NB, [&](int64_t k) {
+                        const int a = (int)(k / NB), t = (int)(k % NB);
+                        const size_t w = a == 2 ? 16 : 4, n0 = no * t / NB, n1 = no * (t + 1) / NB;
+                        const char *src = a == 0 ? (const char *)cam : a == 1 ? (const char *)pt : (const char *)obs;
+                        char *dst = h + (a == 0 ? 0 : a == 1 ? (size_t)no * 4 : (size_t)no * 8);
+                        std::memcpy(dst + n0 * w, src + n0 * w, (n1 - n0) * w);
+                    });
+                }
                 SFM_HIP(hipMemcpyAsync(p->d_cam, h, no * 4, hipMemcpyHostToDevice, p->stream));
                 SFM_HIP(hipMemcpyAsync(p->d_pt, h + (size_t)no * 4, no * 4, hipMemcpyHostToDevice, p->stream));
                 SFM_HIP(hipMemcpyAsync(p->d_obs, h + (size_t)no * 8, no * 16, hipMemcpyHostToDevice, p->stream));
@@ -3831,6 +3933,15 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         }
         if (!staged) {
             if (stage_lk.owns_lock()) stage_lk.unlock();
+            if (dense) {  // the staging buffer is busy: the pieces through pageable arrays
+                dense_cam.resize(no);
+                dense_pt.resize(no);
+                dense_xy.resize(2 * (size_t)no);
+                dense_obs_copy(dense, dense_cam.data(), dense_pt.data(), dense_xy.data());
+                cam = dense_cam.data();
+                pt = dense_pt.data();
+                obs = dense_xy.data();
+            }
             SFM_HIP(hipMemcpyAsync(p->d_cam, cam, no * 4, hipMemcpyHostToDevice, p->stream));
             SFM_HIP(hipMemcpyAsync(p->d_pt, pt, no * 4, hipMemcpyHostToDevice, p->stream));
             SFM_HIP(hipMemcpyAsync(p->d_obs, obs, no * 16, hipMemcpyHostToDevice, p->stream));
@@ -3942,7 +4053,9 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         }
         ctick("csr+blockcounts (device)");
     }
-    if (stage_lk.owns_lock()) {  // the staged copies are done once the stream has passed them
+    // the staged copies are done once the stream has passed them (the host
+    // planner reads a dense scan's observations from the buffer: kept then)
+    if (stage_lk.owns_lock() && !(dense && host_plan)) {
         SFM_HIP(hipStreamSynchronize(p->stream));
         stage_lk.unlock();
     }
@@ -3965,6 +4078,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
     const bool dev_plan = !host_plan;
     if (dev_plan) {
         dev.s = p->stream;
+        dev.dev = device;
         dev.pstart = p->d_pstart;
         dev.pt = p->d_pt;
         dev.cam = p->d_cam;
@@ -4089,7 +4203,7 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
         p->gjrb.carve(gw, gi, p->nT);
         SFM_HIP(hipMemsetAsync(gw, 0, GjrBufs::words(p->nT) * sizeof(gjr::u64), p->stream));
         SFM_HIP(hipMemsetAsync(gi, 0, GjrBufs::ints * sizeof(int), p->stream));
-        SFM_HIP(hipEventCreateWithFlags(&p->ev_solve, hipEventDisableTiming));
+        if (!p->ev_solve) SFM_HIP(hipEventCreateWithFlags(&p->ev_solve, hipEventDisableTiming));
     }
     if (p->gjp.cb) {
         double *gd = nullptr;
@@ -4099,12 +4213,14 @@ extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t 
             return rc;
         p->gjb.carve(gd, gi, p->nT, p->gjp.nseg);
         SFM_HIP(hipMemsetAsync(gi, 0, GjBufs::ints(p->nT, p->gjp.nseg) * sizeof(int), p->stream));
-        SFM_HIP(hipEventCreateWithFlags(&p->ev_solve, hipEventDisableTiming));
+        if (!p->ev_solve) SFM_HIP(hipEventCreateWithFlags(&p->ev_solve, hipEventDisableTiming));
     }
     ctick("alloc");
-    SFM_HIP(hipHostMalloc((void **)&p->h_ring, kHostRing * sizeof(HostLM), hipHostMallocMapped | hipHostMallocCoherent));
+    if (!p->h_ring) {
+        SFM_HIP(hipHostMalloc((void **)&p->h_ring, kHostRing * sizeof(HostLM), hipHostMallocMapped | hipHostMallocCoherent));
+        SFM_HIP(hipHostGetDevicePointer((void **)&p->d_ring, p->h_ring, 0));
+    }
     std::memset((void *)p->h_ring, 0, kHostRing * sizeof(HostLM));
-    SFM_HIP(hipHostGetDevicePointer((void **)&p->d_ring, p->h_ring, 0));
     hipStream_t s = p->stream;
     SFM_HIP(hipMemsetAsync(p->d_camlin, 0, (size_t)CAMLIN * nc * sizeof(double), s));
     SFM_HIP(hipMemsetAsync(p->d_count, 0, 3 * GS_WORDS * sizeof(unsigned), s));
@@ -4190,6 +4306,12 @@ extern "C" int sfm_ba_plan_digest(sfm_ba_problem *p, uint64_t *out) {
     SFM_CHECK_ARG(p && out, "null pointer");
     *out = p->plan_digest;
     return 0;
+}
+
+extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt,
+                             const double *obs, const double *K, const double *cams, const double *pts, int device,
+                             sfm_comm *comm, sfm_ba_problem **out) {
+    return ba_create(nc, np_, no, cam, pt, obs, nullptr, K, cams, pts, device, comm, out);
 }
 
 extern "C" int sfm_ba_reset(sfm_ba_problem *p) {
@@ -4825,13 +4947,13 @@ extern "C" int sfm_ba_kernel_times(sfm_ba_problem *p, double *ms, int n, char *n
     return m;
 }
 
-extern "C" int sfm_ba_lm(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt,
-                         const double *obs, const double *K, double *cams, double *pts, const sfm_ba_opts *o,
-                         sfm_ba_report *rep, int device) {
+static int ba_lm(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt, const double *obs,
+                 void *dense, const double *K, double *cams, double *pts, const sfm_ba_opts *o, sfm_ba_report *rep,
+                 int device) {
     SFM_CHECK_ARG(o && cams, "null pointer");
     const auto t0 = std::chrono::steady_clock::now();
     sfm_ba_problem *p = nullptr;
-    int rc = sfm_ba_create(nc, np_, no, cam, pt, obs, K, cams, pts, device, nullptr, &p);
+    int rc = ba_create(nc, np_, no, cam, pt, obs, dense, K, cams, pts, device, nullptr, &p);
     if (rc) return rc;
     const auto t1 = std::chrono::steady_clock::now();
     rc = sfm_ba_solve(p, o, rep);
@@ -4844,6 +4966,24 @@ extern "C" int sfm_ba_lm(int32_t nc, int64_t np_, int64_t no, const int32_t *cam
     }
     sfm_ba_destroy(p);
     return rc;
+}
+
+extern "C" int sfm_ba_lm(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt,
+                         const double *obs, const double *K, double *cams, double *pts, const sfm_ba_opts *o,
+                         sfm_ba_report *rep, int device) {
+    return ba_lm(nc, np_, no, cam, pt, obs, nullptr, K, cams, pts, o, rep, device);
+}
+
+// perform_bundle_adjustment from the dense scan (sfm_dense_obs_scan's
+// handle, not freed here): the observations go from the scan's pieces into
+// the pinned upload buffer, never through COO arrays
+extern "C" int sfm_ba_lm_dense(void *obs_handle, int32_t nc, int64_t np_, const double *K, double *cams, double *pts,
+                               const sfm_ba_opts *o, sfm_ba_report *rep, int device) {
+    int64_t no, nrows;
+    int32_t ncams;
+    SFM_CHECK_ARG(dense_obs_info(obs_handle, &no, &nrows, &ncams), "null observation handle");
+    SFM_CHECK_ARG(nrows == np_ && ncams <= nc, "the scan's rows / cameras do not match the problem");
+    return ba_lm(nc, np_, no, nullptr, nullptr, nullptr, obs_handle, K, cams, pts, o, rep, device);
 }
 
 // Single-process multi-GPU bundle adjustment: points (with their

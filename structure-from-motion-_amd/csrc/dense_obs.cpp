@@ -1,4 +1,4 @@
-// Dense visibility -> COO observations for the BA drop-in (round 4).
+// Dense visibility -> COO observations for the BA drop-in (rounds 4-5).
 // perform_bundle_adjustment's interface (Phase 1/BundleAdjustment.py:113-
 // 169) hands over n_features x n_cameras matrices (feature_x, feature_y,
 // filtered_feature_flags) and builds the observation list with
@@ -7,64 +7,195 @@
 //   points_2d = (feature_x[rows, cam], feature_y[rows, cam])
 // At cfg5 (500k points x 200 cameras, 8-byte flags) numpy's fancy-indexed
 // copy of the flag matrix, the comparison and np.where took ~0.4 s, half of
-// the drop-in's call.  Here the rows are scanned once by a thread pool (each
-// thread a contiguous block of rows, so the output stays point-major with
-// cameras ascending: np.where's row-major order), the coordinates gathered
-// at the hits, and the per-thread pieces concatenated in row order.
+// the drop-in's call.  Here the rows are scanned once by the host thread
+// pool (each job a contiguous block of rows, so the output stays
+// point-major with cameras ascending: np.where's row-major order), the
+// coordinates gathered at the hits, and the per-job pieces concatenated in
+// row order -- into numpy arrays (sfm_dense_obs_read) or straight into the
+// BA create's pinned upload buffer (sfm_ba_lm_dense).
+//
+// Round 5: the comparisons run 8-64 flags per AVX-512 instruction (run-time
+// dispatch; the scalar loop otherwise), a block of rows is scanned before its
+// coordinates are gathered (the gathers are then independent loads), and
+// the pieces are kept across calls, so a repeated call writes into memory
+// that is already mapped (first-touch page faults of the ~100 MB of pieces
+// had cost more than the scan).
+#include <immintrin.h>
+
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <vector>
 
+#include "host_pool.hpp"
 #include "sfm_common.hpp"
 
 namespace {
 
 struct Piece {
-    std::vector<int32_t> cam, pt;
+    std::vector<int32_t> cam, pt;  // grown, never shrunk: size() is capacity
     std::vector<double> xy;
+    int64_t n = 0;
+    void ensure(int64_t need) {
+        if ((int64_t)cam.size() >= need) return;
+        const size_t c = (size_t)std::max<int64_t>(need, (int64_t)cam.size() * 3 / 2);
+        cam.resize(c);
+        pt.resize(c);
+        xy.resize(2 * c);
+    }
 };
 
 struct DenseObs {
     std::vector<Piece> pieces;
-    int64_t n = 0;
+    int64_t n = 0, n_rows = 0;
+    int32_t n_cams = 0;
 };
 
-// a row in 64-camera words: the comparisons into a bit mask (branch-free,
-// vectorised), then one visit per hit
+// the pieces of the last call, reused by the next one (one user at a time;
+// a concurrent caller gets its own)
+std::mutex g_pool_mu;
+DenseObs *g_pool = nullptr;
+
+constexpr int ROW_BLOCK = 32;  // rows scanned before their coordinates are gathered
+
+inline bool have_avx512() {
+    static const bool v = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+                          !std::getenv("SFM_DENSE_SCALAR");
+    return v;
+}
+
+// flags[0..w) == 1 as a bit mask, w <= 64
 template <class T>
+inline uint64_t mask_scalar(const T *f, int w) {
+    uint64_t mk = 0;
+    for (int j = 0; j < w; ++j) mk |= (uint64_t)(f[j] == static_cast<T>(1)) << j;
+    return mk;
+}
+
+__attribute__((target("avx512f,avx512bw"))) inline uint64_t mask512(const double *f, int w) {
+    const __m512d one = _mm512_set1_pd(1.0);
+    uint64_t mk = 0;
+    for (int j = 0; j < w; j += 8) {
+        const __mmask8 m = (__mmask8)(w - j >= 8 ? 0xFF : (1u << (w - j)) - 1);
+        mk |= (uint64_t)_mm512_mask_cmp_pd_mask(m, _mm512_maskz_loadu_pd(m, f + j), one, _CMP_EQ_OQ) << j;
+    }
+    return mk;
+}
+__attribute__((target("avx512f,avx512bw"))) inline uint64_t mask512(const float *f, int w) {
+    const __m512 one = _mm512_set1_ps(1.0f);
+    uint64_t mk = 0;
+    for (int j = 0; j < w; j += 16) {
+        const __mmask16 m = (__mmask16)(w - j >= 16 ? 0xFFFF : (1u << (w - j)) - 1);
+        mk |= (uint64_t)_mm512_mask_cmp_ps_mask(m, _mm512_maskz_loadu_ps(m, f + j), one, _CMP_EQ_OQ) << j;
+    }
+    return mk;
+}
+__attribute__((target("avx512f,avx512bw"))) inline uint64_t mask512(const int64_t *f, int w) {
+    const __m512i one = _mm512_set1_epi64(1);
+    uint64_t mk = 0;
+    for (int j = 0; j < w; j += 8) {
+        const __mmask8 m = (__mmask8)(w - j >= 8 ? 0xFF : (1u << (w - j)) - 1);
+        mk |= (uint64_t)_mm512_mask_cmpeq_epi64_mask(m, _mm512_maskz_loadu_epi64(m, f + j), one) << j;
+    }
+    return mk;
+}
+__attribute__((target("avx512f,avx512bw"))) inline uint64_t mask512(const int32_t *f, int w) {
+    const __m512i one = _mm512_set1_epi32(1);
+    uint64_t mk = 0;
+    for (int j = 0; j < w; j += 16) {
+        const __mmask16 m = (__mmask16)(w - j >= 16 ? 0xFFFF : (1u << (w - j)) - 1);
+        mk |= (uint64_t)_mm512_mask_cmpeq_epi32_mask(m, _mm512_maskz_loadu_epi32(m, f + j), one) << j;
+    }
+    return mk;
+}
+__attribute__((target("avx512f,avx512bw"))) inline uint64_t mask512(const uint8_t *f, int w) {
+    const __mmask64 m = w >= 64 ? ~0ull : (1ull << w) - 1;
+    return _mm512_mask_cmpeq_epi8_mask(m, _mm512_maskz_loadu_epi8(m, f), _mm512_set1_epi8(1));
+}
+
+// rows[r0, r1) into p: per block of ROW_BLOCK rows, the hits (row, camera)
+// first, then their coordinates
+template <class T, bool AVX>
 void scan_rows(const char *flags, int64_t flag_row_bytes, const int64_t *rows, int64_t r0, int64_t r1, int32_t n_cams,
-               const char *fx, const char *fy, int64_t xy_row_bytes, Piece &out) {
-    out.cam.reserve((size_t)(r1 - r0) * 8);
-    out.pt.reserve((size_t)(r1 - r0) * 8);
-    out.xy.reserve((size_t)(r1 - r0) * 16);
-    for (int64_t i = r0; i < r1; ++i) {
-        const int64_t r = rows[i];
-        const T *fr = reinterpret_cast<const T *>(flags + r * flag_row_bytes);
-        const double *xr = reinterpret_cast<const double *>(fx + r * xy_row_bytes);
-        const double *yr = reinterpret_cast<const double *>(fy + r * xy_row_bytes);
-        for (int32_t c0 = 0; c0 < n_cams; c0 += 64) {
-            const int w = std::min(64, n_cams - c0);
-            uint64_t mk = 0;
-            if (w == 64) {
-                for (int j = 0; j < 64; ++j) mk |= (uint64_t)(fr[c0 + j] == static_cast<T>(1)) << j;
-            } else {
-                for (int j = 0; j < w; ++j) mk |= (uint64_t)(fr[c0 + j] == static_cast<T>(1)) << j;
-            }
-            while (mk) {
-                const int c = c0 + __builtin_ctzll(mk);
-                mk &= mk - 1;
-                out.cam.push_back(c);
-                out.pt.push_back((int32_t)i);
-                out.xy.push_back(xr[c]);
-                out.xy.push_back(yr[c]);
+               const char *fx, const char *fy, int64_t xy_row_bytes, Piece &p) {
+    p.n = 0;
+    std::vector<int32_t> hr, hc;
+    hr.resize((size_t)ROW_BLOCK * n_cams);
+    hc.resize((size_t)ROW_BLOCK * n_cams);
+    for (int64_t b0 = r0; b0 < r1; b0 += ROW_BLOCK) {
+        const int64_t b1 = std::min(r1, b0 + ROW_BLOCK);
+        int64_t nh = 0;
+        for (int64_t i = b0; i < b1; ++i) {
+            const T *fr = reinterpret_cast<const T *>(flags + rows[i] * flag_row_bytes);
+            for (int32_t c0 = 0; c0 < n_cams; c0 += 64) {
+                const int w = std::min(64, n_cams - c0);
+                uint64_t mk;
+                if constexpr (AVX) mk = mask512(fr + c0, w);
+                else mk = mask_scalar(fr + c0, w);
+                while (mk) {
+                    hc[nh] = c0 + __builtin_ctzll(mk);
+                    hr[nh++] = (int32_t)i;
+                    mk &= mk - 1;
+                }
             }
         }
+        p.ensure(p.n + nh);
+        int32_t *cam = p.cam.data() + p.n, *pt = p.pt.data() + p.n;
+        double *xy = p.xy.data() + 2 * p.n;
+        for (int64_t k = 0; k < nh; ++k) {
+            const int64_t off = rows[hr[k]] * xy_row_bytes + (int64_t)hc[k] * 8;
+            cam[k] = hc[k];
+            pt[k] = hr[k];
+            xy[2 * k] = *reinterpret_cast<const double *>(fx + off);
+            xy[2 * k + 1] = *reinterpret_cast<const double *>(fy + off);
+        }
+        p.n += nh;
+    }
+}
+
+template <bool AVX>
+void scan_dispatch(int32_t dtype, const char *f, int64_t frb, const int64_t *rows, int64_t r0, int64_t r1, int32_t nc,
+                   const char *x, const char *y, int64_t xyrb, Piece &p) {
+    switch (dtype) {
+    case 0: scan_rows<double, AVX>(f, frb, rows, r0, r1, nc, x, y, xyrb, p); break;
+    case 1: scan_rows<float, AVX>(f, frb, rows, r0, r1, nc, x, y, xyrb, p); break;
+    case 2: scan_rows<int64_t, AVX>(f, frb, rows, r0, r1, nc, x, y, xyrb, p); break;
+    case 3: scan_rows<int32_t, AVX>(f, frb, rows, r0, r1, nc, x, y, xyrb, p); break;
+    default: scan_rows<uint8_t, AVX>(f, frb, rows, r0, r1, nc, x, y, xyrb, p); break;
     }
 }
 
 }  // namespace
+
+namespace sfm {
+
+// for sfm_ba_lm_dense (ba.hip): the scan's size and its concatenation
+bool dense_obs_info(void *handle, int64_t *n, int64_t *n_rows, int32_t *n_cams) {
+    if (!handle) return false;
+    auto *h = static_cast<DenseObs *>(handle);
+    *n = h->n;
+    *n_rows = h->n_rows;
+    *n_cams = h->n_cams;
+    return true;
+}
+
+void dense_obs_copy(void *handle, int32_t *cam, int32_t *pt, double *obs) {
+    auto *h = static_cast<DenseObs *>(handle);
+    const size_t np = h->pieces.size();
+    std::vector<int64_t> off(np + 1, 0);
+    for (size_t t = 0; t < np; ++t) off[t + 1] = off[t] + h->pieces[t].n;
+    par_for((int64_t)np, [&](int64_t t) {
+        const Piece &p = h->pieces[t];
+        if (!p.n) return;
+        std::memcpy(cam + off[t], p.cam.data(), p.n * sizeof(int32_t));
+        std::memcpy(pt + off[t], p.pt.data(), p.n * sizeof(int32_t));
+        std::memcpy(obs + 2 * off[t], p.xy.data(), 2 * p.n * sizeof(double));
+    });
+}
+
+}  // namespace sfm
 
 extern "C" int sfm_dense_obs_scan(const void *flags, int32_t dtype, int64_t flag_row_bytes, int64_t n_matrix_rows,
                                   const int64_t *rows, int64_t n_rows, int32_t n_cams, const double *fx,
@@ -77,28 +208,33 @@ extern "C" int sfm_dense_obs_scan(const void *flags, int32_t dtype, int64_t flag
     for (int64_t i = 0; i < n_rows; ++i)
         SFM_CHECK_ARG(rows[i] >= 0 && rows[i] < n_matrix_rows, "row index out of bounds of the flag matrix");
     SFM_CHECK_ARG(dtype >= 0 && dtype <= 4, "flag dtype: 0 f64, 1 f32, 2 i64, 3 i32, 4 u8/bool");
-    int nt = n_threads > 0 ? n_threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-    nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, (n_rows + 4095) / 4096));
-    auto *h = new DenseObs();
-    h->pieces.resize(nt);
-    auto work = [&](int t) {
-        const int64_t r0 = n_rows * t / nt, r1 = n_rows * (t + 1) / nt;
-        Piece &p = h->pieces[t];
-        const char *f = static_cast<const char *>(flags);
-        const char *x = reinterpret_cast<const char *>(fx), *y = reinterpret_cast<const char *>(fy);
-        switch (dtype) {
-        case 0: scan_rows<double>(f, flag_row_bytes, rows, r0, r1, n_cams, x, y, xy_row_bytes, p); break;
-        case 1: scan_rows<float>(f, flag_row_bytes, rows, r0, r1, n_cams, x, y, xy_row_bytes, p); break;
-        case 2: scan_rows<int64_t>(f, flag_row_bytes, rows, r0, r1, n_cams, x, y, xy_row_bytes, p); break;
-        case 3: scan_rows<int32_t>(f, flag_row_bytes, rows, r0, r1, n_cams, x, y, xy_row_bytes, p); break;
-        default: scan_rows<uint8_t>(f, flag_row_bytes, rows, r0, r1, n_cams, x, y, xy_row_bytes, p); break;
+    // jobs of >= 4096 rows; the pool runs them on up to 16 threads
+    int nj = n_threads > 0 ? n_threads : 64;
+    nj = (int)std::max<int64_t>(1, std::min<int64_t>(nj, (n_rows + 4095) / 4096));
+    DenseObs *h = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        if (g_pool) {
+            h = g_pool;
+            g_pool = nullptr;
         }
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
-    work(0);
-    for (auto &t : th) t.join();
-    for (auto &p : h->pieces) h->n += (int64_t)p.cam.size();
+    }
+    if (!h) h = new DenseObs();
+    if ((int)h->pieces.size() < nj) h->pieces.resize(nj);
+    for (auto &p : h->pieces) p.n = 0;
+    h->n_rows = n_rows;
+    h->n_cams = n_cams;
+    const char *f = static_cast<const char *>(flags);
+    const char *x = reinterpret_cast<const char *>(fx), *y = reinterpret_cast<const char *>(fy);
+    const bool avx = have_avx512();
+    sfm::par_for(nj, [&](int64_t t) {
+        const int64_t r0 = n_rows * t / nj, r1 = n_rows * (t + 1) / nj;
+        Piece &p = h->pieces[t];
+        if (avx) scan_dispatch<true>(dtype, f, flag_row_bytes, rows, r0, r1, n_cams, x, y, xy_row_bytes, p);
+        else scan_dispatch<false>(dtype, f, flag_row_bytes, rows, r0, r1, n_cams, x, y, xy_row_bytes, p);
+    });
+    h->n = 0;
+    for (auto &p : h->pieces) h->n += p.n;
     *handle = h;
     *n_obs = h->n;
     return 0;
@@ -108,24 +244,18 @@ extern "C" int sfm_dense_obs_read(void *handle, int32_t *cam, int32_t *pt, doubl
     SFM_CHECK_ARG(handle, "null handle");
     auto *h = static_cast<DenseObs *>(handle);
     SFM_CHECK_ARG(h->n == 0 || (cam && pt && obs), "null pointer");
-    std::vector<int64_t> off(h->pieces.size() + 1, 0);
-    for (size_t t = 0; t < h->pieces.size(); ++t) off[t + 1] = off[t] + (int64_t)h->pieces[t].cam.size();
-    auto copy = [&](size_t t) {
-        const Piece &p = h->pieces[t];
-        const size_t n = p.cam.size();
-        if (!n) return;
-        std::memcpy(cam + off[t], p.cam.data(), n * sizeof(int32_t));
-        std::memcpy(pt + off[t], p.pt.data(), n * sizeof(int32_t));
-        std::memcpy(obs + 2 * off[t], p.xy.data(), 2 * n * sizeof(double));
-    };
-    std::vector<std::thread> th;
-    for (size_t t = 1; t < h->pieces.size(); ++t) th.emplace_back(copy, t);
-    if (!h->pieces.empty()) copy(0);
-    for (auto &t : th) t.join();
+    sfm::dense_obs_copy(handle, cam, pt, obs);
     return 0;
 }
 
 extern "C" int sfm_dense_obs_free(void *handle) {
-    delete static_cast<DenseObs *>(handle);
+    auto *h = static_cast<DenseObs *>(handle);
+    if (!h) return 0;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (!g_pool) {
+        g_pool = h;  // kept for the next scan
+        return 0;
+    }
+    delete h;
     return 0;
 }

@@ -180,10 +180,19 @@ __device__ __forceinline__ bool lds_wait(const int *w, int target, Smem &S) {
 // loop (cdna_hip_programming.md T20), which serialised this solve's
 // hand-offs.  A store's record offset rides in the per-lane voffset
 // (soffset 0): the same offset handed to the soffset through readfirstlane
-// gave wrong, nondeterministic (~1e-6) solves on gfx950 although every lane
-// holds the same value (cause not isolated; the voffset form is exact and
-// as fast -- DESIGN.md section 6).  The polls' offsets stay readfirstlane'd
-// soffsets (exact; a voffset there costs VGPRs and spills the tile slots).
+// gave wrong, nondeterministic (~1e-6) solves on gfx950.  The ISA of that
+// build (round 5, tools/isa_war_scan.py) shows the likely cause: the
+// compiler reuses the soffset SGPR for the next record's offset, rewriting
+// it with a v_readfirstlane 1-5 instructions after the record's last
+// dwordx4 store.  A store wider than 8 bytes reads its operands after issue
+// (LLVM's gfx950 hazard model covers only its data VGPRs, one wait state),
+// so an SGPR soffset rewritten right behind it can move the store to the
+// next record.  No store here reads an SGPR offset.  The polls (loads) keep
+// readfirstlane'd soffsets: a load takes its address at issue -- in the
+// TREG_L build 36 poll loads have their soffset rewritten 3-4 instructions
+// later, and its solves are exact and bitwise repeatable (test_reduced_solve
+// at n = 1800, nT = 113, instantiates it) -- and a voffset there costs VGPRs
+// and spills the tile slots.
 struct Buf {
     const void *base;
     int bytes;

@@ -759,6 +759,7 @@ struct NlX {
     unsigned long long *flag;    // [NL_MAXWG] (epoch << 32) | seq of the block's last publication
     unsigned long long *abort_;  // = epoch once a poll has timed out
     unsigned long long epoch;
+    long long limit;             // poll bound in s_memrealtime ticks; < 0: time out at once (test hook)
     int nb;
 };
 constexpr int NL_MAXWG = 64;
@@ -791,6 +792,11 @@ __device__ __forceinline__ bool nlx_sum(double (&v)[NV], double (*red)[NV], cons
         };
         bool done = seen(), ab = false;
         long long t0 = -1;
+        if (X.limit < 0) {  // SFM_NLPNP_FORCE_TIMEOUT: this hand-off times out
+            if (lane == 0) __hip_atomic_store(X.abort_, X.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ab = true;
+            done = true;
+        }
         for (unsigned it = 1; !__all(done); ++it) {  // wave-uniform loop
             __builtin_amdgcn_s_sleep(1);
             if (!done) done = seen();
@@ -798,7 +804,7 @@ __device__ __forceinline__ bool nlx_sum(double (&v)[NV], double (*red)[NV], cons
                 bool a = __hip_atomic_load(X.abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == X.epoch;
                 const long long t = __builtin_amdgcn_s_memrealtime();
                 if (t0 < 0) t0 = t;
-                else if (t - t0 > NL_POLL_LIMIT) {
+                else if (t - t0 > X.limit) {
                     a = true;
                     if (lane == 0)
                         __hip_atomic_store(X.abort_, X.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1408,18 +1414,18 @@ extern "C" int sfm_nonlinear_pnp(const double *X, const double *x, int64_t N, co
     // and never more than can be resident at once (the workgroups wait on
     // each other's sums)
     int nb = std::max(1, std::min(NL_MAXWG, env_int("SFM_NLPNP_WGS", ceil_div((int64_t)N, 1024))));
-    {
-        static int resident = -1;
-        if (resident < 0) {
-            int per_cu = 0, ncu = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_nonlinear_pnp, NL2_THREADS, 0) != hipSuccess ||
-                hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
-                per_cu = ncu = 0;
-            (void)hipGetLastError();
-            resident = std::max(1, per_cu * ncu);
-        }
-        nb = std::min(nb, resident);
+    if (c->nl_resident < 0) {  // per thread context (device): no shared state between host threads
+        int per_cu = 0, ncu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_nonlinear_pnp, NL2_THREADS, 0) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
+            per_cu = ncu = 0;
+        (void)hipGetLastError();
+        c->nl_resident = std::max(1, per_cu * ncu);
     }
+    nb = std::min(nb, c->nl_resident);
+    // SFM_NLPNP_FORCE_TIMEOUT=1 (tests): the first multi-workgroup launch's
+    // first hand-off times out, so the one-workgroup retry below runs
+    const bool force_timeout = env_int("SFM_NLPNP_FORCE_TIMEOUT", 0) != 0;
     for (int attempt = 0;; ++attempt) {
     NlX xg{};
     xg.nb = nb;
@@ -1433,6 +1439,7 @@ extern "C" int sfm_nonlinear_pnp(const double *X, const double *x, int64_t N, co
         xg.flag = reinterpret_cast<unsigned long long *>(xg.part + 2 * NL_MAXWG * 32);
         xg.abort_ = xg.flag + NL_MAXWG;
         xg.epoch = ++c->nl_epoch;
+        xg.limit = force_timeout && attempt == 0 ? -1 : NL_POLL_LIMIT;
     }
     hipLaunchKernelGGL(k_nonlinear_pnp, dim3(nb), dim3(NL2_THREADS), 0, s, c->buf[0].as<double>(),
                        c->buf[1].as<double2>(), (int64_t)N, cam, dIn, dIn + 3, max_nfev, hres, xg);

@@ -40,6 +40,18 @@ extern "C" int sfm_ransac_f8_pyrandom(const double *x1, const double *x2, int64_
                                          samples_out, device);
 }
 
+// The drop-in's form of sfm_ransac_f8_pyrandom: the winner's inlier
+// positions (ascending) in split[0, n_inliers) and the outliers' in
+// split[n_inliers, N) instead of a mask -- GetInliersRANSAC.py:95-106's
+// np.where(inlier_mask)[0] and index[~inlier_mask] without a pass over the
+// mask in numpy.  n_inliers = 0 when no hypothesis wins (split untouched).
+extern "C" int sfm_ransac_f8_dropin(const double *x1, const double *x2, int64_t N, uint32_t *st, int64_t H,
+                                    double thr, int64_t *best_iter, double *F_best, int64_t *split,
+                                    int64_t *n_inliers, int device) {
+    SFM_CHECK_ARG(split && n_inliers, "null pointer");
+    return ransac_run_pysample<EpiModel>(x1, x2, N, st, H, thr, nullptr, best_iter, F_best, nullptr, nullptr,
+                                         device, split, n_inliers);
+}
 
 // One hypothesis shard [h0, h1) of sfm_ransac_f8 / sfm_ransac_f8_pyrandom
 // (SURVEY §8(e)): the shard's key (count << 32 | 0xFFFFFFFF - iteration,

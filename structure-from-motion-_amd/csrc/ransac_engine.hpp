@@ -174,15 +174,24 @@ __device__ __forceinline__ void fit_next_group(const double2 *__restrict__ x1, c
 #ifndef SFM_SCORE_FIT_OCC
 #define SFM_SCORE_FIT_OCC 8
 #endif
+// score_split bits: 1 the wave-level outlier skip after stage A, 2 the float
+// prefilter ahead of it (needs tmax, EpiModel)
+constexpr int SCORE_SKIP_A = 1, SCORE_PRE32 = 2;
 template <class M, bool FIT = false>
 __global__ void __launch_bounds__(64 * SCORE_WAVES, FIT ? SFM_SCORE_FIT_OCC : 1) k_ransac_score(const double2 *__restrict__ x1,
                                                                    const double2 *__restrict__ x2,
                                                                    int64_t N, const double *__restrict__ F,
                                                                    int64_t H, double thr,
                                                                    int32_t *__restrict__ counts, int64_t slice,
-                                                                   FitNext fn, int score_split) {
+                                                                   FitNext fn, int score_split,
+                                                                   const float4 *__restrict__ tmax) {
     __shared__ double2 s1[SCORE_TILE];
     __shared__ double2 s2[SCORE_TILE];
+    // the float prefilter's copy of the tile: per 128-pair pass, lane l holds
+    // pairs l and 64 + l as (x, x', y, y') in sA and (u, u', v, v') in sB
+    constexpr int PT = M::SPLIT ? SCORE_TILE / 2 : 1;
+    __shared__ float4 sA[PT];
+    __shared__ float4 sB[PT];
     int bx = blockIdx.x;
     if (FIT) {
         if (bx < fn.nfb) {
@@ -209,11 +218,37 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES, FIT ? SFM_SCORE_FIT_OCC : 1)
     const double thr_hi = 2.0 * (thr >= 0 ? thr * (1.0 + 1e-4) : thr * (1.0 - 1e-4));
     // gridDim.y > 1: this workgroup scores correspondences [y*slice, (y+1)*slice)
     const int64_t p0 = (int64_t)blockIdx.y * slice, p1 = min<int64_t>(N, p0 + slice);
+    // the float prefilter (sfm_geom.hpp epi_pre_setup): per hypothesis, with
+    // the coordinate bounds of this slice's tiles
+    const bool pre_fill = M::SPLIT && tmax && (score_split & SCORE_PRE32);
+    EpiPre pre;
+    pre.on = false;
+    if constexpr (M::SPLIT) {
+        if (pre_fill && active && finite) {
+            float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int64_t t = p0 / SCORE_TILE; t * SCORE_TILE < p1; ++t) {
+                const float4 q = tmax[t];
+                b = make_float4(fmaxf(b.x, q.x), fmaxf(b.y, q.y), fmaxf(b.z, q.z), fmaxf(b.w, q.w));
+            }
+            pre = epi_pre_setup(f, thr_hi, b);
+        }
+    }
     for (int64_t base = p0; base < p1; base += SCORE_TILE) {
         const int n = (int)min<int64_t>(SCORE_TILE, p1 - base);
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            s1[i] = x1[base + i];
-            s2[i] = x2[base + i];
+            const double2 p = x1[base + i], q = x2[base + i];
+            s1[i] = p;
+            s2[i] = q;
+            if constexpr (M::SPLIT) {
+                if (pre_fill) {
+                    const int l = (i >> 7) * 64 + (i & 63), h = (i >> 6) & 1;
+                    float *a = reinterpret_cast<float *>(&sA[l]), *b = reinterpret_cast<float *>(&sB[l]);
+                    a[h] = (float)p.x;
+                    a[2 + h] = (float)p.y;
+                    b[h] = (float)q.x;
+                    b[2 + h] = (float)q.y;
+                }
+            }
         }
         __syncthreads();
         if (active && finite) {
@@ -225,14 +260,19 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES, FIT ? SFM_SCORE_FIT_OCC : 1)
                 const double2 p1 = s1[j + 64 + lane], q1 = s2[j + 64 + lane];
                 bool in0 = false, in1 = false;
                 if constexpr (M::SPLIT) {
+                    if (pre.on) {  // both sets proven outliers in float: nothing to count
+                        bool o0, o1;
+                        epi_pre_test(pre, sA[(j >> 7) * 64 + lane], sB[(j >> 7) * 64 + lane], o0, o1);
+                        if (__ballot(!(o0 && o1)) == 0) continue;
+                    }
                     // stage A of both pairs; each 64-pair set whose pairs are
                     // all decided outliers there counts nothing and skips stage
                     // B (most sets: the mean cfg2 hypothesis has ~2 inliers);
                     // both sets needed: both stage Bs before either exact tail
                     const typename M::PartA a0 = M::fast_a(f, p0, q0, thr_hi);
                     const typename M::PartA a1 = M::fast_a(f, p1, q1, thr_hi);
-                    const bool n0 = !score_split || __ballot(!a0.out) != 0;
-                    const bool n1 = !score_split || __ballot(!a1.out) != 0;
+                    const bool n0 = !(score_split & SCORE_SKIP_A) || __ballot(!a0.out) != 0;
+                    const bool n1 = !(score_split & SCORE_SKIP_A) || __ballot(!a1.out) != 0;
                     if (!n0 && !n1) continue;
                     if (n0 && n1) {
                         const typename M::Part r0 = M::fast_b(a0, f, q0, thr_lo, thr_hi);
@@ -280,14 +320,13 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES, FIT ? SFM_SCORE_FIT_OCC : 1)
     }
 }
 
-// the score's wave-level outlier skip (EpiModel stage A); SFM_SCORE_SPLIT=0
-// turns it off, for same-box A/B
+// the score's wave-level outlier skip (EpiModel stage A) and its float
+// prefilter; SFM_SCORE_SPLIT=0 / SFM_SCORE_PRE=0 turn them off (same-box
+// A/B; the tests' check that the counts do not move)
 static inline int score_split_on() {
-    static const int v = [] {
-        const char *e = std::getenv("SFM_SCORE_SPLIT");
-        return e ? std::atoi(e) != 0 : 1;
-    }();
-    return v;
+    const char *e = std::getenv("SFM_SCORE_SPLIT");
+    const char *q = std::getenv("SFM_SCORE_PRE");
+    return ((e && std::atoi(e) == 0) ? 0 : SCORE_SKIP_A) | ((q && std::atoi(q) == 0) ? 0 : SCORE_PRE32);
 }
 
 // Point slices for scoring nh hypotheses: enough workgroups to put ~4 on
@@ -354,6 +393,55 @@ static inline float ev_ms(hipEvent_t a, hipEvent_t b) {
 }
 
 
+// Correspondences from the pinned host staging buffer into device memory
+// with a kernel on the compute queue (two SDMA copies plus the copy-engine
+// to compute handoff cost ~24 us before the first fit; this ~3 us), one
+// workgroup per score tile, which also records the tile's coordinate bounds
+// for the score's float prefilter: max |x|, |y|, |u|, |v| rounded up to
+// float (+inf for a non-finite coordinate).  h null: d1 / d2 already hold
+// the correspondences (bounds only).
+constexpr int TB_THREADS = SCORE_TILE;
+__device__ __forceinline__ float abs_ru(double v) {
+    const double a = fabs(v);
+    return a <= 3.0e38 ? __double2float_ru(a) : __builtin_inff();  // NaN -> inf
+}
+static __global__ void __launch_bounds__(TB_THREADS) k_stage_tiles(const double2 *__restrict__ h, int64_t N,
+                                                                   double2 *__restrict__ d1, double2 *__restrict__ d2,
+                                                                   float4 *__restrict__ tmax) {
+    __shared__ float4 red[TB_THREADS / 64];
+    const int64_t i = (int64_t)blockIdx.x * TB_THREADS + threadIdx.x;
+    float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < N) {
+        double2 p, q;
+        if (h) {
+            p = h[i];
+            q = h[N + i];
+            d1[i] = p;
+            d2[i] = q;
+        } else {
+            p = d1[i];
+            q = d2[i];
+        }
+        m = make_float4(abs_ru(p.x), abs_ru(p.y), abs_ru(q.x), abs_ru(q.y));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        m.x = fmaxf(m.x, __shfl_xor(m.x, o));
+        m.y = fmaxf(m.y, __shfl_xor(m.y, o));
+        m.z = fmaxf(m.z, __shfl_xor(m.z, o));
+        m.w = fmaxf(m.w, __shfl_xor(m.w, o));
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float4 r = red[0];
+        for (int k = 1; k < TB_THREADS / 64; ++k)
+            r = make_float4(fmaxf(r.x, red[k].x), fmaxf(r.y, red[k].y), fmaxf(r.z, red[k].z), fmaxf(r.w, red[k].w));
+        tmax[blockIdx.x] = r;
+    }
+}
+static inline int64_t n_tiles(int64_t N) { return (N + SCORE_TILE - 1) / SCORE_TILE; }
+
 // Whole RANSAC on one device: upload, fit, score, select, download.
 // Timings (sfm_last_timings): upload, kernels, download, score, fit, select.
 template <class M>
@@ -373,9 +461,11 @@ int ransac_run(const double *x1, const double *x2, int64_t N, const int32_t *sam
         (rc = c->buf[2].reserve((size_t)H * M::K * sizeof(int32_t))) ||
         (rc = c->buf[3].reserve((size_t)H * 9 * sizeof(double))) ||
         (rc = c->buf[4].reserve((size_t)H * sizeof(int32_t))) ||
-        (rc = c->buf[5].reserve(16 * sizeof(double) + (size_t)N)))
+        (rc = c->buf[5].reserve(16 * sizeof(double) + (size_t)N)) ||
+        (rc = c->buf[10].reserve((size_t)n_tiles(N) * sizeof(float4))))
         return rc;
     double2 *d1 = c->buf[0].as<double2>(), *d2 = c->buf[1].as<double2>();
+    float4 *tmax = c->buf[10].as<float4>();
     int32_t *ds = c->buf[2].as<int32_t>(), *dcnt = c->buf[4].as<int32_t>();
     double *dF = c->buf[3].as<double>();
     int64_t *dbest = c->buf[5].as<int64_t>();
@@ -386,13 +476,18 @@ int ransac_run(const double *x1, const double *x2, int64_t N, const int32_t *sam
     SFM_HIP(hipMemcpyAsync(d1, x1, pb, hipMemcpyHostToDevice, s));
     SFM_HIP(hipMemcpyAsync(d2, x2, pb, hipMemcpyHostToDevice, s));
     SFM_HIP(hipMemcpyAsync(ds, samples, (size_t)H * M::K * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    if (M::SPLIT) {
+        hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)n_tiles(N)), dim3(TB_THREADS), 0, s, (const double2 *)nullptr,
+                           N, d1, d2, tmax);
+        SFM_HIP(hipGetLastError());
+    }
     SFM_HIP(hipEventRecord(c->ev[1], s));
     int ny;
     const int64_t slice = score_slice(H, N, &ny);
     if ((rc = launch_fit<M>(d1, d2, ds, H, dF, ny > 1 ? dcnt : nullptr, s))) return rc;
     SFM_HIP(hipEventRecord(c->ev[2], s));
     hipLaunchKernelGGL((k_ransac_score<M, false>), dim3(ceil_div(H, SCORE_WAVES), ny), dim3(64 * SCORE_WAVES), 0, s,
-                       d1, d2, N, dF, H, thr, dcnt, slice, FitNext{}, score_split_on());
+                       d1, d2, N, dF, H, thr, dcnt, slice, FitNext{}, score_split_on(), tmax);
     SFM_HIP(hipGetLastError());
     SFM_HIP(hipEventRecord(c->ev[3], s));
     hipLaunchKernelGGL(k_ransac_select<M>, dim3(1), dim3(1024), 0, s, d1, d2, N, dF, dcnt, H, thr, dbest, dFb, dmask);
@@ -408,18 +503,6 @@ int ransac_run(const double *x1, const double *x2, int64_t N, const int32_t *sam
                          ev_ms(c->ev[2], c->ev[3]), ev_ms(c->ev[1], c->ev[2]), ev_ms(c->ev[3], c->ev[4])};
     set_timings(t, 6);
     return 0;
-}
-
-// Correspondences from the pinned host staging buffer into device memory
-// with a kernel on the compute queue (two SDMA copies plus the copy-engine
-// to compute handoff cost ~24 us before the first fit; this ~3 us).
-static __global__ void __launch_bounds__(256) k_stage_pts(const double2 *__restrict__ h, int64_t N, double2 *__restrict__ d1,
-                                                   double2 *__restrict__ d2) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < N) {
-        d1[i] = h[i];
-        d2[i] = h[N + i];
-    }
 }
 
 // The drop-in's whole call with the samples drawn inside it: the CPython
@@ -504,6 +587,7 @@ struct ScorePipe {
     double *dF;      // models of hypotheses off..: dF + 9 (h - off)
     int32_t *dcnt;   // counts likewise
     int64_t off;
+    const float4 *tmax;      // per-tile coordinate bounds (k_stage_tiles) for the float prefilter
     int64_t pa = 0, pb = 0;  // the fitted, not yet scored piece
     bool fused = M::GROUP_FIT && ransac_fused();
 
@@ -514,13 +598,13 @@ struct ScorePipe {
         if constexpr (M::GROUP_FIT) {
             if (fn) {
                 hipLaunchKernelGGL((k_ransac_score<M, true>), grid, dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
-                                   dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, *fn, score_split_on());
+                                   dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, *fn, score_split_on(), tmax);
                 SFM_HIP(hipGetLastError());
                 return 0;
             }
         }
         hipLaunchKernelGGL((k_ransac_score<M, false>), grid, dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
-                           dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, FitNext{}, score_split_on());
+                           dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, FitNext{}, score_split_on(), tmax);
         SFM_HIP(hipGetLastError());
         return 0;
     }
@@ -555,9 +639,10 @@ struct ScorePipe {
 template <class M>
 int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t *st, int64_t H, double thr,
                         int32_t *counts_out, int64_t *best_iter, double *F_best, uint8_t *best_mask,
-                        int32_t *samples_out, int device) {
+                        int32_t *samples_out, int device, int64_t *split = nullptr, int64_t *n_inliers = nullptr) {
     SFM_CHECK_ARG(N >= M::K && H >= 0, "need N >= sample size and H >= 0");
-    SFM_CHECK_ARG(x1 && x2 && st && best_iter && F_best && best_mask, "null pointer");
+    SFM_CHECK_ARG(x1 && x2 && st && best_iter && F_best && (best_mask || (split && n_inliers)), "null pointer");
+    if (n_inliers) *n_inliers = 0;
     SFM_CHECK_ARG(N < ((int64_t)1 << 31) && st[624] <= 624, "bad sizes / MT19937 position");
     *best_iter = -1;
     if (H == 0) return 0;
@@ -570,11 +655,13 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
     if ((rc = c->buf[0].reserve(pb)) || (rc = c->buf[1].reserve(pb)) ||
         (rc = c->buf[3].reserve((size_t)H * 9 * sizeof(double))) ||
         (rc = c->buf[4].reserve((size_t)H * sizeof(int32_t))) ||
+        (rc = c->buf[10].reserve((size_t)n_tiles(N) * sizeof(float4))) ||
         (rc = c->pinned.reserve(sbp + xoff_of(N) + 2 * pb)))
         return rc;
     double2 *d1 = c->buf[0].as<double2>(), *d2 = c->buf[1].as<double2>();
     int32_t *dcnt = c->buf[4].as<int32_t>();
     double *dF = c->buf[3].as<double>();
+    float4 *tmax = c->buf[10].as<float4>();
     // Zero-copy through pinned host memory: the fit kernels read each chunk's
     // sample rows straight from where the host replay wrote them, and the
     // select kernel writes (best, F, mask) back the same way, so no SDMA copy
@@ -593,13 +680,13 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
     hipStream_t s = c->stream;
     const bool tm = call_timing();
     if (tm) SFM_HIP(hipEventRecord(c->ev[0], s));
-    hipLaunchKernelGGL(k_stage_pts, dim3(ceil_div(N, 256)), dim3(256), 0, s, reinterpret_cast<const double2 *>(hx), N,
-                       d1, d2);
+    hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)n_tiles(N)), dim3(TB_THREADS), 0, s,
+                       reinterpret_cast<const double2 *>(hx), N, d1, d2, tmax);
     SFM_HIP(hipGetLastError());
     if (tm) SFM_HIP(hipEventRecord(c->ev[1], s));
     PySampler ps(st, N, M::K);
     double t_draw = 0;
-    ScorePipe<M> pipe{d1, d2, N, thr, s, dF, dcnt, 0};
+    ScorePipe<M> pipe{d1, d2, N, thr, s, dF, dcnt, 0, tmax};
     for (int64_t h0 = 0, h1; h0 < H; h0 = h1) {
         h1 = rp_next(h0, H);
         const auto ta = std::chrono::steady_clock::now();
@@ -619,8 +706,20 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
     *best_iter = *dbest;
     if (*best_iter >= 0) {
         std::memcpy(F_best, dFb, 9 * sizeof(double));
-        std::memcpy(best_mask, dmask, (size_t)N);
-    } else {
+        if (best_mask) std::memcpy(best_mask, dmask, (size_t)N);
+        if (split) {  // inlier positions ascending, then the outliers' (branch-free)
+            int64_t ni = 0;
+            for (int64_t i = 0; i < N; ++i) ni += dmask[i] != 0;
+            int64_t a = 0, b = ni;
+            for (int64_t i = 0; i < N; ++i) {
+                const bool in = dmask[i] != 0;
+                split[in ? a : b] = i;
+                a += in;
+                b += !in;
+            }
+            *n_inliers = ni;
+        }
+    } else if (best_mask) {
         std::memset(best_mask, 0, (size_t)N);
     }
     if (samples_out) std::memcpy(samples_out, hs, sb);
@@ -683,11 +782,13 @@ int ransac_run_range(const double *x1, const double *x2, int64_t N, const int32_
     if ((rc = c->buf[0].reserve(pb)) || (rc = c->buf[1].reserve(pb)) ||
         (rc = c->buf[3].reserve((size_t)std::max<int64_t>(nh, 1) * 9 * sizeof(double))) ||
         (rc = c->buf[4].reserve((size_t)std::max<int64_t>(nh, 1) * sizeof(int32_t))) ||
+        (rc = c->buf[10].reserve((size_t)n_tiles(N) * sizeof(float4))) ||
         (rc = c->pinned.reserve(sbp + xoff_of(N) + 2 * pb)))
         return rc;
     double2 *d1 = c->buf[0].as<double2>(), *d2 = c->buf[1].as<double2>();
     int32_t *dcnt = c->buf[4].as<int32_t>();
     double *dF = c->buf[3].as<double>();
+    float4 *tmax = c->buf[10].as<float4>();
     int32_t *hs = c->pinned.as<int32_t>();
     char *hout = c->pinned.as<char>() + sbp;
     char *hx = hout + xoff_of(N);
@@ -698,13 +799,13 @@ int ransac_run_range(const double *x1, const double *x2, int64_t N, const int32_
     hipStream_t s = c->stream;
     const bool tm = call_timing();
     if (tm) SFM_HIP(hipEventRecord(c->ev[0], s));
-    hipLaunchKernelGGL(k_stage_pts, dim3(ceil_div(N, 256)), dim3(256), 0, s, reinterpret_cast<const double2 *>(hx), N,
-                       d1, d2);
+    hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)n_tiles(N)), dim3(TB_THREADS), 0, s,
+                       reinterpret_cast<const double2 *>(hx), N, d1, d2, tmax);
     SFM_HIP(hipGetLastError());
     if (tm) SFM_HIP(hipEventRecord(c->ev[1], s));
     double t_draw = 0;
     // fit + score the hypotheses of the shard, hypothesis h at dF + 9 (h - r0)
-    ScorePipe<M> pipe{d1, d2, N, thr, s, dF, dcnt, r0};
+    ScorePipe<M> pipe{d1, d2, N, thr, s, dF, dcnt, r0, tmax};
     if (st) {
         PySampler ps(st, N, M::K);
         for (int64_t h0 = 0, h1; h0 < H; h0 = h1) {

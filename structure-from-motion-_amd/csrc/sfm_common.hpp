@@ -98,6 +98,7 @@ struct ThreadCtx {
     int gjr_nT = 0;
     void *nl_sync = nullptr;     // sfm_nonlinear_pnp's cross-workgroup sums (zeroed once; epoch-tagged flags)
     unsigned nl_epoch = 0;
+    int nl_resident = -1;        // sfm_nonlinear_pnp: workgroups resident at once (computed on first use)
     ~ThreadCtx() {
         if (stream) {
             (void)hipSetDevice(device);

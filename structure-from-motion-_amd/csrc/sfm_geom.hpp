@@ -125,6 +125,90 @@ __device__ __forceinline__ EpiPart epi_fast_b(const EpiPartA &a, const double *F
     return r;
 }
 
+// A float prefilter ahead of stage A (round 5): two pairs per packed FP32
+// instruction (v_pk_fma_f32), seven instructions a pair against stage A's
+// ~20 FP64 ones, proving "outlier" for the pairs far from the threshold.
+// The proof is rigorous, not a tolerance.  Per hypothesis F is scaled by a
+// power of two g = s F (max |g| in [0.5, 1), exact; the reference's d1 is
+// then |e'| / (sqrt(qa') + s 1e-8) in the scaled terms) and rounded to
+// float.  With the point coordinates bounded by the slice's maxima X, Y, U, V
+// (<= 2^24, k_stage_tiles), the float evaluation
+//   a_k = fma(g_k1, y, fma(g_k0, x, g_k2)),  e = fma(u, a0, fma(v, a1, a2))
+// (at most 4 + 3 roundings per term, inputs included) obeys
+//   |e_ref| >= |e~| - E,  E = 1e-6 Mt + 2^-70,  Mt = (U, V, 1) |g| (X, Y, 1)
+//   sqrt(qa_ref) <= (1 + 1e-6) sqrt(qa~) + 1e-6 At + 2^-60,
+//   At = |((|g0| X + |g1| Y + |g2|), (|g3| X + |g4| Y + |g5|))|
+// (gamma_8 of float is 4.8e-7 < 1e-6; the reference's own FP64 rounding and
+// float underflow of tiny g or coordinates fit in the absolute terms).  Stage
+// A's condition |e_ref| > thr_hi2 (sqrt(qa_ref) + s 1e-8) therefore holds when
+//   |e~| > K1 sqrt(qa~) + K0,   K1 = thr_hi2 (1 + 1e-6),
+//   K0 = thr_hi2 (1e-6 At + 2^-60 + s 1e-8) + E,
+// and, squared with (a + b)^2 <= (1 + d) a^2 + (1 + 1/d) b^2 (d = 2^-8), when
+//   e~^2 > q1 qa~ + q0,  q1 = (1 + d) K1^2, q0 = (1 + 1/d) K0^2,
+// both rounded up to float after a (1 + 2^-20) factor that covers the three
+// roundings of evaluating this test in float.  Inf / NaN anywhere makes the
+// comparison false: the pair is simply not proven (stage A decides it).
+struct EpiPre {
+    float g[9];
+    float q1, q0;
+    bool on;  // wave-uniform: the prefilter applies to this hypothesis and slice
+};
+
+// per hypothesis f (finite) and slice bounds b = (X, Y, U, V)
+__device__ __forceinline__ EpiPre epi_pre_setup(const double *f, double thr_hi2, float4 b) {
+    EpiPre r;
+    r.on = false;
+    double m = 0.0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) m = fmax(m, fabs(f[k]));
+    const float lim = 0x1p24f;
+    if (!(m > 0.0) || !(b.x <= lim && b.y <= lim && b.z <= lim && b.w <= lim)) return r;
+    if (!(thr_hi2 >= 0x1p-60 && thr_hi2 <= 0x1p60)) return r;
+    const int ex = ilogb(m);
+    // |scale| <= 2^400 both ways: the reference's own FP64 evaluation then
+    // neither overflows (a non-finite qa would make its d1 0) nor loses more
+    // than 2^-270 to underflow in the scaled terms
+    if (ex < -399 || ex > 398) return r;
+    double g[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) g[k] = ldexp(f[k], -ex - 1);
+    const double c = ldexp(1e-8, -ex - 1);
+    const double X = b.x, Y = b.y, U = b.z, V = b.w;
+    const double A0 = fabs(g[0]) * X + fabs(g[1]) * Y + fabs(g[2]);
+    const double A1 = fabs(g[3]) * X + fabs(g[4]) * Y + fabs(g[5]);
+    const double A2 = fabs(g[6]) * X + fabs(g[7]) * Y + fabs(g[8]);
+    const double Mt = U * A0 + V * A1 + A2;
+    const double At = sqrt(A0 * A0 + A1 * A1);
+    const double E = 1e-6 * Mt + 0x1p-70;
+    const double K1 = thr_hi2 * (1.0 + 1e-6);
+    const double K0 = thr_hi2 * (1e-6 * At + 0x1p-60 + c) + E;
+    const double d = 0x1p-8;
+    r.q1 = __double2float_ru((1.0 + d) * K1 * K1 * (1.0 + 0x1p-20));
+    r.q0 = __double2float_ru((1.0 + 1.0 / d) * K0 * K0 * (1.0 + 0x1p-20));
+#pragma unroll
+    for (int k = 0; k < 9; ++k) r.g[k] = (float)g[k];
+    r.on = true;
+    return r;
+}
+
+typedef float epi_f2 __attribute__((ext_vector_type(2)));
+
+// two pairs: pa = (x_0, x_1, y_0, y_1), pb = (u_0, u_1, v_0, v_1) (pair 0 in
+// the low halves); out0 / out1: proven outliers
+__device__ __forceinline__ void epi_pre_test(const EpiPre &p, float4 pa, float4 pb, bool &out0, bool &out1) {
+    const epi_f2 x = {pa.x, pa.y}, y = {pa.z, pa.w}, u = {pb.x, pb.y}, v = {pb.z, pb.w};
+    auto bc = [](float s) { return epi_f2{s, s}; };
+    const epi_f2 a0 = __builtin_elementwise_fma(bc(p.g[1]), y, __builtin_elementwise_fma(bc(p.g[0]), x, bc(p.g[2])));
+    const epi_f2 a1 = __builtin_elementwise_fma(bc(p.g[4]), y, __builtin_elementwise_fma(bc(p.g[3]), x, bc(p.g[5])));
+    const epi_f2 a2 = __builtin_elementwise_fma(bc(p.g[7]), y, __builtin_elementwise_fma(bc(p.g[6]), x, bc(p.g[8])));
+    const epi_f2 e = __builtin_elementwise_fma(u, a0, __builtin_elementwise_fma(v, a1, a2));
+    const epi_f2 qa = __builtin_elementwise_fma(a0, a0, a1 * a1);
+    const epi_f2 rhs = __builtin_elementwise_fma(bc(p.q1), qa, bc(p.q0));
+    const epi_f2 e2 = e * e;
+    out0 = e2.x > rhs.x;
+    out1 = e2.y > rhs.y;
+}
+
 // the exact tail of epi_inlier from epi_fast's terms (same operations)
 __device__ __forceinline__ bool epi_exact(const EpiPart &r, double thr) {
 #pragma clang fp contract(off)

@@ -99,6 +99,34 @@ def test_sample_table_replays_python_random(n, k, H):
     assert after == random.getstate()
 
 
+@pytest.mark.parametrize("direct", [True, False])
+def test_mt_state_round_trip_both_paths(monkeypatch, direct):
+    """The global generator's state out to the C-ABI and back: in place
+    (the verified CPython layout, _MT_DIRECT) and through getstate /
+    setstate; the gauss_next cache is never touched, positions across a
+    twist (623, 624, 0) survive, and a sample_table replay leaves the stream
+    where H random.sample calls leave it."""
+    import _sfmcore
+    if direct and not _sfmcore._MT_DIRECT:
+        pytest.skip("CPython layout not verified here")
+    monkeypatch.setattr(_sfmcore, "_MT_DIRECT", direct)
+    for pos in (0, 5, 623, 624):
+        random.seed(pos)
+        random.gauss(0, 1)  # leaves a cached gauss_next
+        v, st, g = random.getstate()
+        random.setstate((v, st[:624] + (pos,), g))
+        before = random.getstate()
+        h, s, gg = _sfmcore._mt_state()
+        assert tuple(s) == before[1]
+        _sfmcore._mt_restore(h, s, gg)
+        assert random.getstate() == before
+        t = _sfmcore.sample_table(5000, 8, 300)
+        after = random.getstate()
+        random.setstate(before)
+        ref = np.array([random.sample(range(5000), 8) for _ in range(300)], dtype=np.int32)
+        assert np.array_equal(t, ref) and after == random.getstate()
+
+
 def test_ba_observation_order_matches_reference_loop():
     """Dense flags -> COO exactly as BundleAdjustment.py:164-169 assembles it."""
     from BundleAdjustment import _observations

@@ -690,6 +690,25 @@ def test_nonlinear_pnp_workgroups_vs_oracle(core, monkeypatch, wgs, n, outl):
     assert abs(cg - co) <= 1e-9 * co + 1e-12
 
 
+def test_nonlinear_pnp_timeout_retry_equals_one_workgroup(core, monkeypatch):
+    """A cross-workgroup hand-off that times out (forced by
+    SFM_NLPNP_FORCE_TIMEOUT=1: every workgroup of the 8-workgroup launch
+    aborts at its first hand-off) makes the host re-run the solve on one
+    workgroup: the result is bitwise the one-workgroup solve's."""
+    X, x, C, R = _pnp_scene(8000, 33, 0.2)
+    C0 = C + 0.05
+    R0 = syn.rotvec_to_matrix([0.03, -0.13, 0.02])[0]
+    monkeypatch.setenv("SFM_NLPNP_WGS", "1")
+    C1, R1, i1 = core.nonlinear_pnp(X, x, K, C0, R0)
+    monkeypatch.setenv("SFM_NLPNP_WGS", "8")
+    monkeypatch.setenv("SFM_NLPNP_FORCE_TIMEOUT", "1")
+    Cr, Rr, ir = core.nonlinear_pnp(X, x, K, C0, R0)
+    assert ir == i1 and np.array_equal(Cr, C1) and np.array_equal(Rr, R1)
+    monkeypatch.delenv("SFM_NLPNP_FORCE_TIMEOUT")
+    C8, R8, i8 = core.nonlinear_pnp(X, x, K, C0, R0)  # and the 8-workgroup solve itself still runs
+    assert i8 == i1 and np.abs(C8 - C1).max() <= 1e-9 * max(1.0, np.abs(C1).max())
+
+
 def test_nonlinear_pnp_rank_deficient_flags(core):
     """A rank-deficient Jacobian (one point repeated): the Gram factor needs
     the shift, the third CholeskyQR pass runs and the flags say so; lmdif
@@ -832,6 +851,36 @@ def test_perform_bundle_adjustment_coo_equals_dense(core, capsys):
     assert all(np.array_equal(u, v) for u, v in zip(a[0], b[0]))
     out = capsys.readouterr().out
     assert out.count("Bundle adjustment completed") == 2
+
+
+def test_ba_reused_device_blocks_poisoned(core, monkeypatch, capsys):
+    """Problems reuse the device blocks, stream and events of destroyed ones
+    (the create/destroy cache): with every reused block filled with 0xFF
+    first (SFM_POOL_POISON=1) the solves of a sequence of problems -- sizes
+    shrinking, so each one gets blocks that held another problem's data --
+    are bitwise those of the first, unpoisoned run, through both entries
+    (COO arrays and the dense scan)."""
+    from BundleAdjustment import perform_bundle_adjustment
+    probs = [syn.ba_problem(12, 5000, 6, seed=5, dense=True), syn.ba_problem(10, 3000, 5, seed=6, dense=True),
+             syn.ba_problem(8, 2000, 4, seed=7, dense=True)]
+
+    def run():
+        out = []
+        for p in probs:
+            cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
+            c, x, rep = core.ba_lm(cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K)
+            d = perform_bundle_adjustment(p["X0"], p["filtered_world_coords"], p["feature_x"], p["feature_y"],
+                                          p["flags"], list(p["R0"]), list(p["C0"]), K, 0)
+            out.append((c, x, rep["cost"], d[2], np.array(d[0])))
+        return out
+
+    clean = run()
+    monkeypatch.setenv("SFM_POOL_POISON", "1")
+    poisoned = run()
+    for a, b in zip(clean, poisoned):
+        for u, v in zip(a, b):
+            assert np.array_equal(u, v)
+    assert capsys.readouterr().out.count("Bundle adjustment completed") == 2 * len(probs)
 
 
 def test_ba_failure_contract(core, capsys):
@@ -1238,6 +1287,42 @@ def test_ransac_fast_tests_exact_at_threshold(core):
         assert np.array_equal(core.ransac_mask(x1, x2, Hm, float(thr), model=4), ref), thr
         if counts[0] > 0:
             assert np.array_equal(mask, ref), thr
+
+
+@pytest.mark.parametrize("scale", [1e-3, 1.0, 1e3, 1e5, 3e7])
+def test_ransac_float_prefilter_never_changes_a_count(core, monkeypatch, scale):
+    """The score's float prefilter (sfm_geom.hpp epi_pre_setup / epi_pre_test:
+    packed FP32, proving outliers with a rigorous error bound) leaves every
+    per-hypothesis count equal to the reference expression's count with that
+    hypothesis' F (O.epi_err, bit-exact to numpy) and to the counts without
+    the prefilter (SFM_SCORE_PRE=0): coordinates from 1e-3 to 3e7 (above
+    2^24 the prefilter switches itself off), thresholds placed on the first
+    hypothesis' distances and one ulp around them, a NaN correspondence (its
+    tile's bound is inf) and both entries (given table, in-call draws)."""
+    x1, x2, _, _ = syn.two_view(n=2500, seed=13)
+    x1, x2 = x1 * scale, x2 * scale
+    x1[1700] = np.nan
+    rng = np.random.default_rng(5)
+    H = 48
+    samples = np.stack([rng.choice(1600, 8, replace=False) for _ in range(H)]).astype(np.int32)
+    # each hypothesis' F as the score sees it: the winner of a one-row table
+    Fs = [core.ransac_f8(x1, x2, samples[h:h + 1], 1e300)[1] for h in range(H)]
+    errs = [O.epi_err(x1, x2, F) for F in Fs]
+    d = np.sort(errs[0][np.isfinite(errs[0]) & (errs[0] > 0)])
+    pick = d[(np.array([0.005, 0.05, 0.3]) * (len(d) - 1)).astype(int)]
+    for thr in list(pick) + list(np.nextafter(pick, np.inf)) + list(np.nextafter(pick, -np.inf)) + [0.5 * scale]:
+        ref = np.array([(e < thr).sum() for e in errs], dtype=np.int32)
+        monkeypatch.delenv("SFM_SCORE_PRE", raising=False)
+        got = core.ransac_f8(x1, x2, samples, float(thr), want_counts=True)[3]
+        random.seed(21)
+        pyr = core.ransac_f8_pyrandom(x1, x2, 40, float(thr), want_counts=True)[3]
+        monkeypatch.setenv("SFM_SCORE_PRE", "0")
+        off = core.ransac_f8(x1, x2, samples, float(thr), want_counts=True)[3]
+        random.seed(21)
+        pyr_off = core.ransac_f8_pyrandom(x1, x2, 40, float(thr), want_counts=True)[3]
+        assert np.array_equal(got, ref), thr
+        assert np.array_equal(off, ref), thr
+        assert np.array_equal(pyr, pyr_off), thr
 
 
 def test_pnp_fast_test_exact_at_threshold(core):

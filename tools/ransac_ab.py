@@ -1,0 +1,44 @@
+"""A/B of the RANSAC score's float prefilter at cfg2 (5000 corr, 16384
+hypotheses, thr 0.06), alternated in one process (SFM_SCORE_PRE is read per
+call): the drop-in GetInliersRANSAC's wall time, the library call alone, and
+the one-shot score kernel (HIP events).  Prints medians."""
+import os
+import random
+import statistics as stt
+import sys
+import time
+
+sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "structure-from-motion-_amd")]
+import numpy as np  # noqa: E402
+import _sfmcore as core  # noqa: E402
+import sfm_synthetic as syn  # noqa: E402
+from GetInliersRANSAC import GetInliersRANSAC  # noqa: E402
+
+x1, x2, _, _ = syn.two_view(n=5000, seed=0)
+idx = np.arange(5000)
+H = 16384
+random.seed(0)
+table = core.sample_table(5000, 8, H)
+res = {}
+core.set_call_timing(True)
+for rep in range(40):
+    for mode in ("1", "0"):
+        os.environ["SFM_SCORE_PRE"] = mode
+        random.seed(0)
+        t = time.perf_counter()
+        GetInliersRANSAC(x1, x2, idx, 0.06, H)
+        res.setdefault(("dropin", mode), []).append((time.perf_counter() - t) * 1e3)
+        random.seed(0)
+        t = time.perf_counter()
+        core.ransac_f8_pyrandom(x1, x2, H, 0.06)
+        res.setdefault(("call", mode), []).append((time.perf_counter() - t) * 1e3)
+        tm = core.last_timings()
+        res.setdefault(("call_kernels", mode), []).append(tm[1])
+        res.setdefault(("call_draw", mode), []).append(tm[6])
+        core.ransac_f8(x1, x2, table, 0.06)
+        tm = core.last_timings()
+        res.setdefault(("oneshot_score", mode), []).append(tm[3])
+        res.setdefault(("oneshot_fit", mode), []).append(tm[4])
+for k in sorted(res):
+    v = res[k][5:]
+    print(f"{k[0]:14s} pre={k[1]}  median {stt.median(v):.4f} ms  min {min(v):.4f}")
