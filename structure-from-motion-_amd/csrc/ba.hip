@@ -371,6 +371,17 @@ __global__ void __launch_bounds__(PT_THREADS) k_linearize(int64_t np_, const int
 // partials are summed over a different grid.
 constexpr int LIN_PRE = 4;
 constexpr int LIN_CL_THREADS = 256;
+// the cameras' LDS stride in doubles (round 5): the
+// camera reads are ds_read_b128, 16 lanes a group, 4 banks a lane; 12
+// doubles (48 dwords) left the rows on 8 of the 16 bank positions (48 c mod
+// 64), 14 (56 B of padding a camera) uses all 16: cfg5 LDS bank-conflict
+// cycles 1.37 M -> 0.84 M per launch, 0.0179 -> 0.0174 ms.  An odd stride
+// (13) spreads 8-B reads further but loses the 16-B alignment: b64 reads,
+// 0.0184 ms.
+#ifndef SFM_LIN_CAM_STRIDE
+#define SFM_LIN_CAM_STRIDE 14
+#endif
+constexpr int LIN_CAM = SFM_LIN_CAM_STRIDE;
 template <int G, int NT = LIN_CL_THREADS>
 __global__ void __launch_bounds__(NT) k_linearize_cl(int64_t np_, int32_t nc, const int32_t *__restrict__ pstart,
                                                      const int32_t *__restrict__ cam, const double2 *__restrict__ obs,
@@ -398,7 +409,7 @@ __global__ void __launch_bounds__(NT) k_linearize_cl(int64_t np_, int32_t nc, co
     fetch((int64_t)blockIdx.x * NT + threadIdx.x, cur);
     extern __shared__ __attribute__((aligned(16))) double lin_cam[];
 #pragma unroll 4
-    for (int i = threadIdx.x; i < 12 * nc; i += NT) lin_cam[i] = Rt[i];
+    for (int i = threadIdx.x; i < 12 * nc; i += NT) lin_cam[LIN_CAM * (i / 12) + i % 12] = Rt[i];
     __syncthreads();
     double K[9];
 #pragma unroll
@@ -422,7 +433,7 @@ __global__ void __launch_bounds__(NT) k_linearize_cl(int64_t np_, int32_t nc, co
         const double x[3] = {cur.x[0], cur.x[1], cur.x[2]};
         double V[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
         auto add = [&](int32_t c, double2 ob) {
-            const double *Rt_c = lin_cam + 12 * c;
+            const double *Rt_c = lin_cam + LIN_CAM * c;
             double r[2], A[2][3], q[3];
             obs_model(Rt_c, x, K, ob, r, A, q);
             double Jp[2][3];
@@ -2395,7 +2406,16 @@ constexpr int BS_PRE = 6;  // observations per lane prefetched by k_backsub_tria
 // CL: the cameras (Rt 12 | Rt_new 12 | dc 6 doubles, 240 B each) staged in
 // LDS once per workgroup, so the per-observation camera reads (30 doubles,
 // 240 B) are LDS reads instead of L1/L2 gathers
-constexpr int BS_CAM = 30;
+// 30 doubles (60 dwords) already put the 16-B camera reads on all 16 bank
+// positions of a ds_read_b128 group; an odd stride (31, 33) lost the 16-B
+// alignment and ran 0.051 -> 0.060 ms at cfg5 (round 5).  What conflicts
+// remain (0.53 of the LDS cycles) are random cameras of a lane group
+// sharing a position, inherent to the gather.
+#ifndef SFM_BS_CAM_STRIDE
+#define SFM_BS_CAM_STRIDE 30
+#endif
+constexpr int BS_CAM = SFM_BS_CAM_STRIDE;
+static_assert(BS_CAM >= 30, "Rt 12 | Rt_new 12 | dc 6");
 constexpr int BS_CAM_LDS_MAX = 64 * 1024;
 template <int G, bool CL, int NT = PT_THREADS>
 __global__ void __launch_bounds__(NT) k_backsub_trial(int64_t np_, int32_t nc, const int32_t *__restrict__ pstart,
@@ -2653,7 +2673,7 @@ static int backsub_cl_blocks(int32_t nc, int ncu, int max_blocks, int nt) {
 // (0: more than 64 KB of cameras, or SFM_LINEARIZE_CAM_LDS=0)
 static int linearize_cl_blocks(int32_t nc, int ncu, int max_blocks) {
     if (env_int("SFM_LINEARIZE_CAM_LDS", 1) == 0) return 0;
-    const size_t lds = (size_t)96 * nc;
+    const size_t lds = (size_t)8 * LIN_CAM * nc;
     if (nc < 1 || lds > (size_t)BS_CAM_LDS_MAX) return 0;
     int nb = 0;
     auto occ = [&](auto kern) {
@@ -4536,7 +4556,7 @@ static int run_linearize(sfm_ba_problem *p, int par, int want_cost) {
         const int gc = lanes_per_point("SFM_LINEARIZE_LANES", 2);
         const int nb = std::max(1, std::min(ceil_div(p->np * gc, LIN_CL_THREADS), p->lin_cl_blocks));
 #define SFM_LINC(G)                                                                                               \
-    hipLaunchKernelGGL(k_linearize_cl<G>, dim3(nb), dim3(LIN_CL_THREADS), (size_t)96 * p->nc, s, p->np, p->nc,     \
+    hipLaunchKernelGGL(k_linearize_cl<G>, dim3(nb), dim3(LIN_CL_THREADS), (size_t)8 * LIN_CAM * p->nc, s, p->np, p->nc,     \
                        p->d_pstart, p->d_cam, p->d_obs, p->K, p->d_Rt, p->d_X, p->d_Vg, p->d_partial, p->d_count,  \
                        p->d_scal + 8, want_cost, glin, p->gtol, p->d_nbig)
         switch (gc) { case 1: SFM_LINC(1); break; case 2: SFM_LINC(2); break; case 4: SFM_LINC(4); break; default: SFM_LINC(8); }

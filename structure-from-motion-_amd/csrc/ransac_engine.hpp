@@ -167,31 +167,32 @@ __device__ __forceinline__ void fit_next_group(const double2 *__restrict__ x1, c
     f8_points_group8(p.x, p.y, q.x, q.y, fn.F + 9 * h);
 }
 
-// waves per SIMD the fused launch is compiled for: the score alone needs 50
-// VGPRs, the fit's rank-2 step (with its Jacobi fallback) ~120, so the cap
-// makes the fit spill (off the critical path) rather than the score lose
-// occupancy
+// waves per SIMD the fused launch is compiled for: the F score needs 64
+// VGPRs (six waves a SIMD: its 48-KB LDS tiles allow three workgroups a CU),
+// the fit's rank-2 step (with its Jacobi fallback) ~120, so the cap makes
+// the fit spill (off the critical path) rather than the score lose
+// occupancy (round 5: 8 could not be met, the compiler then gave the whole
+// launch 126 VGPRs)
 #ifndef SFM_SCORE_FIT_OCC
-#define SFM_SCORE_FIT_OCC 8
+#define SFM_SCORE_FIT_OCC 6
 #endif
 // score_split bits: 1 the wave-level outlier skip after stage A, 2 the float
-// prefilter ahead of it (needs tmax, EpiModel)
+// prefilter ahead of it (k_epi_score)
 constexpr int SCORE_SKIP_A = 1, SCORE_PRE32 = 2;
+
+// The H score (and, before round 5, the F one): correspondence tiles staged
+// in LDS, every wave sweeping them for its hypothesis, both fast decisions
+// of a pass before either branch to the exact tail.
 template <class M, bool FIT = false>
 __global__ void __launch_bounds__(64 * SCORE_WAVES, FIT ? SFM_SCORE_FIT_OCC : 1) k_ransac_score(const double2 *__restrict__ x1,
                                                                    const double2 *__restrict__ x2,
                                                                    int64_t N, const double *__restrict__ F,
                                                                    int64_t H, double thr,
                                                                    int32_t *__restrict__ counts, int64_t slice,
-                                                                   FitNext fn, int score_split,
-                                                                   const float4 *__restrict__ tmax) {
+                                                                   FitNext fn) {
+    static_assert(!M::SPLIT, "the F model scores in k_epi_score");
     __shared__ double2 s1[SCORE_TILE];
     __shared__ double2 s2[SCORE_TILE];
-    // the float prefilter's copy of the tile: per 128-pair pass, lane l holds
-    // pairs l and 64 + l as (x, x', y, y') in sA and (u, u', v, v') in sB
-    constexpr int PT = M::SPLIT ? SCORE_TILE / 2 : 1;
-    __shared__ float4 sA[PT];
-    __shared__ float4 sB[PT];
     int bx = blockIdx.x;
     if (FIT) {
         if (bx < fn.nfb) {
@@ -218,37 +219,11 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES, FIT ? SFM_SCORE_FIT_OCC : 1)
     const double thr_hi = 2.0 * (thr >= 0 ? thr * (1.0 + 1e-4) : thr * (1.0 - 1e-4));
     // gridDim.y > 1: this workgroup scores correspondences [y*slice, (y+1)*slice)
     const int64_t p0 = (int64_t)blockIdx.y * slice, p1 = min<int64_t>(N, p0 + slice);
-    // the float prefilter (sfm_geom.hpp epi_pre_setup): per hypothesis, with
-    // the coordinate bounds of this slice's tiles
-    const bool pre_fill = M::SPLIT && tmax && (score_split & SCORE_PRE32);
-    EpiPre pre;
-    pre.on = false;
-    if constexpr (M::SPLIT) {
-        if (pre_fill && active && finite) {
-            float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
-            for (int64_t t = p0 / SCORE_TILE; t * SCORE_TILE < p1; ++t) {
-                const float4 q = tmax[t];
-                b = make_float4(fmaxf(b.x, q.x), fmaxf(b.y, q.y), fmaxf(b.z, q.z), fmaxf(b.w, q.w));
-            }
-            pre = epi_pre_setup(f, thr_hi, b);
-        }
-    }
     for (int64_t base = p0; base < p1; base += SCORE_TILE) {
         const int n = (int)min<int64_t>(SCORE_TILE, p1 - base);
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            const double2 p = x1[base + i], q = x2[base + i];
-            s1[i] = p;
-            s2[i] = q;
-            if constexpr (M::SPLIT) {
-                if (pre_fill) {
-                    const int l = (i >> 7) * 64 + (i & 63), h = (i >> 6) & 1;
-                    float *a = reinterpret_cast<float *>(&sA[l]), *b = reinterpret_cast<float *>(&sB[l]);
-                    a[h] = (float)p.x;
-                    a[2 + h] = (float)p.y;
-                    b[h] = (float)q.x;
-                    b[2 + h] = (float)q.y;
-                }
-            }
+            s1[i] = x1[base + i];
+            s2[i] = x2[base + i];
         }
         __syncthreads();
         if (active && finite) {
@@ -258,46 +233,11 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES, FIT ? SFM_SCORE_FIT_OCC : 1)
             for (; j + 128 <= n; j += 128) {
                 const double2 p0 = s1[j + lane], q0 = s2[j + lane];
                 const double2 p1 = s1[j + 64 + lane], q1 = s2[j + 64 + lane];
-                bool in0 = false, in1 = false;
-                if constexpr (M::SPLIT) {
-                    if (pre.on) {  // both sets proven outliers in float: nothing to count
-                        bool o0, o1;
-                        epi_pre_test(pre, sA[(j >> 7) * 64 + lane], sB[(j >> 7) * 64 + lane], o0, o1);
-                        if (__ballot(!(o0 && o1)) == 0) continue;
-                    }
-                    // stage A of both pairs; each 64-pair set whose pairs are
-                    // all decided outliers there counts nothing and skips stage
-                    // B (most sets: the mean cfg2 hypothesis has ~2 inliers);
-                    // both sets needed: both stage Bs before either exact tail
-                    const typename M::PartA a0 = M::fast_a(f, p0, q0, thr_hi);
-                    const typename M::PartA a1 = M::fast_a(f, p1, q1, thr_hi);
-                    const bool n0 = !(score_split & SCORE_SKIP_A) || __ballot(!a0.out) != 0;
-                    const bool n1 = !(score_split & SCORE_SKIP_A) || __ballot(!a1.out) != 0;
-                    if (!n0 && !n1) continue;
-                    if (n0 && n1) {
-                        const typename M::Part r0 = M::fast_b(a0, f, q0, thr_lo, thr_hi);
-                        const typename M::Part r1 = M::fast_b(a1, f, q1, thr_lo, thr_hi);
-                        in0 = r0.in;
-                        in1 = r1.in;
-                        if (r0.unsure) in0 = M::exact(r0, p0, q0, f, thr);
-                        if (r1.unsure) in1 = M::exact(r1, p1, q1, f, thr);
-                    } else {
-                        const bool first = n0;  // the one set that needs stage B
-                        const typename M::Part r = M::fast_b(first ? a0 : a1, f, first ? q0 : q1, thr_lo, thr_hi);
-                        bool in = r.in;
-                        if (r.unsure) in = M::exact(r, first ? p0 : p1, first ? q0 : q1, f, thr);
-                        in0 = first && in;
-                        in1 = !first && in;
-                    }
-                } else {
-                    // both fast decisions before either branch to the exact tail
-                    const typename M::Part r0 = M::fast(f, p0, q0, thr, thr_lo, thr_hi);
-                    const typename M::Part r1 = M::fast(f, p1, q1, thr, thr_lo, thr_hi);
-                    in0 = r0.in;
-                    in1 = r1.in;
-                    if (r0.unsure) in0 = M::exact(r0, p0, q0, f, thr);
-                    if (r1.unsure) in1 = M::exact(r1, p1, q1, f, thr);
-                }
+                const typename M::Part r0 = M::fast(f, p0, q0, thr, thr_lo, thr_hi);
+                const typename M::Part r1 = M::fast(f, p1, q1, thr, thr_lo, thr_hi);
+                bool in0 = r0.in, in1 = r1.in;
+                if (r0.unsure) in0 = M::exact(r0, p0, q0, f, thr);
+                if (r1.unsure) in1 = M::exact(r1, p1, q1, f, thr);
                 cnt += __popcll(__ballot(in0)) + __popcll(__ballot(in1));
             }
             for (; j < n; j += 64) {
@@ -307,6 +247,152 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES, FIT ? SFM_SCORE_FIT_OCC : 1)
                     const double2 p = s1[i], q = s2[i];
                     inl = M::inlier_fast(f, p, q, thr, thr_lo, thr_hi);
                 }
+                cnt += __popcll(__ballot(inl));
+            }
+        }
+        __syncthreads();
+    }
+    if (active && lane == 0) {
+        if (gridDim.y == 1)
+            counts[h] = cnt;
+        else
+            atomicAdd(counts + h, cnt);
+    }
+}
+
+// The F score with the float prefilter (round 5).  One wave per hypothesis,
+// as the round-4 score, whose FP64 test (stage A, the wave-level skip, stage
+// B, the exact tail) stays for the 64-pair sets the prefilter does not prove:
+// a 128-pair pass first runs the packed float test (7 instructions a pair)
+// on the tile's float copy -- per lane pairs l and 64 + l as (x, x', y, y')
+// then (u, u', v, v'), copied in 16-B pieces from the array k_stage_tiles
+// writes -- and reads the FP64 correspondences from the LDS tile only when a
+// set is left.  cfg2: the prefilter proves ~89 % of the sets (stage A 95 %);
+// the FP64 sets read from global memory instead had cost 70 of the score's
+// 85 us (L2 round trips), the float sweep alone 16 us.  pk null or
+// SFM_SCORE_PRE=0: every set in FP64.
+#ifndef SFM_EPI_OCC
+#define SFM_EPI_OCC 1
+#endif
+
+// the FP64 test of two 64-pair sets (pair a = lane, b = 64 + lane) for one
+// hypothesis: the number of inliers among the 128 pairs
+__device__ __forceinline__ int epi_sets_f64(const double *f, double2 pa, double2 qa, double2 pb, double2 qb, double thr,
+                                            double thr_lo, double thr_hi, int score_split) {
+    using M = EpiModel;
+    const M::PartA sa = M::fast_a(f, pa, qa, thr_hi);
+    const M::PartA sb = M::fast_a(f, pb, qb, thr_hi);
+    const bool n0 = !(score_split & SCORE_SKIP_A) || __ballot(!sa.out) != 0;
+    const bool n1 = !(score_split & SCORE_SKIP_A) || __ballot(!sb.out) != 0;
+    if (!n0 && !n1) return 0;
+    bool in0 = false, in1 = false;
+    if (n0 && n1) {
+        const M::Part r0 = M::fast_b(sa, f, qa, thr_lo, thr_hi);
+        const M::Part r1 = M::fast_b(sb, f, qb, thr_lo, thr_hi);
+        in0 = r0.in;
+        in1 = r1.in;
+        if (r0.unsure) in0 = M::exact(r0, pa, qa, f, thr);
+        if (r1.unsure) in1 = M::exact(r1, pb, qb, f, thr);
+    } else {
+        const bool first = n0;  // the one set that needs stage B
+        const M::Part r = M::fast_b(first ? sa : sb, f, first ? qa : qb, thr_lo, thr_hi);
+        bool in = r.in;
+        if (r.unsure) in = M::exact(r, first ? pa : pb, first ? qa : qb, f, thr);
+        in0 = first && in;
+        in1 = !first && in;
+    }
+    return __popcll(__ballot(in0)) + __popcll(__ballot(in1));
+}
+
+// ... and of one 64-pair set (the other one proven by the prefilter)
+__device__ __forceinline__ int epi_set_f64(const double *f, double2 p, double2 q, double thr, double thr_lo,
+                                           double thr_hi, int score_split) {
+    using M = EpiModel;
+    const M::PartA a = M::fast_a(f, p, q, thr_hi);
+    if ((score_split & SCORE_SKIP_A) && __ballot(!a.out) == 0) return 0;
+    const M::Part r = M::fast_b(a, f, q, thr_lo, thr_hi);
+    bool in = r.in;
+    if (r.unsure) in = M::exact(r, p, q, f, thr);
+    return __popcll(__ballot(in));
+}
+
+template <bool FIT = false>
+__global__ void __launch_bounds__(64 * SCORE_WAVES, FIT ? SFM_SCORE_FIT_OCC : SFM_EPI_OCC)
+    k_epi_score(const double2 *__restrict__ x1, const double2 *__restrict__ x2, int64_t N, const double *__restrict__ F,
+                int64_t H, double thr, int32_t *__restrict__ counts, int64_t slice, FitNext fn, int score_split,
+                const float4 *__restrict__ tmax, const float4 *__restrict__ pk) {
+    using M = EpiModel;
+    __shared__ double2 s1[SCORE_TILE];
+    __shared__ double2 s2[SCORE_TILE];
+    __shared__ float4 sP[SCORE_TILE];
+    int bx = blockIdx.x;
+    if (FIT) {
+        if (bx < fn.nfb) {
+            if (blockIdx.y == 0) fit_next_group<M>(x1, x2, fn);
+            return;
+        }
+        bx -= fn.nfb;
+    }
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t h = (int64_t)bx * SCORE_WAVES + wave;
+    const bool active = h < H;
+    double f[9];
+    int finite = 1;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        f[k] = active ? F[9 * h + k] : 0.0;
+        finite &= isfinite(f[k]) ? 1 : 0;
+    }
+    int cnt = 0;
+    const double thr_lo = 2.0 * (thr >= 0 ? thr * (1.0 - 1e-4) : thr * (1.0 + 1e-4));
+    const double thr_hi = 2.0 * (thr >= 0 ? thr * (1.0 + 1e-4) : thr * (1.0 - 1e-4));
+    const int64_t p0 = (int64_t)blockIdx.y * slice, p1 = min<int64_t>(N, p0 + slice);
+    const bool use_pre = pk && tmax && (score_split & SCORE_PRE32);  // workgroup-uniform
+    EpiPre pre;
+    pre.on = false;
+    if (use_pre && active && finite) {
+        float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int64_t t = p0 / SCORE_TILE; t * SCORE_TILE < p1; ++t) {
+            const float4 q = tmax[t];
+            b = make_float4(fmaxf(b.x, q.x), fmaxf(b.y, q.y), fmaxf(b.z, q.z), fmaxf(b.w, q.w));
+        }
+        pre = epi_pre_uniform(epi_pre_setup(f, thr_hi, b));
+    }
+    for (int64_t base = p0; base < p1; base += SCORE_TILE) {
+        const int n = (int)min<int64_t>(SCORE_TILE, p1 - base);
+        const int nfull = n & ~127;
+        for (int i = threadIdx.x; i < n; i += 64 * SCORE_WAVES) {
+            s1[i] = x1[base + i];
+            s2[i] = x2[base + i];
+        }
+        if (use_pre) {
+            const float4 *src = pk + base;  // a tile starts on a 128-pair pass
+            for (int i = threadIdx.x; i < nfull; i += 64 * SCORE_WAVES) sP[i] = src[i];
+        }
+        __syncthreads();
+        if (active && finite) {
+            int j = 0;
+            for (; j < nfull; j += 128) {
+                bool n0 = true, n1 = true;  // the sets the FP64 test must see
+                if (pre.on) {  // a set proven outliers in float counts nothing
+                    bool o0, o1;
+                    epi_pre_test(pre, sP[j + lane], sP[j + 64 + lane], o0, o1);
+                    n0 = __ballot(!o0) != 0;
+                    n1 = __ballot(!o1) != 0;
+                    if (!n0 && !n1) continue;
+                }
+                if (n0 && n1)
+                    cnt += epi_sets_f64(f, s1[j + lane], s2[j + lane], s1[j + 64 + lane], s2[j + 64 + lane], thr,
+                                        thr_lo, thr_hi, score_split);
+                else
+                    cnt += n0 ? epi_set_f64(f, s1[j + lane], s2[j + lane], thr, thr_lo, thr_hi, score_split)
+                              : epi_set_f64(f, s1[j + 64 + lane], s2[j + 64 + lane], thr, thr_lo, thr_hi, score_split);
+            }
+            for (; j < n; j += 64) {  // the partial last pass, one 64-pair set at a time
+                const int i = j + lane;
+                bool inl = false;
+                if (i < n) inl = M::inlier_fast(f, s1[i], s2[i], thr, thr_lo, thr_hi);
                 cnt += __popcll(__ballot(inl));
             }
         }
@@ -332,8 +418,13 @@ static inline int score_split_on() {
 // Point slices for scoring nh hypotheses: enough workgroups to put ~4 on
 // every CU (a lone 8-wave group per CU leaves the DP pipes latency-bound),
 // slices a whole number of LDS tiles.
-static inline int64_t score_slice(int64_t nh, int64_t N, int *ny) {
-    const int64_t wg = (nh + SCORE_WAVES - 1) / SCORE_WAVES;
+// hypotheses one score workgroup takes (one a wave)
+template <class M>
+constexpr int score_per_wg() {
+    return SCORE_WAVES;
+}
+static inline int64_t score_slice(int64_t nh, int64_t N, int *ny, int per_wg) {
+    const int64_t wg = (nh + per_wg - 1) / per_wg;
     const int64_t tiles = (N + SCORE_TILE - 1) / SCORE_TILE;
     int64_t y = std::min<int64_t>(tiles, std::max<int64_t>(1, (1024 + wg - 1) / wg));
     const int64_t per = (tiles + y - 1) / y;
@@ -407,7 +498,7 @@ __device__ __forceinline__ float abs_ru(double v) {
 }
 static __global__ void __launch_bounds__(TB_THREADS) k_stage_tiles(const double2 *__restrict__ h, int64_t N,
                                                                    double2 *__restrict__ d1, double2 *__restrict__ d2,
-                                                                   float4 *__restrict__ tmax) {
+                                                                   float4 *__restrict__ tmax, float4 *__restrict__ pk) {
     __shared__ float4 red[TB_THREADS / 64];
     const int64_t i = (int64_t)blockIdx.x * TB_THREADS + threadIdx.x;
     float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -423,6 +514,15 @@ static __global__ void __launch_bounds__(TB_THREADS) k_stage_tiles(const double2
             q = d2[i];
         }
         m = make_float4(abs_ru(p.x), abs_ru(p.y), abs_ru(q.x), abs_ru(q.y));
+        if (pk) {  // the score's packed float copy (k_epi_score)
+            const int64_t b = i >> 7;
+            const int r = (int)(i & 127), l = r & 63, hh = r >> 6;
+            float *A = reinterpret_cast<float *>(pk + b * 128 + l), *B = reinterpret_cast<float *>(pk + b * 128 + 64 + l);
+            A[hh] = (float)p.x;
+            A[2 + hh] = (float)p.y;
+            B[hh] = (float)q.x;
+            B[2 + hh] = (float)q.y;
+        }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -441,6 +541,7 @@ static __global__ void __launch_bounds__(TB_THREADS) k_stage_tiles(const double2
     }
 }
 static inline int64_t n_tiles(int64_t N) { return (N + SCORE_TILE - 1) / SCORE_TILE; }
+static inline size_t pk_bytes(int64_t N) { return (size_t)((N + 127) / 128) * 128 * sizeof(float4); }
 
 // Whole RANSAC on one device: upload, fit, score, select, download.
 // Timings (sfm_last_timings): upload, kernels, download, score, fit, select.
@@ -462,10 +563,10 @@ int ransac_run(const double *x1, const double *x2, int64_t N, const int32_t *sam
         (rc = c->buf[3].reserve((size_t)H * 9 * sizeof(double))) ||
         (rc = c->buf[4].reserve((size_t)H * sizeof(int32_t))) ||
         (rc = c->buf[5].reserve(16 * sizeof(double) + (size_t)N)) ||
-        (rc = c->buf[10].reserve((size_t)n_tiles(N) * sizeof(float4))))
+        (rc = c->buf[10].reserve((size_t)n_tiles(N) * sizeof(float4))) || (rc = c->buf[9].reserve(pk_bytes(N))))
         return rc;
     double2 *d1 = c->buf[0].as<double2>(), *d2 = c->buf[1].as<double2>();
-    float4 *tmax = c->buf[10].as<float4>();
+    float4 *tmax = c->buf[10].as<float4>(), *pk = c->buf[9].as<float4>();
     int32_t *ds = c->buf[2].as<int32_t>(), *dcnt = c->buf[4].as<int32_t>();
     double *dF = c->buf[3].as<double>();
     int64_t *dbest = c->buf[5].as<int64_t>();
@@ -478,16 +579,20 @@ int ransac_run(const double *x1, const double *x2, int64_t N, const int32_t *sam
     SFM_HIP(hipMemcpyAsync(ds, samples, (size_t)H * M::K * sizeof(int32_t), hipMemcpyHostToDevice, s));
     if (M::SPLIT) {
         hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)n_tiles(N)), dim3(TB_THREADS), 0, s, (const double2 *)nullptr,
-                           N, d1, d2, tmax);
+                           N, d1, d2, tmax, pk);
         SFM_HIP(hipGetLastError());
     }
     SFM_HIP(hipEventRecord(c->ev[1], s));
     int ny;
-    const int64_t slice = score_slice(H, N, &ny);
+    const int64_t slice = score_slice(H, N, &ny, score_per_wg<M>());
     if ((rc = launch_fit<M>(d1, d2, ds, H, dF, ny > 1 ? dcnt : nullptr, s))) return rc;
     SFM_HIP(hipEventRecord(c->ev[2], s));
-    hipLaunchKernelGGL((k_ransac_score<M, false>), dim3(ceil_div(H, SCORE_WAVES), ny), dim3(64 * SCORE_WAVES), 0, s,
-                       d1, d2, N, dF, H, thr, dcnt, slice, FitNext{}, score_split_on(), tmax);
+    if constexpr (M::SPLIT)
+        hipLaunchKernelGGL((k_epi_score<false>), dim3(ceil_div(H, score_per_wg<M>()), ny), dim3(64 * SCORE_WAVES), 0, s,
+                           d1, d2, N, dF, H, thr, dcnt, slice, FitNext{}, score_split_on(), tmax, pk);
+    else
+        hipLaunchKernelGGL((k_ransac_score<M, false>), dim3(ceil_div(H, SCORE_WAVES), ny), dim3(64 * SCORE_WAVES), 0, s,
+                           d1, d2, N, dF, H, thr, dcnt, slice, FitNext{});
     SFM_HIP(hipGetLastError());
     SFM_HIP(hipEventRecord(c->ev[3], s));
     hipLaunchKernelGGL(k_ransac_select<M>, dim3(1), dim3(1024), 0, s, d1, d2, N, dF, dcnt, H, thr, dbest, dFb, dmask);
@@ -587,24 +692,26 @@ struct ScorePipe {
     double *dF;      // models of hypotheses off..: dF + 9 (h - off)
     int32_t *dcnt;   // counts likewise
     int64_t off;
-    const float4 *tmax;      // per-tile coordinate bounds (k_stage_tiles) for the float prefilter
+    const float4 *tmax, *pk;  // per-tile coordinate bounds and the packed float copy (k_stage_tiles)
     int64_t pa = 0, pb = 0;  // the fitted, not yet scored piece
     bool fused = M::GROUP_FIT && ransac_fused();
 
     int score(int64_t a, int64_t b, const FitNext *fn) {
         int ny;
-        const int64_t n = b - a, slice = score_slice(n, N, &ny);
-        const dim3 grid((unsigned)(ceil_div(n, SCORE_WAVES) + (fn ? fn->nfb : 0)), ny);
-        if constexpr (M::GROUP_FIT) {
-            if (fn) {
-                hipLaunchKernelGGL((k_ransac_score<M, true>), grid, dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
-                                   dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, *fn, score_split_on(), tmax);
-                SFM_HIP(hipGetLastError());
-                return 0;
-            }
+        const int64_t n = b - a, slice = score_slice(n, N, &ny, score_per_wg<M>());
+        const dim3 grid((unsigned)(ceil_div(n, score_per_wg<M>()) + (fn ? fn->nfb : 0)), ny);
+        if constexpr (M::SPLIT) {
+            if (fn)
+                hipLaunchKernelGGL((k_epi_score<true>), grid, dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
+                                   dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, *fn, score_split_on(), tmax, pk);
+            else
+                hipLaunchKernelGGL((k_epi_score<false>), grid, dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
+                                   dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, FitNext{}, score_split_on(), tmax,
+                                   pk);
+        } else {  // the H model (no group fit: its fits run on their own)
+            hipLaunchKernelGGL((k_ransac_score<M, false>), grid, dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
+                               dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, FitNext{});
         }
-        hipLaunchKernelGGL((k_ransac_score<M, false>), grid, dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
-                           dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, FitNext{}, score_split_on(), tmax);
         SFM_HIP(hipGetLastError());
         return 0;
     }
@@ -612,7 +719,7 @@ struct ScorePipe {
     int add(int64_t a, int64_t b, const int32_t *rows) {
         if (b <= a) return 0;
         int ny, rc;
-        (void)score_slice(b - a, N, &ny);
+        (void)score_slice(b - a, N, &ny, score_per_wg<M>());  // as score() will cut it
         int32_t *cz = ny > 1 ? dcnt + (a - off) : nullptr;
         if (!fused) {
             if ((rc = launch_fit<M>(d1, d2, rows, b - a, dF + (a - off) * 9, cz, s))) return rc;
@@ -655,13 +762,13 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
     if ((rc = c->buf[0].reserve(pb)) || (rc = c->buf[1].reserve(pb)) ||
         (rc = c->buf[3].reserve((size_t)H * 9 * sizeof(double))) ||
         (rc = c->buf[4].reserve((size_t)H * sizeof(int32_t))) ||
-        (rc = c->buf[10].reserve((size_t)n_tiles(N) * sizeof(float4))) ||
+        (rc = c->buf[10].reserve((size_t)n_tiles(N) * sizeof(float4))) || (rc = c->buf[9].reserve(pk_bytes(N))) ||
         (rc = c->pinned.reserve(sbp + xoff_of(N) + 2 * pb)))
         return rc;
     double2 *d1 = c->buf[0].as<double2>(), *d2 = c->buf[1].as<double2>();
     int32_t *dcnt = c->buf[4].as<int32_t>();
     double *dF = c->buf[3].as<double>();
-    float4 *tmax = c->buf[10].as<float4>();
+    float4 *tmax = c->buf[10].as<float4>(), *pk = c->buf[9].as<float4>();
     // Zero-copy through pinned host memory: the fit kernels read each chunk's
     // sample rows straight from where the host replay wrote them, and the
     // select kernel writes (best, F, mask) back the same way, so no SDMA copy
@@ -681,12 +788,12 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
     const bool tm = call_timing();
     if (tm) SFM_HIP(hipEventRecord(c->ev[0], s));
     hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)n_tiles(N)), dim3(TB_THREADS), 0, s,
-                       reinterpret_cast<const double2 *>(hx), N, d1, d2, tmax);
+                       reinterpret_cast<const double2 *>(hx), N, d1, d2, tmax, pk);
     SFM_HIP(hipGetLastError());
     if (tm) SFM_HIP(hipEventRecord(c->ev[1], s));
     PySampler ps(st, N, M::K);
     double t_draw = 0;
-    ScorePipe<M> pipe{d1, d2, N, thr, s, dF, dcnt, 0, tmax};
+    ScorePipe<M> pipe{d1, d2, N, thr, s, dF, dcnt, 0, tmax, pk};
     for (int64_t h0 = 0, h1; h0 < H; h0 = h1) {
         h1 = rp_next(h0, H);
         const auto ta = std::chrono::steady_clock::now();
@@ -782,13 +889,13 @@ int ransac_run_range(const double *x1, const double *x2, int64_t N, const int32_
     if ((rc = c->buf[0].reserve(pb)) || (rc = c->buf[1].reserve(pb)) ||
         (rc = c->buf[3].reserve((size_t)std::max<int64_t>(nh, 1) * 9 * sizeof(double))) ||
         (rc = c->buf[4].reserve((size_t)std::max<int64_t>(nh, 1) * sizeof(int32_t))) ||
-        (rc = c->buf[10].reserve((size_t)n_tiles(N) * sizeof(float4))) ||
+        (rc = c->buf[10].reserve((size_t)n_tiles(N) * sizeof(float4))) || (rc = c->buf[9].reserve(pk_bytes(N))) ||
         (rc = c->pinned.reserve(sbp + xoff_of(N) + 2 * pb)))
         return rc;
     double2 *d1 = c->buf[0].as<double2>(), *d2 = c->buf[1].as<double2>();
     int32_t *dcnt = c->buf[4].as<int32_t>();
     double *dF = c->buf[3].as<double>();
-    float4 *tmax = c->buf[10].as<float4>();
+    float4 *tmax = c->buf[10].as<float4>(), *pk = c->buf[9].as<float4>();
     int32_t *hs = c->pinned.as<int32_t>();
     char *hout = c->pinned.as<char>() + sbp;
     char *hx = hout + xoff_of(N);
@@ -800,12 +907,12 @@ int ransac_run_range(const double *x1, const double *x2, int64_t N, const int32_
     const bool tm = call_timing();
     if (tm) SFM_HIP(hipEventRecord(c->ev[0], s));
     hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)n_tiles(N)), dim3(TB_THREADS), 0, s,
-                       reinterpret_cast<const double2 *>(hx), N, d1, d2, tmax);
+                       reinterpret_cast<const double2 *>(hx), N, d1, d2, tmax, pk);
     SFM_HIP(hipGetLastError());
     if (tm) SFM_HIP(hipEventRecord(c->ev[1], s));
     double t_draw = 0;
     // fit + score the hypotheses of the shard, hypothesis h at dF + 9 (h - r0)
-    ScorePipe<M> pipe{d1, d2, N, thr, s, dF, dcnt, r0, tmax};
+    ScorePipe<M> pipe{d1, d2, N, thr, s, dF, dcnt, r0, tmax, pk};
     if (st) {
         PySampler ps(st, N, M::K);
         for (int64_t h0 = 0, h1; h0 < H; h0 = h1) {

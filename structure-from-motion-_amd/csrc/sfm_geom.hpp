@@ -135,14 +135,15 @@ __device__ __forceinline__ EpiPart epi_fast_b(const EpiPartA &a, const double *F
 // (<= 2^24, k_stage_tiles), the float evaluation
 //   a_k = fma(g_k1, y, fma(g_k0, x, g_k2)),  e = fma(u, a0, fma(v, a1, a2))
 // (at most 4 + 3 roundings per term, inputs included) obeys
-//   |e_ref| >= |e~| - E,  E = 1e-6 Mt + 2^-70,  Mt = (U, V, 1) |g| (X, Y, 1)
-//   sqrt(qa_ref) <= (1 + 1e-6) sqrt(qa~) + 1e-6 At + 2^-60,
+//   |e_ref| >= |e~| - E,  E = 5e-7 Mt + 2^-70,  Mt = (U, V, 1) |g| (X, Y, 1)
+//   sqrt(qa_ref) <= (1 + 1e-6) sqrt(qa~) + 3e-7 At + 2^-60,
 //   At = |((|g0| X + |g1| Y + |g2|), (|g3| X + |g4| Y + |g5|))|
-// (gamma_8 of float is 4.8e-7 < 1e-6; the reference's own FP64 rounding and
-// float underflow of tiny g or coordinates fit in the absolute terms).  Stage
+// (a_k carries at most 4 roundings a term, gamma_4 = 2.4e-7 of A_k; e adds
+// 3, 7u = 4.2e-7 of Mt; the reference's own FP64 rounding and float
+// underflow of tiny g or coordinates fit in the absolute terms).  Stage
 // A's condition |e_ref| > thr_hi2 (sqrt(qa_ref) + s 1e-8) therefore holds when
 //   |e~| > K1 sqrt(qa~) + K0,   K1 = thr_hi2 (1 + 1e-6),
-//   K0 = thr_hi2 (1e-6 At + 2^-60 + s 1e-8) + E,
+//   K0 = thr_hi2 (3e-7 At + 2^-60 + s 1e-8) + E,
 // and, squared with (a + b)^2 <= (1 + d) a^2 + (1 + 1/d) b^2 (d = 2^-8), when
 //   e~^2 > q1 qa~ + q0,  q1 = (1 + d) K1^2, q0 = (1 + 1/d) K0^2,
 // both rounded up to float after a (1 + 2^-20) factor that covers the three
@@ -179,15 +180,26 @@ __device__ __forceinline__ EpiPre epi_pre_setup(const double *f, double thr_hi2,
     const double A2 = fabs(g[6]) * X + fabs(g[7]) * Y + fabs(g[8]);
     const double Mt = U * A0 + V * A1 + A2;
     const double At = sqrt(A0 * A0 + A1 * A1);
-    const double E = 1e-6 * Mt + 0x1p-70;
+    const double E = 5e-7 * Mt + 0x1p-70;
     const double K1 = thr_hi2 * (1.0 + 1e-6);
-    const double K0 = thr_hi2 * (1e-6 * At + 0x1p-60 + c) + E;
+    const double K0 = thr_hi2 * (3e-7 * At + 0x1p-60 + c) + E;
     const double d = 0x1p-8;
     r.q1 = __double2float_ru((1.0 + d) * K1 * K1 * (1.0 + 0x1p-20));
     r.q0 = __double2float_ru((1.0 + 1.0 / d) * K0 * K0 * (1.0 + 0x1p-20));
 #pragma unroll
     for (int k = 0; k < 9; ++k) r.g[k] = (float)g[k];
     r.on = true;
+    return r;
+}
+// the same, its values in scalar registers (wave-uniform: f and b are), so
+// the packed test takes them as broadcast SGPR operands instead of VGPR pairs
+__device__ __forceinline__ EpiPre epi_pre_uniform(const EpiPre &p) {
+    EpiPre r;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) r.g[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(p.g[k])));
+    r.q1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(p.q1)));
+    r.q0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(p.q0)));
+    r.on = __builtin_amdgcn_readfirstlane((int)p.on) != 0;
     return r;
 }
 

@@ -1,4 +1,4 @@
-# GPU session: -m gpu suite, the RANSAC prefilter A/B, bench, create/obs phases.
+# GPU session: -m gpu suite, RANSAC drop-in vs the round-4 build (abso/head), smoke, bench.
 set -o pipefail
 mkdir -p gpurun_out
 step() {  # step NAME SECONDS CMD...
@@ -9,9 +9,10 @@ step() {  # step NAME SECONDS CMD...
     if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
 TAILN=3 step tests 700 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests -m gpu
-TAILN=12 step rab 300 python tools/ransac_ab.py
+: > gpurun_out/rab.txt
+for r in 1 2; do for d in abso/head structure-from-motion-_amd; do
+  timeout -k 10 120 python tools/ransac_ab.py $d 1 >> gpurun_out/rab.txt 2>&1 || { echo "rab $d failed"; exit 1; }
+done; done
+grep -E "package|dropin|oneshot_score|call_kernels|call " gpurun_out/rab.txt | sed 's#.*/repo/##'
 TAILN=2 step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
 TAILN=1 step bench 400 python bench.py
-TAILN=4 step create5 200 python tools/create_once.py cfg5
-TAILN=4 step create4 200 python tools/create_once.py cfg4
-TAILN=8 step obs5 300 python tools/obs_probe.py cfg5

@@ -8,7 +8,13 @@ import statistics as stt
 import sys
 import time
 
-sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "structure-from-motion-_amd")]
+# argv: [PKGDIR] [MODES]: a package build to load (default the tree's), and
+# the SFM_SCORE_PRE values to alternate (default "1,0")
+_here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path[:0] = [os.path.join(_here, "structure-from-motion-_amd")]
+if len(sys.argv) > 1 and sys.argv[1] != "-":
+    sys.path.insert(0, os.path.abspath(sys.argv[1]))
+MODES = sys.argv[2].split(",") if len(sys.argv) > 2 else ["1", "0"]
 import numpy as np  # noqa: E402
 import _sfmcore as core  # noqa: E402
 import sfm_synthetic as syn  # noqa: E402
@@ -21,8 +27,8 @@ random.seed(0)
 table = core.sample_table(5000, 8, H)
 res = {}
 core.set_call_timing(True)
-for rep in range(40):
-    for mode in ("1", "0"):
+for rep in range(30):
+    for mode in MODES:
         os.environ["SFM_SCORE_PRE"] = mode
         random.seed(0)
         t = time.perf_counter()
@@ -39,6 +45,7 @@ for rep in range(40):
         tm = core.last_timings()
         res.setdefault(("oneshot_score", mode), []).append(tm[3])
         res.setdefault(("oneshot_fit", mode), []).append(tm[4])
+print("package", core.__file__)
 for k in sorted(res):
     v = res[k][5:]
     print(f"{k[0]:14s} pre={k[1]}  median {stt.median(v):.4f} ms  min {min(v):.4f}")
