@@ -432,6 +432,17 @@ def ransac_leg(args, world, rank, local_rank, comm):
         random.seed(0)  # the winner's iteration (the drop-in returns inlier positions and F only)
         best, F, mask, _, _ = core.ransac_f8_pyrandom(x1, x2, H, 0.06, device=local_rank)
         out["host_sampling_ms"] = round(float(core.last_timings()[6]), 3)
+        # the drop-in path's own GPU time (HIP events inside the call: the
+        # chunked fits + scores, and the whole span to the select's end)
+        core.set_call_timing(True)
+        dk = []
+        for _ in range(reps):
+            random.seed(0)
+            core.ransac_f8_pyrandom(x1, x2, H, 0.06, device=local_rank)
+            tm = core.last_timings()
+            dk.append((tm[3], tm[1]))
+        core.set_call_timing(False)
+        dropin_fit_score, dropin_span = (float(np.median([v[i] for v in dk])) for i in range(2))
         out["end_to_end_call"] = "GetInliersRANSAC(points1, points2, index, 0.06, n_max=H), the drop-in's whole call"
     else:
         h0, h1 = sfm_dist.hypothesis_range(H, world, rank)
@@ -474,6 +485,13 @@ def ransac_leg(args, world, rank, local_rank, comm):
                  "kernels_tflops": round(all_flops / (k_all * 1e-3) / 1e12, 2), "peak_tflops": FP64_PEAK_TFLOPS,
                  "score_frac": round(score_flops / (k_score * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 4),
                  "formula": "score: H*N*50 flop; kernels: H*(N*50 + 25e3) flop (SURVEY §8(d)); algorithmic-equivalent: the score skips the second stage of the test for waves of proven outliers, so it executes fewer flops"}})
+    if world == 1:
+        out["fp64"].update({
+            "dropin_fit_score_ms": round(dropin_fit_score, 4), "dropin_span_ms": round(dropin_span, 4),
+            "dropin_tflops": round(all_flops / (dropin_fit_score * 1e-3) / 1e12, 2),
+            "dropin_frac": round(all_flops / (dropin_fit_score * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 4),
+            "dropin_note": "the drop-in path's own fits + scores (chunked, in-call sampling; HIP events from the "
+                           "first fit to the last score), not the one-shot given-table launch"})
     return out, (x1, x2, samples)
 
 

@@ -26,6 +26,7 @@
 #include "sfm_geom.hpp"
 #include "pyrandom.hpp"
 #include "select.hpp"
+#include "host_pool.hpp"
 
 namespace sfm {
 
@@ -153,12 +154,12 @@ struct FitNext {
     int32_t *counts;      // zeroed when the next score is point-sliced, else null
     int nfb;              // fit workgroups (64 hypotheses each)
 };
-constexpr int FIT_PER_WG = 64 * SCORE_WAVES / 8;
+constexpr int FIT_PER_WG = 64 * SCORE_WAVES / 8;  // k_ransac_score's fit workgroups (8 lanes a hypothesis)
 
-template <class M>
+template <class M, int PER_WG = FIT_PER_WG>
 __device__ __forceinline__ void fit_next_group(const double2 *__restrict__ x1, const double2 *__restrict__ x2,
                                                const FitNext &fn) {
-    const int64_t h = (int64_t)blockIdx.x * FIT_PER_WG + (threadIdx.x >> 3);
+    const int64_t h = (int64_t)blockIdx.x * PER_WG + (threadIdx.x >> 3);
     if (h >= fn.nh) return;
     const int i = threadIdx.x & 7;
     if (fn.counts && i == 0) fn.counts[h] = 0;
@@ -261,18 +262,36 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES, FIT ? SFM_SCORE_FIT_OCC : 1)
 }
 
 // The F score with the float prefilter (round 5).  One wave per hypothesis,
-// as the round-4 score, whose FP64 test (stage A, the wave-level skip, stage
-// B, the exact tail) stays for the 64-pair sets the prefilter does not prove:
-// a 128-pair pass first runs the packed float test (7 instructions a pair)
-// on the tile's float copy -- per lane pairs l and 64 + l as (x, x', y, y')
-// then (u, u', v, v'), copied in 16-B pieces from the array k_stage_tiles
-// writes -- and reads the FP64 correspondences from the LDS tile only when a
-// set is left.  cfg2: the prefilter proves ~89 % of the sets (stage A 95 %);
-// the FP64 sets read from global memory instead had cost 70 of the score's
-// 85 us (L2 round trips), the float sweep alone 16 us.  pk null or
-// SFM_SCORE_PRE=0: every set in FP64.
+// sixteen a workgroup sharing each LDS tile: the tile holds only the
+// packed float copy of 1024 correspondences (16 KB; per 128-pair pass, lane
+// l reads pairs l and 64 + l as (x, x', y, y') then (u, u', v, v'), copied
+// in 16-B pieces from the array k_stage_tiles writes).  A pass runs the
+// packed prefilter (outliers, 7 instructions a pair); a set it leaves runs
+// the full float test (epi_full_test: outliers and inliers, both lines);
+// lanes that test leaves undecided (pairs within ~1e-5 of the band, ~1 %
+// of the cfg2 sets) take the FP64 test on their correspondences from global
+// memory.  cfg2, same box: the fills of 8-wave workgroups with an FP64 tile
+// as well had cost 27 of the score's 71 us (each workgroup re-reads all the
+// correspondences from L2).  A hypothesis whose prefilter is off (pk null,
+// SFM_SCORE_PRE=0, coordinates past 2^24 or non-finite) runs the round-4
+// FP64 test on every set, from global memory.
+#ifndef SFM_EPI_WAVES
+#define SFM_EPI_WAVES 8
+#endif
+constexpr int EPI_WAVES = SFM_EPI_WAVES;
+// waves per SIMD k_epi_score is compiled for (80 VGPRs; the fused launch's
+// fit spills there, off the critical path).  Measured, cfg2 one-shot score:
+// 8 waves a workgroup at 6 a SIMD 0.068 ms; 16 waves a workgroup (half the
+// fill traffic) at 8 a SIMD 0.083, at 4 0.086 -- the prefilter loop filled
+// with spilled-SGPR reloads
 #ifndef SFM_EPI_OCC
-#define SFM_EPI_OCC 1
+#define SFM_EPI_OCC 6
+#endif
+#ifndef SFM_EPI_FIT_OCC
+#define SFM_EPI_FIT_OCC 6
+#endif
+#ifndef SFM_EPI_PROBE
+#define SFM_EPI_PROBE 0
 #endif
 
 // the FP64 test of two 64-pair sets (pair a = lane, b = 64 + lane) for one
@@ -304,46 +323,34 @@ __device__ __forceinline__ int epi_sets_f64(const double *f, double2 pa, double2
     return __popcll(__ballot(in0)) + __popcll(__ballot(in1));
 }
 
-// ... and of one 64-pair set (the other one proven by the prefilter)
-__device__ __forceinline__ int epi_set_f64(const double *f, double2 p, double2 q, double thr, double thr_lo,
-                                           double thr_hi, int score_split) {
-    using M = EpiModel;
-    const M::PartA a = M::fast_a(f, p, q, thr_hi);
-    if ((score_split & SCORE_SKIP_A) && __ballot(!a.out) == 0) return 0;
-    const M::Part r = M::fast_b(a, f, q, thr_lo, thr_hi);
-    bool in = r.in;
-    if (r.unsure) in = M::exact(r, p, q, f, thr);
-    return __popcll(__ballot(in));
-}
-
 template <bool FIT = false>
-__global__ void __launch_bounds__(64 * SCORE_WAVES, FIT ? SFM_SCORE_FIT_OCC : SFM_EPI_OCC)
+__global__ void __launch_bounds__(64 * EPI_WAVES, FIT ? SFM_EPI_FIT_OCC : SFM_EPI_OCC)
     k_epi_score(const double2 *__restrict__ x1, const double2 *__restrict__ x2, int64_t N, const double *__restrict__ F,
                 int64_t H, double thr, int32_t *__restrict__ counts, int64_t slice, FitNext fn, int score_split,
                 const float4 *__restrict__ tmax, const float4 *__restrict__ pk) {
     using M = EpiModel;
-    __shared__ double2 s1[SCORE_TILE];
-    __shared__ double2 s2[SCORE_TILE];
     __shared__ float4 sP[SCORE_TILE];
     int bx = blockIdx.x;
     if (FIT) {
         if (bx < fn.nfb) {
-            if (blockIdx.y == 0) fit_next_group<M>(x1, x2, fn);
+            if (blockIdx.y == 0) fit_next_group<M, 64 * EPI_WAVES / 8>(x1, x2, fn);
             return;
         }
         bx -= fn.nfb;
     }
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t h = (int64_t)bx * SCORE_WAVES + wave;
+    const int64_t h = (int64_t)bx * EPI_WAVES + wave;
     const bool active = h < H;
-    double f[9];
-    int finite = 1;
+    // the model in FP64 (setup, and every FP64 test: reloaded there from
+    // memory -- the scalar cache -- rather than held in 18 scalar registers
+    // across the sweep, which spilled the prefilter's constants)
+    auto load_f = [&](double (&f)[9]) {
+        asm volatile("" ::: "memory");
 #pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        f[k] = active ? F[9 * h + k] : 0.0;
-        finite &= isfinite(f[k]) ? 1 : 0;
-    }
+        for (int k = 0; k < 9; ++k) f[k] = active ? F[9 * h + k] : 0.0;
+    };
+    int finite = 1;
     int cnt = 0;
     const double thr_lo = 2.0 * (thr >= 0 ? thr * (1.0 - 1e-4) : thr * (1.0 + 1e-4));
     const double thr_hi = 2.0 * (thr >= 0 ? thr * (1.0 + 1e-4) : thr * (1.0 - 1e-4));
@@ -351,52 +358,79 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES, FIT ? SFM_SCORE_FIT_OCC : SF
     const bool use_pre = pk && tmax && (score_split & SCORE_PRE32);  // workgroup-uniform
     EpiPre pre;
     pre.on = false;
-    if (use_pre && active && finite) {
-        float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int64_t t = p0 / SCORE_TILE; t * SCORE_TILE < p1; ++t) {
-            const float4 q = tmax[t];
-            b = make_float4(fmaxf(b.x, q.x), fmaxf(b.y, q.y), fmaxf(b.z, q.z), fmaxf(b.w, q.w));
+    {
+        double f[9];
+        load_f(f);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) finite &= isfinite(f[k]) ? 1 : 0;
+        if (use_pre && active && finite) {
+            float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int64_t t = p0 / SCORE_TILE; t * SCORE_TILE < p1; ++t) {
+                const float4 q = tmax[t];
+                b = make_float4(fmaxf(b.x, q.x), fmaxf(b.y, q.y), fmaxf(b.z, q.z), fmaxf(b.w, q.w));
+            }
+            pre = epi_pre_uniform(epi_pre_setup(f, thr_hi, b));
         }
-        pre = epi_pre_uniform(epi_pre_setup(f, thr_hi, b));
     }
     for (int64_t base = p0; base < p1; base += SCORE_TILE) {
         const int n = (int)min<int64_t>(SCORE_TILE, p1 - base);
         const int nfull = n & ~127;
-        for (int i = threadIdx.x; i < n; i += 64 * SCORE_WAVES) {
-            s1[i] = x1[base + i];
-            s2[i] = x2[base + i];
-        }
         if (use_pre) {
             const float4 *src = pk + base;  // a tile starts on a 128-pair pass
-            for (int i = threadIdx.x; i < nfull; i += 64 * SCORE_WAVES) sP[i] = src[i];
+            for (int i = threadIdx.x; i < nfull; i += 64 * EPI_WAVES) sP[i] = src[i];
+            __syncthreads();
         }
-        __syncthreads();
         if (active && finite) {
+            const double2 *a1 = x1 + base, *a2 = x2 + base;
             int j = 0;
+#if SFM_EPI_PROBE == 2  // timing probe (wrong counts): the tile fills alone
+            j = nfull;
+#endif
             for (; j < nfull; j += 128) {
-                bool n0 = true, n1 = true;  // the sets the FP64 test must see
-                if (pre.on) {  // a set proven outliers in float counts nothing
+                if (pre.on) {
                     bool o0, o1;
-                    epi_pre_test(pre, sP[j + lane], sP[j + 64 + lane], o0, o1);
-                    n0 = __ballot(!o0) != 0;
-                    n1 = __ballot(!o1) != 0;
+                    const float4 A = sP[j + lane], B = sP[j + 64 + lane];
+                    epi_pre_test(pre, A, B, o0, o1);  // a set proven outliers counts nothing
+                    const bool n0 = __ballot(!o0) != 0, n1 = __ballot(!o1) != 0;
+#if SFM_EPI_PROBE == 1  // timing probe (wrong counts): no test past the prefilter
+                    cnt += n0 + n1;
+                    continue;
+#endif
                     if (!n0 && !n1) continue;
+                    // the sets left: the full float test, FP64 only for its undecided lanes
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        if (!(t ? n1 : n0)) continue;
+                        const int r = t ? epi_full_test(pre, A.y, A.w, B.y, B.w) : epi_full_test(pre, A.x, A.z, B.x, B.z);
+                        bool in = r == 1;
+                        if (__ballot(r == 2) != 0) {
+                            const int i = j + 64 * t + lane;
+                            double f[9];
+                            load_f(f);
+                            const bool in64 = M::inlier_fast(f, a1[i], a2[i], thr, thr_lo, thr_hi);
+                            if (r == 2) in = in64;
+                        }
+                        cnt += __popcll(__ballot(in));
+                    }
+                    continue;
                 }
-                if (n0 && n1)
-                    cnt += epi_sets_f64(f, s1[j + lane], s2[j + lane], s1[j + 64 + lane], s2[j + 64 + lane], thr,
-                                        thr_lo, thr_hi, score_split);
-                else
-                    cnt += n0 ? epi_set_f64(f, s1[j + lane], s2[j + lane], thr, thr_lo, thr_hi, score_split)
-                              : epi_set_f64(f, s1[j + 64 + lane], s2[j + 64 + lane], thr, thr_lo, thr_hi, score_split);
+                double f[9];
+                load_f(f);
+                cnt += epi_sets_f64(f, a1[j + lane], a2[j + lane], a1[j + 64 + lane], a2[j + 64 + lane], thr, thr_lo,
+                                    thr_hi, score_split);
             }
             for (; j < n; j += 64) {  // the partial last pass, one 64-pair set at a time
                 const int i = j + lane;
                 bool inl = false;
-                if (i < n) inl = M::inlier_fast(f, s1[i], s2[i], thr, thr_lo, thr_hi);
+                if (i < n) {
+                    double f[9];
+                    load_f(f);
+                    inl = M::inlier_fast(f, a1[i], a2[i], thr, thr_lo, thr_hi);
+                }
                 cnt += __popcll(__ballot(inl));
             }
         }
-        __syncthreads();
+        if (use_pre) __syncthreads();
     }
     if (active && lane == 0) {
         if (gridDim.y == 1)
@@ -421,7 +455,16 @@ static inline int score_split_on() {
 // hypotheses one score workgroup takes (one a wave)
 template <class M>
 constexpr int score_per_wg() {
-    return SCORE_WAVES;
+    return M::SPLIT ? EPI_WAVES : SCORE_WAVES;
+}
+template <class M>
+constexpr int score_threads() {
+    return 64 * score_per_wg<M>();
+}
+// hypotheses a fit workgroup of a fused launch takes (8 lanes each)
+template <class M>
+constexpr int fit_per_wg() {
+    return score_threads<M>() / 8;
 }
 static inline int64_t score_slice(int64_t nh, int64_t N, int *ny, int per_wg) {
     const int64_t wg = (nh + per_wg - 1) / per_wg;
@@ -460,6 +503,9 @@ __global__ void __launch_bounds__(1024) k_ransac_select(const double2 *__restric
     for (int k = 0; k < 9; ++k) f[k] = F[9 * best + k];
     if (t < 9) F_best[t] = f[t];
     if (!mask) return;  // a hypothesis shard: the mask is emitted after the combine
+    // the score's fast test with its exact tail: the same decisions as M::inlier
+    const double thr_lo = 2.0 * (thr >= 0 ? thr * (1.0 - 1e-4) : thr * (1.0 + 1e-4));
+    const double thr_hi = 2.0 * (thr >= 0 ? thr * (1.0 + 1e-4) : thr * (1.0 - 1e-4));
     for (int64_t base = t; base < N; base += (int64_t)MU * NT) {
         double2 p[MU], q[MU];
 #pragma unroll
@@ -471,7 +517,7 @@ __global__ void __launch_bounds__(1024) k_ransac_select(const double2 *__restric
 #pragma unroll
         for (int u = 0; u < MU; ++u) {
             const int64_t i = base + (int64_t)u * NT;
-            if (i < N) mask[i] = M::inlier(f, p[u], q[u], thr) ? 1 : 0;
+            if (i < N) mask[i] = M::inlier_fast(f, p[u], q[u], thr, thr_lo, thr_hi) ? 1 : 0;
         }
     }
 }
@@ -588,8 +634,8 @@ int ransac_run(const double *x1, const double *x2, int64_t N, const int32_t *sam
     if ((rc = launch_fit<M>(d1, d2, ds, H, dF, ny > 1 ? dcnt : nullptr, s))) return rc;
     SFM_HIP(hipEventRecord(c->ev[2], s));
     if constexpr (M::SPLIT)
-        hipLaunchKernelGGL((k_epi_score<false>), dim3(ceil_div(H, score_per_wg<M>()), ny), dim3(64 * SCORE_WAVES), 0, s,
-                           d1, d2, N, dF, H, thr, dcnt, slice, FitNext{}, score_split_on(), tmax, pk);
+        hipLaunchKernelGGL((k_epi_score<false>), dim3(ceil_div(H, score_per_wg<M>()), ny), dim3(score_threads<M>()), 0,
+                           s, d1, d2, N, dF, H, thr, dcnt, slice, FitNext{}, score_split_on(), tmax, pk);
     else
         hipLaunchKernelGGL((k_ransac_score<M, false>), dim3(ceil_div(H, SCORE_WAVES), ny), dim3(64 * SCORE_WAVES), 0, s,
                            d1, d2, N, dF, H, thr, dcnt, slice, FitNext{});
@@ -702,10 +748,10 @@ struct ScorePipe {
         const dim3 grid((unsigned)(ceil_div(n, score_per_wg<M>()) + (fn ? fn->nfb : 0)), ny);
         if constexpr (M::SPLIT) {
             if (fn)
-                hipLaunchKernelGGL((k_epi_score<true>), grid, dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
+                hipLaunchKernelGGL((k_epi_score<true>), grid, dim3(score_threads<M>()), 0, s, d1, d2, N,
                                    dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, *fn, score_split_on(), tmax, pk);
             else
-                hipLaunchKernelGGL((k_epi_score<false>), grid, dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
+                hipLaunchKernelGGL((k_epi_score<false>), grid, dim3(score_threads<M>()), 0, s, d1, d2, N,
                                    dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, FitNext{}, score_split_on(), tmax,
                                    pk);
         } else {  // the H model (no group fit: its fits run on their own)
@@ -726,7 +772,7 @@ struct ScorePipe {
             return score(a, b, nullptr);
         }
         if (pb > pa) {
-            const FitNext fn{rows, b - a, dF + (a - off) * 9, cz, (int)ceil_div(b - a, FIT_PER_WG)};
+            const FitNext fn{rows, b - a, dF + (a - off) * 9, cz, (int)ceil_div(b - a, fit_per_wg<M>())};
             if ((rc = score(pa, pb, &fn))) return rc;
         } else if ((rc = launch_fit<M>(d1, d2, rows, b - a, dF + (a - off) * 9, cz, s))) {
             return rc;
@@ -779,8 +825,24 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
     // upload is a true async copy that overlaps the first chunk's draw (from
     // pageable memory the copy would hold the host until it lands)
     char *hx = hout + xoff_of(N);
-    std::memcpy(hx, x1, pb);
-    std::memcpy(hx + pb, x2, pb);
+    PySampler ps(st, N, M::K);
+    double t_draw = 0;
+    // the correspondences' copy into pinned memory and the first chunk's
+    // draw on two host threads at once (each ~6-10 us at cfg2), then the
+    // staging kernel and the first fit
+    const int64_t hfirst = rp_next(0, H);
+    {
+        const auto ta = std::chrono::steady_clock::now();
+        par_for(2, [&](int64_t t) {
+            if (t == 0) {
+                std::memcpy(hx, x1, pb);
+                std::memcpy(hx + pb, x2, pb);
+            } else {
+                ps.draw(0, hfirst, hs);
+            }
+        });
+        t_draw += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
+    }
     int64_t *dbest = reinterpret_cast<int64_t *>(hout);
     double *dFb = reinterpret_cast<double *>(hout) + 2;
     uint8_t *dmask = reinterpret_cast<uint8_t *>(hout) + 16 * sizeof(double);
@@ -791,10 +853,9 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
                        reinterpret_cast<const double2 *>(hx), N, d1, d2, tmax, pk);
     SFM_HIP(hipGetLastError());
     if (tm) SFM_HIP(hipEventRecord(c->ev[1], s));
-    PySampler ps(st, N, M::K);
-    double t_draw = 0;
     ScorePipe<M> pipe{d1, d2, N, thr, s, dF, dcnt, 0, tmax, pk};
-    for (int64_t h0 = 0, h1; h0 < H; h0 = h1) {
+    if ((rc = pipe.add(0, hfirst, hs))) return rc;
+    for (int64_t h0 = hfirst, h1; h0 < H; h0 = h1) {
         h1 = rp_next(h0, H);
         const auto ta = std::chrono::steady_clock::now();
         ps.draw(h0, h1, hs);
