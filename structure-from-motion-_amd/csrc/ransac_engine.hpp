@@ -261,37 +261,55 @@ __global__ void __launch_bounds__(64 * SCORE_WAVES, FIT ? SFM_SCORE_FIT_OCC : 1)
     }
 }
 
-// The F score with the float prefilter (round 5).  One wave per hypothesis,
-// sixteen a workgroup sharing each LDS tile: the tile holds only the
-// packed float copy of 1024 correspondences (16 KB; per 128-pair pass, lane
-// l reads pairs l and 64 + l as (x, x', y, y') then (u, u', v, v'), copied
-// in 16-B pieces from the array k_stage_tiles writes).  A pass runs the
-// packed prefilter (outliers, 7 instructions a pair); a set it leaves runs
-// the full float test (epi_full_test: outliers and inliers, both lines);
-// lanes that test leaves undecided (pairs within ~1e-5 of the band, ~1 %
-// of the cfg2 sets) take the FP64 test on their correspondences from global
-// memory.  cfg2, same box: the fills of 8-wave workgroups with an FP64 tile
-// as well had cost 27 of the score's 71 us (each workgroup re-reads all the
-// correspondences from L2).  A hypothesis whose prefilter is off (pk null,
-// SFM_SCORE_PRE=0, coordinates past 2^24 or non-finite) runs the round-4
-// FP64 test on every set, from global memory.
-#ifndef SFM_EPI_WAVES
-#define SFM_EPI_WAVES 8
+// The F score (round 5): the correspondences stay in registers and the
+// hypotheses stream through them.  A workgroup of EPI_W waves takes hb
+// hypotheses (hb <= 64) and a range of 128-pair passes; a wave holds
+// EPI_SLOTS passes at a time in registers (the packed float copy
+// k_stage_tiles writes: lane l of a pass has (x, x', y, y') and
+// (u, u', v, v') of pairs l and 64 + l), loaded once, and runs every
+// hypothesis of the workgroup over them.  Per hypothesis:
+//  * its prefilter constants (epi_pre_setup: the model scaled by a power of
+//    two and rounded to float, the bounds for the workgroup's coordinate
+//    range) are computed once per workgroup, by lane t of wave 0 for
+//    hypothesis t, and read back from LDS as broadcast pairs;
+//  * the packed prefilter runs on every slot (rigorous "outlier" proofs,
+//    14 instructions per 128 pairs); the pairs it leaves (cfg2: ~6 of 5000
+//    a hypothesis) go to the workgroup's LDS queue, and after the loop
+//    every lane takes one queued (hypothesis, pair) through the FP64 test
+//    (the reference's decision bit for bit), so the rare survivors cost
+//    one lane each instead of a wave-wide test; a full queue falls back to
+//    the FP64 test in place;
+//  * a hypothesis whose prefilter is off (pk null, SFM_SCORE_PRE=0,
+//    coordinates past 2^24, a model too large or small to scale) runs the
+//    round-4 FP64 test over the wave's passes, from global memory.
+// Counts: a wave's in lane k of a register, the workgroup's summed in LDS,
+// stored (one pass range) or added (several) per hypothesis.
+// Measured, cfg2 one-shot (16384 hypotheses x 5000 pairs), same box:
+// round-4 FP64 score 86 us; the round-5 first form (one wave per
+// hypothesis sweeping LDS tiles of the float copy, the survivors through a
+// wave-wide float test) 66.6; this form 58.5 with the wave-wide test, 55.0
+// with the queue at 4 slots, 49.6 at 5 (cfg2's 40 passes in one range of 8
+// waves), 51.6 at 6 (registers spill).  The instruction count bounds it:
+// 20.8 M VALU per launch (5 of 9 in the prefilter) against 58 us at 4
+// cycles each over 1024 SIMDs.
+#ifndef SFM_EPI_SLOTS
+#define SFM_EPI_SLOTS 5
 #endif
-constexpr int EPI_WAVES = SFM_EPI_WAVES;
-// waves per SIMD k_epi_score is compiled for (80 VGPRs; the fused launch's
-// fit spills there, off the critical path).  Measured, cfg2 one-shot score:
-// 8 waves a workgroup at 6 a SIMD 0.068 ms; 16 waves a workgroup (half the
-// fill traffic) at 8 a SIMD 0.083, at 4 0.086 -- the prefilter loop filled
-// with spilled-SGPR reloads
+constexpr int EPI_SLOTS = SFM_EPI_SLOTS;  // 128-pair passes a wave holds
+constexpr int EPI_W = 8;                  // waves a workgroup
+constexpr int EPI_HB_MAX = 64;            // hypotheses a workgroup (a setup lane each)
+constexpr int EPI_QCAP = 4096;            // candidates a workgroup queues
 #ifndef SFM_EPI_OCC
-#define SFM_EPI_OCC 6
-#endif
-#ifndef SFM_EPI_FIT_OCC
-#define SFM_EPI_FIT_OCC 6
+#define SFM_EPI_OCC 4
 #endif
 #ifndef SFM_EPI_PROBE
 #define SFM_EPI_PROBE 0
+#endif
+#ifndef SFM_EPI_PREFETCH
+#define SFM_EPI_PREFETCH 0
+#endif
+#ifndef SFM_EPI_FIT_OCC
+#define SFM_EPI_FIT_OCC 4
 #endif
 
 // the FP64 test of two 64-pair sets (pair a = lane, b = 64 + lane) for one
@@ -324,119 +342,252 @@ __device__ __forceinline__ int epi_sets_f64(const double *f, double2 pa, double2
 }
 
 template <bool FIT = false>
-__global__ void __launch_bounds__(64 * EPI_WAVES, FIT ? SFM_EPI_FIT_OCC : SFM_EPI_OCC)
+__global__ void __launch_bounds__(64 * EPI_W, FIT ? SFM_EPI_FIT_OCC : SFM_EPI_OCC)
     k_epi_score(const double2 *__restrict__ x1, const double2 *__restrict__ x2, int64_t N, const double *__restrict__ F,
-                int64_t H, double thr, int32_t *__restrict__ counts, int64_t slice, FitNext fn, int score_split,
+                int64_t H, double thr, int32_t *__restrict__ counts, int hb, FitNext fn, int score_split,
                 const float4 *__restrict__ tmax, const float4 *__restrict__ pk) {
     using M = EpiModel;
-    __shared__ float4 sP[SCORE_TILE];
+    // per hypothesis, 6 quads: (flags, -, q1, q1) (q0, q0, g0, g0) (g1, g1, g2, g2)
+    // (g3, g3, g4, g4) (g5, g5, g6, g6) (g7, g7, g8, g8)
+    __shared__ float4 sC[EPI_HB_MAX][6];
+    __shared__ int sCnt[EPI_HB_MAX];
+    // the candidates the prefilter leaves, (hypothesis << 26 | pair - 128 P0)
+    __shared__ uint32_t sQ[EPI_QCAP];
+    __shared__ int sQn;
     int bx = blockIdx.x;
     if (FIT) {
         if (bx < fn.nfb) {
-            if (blockIdx.y == 0) fit_next_group<M, 64 * EPI_WAVES / 8>(x1, x2, fn);
+            if (blockIdx.y == 0) fit_next_group<M, 64 * EPI_W / 8>(x1, x2, fn);
             return;
         }
         bx -= fn.nfb;
     }
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t h = (int64_t)bx * EPI_WAVES + wave;
-    const bool active = h < H;
-    // the model in FP64 (setup, and every FP64 test: reloaded there from
-    // memory -- the scalar cache -- rather than held in 18 scalar registers
-    // across the sweep, which spilled the prefilter's constants)
-    auto load_f = [&](double (&f)[9]) {
+    const int64_t h0 = (int64_t)bx * hb;
+    const int nh = (int)min<int64_t>(hb, H - h0);
+    // a model in FP64 (the FP64 tests: from memory -- the scalar cache --
+    // rather than held in scalar registers across the hypothesis loop)
+    auto load_f = [&](int64_t h, double (&f)[9]) {
         asm volatile("" ::: "memory");
 #pragma unroll
-        for (int k = 0; k < 9; ++k) f[k] = active ? F[9 * h + k] : 0.0;
+        for (int q = 0; q < 9; ++q) f[q] = F[9 * h + q];
     };
-    int finite = 1;
-    int cnt = 0;
-    const double thr_lo = 2.0 * (thr >= 0 ? thr * (1.0 - 1e-4) : thr * (1.0 + 1e-4));
-    const double thr_hi = 2.0 * (thr >= 0 ? thr * (1.0 + 1e-4) : thr * (1.0 - 1e-4));
-    const int64_t p0 = (int64_t)blockIdx.y * slice, p1 = min<int64_t>(N, p0 + slice);
+    auto band = [&](double &lo, double &hi) {  // the FP64 test's band around 2 thr
+        lo = 2.0 * (thr >= 0 ? thr * (1.0 - 1e-4) : thr * (1.0 + 1e-4));
+        hi = 2.0 * (thr >= 0 ? thr * (1.0 + 1e-4) : thr * (1.0 - 1e-4));
+    };
+    const int P = (int)((N + 127) >> 7);  // 128-pair passes (N < 2^31)
+    const int P0 = (int)((int64_t)blockIdx.y * P / gridDim.y), P1 = (int)((int64_t)(blockIdx.y + 1) * P / gridDim.y);
     const bool use_pre = pk && tmax && (score_split & SCORE_PRE32);  // workgroup-uniform
-    EpiPre pre;
-    pre.on = false;
-    {
+    if (threadIdx.x < EPI_HB_MAX) {  // wave 0: hypothesis h0 + t's constants
+        const int t = threadIdx.x;
+        int flags = 0;
+        EpiPre p{};
         double f[9];
-        load_f(f);
+        bool fin = t < nh;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) finite &= isfinite(f[k]) ? 1 : 0;
-        if (use_pre && active && finite) {
-            float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
-            for (int64_t t = p0 / SCORE_TILE; t * SCORE_TILE < p1; ++t) {
-                const float4 q = tmax[t];
+        for (int q = 0; q < 9; ++q) {
+            f[q] = t < nh ? F[9 * (h0 + t) + q] : 0.0;
+            fin = fin && isfinite(f[q]);
+        }
+        // the coordinate bounds of the workgroup's passes: the wave's lanes
+        // take the tiles in turn (one load latency for the usual few), then
+        // a wave max
+        float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (use_pre) {
+            const int64_t e = min<int64_t>(N, (int64_t)P1 * 128);
+            for (int64_t i = (int64_t)P0 * 128 / SCORE_TILE + t; i * SCORE_TILE < e; i += 64) {
+                const float4 q = tmax[i];
                 b = make_float4(fmaxf(b.x, q.x), fmaxf(b.y, q.y), fmaxf(b.z, q.z), fmaxf(b.w, q.w));
             }
-            pre = epi_pre_uniform(epi_pre_setup(f, thr_hi, b));
-        }
-    }
-    for (int64_t base = p0; base < p1; base += SCORE_TILE) {
-        const int n = (int)min<int64_t>(SCORE_TILE, p1 - base);
-        const int nfull = n & ~127;
-        if (use_pre) {
-            const float4 *src = pk + base;  // a tile starts on a 128-pair pass
-            for (int i = threadIdx.x; i < nfull; i += 64 * EPI_WAVES) sP[i] = src[i];
-            __syncthreads();
-        }
-        if (active && finite) {
-            const double2 *a1 = x1 + base, *a2 = x2 + base;
-            int j = 0;
-#if SFM_EPI_PROBE == 2  // timing probe (wrong counts): the tile fills alone
-            j = nfull;
-#endif
-            for (; j < nfull; j += 128) {
-                if (pre.on) {
-                    bool o0, o1;
-                    const float4 A = sP[j + lane], B = sP[j + 64 + lane];
-                    epi_pre_test(pre, A, B, o0, o1);  // a set proven outliers counts nothing
-                    const bool n0 = __ballot(!o0) != 0, n1 = __ballot(!o1) != 0;
-#if SFM_EPI_PROBE == 1  // timing probe (wrong counts): no test past the prefilter
-                    cnt += n0 + n1;
-                    continue;
-#endif
-                    if (!n0 && !n1) continue;
-                    // the sets left: the full float test, FP64 only for its undecided lanes
 #pragma unroll
-                    for (int t = 0; t < 2; ++t) {
-                        if (!(t ? n1 : n0)) continue;
-                        const int r = t ? epi_full_test(pre, A.y, A.w, B.y, B.w) : epi_full_test(pre, A.x, A.z, B.x, B.z);
-                        bool in = r == 1;
-                        if (__ballot(r == 2) != 0) {
-                            const int i = j + 64 * t + lane;
-                            double f[9];
-                            load_f(f);
-                            const bool in64 = M::inlier_fast(f, a1[i], a2[i], thr, thr_lo, thr_hi);
-                            if (r == 2) in = in64;
+            for (int o = 32; o > 0; o >>= 1)
+                b = make_float4(fmaxf(b.x, __shfl_xor(b.x, o)), fmaxf(b.y, __shfl_xor(b.y, o)),
+                                fmaxf(b.z, __shfl_xor(b.z, o)), fmaxf(b.w, __shfl_xor(b.w, o)));
+        }
+        if (fin) {
+            flags = 1;
+            if (use_pre) {
+                double lo, hi;
+                band(lo, hi);
+                p = epi_pre_setup(f, hi, b);
+                if (p.on) flags |= 2;
+            }
+        }
+        sC[t][0] = make_float4(__int_as_float(flags), 0.f, p.q1, p.q1);
+        sC[t][1] = make_float4(p.q0, p.q0, p.g[0], p.g[0]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sC[t][2 + k] = make_float4(p.g[1 + 2 * k], p.g[1 + 2 * k], p.g[2 + 2 * k], p.g[2 + 2 * k]);
+        sCnt[t] = 0;
+        if (t == 0) sQn = 0;
+    }
+    int cntv = 0;  // lane k: this wave's count for hypothesis h0 + k
+    bool first = true;
+#if SFM_EPI_PREFETCH
+    float4 n[6];
+#endif
+    for (int base = P0 + wave; base < P1; base += EPI_W * EPI_SLOTS) {
+        // slot s: pass base + s EPI_W
+        float4 A[EPI_SLOTS], B[EPI_SLOTS];
+#pragma unroll
+        for (int s = 0; s < EPI_SLOTS; ++s) {
+            const int q = base + s * EPI_W;
+            A[s] = B[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (use_pre && q < P1) {
+                A[s] = pk[(int64_t)q * 128 + lane];
+                B[s] = pk[(int64_t)q * 128 + 64 + lane];
+                const int nl = (int)min<int64_t>(128, N - (int64_t)q * 128);  // pairs in the pass
+                if (nl < 128) {
+                    // the last, partial pass: its missing pairs repeat the pass's
+                    // first one (a candidate past N is dropped by the FP64 stage)
+                    const float4 A0 = pk[(int64_t)q * 128], B0 = pk[(int64_t)q * 128 + 64];
+                    if (lane >= nl) {
+                        A[s].x = A0.x; A[s].z = A0.z; B[s].x = B0.x; B[s].z = B0.z;
+                    }
+                    if (64 + lane >= nl) {
+                        A[s].y = A0.x; A[s].w = A0.z; B[s].y = B0.x; B[s].w = B0.z;
+                    }
+                }
+            }
+        }
+        // slots holding passes (wave-uniform)
+        const int ns = min(EPI_SLOTS, (P1 - base + EPI_W - 1) / EPI_W);
+        if (first) __syncthreads();  // the constants (the loads above in flight)
+        first = false;
+        for (int k = 0; k < nh; ++k) {
+#if SFM_EPI_PREFETCH
+            // hypothesis k's prefilter quads, read one hypothesis ahead (the LDS
+            // latency off the loop's critical path)
+            float4 c[6];
+            if (k == 0)
+#pragma unroll
+                for (int j = 0; j < 6; ++j) n[j] = sC[0][j];
+            const int kn = min(k + 1, EPI_HB_MAX - 1);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                c[j] = n[j];
+                n[j] = sC[kn][j];
+            }
+#else
+            float4 c[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) c[j] = sC[k][j];
+#endif
+            const int flags = __builtin_amdgcn_readfirstlane(__float_as_int(c[0].x));
+            if (!(flags & 1)) continue;
+#if SFM_EPI_PROBE == 2  // timing probe (wrong counts): the loop without tests
+            cntv += lane == k ? flags : 0;
+            continue;
+#endif
+            const int64_t h = h0 + k;
+            int cnt = 0;
+            if (flags & 2) {
+                EpiPk p;
+                p.q1 = epi_f2{c[0].z, c[0].w};
+                p.q0 = epi_f2{c[1].x, c[1].y};
+                p.g[0] = epi_f2{c[1].z, c[1].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    p.g[1 + 2 * j] = epi_f2{c[2 + j].x, c[2 + j].y};
+                    p.g[2 + 2 * j] = epi_f2{c[2 + j].z, c[2 + j].w};
+                }
+                uint64_t cand[EPI_SLOTS][2], any = 0;
+#pragma unroll
+                for (int s = 0; s < EPI_SLOTS; ++s) {
+                    cand[s][0] = cand[s][1] = 0;
+                    if (s >= ns) continue;
+                    bool o0, o1;
+                    epi_pre_test(p, A[s], B[s], o0, o1);
+                    cand[s][0] = ~__ballot(o0);
+                    cand[s][1] = ~__ballot(o1);
+                    any |= cand[s][0] | cand[s][1];
+                }
+#if SFM_EPI_PROBE == 1  // timing probe (wrong counts): the prefilter alone
+                cnt += any != 0;
+                any = 0;
+#endif
+                if (any) {  // the candidates into the workgroup's queue
+                    int ubits = 0;  // bit 2 s + t: the lane's pair of slot s, half t, past a full queue
+#pragma unroll
+                    for (int s = 0; s < EPI_SLOTS; ++s)
+#pragma unroll
+                        for (int t = 0; t < 2; ++t) {
+                            const uint64_t cm = cand[s][t];
+                            if (!cm) continue;
+                            int at = 0;
+                            if (lane == 0) at = atomicAdd(&sQn, __popcll(cm));
+                            at = __builtin_amdgcn_readfirstlane(at);
+                            const int slot =
+                                at + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+                            const bool mine = (cm >> lane) & 1;
+                            const int pi = (base + s * EPI_W - P0) * 128 + 64 * t + lane;  // the workgroup's pair
+                            if (mine && slot < EPI_QCAP) sQ[slot] = ((uint32_t)k << 26) | (uint32_t)pi;
+                            if (mine && slot >= EPI_QCAP) ubits |= 1 << (2 * s + t);
+                        }
+                    // past a full queue: the FP64 test here, one of a lane's pairs a round
+                    while (__ballot(ubits != 0)) {
+                        bool in = false;
+                        if (ubits) {
+                            const int b = __builtin_ctz(ubits);
+                            ubits &= ubits - 1;
+                            const int64_t i = (int64_t)(base + (b >> 1) * EPI_W) * 128 + 64 * (b & 1) + lane;
+                            if (i < N) {
+                                double f[9], lo, hi;
+                                load_f(h, f);
+                                band(lo, hi);
+                                in = M::inlier_fast(f, x1[i], x2[i], thr, lo, hi);
+                            }
                         }
                         cnt += __popcll(__ballot(in));
                     }
-                    continue;
                 }
-                double f[9];
-                load_f(f);
-                cnt += epi_sets_f64(f, a1[j + lane], a2[j + lane], a1[j + 64 + lane], a2[j + 64 + lane], thr, thr_lo,
-                                    thr_hi, score_split);
-            }
-            for (; j < n; j += 64) {  // the partial last pass, one 64-pair set at a time
-                const int i = j + lane;
-                bool inl = false;
-                if (i < n) {
-                    double f[9];
-                    load_f(f);
-                    inl = M::inlier_fast(f, a1[i], a2[i], thr, thr_lo, thr_hi);
+            } else {  // the FP64 test on every pair of the wave's passes
+                double f[9], lo, hi;
+                load_f(h, f);
+                band(lo, hi);
+                for (int s = 0; s < ns; ++s) {
+                    const int64_t i = (int64_t)(base + s * EPI_W) * 128 + lane;
+                    if (i - lane + 128 <= N) {
+                        cnt += epi_sets_f64(f, x1[i], x2[i], x1[i + 64], x2[i + 64], thr, lo, hi, score_split);
+                    } else {
+                        const bool in0 = i < N && M::inlier_fast(f, x1[i], x2[i], thr, lo, hi);
+                        const bool in1 = i + 64 < N && M::inlier_fast(f, x1[i + 64], x2[i + 64], thr, lo, hi);
+                        cnt += __popcll(__ballot(in0)) + __popcll(__ballot(in1));
+                    }
                 }
-                cnt += __popcll(__ballot(inl));
             }
+            cntv += lane == k ? cnt : 0;
         }
-        if (use_pre) __syncthreads();
     }
-    if (active && lane == 0) {
+    if (first) __syncthreads();  // a wave without passes still meets the barrier
+    if (lane < nh && cntv) atomicAdd(&sCnt[lane], cntv);
+    __syncthreads();
+    {  // the queued candidates: the FP64 test, one a lane
+        double lo, hi;
+        band(lo, hi);
+        const int qn = min(sQn, EPI_QCAP);
+        for (int e = threadIdx.x; e < qn; e += 64 * EPI_W) {
+            const uint32_t v = sQ[e];
+            const int k = (int)(v >> 26);
+            const int64_t i = (int64_t)P0 * 128 + (v & ((1u << 26) - 1));
+            if (i >= N) continue;  // a repeat in the partial pass
+            const double *fk = F + 9 * (h0 + k);
+            double f[9];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) f[q] = fk[q];
+            if (M::inlier_fast(f, x1[i], x2[i], thr, lo, hi)) atomicAdd(&sCnt[k], 1);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < nh) {
+        const int64_t h = h0 + threadIdx.x;
+        const int c = sCnt[threadIdx.x];
         if (gridDim.y == 1)
-            counts[h] = cnt;
-        else
-            atomicAdd(counts + h, cnt);
+            counts[h] = c;
+        else if (c)
+            atomicAdd(counts + h, c);
     }
 }
 
@@ -449,31 +600,54 @@ static inline int score_split_on() {
     return ((e && std::atoi(e) == 0) ? 0 : SCORE_SKIP_A) | ((q && std::atoi(q) == 0) ? 0 : SCORE_PRE32);
 }
 
-// Point slices for scoring nh hypotheses: enough workgroups to put ~4 on
-// every CU (a lone 8-wave group per CU leaves the DP pipes latency-bound),
-// slices a whole number of LDS tiles.
-// hypotheses one score workgroup takes (one a wave)
-template <class M>
-constexpr int score_per_wg() {
-    return M::SPLIT ? EPI_WAVES : SCORE_WAVES;
-}
 template <class M>
 constexpr int score_threads() {
-    return 64 * score_per_wg<M>();
+    return 64 * (M::SPLIT ? EPI_W : SCORE_WAVES);
 }
 // hypotheses a fit workgroup of a fused launch takes (8 lanes each)
 template <class M>
 constexpr int fit_per_wg() {
     return score_threads<M>() / 8;
 }
-static inline int64_t score_slice(int64_t nh, int64_t N, int *ny, int per_wg) {
-    const int64_t wg = (nh + per_wg - 1) / per_wg;
-    const int64_t tiles = (N + SCORE_TILE - 1) / SCORE_TILE;
-    int64_t y = std::min<int64_t>(tiles, std::max<int64_t>(1, (1024 + wg - 1) / wg));
-    const int64_t per = (tiles + y - 1) / y;
-    y = (tiles + per - 1) / per;
-    *ny = (int)y;
-    return per * SCORE_TILE;
+static inline int64_t env_pos(const char *name, int64_t dflt) {
+    const char *e = std::getenv(name);
+    const long long v = e ? std::atoll(e) : 0;
+    return v > 0 ? (int64_t)v : dflt;
+}
+// The score grid for nh hypotheses: *gx score workgroups (hypothesis
+// groups) by *gy correspondence ranges; returns the launch's argument.
+//  H: one hypothesis a wave, point slices (a whole number of LDS tiles)
+//     for enough workgroups to put ~4 on every CU; returns the slice.
+//  F: hb hypotheses a workgroup (returned) and pass ranges of about
+//     EPI_W x EPI_SLOTS passes; hb from the target workgroup count
+//     (SFM_EPI_WGS, default 512: one round of two workgroups a CU; cfg2,
+//     16384 / 4096 / 1024 hypotheses: 44.6 / 19.2 / 11.9 us, against 47.0 /
+//     22.8 / 17.2 at 1024 workgroups and 61.2 / 25.1 / 11.8 at 384), at
+//     least SFM_EPI_HB_MIN (default 4), and more ranges when the
+//     hypotheses alone leave the chip short.
+template <class M>
+static inline int64_t score_grid(int64_t nh, int64_t N, int64_t *gx, int *gy) {
+    if constexpr (M::SPLIT) {
+        static const int64_t target = env_pos("SFM_EPI_WGS", 512);
+        static const int64_t hb_min = std::min<int64_t>(EPI_HB_MAX, env_pos("SFM_EPI_HB_MIN", 4));
+        const int64_t P = (N + 127) / 128;
+        // (a workgroup's passes < 2^19: its queue entries hold pair - 128 P0 in 26 bits)
+        int64_t y = std::min<int64_t>(65535, std::max(ceil_div(P, (int64_t)EPI_W * EPI_SLOTS), ceil_div(P, 1 << 19)));
+        const int64_t hb = std::max(hb_min, std::min<int64_t>(EPI_HB_MAX, ceil_div(nh * y, target)));
+        *gx = ceil_div(nh, hb);
+        if (*gx * y < target) y = std::min<int64_t>({65535, ceil_div(P, (int64_t)EPI_W), ceil_div(target, *gx)});
+        *gy = (int)y;
+        return hb;
+    } else {
+        const int64_t wg = ceil_div(nh, (int64_t)SCORE_WAVES);
+        const int64_t tiles = (N + SCORE_TILE - 1) / SCORE_TILE;
+        int64_t y = std::min<int64_t>(tiles, std::max<int64_t>(1, (1024 + wg - 1) / wg));
+        const int64_t per = (tiles + y - 1) / y;
+        y = (tiles + per - 1) / per;
+        *gx = wg;
+        *gy = (int)y;
+        return per * SCORE_TILE;
+    }
 }
 
 // grid = 1 workgroup of 1024 threads: the winner (wg_select_best), then the
@@ -630,15 +804,16 @@ int ransac_run(const double *x1, const double *x2, int64_t N, const int32_t *sam
     }
     SFM_HIP(hipEventRecord(c->ev[1], s));
     int ny;
-    const int64_t slice = score_slice(H, N, &ny, score_per_wg<M>());
+    int64_t gx;
+    const int64_t arg = score_grid<M>(H, N, &gx, &ny);
     if ((rc = launch_fit<M>(d1, d2, ds, H, dF, ny > 1 ? dcnt : nullptr, s))) return rc;
     SFM_HIP(hipEventRecord(c->ev[2], s));
     if constexpr (M::SPLIT)
-        hipLaunchKernelGGL((k_epi_score<false>), dim3(ceil_div(H, score_per_wg<M>()), ny), dim3(score_threads<M>()), 0,
-                           s, d1, d2, N, dF, H, thr, dcnt, slice, FitNext{}, score_split_on(), tmax, pk);
+        hipLaunchKernelGGL((k_epi_score<false>), dim3((unsigned)gx, ny), dim3(score_threads<M>()), 0, s, d1, d2, N, dF,
+                           H, thr, dcnt, (int)arg, FitNext{}, score_split_on(), tmax, pk);
     else
-        hipLaunchKernelGGL((k_ransac_score<M, false>), dim3(ceil_div(H, SCORE_WAVES), ny), dim3(64 * SCORE_WAVES), 0, s,
-                           d1, d2, N, dF, H, thr, dcnt, slice, FitNext{});
+        hipLaunchKernelGGL((k_ransac_score<M, false>), dim3((unsigned)gx, ny), dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
+                           dF, H, thr, dcnt, arg, FitNext{});
     SFM_HIP(hipGetLastError());
     SFM_HIP(hipEventRecord(c->ev[3], s));
     hipLaunchKernelGGL(k_ransac_select<M>, dim3(1), dim3(1024), 0, s, d1, d2, N, dF, dcnt, H, thr, dbest, dFb, dmask);
@@ -744,19 +919,21 @@ struct ScorePipe {
 
     int score(int64_t a, int64_t b, const FitNext *fn) {
         int ny;
-        const int64_t n = b - a, slice = score_slice(n, N, &ny, score_per_wg<M>());
-        const dim3 grid((unsigned)(ceil_div(n, score_per_wg<M>()) + (fn ? fn->nfb : 0)), ny);
+        int64_t gx;
+        const int64_t n = b - a, arg = score_grid<M>(n, N, &gx, &ny);
+        const dim3 grid((unsigned)(gx + (fn ? fn->nfb : 0)), ny);
         if constexpr (M::SPLIT) {
             if (fn)
                 hipLaunchKernelGGL((k_epi_score<true>), grid, dim3(score_threads<M>()), 0, s, d1, d2, N,
-                                   dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, *fn, score_split_on(), tmax, pk);
+                                   dF + (a - off) * 9, n, thr, dcnt + (a - off), (int)arg, *fn, score_split_on(), tmax,
+                                   pk);
             else
                 hipLaunchKernelGGL((k_epi_score<false>), grid, dim3(score_threads<M>()), 0, s, d1, d2, N,
-                                   dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, FitNext{}, score_split_on(), tmax,
-                                   pk);
+                                   dF + (a - off) * 9, n, thr, dcnt + (a - off), (int)arg, FitNext{}, score_split_on(),
+                                   tmax, pk);
         } else {  // the H model (no group fit: its fits run on their own)
             hipLaunchKernelGGL((k_ransac_score<M, false>), grid, dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
-                               dF + (a - off) * 9, n, thr, dcnt + (a - off), slice, FitNext{});
+                               dF + (a - off) * 9, n, thr, dcnt + (a - off), arg, FitNext{});
         }
         SFM_HIP(hipGetLastError());
         return 0;
@@ -765,7 +942,8 @@ struct ScorePipe {
     int add(int64_t a, int64_t b, const int32_t *rows) {
         if (b <= a) return 0;
         int ny, rc;
-        (void)score_slice(b - a, N, &ny, score_per_wg<M>());  // as score() will cut it
+        int64_t gx;
+        (void)score_grid<M>(b - a, N, &gx, &ny);  // as score() will cut it
         int32_t *cz = ny > 1 ? dcnt + (a - off) : nullptr;
         if (!fused) {
             if ((rc = launch_fit<M>(d1, d2, rows, b - a, dF + (a - off) * 9, cz, s))) return rc;

@@ -152,10 +152,7 @@ __device__ __forceinline__ EpiPart epi_fast_b(const EpiPartA &a, const double *F
 struct EpiPre {
     float g[9];
     float q1, q0;
-    // the full float test (epi_full_test): bounds of e and of the two line
-    // norms, the scaled 1e-8, and the band edges of 2 thr
-    float E, Ea, Eb, c, Thi, Tlo;
-    bool on;  // wave-uniform: the prefilter applies to this hypothesis and slice
+    bool on;  // the prefilter applies to this hypothesis and coordinate range
 };
 
 // per hypothesis f (finite) and slice bounds b = (X, Y, U, V)
@@ -183,9 +180,6 @@ __device__ __forceinline__ EpiPre epi_pre_setup(const double *f, double thr_hi2,
     const double A2 = fabs(g[6]) * X + fabs(g[7]) * Y + fabs(g[8]);
     const double Mt = U * A0 + V * A1 + A2;
     const double At = sqrt(A0 * A0 + A1 * A1);
-    const double B0 = fabs(g[0]) * U + fabs(g[3]) * V + fabs(g[6]);  // |F^T x2|'s row terms
-    const double B1 = fabs(g[1]) * U + fabs(g[4]) * V + fabs(g[7]);
-    const double Bt = sqrt(B0 * B0 + B1 * B1);
     const double E = 5e-7 * Mt + 0x1p-70;
     const double K1 = thr_hi2 * (1.0 + 1e-6);
     const double K0 = thr_hi2 * (3e-7 * At + 0x1p-60 + c) + E;
@@ -194,82 +188,31 @@ __device__ __forceinline__ EpiPre epi_pre_setup(const double *f, double thr_hi2,
     r.q0 = __double2float_ru((1.0 + 1.0 / d) * K0 * K0 * (1.0 + 0x1p-20));
 #pragma unroll
     for (int k = 0; k < 9; ++k) r.g[k] = (float)g[k];
-    r.E = __double2float_ru(E);
-    r.Ea = __double2float_ru(3e-7 * At + 0x1p-60);
-    r.Eb = __double2float_ru(3e-7 * Bt + 0x1p-60);
-    r.c = (float)c;  // its rounding (relative 2^-24 of c <= the line norms' terms) is inside the 1e-5
-    r.Thi = __double2float_ru(thr_hi2 * (1.0 + 1e-5));
-    const double tlo = thr_hi2 / (1.0 + 1e-4) * (1.0 - 1e-4);  // 2 thr (1 - 1e-4): thr_lo2 of the FP64 test
-    r.Tlo = __double2float_rd(tlo * (1.0 - 1e-5));
     r.on = true;
     return r;
 }
-// the same, its values in scalar registers (wave-uniform: f and b are), so
-// the packed test takes them as broadcast SGPR operands instead of VGPR pairs
-__device__ __forceinline__ EpiPre epi_pre_uniform(const EpiPre &p) {
-    EpiPre r;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) r.g[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(p.g[k])));
-    r.q1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(p.q1)));
-    r.q0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(p.q0)));
-    // the full test's constants stay in vector registers (scalar ones
-    // spilled: the kernel is at its SGPR limit)
-    r.E = p.E;
-    r.Ea = p.Ea;
-    r.Eb = p.Eb;
-    r.c = p.c;
-    r.Thi = p.Thi;
-    r.Tlo = p.Tlo;
-    r.on = __builtin_amdgcn_readfirstlane((int)p.on) != 0;
-    return r;
-}
-
 typedef float epi_f2 __attribute__((ext_vector_type(2)));
+
+// the prefilter's constants as broadcast pairs (both halves equal), the
+// operands the packed instructions take as they are (from single floats the
+// compiler copied each into an aligned register pair per hypothesis)
+struct EpiPk {
+    epi_f2 q1, q0, g[9];
+};
 
 // two pairs: pa = (x_0, x_1, y_0, y_1), pb = (u_0, u_1, v_0, v_1) (pair 0 in
 // the low halves); out0 / out1: proven outliers
-__device__ __forceinline__ void epi_pre_test(const EpiPre &p, float4 pa, float4 pb, bool &out0, bool &out1) {
+__device__ __forceinline__ void epi_pre_test(const EpiPk &p, float4 pa, float4 pb, bool &out0, bool &out1) {
     const epi_f2 x = {pa.x, pa.y}, y = {pa.z, pa.w}, u = {pb.x, pb.y}, v = {pb.z, pb.w};
-    auto bc = [](float s) { return epi_f2{s, s}; };
-    const epi_f2 a0 = __builtin_elementwise_fma(bc(p.g[1]), y, __builtin_elementwise_fma(bc(p.g[0]), x, bc(p.g[2])));
-    const epi_f2 a1 = __builtin_elementwise_fma(bc(p.g[4]), y, __builtin_elementwise_fma(bc(p.g[3]), x, bc(p.g[5])));
-    const epi_f2 a2 = __builtin_elementwise_fma(bc(p.g[7]), y, __builtin_elementwise_fma(bc(p.g[6]), x, bc(p.g[8])));
+    const epi_f2 a0 = __builtin_elementwise_fma(p.g[1], y, __builtin_elementwise_fma(p.g[0], x, p.g[2]));
+    const epi_f2 a1 = __builtin_elementwise_fma(p.g[4], y, __builtin_elementwise_fma(p.g[3], x, p.g[5]));
+    const epi_f2 a2 = __builtin_elementwise_fma(p.g[7], y, __builtin_elementwise_fma(p.g[6], x, p.g[8]));
     const epi_f2 e = __builtin_elementwise_fma(u, a0, __builtin_elementwise_fma(v, a1, a2));
     const epi_f2 qa = __builtin_elementwise_fma(a0, a0, a1 * a1);
-    const epi_f2 rhs = __builtin_elementwise_fma(bc(p.q1), qa, bc(p.q0));
+    const epi_f2 rhs = __builtin_elementwise_fma(p.q1, qa, p.q0);
     const epi_f2 e2 = e * e;
     out0 = e2.x > rhs.x;
     out1 = e2.y > rhs.y;
-}
-
-// The full float test of one pair (round 5), for the sets the prefilter
-// leaves: both lines, proving "outlier" or "inlier" against the FP64 test's
-// band (2 thr (1 -/+ 1e-4), which absorbs the reference's own rounding of
-// d1, d2 and the mean) widened by 1e-5 for this evaluation's roundings.
-// With the prefilter's bounds (e within E; each line norm, here sqrt of the
-// float qa / qb, within a factor 1 -/+ 1e-6 and Ea / Eb):
-//   2 mean >= (|e~| - E) (1 / (sa (1 + 1e-6) + Ea + c) + 1 / (sb ... + c))
-//   2 mean <= (|e~| + E) (1 / (max(0, sa (1 - 1e-6) - Ea) + c) + ...)
-// Each bound term comes from one fma or one add of floats (a single
-// rounding of the exact value, relative 2^-24 of the result, so no
-// cancellation error), v_sqrt_f32 and v_rcp_f32 are within an ulp: a few
-// 1e-7 in all, inside the 1e-5.  Returns 0 outlier, 1 inlier,
-// 2 undecided (NaN anywhere fails both comparisons: undecided).
-__device__ __forceinline__ int epi_full_test(const EpiPre &p, float x, float y, float u, float v) {
-    const float a0 = fmaf(p.g[1], y, fmaf(p.g[0], x, p.g[2]));
-    const float a1 = fmaf(p.g[4], y, fmaf(p.g[3], x, p.g[5]));
-    const float a2 = fmaf(p.g[7], y, fmaf(p.g[6], x, p.g[8]));
-    const float e = fmaf(u, a0, fmaf(v, a1, a2));
-    const float b0 = fmaf(p.g[3], v, fmaf(p.g[0], u, p.g[6]));
-    const float b1 = fmaf(p.g[4], v, fmaf(p.g[1], u, p.g[7]));
-    const float sa = __builtin_amdgcn_sqrtf(fmaf(a0, a0, a1 * a1)), sb = __builtin_amdgcn_sqrtf(fmaf(b0, b0, b1 * b1));
-    const float ae = fabsf(e);
-    const float ha = fmaf(sa, 1.0f + 1e-6f, p.Ea) + p.c, hb = fmaf(sb, 1.0f + 1e-6f, p.Eb) + p.c;
-    const float la = fmaxf(fmaf(sa, 1.0f - 1e-6f, -p.Ea), 0.0f) + p.c;
-    const float lb = fmaxf(fmaf(sb, 1.0f - 1e-6f, -p.Eb), 0.0f) + p.c;
-    const float lo = (ae - p.E) * (__builtin_amdgcn_rcpf(ha) + __builtin_amdgcn_rcpf(hb));
-    const float hi = (ae + p.E) * (__builtin_amdgcn_rcpf(la) + __builtin_amdgcn_rcpf(lb));
-    return lo > p.Thi ? 0 : hi < p.Tlo ? 1 : 2;
 }
 
 // the exact tail of epi_inlier from epi_fast's terms (same operations)
