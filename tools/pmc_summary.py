@@ -23,7 +23,14 @@ import shutil
 import sys
 
 
-SETUP_KERNELS = ("k_gather_cam_major",)  # sfm_ba_create's device-side camera-major copies
+# sfm_ba_create's device-side work (once per problem, not per LM iteration):
+# the camera-major copies, the CSR / radix sort, the sweep planner's passes
+SETUP_KERNELS = ("k_gather_cam_major", "k_csr_cnt", "k_csr_pstart", "k_csr_cstart", "k_plan_counts",
+                 "k_plan_chunkmax", "k_plan_lists", "k_plan_narrow")
+
+
+def is_setup(name):
+    return short(name) in SETUP_KERNELS or "rocprim" in name
 
 
 def short(name):
@@ -65,7 +72,7 @@ def main(src, dst, iterations=0, workload=""):
     if iterations:
         # create-time launches (once per problem, not per LM iteration) are
         # kept out of the per-iteration bytes and listed beside them
-        setup = [k for k in out if short(k) in SETUP_KERNELS]
+        setup = [k for k in out if is_setup(k)]
         per = {k: (2 * d["FETCH_SIZE_total"] + d["WRITE_SIZE_total"]) * 1024 / iterations
                for k, d in out.items() if "FETCH_SIZE_total" in d and "WRITE_SIZE_total" in d and k not in setup}
         json.dump({"iterations": iterations, "source": src, "total_bytes_per_iteration": sum(per.values()),
