@@ -2793,6 +2793,39 @@ __global__ void __launch_bounds__(256) k_csr_cnt(int64_t no, int32_t nc, const i
     }
 }
 
+// the same counts through a per-workgroup LDS histogram of the upper
+// triangle (nc (nc + 1) / 2 counters, up to 160 KB), flushed with one global
+// atomic per nonzero counter and workgroup: the global form's atomics all
+// land on those few addresses (cfg4: 5.5 M atomics on 1,275 counters, 1.0 ms;
+// cfg5 1.06 ms).  A bounded grid (CSR_CNT_WGS) keeps the flush small.
+constexpr int CSR_CNT_WGS = 128;
+__global__ void __launch_bounds__(256) k_csr_cnt_lds(int64_t no, int32_t nc, const int32_t *__restrict__ pstart,
+                                                     const int32_t *__restrict__ pt, const int32_t *__restrict__ cam,
+                                                     uint32_t *__restrict__ cnt, uint32_t *__restrict__ dup) {
+    extern __shared__ uint32_t csr_hist[];
+    const int ntri = nc * (nc + 1) / 2;
+    for (int i = threadIdx.x; i < ntri; i += 256) csr_hist[i] = 0;
+    __syncthreads();
+    bool twice = false;
+    for (int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x; a < no; a += (int64_t)gridDim.x * 256) {
+        const int ca = cam[a];
+        const int32_t e = pstart[pt[a] + 1];
+        atomicAdd(&csr_hist[dense_blk_d(nc, ca, ca)], 1u);
+        for (int32_t b = (int32_t)a + 1; b < e; ++b) {
+            const int cb = cam[b];
+            twice |= cb == ca;
+            atomicAdd(&csr_hist[ca < cb ? dense_blk_d(nc, ca, cb) : dense_blk_d(nc, cb, ca)], 1u);
+        }
+    }
+    if (twice) atomicOr(dup, 1u);
+    __syncthreads();
+    for (int r = 0; r < nc; ++r)
+        for (int c = r + (int)threadIdx.x; c < nc; c += 256) {
+            const uint32_t v = csr_hist[dense_blk_d(nc, r, c)];
+            if (v) atomicAdd(&cnt[(size_t)r * nc + c], v);
+        }
+}
+
 // the pinned staging buffer of create's uploads (grown, never shrunk; one
 // user at a time)
 struct PinnedStage {
@@ -2837,6 +2870,52 @@ __global__ void __launch_bounds__(256) k_plan_chunkmax(int32_t nc, int32_t nspec
     if (threadIdx.x < 2) out[2 * q + threadIdx.x] = mx[threadIdx.x];
 }
 
+// The same statistics with each chunk split over gridDim.y workgroups
+// (one workgroup per chunk walked up to 65,535 observations and their pairs
+// on 256 threads: cfg5 0.49 ms per trial cut, cfg4 0.29, two to four trials
+// per create): partial counts in LDS, added into cnt[q][nc + nspec]
+// (zeroed), then k_plan_chunkmax_fin takes the two maxima per chunk.
+__global__ void __launch_bounds__(256) k_plan_chunkcnt(int32_t nc, int32_t nspec, const int32_t *__restrict__ pstart,
+                                                       const int32_t *__restrict__ pt, const int32_t *__restrict__ cam,
+                                                       const int32_t *__restrict__ cut, const int32_t *__restrict__ cend,
+                                                       const int32_t *__restrict__ spec_of, uint32_t *__restrict__ cnt) {
+    extern __shared__ int32_t plan_sh[];
+    int32_t *cc = plan_sh, *cp = plan_sh + nc;
+    const int q = blockIdx.x;
+    for (int i = threadIdx.x; i < nc + nspec; i += blockDim.x) plan_sh[i] = 0;
+    __syncthreads();
+    const int32_t o0 = pstart[cut[q]], o1 = pstart[cend[q]], len = o1 - o0;
+    const int32_t a0 = o0 + (int32_t)((int64_t)len * blockIdx.y / gridDim.y);
+    const int32_t a1 = o0 + (int32_t)((int64_t)len * (blockIdx.y + 1) / gridDim.y);
+    for (int32_t a = a0 + (int32_t)threadIdx.x; a < a1; a += blockDim.x) {
+        const int ca = cam[a], pnt = pt[a];
+        atomicAdd(&cc[ca], 1);
+        for (int32_t b = pstart[pnt]; b < pstart[pnt + 1]; ++b) {
+            const int cb = cam[b];
+            if (cb > ca) atomicAdd(&cp[spec_of[ca * nc + cb]], 1);
+        }
+    }
+    __syncthreads();
+    uint32_t *row = cnt + (size_t)q * (nc + nspec);
+    for (int i = threadIdx.x; i < nc + nspec; i += blockDim.x)
+        if (plan_sh[i]) atomicAdd(&row[i], (uint32_t)plan_sh[i]);
+}
+__global__ void __launch_bounds__(256) k_plan_chunkmax_fin(int32_t nc, int32_t nspec, const uint32_t *__restrict__ cnt,
+                                                           const int32_t *__restrict__ spec_cam,
+                                                           int32_t *__restrict__ out) {
+    __shared__ int32_t mx[2];
+    if (threadIdx.x < 2) mx[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t *cc = cnt + (size_t)blockIdx.x * (nc + nspec), *cp = cc + nc;
+    for (int w = threadIdx.x; w < nspec; w += blockDim.x) {
+        const int c0 = spec_cam[2 * w], c1 = spec_cam[2 * w + 1];
+        atomicMax(&mx[0], (int32_t)(cc[c0] + (c1 >= 0 ? cc[c1] : 0)));
+        atomicMax(&mx[1], (int32_t)cp[w]);
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) out[2 * blockIdx.x + threadIdx.x] = mx[threadIdx.x];
+}
+
 // per chunk (cut: the chunks' first points, nchunk + 1 entries, the last
 // np_): pairs per camera block, bq[blk][q], and observations per camera,
 // cq[c][q] (32-bit counters; k_plan_narrow makes the host planner's uint16)
@@ -2852,6 +2931,38 @@ __global__ void __launch_bounds__(256) k_plan_counts(int64_t no, int32_t nc, int
     for (int32_t b = pstart[pnt]; b < pstart[pnt + 1]; ++b) {
         const int cb = cam[b];
         if (cb > ca) atomicAdd(&bq[(size_t)dense_blk_d(nc, ca, cb) * nchunk + q], 1u);
+    }
+}
+// k_plan_counts with a chunk's observations split over gridDim.y
+// workgroups: the counts in an LDS histogram (blocks, then cameras), added
+// into bq / cq once per nonzero counter and workgroup.  The global form's
+// atomics of a chunk land on its nbd block counters (cfg4: 1,275 of them,
+// 0.35 ms; cfg5 0.80 ms).
+__global__ void __launch_bounds__(256) k_plan_counts_lds(int32_t nc, int32_t nchunk, const int32_t *__restrict__ pstart,
+                                                         const int32_t *__restrict__ pt, const int32_t *__restrict__ cam,
+                                                         const int32_t *__restrict__ cut, uint32_t *__restrict__ bq,
+                                                         uint32_t *__restrict__ cq) {
+    extern __shared__ uint32_t pc_hist[];
+    const int nbd = nc * (nc + 1) / 2;
+    uint32_t *hb = pc_hist, *hc = pc_hist + nbd;
+    for (int i = threadIdx.x; i < nbd + nc; i += 256) pc_hist[i] = 0;
+    __syncthreads();
+    const int q = blockIdx.x;
+    const int32_t o0 = pstart[cut[q]], o1 = pstart[cut[q + 1]], len = o1 - o0;
+    const int32_t a0 = o0 + (int32_t)((int64_t)len * blockIdx.y / gridDim.y);
+    const int32_t a1 = o0 + (int32_t)((int64_t)len * (blockIdx.y + 1) / gridDim.y);
+    for (int32_t a = a0 + (int32_t)threadIdx.x; a < a1; a += 256) {
+        const int32_t pnt = pt[a], ca = cam[a];
+        atomicAdd(&hc[ca], 1u);
+        for (int32_t b = pstart[pnt]; b < pstart[pnt + 1]; ++b) {
+            const int cb = cam[b];
+            if (cb > ca) atomicAdd(&hb[dense_blk_d(nc, ca, cb)], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nbd + nc; i += 256) {
+        const uint32_t v = pc_hist[i];
+        if (v) atomicAdd(i < nbd ? &bq[(size_t)i * nchunk + q] : &cq[(size_t)(i - nbd) * nchunk + q], v);
     }
 }
 __global__ void __launch_bounds__(256) k_plan_narrow(int64_t n, const uint32_t *__restrict__ in, uint16_t *__restrict__ out) {
@@ -3318,9 +3429,22 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
             int32_t *d_cc = dev->scratch<int32_t>(2 * nk), *d_out = dev->scratch<int32_t>(2 * nk);
             if (dev->err) return;
             dev->ok(hipMemcpyAsync(d_cc, cc.data(), 2 * nk * 4, hipMemcpyHostToDevice, dev->s));
-            hipLaunchKernelGGL(k_plan_chunkmax, dim3((unsigned)nk), dim3(256), (nc + P.nspec + 2) * sizeof(int32_t),
-                               dev->s, nc, P.nspec, dev->pstart, dev->pt, dev->cam, d_cc, d_cc + nk, d_spec_of, d_scam,
-                               d_out);
+            const int split = env_int("SFM_PLAN_CHUNK_SPLIT", std::max(1, std::min(16, (int)ceil_div(1024, (int64_t)nk))));
+            if (split > 1) {
+                uint32_t *d_cnt = dev->scratch<uint32_t>(nk * (size_t)(nc + P.nspec));
+                if (dev->err) return;
+                dev->ok(hipMemsetAsync(d_cnt, 0, nk * (size_t)(nc + P.nspec) * 4, dev->s));
+                hipLaunchKernelGGL(k_plan_chunkcnt, dim3((unsigned)nk, (unsigned)split), dim3(256),
+                                   (nc + P.nspec) * sizeof(int32_t), dev->s, nc, P.nspec, dev->pstart, dev->pt,
+                                   dev->cam, d_cc, d_cc + nk, d_spec_of, d_cnt);
+                dev->ok(hipGetLastError());
+                hipLaunchKernelGGL(k_plan_chunkmax_fin, dim3((unsigned)nk), dim3(256), 0, dev->s, nc, P.nspec, d_cnt,
+                                   d_scam, d_out);
+            } else {
+                hipLaunchKernelGGL(k_plan_chunkmax, dim3((unsigned)nk), dim3(256), (nc + P.nspec + 2) * sizeof(int32_t),
+                                   dev->s, nc, P.nspec, dev->pstart, dev->pt, dev->cam, d_cc, d_cc + nk, d_spec_of,
+                                   d_scam, d_out);
+            }
             dev->ok(hipGetLastError());
             dev->ok(hipMemcpyAsync(out.data(), d_out, 2 * nk * 4, hipMemcpyDeviceToHost, dev->s));
             dev->ok(hipStreamSynchronize(dev->s));
@@ -3372,8 +3496,20 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
         dev->ok(hipMemcpyAsync(dev->d_cut, P.cut.data(), P.cut.size() * 4, hipMemcpyHostToDevice, dev->s));
         dev->ok(hipMemsetAsync(b32, 0, (nb + ncq) * 4, dev->s));
         if (no) {
-            hipLaunchKernelGGL(k_plan_counts, dim3((unsigned)ceil_div(no, 256)), dim3(256), 0, dev->s, no, nc, P.nchunk,
-                               dev->pstart, dev->pt, dev->cam, dev->d_cut, b32, b32 + nb);
+            // the LDS form while its histogram fits, split so that a
+            // workgroup's pairs are several times its counters (the flush)
+            const size_t hist = ((size_t)P.nbd + nc) * sizeof(uint32_t);
+            static const bool big_lds =
+                hipFuncSetAttribute(reinterpret_cast<const void *>(&k_plan_counts_lds),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+            const double pairs = (double)std::accumulate(cnt.begin(), cnt.end(), int64_t(0)) - (double)no;
+            const int split = std::max(1, std::min(16, (int)(pairs / P.nchunk / (4.0 * (P.nbd + nc)))));
+            if (hist <= (big_lds ? 160 * 1024 : 64 * 1024) && !env_int("SFM_PLAN_COUNTS_GLOBAL", 0))
+                hipLaunchKernelGGL(k_plan_counts_lds, dim3((unsigned)P.nchunk, (unsigned)split), dim3(256), hist,
+                                   dev->s, nc, P.nchunk, dev->pstart, dev->pt, dev->cam, dev->d_cut, b32, b32 + nb);
+            else
+                hipLaunchKernelGGL(k_plan_counts, dim3((unsigned)ceil_div(no, 256)), dim3(256), 0, dev->s, no, nc,
+                                   P.nchunk, dev->pstart, dev->pt, dev->cam, dev->d_cut, b32, b32 + nb);
             dev->ok(hipGetLastError());
         }
         hipLaunchKernelGGL(k_plan_narrow, dim3((unsigned)ceil_div((int64_t)(nb + ncq), 256)), dim3(256), 0, dev->s,
@@ -4053,8 +4189,17 @@ static int ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, co
                            p->d_cstart);
         SFM_HIP(hipGetLastError());
         if (no) {
-            hipLaunchKernelGGL(k_csr_cnt, dim3((unsigned)ceil_div(no, 256)), dim3(256), 0, s, no, nc, p->d_pstart,
-                               p->d_pt, p->d_cam, cnt32, cnt32 + (size_t)nc * nc);
+            const size_t hist = (size_t)nc * (nc + 1) / 2 * sizeof(uint32_t);
+            static const bool big_lds =
+                hipFuncSetAttribute(reinterpret_cast<const void *>(&k_csr_cnt_lds),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+            if (hist <= (big_lds ? 160 * 1024 : 64 * 1024) && !env_int("SFM_CSR_CNT_GLOBAL", 0))
+                hipLaunchKernelGGL(k_csr_cnt_lds, dim3((unsigned)std::min<int64_t>(CSR_CNT_WGS, ceil_div(no, 256))),
+                                   dim3(256), hist, s, no, nc, p->d_pstart, p->d_pt, p->d_cam, cnt32,
+                                   cnt32 + (size_t)nc * nc);
+            else
+                hipLaunchKernelGGL(k_csr_cnt, dim3((unsigned)ceil_div(no, 256)), dim3(256), 0, s, no, nc,
+                                   p->d_pstart, p->d_pt, p->d_cam, cnt32, cnt32 + (size_t)nc * nc);
             SFM_HIP(hipGetLastError());
         }
         std::vector<uint32_t> c32((size_t)nc * nc + 1);

@@ -408,13 +408,16 @@ __global__ void __launch_bounds__(64 * EPI_W, FIT ? SFM_EPI_FIT_OCC : SFM_EPI_OC
         }
         if (fin) {
             flags = 1;
-            if (use_pre) {
+            if (use_pre && SFM_EPI_PROBE != 3) {
                 double lo, hi;
                 band(lo, hi);
                 p = epi_pre_setup(f, hi, b);
                 if (p.on) flags |= 2;
             }
         }
+#if SFM_EPI_PROBE == 3 || SFM_EPI_PROBE == 4  // timing probes (wrong counts): no setup / setup, no loop
+        flags = 0;
+#endif
         sC[t][0] = make_float4(__int_as_float(flags), 0.f, p.q1, p.q1);
         sC[t][1] = make_float4(p.q0, p.q0, p.g[0], p.g[0]);
 #pragma unroll
