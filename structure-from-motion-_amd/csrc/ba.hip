@@ -3358,26 +3358,38 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     // chunk staged, ~7 us) and the end-of-range reduction, so fewer, longer
     // workgroups win even with a partial last pass over the CUs (cfg5, 100
     // specs: 16 ranges 0.539 ms, 8 ranges 0.505 ms; cfg4: 0.145 -> 0.161 ms at 16)
-    // Round 5: a rank's shard (1/N of the points) keeps 8 ranges only while
-    // its work fills the dispatch rounds; a small shard takes 4, 2 or 1 range
-    // (every range then spans 8 / nrange XCDs): fewer, longer workgroups in
-    // one round instead of four short rounds of mostly prologue and
-    // reduction.  Model per candidate: rounds x (13.3 us fixed + 4.7 ns per
-    // pair / workgroups), calibrated on cfg5's measured sweep (800
-    // workgroups, 95 us each); rounds fractional for 8 (the dispatch tail is
-    // split) and whole below.  cfg4 / cfg5 whole: 8; cfg5 points over 4 or 8
-    // ranks: 2.  SFM_SWEEP_RANGES overrides (a multiple of 8, or 1, 2, 4).
+    // Round 5, late: one round of workgroups, as many as fit -- the largest
+    // range count with nspec x nrange <= the CU count (one sweep workgroup a
+    // CU: ~150 KB of LDS).  Measured, cfg5 (100 specs) sweep + finish, rank
+    // 0's shard of N (tools/gpu_sweepvar.sh, same box):
+    //   N = 1: 8 ranges 0.330 ms, 4 0.324, 2 0.306, 1 0.557, 16 0.387
+    //   N = 2: 8 0.208, 4 0.182, 2 0.168, 1 0.288
+    //   N = 4: 8 0.139, 4 0.114, 2 0.102, 1 0.155
+    //   N = 8: 8 0.115, 4 0.083, 2 0.075, 1 0.095
+    // so 2 at every N (200 workgroups); cfg4 (25 specs) keeps 8 (its 16 had
+    // measured 0.161 against 0.145 ms).  More specs than CUs: the round-4
+    // model (rounds x (13.3 us + 4.7 ns per pair / workgroups), fractional
+    // rounds for 8, whose dispatch tail is split).  SFM_SWEEP_RANGES
+    // overrides (a multiple of 8, or 1, 2, 4).
     {
-        const double pairs = (double)std::accumulate(cnt.begin(), cnt.end(), int64_t(0)) - (double)no;
-        int best = NXCD;
-        double tbest = 1e300;
-        for (int nr : {8, 4, 2, 1}) {
-            const double wgs = (double)P.nspec * nr;
-            const double rounds = nr >= NXCD ? std::max(1.0, wgs / ncu) : std::ceil(wgs / ncu);
-            const double t = rounds * (13.3 + pairs * 4.7e-3 / wgs);
-            if (t < tbest * 0.97) {  // a smaller count only for a clear win
-                tbest = t;
+        int best = 0;
+        for (int nr : {8, 4, 2, 1})
+            if ((int64_t)P.nspec * nr <= ncu) {
                 best = nr;
+                break;
+            }
+        if (!best) {
+            const double pairs = (double)std::accumulate(cnt.begin(), cnt.end(), int64_t(0)) - (double)no;
+            double tbest = 1e300;
+            best = NXCD;
+            for (int nr : {8, 4, 2, 1}) {
+                const double wgs = (double)P.nspec * nr;
+                const double rounds = nr >= NXCD ? std::max(1.0, wgs / ncu) : std::ceil(wgs / ncu);
+                const double t = rounds * (13.3 + pairs * 4.7e-3 / wgs);
+                if (t < tbest * 0.97) {  // a smaller count only for a clear win
+                    tbest = t;
+                    best = nr;
+                }
             }
         }
         const int e = env_int("SFM_SWEEP_RANGES", 0);

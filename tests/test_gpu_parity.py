@@ -1012,11 +1012,16 @@ def test_ba_sweep_split_and_gjr_fold_paths(core, monkeypatch):
     order, so the LM agrees to rounding), and k_schur_finish folded into the
     row solve's prologue (SFM_GJR_FOLD=1: the slabs read in the finish's
     order, camera U / g from the camera-block partials) against the finish
-    launch: the same sums in the same order, so bitwise the same solve."""
+    launch: the same sums in the same order, so bitwise the same solve.
+    The split needs 8 ranges (one a XCD); cfg5 plans 2 by default since
+    round 5, so the test asks for 8, and the default plan joins the
+    comparison."""
     p = syn.ba_problem_cfg("cfg5", dense=False)
     cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
     args = (cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K)
     out = {}
+    out["default", "0"] = core.ba_lm(*args, max_iterations=12)
+    monkeypatch.setenv("SFM_SWEEP_RANGES", "8")
     for split, fold in (("8", "0"), ("0", "0"), ("8", "1"), ("0", "1")):
         monkeypatch.setenv("SFM_SWEEP_SPLIT", split)
         monkeypatch.setenv("SFM_GJR_FOLD", fold)
