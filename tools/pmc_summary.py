@@ -25,8 +25,9 @@ import sys
 
 # sfm_ba_create's device-side work (once per problem, not per LM iteration):
 # the camera-major copies, the CSR / radix sort, the sweep planner's passes
-SETUP_KERNELS = ("k_gather_cam_major", "k_csr_cnt", "k_csr_pstart", "k_csr_cstart", "k_plan_counts",
-                 "k_plan_chunkmax", "k_plan_lists", "k_plan_narrow")
+SETUP_KERNELS = ("k_gather_cam_major", "k_csr_cnt", "k_csr_cnt_lds", "k_csr_pstart", "k_csr_cstart",
+                 "k_plan_counts", "k_plan_counts_lds", "k_plan_chunkmax", "k_plan_chunkcnt", "k_plan_chunkmax_fin",
+                 "k_plan_lists", "k_plan_narrow")
 
 
 def is_setup(name):
