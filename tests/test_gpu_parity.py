@@ -1330,6 +1330,34 @@ def test_ransac_float_prefilter_never_changes_a_count(core, monkeypatch, scale):
         assert np.array_equal(pyr, pyr_off), thr
 
 
+def test_ransac_score_queue_overflow(core, monkeypatch):
+    """k_epi_score's survivor queue past its capacity: a threshold far above
+    every distance (but below the prefilter's own cutoff) leaves every pair
+    a candidate, so each workgroup queues 4096 of its ~20,000 (4 hypotheses
+    x 5,000 pairs) and tests the rest in place.  Counts equal the FP64 path's
+    (SFM_SCORE_PRE=0) and, for the first hypotheses, the reference
+    expression's (O.epi_err with the hypothesis' own F); a second case puts
+    the pairs over several ranges (atomically summed counts)."""
+    x1, x2, _, _ = syn.two_view(n=5000, seed=3)
+    random.seed(3)
+    samples = core.sample_table(5000, 8, 2048)
+    for thr in (1e5, 40.0):
+        monkeypatch.delenv("SFM_SCORE_PRE", raising=False)
+        got = core.ransac_f8(x1, x2, samples, thr, want_counts=True)[3]
+        monkeypatch.setenv("SFM_SCORE_PRE", "0")
+        off = core.ransac_f8(x1, x2, samples, thr, want_counts=True)[3]
+        assert np.array_equal(got, off), thr
+        for h in range(4):
+            F = core.ransac_f8(x1, x2, samples[h:h + 1], 1e300)[1]
+            assert got[h] == (O.epi_err(x1, x2, F) < thr).sum(), (thr, h)
+    monkeypatch.delenv("SFM_SCORE_PRE", raising=False)
+    xa, xb, _, _ = syn.two_view(n=20011, seed=4)  # 157 passes, the last partial
+    few = samples[:24] % 20011
+    got = core.ransac_f8(xa, xb, few, 1e5, want_counts=True)[3]
+    monkeypatch.setenv("SFM_SCORE_PRE", "0")
+    assert np.array_equal(got, core.ransac_f8(xa, xb, few, 1e5, want_counts=True)[3])
+
+
 def test_pnp_fast_test_exact_at_threshold(core):
     """The PnP score kernel's fast reprojection test (v_rcp_f64 + Newton, a
     widened band, the exact tail inside it; pnp.hip pnp_fast) against the
