@@ -991,18 +991,27 @@ def test_ba_device_plan_equals_host_plan(core, monkeypatch, shape):
     lists from the uploaded COO) is the host planner's plan (SFM_PLAN_HOST=1)
     byte for byte: the same digest over every plan array, the lists read back
     from the device in both cases.  "many": 356 cameras, long rows split over
-    several specs."""
+    several specs (its block counts exceed the LDS histograms: the global
+    atomic kernels).  The device's global-atomic forms of the block counts,
+    per-chunk counts and chunk statistics (round 5's LDS-histogram kernels
+    off) give the same plan too."""
     p = syn.ba_problem_cfg(shape, dense=False) if shape != "many" else syn.ba_problem(356, 2000, 3, seed=11,
                                                                                      dense=False)
     cams0 = np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])])
     monkeypatch.setenv("SFM_PLAN_DIGEST", "1")
     dig = {}
-    for host in ("0", "1"):
+    for host, glob in (("0", "0"), ("1", "0"), ("0", "1")):
         monkeypatch.setenv("SFM_PLAN_HOST", host)
+        for e in ("SFM_CSR_CNT_GLOBAL", "SFM_PLAN_COUNTS_GLOBAL"):
+            monkeypatch.setenv(e, glob)
+        if glob == "1":
+            monkeypatch.setenv("SFM_PLAN_CHUNK_SPLIT", "1")
+        else:
+            monkeypatch.delenv("SFM_PLAN_CHUNK_SPLIT", raising=False)
         prob = core.BAProblem(cams0, p["X0"], p["cam_idx"], p["pt_idx"], p["obs"], K)
-        dig[host] = prob.plan_digest()
+        dig[host, glob] = prob.plan_digest()
         prob.close()
-    assert dig["0"] != 0 and dig["0"] == dig["1"], dig
+    assert dig["0", "0"] != 0 and dig["0", "0"] == dig["1", "0"] == dig["0", "1"], dig
 
 
 def test_ba_sweep_split_and_gjr_fold_paths(core, monkeypatch):
