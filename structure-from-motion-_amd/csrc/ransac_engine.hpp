@@ -305,9 +305,6 @@ constexpr int EPI_QCAP = 4096;            // candidates a workgroup queues
 #ifndef SFM_EPI_PROBE
 #define SFM_EPI_PROBE 0
 #endif
-#ifndef SFM_EPI_PREFETCH
-#define SFM_EPI_PREFETCH 0
-#endif
 #ifndef SFM_EPI_FIT_OCC
 #define SFM_EPI_FIT_OCC 4
 #endif
@@ -427,9 +424,6 @@ __global__ void __launch_bounds__(64 * EPI_W, FIT ? SFM_EPI_FIT_OCC : SFM_EPI_OC
     }
     int cntv = 0;  // lane k: this wave's count for hypothesis h0 + k
     bool first = true;
-#if SFM_EPI_PREFETCH
-    float4 n[6];
-#endif
     for (int base = P0 + wave; base < P1; base += EPI_W * EPI_SLOTS) {
         // slot s: pass base + s EPI_W
         float4 A[EPI_SLOTS], B[EPI_SLOTS];
@@ -459,24 +453,9 @@ __global__ void __launch_bounds__(64 * EPI_W, FIT ? SFM_EPI_FIT_OCC : SFM_EPI_OC
         if (first) __syncthreads();  // the constants (the loads above in flight)
         first = false;
         for (int k = 0; k < nh; ++k) {
-#if SFM_EPI_PREFETCH
-            // hypothesis k's prefilter quads, read one hypothesis ahead (the LDS
-            // latency off the loop's critical path)
-            float4 c[6];
-            if (k == 0)
-#pragma unroll
-                for (int j = 0; j < 6; ++j) n[j] = sC[0][j];
-            const int kn = min(k + 1, EPI_HB_MAX - 1);
-#pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                c[j] = n[j];
-                n[j] = sC[kn][j];
-            }
-#else
-            float4 c[6];
+            float4 c[6];  // hypothesis k's prefilter quads (LDS broadcasts)
 #pragma unroll
             for (int j = 0; j < 6; ++j) c[j] = sC[k][j];
-#endif
             const int flags = __builtin_amdgcn_readfirstlane(__float_as_int(c[0].x));
             if (!(flags & 1)) continue;
 #if SFM_EPI_PROBE == 2  // timing probe (wrong counts): the loop without tests
