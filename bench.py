@@ -485,7 +485,7 @@ def ransac_leg(args, world, rank, local_rank, comm):
                  "kernels_tflops": round(all_flops / (k_all * 1e-3) / 1e12, 2), "peak_tflops": FP64_PEAK_TFLOPS,
                  "score_frac": round(score_flops / (k_score * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 4),
                  "formula": "score: H*N*50 flop; kernels: H*(N*50 + 25e3) flop (SURVEY §8(d)); algorithmic-equivalent: the score proves most pairs outliers with a packed float prefilter and runs the FP64 test only on the survivors, so it executes far fewer FP64 flops",
-                 "score_bound": "VALU issue, not FP64: score_frac above 1 is the FP64-equivalent rate of mostly FP32 work. Executed: ~21 M VALU instructions per one-shot launch (4 cycles each over 1024 SIMDs, ~0.75 of the issue rate); the drop-in's fused launches 4.0 M in 22 us, ~0.29 (profiles/round5/pmc_traffic_ransac.json, DESIGN \u00a74)"}})
+                 "score_bound": "VALU issue, not FP64: score_frac above 1 is the FP64-equivalent rate of mostly FP32 work. Executed: ~13 M VALU instructions per one-shot launch (4 cycles each over 1024 SIMDs, ~0.47 of the issue rate at 45 us); the drop-in's fused launches 4.0 M in 22 us, ~0.29 (profiles/round5/pmc_traffic_ransac.json, DESIGN \u00a74)"}})
     if comm is None:  # the drop-in call's own kernels (timed above)
         out["fp64"].update({
             "dropin_fit_score_ms": round(dropin_fit_score, 4), "dropin_span_ms": round(dropin_span, 4),
