@@ -158,8 +158,8 @@ def set_call_timing(on=True):
 
 
 def last_timings():
-    out = np.zeros(8)
-    n = _lib.sfm_last_timings(_p(out), 8)
+    out = np.zeros(12)
+    n = _lib.sfm_last_timings(_p(out), 12)
     return out[:n]
 
 

@@ -959,6 +959,8 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
     SFM_CHECK_ARG(N < ((int64_t)1 << 31) && st[624] <= 624, "bad sizes / MT19937 position");
     *best_iter = -1;
     if (H == 0) return 0;
+    const auto t_entry = std::chrono::steady_clock::now();
+    auto since = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_entry).count(); };
     ThreadCtx *c = thread_ctx(device);
     if (!c) return SFM_ERR_HIP;
     const size_t pb = (size_t)N * sizeof(double2);
@@ -1003,6 +1005,7 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
         });
         t_draw += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
     }
+    const double h_pre = since();
     int64_t *dbest = reinterpret_cast<int64_t *>(hout);
     double *dFb = reinterpret_cast<double *>(hout) + 2;
     uint8_t *dmask = reinterpret_cast<uint8_t *>(hout) + 16 * sizeof(double);
@@ -1030,7 +1033,9 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
     if (tm) SFM_HIP(hipEventRecord(c->ev[4], s));
     if (counts_out) SFM_HIP(hipMemcpyAsync(counts_out, dcnt, (size_t)H * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     if (tm) SFM_HIP(hipEventRecord(c->ev[5], s));
+    const double h_enq = since();
     SFM_HIP(hipStreamSynchronize(s));
+    const double h_sync = since();
     *best_iter = *dbest;
     if (*best_iter >= 0) {
         std::memcpy(F_best, dFb, 9 * sizeof(double));
@@ -1051,12 +1056,14 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
         std::memset(best_mask, 0, (size_t)N);
     }
     if (samples_out) std::memcpy(samples_out, hs, sb);
-    double t[7] = {0, 0, 0, 0, 0, 0, t_draw};
+    // [7..10]: host ms from entry to the first chunk drawn, the last launch
+    // enqueued, the stream drained and the return
+    double t[11] = {0, 0, 0, 0, 0, 0, t_draw, h_pre, h_enq, h_sync, since()};
     if (tm) {
         t[0] = ev_ms(c->ev[0], c->ev[1]); t[1] = ev_ms(c->ev[1], c->ev[4]); t[2] = ev_ms(c->ev[4], c->ev[5]);
         t[3] = ev_ms(c->ev[1], c->ev[3]); t[5] = ev_ms(c->ev[3], c->ev[4]);
     }
-    set_timings(t, 7);
+    set_timings(t, 11);
     return 0;
 }
 

@@ -15,7 +15,7 @@
 namespace sfm {
 
 static thread_local std::string g_err;
-static thread_local double g_timings[8];
+static thread_local double g_timings[12];
 static thread_local int g_ntimings = 0;
 
 void set_error(const char *fmt, ...) {
@@ -30,7 +30,7 @@ void clear_error() { g_err.clear(); }
 static std::atomic<int> g_call_timing{0};
 bool call_timing() { return g_call_timing.load(std::memory_order_relaxed) != 0; }
 void set_timings(const double *t, int n) {
-    g_ntimings = n < 8 ? n : 8;
+    g_ntimings = n < 12 ? n : 12;
     for (int i = 0; i < g_ntimings; ++i) g_timings[i] = t[i];
 }
 
