@@ -17,6 +17,8 @@
 //                      mask of the winner.
 #pragma once
 #include <algorithm>
+#include <atomic>
+#include <immintrin.h>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -988,42 +990,77 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
     // pageable memory the copy would hold the host until it lands)
     char *hx = hout + xoff_of(N);
     PySampler ps(st, N, M::K);
-    double t_draw = 0;
-    // the correspondences' copy into pinned memory and the first chunk's
-    // draw on two host threads at once (each ~6-10 us at cfg2), then the
-    // staging kernel and the first fit
+    double t_draw = 0, h_pre = 0;
     const int64_t hfirst = rp_next(0, H);
-    {
-        const auto ta = std::chrono::steady_clock::now();
-        par_for(2, [&](int64_t t) {
-            if (t == 0) {
-                std::memcpy(hx, x1, pb);
-                std::memcpy(hx + pb, x2, pb);
-            } else {
-                ps.draw(0, hfirst, hs);
-            }
-        });
-        t_draw += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
-    }
-    const double h_pre = since();
     int64_t *dbest = reinterpret_cast<int64_t *>(hout);
     double *dFb = reinterpret_cast<double *>(hout) + 2;
     uint8_t *dmask = reinterpret_cast<uint8_t *>(hout) + 16 * sizeof(double);
     hipStream_t s = c->stream;
     const bool tm = call_timing();
-    if (tm) SFM_HIP(hipEventRecord(c->ev[0], s));
-    hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)n_tiles(N)), dim3(TB_THREADS), 0, s,
-                       reinterpret_cast<const double2 *>(hx), N, d1, d2, tmax, pk);
-    SFM_HIP(hipGetLastError());
-    if (tm) SFM_HIP(hipEventRecord(c->ev[1], s));
     ScorePipe<M> pipe{d1, d2, N, thr, s, dF, dcnt, 0, tmax, pk};
-    if ((rc = pipe.add(0, hfirst, hs))) return rc;
-    for (int64_t h0 = hfirst, h1; h0 < H; h0 = h1) {
-        h1 = rp_next(h0, H);
+    // the correspondences into pinned memory and the staging kernel
+    auto stage = [&]() -> int {
+        std::memcpy(hx, x1, pb);
+        std::memcpy(hx + pb, x2, pb);
+        if (tm) SFM_HIP(hipEventRecord(c->ev[0], s));
+        hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)n_tiles(N)), dim3(TB_THREADS), 0, s,
+                           reinterpret_cast<const double2 *>(hx), N, d1, d2, tmax, pk);
+        SFM_HIP(hipGetLastError());
+        if (tm) SFM_HIP(hipEventRecord(c->ev[1], s));
+        return 0;
+    };
+    auto draw = [&](int64_t h0, int64_t h1) {
         const auto ta = std::chrono::steady_clock::now();
         ps.draw(h0, h1, hs);
         t_draw += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
-        if ((rc = pipe.add(h0, h1, hs + h0 * M::K))) return rc;
+        if (h0 == 0) h_pre = since();
+    };
+    // Two host threads (round 5): the caller draws every chunk, a pool
+    // worker copies the points, launches the staging kernel and enqueues
+    // each chunk's fit / score as soon as its rows are drawn, so the ~4-us
+    // launch calls leave the sequential draw's path (one thread had
+    // interleaved them: the last launch at ~129 us after ~101 us of draws).
+    // SFM_RANSAC_LAUNCHER=0, or a busy pool, keeps the one-thread order.
+    static const bool two = [] {
+        const char *e = std::getenv("SFM_RANSAC_LAUNCHER");
+        return !(e && std::atoi(e) == 0) && std::thread::hardware_concurrency() > 1;
+    }();
+    std::atomic<int64_t> drawn{0};
+    int lrc = 0;
+    const bool ran = two && HostPool::get().try_run(2, [&](int t) {
+        if (t == 0) {  // the launcher (a pool worker)
+            if (hipSetDevice(c->device) != hipSuccess) {
+                lrc = SFM_ERR_HIP;
+                return;
+            }
+            if ((lrc = stage())) return;
+            for (int64_t h0 = 0, h1; h0 < H; h0 = h1) {
+                h1 = rp_next(h0, H);
+                while (drawn.load(std::memory_order_acquire) < h1) _mm_pause();
+                if ((lrc = pipe.add(h0, h1, hs + h0 * M::K))) return;
+            }
+        } else {  // the drawer (the caller): every chunk, in the reference's order
+            for (int64_t h0 = 0, h1; h0 < H; h0 = h1) {
+                h1 = rp_next(h0, H);
+                draw(h0, h1);
+                drawn.store(h1, std::memory_order_release);
+            }
+        }
+    });
+    if (ran) {
+        if (lrc) {
+            set_error("RANSAC launcher thread: HIP error %d", lrc);
+            return lrc;
+        }
+    } else {  // one thread: the first chunk's draw, then each launch after its draw
+        draw(0, hfirst);
+        if ((rc = stage())) return rc;
+        if ((rc = pipe.add(0, hfirst, hs))) return rc;
+        for (int64_t h0 = hfirst, h1; h0 < H; h0 = h1) {
+            h1 = rp_next(h0, H);
+            draw(h0, h1);
+            if ((rc = pipe.add(h0, h1, hs + h0 * M::K))) return rc;
+        }
     }
     if ((rc = pipe.flush())) return rc;
     ps.save(st);
