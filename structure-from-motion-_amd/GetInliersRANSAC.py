@@ -7,12 +7,15 @@ update) becomes one batched evaluation on the MI355X:
 1. the n_max samples are drawn from the GLOBAL ``random`` instance exactly as
    the reference draws them (n_max calls of random.sample(range(N), 8) in
    iteration order, replayed natively inside the C-ABI call, chunk by chunk
-   while the GPU scores the chunks already drawn, and written back with
-   setstate), so the stream seen by later callers (PnPRANSAC, the next image
-   pair) is unchanged;
-2. libsfmcore builds every hypothesis F (8 lanes each, the next chunk's fits riding in the current chunk's score launch), scores every
-   (hypothesis, correspondence) pair (one wavefront per hypothesis, LDS
-   tiles, ballot popcount) and picks the first hypothesis with the strictly
+   while the GPU scores the chunks already drawn, the generator's state
+   read and written back in place), so the stream seen by later callers
+   (PnPRANSAC, the next image pair) is unchanged;
+2. libsfmcore builds every hypothesis F (8 lanes each, the next chunk's
+   fits riding in the current chunk's score launch), scores every
+   (hypothesis, correspondence) pair (correspondences held in registers,
+   hypotheses streamed through them: a packed float prefilter proves the
+   outliers, the FP64 test -- the reference's decision bit for bit --
+   decides the rest) and picks the first hypothesis with the strictly
    largest count -- the reference's tie rule (:85-88).
 """
 import numpy as np
