@@ -7,11 +7,15 @@
 //   k_fit_samples<M>   gather the K sampled correspondences and fit the 3x3
 //                      model: 8 lanes per hypothesis for F (f8_points_group8),
 //                      one thread per hypothesis for H.
-//   k_ransac_score<M>  one WAVE per hypothesis: the model is wave-uniform
-//                      (scalar registers); correspondence tiles are staged
-//                      once per workgroup in LDS and every wave sweeps them,
-//                      one correspondence per lane; inlier count = popcount
-//                      of the wave ballot (scalar unit).
+//   k_epi_score        (F) correspondences resident in registers (a packed
+//                      float copy), a workgroup's hypotheses streamed through
+//                      them: packed float prefilter, survivors queued in LDS
+//                      for the FP64 test one lane each (round 5).
+//   k_ransac_score<M>  (H) one WAVE per hypothesis: the model is
+//                      wave-uniform (scalar registers); correspondence tiles
+//                      are staged once per workgroup in LDS and every wave
+//                      sweeps them, one correspondence per lane; inlier
+//                      count = popcount of the wave ballot (scalar unit).
 //   k_ransac_select<M> one workgroup: (max count, min iteration) reduction ==
 //                      the reference's strict '>' update, then the inlier
 //                      mask of the winner.
