@@ -1025,10 +1025,9 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
     // launch calls leave the sequential draw's path (one thread had
     // interleaved them: the last launch at ~129 us after ~101 us of draws).
     // SFM_RANSAC_LAUNCHER=0, or a busy pool, keeps the one-thread order.
-    static const bool two = [] {
-        const char *e = std::getenv("SFM_RANSAC_LAUNCHER");
-        return !(e && std::atoi(e) == 0) && std::thread::hardware_concurrency() > 1;
-    }();
+    static const bool multi_core = std::thread::hardware_concurrency() > 1;
+    const char *le = std::getenv("SFM_RANSAC_LAUNCHER");  // read per call (the tests flip it)
+    const bool two = multi_core && !(le && std::atoi(le) == 0);
     std::atomic<int64_t> drawn{0};
     int lrc = 0;
     const bool ran = two && HostPool::get().try_run(2, [&](int t) {

@@ -1339,6 +1339,30 @@ def test_ransac_float_prefilter_never_changes_a_count(core, monkeypatch, scale):
         assert np.array_equal(pyr, pyr_off), thr
 
 
+def test_ransac_launcher_thread_equals_one_thread(core, monkeypatch):
+    """The in-call pipeline's two host threads (the caller draws, a pool
+    worker enqueues each chunk's launches as its rows are published) against
+    the one-thread order (SFM_RANSAC_LAUNCHER=0): the same counts, winner,
+    F and mask, and the global random stream left in the same state; F and
+    H models."""
+    x1, x2, _, _ = syn.two_view(n=5000, seed=0)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SFM_RANSAC_LAUNCHER", mode)
+        random.seed(7)
+        f = core.ransac_f8_pyrandom(x1, x2, 16384, 0.06, want_counts=True)
+        st_f = random.getstate()
+        random.seed(7)
+        h = core.ransac_h4_pyrandom(x1, x2, 4096, 30.0, want_counts=True)
+        out[mode] = (f, st_f, h, random.getstate())
+    (f1, s1, h1, t1), (f0, s0, h0, t0) = out["1"], out["0"]
+    for a, b in ((f1, f0), (h1, h0)):
+        assert a[0] == b[0]
+        for x, y in zip(a[1:4], b[1:4]):
+            assert np.array_equal(np.asarray(x), np.asarray(y))
+    assert s1 == s0 and t1 == t0
+
+
 def test_ransac_score_queue_overflow(core, monkeypatch):
     """k_epi_score's survivor queue past its capacity: a threshold far above
     every distance (but below the prefilter's own cutoff) leaves every pair
