@@ -18,4 +18,4 @@ for H in (1024, 3072, 4096, 8192, 16384):
         core.ransac_f8(x1, x2, table[:H], 0.06)
         v.append(core.last_timings()[3])
     out.append(f"H={H}:{st.median(v[5:]) * 1e3:.1f}us")
-print(os.environ.get("TAG", ""), " ".join(out), flush=True)
+print(sys.argv[1] if len(sys.argv) > 1 else "", os.environ.get("TAG", ""), " ".join(out), flush=True)
