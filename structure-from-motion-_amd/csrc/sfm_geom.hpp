@@ -373,8 +373,12 @@ __device__ __forceinline__ bool smallest_right_sv(const double (&f)[9], double (
     return true;
 }
 
+// lane < 0: one thread writes all of F.  lane in [0, 8): the 8 lanes of a
+// group run it together on the same inputs (the same bits) and lane i
+// divides and writes entry i, lane 0 entry 8 as well: two divisions in
+// flight per lane instead of nine on one.
 __device__ __forceinline__ void f8_finish(const double (&f)[9], const Hartley &h1, const Hartley &h2,
-                                          double *F_out) {
+                                          double *F_out, int lane = -1) {
 #pragma clang fp contract(off)
     // rank 2 (EstimateFundamentalMatrix.py:70-72): U diag(s1, s2, 0) V^T =
     // F - (F v3) v3^T with v3 the smallest right singular vector
@@ -429,6 +433,14 @@ __device__ __forceinline__ void f8_finish(const double (&f)[9], const Hartley &h
             G[r][c] = acc;
         }
     const double d = G[2][2];
+    if (lane >= 0) {
+        double num = G[0][0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) num = lane == k ? G[k / 3][k % 3] : num;
+        F_out[lane] = num / d;
+        if (lane == 0) F_out[8] = G[2][2] / d;
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
@@ -509,7 +521,8 @@ __device__ __forceinline__ void f8_points(const double (&x1)[8], const double (&
 // are broadcast to the group for the rows below and again for the
 // back-substitution, which every lane runs on its own copy of n.  ~60 VGPRs
 // against the one-thread fit's 136, so it can share a launch with the score.
-// Lane 0 of the group writes F_out.
+// Every lane of the group runs the rank-2 step (the same bits: the lanes'
+// n, h1 and h2 are equal) and writes one entry of F_out (lane 0 two).
 __device__ __forceinline__ double hartley_sum8(double v) {
 #pragma clang fp contract(off)
     double s = 0;
@@ -586,7 +599,7 @@ __device__ __forceinline__ void f8_points_group8(double px, double py, double qx
 #pragma unroll
         for (int j = k; j < 9; ++j) n[j] -= d * v[j];
     }
-    if (i == 0) f8_finish(n, h1, h2, F_out);
+    f8_finish(n, h1, h2, F_out, i);
 }
 
 // ------------------------------------------------------------ homography
