@@ -4,6 +4,8 @@ stamps, sfm_last_timings [6..10]) beside the Python wall times: medians of
 import os, random, statistics as st, sys, time
 _here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path[:0] = [os.path.join(_here, "structure-from-motion-_amd")]
+if len(sys.argv) > 1 and sys.argv[1] != "-":
+    sys.path.insert(0, os.path.abspath(sys.argv[1]))
 import numpy as np  # noqa: E402
 import _sfmcore as core  # noqa: E402
 import sfm_synthetic as syn  # noqa: E402
