@@ -60,7 +60,21 @@ def GetInliersRANSAC(points1, points2, index, threshold=0.06, n_max=1000):
     n_points = len(points1)
     if n_points < 8:  # :38-40
         return np.array([]), index, None
+    # :48-50 builds the homogeneous copies with np.hstack before the loop: it
+    # raises for anything but a 2-D array of n_points rows, before any draw
+    # (checked here, and np.hstack itself raises the reference's ValueError)
+    for pts in (points1, points2):
+        if pts.ndim != 2 or pts.shape[0] != n_points:
+            np.hstack([pts, np.ones((n_points, 1))])
     n_iter = max(int(n_max), 0)
+    if points1.shape[1] != 2 or points2.shape[1] != 2:
+        # every iteration then raises inside the loop's try -- in
+        # EstimateFundamentalMatrix (not N x 2, EstimateFundamentalMatrix.py:80-81)
+        # or in the scoring's shapes (:67-69) -- and is skipped (:90-92), but
+        # its random.sample has been drawn: n_max draws, then the sentinel (:95-96)
+        if n_iter:
+            _core.sample_table(n_points, 8, n_iter)
+        return np.array([]), index, None
     # n_iter draws of random.sample(range(N), 8) from the global stream,
     # replayed inside the call while the GPU scores the drawn chunks
     best, F_best, split, n_in = _core.ransac_f8_dropin(points1.reshape(n_points, 2), points2.reshape(n_points, 2),

@@ -2312,21 +2312,22 @@ static int launch_gj(const GjPlan &g, int nT, int32_t ns, const double *payload,
 // above (or the Cholesky) runs instead; SFM_SOLVE=gjseg / chol force those.
 struct GjrPlan {
     int nT = 0, tpw = 0;
+    bool pwg = false;  // the pivot workgroup (block nT runs every pivot)
     bool ok() const { return tpw > 0; }
 };
-template <int TR, int TLS>
+template <int TR, int TLS, bool PWG>
 static bool gjr_resident(int nT, int ncu) {
     static int nb = -1;  // resident workgroups per CU (queried once per instantiation)
     if (nb < 0) {
         nb = 0;
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&gjr::k_gjr_solve<TR, TLS>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&gjr::k_gjr_solve<TR, TLS, PWG>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, gjr::DYN_LDS) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gjr::k_gjr_solve<TR, TLS>, gjr::THREADS, gjr::DYN_LDS) !=
-                hipSuccess)
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gjr::k_gjr_solve<TR, TLS, PWG>, gjr::THREADS,
+                                                         gjr::DYN_LDS) != hipSuccess)
             nb = 0;
         (void)hipGetLastError();
     }
-    return nb >= 1 && nT <= nb * ncu;
+    return nb >= 1 && nT + (PWG ? 1 : 0) <= nb * ncu;
 }
 static GjrPlan gjr_plan(int nT, int ncu) {
     GjrPlan g;
@@ -2334,32 +2335,41 @@ static GjrPlan gjr_plan(int nT, int ncu) {
         if (std::strcmp(e, "chol") == 0 || std::strcmp(e, "gjseg") == 0) return g;
     // tile slots per U wave: 4 or TREG in registers (up to 28 / 77 tile
     // rows), past that TREG_L + TLDS_L (the latter in LDS: up to gjr::NTMAX = 128)
-    if (nT < 1 || nT > gjr::NTMAX || nT > ncu) return g;
+    const char *pe = std::getenv("SFM_GJR_PWG");  // 0: the owner-only layout (round 4/5)
+    const bool pwg = !pe || std::atoi(pe) != 0;
+    if (nT < 1 || nT > gjr::NTMAX || nT + (pwg ? 1 : 0) > ncu) return g;
     const int tpw = nT <= 4 * gjr::NUW ? 4 : nT <= gjr::TREG * gjr::NUW ? gjr::TREG : gjr::TREG_L + gjr::TLDS_L;
-    const bool res = tpw == 4 ? gjr_resident<4, 0>(nT, ncu)
-                   : tpw == gjr::TREG ? gjr_resident<gjr::TREG, 0>(nT, ncu)
-                                      : gjr_resident<gjr::TREG_L, gjr::TLDS_L>(nT, ncu);
+    const bool res = pwg ? (tpw == 4 ? gjr_resident<4, 0, true>(nT, ncu)
+                            : tpw == gjr::TREG ? gjr_resident<gjr::TREG, 0, true>(nT, ncu)
+                                               : gjr_resident<gjr::TREG_L, gjr::TLDS_L, true>(nT, ncu))
+                         : (tpw == 4 ? gjr_resident<4, 0, false>(nT, ncu)
+                            : tpw == gjr::TREG ? gjr_resident<gjr::TREG, 0, false>(nT, ncu)
+                                               : gjr_resident<gjr::TREG_L, gjr::TLDS_L, false>(nT, ncu));
     if (!res) return g;
     g.nT = nT;
     g.tpw = tpw;
+    g.pwg = pwg;
     return g;
 }
 // granule records (zeroed once; tags only grow) and the err / arrival words
 struct GjrBufs {
-    gjr::u64 *P = nullptr, *G = nullptr;
+    gjr::u64 *P = nullptr, *G = nullptr, *W = nullptr, *Lr = nullptr;
     double *Gd = nullptr;
     unsigned *Gf = nullptr;
     int *err = nullptr;
     unsigned *arrive = nullptr;
     static size_t words(int nT) {
         const size_t t = (size_t)nT * nT;
-        return ((size_t)2 * nT * gjr::PBYTES + t * gjr::GBYTES + t * gjr::GDBYTES) / 8 + (t + 1) / 2;
+        return ((size_t)2 * nT * gjr::PBYTES + (size_t)nT * (gjr::WBYTES + gjr::LBYTES) + t * gjr::GBYTES +
+                t * gjr::GDBYTES) / 8 + (t + 1) / 2;
     }
     static constexpr size_t ints = 64;
     void carve(gjr::u64 *w, int *i, int nT) {
         const size_t t = (size_t)nT * nT;
         P = w;
-        G = P + (size_t)2 * nT * gjr::PBYTES / 8;
+        W = P + (size_t)2 * nT * gjr::PBYTES / 8;
+        Lr = W + (size_t)nT * gjr::WBYTES / 8;
+        G = Lr + (size_t)nT * gjr::LBYTES / 8;
         Gd = reinterpret_cast<double *>(G + t * gjr::GBYTES / 8);
         Gf = reinterpret_cast<unsigned *>(Gd + t * gjr::GDBYTES / 8);
         err = i;
@@ -2380,6 +2390,8 @@ static int launch_gjr(const GjrPlan &g, int32_t ns, const double *payload, const
     a.G = b.G;
     a.Gd = b.Gd;
     a.Gf = b.Gf;
+    a.W = b.W;
+    a.Lr = b.Lr;
     a.tag = tag;
     a.x = x;
     a.bad = bad;
@@ -2387,15 +2399,29 @@ static int launch_gjr(const GjrPlan &g, int32_t ns, const double *payload, const
     a.arrive = b.arrive;
     a.ct = ct;
     a.dbg = gj_dbg_ptr();
-    switch (g.tpw) {
-    case 4: hipLaunchKernelGGL((gjr::k_gjr_solve<4, 0>), dim3(g.nT), dim3(gjr::THREADS), gjr::DYN_LDS, s, a); break;
-    case gjr::TREG:
-        hipLaunchKernelGGL((gjr::k_gjr_solve<gjr::TREG, 0>), dim3(g.nT), dim3(gjr::THREADS), gjr::DYN_LDS, s, a);
-        break;
-    default:
-        hipLaunchKernelGGL((gjr::k_gjr_solve<gjr::TREG_L, gjr::TLDS_L>), dim3(g.nT), dim3(gjr::THREADS), gjr::DYN_LDS,
-                           s, a);
-        break;
+    const dim3 grid(g.nT + (g.pwg ? 1 : 0));
+    if (g.pwg) {
+        switch (g.tpw) {
+        case 4: hipLaunchKernelGGL((gjr::k_gjr_solve<4, 0, true>), grid, dim3(gjr::THREADS), gjr::DYN_LDS, s, a); break;
+        case gjr::TREG:
+            hipLaunchKernelGGL((gjr::k_gjr_solve<gjr::TREG, 0, true>), grid, dim3(gjr::THREADS), gjr::DYN_LDS, s, a);
+            break;
+        default:
+            hipLaunchKernelGGL((gjr::k_gjr_solve<gjr::TREG_L, gjr::TLDS_L, true>), grid, dim3(gjr::THREADS),
+                               gjr::DYN_LDS, s, a);
+            break;
+        }
+    } else {
+        switch (g.tpw) {
+        case 4: hipLaunchKernelGGL((gjr::k_gjr_solve<4, 0, false>), grid, dim3(gjr::THREADS), gjr::DYN_LDS, s, a); break;
+        case gjr::TREG:
+            hipLaunchKernelGGL((gjr::k_gjr_solve<gjr::TREG, 0, false>), grid, dim3(gjr::THREADS), gjr::DYN_LDS, s, a);
+            break;
+        default:
+            hipLaunchKernelGGL((gjr::k_gjr_solve<gjr::TREG_L, gjr::TLDS_L, false>), grid, dim3(gjr::THREADS),
+                               gjr::DYN_LDS, s, a);
+            break;
+        }
     }
     SFM_HIP(hipGetLastError());
     return 0;
@@ -4186,7 +4212,9 @@ static int ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, co
               // stable radix sort of the camera indices for the permutation,
               // and the block counts with the duplicate check in one pass
         hipStream_t s = p->stream;
-        DevPlan tmp;
+        DevPlan tmp;  // scratch on this problem's device and stream (the pool is per device)
+        tmp.s = s;
+        tmp.dev = device;
         uint32_t *keys = tmp.scratch<uint32_t>(no), *cnt32 = tmp.scratch<uint32_t>((size_t)nc * nc + 1);
         size_t tb = 0;
         if ((rc = sfm::cam_major_sort(nullptr, tb, p->d_cam, keys, p->d_cm_pt, no, nc, s))) return rc;
@@ -4230,9 +4258,10 @@ static int ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, co
         }
         ctick("csr+blockcounts (device)");
     }
-    // the staged copies are done once the stream has passed them (the host
-    // planner reads a dense scan's observations from the buffer: kept then)
-    if (stage_lk.owns_lock() && !(dense && host_plan)) {
+    // the staged copies are done once the stream has passed them (a dense
+    // scan's observations live in the buffer, and plan_sweep may read them on
+    // the host whichever planner runs: kept until it returns)
+    if (stage_lk.owns_lock() && !dense) {
         SFM_HIP(hipStreamSynchronize(p->stream));
         stage_lk.unlock();
     }
@@ -4263,6 +4292,10 @@ static int ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, co
     }
     plan_sweep(nc, np_, no, cam, pt, pstart, cnt, p->sw_lpp, plan_only ? 256 : device_cus(device), split_ok, sw,
                dev_plan ? &dev : nullptr);
+    if (stage_lk.owns_lock()) {
+        SFM_HIP(hipStreamSynchronize(p->stream));
+        stage_lk.unlock();
+    }
     if (dev.err) {
         set_error("sweep plan on the device: %s", dev.err == SFM_ERR_NOMEM ? "hipMalloc failed" : "HIP error");
         return dev.err;
@@ -4488,7 +4521,7 @@ extern "C" int sfm_ba_plan_digest(sfm_ba_problem *p, uint64_t *out) {
 extern "C" int sfm_ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt,
                              const double *obs, const double *K, const double *cams, const double *pts, int device,
                              sfm_comm *comm, sfm_ba_problem **out) {
-    return ba_create(nc, np_, no, cam, pt, obs, nullptr, K, cams, pts, device, comm, out);
+    return abi_guard("sfm_ba_create", [&] { return ba_create(nc, np_, no, cam, pt, obs, nullptr, K, cams, pts, device, comm, out); });
 }
 
 extern "C" int sfm_ba_reset(sfm_ba_problem *p) {
@@ -5148,7 +5181,7 @@ static int ba_lm(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const 
 extern "C" int sfm_ba_lm(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt,
                          const double *obs, const double *K, double *cams, double *pts, const sfm_ba_opts *o,
                          sfm_ba_report *rep, int device) {
-    return ba_lm(nc, np_, no, cam, pt, obs, nullptr, K, cams, pts, o, rep, device);
+    return abi_guard("sfm_ba_lm", [&] { return ba_lm(nc, np_, no, cam, pt, obs, nullptr, K, cams, pts, o, rep, device); });
 }
 
 // perform_bundle_adjustment from the dense scan (sfm_dense_obs_scan's
@@ -5160,7 +5193,8 @@ extern "C" int sfm_ba_lm_dense(void *obs_handle, int32_t nc, int64_t np_, const 
     int32_t ncams;
     SFM_CHECK_ARG(dense_obs_info(obs_handle, &no, &nrows, &ncams), "null observation handle");
     SFM_CHECK_ARG(nrows == np_ && ncams <= nc, "the scan's rows / cameras do not match the problem");
-    return ba_lm(nc, np_, no, nullptr, nullptr, nullptr, obs_handle, K, cams, pts, o, rep, device);
+    return abi_guard("sfm_ba_lm_dense",
+                     [&] { return ba_lm(nc, np_, no, nullptr, nullptr, nullptr, obs_handle, K, cams, pts, o, rep, device); });
 }
 
 // Single-process multi-GPU bundle adjustment: points (with their

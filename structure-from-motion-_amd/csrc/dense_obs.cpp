@@ -227,12 +227,19 @@ extern "C" int sfm_dense_obs_scan(const void *flags, int32_t dtype, int64_t flag
     const char *f = static_cast<const char *>(flags);
     const char *x = reinterpret_cast<const char *>(fx), *y = reinterpret_cast<const char *>(fy);
     const bool avx = have_avx512();
-    sfm::par_for(nj, [&](int64_t t) {
-        const int64_t r0 = n_rows * t / nj, r1 = n_rows * (t + 1) / nj;
-        Piece &p = h->pieces[t];
-        if (avx) scan_dispatch<true>(dtype, f, flag_row_bytes, rows, r0, r1, n_cams, x, y, xy_row_bytes, p);
-        else scan_dispatch<false>(dtype, f, flag_row_bytes, rows, r0, r1, n_cams, x, y, xy_row_bytes, p);
+    const int rc = sfm::abi_guard("sfm_dense_obs_scan", [&] {
+        sfm::par_for(nj, [&](int64_t t) {
+            const int64_t r0 = n_rows * t / nj, r1 = n_rows * (t + 1) / nj;
+            Piece &p = h->pieces[t];
+            if (avx) scan_dispatch<true>(dtype, f, flag_row_bytes, rows, r0, r1, n_cams, x, y, xy_row_bytes, p);
+            else scan_dispatch<false>(dtype, f, flag_row_bytes, rows, r0, r1, n_cams, x, y, xy_row_bytes, p);
+        });
+        return 0;
     });
+    if (rc) {
+        delete h;
+        return rc;
+    }
     h->n = 0;
     for (auto &p : h->pieces) h->n += p.n;
     *handle = h;

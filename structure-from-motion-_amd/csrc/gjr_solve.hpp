@@ -54,6 +54,15 @@ constexpr int GPAIRS = 4;        // granule pairs a lane of a published G tile
 constexpr int PBYTES = PPAIRS * 64 * 16;
 constexpr int GBYTES = GPAIRS * 64 * 16;
 constexpr int GDBYTES = 2 * 64 * 16;  // a G tile untagged: two 16-byte rows of 64 lanes (the bulk copy)
+// the pivot workgroup (PWG, round 6): owner r ships its window W_r = {A_r,r-LA
+// .. A_rr, b_r} after step r - LA - 1; the pivot workgroup's L_r fragment
+// record goes back to owner r for its import
+constexpr int LA = 3;       // look-ahead: owner r ships its window after step r - LA - 1
+constexpr int WT = LA + 1;  // window tiles A_r,r-LA .. A_rr
+constexpr int WPAIRS = 4 * WT + 1;  // granule pairs a lane of a window: the tiles (4 each), b (1)
+constexpr int WBYTES = WPAIRS * 64 * 16;
+constexpr int LPAIRS = 4;  // the L_r fragment
+constexpr int LBYTES = LPAIRS * 64 * 16;
 constexpr int NB = 6;                 // bulk G tiles a U wave has in flight
 constexpr long long POLL_LIMIT = 20000000;  // s_memrealtime ticks (100 MHz): 200 ms
 constexpr int TREG = 11;                    // tile slots a U wave holds in registers (more would spill)
@@ -75,6 +84,8 @@ struct Args {
     u64 *G;         // [nT][nT] G_r of step p at (p, r), GBYTES each (granules: W0 of owner r + 1)
     double *Gd;     // [nT][nT] the same untagged, GDBYTES each (the U waves' bulk updates) ...
     unsigned *Gf;   // [nT][nT] ... published by a flag (= tag) behind the drained stores
+    u64 *W;         // [nT] windows of WBYTES (PWG)
+    u64 *Lr;        // [nT] L_r fragments of LBYTES (PWG)
     unsigned tag;   // this launch's granule tag (>= 1)
     double *x;      // [nT * 16] solution
     int *bad;       // not positive definite (the LM rejects the step)
@@ -98,10 +109,15 @@ __device__ __forceinline__ int xcd_of_row(int r, int nT) {
     const int q = nT / NXCD_, m = nT % NXCD_;
     return r < m * (q + 1) ? r / (q + 1) : m + (r - m * (q + 1)) / max(q, 1);
 }
-__device__ __forceinline__ void stamp(const Args &a, int p, int slot) {
+__device__ __forceinline__ void stamp_row(const Args &a, int row, int p, int slot) {
     if (a.dbg && (threadIdx.x & 63) == 0)
-        a.dbg[((int64_t)row_of(blockIdx.x, a.nT) * (a.nT + 1) + p) * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+        a.dbg[((int64_t)row * (a.nT + 1) + p) * 16 + slot] = __builtin_amdgcn_s_memrealtime();
 }
+// the pivot workgroup (block nT) stamps as row nT
+__device__ __forceinline__ void stamp(const Args &a, int p, int slot) {
+    stamp_row(a, (int)blockIdx.x < a.nT ? row_of(blockIdx.x, a.nT) : a.nT, p, slot);
+}
+enum { PW_WIN = 0, PW_GPUB, PW_CH0, PW_CH1, PW_PPUB, PW_AWIN, PW_AOUT, PW_BPUB };
 
 struct Smem {
     double PL[RING][4][64];  // L_p^-1 fragments for the holder of A_rp
@@ -198,7 +214,7 @@ struct Buf {
     int bytes;
 };
 struct Rs {
-    Buf P, G, Gd;
+    Buf P, G, Gd, W, Lr;
 };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const Buf &b) {
     const u64 a = (u64)b.base;
@@ -392,10 +408,10 @@ __device__ __forceinline__ double gy(const d4 &g, double yl, int lane) {
 // U waves' prologue from the payload: pay_index in 32-bit arithmetic with the
 // lane's row terms hoisted, zero unless live, every load unconditional (in
 // bounds) so that a group of tiles has its loads in flight together
-__device__ __forceinline__ d4 load_lower(const Args &a, int r, int j, int lane) {
+__device__ __forceinline__ d4 load_lower(const Args &a, int r, int j, int jmax, int lane) {
     const int I = TL * r + (lane & 15), nc = (a.ns + 5) / 6;
     const int ib = I / 6, ir = I - 6 * ib;
-    const bool live = j <= r - 2 && I < a.ns;
+    const bool live = j <= jmax && I < a.ns;  // jmax <= r - 2
     int idx[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -444,9 +460,13 @@ __device__ __forceinline__ d4 load_tile(const Args &a, double lambda, int r, int
 __device__ __forceinline__ int g_uses(int p, int r) {
     return p / RING - (r < p && (r & (RING - 1)) == (p & (RING - 1)) ? 1 : 0);
 }
+// (PWG: no holder at r - 2 either, W0 holds that tile)
+template <bool PWG = false>
 __device__ __forceinline__ int p_uses(int p, int r) {
     int u = g_uses(p, r);
-    if (r >= 1 && r - 1 < p && ((r - 1) & (RING - 1)) == (p & (RING - 1))) --u;
+#pragma unroll
+    for (int d = 1; d <= (PWG ? LA : 1); ++d)
+        if (r >= d && r - d < p && ((r - d) & (RING - 1)) == (p & (RING - 1))) --u;
     return u;
 }
 
@@ -454,20 +474,23 @@ __device__ __forceinline__ int p_uses(int p, int r) {
 // The pivot: the chain on the diagonal tile with the b row (lane 0) and the
 // identity (lanes 16..31) as panel rows -> L_r (rows), y_r, L_r^-T rows.
 // Publishes P_r; leaves L_r^-1 in S.Li and the L_r fragment in S.Lf.
-__device__ __forceinline__ void pivot(const Args &a, const Rs &rs, Smem &S, int r, int lane, const d4 &Td, double b) {
+// the chain itself: L_r rows in rw (lanes 0..15), the L_r^-1 fragment (lv)
+// and y_r (yr = y_r(l & 15)) out
+__device__ __forceinline__ void pivot_core(const Args &a, Smem &S, int r, int lane, const d4 &Td, double b,
+                                           double (&rw)[16], d4 &lv, double &yr, int ch0, int ch1) {
     const int li = lane & 15, grp = lane >> 4;
 #pragma unroll
     for (int e = 0; e < 4; ++e) S.Dm[li][grp + 4 * e] = Td[e];  // symmetric: column li = row li
     if (lane < 16) S.bv[lane] = b;
     wave_lds();
-    double rw[16], pw[16], dinv[16];
+    double pw[16], dinv[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) rw[j] = S.Dm[li][j];
 #pragma unroll
     for (int j = 0; j < 16; ++j) pw[j] = grp == 0 ? (lane == 0 ? S.bv[j] : 0.0) : (grp == 1 && j == li ? 1.0 : 0.0);
-    stamp(a, r, DBG_CHAIN0);
+    stamp(a, r, ch0);
     gj::gj_factor16(rw, pw, dinv, lane, a.bad);
-    stamp(a, r, DBG_CHAIN1);
+    stamp(a, r, ch1);
     if (grp == 1)
 #pragma unroll
         for (int j = 0; j < 16; ++j) S.Li[j][li] = pw[j];  // row li of L^-T = column li of L^-1
@@ -475,22 +498,35 @@ __device__ __forceinline__ void pivot(const Args &a, const Rs &rs, Smem &S, int 
 #pragma unroll
         for (int j = 0; j < 16; ++j) S.yv[j] = pw[j];
     wave_lds();
-    d4 lv;
 #pragma unroll
     for (int e = 0; e < 4; ++e) lv[e] = S.Li[li][4 * e + grp];  // L^-1(l & 15, 4e + (l >> 4))
-    const double yr = S.yv[li];
+    yr = S.yv[li];
+}
+// the L_r fragment (the imports' B operand) from the chain's rows
+__device__ __forceinline__ d4 l_frag(Smem &S, int lane, const double (&rw)[16]) {
+    const int li = lane & 15, grp = lane >> 4;
+    if (grp == 0)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) S.Dm[li][j] = j <= li ? rw[j] : 0.0;
+    wave_lds();
+    d4 lf;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lf[e] = S.Dm[li][4 * e + grp];
+    return lf;
+}
+__device__ __forceinline__ void pivot(const Args &a, const Rs &rs, Smem &S, int r, int lane, const d4 &Td, double b) {
+    double rw[16], yr;
+    d4 lv;
+    pivot_core(a, S, r, lane, Td, b, rw, lv, yr, DBG_CHAIN0, DBG_CHAIN1);
     put4<0>(rs.P, (a.nT + r) * PBYTES, a.tag, lv, lane);  // the L2-local copy first (the next owner)
     put_pair<0>(rs.P, (a.nT + r) * PBYTES, 4, a.tag, yr, lane);
     put4(rs.P, r * PBYTES, a.tag, lv, lane);
     put_pair(rs.P, r * PBYTES, 4, a.tag, yr, lane);
     stamp(a, r, DBG_PPUB);
     // the L_r rows (for the import's fragment) after the publication
-    if (grp == 0)
+    const d4 lf = l_frag(S, lane, rw);
 #pragma unroll
-        for (int j = 0; j < 16; ++j) S.Dm[li][j] = j <= li ? rw[j] : 0.0;
-    wave_lds();
-#pragma unroll
-    for (int e = 0; e < 4; ++e) S.Lf[e][lane] = S.Dm[li][4 * e + grp];
+    for (int e = 0; e < 4; ++e) S.Lf[e][lane] = lf[e];
     lds_release();
     lds_set(&S.lready, 1);
 }
@@ -596,6 +632,131 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
     return true;
 }
 
+// W0 of owner r with the pivot workgroup (PWG): the tiles A_r,r-LA .. A_rr
+// (T[0..LA]) and b_r.  Through step r - LA - 1 the holders' G_r update them;
+// then they go out as the window W_r (rows 0..LA: the pivot workgroup reads
+// them from the payload).  At the steps p in [r - LA, r - 1] this wave holds
+// A_rp and forms G_r itself, publishes it (the others' updates, the later
+// owners' windows) and keeps the later tiles current -- the same operations
+// the pivot workgroup repeats on its copy, so the owners never wait for the
+// pivot workgroup's G, only for its pivot records.  At step r: P_r and the
+// L_r fragment record (the U waves' import).
+__device__ __forceinline__ bool w0_loop_pwg(const Args &a, const Rs &rs, Smem &S, int r, int lane, double lambda) {
+    const int nT = a.nT, li = lane & 15, grp = lane >> 4, lo = r - LA;
+    d4 T[WT];
+#pragma unroll
+    for (int i = 0; i < WT; ++i)
+        T[i] = lo + i >= 0 && (i < LA || lo > 0) ? load_tile(a, lambda, r, lo + i, lane) : zero4();
+    double b = assembled_b_src(a.src, a.payload, a.ns, TL * r + li);
+    stamp(a, nT, DBG_PROLOGUE);
+    for (int p = 0; p < nT; ++p) {
+        const int s = p & (RING - 1);
+        u32x4 v[1][PPAIRS];
+        {
+            const int soff[1] = {p * PBYTES};
+            const bool need[1] = {true};
+            if (!sweep<1, PPAIRS>(rs.P, soff, need, a.tag, v, lane, S)) return false;
+        }
+        stamp(a, p, DBG_PIN);
+        const d4 lv = dec4(v[0]);
+        const double yl = dec(v[0][4]);
+        if (p == r) {  // L_r^-1 for x_r, the L_r fragment for the U waves' import
+            const int soff[1] = {r * LBYTES};
+            const bool need[1] = {true};
+            u32x4 lfv[1][LPAIRS];
+            if (!sweep<1, LPAIRS>(rs.Lr, soff, need, a.tag, lfv, lane, S)) return false;
+            const d4 lf = dec4(lfv[0]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                S.Li[li][4 * e + grp] = lv[e];
+                S.Lf[e][lane] = lf[e];
+            }
+            lds_release();
+            lds_set(&S.lready, 1);
+            continue;
+        }
+        const bool own = p >= lo && p < r;  // this wave holds A_rp
+        if (!own) {  // the holder of A_rp forms G_r from L_p^-1
+            if (!lds_wait(&S.pdone[s], p_uses<true>(p, r), S)) return false;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) S.PL[s][e][lane] = lv[e];
+            lds_release();
+            lds_set(&S.pready[s], p + 1);
+        }
+        // G_j of this step for the window tiles j in (p, r) (remote)
+        d4 gr[LA];
+        {
+            int soff[LA];
+            bool need[LA], any = false;
+#pragma unroll
+            for (int i = 0; i < LA; ++i) {
+                const int j = lo + i;
+                need[i] = p < r && j > p && j >= 0;
+                soff[i] = need[i] ? gsoff(a, p, j) : 0;
+                any |= need[i];
+            }
+            u32x4 gv[LA][GPAIRS];
+            if (any && !sweep<LA, GPAIRS>(rs.G, soff, need, a.tag, gv, lane, S)) return false;
+#pragma unroll
+            for (int i = 0; i < LA; ++i) gr[i] = need[i] ? dec4(gv[i]) : zero4();
+        }
+        stamp(a, p, DBG_GREM);
+        d4 g;
+        if (own) {
+            d4 tp = zero4();
+#pragma unroll
+            for (int i = 0; i < LA; ++i)
+                if (lo + i == p) tp = T[i];
+            g = mfma4(zero4(), lv, tp);
+            put4(rs.G, gsoff(a, p, r), a.tag, g, lane);  // the later owners' windows
+            // the ring slot of the step (the U waves count it: no live tile)
+            if (!lds_wait(&S.gdone[s], NW * g_uses(p, r), S)) return false;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) S.GL[s][e][lane] = g[e];
+            lds_release();
+            lds_set(&S.gready[s], p + 1);
+            lds_add(&S.gdone[s], 1);
+            put_bulk(rs.Gd, gdoff(a, p, r), g, lane);  // every other owner's U waves
+            flag_bulk(a, p, r);
+        } else {
+            if (!lds_wait(&S.gready[s], p + 1, S)) return false;
+            stamp(a, p, DBG_GRDY);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) g[e] = S.GL[s][e][lane];
+            lds_release();
+            lds_add(&S.gdone[s], 1);
+        }
+        b -= gy(g, yl, lane);
+        if (p < r) {
+#pragma unroll
+            for (int i = 0; i < LA; ++i)
+                if (lo + i > p && lo + i >= 0) T[i] = mfma4(T[i], -gr[i], g);
+            if (p < lo) T[LA] = mfma4(T[LA], -g, g);  // A_rr: only until the window is out
+            if (p == lo - 1) {  // the window W_r, through step r - LA - 1
+                const int wo = r * WBYTES;
+#pragma unroll
+                for (int i = 0; i < WT; ++i) put4(rs.W, wo + 4 * i * 1024, a.tag, T[i], lane);
+                put_pair(rs.W, wo, 4 * WT, a.tag, b, lane);
+                stamp(a, p, DBG_GCRIT);
+            }
+        }
+    }
+    // x_r = L_r^-T (L_r^-1 b_r)
+    if (lane < 16) S.bv[lane] = b;
+    wave_lds();
+    double u = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) u = fma(S.Li[li][k], S.bv[k], u);
+    if (lane < 16) S.yv[lane] = u;
+    wave_lds();
+    double x = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x = fma(S.Li[i][li], S.yv[i], x);
+    if (lane < 16) __hip_atomic_store(a.x + TL * r + lane, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    stamp(a, nT, DBG_W0END);
+    return true;
+}
+
 // ------------------------------------------------------------- U waves
 // U_w of owner r holds the tiles j = w + NUW k (k < TPW) other than r - 1
 // and r: the lower ones from the start, the ones right of the diagonal from
@@ -604,11 +765,12 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
 // tiles j in (p, hi), two tiles' remote G loads in flight at a time.
 // Slots: TR in registers, TLS more in LDS (tl: this wave's [TLS][4][64]
 // doubles; large systems only, the register file holds 11 a wave).
-template <int TR, int TLS>
+template <int TR, int TLS, bool PWG>
 __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int r, int w, int lane, double lambda,
                                        double *tl) {
     constexpr int TPW = TR + TLS;
     const int nT = a.nT;
+    const int jmax = PWG ? r - LA - 1 : r - 2;  // the lower tiles this wave holds (W0: the rest up to r)
     d4 T[TR];
     auto tget = [&](int k) -> d4 {  // k is a constant after unrolling: the branch folds
         if (k < TR) return T[k < TR ? k : 0];
@@ -638,10 +800,10 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
         constexpr int PG = 4;
 #pragma unroll 1
         for (int k0 = 0; k0 < TPW; k0 += PG) {
-            if (w + NUW * k0 > r - 2) break;  // nothing live from here on
+            if (w + NUW * k0 > jmax) break;  // nothing live from here on
             d4 v[PG];
 #pragma unroll
-            for (int q = 0; q < PG; ++q) v[q] = load_lower(a, r, w + NUW * (k0 + q), lane);
+            for (int q = 0; q < PG; ++q) v[q] = load_lower(a, r, w + NUW * (k0 + q), jmax, lane);
 #pragma unroll
             for (int q = 0; q < PG; ++q) {
                 const int k = k0 + q;
@@ -655,7 +817,7 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
 #pragma unroll 1
         for (int k = 0; k < TPW; ++k) {
             const int j = w + NUW * k;
-            const d4 v = j <= r - 2 ? load_tile(a, lambda, r, j, lane) : zero4();
+            const d4 v = j <= jmax ? load_tile(a, lambda, r, j, lane) : zero4();
 #pragma unroll
             for (int kk = 0; kk < TR; ++kk)
                 if (kk == k) T[kk] = v;
@@ -677,7 +839,7 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
             bulk_update<TPW, true>(a, rs, p, w, r, nT, lf, lane, tget, tset);
             continue;
         }
-        if (p % NUW == w && p != r - 1) {  // holder of A_rp: G_r = A_rp L_p^-T
+        if (p % NUW == w && (PWG ? p <= jmax || p > r : p != r - 1)) {  // holder of A_rp: G_r = A_rp L_p^-T
             if (!lds_wait(&S.pready[s], p + 1, S)) return false;
             stamp(a, p, DBG_HPRDY);
             d4 lv;
@@ -702,7 +864,7 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
                 flag_bulk(a, p, r);
             }
         }
-        const int hi = r > p ? r - 1 : nT;  // live tiles j in (p, hi); W0 holds r - 1 and r
+        const int hi = r > p ? jmax + 1 : nT;  // live tiles j in (p, hi); W0 holds the rest up to r
         if (!lds_wait(&S.gready[s], p + 1, S)) return false;
         d4 g;
 #pragma unroll
@@ -716,7 +878,149 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
     return true;
 }
 
-template <int TR, int TLS>
+// ------------------------------------------------------ the pivot workgroup
+// (PWG, round 6) Block nT runs EVERY pivot, so no pivot-to-pivot hop crosses
+// a workgroup boundary.  Owner q ships its window (A_q,q-LA .. A_qq, b_q
+// through step q - LA - 1) LA steps ahead; this workgroup applies those LA
+// steps itself:
+//  * wave A (look-ahead), window q: W_q from owner q (rows 0..LA: the
+//    payload, nothing has touched them); steps q - LA .. q - 2 on it, each
+//    G_q,s = L_s^-1 A_q,s with the G_j,s of the earlier rows kept in LDS (Gr);
+//  * wave C (the chain), step q: G_q,q-1 = L_{q-1}^-1 A_q,q-1, A_qq -= G G^T,
+//    b_q -= G y_{q-1}, the chain, P_q out; L_q^-1, y_q and G_q,q-1 to wave A;
+//  * wave B: the L_q fragment record for owner q (its import).
+// Nothing the owners need from here but P_q and that record: each owner forms
+// its own G_r of the last LA steps (w0_loop_pwg), so the owners' progress is
+// one hop behind the pivot records and never waits on this workgroup's G.
+// The operations and their order per tile are the owner-only layout's (the
+// same MFMA calls on the same operands), so the solve is bitwise the same.
+constexpr int GR = LA + 1;  // rows of G_j,j-d (d = 1..LA) kept for wave A
+struct PSm {
+    double Wm[2][4][64], Wd[2][4][64], Wb[2][16];  // windows for wave C (A_q,q-1, A_qq, b_q through step q - 2)
+    double Pl[4][4][64], Py[4][16];                 // L_q^-1 fragment, y_q (read by windows up to q + LA)
+    double Gr[GR][LA][4][64];                       // Gr[j % GR][d - 1] = G_j,j-d
+    double Lfr[2][4][64];                           // the L_q fragment for wave B
+    int win_ready, win_done, pl_ready, gc_ready, lf_ready, b_done;
+};
+static_assert(sizeof(PSm) <= DYN_LDS, "pivot workgroup LDS");
+static_assert(LA >= 2 && LA < 4, "PSm.Pl ring depth");
+
+__device__ __forceinline__ d4 lds4(const double (&t)[4][64], int lane) {
+    return d4{t[0][lane], t[1][lane], t[2][lane], t[3][lane]};
+}
+__device__ __forceinline__ void sto4(double (&t)[4][64], int lane, const d4 &v) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) t[e][lane] = v[e];
+}
+
+__device__ __forceinline__ bool pw_chain(const Args &a, const Rs &rs, Smem &S, PSm &P, int lane) {
+    const int nT = a.nT, li = lane & 15;
+    d4 lvp = zero4();
+    double yp = 0.0;
+    for (int q = 0; q < nT; ++q) {
+        const int s2 = q & 1;
+        if (!lds_wait(&P.win_ready, q + 1, S)) return false;
+        stamp(a, q, PW_WIN);
+        d4 Tm = lds4(P.Wm[s2], lane), Td = lds4(P.Wd[s2], lane);
+        double b = P.Wb[s2][li];
+        lds_release();
+        lds_set(&P.win_done, q + 1);
+        if (q > 0) {
+            const d4 g = mfma4(zero4(), lvp, Tm);
+            sto4(P.Gr[q % GR][0], lane, g);  // the previous content was read by windows up to q - 2
+            lds_release();
+            lds_set(&P.gc_ready, q + 1);
+            stamp(a, q, PW_GPUB);
+            Td = mfma4(Td, -g, g);
+            b -= gy(g, yp, lane);
+        }
+        double rw[16], yr;
+        d4 lv;
+        pivot_core(a, S, q, lane, Td, b, rw, lv, yr, PW_CH0, PW_CH1);
+        put4(rs.P, q * PBYTES, a.tag, lv, lane);
+        put_pair(rs.P, q * PBYTES, 4, a.tag, yr, lane);
+        stamp(a, q, PW_PPUB);
+        sto4(P.Pl[q & 3], lane, lv);  // L_{q-4}^-1 was read by windows up to q - 4 + LA < q
+        if (lane < 16) P.Py[q & 3][lane] = yr;
+        lds_release();
+        lds_set(&P.pl_ready, q + 1);
+        const d4 lf = l_frag(S, lane, rw);
+        if (!lds_wait(&P.b_done, q - 1, S)) return false;  // wave B read the fragment of q - 2
+        sto4(P.Lfr[s2], lane, lf);
+        lds_release();
+        lds_set(&P.lf_ready, q + 1);
+        lvp = lv;
+        yp = yr;
+    }
+    return true;
+}
+
+__device__ __forceinline__ bool pw_ahead(const Args &a, const Rs &rs, Smem &S, PSm &P, int lane, double lambda) {
+    const int nT = a.nT, li = lane & 15;
+    for (int q = 0; q < nT; ++q) {
+        const int s2 = q & 1, lo = q - LA;
+        d4 T[WT];
+        double b;
+        if (lo <= 0) {  // untouched rows: straight from the payload, as their owner would load them
+#pragma unroll
+            for (int i = 0; i < WT; ++i) T[i] = lo + i >= 0 ? load_tile(a, lambda, q, lo + i, lane) : zero4();
+            b = assembled_b_src(a.src, a.payload, a.ns, TL * q + li);
+        } else {
+            const int soff[1] = {q * WBYTES};
+            const bool need[1] = {true};
+            u32x4 v[1][WPAIRS];
+            if (!sweep<1, WPAIRS>(rs.W, soff, need, a.tag, v, lane, S)) return false;
+#pragma unroll
+            for (int i = 0; i < WT; ++i)
+                T[i] = d4{dec(v[0][4 * i]), dec(v[0][4 * i + 1]), dec(v[0][4 * i + 2]), dec(v[0][4 * i + 3])};
+            b = dec(v[0][4 * WT]);
+        }
+        stamp(a, q, PW_AWIN);
+        // steps s = q - d, d = LA .. 2, on the window (tile T[LA - d] is A_q,s)
+#pragma unroll
+        for (int d = LA; d >= 2; --d) {
+            const int s = q - d;
+            if (s < 0) continue;
+            if (!lds_wait(&P.pl_ready, s + 1, S)) return false;
+            const d4 lv = lds4(P.Pl[s & 3], lane);
+            const double ys = P.Py[s & 3][li];
+            const d4 g = mfma4(zero4(), lv, T[LA - d]);
+            sto4(P.Gr[q % GR][d - 1], lane, g);
+#pragma unroll
+            for (int i = LA - d + 1; i < LA; ++i) {  // A_q,j for j = s + 1 .. q - 1: G_j,s of row j
+                const int j = q - LA + i;
+                if (j == s + 1 && !lds_wait(&P.gc_ready, s + 2, S)) return false;  // wave C's G_s+1,s
+                const d4 gj = lds4(P.Gr[j % GR][j - s - 1], lane);
+                T[i] = mfma4(T[i], -gj, g);
+            }
+            T[LA] = mfma4(T[LA], -g, g);
+            b -= gy(g, ys, lane);
+        }
+        if (!lds_wait(&P.win_done, q - 1, S)) return false;  // wave C read window q - 2 (the slot)
+        sto4(P.Wm[s2], lane, T[LA - 1]);
+        sto4(P.Wd[s2], lane, T[LA]);
+        if (lane < 16) P.Wb[s2][lane] = b;
+        lds_release();
+        lds_set(&P.win_ready, q + 1);
+        stamp(a, q, PW_AOUT);
+    }
+    return true;
+}
+
+__device__ __forceinline__ bool pw_pub(const Args &a, const Rs &rs, Smem &S, PSm &P, int lane) {
+    const int nT = a.nT;
+    for (int q = 0; q < nT; ++q) {
+        if (!lds_wait(&P.lf_ready, q + 1, S)) return false;
+        const d4 lf = lds4(P.Lfr[q & 1], lane);
+        lds_release();
+        lds_set(&P.b_done, q + 1);
+        put4(rs.Lr, q * LBYTES, a.tag, lf, lane);
+        stamp(a, q, PW_BPUB);
+    }
+    return true;
+}
+
+template <int TR, int TLS, bool PWG>
 __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
     if (a.gate && !*a.gate) return;  // device-side LM control: iteration gated off
     __shared__ Smem S;
@@ -725,20 +1029,35 @@ __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
     stamp(a, a.nT, DBG_START);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = row_of(blockIdx.x, a.nT);
     const double lambda = *a.lam;
+    const bool pwg = PWG && (int)blockIdx.x == a.nT;  // the pivot workgroup
+    PSm &PS = *reinterpret_cast<PSm *>(dyn);
     if (threadIdx.x < RING) S.pready[threadIdx.x] = S.pdone[threadIdx.x] = S.gready[threadIdx.x] = S.gdone[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
         S.lready = S.abort_ = S.last = 0;
         S.err = a.err;
         S.bad = a.bad;
+        if (pwg) PS.win_ready = PS.win_done = PS.pl_ready = PS.gc_ready = PS.lf_ready = PS.b_done = 0;
     }
     Rs rs;
     rs.P = Buf{a.P, 2 * a.nT * PBYTES};
     rs.G = Buf{a.G, a.nT * a.nT * GBYTES};
     rs.Gd = Buf{a.Gd, a.nT * a.nT * GDBYTES};
+    rs.W = Buf{a.W, a.nT * WBYTES};
+    rs.Lr = Buf{a.Lr, a.nT * LBYTES};
     __syncthreads();
     const int wu = __builtin_amdgcn_readfirstlane(wave);  // provably uniform: scalar record offsets
-    if (wu == 0) w0_loop(a, rs, S, r, lane, lambda);
-    else u_loop<TR, TLS>(a, rs, S, r, wu - 1, lane, lambda, dyn + (wu - 1) * TLS * 256);
+    if (pwg) {  // no arrival: the owners' x is the result
+        if (wu == 0) pw_chain(a, rs, S, PS, lane);
+        else if (wu == 1) pw_ahead(a, rs, S, PS, lane, lambda);
+        else if (wu == 2) pw_pub(a, rs, S, PS, lane);
+        return;
+    }
+    if (wu == 0) {
+        if (PWG) w0_loop_pwg(a, rs, S, r, lane, lambda);
+        else w0_loop(a, rs, S, r, lane, lambda);
+    } else {
+        u_loop<TR, TLS, PWG>(a, rs, S, r, wu - 1, lane, lambda, dyn + (wu - 1) * TLS * 256);
+    }
     // every owner arrives (an aborted one too, so the count stays whole); the
     // last one forms the trial cameras unless the solve failed
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // W0's x stores drained before the barrier

@@ -5,10 +5,15 @@
 #include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
+#include <exception>
+#include <new>
+#include <stdexcept>
 #include <functional>
 #include <mutex>
 #include <thread>
 #include <vector>
+
+#include "sfm_common.hpp"
 
 namespace sfm {
 
@@ -23,7 +28,10 @@ class HostPool {
         static HostPool *p = new HostPool();  // never destroyed: workers may outlive static teardown
         return *p;
     }
-    // f(t) for t in [0, nt), the caller taking t = nt - 1; false if busy
+    // f(t) for t in [0, nt), the caller taking t = nt - 1; false if busy.
+    // An exception from any f(t) (the caller's or a worker's) is held until
+    // every worker has finished with f, then rethrown on the caller: no
+    // worker ever runs a job whose frame has unwound.
     template <class F>
     bool try_run(int nt, F &&f) {
         std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
@@ -39,13 +47,26 @@ class HostPool {
             job_ = [&f](int t) { f(t); };
             njob_ = nw;
             remaining_ = nw;
+            eptr_ = nullptr;
             ++gen_;
         }
         cv_.notify_all();
-        f(nt - 1);
-        std::unique_lock<std::mutex> lk(mu_);
-        done_cv_.wait(lk, [this] { return remaining_ == 0; });
-        job_ = nullptr;
+        std::exception_ptr mine;
+        try {
+            f(nt - 1);
+        } catch (...) {
+            mine = std::current_exception();
+        }
+        std::exception_ptr theirs;
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            done_cv_.wait(lk, [this] { return remaining_ == 0; });
+            job_ = nullptr;
+            theirs = eptr_;
+            eptr_ = nullptr;
+        }
+        if (mine) std::rethrow_exception(mine);
+        if (theirs) std::rethrow_exception(theirs);
         return true;
     }
 
@@ -61,8 +82,14 @@ class HostPool {
                 if (id >= njob_) continue;
                 job = job_;
             }
-            job(id);
+            std::exception_ptr e;
+            try {
+                job(id);
+            } catch (...) {
+                e = std::current_exception();
+            }
             std::lock_guard<std::mutex> lk(mu_);
+            if (e && !eptr_) eptr_ = e;
             if (--remaining_ == 0) done_cv_.notify_all();
         }
     }
@@ -70,6 +97,7 @@ class HostPool {
     std::condition_variable cv_, done_cv_;
     std::vector<std::thread> workers_;
     std::function<void(int)> job_;
+    std::exception_ptr eptr_;  // the first worker exception of the current job
     uint64_t gen_ = 0;
     int njob_ = 0, remaining_ = 0;
 };
@@ -92,9 +120,39 @@ inline void par_for(int64_t n, F &&f) {
         for (int64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) f(i);
     };
     if (HostPool::get().try_run(nt, block)) return;
+    // the pool is busy: threads of our own, with the same exception contract
+    std::vector<std::exception_ptr> ex(nt);
     std::vector<std::thread> th;
-    for (int t = 0; t < nt; ++t) th.emplace_back(block, t);
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            try {
+                block(t);
+            } catch (...) {
+                ex[t] = std::current_exception();
+            }
+        });
     for (auto &x : th) x.join();
+    for (auto &e : ex)
+        if (e) std::rethrow_exception(e);
+}
+
+// The C-ABI never lets a C++ exception out: a host allocation that fails
+// inside an entry point (a vector of a create, a dense scan's pieces) comes
+// back as SFM_ERR_NOMEM with the reason in sfm_last_error.
+template <class F>
+inline int abi_guard(const char *what, F &&f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc &) {
+        set_error("%s: host memory allocation failed", what);
+        return SFM_ERR_NOMEM;
+    } catch (const std::exception &e) {
+        set_error("%s: %s", what, e.what());
+        return SFM_ERR_ARG;
+    } catch (...) {
+        set_error("%s: unknown C++ exception", what);
+        return SFM_ERR_ARG;
+    }
 }
 
 }  // namespace sfm

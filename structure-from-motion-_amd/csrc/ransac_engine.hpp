@@ -26,6 +26,8 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <sched.h>
+#include <thread>
 #include <vector>
 
 #include "sfm_common.hpp"
@@ -904,6 +906,7 @@ struct ScorePipe {
     const float4 *tmax, *pk;  // per-tile coordinate bounds and the packed float copy (k_stage_tiles)
     int64_t pa = 0, pb = 0;  // the fitted, not yet scored piece
     bool fused = M::GROUP_FIT && ransac_fused();
+    int split = score_split_on();  // read once, on the caller's thread (the launcher thread reads no environment)
 
     int score(int64_t a, int64_t b, const FitNext *fn) {
         int ny;
@@ -913,12 +916,11 @@ struct ScorePipe {
         if constexpr (M::SPLIT) {
             if (fn)
                 hipLaunchKernelGGL((k_epi_score<true>), grid, dim3(score_threads<M>()), 0, s, d1, d2, N,
-                                   dF + (a - off) * 9, n, thr, dcnt + (a - off), (int)arg, *fn, score_split_on(), tmax,
-                                   pk);
+                                   dF + (a - off) * 9, n, thr, dcnt + (a - off), (int)arg, *fn, split, tmax, pk);
             else
                 hipLaunchKernelGGL((k_epi_score<false>), grid, dim3(score_threads<M>()), 0, s, d1, d2, N,
-                                   dF + (a - off) * 9, n, thr, dcnt + (a - off), (int)arg, FitNext{}, score_split_on(),
-                                   tmax, pk);
+                                   dF + (a - off) * 9, n, thr, dcnt + (a - off), (int)arg, FitNext{}, split, tmax,
+                                   pk);
         } else {  // the H model (no group fit: its fits run on their own)
             hipLaunchKernelGGL((k_ransac_score<M, false>), grid, dim3(64 * SCORE_WAVES), 0, s, d1, d2, N,
                                dF + (a - off) * 9, n, thr, dcnt + (a - off), arg, FitNext{});
@@ -1025,7 +1027,13 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
     // launch calls leave the sequential draw's path (one thread had
     // interleaved them: the last launch at ~129 us after ~101 us of draws).
     // SFM_RANSAC_LAUNCHER=0, or a busy pool, keeps the one-thread order.
-    static const bool multi_core = std::thread::hardware_concurrency() > 1;
+    // the CPUs this process may run on (taskset / cpuset), not the machine's:
+    // on one CPU the launcher would only compete with the drawer
+    static const bool multi_core = [] {
+        cpu_set_t cs;
+        CPU_ZERO(&cs);
+        return sched_getaffinity(0, sizeof cs, &cs) == 0 ? CPU_COUNT(&cs) > 1 : std::thread::hardware_concurrency() > 1;
+    }();
     const char *le = std::getenv("SFM_RANSAC_LAUNCHER");  // read per call (the tests flip it)
     const bool two = multi_core && !(le && std::atoi(le) == 0);
     std::atomic<int64_t> drawn{0};
@@ -1039,7 +1047,10 @@ int ransac_run_pysample(const double *x1, const double *x2, int64_t N, uint32_t 
             if ((lrc = stage())) return;
             for (int64_t h0 = 0, h1; h0 < H; h0 = h1) {
                 h1 = rp_next(h0, H);
-                while (drawn.load(std::memory_order_acquire) < h1) _mm_pause();
+                // a bounded spin, then yield (an oversubscribed host must not starve the drawer)
+                for (int spin = 0; drawn.load(std::memory_order_acquire) < h1; ++spin)
+                    if (spin < 20000) _mm_pause();
+                    else std::this_thread::yield();
                 if ((lrc = pipe.add(h0, h1, hs + h0 * M::K))) return;
             }
         } else {  // the drawer (the caller): every chunk, in the reference's order
