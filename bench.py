@@ -348,9 +348,10 @@ def end_to_end_ba(workload):
             "phases_ms": phases,
             "phase_frac": {k: round(v / total, 4) for k, v in phases.items() if not k.startswith("ba_lm_")
                            or k == "ba_lm_create"},
-            "note": "phases: observations = dense flags -> COO (np.nonzero over n_pts x n_cams), cams0 = Rotation "
-                    "-> rotvec (stacked), the non-finite-x0 check = the device's initial cost (status 6), ba_lm = the "
-                    "C-ABI call (create: host prep + sweep plan + uploads; loop; download), post = rotvec -> R, C"}
+            "note": "phases: observations = the valid rows and the dense flags -> COO scan (native, host threads), "
+                    "cams0 = R -> rotvec and t for the cameras (stacked), pts0 = the valid rows of all_world_coords "
+                    "(native gather), ba_lm = the C-ABI call (create: host prep + sweep plan + uploads; loop, whose "
+                    "first linearisation is also scipy's non-finite-x0 check; download), post = rotvec -> R, C"}
 
 
 def shard_local(workload, steps, warmup):

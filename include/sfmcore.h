@@ -173,6 +173,10 @@ int sfm_dense_obs_scan(const void *flags, int32_t dtype, int64_t flag_row_bytes,
                        int64_t xy_row_bytes, int32_t n_threads, void **handle, int64_t *n_obs);
 int sfm_dense_obs_read(void *handle, int32_t *cam, int32_t *pt, double *obs);
 int sfm_dense_obs_free(void *handle);
+/* perform_bundle_adjustment's x0 points (BundleAdjustment.py:196-197):
+ * dst[i] = src[rows[i]] for 3-double rows (rows NULL: src[i]), on the host
+ * thread pool; SFM_ERR_ARG for a row outside [0, src_rows). */
+int sfm_gather_rows3(const double *src, int64_t src_rows, const int64_t *rows, int64_t n, double *dst);
 
 /* ---------------------------------------------------------------------
  * LinearTriangulation (LinearTriangulation.py:3-92)

@@ -212,9 +212,11 @@ def _adjust(all_world_coords, valid_point_indices, src, R_set, C_set, K, max_ite
     cams0 = np.empty((n_cameras, 6))
     cams0[:, :3] = Rotation.from_matrix(Rs).as_rotvec()
     cams0[:, 3:] = (-Rs @ Cs[:, :, None])[:, :, 0]
-    pts0 = np.asarray(all_world_coords, dtype=np.float64)[valid_point_indices]
     t1 = time.perf_counter()
-    last_timings["cams0"] = (t1 - t0) * 1e3
+    last_timings["cams0"] = (t1 - t0) * 1e3  # :183-193, the stacked rotvec / t conversion
+    pts0 = _core.gather_points(all_world_coords, valid_point_indices)  # :196-197 (host pool)
+    t2 = time.perf_counter()
+    last_timings["pts0"] = (t2 - t1) * 1e3
     print(f"  Bundle adjustment: {n_cameras} cameras, {n_points} points, {n_obs} observations")
     _core.require_device()  # a missing GPU is an error, never a silent "failed"
     try:

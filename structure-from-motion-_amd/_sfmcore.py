@@ -90,6 +90,7 @@ SIGNATURES = [
                                 ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p), _i64]),
     ("sfm_dense_obs_read", _c, [ctypes.c_void_p, _i32, _i32, _d]),
     ("sfm_dense_obs_free", _c, [ctypes.c_void_p]),
+    ("sfm_gather_rows3", _c, [_d, _i, _i64, _i, _d]),
     ("sfm_triangulate_dlt", _c, [_d, _d, _d, _d, _i, _d, _c]),
     ("sfm_triangulate_nonlinear", _c, [_d, _d, _d, _d, _d, _i, ctypes.c_int32, _d, _i32, _c]),
     ("sfm_project_points", _c, [_d, _d, _i, _d, _c]),
@@ -588,6 +589,22 @@ def dense_observations(flags, feature_x, feature_y, rows, n_cams, n_threads=0):
         return None
     with scan:
         return scan.arrays()
+
+
+def gather_points(all_world_coords, rows):
+    """np.asarray(all_world_coords, dtype=float64)[rows] for the BA drop-in's
+    x0 (BundleAdjustment.py:196-197), gathered by the host pool when the array
+    is a C-ordered float64 n x 3 one and every row is in range; otherwise the
+    numpy expression (its conversions and its IndexError)."""
+    a = np.asarray(all_world_coords)
+    rows = np.asarray(rows)
+    if (a.dtype != np.float64 or a.ndim != 2 or a.shape[1] != 3 or not a.flags.c_contiguous
+            or rows.dtype != np.int64 or rows.ndim != 1 or not rows.flags.c_contiguous):
+        return np.asarray(all_world_coords, dtype=np.float64)[rows]
+    out = np.empty((len(rows), 3))
+    if _lib.sfm_gather_rows3(a.ctypes.data_as(_d), a.shape[0], _p(rows, _i64), len(rows), _p(out)) != 0:
+        return a[rows]  # an index out of range: numpy's IndexError
+    return out
 
 
 def triangulate(P1, P2, x1, x2):

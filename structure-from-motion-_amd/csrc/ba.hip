@@ -3387,7 +3387,7 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     // Round 5, late: one round of workgroups, as many as fit -- the largest
     // range count with nspec x nrange <= the CU count (one sweep workgroup a
     // CU: ~150 KB of LDS).  Measured, cfg5 (100 specs) sweep + finish, rank
-    // 0's shard of N (tools/gpu_sweepvar.sh, same box):
+    // 0's shard of N (a round-5 one-off script, same box):
     //   N = 1: 8 ranges 0.330 ms, 4 0.324, 2 0.306, 1 0.557, 16 0.387
     //   N = 2: 8 0.208, 4 0.182, 2 0.168, 1 0.288
     //   N = 4: 8 0.139, 4 0.114, 2 0.102, 1 0.155

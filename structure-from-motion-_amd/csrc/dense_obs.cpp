@@ -266,3 +266,33 @@ extern "C" int sfm_dense_obs_free(void *handle) {
     delete h;
     return 0;
 }
+
+// perform_bundle_adjustment's x0 points (BundleAdjustment.py:196-197: the
+// valid rows of all_world_coords, 3 doubles each) gathered on the host pool:
+// dst[i] = src[rows[i]] (rows null: src[i]).  numpy's fancy-indexed copy of
+// 500k rows took ~3 ms of the cfg5 call on one thread.
+extern "C" int sfm_gather_rows3(const double *src, int64_t src_rows, const int64_t *rows, int64_t n, double *dst) {
+    SFM_CHECK_ARG(n == 0 || (src && dst), "null pointer");
+    SFM_CHECK_ARG(n >= 0 && src_rows >= 0, "bad sizes");
+    constexpr int NJ = 16;
+    const int nj = n >= 65536 ? NJ : 1;  // small gathers: one thread
+    int bad[NJ] = {0};
+    const int rc = sfm::abi_guard("sfm_gather_rows3", [&] {
+        sfm::par_for(nj, [&](int64_t t) {
+            for (int64_t i = n * t / nj; i < n * (t + 1) / nj; ++i) {
+                const int64_t r = rows ? rows[i] : i;
+                if (r < 0 || r >= src_rows) {
+                    bad[t] = 1;
+                    continue;
+                }
+                dst[3 * i] = src[3 * r];
+                dst[3 * i + 1] = src[3 * r + 1];
+                dst[3 * i + 2] = src[3 * r + 2];
+            }
+        });
+        return 0;
+    });
+    if (rc) return rc;
+    for (int t = 0; t < NJ; ++t) SFM_CHECK_ARG(!bad[t], "row index out of bounds");
+    return 0;
+}

@@ -128,6 +128,7 @@ struct Smem {
     double bv[TL], yv[TL];
     int pready[RING], pdone[RING], gready[RING], gdone[RING];
     int lready, abort_, last;
+    int hgready[RING], w0done;  // (PWG) the holders' G_r for W0 through PL (the mailbox), W0's progress
     int *err, *bad;
 };
 
@@ -460,7 +461,15 @@ __device__ __forceinline__ d4 load_tile(const Args &a, double lambda, int r, int
 __device__ __forceinline__ int g_uses(int p, int r) {
     return p / RING - (r < p && (r & (RING - 1)) == (p & (RING - 1)) ? 1 : 0);
 }
-// (PWG: no holder at r - 2 either, W0 holds that tile)
+// PWG: the ring carries the holders' G to the U waves only, at every step
+// but W0's [r - LA, r]
+__device__ __forceinline__ int g_uses_pwg(int p, int r) {
+    int u = p / RING;
+#pragma unroll
+    for (int d = 0; d <= LA; ++d)
+        if (r - d >= 0 && r - d < p && ((r - d) & (RING - 1)) == (p & (RING - 1))) --u;
+    return u;
+}
 template <bool PWG = false>
 __device__ __forceinline__ int p_uses(int p, int r) {
     int u = g_uses(p, r);
@@ -632,6 +641,29 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
     return true;
 }
 
+// W0 (PWG): the loads of what step p needs first -- P_p and, at a holder
+// step, the holder's G_r,p granules -- issued a step ahead (w0_ok checks them)
+__device__ __forceinline__ void w0_issue(const Rs &rs, int p, int goff, bool ng, unsigned tag, u32x4 (&pv)[PPAIRS],
+                                         u32x4 (&hg)[GPAIRS], int lane) {
+    const __amdgpu_buffer_rsrc_t rp = rsrc(rs.P);
+#pragma unroll
+    for (int k = 0; k < PPAIRS; ++k)
+        pv[k] = __builtin_amdgcn_raw_buffer_load_b128(rp, k * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(p * PBYTES), SC1);
+    const __amdgpu_buffer_rsrc_t rg = rsrc(rs.G);
+#pragma unroll
+    for (int k = 0; k < GPAIRS; ++k)
+        hg[k] = ng ? __builtin_amdgcn_raw_buffer_load_b128(rg, k * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(goff), SC1)
+                   : u32x4{0u, tag, 0u, tag};
+}
+__device__ __forceinline__ bool w0_ok(const u32x4 (&pv)[PPAIRS], const u32x4 (&hg)[GPAIRS], unsigned tag) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < PPAIRS; ++k) ok &= pv[k].y == tag && pv[k].w == tag;
+#pragma unroll
+    for (int k = 0; k < GPAIRS; ++k) ok &= hg[k].y == tag && hg[k].w == tag;
+    return __all(ok);
+}
+
 // W0 of owner r with the pivot workgroup (PWG): the tiles A_r,r-LA .. A_rr
 // (T[0..LA]) and b_r.  Through step r - LA - 1 the holders' G_r update them;
 // then they go out as the window W_r (rows 0..LA: the pivot workgroup reads
@@ -640,7 +672,15 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
 // owners' windows) and keeps the later tiles current -- the same operations
 // the pivot workgroup repeats on its copy, so the owners never wait for the
 // pivot workgroup's G, only for its pivot records.  At step r: P_r and the
-// L_r fragment record (the U waves' import).
+// L_r fragment record (the U waves' import).  W0 reads everything from
+// global memory and feeds no ring: the holders poll the pivot records
+// themselves, so a W0 behind the pivots holds up nobody's step.
+// The W0 of consecutive owners form a chain, one link a step (owner r's G_r
+// of step p needs A_r,p current, i.e. G_r-1 of step p - 1 from owner r - 1's
+// W0), so a link is kept short: the step's pivot record (and holder's G) are
+// loaded a step ahead, W0's own G leaves (granules) before anything else of
+// the step, and the bulk copy's flag waits until the remote poll has drained
+// the stores.
 __device__ __forceinline__ bool w0_loop_pwg(const Args &a, const Rs &rs, Smem &S, int r, int lane, double lambda) {
     const int nT = a.nT, li = lane & 15, grp = lane >> 4, lo = r - LA;
     d4 T[WT];
@@ -649,17 +689,24 @@ __device__ __forceinline__ bool w0_loop_pwg(const Args &a, const Rs &rs, Smem &S
         T[i] = lo + i >= 0 && (i < LA || lo > 0) ? load_tile(a, lambda, r, lo + i, lane) : zero4();
     double b = assembled_b_src(a.src, a.payload, a.ns, TL * r + li);
     stamp(a, nT, DBG_PROLOGUE);
+    auto hneed = [&](int) { return false; };  // the holder's G_r comes through the LDS mailbox
+    u32x4 pv[PPAIRS], hg[GPAIRS];
+    w0_issue(rs, 0, hneed(0) ? gsoff(a, 0, r) : 0, hneed(0), a.tag, pv, hg, lane);
     for (int p = 0; p < nT; ++p) {
-        const int s = p & (RING - 1);
-        u32x4 v[1][PPAIRS];
+        const bool own = p >= lo && p < r;  // this wave holds A_rp
         {
-            const int soff[1] = {p * PBYTES};
-            const bool need[1] = {true};
-            if (!sweep<1, PPAIRS>(rs.P, soff, need, a.tag, v, lane, S)) return false;
+            long long t0 = -1;
+            for (unsigned it = 1; !w0_ok(pv, hg, a.tag); ++it) {
+                __builtin_amdgcn_s_sleep(1);
+                if (it % 64 == 0 && give_up(S, it, t0)) return false;
+                w0_issue(rs, p, hneed(p) ? gsoff(a, p, r) : 0, hneed(p), a.tag, pv, hg, lane);
+            }
         }
         stamp(a, p, DBG_PIN);
-        const d4 lv = dec4(v[0]);
-        const double yl = dec(v[0][4]);
+        const d4 lv = dec4(pv);
+        const double yl = dec(pv[4]);
+        const d4 gh = dec4(hg);
+        if (p + 1 < nT) w0_issue(rs, p + 1, hneed(p + 1) ? gsoff(a, p + 1, r) : 0, hneed(p + 1), a.tag, pv, hg, lane);
         if (p == r) {  // L_r^-1 for x_r, the L_r fragment for the U waves' import
             const int soff[1] = {r * LBYTES};
             const bool need[1] = {true};
@@ -673,64 +720,46 @@ __device__ __forceinline__ bool w0_loop_pwg(const Args &a, const Rs &rs, Smem &S
             }
             lds_release();
             lds_set(&S.lready, 1);
+            lds_set(&S.w0done, p + 1);
             continue;
         }
-        const bool own = p >= lo && p < r;  // this wave holds A_rp
-        if (!own) {  // the holder of A_rp forms G_r from L_p^-1
-            if (!lds_wait(&S.pdone[s], p_uses<true>(p, r), S)) return false;
+        d4 g = gh;
+        if (!own) {  // the holder's G_r of this step (LDS mailbox PL[p % RING])
+            if (!lds_wait(&S.hgready[p & (RING - 1)], p + 1, S)) return false;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) S.PL[s][e][lane] = lv[e];
+            for (int e = 0; e < 4; ++e) g[e] = S.PL[p & (RING - 1)][e][lane];
             lds_release();
-            lds_set(&S.pready[s], p + 1);
         }
-        // G_j of this step for the window tiles j in (p, r) (remote)
-        d4 gr[LA];
-        {
-            int soff[LA];
-            bool need[LA], any = false;
-#pragma unroll
-            for (int i = 0; i < LA; ++i) {
-                const int j = lo + i;
-                need[i] = p < r && j > p && j >= 0;
-                soff[i] = need[i] ? gsoff(a, p, j) : 0;
-                any |= need[i];
-            }
-            u32x4 gv[LA][GPAIRS];
-            if (any && !sweep<LA, GPAIRS>(rs.G, soff, need, a.tag, gv, lane, S)) return false;
-#pragma unroll
-            for (int i = 0; i < LA; ++i) gr[i] = need[i] ? dec4(gv[i]) : zero4();
-        }
-        stamp(a, p, DBG_GREM);
-        d4 g;
         if (own) {
             d4 tp = zero4();
 #pragma unroll
             for (int i = 0; i < LA; ++i)
                 if (lo + i == p) tp = T[i];
             g = mfma4(zero4(), lv, tp);
-            put4(rs.G, gsoff(a, p, r), a.tag, g, lane);  // the later owners' windows
-            // the ring slot of the step (the U waves count it: no live tile)
-            if (!lds_wait(&S.gdone[s], NW * g_uses(p, r), S)) return false;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) S.GL[s][e][lane] = g[e];
-            lds_release();
-            lds_set(&S.gready[s], p + 1);
-            lds_add(&S.gdone[s], 1);
-            put_bulk(rs.Gd, gdoff(a, p, r), g, lane);  // every other owner's U waves
-            flag_bulk(a, p, r);
-        } else {
-            if (!lds_wait(&S.gready[s], p + 1, S)) return false;
-            stamp(a, p, DBG_GRDY);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) g[e] = S.GL[s][e][lane];
-            lds_release();
-            lds_add(&S.gdone[s], 1);
+            // granules first: the later owners' W0 and every owner's wave that
+            // forms its G of step p + 1 (the look-ahead) poll them; then the
+            // bulk copy for the other owners' U waves (its flag below)
+            put4(rs.G, gsoff(a, p, r), a.tag, g, lane);
+            put_bulk(rs.Gd, gdoff(a, p, r), g, lane);
         }
+        lds_set(&S.w0done, p + 1);  // the mailbox slot is free again
         b -= gy(g, yl, lane);
         if (p < r) {
+            int soff[LA];
+            bool need[LA], any = false;
+#pragma unroll
+            for (int i = 0; i < LA; ++i) {
+                need[i] = lo + i > p && lo + i >= 0;
+                soff[i] = need[i] ? gsoff(a, p, lo + i) : 0;
+                any |= need[i];
+            }
+            u32x4 rv[LA][GPAIRS];
+            if (any && !sweep<LA, GPAIRS>(rs.G, soff, need, a.tag, rv, lane, S)) return false;
+            stamp(a, p, DBG_GREM);
+            if (own) flag_bulk(a, p, r);  // the stores have drained behind the poll
 #pragma unroll
             for (int i = 0; i < LA; ++i)
-                if (lo + i > p && lo + i >= 0) T[i] = mfma4(T[i], -gr[i], g);
+                if (need[i]) T[i] = mfma4(T[i], -dec4(rv[i]), g);
             if (p < lo) T[LA] = mfma4(T[LA], -g, g);  // A_rr: only until the window is out
             if (p == lo - 1) {  // the window W_r, through step r - LA - 1
                 const int wo = r * WBYTES;
@@ -824,6 +853,53 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
             if (k >= TR) tset(k, v);
         }
     }
+    // the holder of A_rq: G_r = A_rq L_q^-T into the ring slot of step q,
+    // then its publication
+    auto form_g = [&](int q) -> bool {
+        const int sq = q & (RING - 1);
+        d4 lv;
+        if (PWG) {  // straight from the pivot record (no hand-off through W0)
+            const int soff[1] = {q * PBYTES};
+            const bool need[1] = {true};
+            u32x4 v[1][4];
+            if (!sweep<1, 4>(rs.P, soff, need, a.tag, v, lane, S)) return false;
+            lv = dec4(v[0]);
+        } else {
+            if (!lds_wait(&S.pready[sq], q + 1, S)) return false;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) lv[e] = S.PL[sq][e][lane];
+            lds_release();
+            lds_add(&S.pdone[sq], 1);
+        }
+        stamp(a, q, DBG_HPRDY);
+        d4 tp = zero4();
+#pragma unroll
+        for (int k = 0; k < TPW; ++k)
+            if (k == q / NUW) tp = tget(k);
+        const d4 g = mfma4(zero4(), lv, tp);
+        if (!lds_wait(&S.gdone[sq], PWG ? NUW * g_uses_pwg(q, r) : NW * g_uses(q, r), S)) return false;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) S.GL[sq][e][lane] = g[e];
+        lds_release();
+        lds_set(&S.gready[sq], q + 1);
+        stamp(a, q, DBG_GHOLD);
+        if (PWG) {  // W0's copy (the mailbox; W0 has read step q - RING's)
+            if (!lds_wait(&S.w0done, q - RING + 1, S)) return false;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) S.PL[sq][e][lane] = g[e];
+            lds_release();
+            lds_set(&S.hgready[sq], q + 1);
+        }
+        // granules: W0 of owners r + 1 .. r + LA (and with PWG this owner's
+        // W0 at every step); bulk: every other owner's U waves
+        if (r > q) put4(rs.G, gsoff(a, q, r), a.tag, g, lane);
+        if (r > q) {
+            put_bulk(rs.Gd, gdoff(a, q, r), g, lane);
+            flag_bulk(a, q, r);
+        }
+        return true;
+    };
+    if (!PWG) {
     for (int p = 0; p < nT; ++p) {
         const int s = p & (RING - 1);
         if (p == r) {  // the import: A_rj^T = G_j L_r^T for j > r (G_j of step r from owner j)
@@ -839,7 +915,7 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
             bulk_update<TPW, true>(a, rs, p, w, r, nT, lf, lane, tget, tset);
             continue;
         }
-        if (p % NUW == w && (PWG ? p <= jmax || p > r : p != r - 1)) {  // holder of A_rp: G_r = A_rp L_p^-T
+        if (p % NUW == w && p != r - 1) {  // holder of A_rp: G_r = A_rp L_p^-T
             if (!lds_wait(&S.pready[s], p + 1, S)) return false;
             stamp(a, p, DBG_HPRDY);
             d4 lv;
@@ -864,7 +940,7 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
                 flag_bulk(a, p, r);
             }
         }
-        const int hi = r > p ? jmax + 1 : nT;  // live tiles j in (p, hi); W0 holds the rest up to r
+        const int hi = r > p ? r - 1 : nT;  // live tiles j in (p, hi); W0 holds r - 1 and r
         if (!lds_wait(&S.gready[s], p + 1, S)) return false;
         d4 g;
 #pragma unroll
@@ -874,6 +950,64 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
         if (!wait_bulk<TPW>(a, p, w, p, hi, lane, S)) return false;
         bulk_update<TPW, false>(a, rs, p, w, p, hi, g, lane, tget, tset);
         if (w == 0) stamp(a, p, DBG_UDONE);
+    }
+        return true;
+    }
+    // (PWG) Every G_r is formed one step early, by the wave that holds
+    // A_rq, right after that tile's update of step q - 1 and before the rest
+    // of that step: the owners' G of a step leave a step ahead, so no
+    // owner's step waits on every other owner's same step (the lockstep that
+    // had set the owners' pace).  One formation site per iteration (fq):
+    // iteration p = -1 forms step 0's, the import step forms step r + 1's.
+    for (int p = -1; p < nT; ++p) {
+        const int s = p & (RING - 1);
+        const bool normal = p >= 0 && p != r && !(p >= r - LA && p < r);  // W0's steps: no live tile, no ring slot
+        const int hi = r > p ? jmax + 1 : nT;  // live tiles j in (p, hi); W0 holds the rest up to r
+        int fq = -1;
+        d4 g = zero4();
+        if (p == -1) {
+            if (w == 0 && 0 <= jmax) fq = 0;
+        } else if (p == r) {  // the import: A_rj^T = G_j L_r^T for j > r (G_j of step r from owner j)
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < TPW; ++k) any |= w + NUW * k > r && w + NUW * k < nT;
+            if (any) {
+                if (!lds_wait(&S.lready, 1, S)) return false;
+                d4 lf;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) lf[e] = S.Lf[e][lane];
+                if (!wait_bulk<TPW>(a, p, w, r, nT, lane, S)) return false;
+                bulk_update<TPW, true>(a, rs, p, w, r, nT, lf, lane, tget, tset);
+            }
+            if ((r + 1) % NUW == w && r + 1 < nT) fq = r + 1;
+        } else if (normal) {
+            if (!lds_wait(&S.gready[s], p + 1, S)) return false;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) g[e] = S.GL[s][e][lane];
+            lds_release();
+            lds_add(&S.gdone[s], 1);
+            if ((p + 1) % NUW == w && p + 1 < hi) {  // this wave forms G_r of step p + 1: its tile first
+                // G_p+1,p from its granules (owner p + 1's W0 writes them
+                // first): one round trip, no flag then payload
+                const int k1 = (p + 1) / NUW;
+                const int soff[1] = {gsoff(a, p, p + 1)};
+                const bool need[1] = {true};
+                u32x4 x[1][GPAIRS];
+                if (!sweep<1, GPAIRS>(rs.G, soff, need, a.tag, x, lane, S)) return false;
+                const d4 gj = -dec4(x[0]);
+#pragma unroll
+                for (int k = 0; k < TPW; ++k)  // constant slot indices: the tiles stay in registers
+                    if (k == k1) tset(k, mfma4(tget(k), gj, g));
+                fq = p + 1;
+            }
+        }
+        if (fq >= 0 && !form_g(fq)) return false;
+        if (normal) {
+            const int lo = fq == p + 1 ? p + 1 : p;
+            if (!wait_bulk<TPW>(a, p, w, lo, hi, lane, S)) return false;
+            bulk_update<TPW, false>(a, rs, p, w, lo, hi, g, lane, tget, tset);
+            if (w == 0) stamp(a, p, DBG_UDONE);
+        }
     }
     return true;
 }
@@ -1031,9 +1165,10 @@ __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
     const double lambda = *a.lam;
     const bool pwg = PWG && (int)blockIdx.x == a.nT;  // the pivot workgroup
     PSm &PS = *reinterpret_cast<PSm *>(dyn);
-    if (threadIdx.x < RING) S.pready[threadIdx.x] = S.pdone[threadIdx.x] = S.gready[threadIdx.x] = S.gdone[threadIdx.x] = 0;
+    if (threadIdx.x < RING)
+        S.pready[threadIdx.x] = S.pdone[threadIdx.x] = S.gready[threadIdx.x] = S.gdone[threadIdx.x] = S.hgready[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
-        S.lready = S.abort_ = S.last = 0;
+        S.lready = S.abort_ = S.last = S.w0done = 0;
         S.err = a.err;
         S.bad = a.bad;
         if (pwg) PS.win_ready = PS.win_done = PS.pl_ready = PS.gc_ready = PS.lf_ready = PS.b_done = 0;

@@ -83,3 +83,20 @@ def test_dense_observations_row_out_of_bounds():
         BA.perform_bundle_adjustment(np.zeros((120, 3)), big, fx, fy, flags, R, C, np.eye(3), 4)
     with pytest.raises(IndexError, match="axis 1"):  # more cameras than flag columns
         BA.perform_bundle_adjustment(np.zeros((100, 3)), fwc, fx, fy, flags, R + R, C + C, np.eye(3), 4)
+
+
+def test_gather_points_equals_numpy_fancy_index():
+    """The BA drop-in's x0 points (BundleAdjustment.py:196-197): the native
+    gather equals np.asarray(a, float64)[rows] for every row pattern, falls
+    back to numpy for other dtypes / layouts, and raises numpy's IndexError."""
+    import _sfmcore as core
+    rng = np.random.default_rng(4)
+    a = rng.standard_normal((200_000, 3))
+    for rows in (np.arange(len(a)), np.sort(rng.choice(len(a), 70_000, replace=False)), np.array([7], np.int64),
+                 np.zeros(0, np.int64)):
+        assert np.array_equal(core.gather_points(a, rows), a[rows])
+    assert np.array_equal(core.gather_points(a.astype(np.float32), np.array([1, 2])),
+                          a.astype(np.float32).astype(np.float64)[[1, 2]])
+    assert np.array_equal(core.gather_points(np.asfortranarray(a), np.array([3, 9])), a[[3, 9]])
+    with pytest.raises(IndexError):
+        core.gather_points(a, np.array([len(a)], np.int64))

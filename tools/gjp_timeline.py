@@ -43,3 +43,13 @@ fin = ["start", "prologue", "w0end", "arrived"]
 ends = [d[w, nT, 2] for w in range(nT)]
 print(f"last P out {pw[nT - 1, PPUB]:.2f} us, last owner x {np.nanmax(ends):.2f} us, "
       f"last arrival {np.nanmax([d[w, nT, 3] for w in range(nT)]):.2f} us")
+# owners: per step p, when P_p left the pivot workgroup, reached owner r's W0,
+# the holder had it (pready) and published G_r,p, the remote G's of W0's
+# window tiles arrived, W0 had the holder's G, U0 finished the step; W = the
+# window shipped (step r - LA - 1)
+PIN, GCRIT, GHOLD, UDONE, GREM, GRDY, HPRDY = 0, 1, 5, 6, 7, 9, 10
+for r in [int(v) for v in (sys.argv[3].split(",") if len(sys.argv) > 3 else [])]:
+    print(f"owner {r}:    p   Pout  P@W0  Hprdy  Ghold   Grem   Grdy  U0done")
+    for p in range(0, min(r, nT)):
+        row = [pw[p, PPUB], d[r, p, PIN], d[r, p, HPRDY], d[r, p, GHOLD], d[r, p, GREM], d[r, p, GRDY], d[r, p, UDONE]]
+        print(f"        {p:4d} " + " ".join(f"{v:6.1f}" for v in row) + (f"  W {d[r, p, GCRIT]:.1f}" if not np.isnan(d[r, p, GCRIT]) else ""))
