@@ -117,7 +117,7 @@ __attribute__((target("avx512f,avx512bw"))) inline uint64_t mask512(const uint8_
 
 // rows[r0, r1) into p: per block of ROW_BLOCK rows, the hits (row, camera)
 // first, then their coordinates
-template <class T, bool AVX>
+template <class T, bool AVX, bool PF = true>
 void scan_rows(const char *flags, int64_t flag_row_bytes, const int64_t *rows, int64_t r0, int64_t r1, int32_t n_cams,
                const char *fx, const char *fy, int64_t xy_row_bytes, Piece &p) {
     p.n = 0;
@@ -135,7 +135,13 @@ void scan_rows(const char *flags, int64_t flag_row_bytes, const int64_t *rows, i
                 if constexpr (AVX) mk = mask512(fr + c0, w);
                 else mk = mask_scalar(fr + c0, w);
                 while (mk) {
-                    hc[nh] = c0 + __builtin_ctzll(mk);
+                    const int c = c0 + __builtin_ctzll(mk);
+                    if (PF) {  // the coordinates' lines, requested while the block's flags are scanned
+                        const int64_t off = rows[i] * xy_row_bytes + (int64_t)c * 8;
+                        _mm_prefetch(fx + off, _MM_HINT_T0);
+                        _mm_prefetch(fy + off, _MM_HINT_T0);
+                    }
+                    hc[nh] = c;
                     hr[nh++] = (int32_t)i;
                     mk &= mk - 1;
                 }

@@ -57,7 +57,7 @@ constexpr int GDBYTES = 2 * 64 * 16;  // a G tile untagged: two 16-byte rows of 
 // the pivot workgroup (PWG, round 6): owner r ships its window W_r = {A_r,r-LA
 // .. A_rr, b_r} after step r - LA - 1; the pivot workgroup's L_r fragment
 // record goes back to owner r for its import
-constexpr int LA = 3;       // look-ahead: owner r ships its window after step r - LA - 1
+constexpr int LA = 4;       // look-ahead: owner r ships its window after step r - LA - 1
 constexpr int WT = LA + 1;  // window tiles A_r,r-LA .. A_rr
 constexpr int WPAIRS = 4 * WT + 1;  // granule pairs a lane of a window: the tiles (4 each), b (1)
 constexpr int WBYTES = WPAIRS * 64 * 16;
@@ -641,26 +641,17 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
     return true;
 }
 
-// W0 (PWG): the loads of what step p needs first -- P_p and, at a holder
-// step, the holder's G_r,p granules -- issued a step ahead (w0_ok checks them)
-__device__ __forceinline__ void w0_issue(const Rs &rs, int p, int goff, bool ng, unsigned tag, u32x4 (&pv)[PPAIRS],
-                                         u32x4 (&hg)[GPAIRS], int lane) {
+// W0 (PWG): the loads of P_p, issued a step ahead (w0_ok checks them)
+__device__ __forceinline__ void w0_issue(const Rs &rs, int p, u32x4 (&pv)[PPAIRS], int lane) {
     const __amdgpu_buffer_rsrc_t rp = rsrc(rs.P);
 #pragma unroll
     for (int k = 0; k < PPAIRS; ++k)
         pv[k] = __builtin_amdgcn_raw_buffer_load_b128(rp, k * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(p * PBYTES), SC1);
-    const __amdgpu_buffer_rsrc_t rg = rsrc(rs.G);
-#pragma unroll
-    for (int k = 0; k < GPAIRS; ++k)
-        hg[k] = ng ? __builtin_amdgcn_raw_buffer_load_b128(rg, k * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(goff), SC1)
-                   : u32x4{0u, tag, 0u, tag};
 }
-__device__ __forceinline__ bool w0_ok(const u32x4 (&pv)[PPAIRS], const u32x4 (&hg)[GPAIRS], unsigned tag) {
+__device__ __forceinline__ bool w0_ok(const u32x4 (&pv)[PPAIRS], unsigned tag) {
     bool ok = true;
 #pragma unroll
     for (int k = 0; k < PPAIRS; ++k) ok &= pv[k].y == tag && pv[k].w == tag;
-#pragma unroll
-    for (int k = 0; k < GPAIRS; ++k) ok &= hg[k].y == tag && hg[k].w == tag;
     return __all(ok);
 }
 
@@ -689,24 +680,22 @@ __device__ __forceinline__ bool w0_loop_pwg(const Args &a, const Rs &rs, Smem &S
         T[i] = lo + i >= 0 && (i < LA || lo > 0) ? load_tile(a, lambda, r, lo + i, lane) : zero4();
     double b = assembled_b_src(a.src, a.payload, a.ns, TL * r + li);
     stamp(a, nT, DBG_PROLOGUE);
-    auto hneed = [&](int) { return false; };  // the holder's G_r comes through the LDS mailbox
-    u32x4 pv[PPAIRS], hg[GPAIRS];
-    w0_issue(rs, 0, hneed(0) ? gsoff(a, 0, r) : 0, hneed(0), a.tag, pv, hg, lane);
+    u32x4 pv[PPAIRS];
+    w0_issue(rs, 0, pv, lane);
     for (int p = 0; p < nT; ++p) {
         const bool own = p >= lo && p < r;  // this wave holds A_rp
         {
             long long t0 = -1;
-            for (unsigned it = 1; !w0_ok(pv, hg, a.tag); ++it) {
+            for (unsigned it = 1; !w0_ok(pv, a.tag); ++it) {
                 __builtin_amdgcn_s_sleep(1);
                 if (it % 64 == 0 && give_up(S, it, t0)) return false;
-                w0_issue(rs, p, hneed(p) ? gsoff(a, p, r) : 0, hneed(p), a.tag, pv, hg, lane);
+                w0_issue(rs, p, pv, lane);
             }
         }
         stamp(a, p, DBG_PIN);
         const d4 lv = dec4(pv);
         const double yl = dec(pv[4]);
-        const d4 gh = dec4(hg);
-        if (p + 1 < nT) w0_issue(rs, p + 1, hneed(p + 1) ? gsoff(a, p + 1, r) : 0, hneed(p + 1), a.tag, pv, hg, lane);
+        if (p + 1 < nT) w0_issue(rs, p + 1, pv, lane);
         if (p == r) {  // L_r^-1 for x_r, the L_r fragment for the U waves' import
             const int soff[1] = {r * LBYTES};
             const bool need[1] = {true};
@@ -723,7 +712,7 @@ __device__ __forceinline__ bool w0_loop_pwg(const Args &a, const Rs &rs, Smem &S
             lds_set(&S.w0done, p + 1);
             continue;
         }
-        d4 g = gh;
+        d4 g;
         if (!own) {  // the holder's G_r of this step (LDS mailbox PL[p % RING])
             if (!lds_wait(&S.hgready[p & (RING - 1)], p + 1, S)) return false;
 #pragma unroll
@@ -1017,9 +1006,13 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
 // a workgroup boundary.  Owner q ships its window (A_q,q-LA .. A_qq, b_q
 // through step q - LA - 1) LA steps ahead; this workgroup applies those LA
 // steps itself:
-//  * wave A (look-ahead), window q: W_q from owner q (rows 0..LA: the
-//    payload, nothing has touched them); steps q - LA .. q - 2 on it, each
-//    G_q,s = L_s^-1 A_q,s with the G_j,s of the earlier rows kept in LDS (Gr);
+//  * waves 2..LA (the look-ahead stages), window q: W_q from owner q (rows
+//    0..LA: the payload, nothing has touched them); stage D applies step
+//    q - D, G_q,s = L_s^-1 A_q,s with the G_j,s of the earlier rows kept in
+//    LDS (Gr), and hands the rest to stage D - 1: each step's part runs as
+//    soon as L_s is out, so the window is current through q - 2 right after
+//    wave C's G_q-1,q-2 (measured, round 6: one wave for all LA steps took
+//    ~2.2 us a window, and wave C waited ~1 us a pivot);
 //  * wave C (the chain), step q: G_q,q-1 = L_{q-1}^-1 A_q,q-1, A_qq -= G G^T,
 //    b_q -= G y_{q-1}, the chain, P_q out; L_q^-1, y_q and G_q,q-1 to wave A;
 //  * wave B: the L_q fragment record for owner q (its import).
@@ -1029,15 +1022,26 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
 // The operations and their order per tile are the owner-only layout's (the
 // same MFMA calls on the same operands), so the solve is bitwise the same.
 constexpr int GR = LA + 1;  // rows of G_j,j-d (d = 1..LA) kept for wave A
+constexpr int PR = 8;  // L_q^-1 / y_q kept for the stages (read up to window q + LA)
+// the window of row q between the stages: stage D (2 < D <= LA) hands the
+// D tiles A_q,q-D+1 .. A_qq (and b_q) to stage D - 1; offsets of those
+// double-buffered links in PSm.Lk
+__host__ __device__ constexpr int lk_off(int D) {  // doubles before the link into stage D - 1
+    int o = 0;
+    for (int d = 3; d < D; ++d) o += 2 * (d * 256 + 16);
+    return o;
+}
 struct PSm {
-    double Wm[2][4][64], Wd[2][4][64], Wb[2][16];  // windows for wave C (A_q,q-1, A_qq, b_q through step q - 2)
-    double Pl[4][4][64], Py[4][16];                 // L_q^-1 fragment, y_q (read by windows up to q + LA)
+    double Wm[2][4][64], Wd[2][4][64], Wb[2][16];  // stage 2 -> C (A_q,q-1, A_qq, b_q through step q - 2)
+    double Lk[lk_off(LA + 1)];                      // stage D -> D - 1, D = 3 .. LA
+    double Pl[PR][4][64], Py[PR][16];               // L_q^-1 fragment, y_q
     double Gr[GR][LA][4][64];                       // Gr[j % GR][d - 1] = G_j,j-d
     double Lfr[2][4][64];                           // the L_q fragment for wave B
     int win_ready, win_done, pl_ready, gc_ready, lf_ready, b_done;
+    int lk_ready[LA + 1], lk_done[LA + 1], grdy[LA + 1];  // link into stage d - 1; G_q,q-d of stage d ready
 };
 static_assert(sizeof(PSm) <= DYN_LDS, "pivot workgroup LDS");
-static_assert(LA >= 2 && LA < 4, "PSm.Pl ring depth");
+static_assert(LA >= 2 && LA <= PR && GR >= LA + 1 && 3 + LA <= NW, "stage waves, ring depths");
 
 __device__ __forceinline__ d4 lds4(const double (&t)[4][64], int lane) {
     return d4{t[0][lane], t[1][lane], t[2][lane], t[3][lane]};
@@ -1074,8 +1078,8 @@ __device__ __forceinline__ bool pw_chain(const Args &a, const Rs &rs, Smem &S, P
         put4(rs.P, q * PBYTES, a.tag, lv, lane);
         put_pair(rs.P, q * PBYTES, 4, a.tag, yr, lane);
         stamp(a, q, PW_PPUB);
-        sto4(P.Pl[q & 3], lane, lv);  // L_{q-4}^-1 was read by windows up to q - 4 + LA < q
-        if (lane < 16) P.Py[q & 3][lane] = yr;
+        sto4(P.Pl[q % PR], lane, lv);  // L_{q-PR}^-1 was read by windows up to q - PR + LA < q
+        if (lane < 16) P.Py[q % PR][lane] = yr;
         lds_release();
         lds_set(&P.pl_ready, q + 1);
         const d4 lf = l_frag(S, lane, rw);
@@ -1089,54 +1093,83 @@ __device__ __forceinline__ bool pw_chain(const Args &a, const Rs &rs, Smem &S, P
     return true;
 }
 
-__device__ __forceinline__ bool pw_ahead(const Args &a, const Rs &rs, Smem &S, PSm &P, int lane, double lambda) {
+// stage D (2 <= D <= LA) of the look-ahead: row q's window through step
+// q - D - 1 in (from owner q's record for D = LA, else from stage D + 1), step
+// q - D applied (G_q,q-D = L_q-D^-1 A_q,q-D with the G of the rows between
+// from LDS), the rest out to stage D - 1 (or wave C).  One wave a stage: a
+// window goes through the stages as the pivot records it needs come out.
+template <int D>
+__device__ __forceinline__ bool pw_stage(const Args &a, const Rs &rs, Smem &S, PSm &P, int lane, double lambda) {
     const int nT = a.nT, li = lane & 15;
     for (int q = 0; q < nT; ++q) {
-        const int s2 = q & 1, lo = q - LA;
-        d4 T[WT];
+        const int s2 = q & 1, s = q - D;
+        d4 T[D + 1];  // A_q,q-D .. A_qq
         double b;
-        if (lo <= 0) {  // untouched rows: straight from the payload, as their owner would load them
+        if (D == LA) {
+            if (q <= LA) {  // untouched rows: straight from the payload, as their owner would load them
 #pragma unroll
-            for (int i = 0; i < WT; ++i) T[i] = lo + i >= 0 ? load_tile(a, lambda, q, lo + i, lane) : zero4();
-            b = assembled_b_src(a.src, a.payload, a.ns, TL * q + li);
-        } else {
-            const int soff[1] = {q * WBYTES};
-            const bool need[1] = {true};
-            u32x4 v[1][WPAIRS];
-            if (!sweep<1, WPAIRS>(rs.W, soff, need, a.tag, v, lane, S)) return false;
+                for (int i = 0; i <= D; ++i) T[i] = s + i >= 0 ? load_tile(a, lambda, q, s + i, lane) : zero4();
+                b = assembled_b_src(a.src, a.payload, a.ns, TL * q + li);
+            } else {
+                const int soff[1] = {q * WBYTES};
+                const bool need[1] = {true};
+                u32x4 v[1][WPAIRS];
+                if (!sweep<1, WPAIRS>(rs.W, soff, need, a.tag, v, lane, S)) return false;
 #pragma unroll
-            for (int i = 0; i < WT; ++i)
-                T[i] = d4{dec(v[0][4 * i]), dec(v[0][4 * i + 1]), dec(v[0][4 * i + 2]), dec(v[0][4 * i + 3])};
-            b = dec(v[0][4 * WT]);
-        }
-        stamp(a, q, PW_AWIN);
-        // steps s = q - d, d = LA .. 2, on the window (tile T[LA - d] is A_q,s)
-#pragma unroll
-        for (int d = LA; d >= 2; --d) {
-            const int s = q - d;
-            if (s < 0) continue;
-            if (!lds_wait(&P.pl_ready, s + 1, S)) return false;
-            const d4 lv = lds4(P.Pl[s & 3], lane);
-            const double ys = P.Py[s & 3][li];
-            const d4 g = mfma4(zero4(), lv, T[LA - d]);
-            sto4(P.Gr[q % GR][d - 1], lane, g);
-#pragma unroll
-            for (int i = LA - d + 1; i < LA; ++i) {  // A_q,j for j = s + 1 .. q - 1: G_j,s of row j
-                const int j = q - LA + i;
-                if (j == s + 1 && !lds_wait(&P.gc_ready, s + 2, S)) return false;  // wave C's G_s+1,s
-                const d4 gj = lds4(P.Gr[j % GR][j - s - 1], lane);
-                T[i] = mfma4(T[i], -gj, g);
+                for (int i = 0; i <= D; ++i)
+                    T[i] = d4{dec(v[0][4 * i]), dec(v[0][4 * i + 1]), dec(v[0][4 * i + 2]), dec(v[0][4 * i + 3])};
+                b = dec(v[0][4 * WT]);
             }
-            T[LA] = mfma4(T[LA], -g, g);
+            stamp(a, q, PW_AWIN);
+        } else {
+            if (!lds_wait(&P.lk_ready[D + 1], q + 1, S)) return false;
+            const double *lk = P.Lk + lk_off(D + 1) + s2 * ((D + 1) * 256 + 16);
+#pragma unroll
+            for (int i = 0; i <= D; ++i) T[i] = d4{lk[i * 256 + lane], lk[i * 256 + 64 + lane], lk[i * 256 + 128 + lane],
+                                                  lk[i * 256 + 192 + lane]};
+            b = lk[(D + 1) * 256 + li];
+            lds_release();
+            lds_set(&P.lk_done[D + 1], q + 1);
+        }
+        if (s >= 0) {
+            if (!lds_wait(&P.pl_ready, s + 1, S)) return false;
+            const d4 lv = lds4(P.Pl[s % PR], lane);
+            const double ys = P.Py[s % PR][li];
+            const d4 g = mfma4(zero4(), lv, T[0]);
+            sto4(P.Gr[q % GR][D - 1], lane, g);
+            lds_release();
+            lds_set(&P.grdy[D], q + 1);
+#pragma unroll
+            for (int i = 1; i < D; ++i) {  // A_q,j, j = s + i: G_j,s of row j (stage i's; wave C's for i = 1)
+                const int j = s + i;
+                if (!lds_wait(i == 1 ? &P.gc_ready : &P.grdy[i], j + 1, S)) return false;
+                T[i] = mfma4(T[i], -lds4(P.Gr[j % GR][i - 1], lane), g);
+            }
+            T[D] = mfma4(T[D], -g, g);
             b -= gy(g, ys, lane);
         }
-        if (!lds_wait(&P.win_done, q - 1, S)) return false;  // wave C read window q - 2 (the slot)
-        sto4(P.Wm[s2], lane, T[LA - 1]);
-        sto4(P.Wd[s2], lane, T[LA]);
-        if (lane < 16) P.Wb[s2][lane] = b;
-        lds_release();
-        lds_set(&P.win_ready, q + 1);
-        stamp(a, q, PW_AOUT);
+        if (D == 2) {
+            if (!lds_wait(&P.win_done, q - 1, S)) return false;  // wave C read window q - 2 (the slot)
+            sto4(P.Wm[s2], lane, T[1]);
+            sto4(P.Wd[s2], lane, T[2]);
+            if (lane < 16) P.Wb[s2][lane] = b;
+            lds_release();
+            lds_set(&P.win_ready, q + 1);
+            stamp(a, q, PW_AOUT);
+        } else {
+            if (!lds_wait(&P.lk_done[D], q - 1, S)) return false;  // stage D - 1 read window q - 2 (the slot)
+            double *lk = P.Lk + lk_off(D) + s2 * (D * 256 + 16);
+#pragma unroll
+            for (int i = 1; i <= D; ++i) {
+                lk[(i - 1) * 256 + lane] = T[i][0];
+                lk[(i - 1) * 256 + 64 + lane] = T[i][1];
+                lk[(i - 1) * 256 + 128 + lane] = T[i][2];
+                lk[(i - 1) * 256 + 192 + lane] = T[i][3];
+            }
+            if (lane < 16) lk[D * 256 + lane] = b;
+            lds_release();
+            lds_set(&P.lk_ready[D], q + 1);
+        }
     }
     return true;
 }
@@ -1173,6 +1206,9 @@ __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
         S.bad = a.bad;
         if (pwg) PS.win_ready = PS.win_done = PS.pl_ready = PS.gc_ready = PS.lf_ready = PS.b_done = 0;
     }
+    if (pwg && threadIdx.x <= LA) {
+        PS.lk_ready[threadIdx.x] = PS.lk_done[threadIdx.x] = PS.grdy[threadIdx.x] = 0;
+    }
     Rs rs;
     rs.P = Buf{a.P, 2 * a.nT * PBYTES};
     rs.G = Buf{a.G, a.nT * a.nT * GBYTES};
@@ -1183,8 +1219,11 @@ __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
     const int wu = __builtin_amdgcn_readfirstlane(wave);  // provably uniform: scalar record offsets
     if (pwg) {  // no arrival: the owners' x is the result
         if (wu == 0) pw_chain(a, rs, S, PS, lane);
-        else if (wu == 1) pw_ahead(a, rs, S, PS, lane, lambda);
-        else if (wu == 2) pw_pub(a, rs, S, PS, lane);
+        else if (wu == 1) pw_pub(a, rs, S, PS, lane);
+        else if (wu == 2) pw_stage<2>(a, rs, S, PS, lane, lambda);
+        else if (wu == 3) pw_stage<3>(a, rs, S, PS, lane, lambda);
+        else if (wu == 4) pw_stage<4>(a, rs, S, PS, lane, lambda);
+        static_assert(LA == 4, "one wave a look-ahead stage: the dispatch above");
         return;
     }
     if (wu == 0) {
