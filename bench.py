@@ -72,6 +72,45 @@ def design_bytes(name, n_obs, n_pts, n_pairs, nblocks, ns):
 
 PMC_ROUND = "round5"
 
+# VALU issue (MI355X_MICROARCH.md): a SIMD issues a wave64 VALU instruction
+# over 2 cycles (32 lanes a cycle); an FP64 op takes the slot twice (78.6 TF
+# FP64 vector = 16 lanes a cycle), a transcendental four times
+VALU_SLOTS_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 issue slots / s, the whole chip
+
+
+def ransac_valu_slots():
+    """Executed VALU issue slots of the F-RANSAC kernels from the committed
+    rocprofv3 PMC passes (SQ_INSTS_VALU and the FP64 / transcendental splits):
+    the one-shot score launch (16,384 x 5,000) and the drop-in call's own fits
+    + scores (tools/ransac_once.py), per launch / per call.
+    ({"oneshot": slots, "dropin": slots}, sources)."""
+    import csv
+    out, src = {}, []
+    base = os.path.join(REPO, "profiles", PMC_ROUND)
+    try:
+        vals = [float(r["Counter_Value"])
+                for r in csv.DictReader(open(os.path.join(base, "ransac_oneshot_pmc", "pmc_counter_collection.csv")))
+                if "k_epi_score" in r["Kernel_Name"] and r["Counter_Name"] == "SQ_INSTS_VALU"]
+        if vals:  # no FP64 split in that pass: one slot each (a lower bound of the slots)
+            out["oneshot"] = float(np.mean(vals))
+            src.append(f"profiles/{PMC_ROUND}/ransac_oneshot_pmc (SQ_INSTS_VALU of k_epi_score, one slot each)")
+    except (OSError, ValueError, KeyError):
+        pass
+    try:
+        d = json.load(open(os.path.join(base, "pmc_traffic_ransac.json")))
+        calls = d["void k_fit_samples<EpiModel>"]["launches"]  # one first-chunk fit per drop-in call
+        tot = 0.0
+        for k in ("void k_epi_score<true>", "void k_epi_score<false>", "void k_fit_samples<EpiModel>"):
+            e = d[k]
+            f64 = sum(e.get(f"SQ_INSTS_VALU_{c}_F64_total", 0.0) for c in ("ADD", "FMA", "MUL"))
+            tot += e["SQ_INSTS_VALU_total"] + f64 + 3 * e.get("SQ_INSTS_VALU_TRANS_F64_total", 0.0)
+        out["dropin"] = tot / calls
+        src.append(f"profiles/{PMC_ROUND}/pmc_traffic_ransac.json (the drop-in's fits + scores per call; FP64 "
+                   f"ops 2 slots, FP64 transcendentals 4)")
+    except (OSError, ValueError, KeyError):
+        pass
+    return out, src
+
 
 def pmc_iteration(workload):
     """HBM bytes per LM iteration by kernel from the committed rocprofv3 PMC
@@ -482,12 +521,26 @@ def ransac_leg(args, world, rank, local_rank, comm):
         "hyps_per_s_kernels": round(H / (k_all * 1e-3), 1),
         "kernel_ms": round(k_all, 4), "score_kernel_ms": round(k_score, 4), "fit_kernel_ms": round(k_fit, 4),
         "best_iter": int(best), "inliers": int(np.count_nonzero(mask)),
-        "fp64": {"bound": "fp64-valu", "score_tflops": round(score_flops / (k_score * 1e-3) / 1e12, 2),
+        "fp64": {"bound": "valu-issue (ransac.roofline)", "score_tflops": round(score_flops / (k_score * 1e-3) / 1e12, 2),
                  "kernels_tflops": round(all_flops / (k_all * 1e-3) / 1e12, 2), "peak_tflops": FP64_PEAK_TFLOPS,
                  "score_frac": round(score_flops / (k_score * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 4),
                  "formula": "score: H*N*50 flop; kernels: H*(N*50 + 25e3) flop (SURVEY §8(d)); algorithmic-equivalent: the score proves most pairs outliers with a packed float prefilter and runs the FP64 test only on the survivors, so it executes far fewer FP64 flops",
-                 "score_bound": "VALU issue, not FP64: score_frac above 1 is the FP64-equivalent rate of mostly FP32 work. Executed: ~13 M VALU instructions per one-shot launch (4 cycles each over 1024 SIMDs, ~0.47 of the issue rate at 45 us); the drop-in's fused launches 4.0 M in 22 us, ~0.29 (profiles/round5/pmc_traffic_ransac.json, DESIGN \u00a74)"}})
+                 "score_bound": "VALU issue, not FP64: score_frac above 1 is an algorithmic-equivalent FP64 rate of mostly FP32 work, not a utilisation; the VALU-issue fraction is ransac.roofline"}})
+    slots, src = ransac_valu_slots()
+    if slots.get("oneshot"):  # the roofline that bounds the score: VALU issue, not FP64
+        ach = slots["oneshot"] / (k_score * 1e-3)
+        out["roofline"] = {"kernel": "k_epi_score (one-shot, 16,384 hypotheses x 5,000 pairs)", "bound": "valu-issue",
+                           "achieved": round(ach / 1e9, 1), "peak": round(VALU_SLOTS_PEAK / 1e9, 1),
+                           "unit": "G VALU issue slots/s (wave64, 2 SIMD cycles each)",
+                           "frac": round(ach / VALU_SLOTS_PEAK, 4), "traffic": None,
+                           "source": src, "time": "the score kernel's HIP events, this run"}
     if comm is None:  # the drop-in call's own kernels (timed above)
+        if slots.get("dropin") and "roofline" in out:
+            ach = slots["dropin"] / (dropin_fit_score * 1e-3)
+            out["roofline"].update({"dropin_achieved": round(ach / 1e9, 1),
+                                    "dropin_frac": round(ach / VALU_SLOTS_PEAK, 4),
+                                    "dropin_note": "the drop-in call's chunked fits + scores (first fit to last "
+                                                   "score, HIP events), executed slots from the PMC passes"})
         out["fp64"].update({
             "dropin_fit_score_ms": round(dropin_fit_score, 4), "dropin_span_ms": round(dropin_span, 4),
             "dropin_tflops": round(all_flops / (dropin_fit_score * 1e-3) / 1e12, 2),
