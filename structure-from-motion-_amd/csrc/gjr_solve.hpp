@@ -117,7 +117,7 @@ __device__ __forceinline__ void stamp_row(const Args &a, int row, int p, int slo
 __device__ __forceinline__ void stamp(const Args &a, int p, int slot) {
     stamp_row(a, (int)blockIdx.x < a.nT ? row_of(blockIdx.x, a.nT) : a.nT, p, slot);
 }
-enum { PW_WIN = 0, PW_GPUB, PW_CH0, PW_CH1, PW_PPUB, PW_AWIN, PW_AOUT, PW_BPUB };
+enum { PW_WIN = 0, PW_GPUB, PW_CH0, PW_CH1, PW_PPUB, PW_AWIN, PW_AOUT, PW_BPUB, PW_LIN, PW_STEP };
 
 struct Smem {
     double PL[RING][4][64];  // L_p^-1 fragments for the holder of A_rp
@@ -844,10 +844,10 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
     }
     // the holder of A_rq: G_r = A_rq L_q^-T into the ring slot of step q,
     // then its publication
-    auto form_g = [&](int q) -> bool {
+    auto form_g = [&](int q, bool have_lv, d4 lv) -> bool {
         const int sq = q & (RING - 1);
-        d4 lv;
-        if (PWG) {  // straight from the pivot record (no hand-off through W0)
+        if (have_lv) {
+        } else if (PWG) {  // straight from the pivot record (no hand-off through W0)
             const int soff[1] = {q * PBYTES};
             const bool need[1] = {true};
             u32x4 v[1][4];
@@ -953,7 +953,8 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
         const bool normal = p >= 0 && p != r && !(p >= r - LA && p < r);  // W0's steps: no live tile, no ring slot
         const int hi = r > p ? jmax + 1 : nT;  // live tiles j in (p, hi); W0 holds the rest up to r
         int fq = -1;
-        d4 g = zero4();
+        d4 g = zero4(), flv = zero4();
+        bool have = false;  // flv: the pivot record of step fq, loaded with the look-ahead's G
         if (p == -1) {
             if (w == 0 && 0 <= jmax) fq = 0;
         } else if (p == r) {  // the import: A_rj^T = G_j L_r^T for j > r (G_j of step r from owner j)
@@ -978,19 +979,36 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
             if ((p + 1) % NUW == w && p + 1 < hi) {  // this wave forms G_r of step p + 1: its tile first
                 // G_p+1,p from its granules (owner p + 1's W0 writes them
                 // first): one round trip, no flag then payload
+                // and the pivot record P_p+1 in the same round of loads
                 const int k1 = (p + 1) / NUW;
-                const int soff[1] = {gsoff(a, p, p + 1)};
-                const bool need[1] = {true};
-                u32x4 x[1][GPAIRS];
-                if (!sweep<1, GPAIRS>(rs.G, soff, need, a.tag, x, lane, S)) return false;
-                const d4 gj = -dec4(x[0]);
+                u32x4 x[GPAIRS], v[4];
+                long long t0 = -1;
+                for (unsigned it = 1;; ++it) {
+                    asm volatile("" ::: "memory");  // every pass reloads
+                    const __amdgpu_buffer_rsrc_t rg = rsrc(rs.G), rp = rsrc(rs.P);
+                    const int go = __builtin_amdgcn_readfirstlane(gsoff(a, p, p + 1));
+                    const int po = __builtin_amdgcn_readfirstlane((p + 1) * PBYTES);
+#pragma unroll
+                    for (int k = 0; k < GPAIRS; ++k) x[k] = __builtin_amdgcn_raw_buffer_load_b128(rg, k * 1024 + lane * 16, go, SC1);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b128(rp, k * 1024 + lane * 16, po, SC1);
+                    bool ok = true;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) ok &= x[k].y == a.tag && x[k].w == a.tag && v[k].y == a.tag && v[k].w == a.tag;
+                    if (__all(ok)) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    if (it % 64 == 0 && give_up(S, it, t0)) return false;
+                }
+                const d4 gj = -dec4(x);
 #pragma unroll
                 for (int k = 0; k < TPW; ++k)  // constant slot indices: the tiles stay in registers
                     if (k == k1) tset(k, mfma4(tget(k), gj, g));
                 fq = p + 1;
+                flv = dec4(v);
+                have = true;
             }
         }
-        if (fq >= 0 && !form_g(fq)) return false;
+        if (fq >= 0 && !form_g(fq, have, flv)) return false;
         if (normal) {
             const int lo = fq == p + 1 ? p + 1 : p;
             if (!wait_bulk<TPW>(a, p, w, lo, hi, lane, S)) return false;
@@ -1036,8 +1054,9 @@ struct PSm {
     double Lk[lk_off(LA + 1)];                      // stage D -> D - 1, D = 3 .. LA
     double Pl[PR][4][64], Py[PR][16];               // L_q^-1 fragment, y_q
     double Gr[GR][LA][4][64];                       // Gr[j % GR][d - 1] = G_j,j-d
-    double Lfr[2][4][64];                           // the L_q fragment for wave B
+    double Lrow[2][TL][TL + 1];                     // the L_q rows for wave B (its fragment for owner q)
     int win_ready, win_done, pl_ready, gc_ready, lf_ready, b_done;
+    int wm_ready, wd_ready;  // the window's A_q,q-1 (look-ahead wave 3) and A_qq, b_q (wave 0) for wave C
     int lk_ready[LA + 1], lk_done[LA + 1], grdy[LA + 1];  // link into stage d - 1; G_q,q-d of stage d ready
 };
 static_assert(sizeof(PSm) <= DYN_LDS, "pivot workgroup LDS");
@@ -1057,7 +1076,7 @@ __device__ __forceinline__ bool pw_chain(const Args &a, const Rs &rs, Smem &S, P
     double yp = 0.0;
     for (int q = 0; q < nT; ++q) {
         const int s2 = q & 1;
-        if (!lds_wait(&P.win_ready, q + 1, S)) return false;
+        if (!lds_wait(&P.wm_ready, q + 1, S) || !lds_wait(&P.wd_ready, q + 1, S)) return false;
         stamp(a, q, PW_WIN);
         d4 Tm = lds4(P.Wm[s2], lane), Td = lds4(P.Wd[s2], lane);
         double b = P.Wb[s2][li];
@@ -1082,9 +1101,10 @@ __device__ __forceinline__ bool pw_chain(const Args &a, const Rs &rs, Smem &S, P
         if (lane < 16) P.Py[q % PR][lane] = yr;
         lds_release();
         lds_set(&P.pl_ready, q + 1);
-        const d4 lf = l_frag(S, lane, rw);
-        if (!lds_wait(&P.b_done, q - 1, S)) return false;  // wave B read the fragment of q - 2
-        sto4(P.Lfr[s2], lane, lf);
+        if (!lds_wait(&P.b_done, q - 1, S)) return false;  // wave B read the rows of q - 2
+        if (lane < 16)  // the rows only: wave B forms the fragment, off this wave's path
+#pragma unroll
+            for (int j = 0; j < 16; ++j) P.Lrow[s2][lane][j] = j <= lane ? rw[j] : 0.0;
         lds_release();
         lds_set(&P.lf_ready, q + 1);
         lvp = lv;
@@ -1093,22 +1113,27 @@ __device__ __forceinline__ bool pw_chain(const Args &a, const Rs &rs, Smem &S, P
     return true;
 }
 
-// stage D (2 <= D <= LA) of the look-ahead: row q's window through step
-// q - D - 1 in (from owner q's record for D = LA, else from stage D + 1), step
-// q - D applied (G_q,q-D = L_q-D^-1 A_q,q-D with the G of the rows between
-// from LDS), the rest out to stage D - 1 (or wave C).  One wave a stage: a
-// window goes through the stages as the pivot records it needs come out.
-template <int D>
+// a stage of the look-ahead: steps q - DHI .. q - DLO of row q's window
+// (2 <= DLO <= DHI <= LA).  The window comes in through step q - DHI - 1
+// (from owner q's record for DHI = LA, else from the stage before), each step
+// s = q - d forms G_q,s = L_s^-1 A_q,s (the G of the rows between from LDS,
+// Gr), and the rest goes to the next stage (or wave C for DLO = 2).  Two
+// stages, steps q - LA .. q - 3 and step q - 2: a window's early steps need
+// only pivots long out, and the last one waits for wave C's G_q-1,q-2 alone.
+// Measured (round 6): one wave for all LA steps took ~2.2 us a window at
+// LA = 3 and wave C waited ~1 us a pivot; one wave a step (LA = 4) paid the
+// hand-offs between the stages (a window ~4.9 us).
+template <int DHI, int DLO>
 __device__ __forceinline__ bool pw_stage(const Args &a, const Rs &rs, Smem &S, PSm &P, int lane, double lambda) {
     const int nT = a.nT, li = lane & 15;
     for (int q = 0; q < nT; ++q) {
-        const int s2 = q & 1, s = q - D;
-        d4 T[D + 1];  // A_q,q-D .. A_qq
+        const int s2 = q & 1, s0 = q - DHI;
+        d4 T[DHI + 1];  // A_q,q-DHI .. A_qq
         double b;
-        if (D == LA) {
+        if (DHI == LA) {
             if (q <= LA) {  // untouched rows: straight from the payload, as their owner would load them
 #pragma unroll
-                for (int i = 0; i <= D; ++i) T[i] = s + i >= 0 ? load_tile(a, lambda, q, s + i, lane) : zero4();
+                for (int i = 0; i <= DHI; ++i) T[i] = s0 + i >= 0 ? load_tile(a, lambda, q, s0 + i, lane) : zero4();
                 b = assembled_b_src(a.src, a.payload, a.ns, TL * q + li);
             } else {
                 const int soff[1] = {q * WBYTES};
@@ -1116,59 +1141,161 @@ __device__ __forceinline__ bool pw_stage(const Args &a, const Rs &rs, Smem &S, P
                 u32x4 v[1][WPAIRS];
                 if (!sweep<1, WPAIRS>(rs.W, soff, need, a.tag, v, lane, S)) return false;
 #pragma unroll
-                for (int i = 0; i <= D; ++i)
+                for (int i = 0; i <= DHI; ++i)
                     T[i] = d4{dec(v[0][4 * i]), dec(v[0][4 * i + 1]), dec(v[0][4 * i + 2]), dec(v[0][4 * i + 3])};
                 b = dec(v[0][4 * WT]);
             }
             stamp(a, q, PW_AWIN);
         } else {
-            if (!lds_wait(&P.lk_ready[D + 1], q + 1, S)) return false;
-            const double *lk = P.Lk + lk_off(D + 1) + s2 * ((D + 1) * 256 + 16);
+            if (!lds_wait(&P.lk_ready[DHI + 1], q + 1, S)) return false;
+            const double *lk = P.Lk + lk_off(DHI + 1) + s2 * ((DHI + 1) * 256 + 16);
 #pragma unroll
-            for (int i = 0; i <= D; ++i) T[i] = d4{lk[i * 256 + lane], lk[i * 256 + 64 + lane], lk[i * 256 + 128 + lane],
-                                                  lk[i * 256 + 192 + lane]};
-            b = lk[(D + 1) * 256 + li];
+            for (int i = 0; i <= DHI; ++i) T[i] = d4{lk[i * 256 + lane], lk[i * 256 + 64 + lane], lk[i * 256 + 128 + lane],
+                                                    lk[i * 256 + 192 + lane]};
+            b = lk[(DHI + 1) * 256 + li];
             lds_release();
-            lds_set(&P.lk_done[D + 1], q + 1);
+            lds_set(&P.lk_done[DHI + 1], q + 1);
+            stamp(a, q, PW_LIN);
         }
-        if (s >= 0) {
+#pragma unroll
+        for (int d = DHI; d >= DLO; --d) {
+            const int s = q - d, t = DHI - d;  // step s; T[t] is A_q,s
+            if (s < 0) continue;
+            // every wait of the step first, then the LDS reads, then the MFMA
+            // chains: a wait is a loop the compiler cannot move work across,
+            // so waits between the tiles' updates had serialised their
+            // dependent MFMA chains (round 6 stamps: ~0.3 us an update)
             if (!lds_wait(&P.pl_ready, s + 1, S)) return false;
+#pragma unroll
+            for (int i = 1; i < d; ++i)  // G_j,s of the rows between, j = s + i (distance i; wave C's for i = 1)
+                if (!lds_wait(i == 1 ? &P.gc_ready : &P.grdy[i], s + i + 1, S)) return false;
             const d4 lv = lds4(P.Pl[s % PR], lane);
             const double ys = P.Py[s % PR][li];
-            const d4 g = mfma4(zero4(), lv, T[0]);
-            sto4(P.Gr[q % GR][D - 1], lane, g);
-            lds_release();
-            lds_set(&P.grdy[D], q + 1);
+            d4 gj[DHI];
 #pragma unroll
-            for (int i = 1; i < D; ++i) {  // A_q,j, j = s + i: G_j,s of row j (stage i's; wave C's for i = 1)
-                const int j = s + i;
-                if (!lds_wait(i == 1 ? &P.gc_ready : &P.grdy[i], j + 1, S)) return false;
-                T[i] = mfma4(T[i], -lds4(P.Gr[j % GR][i - 1], lane), g);
-            }
-            T[D] = mfma4(T[D], -g, g);
+            for (int i = 1; i < d; ++i) gj[i] = -lds4(P.Gr[(s + i) % GR][i - 1], lane);
+            const d4 g = mfma4(zero4(), lv, T[t]);
+            sto4(P.Gr[q % GR][d - 1], lane, g);
+            lds_release();
+            lds_set(&P.grdy[d], q + 1);
+#pragma unroll
+            for (int i = 1; i < d; ++i) T[t + i] = mfma4(T[t + i], gj[i], g);
+            T[DHI] = mfma4(T[DHI], -g, g);
             b -= gy(g, ys, lane);
+            stamp(a, q, PW_STEP + d);  // step q - d done (slots 11 .. 10 + LA)
         }
-        if (D == 2) {
+        constexpr int t0 = DHI - DLO + 1;  // the tiles left: T[t0 .. DHI], DLO of them
+        if (DLO == 2) {
             if (!lds_wait(&P.win_done, q - 1, S)) return false;  // wave C read window q - 2 (the slot)
-            sto4(P.Wm[s2], lane, T[1]);
-            sto4(P.Wd[s2], lane, T[2]);
+            sto4(P.Wm[s2], lane, T[t0]);
+            sto4(P.Wd[s2], lane, T[t0 + 1]);
             if (lane < 16) P.Wb[s2][lane] = b;
             lds_release();
             lds_set(&P.win_ready, q + 1);
             stamp(a, q, PW_AOUT);
         } else {
-            if (!lds_wait(&P.lk_done[D], q - 1, S)) return false;  // stage D - 1 read window q - 2 (the slot)
-            double *lk = P.Lk + lk_off(D) + s2 * (D * 256 + 16);
+            if (!lds_wait(&P.lk_done[DLO], q - 1, S)) return false;  // the next stage read window q - 2 (the slot)
+            double *lk = P.Lk + lk_off(DLO) + s2 * (DLO * 256 + 16);
 #pragma unroll
-            for (int i = 1; i <= D; ++i) {
-                lk[(i - 1) * 256 + lane] = T[i][0];
-                lk[(i - 1) * 256 + 64 + lane] = T[i][1];
-                lk[(i - 1) * 256 + 128 + lane] = T[i][2];
-                lk[(i - 1) * 256 + 192 + lane] = T[i][3];
+            for (int i = 0; i < DLO; ++i) {
+                lk[i * 256 + lane] = T[t0 + i][0];
+                lk[i * 256 + 64 + lane] = T[t0 + i][1];
+                lk[i * 256 + 128 + lane] = T[t0 + i][2];
+                lk[i * 256 + 192 + lane] = T[t0 + i][3];
             }
-            if (lane < 16) lk[D * 256 + lane] = b;
+            if (lane < 16) lk[DLO * 256 + lane] = b;
             lds_release();
-            lds_set(&P.lk_ready[D], q + 1);
+            lds_set(&P.lk_ready[DLO], q + 1);
+        }
+    }
+    return true;
+}
+
+// The look-ahead, tile-parallel (round 6): four waves share row q's window,
+// wave K holding tile A_q,q-LA+K (wave 0 also A_qq and b_q).  Step s = q - d
+// (d = LA .. 2) has its pivot tile t = LA - d: that tile's wave forms
+// G_q,s = L_s^-1 A_q,s into Gr, and every wave updates its later tiles with
+// it (A_q,j -= G_j,s G_q,s^T, G_j,s of row j from Gr or wave C), so a step's
+// MFMA work runs on four SIMDs and its critical path is the pivot tile's G,
+// one LDS hand-off and the next tile's update.  Measured and not kept (same
+// round): one wave for every step (a window ~2.2 us at LA = 3, ~4.3 us at
+// LA = 4 through two stage waves): wave C waited for the window each pivot.
+template <int K>
+__device__ __forceinline__ bool pw_look(const Args &a, const Rs &rs, Smem &S, PSm &P, int lane, double lambda) {
+    static_assert(LA == 4, "tile i of the window on look-ahead wave i % 4");
+    const int nT = a.nT, li = lane & 15;
+    for (int q = 0; q < nT; ++q) {
+        const int s2 = q & 1, lo = q - LA;
+        d4 Ta = zero4(), Tb = zero4();  // tile K; wave 0: tile LA (A_qq) too
+        double b = 0.0;
+        if (lo <= 0) {  // untouched rows: straight from the payload, as their owner would load them
+            if (lo + K >= 0) Ta = load_tile(a, lambda, q, lo + K, lane);
+            if (K == 0) {
+                Tb = load_tile(a, lambda, q, q, lane);
+                b = assembled_b_src(a.src, a.payload, a.ns, TL * q + li);
+            }
+        } else {
+            {
+                const int soff[1] = {q * WBYTES + 4 * K * 1024};
+                const bool need[1] = {true};
+                u32x4 v[1][4];
+                if (!sweep<1, 4>(rs.W, soff, need, a.tag, v, lane, S)) return false;
+                Ta = dec4(v[0]);
+            }
+            if (K == 0) {
+                const int soff[1] = {q * WBYTES + 4 * LA * 1024};
+                const bool need[1] = {true};
+                u32x4 v[1][5];
+                if (!sweep<1, 5>(rs.W, soff, need, a.tag, v, lane, S)) return false;
+                Tb = d4{dec(v[0][0]), dec(v[0][1]), dec(v[0][2]), dec(v[0][3])};
+                b = dec(v[0][4]);
+            }
+        }
+        if (K == 0) stamp(a, q, PW_AWIN);
+#pragma unroll
+        for (int d = LA; d >= 2; --d) {
+            const int s = q - d, t = LA - d;  // step s, pivot tile t
+            if (s < 0) continue;
+            d4 g;
+            if (t == K) {  // this wave's tile is the step's pivot tile
+                if (!lds_wait(&P.pl_ready, s + 1, S)) return false;
+                g = mfma4(zero4(), lds4(P.Pl[s % PR], lane), Ta);
+                sto4(P.Gr[q % GR][d - 1], lane, g);
+                lds_release();
+                lds_set(&P.grdy[d], q + 1);
+            }
+            const bool upA = K > t, upB = K == 0;
+            if (!upA && !upB) continue;
+            if (t != K) {  // the pivot tile's G (another wave's)
+                if (!lds_wait(&P.grdy[d], q + 1, S)) return false;
+                g = lds4(P.Gr[q % GR][d - 1], lane);
+            }
+            if (upA) {  // A_q,j, j = s + (K - t): G_j,s of row j (distance K - t; wave C's for 1)
+                const int e = K - t, j = s + e;
+                if (!lds_wait(e == 1 ? &P.gc_ready : &P.grdy[e], j + 1, S)) return false;
+                Ta = mfma4(Ta, -lds4(P.Gr[j % GR][e - 1], lane), g);
+            }
+            if (upB) {  // A_qq and b_q
+                if (!lds_wait(&P.pl_ready, s + 1, S)) return false;
+                const double ys = P.Py[s % PR][li];
+                Tb = mfma4(Tb, -g, g);
+                b -= gy(g, ys, lane);
+            }
+            if (K == 0) stamp(a, q, PW_STEP + d);
+        }
+        if (K == LA - 1 || K == 0) {  // the window through step q - 2 for wave C
+            if (!lds_wait(&P.win_done, q - 1, S)) return false;  // wave C read window q - 2 (the slot)
+            if (K == LA - 1) {
+                sto4(P.Wm[s2], lane, Ta);
+                lds_release();
+                lds_set(&P.wm_ready, q + 1);
+            } else {
+                sto4(P.Wd[s2], lane, Tb);
+                if (lane < 16) P.Wb[s2][lane] = b;
+                lds_release();
+                lds_set(&P.wd_ready, q + 1);
+                stamp(a, q, PW_AOUT);
+            }
         }
     }
     return true;
@@ -1178,7 +1305,9 @@ __device__ __forceinline__ bool pw_pub(const Args &a, const Rs &rs, Smem &S, PSm
     const int nT = a.nT;
     for (int q = 0; q < nT; ++q) {
         if (!lds_wait(&P.lf_ready, q + 1, S)) return false;
-        const d4 lf = lds4(P.Lfr[q & 1], lane);
+        d4 lf;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) lf[e] = P.Lrow[q & 1][lane & 15][4 * e + (lane >> 4)];  // L_q(l & 15, 4e + (l >> 4))
         lds_release();
         lds_set(&P.b_done, q + 1);
         put4(rs.Lr, q * LBYTES, a.tag, lf, lane);
@@ -1204,7 +1333,8 @@ __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
         S.lready = S.abort_ = S.last = S.w0done = 0;
         S.err = a.err;
         S.bad = a.bad;
-        if (pwg) PS.win_ready = PS.win_done = PS.pl_ready = PS.gc_ready = PS.lf_ready = PS.b_done = 0;
+        if (pwg) PS.win_ready = PS.win_done = PS.pl_ready = PS.gc_ready = PS.lf_ready = PS.b_done = PS.wm_ready =
+            PS.wd_ready = 0;
     }
     if (pwg && threadIdx.x <= LA) {
         PS.lk_ready[threadIdx.x] = PS.lk_done[threadIdx.x] = PS.grdy[threadIdx.x] = 0;
@@ -1220,10 +1350,10 @@ __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
     if (pwg) {  // no arrival: the owners' x is the result
         if (wu == 0) pw_chain(a, rs, S, PS, lane);
         else if (wu == 1) pw_pub(a, rs, S, PS, lane);
-        else if (wu == 2) pw_stage<2>(a, rs, S, PS, lane, lambda);
-        else if (wu == 3) pw_stage<3>(a, rs, S, PS, lane, lambda);
-        else if (wu == 4) pw_stage<4>(a, rs, S, PS, lane, lambda);
-        static_assert(LA == 4, "one wave a look-ahead stage: the dispatch above");
+        else if (wu == 2) pw_look<0>(a, rs, S, PS, lane, lambda);
+        else if (wu == 3) pw_look<1>(a, rs, S, PS, lane, lambda);
+        else if (wu == 4) pw_look<2>(a, rs, S, PS, lane, lambda);
+        else if (wu == 5) pw_look<3>(a, rs, S, PS, lane, lambda);
         return;
     }
     if (wu == 0) {

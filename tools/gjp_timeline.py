@@ -36,6 +36,13 @@ for q in range(nT):
     print(f"{q:4d} {pw[q, WIN]:7.2f} {stall:6.2f} {pw[q, GPUB]:7.2f} {pw[q, CH0]:7.2f} {pw[q, CH1]:7.2f} "
           f"{pw[q, PPUB]:7.2f} {step:6.2f} | {pw[q, AWIN]:7.2f} {pw[q, AOUT]:6.2f} {slack:6.2f}")
     prev = pw[q, PPUB]
+# the look-ahead stages of the pivot workgroup: per window, when its record
+# (or the link from the early stage) was in and each of its steps done
+LIN, STEP = 8, 9
+print("   q   rec   d4done  d3done | link  d2done   out | C:win[q-1]")
+for q in range(2, min(nT, 30)):
+    print(f"{q:4d} {pw[q, AWIN]:7.2f} {pw[q, STEP + 4]:7.2f} {pw[q, STEP + 3]:7.2f} | {pw[q, LIN]:6.2f} "
+          f"{pw[q, STEP + 2]:7.2f} {pw[q, AOUT]:6.2f} | {pw[q - 1, WIN]:7.2f}")
 steps = np.diff(pw[:nT, PPUB])
 chain = pw[:nT, CH1] - pw[:nT, CH0]
 print(f"mean step {np.nanmean(steps):.3f} us, median {np.nanmedian(steps):.3f}, chain median {np.nanmedian(chain):.3f}")
