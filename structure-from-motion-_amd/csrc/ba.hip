@@ -2312,22 +2312,21 @@ static int launch_gj(const GjPlan &g, int nT, int32_t ns, const double *payload,
 // above (or the Cholesky) runs instead; SFM_SOLVE=gjseg / chol force those.
 struct GjrPlan {
     int nT = 0, tpw = 0;
-    bool pwg = false;  // the pivot workgroup (block nT runs every pivot)
     bool ok() const { return tpw > 0; }
 };
-template <int TR, int TLS, bool PWG>
+template <int TR, int TLS>
 static bool gjr_resident(int nT, int ncu) {
     static int nb = -1;  // resident workgroups per CU (queried once per instantiation)
     if (nb < 0) {
         nb = 0;
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&gjr::k_gjr_solve<TR, TLS, PWG>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&gjr::k_gjr_solve<TR, TLS>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, gjr::DYN_LDS) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gjr::k_gjr_solve<TR, TLS, PWG>, gjr::THREADS,
-                                                         gjr::DYN_LDS) != hipSuccess)
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gjr::k_gjr_solve<TR, TLS>, gjr::THREADS, gjr::DYN_LDS) !=
+                hipSuccess)
             nb = 0;
         (void)hipGetLastError();
     }
-    return nb >= 1 && nT + (PWG ? 1 : 0) <= nb * ncu;
+    return nb >= 1 && nT <= nb * ncu;
 }
 static GjrPlan gjr_plan(int nT, int ncu) {
     GjrPlan g;
@@ -2335,41 +2334,32 @@ static GjrPlan gjr_plan(int nT, int ncu) {
         if (std::strcmp(e, "chol") == 0 || std::strcmp(e, "gjseg") == 0) return g;
     // tile slots per U wave: 4 or TREG in registers (up to 28 / 77 tile
     // rows), past that TREG_L + TLDS_L (the latter in LDS: up to gjr::NTMAX = 128)
-    const char *pe = std::getenv("SFM_GJR_PWG");  // 0: the owner-only layout (round 4/5)
-    const bool pwg = !pe || std::atoi(pe) != 0;
-    if (nT < 1 || nT > gjr::NTMAX || nT + (pwg ? 1 : 0) > ncu) return g;
+    if (nT < 1 || nT > gjr::NTMAX || nT > ncu) return g;
     const int tpw = nT <= 4 * gjr::NUW ? 4 : nT <= gjr::TREG * gjr::NUW ? gjr::TREG : gjr::TREG_L + gjr::TLDS_L;
-    const bool res = pwg ? (tpw == 4 ? gjr_resident<4, 0, true>(nT, ncu)
-                            : tpw == gjr::TREG ? gjr_resident<gjr::TREG, 0, true>(nT, ncu)
-                                               : gjr_resident<gjr::TREG_L, gjr::TLDS_L, true>(nT, ncu))
-                         : (tpw == 4 ? gjr_resident<4, 0, false>(nT, ncu)
-                            : tpw == gjr::TREG ? gjr_resident<gjr::TREG, 0, false>(nT, ncu)
-                                               : gjr_resident<gjr::TREG_L, gjr::TLDS_L, false>(nT, ncu));
+    const bool res = tpw == 4 ? gjr_resident<4, 0>(nT, ncu)
+                   : tpw == gjr::TREG ? gjr_resident<gjr::TREG, 0>(nT, ncu)
+                                      : gjr_resident<gjr::TREG_L, gjr::TLDS_L>(nT, ncu);
     if (!res) return g;
     g.nT = nT;
     g.tpw = tpw;
-    g.pwg = pwg;
     return g;
 }
 // granule records (zeroed once; tags only grow) and the err / arrival words
 struct GjrBufs {
-    gjr::u64 *P = nullptr, *G = nullptr, *W = nullptr, *Lr = nullptr;
+    gjr::u64 *P = nullptr, *G = nullptr;
     double *Gd = nullptr;
     unsigned *Gf = nullptr;
     int *err = nullptr;
     unsigned *arrive = nullptr;
     static size_t words(int nT) {
         const size_t t = (size_t)nT * nT;
-        return ((size_t)2 * nT * gjr::PBYTES + (size_t)nT * (gjr::WBYTES + gjr::LBYTES) + t * gjr::GBYTES +
-                t * gjr::GDBYTES) / 8 + (t + 1) / 2;
+        return ((size_t)2 * nT * gjr::PBYTES + t * gjr::GBYTES + t * gjr::GDBYTES) / 8 + (t + 1) / 2;
     }
     static constexpr size_t ints = 64;
     void carve(gjr::u64 *w, int *i, int nT) {
         const size_t t = (size_t)nT * nT;
         P = w;
-        W = P + (size_t)2 * nT * gjr::PBYTES / 8;
-        Lr = W + (size_t)nT * gjr::WBYTES / 8;
-        G = Lr + (size_t)nT * gjr::LBYTES / 8;
+        G = P + (size_t)2 * nT * gjr::PBYTES / 8;
         Gd = reinterpret_cast<double *>(G + t * gjr::GBYTES / 8);
         Gf = reinterpret_cast<unsigned *>(Gd + t * gjr::GDBYTES / 8);
         err = i;
@@ -2390,8 +2380,6 @@ static int launch_gjr(const GjrPlan &g, int32_t ns, const double *payload, const
     a.G = b.G;
     a.Gd = b.Gd;
     a.Gf = b.Gf;
-    a.W = b.W;
-    a.Lr = b.Lr;
     a.tag = tag;
     a.x = x;
     a.bad = bad;
@@ -2399,29 +2387,15 @@ static int launch_gjr(const GjrPlan &g, int32_t ns, const double *payload, const
     a.arrive = b.arrive;
     a.ct = ct;
     a.dbg = gj_dbg_ptr();
-    const dim3 grid(g.nT + (g.pwg ? 1 : 0));
-    if (g.pwg) {
-        switch (g.tpw) {
-        case 4: hipLaunchKernelGGL((gjr::k_gjr_solve<4, 0, true>), grid, dim3(gjr::THREADS), gjr::DYN_LDS, s, a); break;
-        case gjr::TREG:
-            hipLaunchKernelGGL((gjr::k_gjr_solve<gjr::TREG, 0, true>), grid, dim3(gjr::THREADS), gjr::DYN_LDS, s, a);
-            break;
-        default:
-            hipLaunchKernelGGL((gjr::k_gjr_solve<gjr::TREG_L, gjr::TLDS_L, true>), grid, dim3(gjr::THREADS),
-                               gjr::DYN_LDS, s, a);
-            break;
-        }
-    } else {
-        switch (g.tpw) {
-        case 4: hipLaunchKernelGGL((gjr::k_gjr_solve<4, 0, false>), grid, dim3(gjr::THREADS), gjr::DYN_LDS, s, a); break;
-        case gjr::TREG:
-            hipLaunchKernelGGL((gjr::k_gjr_solve<gjr::TREG, 0, false>), grid, dim3(gjr::THREADS), gjr::DYN_LDS, s, a);
-            break;
-        default:
-            hipLaunchKernelGGL((gjr::k_gjr_solve<gjr::TREG_L, gjr::TLDS_L, false>), grid, dim3(gjr::THREADS),
-                               gjr::DYN_LDS, s, a);
-            break;
-        }
+    switch (g.tpw) {
+    case 4: hipLaunchKernelGGL((gjr::k_gjr_solve<4, 0>), dim3(g.nT), dim3(gjr::THREADS), gjr::DYN_LDS, s, a); break;
+    case gjr::TREG:
+        hipLaunchKernelGGL((gjr::k_gjr_solve<gjr::TREG, 0>), dim3(g.nT), dim3(gjr::THREADS), gjr::DYN_LDS, s, a);
+        break;
+    default:
+        hipLaunchKernelGGL((gjr::k_gjr_solve<gjr::TREG_L, gjr::TLDS_L>), dim3(g.nT), dim3(gjr::THREADS), gjr::DYN_LDS,
+                           s, a);
+        break;
     }
     SFM_HIP(hipGetLastError());
     return 0;

@@ -54,15 +54,6 @@ constexpr int GPAIRS = 4;        // granule pairs a lane of a published G tile
 constexpr int PBYTES = PPAIRS * 64 * 16;
 constexpr int GBYTES = GPAIRS * 64 * 16;
 constexpr int GDBYTES = 2 * 64 * 16;  // a G tile untagged: two 16-byte rows of 64 lanes (the bulk copy)
-// the pivot workgroup (PWG, round 6): owner r ships its window W_r = {A_r,r-LA
-// .. A_rr, b_r} after step r - LA - 1; the pivot workgroup's L_r fragment
-// record goes back to owner r for its import
-constexpr int LA = 4;       // look-ahead: owner r ships its window after step r - LA - 1
-constexpr int WT = LA + 1;  // window tiles A_r,r-LA .. A_rr
-constexpr int WPAIRS = 4 * WT + 1;  // granule pairs a lane of a window: the tiles (4 each), b (1)
-constexpr int WBYTES = WPAIRS * 64 * 16;
-constexpr int LPAIRS = 4;  // the L_r fragment
-constexpr int LBYTES = LPAIRS * 64 * 16;
 constexpr int NB = 6;                 // bulk G tiles a U wave has in flight
 constexpr long long POLL_LIMIT = 20000000;  // s_memrealtime ticks (100 MHz): 200 ms
 constexpr int TREG = 11;                    // tile slots a U wave holds in registers (more would spill)
@@ -84,8 +75,6 @@ struct Args {
     u64 *G;         // [nT][nT] G_r of step p at (p, r), GBYTES each (granules: W0 of owner r + 1)
     double *Gd;     // [nT][nT] the same untagged, GDBYTES each (the U waves' bulk updates) ...
     unsigned *Gf;   // [nT][nT] ... published by a flag (= tag) behind the drained stores
-    u64 *W;         // [nT] windows of WBYTES (PWG)
-    u64 *Lr;        // [nT] L_r fragments of LBYTES (PWG)
     unsigned tag;   // this launch's granule tag (>= 1)
     double *x;      // [nT * 16] solution
     int *bad;       // not positive definite (the LM rejects the step)
@@ -109,15 +98,10 @@ __device__ __forceinline__ int xcd_of_row(int r, int nT) {
     const int q = nT / NXCD_, m = nT % NXCD_;
     return r < m * (q + 1) ? r / (q + 1) : m + (r - m * (q + 1)) / max(q, 1);
 }
-__device__ __forceinline__ void stamp_row(const Args &a, int row, int p, int slot) {
-    if (a.dbg && (threadIdx.x & 63) == 0)
-        a.dbg[((int64_t)row * (a.nT + 1) + p) * 16 + slot] = __builtin_amdgcn_s_memrealtime();
-}
-// the pivot workgroup (block nT) stamps as row nT
 __device__ __forceinline__ void stamp(const Args &a, int p, int slot) {
-    stamp_row(a, (int)blockIdx.x < a.nT ? row_of(blockIdx.x, a.nT) : a.nT, p, slot);
+    if (a.dbg && (threadIdx.x & 63) == 0)
+        a.dbg[((int64_t)row_of(blockIdx.x, a.nT) * (a.nT + 1) + p) * 16 + slot] = __builtin_amdgcn_s_memrealtime();
 }
-enum { PW_WIN = 0, PW_GPUB, PW_CH0, PW_CH1, PW_PPUB, PW_AWIN, PW_AOUT, PW_BPUB, PW_LIN, PW_STEP };
 
 struct Smem {
     double PL[RING][4][64];  // L_p^-1 fragments for the holder of A_rp
@@ -128,7 +112,6 @@ struct Smem {
     double bv[TL], yv[TL];
     int pready[RING], pdone[RING], gready[RING], gdone[RING];
     int lready, abort_, last;
-    int hgready[RING], w0done;  // (PWG) the holders' G_r for W0 through PL (the mailbox), W0's progress
     int *err, *bad;
 };
 
@@ -215,7 +198,7 @@ struct Buf {
     int bytes;
 };
 struct Rs {
-    Buf P, G, Gd, W, Lr;
+    Buf P, G, Gd;
 };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const Buf &b) {
     const u64 a = (u64)b.base;
@@ -409,10 +392,10 @@ __device__ __forceinline__ double gy(const d4 &g, double yl, int lane) {
 // U waves' prologue from the payload: pay_index in 32-bit arithmetic with the
 // lane's row terms hoisted, zero unless live, every load unconditional (in
 // bounds) so that a group of tiles has its loads in flight together
-__device__ __forceinline__ d4 load_lower(const Args &a, int r, int j, int jmax, int lane) {
+__device__ __forceinline__ d4 load_lower(const Args &a, int r, int j, int lane) {
     const int I = TL * r + (lane & 15), nc = (a.ns + 5) / 6;
     const int ib = I / 6, ir = I - 6 * ib;
-    const bool live = j <= jmax && I < a.ns;  // jmax <= r - 2
+    const bool live = j <= r - 2 && I < a.ns;
     int idx[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -461,21 +444,9 @@ __device__ __forceinline__ d4 load_tile(const Args &a, double lambda, int r, int
 __device__ __forceinline__ int g_uses(int p, int r) {
     return p / RING - (r < p && (r & (RING - 1)) == (p & (RING - 1)) ? 1 : 0);
 }
-// PWG: the ring carries the holders' G to the U waves only, at every step
-// but W0's [r - LA, r]
-__device__ __forceinline__ int g_uses_pwg(int p, int r) {
-    int u = p / RING;
-#pragma unroll
-    for (int d = 0; d <= LA; ++d)
-        if (r - d >= 0 && r - d < p && ((r - d) & (RING - 1)) == (p & (RING - 1))) --u;
-    return u;
-}
-template <bool PWG = false>
 __device__ __forceinline__ int p_uses(int p, int r) {
     int u = g_uses(p, r);
-#pragma unroll
-    for (int d = 1; d <= (PWG ? LA : 1); ++d)
-        if (r >= d && r - d < p && ((r - d) & (RING - 1)) == (p & (RING - 1))) --u;
+    if (r >= 1 && r - 1 < p && ((r - 1) & (RING - 1)) == (p & (RING - 1))) --u;
     return u;
 }
 
@@ -483,23 +454,20 @@ __device__ __forceinline__ int p_uses(int p, int r) {
 // The pivot: the chain on the diagonal tile with the b row (lane 0) and the
 // identity (lanes 16..31) as panel rows -> L_r (rows), y_r, L_r^-T rows.
 // Publishes P_r; leaves L_r^-1 in S.Li and the L_r fragment in S.Lf.
-// the chain itself: L_r rows in rw (lanes 0..15), the L_r^-1 fragment (lv)
-// and y_r (yr = y_r(l & 15)) out
-__device__ __forceinline__ void pivot_core(const Args &a, Smem &S, int r, int lane, const d4 &Td, double b,
-                                           double (&rw)[16], d4 &lv, double &yr, int ch0, int ch1) {
+__device__ __forceinline__ void pivot(const Args &a, const Rs &rs, Smem &S, int r, int lane, const d4 &Td, double b) {
     const int li = lane & 15, grp = lane >> 4;
 #pragma unroll
     for (int e = 0; e < 4; ++e) S.Dm[li][grp + 4 * e] = Td[e];  // symmetric: column li = row li
     if (lane < 16) S.bv[lane] = b;
     wave_lds();
-    double pw[16], dinv[16];
+    double rw[16], pw[16], dinv[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) rw[j] = S.Dm[li][j];
 #pragma unroll
     for (int j = 0; j < 16; ++j) pw[j] = grp == 0 ? (lane == 0 ? S.bv[j] : 0.0) : (grp == 1 && j == li ? 1.0 : 0.0);
-    stamp(a, r, ch0);
+    stamp(a, r, DBG_CHAIN0);
     gj::gj_factor16(rw, pw, dinv, lane, a.bad);
-    stamp(a, r, ch1);
+    stamp(a, r, DBG_CHAIN1);
     if (grp == 1)
 #pragma unroll
         for (int j = 0; j < 16; ++j) S.Li[j][li] = pw[j];  // row li of L^-T = column li of L^-1
@@ -507,35 +475,22 @@ __device__ __forceinline__ void pivot_core(const Args &a, Smem &S, int r, int la
 #pragma unroll
         for (int j = 0; j < 16; ++j) S.yv[j] = pw[j];
     wave_lds();
+    d4 lv;
 #pragma unroll
     for (int e = 0; e < 4; ++e) lv[e] = S.Li[li][4 * e + grp];  // L^-1(l & 15, 4e + (l >> 4))
-    yr = S.yv[li];
-}
-// the L_r fragment (the imports' B operand) from the chain's rows
-__device__ __forceinline__ d4 l_frag(Smem &S, int lane, const double (&rw)[16]) {
-    const int li = lane & 15, grp = lane >> 4;
-    if (grp == 0)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) S.Dm[li][j] = j <= li ? rw[j] : 0.0;
-    wave_lds();
-    d4 lf;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) lf[e] = S.Dm[li][4 * e + grp];
-    return lf;
-}
-__device__ __forceinline__ void pivot(const Args &a, const Rs &rs, Smem &S, int r, int lane, const d4 &Td, double b) {
-    double rw[16], yr;
-    d4 lv;
-    pivot_core(a, S, r, lane, Td, b, rw, lv, yr, DBG_CHAIN0, DBG_CHAIN1);
+    const double yr = S.yv[li];
     put4<0>(rs.P, (a.nT + r) * PBYTES, a.tag, lv, lane);  // the L2-local copy first (the next owner)
     put_pair<0>(rs.P, (a.nT + r) * PBYTES, 4, a.tag, yr, lane);
     put4(rs.P, r * PBYTES, a.tag, lv, lane);
     put_pair(rs.P, r * PBYTES, 4, a.tag, yr, lane);
     stamp(a, r, DBG_PPUB);
     // the L_r rows (for the import's fragment) after the publication
-    const d4 lf = l_frag(S, lane, rw);
+    if (grp == 0)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) S.Lf[e][lane] = lf[e];
+        for (int j = 0; j < 16; ++j) S.Dm[li][j] = j <= li ? rw[j] : 0.0;
+    wave_lds();
+#pragma unroll
+    for (int e = 0; e < 4; ++e) S.Lf[e][lane] = S.Dm[li][4 * e + grp];
     lds_release();
     lds_set(&S.lready, 1);
 }
@@ -641,140 +596,6 @@ __device__ __forceinline__ bool w0_loop(const Args &a, const Rs &rs, Smem &S, in
     return true;
 }
 
-// W0 (PWG): the loads of P_p, issued a step ahead (w0_ok checks them)
-__device__ __forceinline__ void w0_issue(const Rs &rs, int p, u32x4 (&pv)[PPAIRS], int lane) {
-    const __amdgpu_buffer_rsrc_t rp = rsrc(rs.P);
-#pragma unroll
-    for (int k = 0; k < PPAIRS; ++k)
-        pv[k] = __builtin_amdgcn_raw_buffer_load_b128(rp, k * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(p * PBYTES), SC1);
-}
-__device__ __forceinline__ bool w0_ok(const u32x4 (&pv)[PPAIRS], unsigned tag) {
-    bool ok = true;
-#pragma unroll
-    for (int k = 0; k < PPAIRS; ++k) ok &= pv[k].y == tag && pv[k].w == tag;
-    return __all(ok);
-}
-
-// W0 of owner r with the pivot workgroup (PWG): the tiles A_r,r-LA .. A_rr
-// (T[0..LA]) and b_r.  Through step r - LA - 1 the holders' G_r update them;
-// then they go out as the window W_r (rows 0..LA: the pivot workgroup reads
-// them from the payload).  At the steps p in [r - LA, r - 1] this wave holds
-// A_rp and forms G_r itself, publishes it (the others' updates, the later
-// owners' windows) and keeps the later tiles current -- the same operations
-// the pivot workgroup repeats on its copy, so the owners never wait for the
-// pivot workgroup's G, only for its pivot records.  At step r: P_r and the
-// L_r fragment record (the U waves' import).  W0 reads everything from
-// global memory and feeds no ring: the holders poll the pivot records
-// themselves, so a W0 behind the pivots holds up nobody's step.
-// The W0 of consecutive owners form a chain, one link a step (owner r's G_r
-// of step p needs A_r,p current, i.e. G_r-1 of step p - 1 from owner r - 1's
-// W0), so a link is kept short: the step's pivot record (and holder's G) are
-// loaded a step ahead, W0's own G leaves (granules) before anything else of
-// the step, and the bulk copy's flag waits until the remote poll has drained
-// the stores.
-__device__ __forceinline__ bool w0_loop_pwg(const Args &a, const Rs &rs, Smem &S, int r, int lane, double lambda) {
-    const int nT = a.nT, li = lane & 15, grp = lane >> 4, lo = r - LA;
-    d4 T[WT];
-#pragma unroll
-    for (int i = 0; i < WT; ++i)
-        T[i] = lo + i >= 0 && (i < LA || lo > 0) ? load_tile(a, lambda, r, lo + i, lane) : zero4();
-    double b = assembled_b_src(a.src, a.payload, a.ns, TL * r + li);
-    stamp(a, nT, DBG_PROLOGUE);
-    u32x4 pv[PPAIRS];
-    w0_issue(rs, 0, pv, lane);
-    for (int p = 0; p < nT; ++p) {
-        const bool own = p >= lo && p < r;  // this wave holds A_rp
-        {
-            long long t0 = -1;
-            for (unsigned it = 1; !w0_ok(pv, a.tag); ++it) {
-                __builtin_amdgcn_s_sleep(1);
-                if (it % 64 == 0 && give_up(S, it, t0)) return false;
-                w0_issue(rs, p, pv, lane);
-            }
-        }
-        stamp(a, p, DBG_PIN);
-        const d4 lv = dec4(pv);
-        const double yl = dec(pv[4]);
-        if (p + 1 < nT) w0_issue(rs, p + 1, pv, lane);
-        if (p == r) {  // L_r^-1 for x_r, the L_r fragment for the U waves' import
-            const int soff[1] = {r * LBYTES};
-            const bool need[1] = {true};
-            u32x4 lfv[1][LPAIRS];
-            if (!sweep<1, LPAIRS>(rs.Lr, soff, need, a.tag, lfv, lane, S)) return false;
-            const d4 lf = dec4(lfv[0]);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                S.Li[li][4 * e + grp] = lv[e];
-                S.Lf[e][lane] = lf[e];
-            }
-            lds_release();
-            lds_set(&S.lready, 1);
-            lds_set(&S.w0done, p + 1);
-            continue;
-        }
-        d4 g;
-        if (!own) {  // the holder's G_r of this step (LDS mailbox PL[p % RING])
-            if (!lds_wait(&S.hgready[p & (RING - 1)], p + 1, S)) return false;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) g[e] = S.PL[p & (RING - 1)][e][lane];
-            lds_release();
-        }
-        if (own) {
-            d4 tp = zero4();
-#pragma unroll
-            for (int i = 0; i < LA; ++i)
-                if (lo + i == p) tp = T[i];
-            g = mfma4(zero4(), lv, tp);
-            // granules first: the later owners' W0 and every owner's wave that
-            // forms its G of step p + 1 (the look-ahead) poll them; then the
-            // bulk copy for the other owners' U waves (its flag below)
-            put4(rs.G, gsoff(a, p, r), a.tag, g, lane);
-            put_bulk(rs.Gd, gdoff(a, p, r), g, lane);
-        }
-        lds_set(&S.w0done, p + 1);  // the mailbox slot is free again
-        b -= gy(g, yl, lane);
-        if (p < r) {
-            int soff[LA];
-            bool need[LA], any = false;
-#pragma unroll
-            for (int i = 0; i < LA; ++i) {
-                need[i] = lo + i > p && lo + i >= 0;
-                soff[i] = need[i] ? gsoff(a, p, lo + i) : 0;
-                any |= need[i];
-            }
-            u32x4 rv[LA][GPAIRS];
-            if (any && !sweep<LA, GPAIRS>(rs.G, soff, need, a.tag, rv, lane, S)) return false;
-            stamp(a, p, DBG_GREM);
-            if (own) flag_bulk(a, p, r);  // the stores have drained behind the poll
-#pragma unroll
-            for (int i = 0; i < LA; ++i)
-                if (need[i]) T[i] = mfma4(T[i], -dec4(rv[i]), g);
-            if (p < lo) T[LA] = mfma4(T[LA], -g, g);  // A_rr: only until the window is out
-            if (p == lo - 1) {  // the window W_r, through step r - LA - 1
-                const int wo = r * WBYTES;
-#pragma unroll
-                for (int i = 0; i < WT; ++i) put4(rs.W, wo + 4 * i * 1024, a.tag, T[i], lane);
-                put_pair(rs.W, wo, 4 * WT, a.tag, b, lane);
-                stamp(a, p, DBG_GCRIT);
-            }
-        }
-    }
-    // x_r = L_r^-T (L_r^-1 b_r)
-    if (lane < 16) S.bv[lane] = b;
-    wave_lds();
-    double u = 0.0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) u = fma(S.Li[li][k], S.bv[k], u);
-    if (lane < 16) S.yv[lane] = u;
-    wave_lds();
-    double x = 0.0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) x = fma(S.Li[i][li], S.yv[i], x);
-    if (lane < 16) __hip_atomic_store(a.x + TL * r + lane, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    stamp(a, nT, DBG_W0END);
-    return true;
-}
-
 // ------------------------------------------------------------- U waves
 // U_w of owner r holds the tiles j = w + NUW k (k < TPW) other than r - 1
 // and r: the lower ones from the start, the ones right of the diagonal from
@@ -783,12 +604,11 @@ __device__ __forceinline__ bool w0_loop_pwg(const Args &a, const Rs &rs, Smem &S
 // tiles j in (p, hi), two tiles' remote G loads in flight at a time.
 // Slots: TR in registers, TLS more in LDS (tl: this wave's [TLS][4][64]
 // doubles; large systems only, the register file holds 11 a wave).
-template <int TR, int TLS, bool PWG>
+template <int TR, int TLS>
 __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int r, int w, int lane, double lambda,
                                        double *tl) {
     constexpr int TPW = TR + TLS;
     const int nT = a.nT;
-    const int jmax = PWG ? r - LA - 1 : r - 2;  // the lower tiles this wave holds (W0: the rest up to r)
     d4 T[TR];
     auto tget = [&](int k) -> d4 {  // k is a constant after unrolling: the branch folds
         if (k < TR) return T[k < TR ? k : 0];
@@ -818,10 +638,10 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
         constexpr int PG = 4;
 #pragma unroll 1
         for (int k0 = 0; k0 < TPW; k0 += PG) {
-            if (w + NUW * k0 > jmax) break;  // nothing live from here on
+            if (w + NUW * k0 > r - 2) break;  // nothing live from here on
             d4 v[PG];
 #pragma unroll
-            for (int q = 0; q < PG; ++q) v[q] = load_lower(a, r, w + NUW * (k0 + q), jmax, lane);
+            for (int q = 0; q < PG; ++q) v[q] = load_lower(a, r, w + NUW * (k0 + q), lane);
 #pragma unroll
             for (int q = 0; q < PG; ++q) {
                 const int k = k0 + q;
@@ -835,60 +655,13 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
 #pragma unroll 1
         for (int k = 0; k < TPW; ++k) {
             const int j = w + NUW * k;
-            const d4 v = j <= jmax ? load_tile(a, lambda, r, j, lane) : zero4();
+            const d4 v = j <= r - 2 ? load_tile(a, lambda, r, j, lane) : zero4();
 #pragma unroll
             for (int kk = 0; kk < TR; ++kk)
                 if (kk == k) T[kk] = v;
             if (k >= TR) tset(k, v);
         }
     }
-    // the holder of A_rq: G_r = A_rq L_q^-T into the ring slot of step q,
-    // then its publication
-    auto form_g = [&](int q, bool have_lv, d4 lv) -> bool {
-        const int sq = q & (RING - 1);
-        if (have_lv) {
-        } else if (PWG) {  // straight from the pivot record (no hand-off through W0)
-            const int soff[1] = {q * PBYTES};
-            const bool need[1] = {true};
-            u32x4 v[1][4];
-            if (!sweep<1, 4>(rs.P, soff, need, a.tag, v, lane, S)) return false;
-            lv = dec4(v[0]);
-        } else {
-            if (!lds_wait(&S.pready[sq], q + 1, S)) return false;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) lv[e] = S.PL[sq][e][lane];
-            lds_release();
-            lds_add(&S.pdone[sq], 1);
-        }
-        stamp(a, q, DBG_HPRDY);
-        d4 tp = zero4();
-#pragma unroll
-        for (int k = 0; k < TPW; ++k)
-            if (k == q / NUW) tp = tget(k);
-        const d4 g = mfma4(zero4(), lv, tp);
-        if (!lds_wait(&S.gdone[sq], PWG ? NUW * g_uses_pwg(q, r) : NW * g_uses(q, r), S)) return false;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) S.GL[sq][e][lane] = g[e];
-        lds_release();
-        lds_set(&S.gready[sq], q + 1);
-        stamp(a, q, DBG_GHOLD);
-        if (PWG) {  // W0's copy (the mailbox; W0 has read step q - RING's)
-            if (!lds_wait(&S.w0done, q - RING + 1, S)) return false;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) S.PL[sq][e][lane] = g[e];
-            lds_release();
-            lds_set(&S.hgready[sq], q + 1);
-        }
-        // granules: W0 of owners r + 1 .. r + LA (and with PWG this owner's
-        // W0 at every step); bulk: every other owner's U waves
-        if (r > q) put4(rs.G, gsoff(a, q, r), a.tag, g, lane);
-        if (r > q) {
-            put_bulk(rs.Gd, gdoff(a, q, r), g, lane);
-            flag_bulk(a, q, r);
-        }
-        return true;
-    };
-    if (!PWG) {
     for (int p = 0; p < nT; ++p) {
         const int s = p & (RING - 1);
         if (p == r) {  // the import: A_rj^T = G_j L_r^T for j > r (G_j of step r from owner j)
@@ -940,383 +713,10 @@ __device__ __forceinline__ bool u_loop(const Args &a, const Rs &rs, Smem &S, int
         bulk_update<TPW, false>(a, rs, p, w, p, hi, g, lane, tget, tset);
         if (w == 0) stamp(a, p, DBG_UDONE);
     }
-        return true;
-    }
-    // (PWG) Every G_r is formed one step early, by the wave that holds
-    // A_rq, right after that tile's update of step q - 1 and before the rest
-    // of that step: the owners' G of a step leave a step ahead, so no
-    // owner's step waits on every other owner's same step (the lockstep that
-    // had set the owners' pace).  One formation site per iteration (fq):
-    // iteration p = -1 forms step 0's, the import step forms step r + 1's.
-    for (int p = -1; p < nT; ++p) {
-        const int s = p & (RING - 1);
-        const bool normal = p >= 0 && p != r && !(p >= r - LA && p < r);  // W0's steps: no live tile, no ring slot
-        const int hi = r > p ? jmax + 1 : nT;  // live tiles j in (p, hi); W0 holds the rest up to r
-        int fq = -1;
-        d4 g = zero4(), flv = zero4();
-        bool have = false;  // flv: the pivot record of step fq, loaded with the look-ahead's G
-        if (p == -1) {
-            if (w == 0 && 0 <= jmax) fq = 0;
-        } else if (p == r) {  // the import: A_rj^T = G_j L_r^T for j > r (G_j of step r from owner j)
-            bool any = false;
-#pragma unroll
-            for (int k = 0; k < TPW; ++k) any |= w + NUW * k > r && w + NUW * k < nT;
-            if (any) {
-                if (!lds_wait(&S.lready, 1, S)) return false;
-                d4 lf;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) lf[e] = S.Lf[e][lane];
-                if (!wait_bulk<TPW>(a, p, w, r, nT, lane, S)) return false;
-                bulk_update<TPW, true>(a, rs, p, w, r, nT, lf, lane, tget, tset);
-            }
-            if ((r + 1) % NUW == w && r + 1 < nT) fq = r + 1;
-        } else if (normal) {
-            if (!lds_wait(&S.gready[s], p + 1, S)) return false;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) g[e] = S.GL[s][e][lane];
-            lds_release();
-            lds_add(&S.gdone[s], 1);
-            if ((p + 1) % NUW == w && p + 1 < hi) {  // this wave forms G_r of step p + 1: its tile first
-                // G_p+1,p from its granules (owner p + 1's W0 writes them
-                // first): one round trip, no flag then payload
-                // and the pivot record P_p+1 in the same round of loads
-                const int k1 = (p + 1) / NUW;
-                u32x4 x[GPAIRS], v[4];
-                long long t0 = -1;
-                for (unsigned it = 1;; ++it) {
-                    asm volatile("" ::: "memory");  // every pass reloads
-                    const __amdgpu_buffer_rsrc_t rg = rsrc(rs.G), rp = rsrc(rs.P);
-                    const int go = __builtin_amdgcn_readfirstlane(gsoff(a, p, p + 1));
-                    const int po = __builtin_amdgcn_readfirstlane((p + 1) * PBYTES);
-#pragma unroll
-                    for (int k = 0; k < GPAIRS; ++k) x[k] = __builtin_amdgcn_raw_buffer_load_b128(rg, k * 1024 + lane * 16, go, SC1);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b128(rp, k * 1024 + lane * 16, po, SC1);
-                    bool ok = true;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) ok &= x[k].y == a.tag && x[k].w == a.tag && v[k].y == a.tag && v[k].w == a.tag;
-                    if (__all(ok)) break;
-                    __builtin_amdgcn_s_sleep(1);
-                    if (it % 64 == 0 && give_up(S, it, t0)) return false;
-                }
-                const d4 gj = -dec4(x);
-#pragma unroll
-                for (int k = 0; k < TPW; ++k)  // constant slot indices: the tiles stay in registers
-                    if (k == k1) tset(k, mfma4(tget(k), gj, g));
-                fq = p + 1;
-                flv = dec4(v);
-                have = true;
-            }
-        }
-        if (fq >= 0 && !form_g(fq, have, flv)) return false;
-        if (normal) {
-            const int lo = fq == p + 1 ? p + 1 : p;
-            if (!wait_bulk<TPW>(a, p, w, lo, hi, lane, S)) return false;
-            bulk_update<TPW, false>(a, rs, p, w, lo, hi, g, lane, tget, tset);
-            if (w == 0) stamp(a, p, DBG_UDONE);
-        }
-    }
     return true;
 }
 
-// ------------------------------------------------------ the pivot workgroup
-// (PWG, round 6) Block nT runs EVERY pivot, so no pivot-to-pivot hop crosses
-// a workgroup boundary.  Owner q ships its window (A_q,q-LA .. A_qq, b_q
-// through step q - LA - 1) LA steps ahead; this workgroup applies those LA
-// steps itself:
-//  * waves 2..LA (the look-ahead stages), window q: W_q from owner q (rows
-//    0..LA: the payload, nothing has touched them); stage D applies step
-//    q - D, G_q,s = L_s^-1 A_q,s with the G_j,s of the earlier rows kept in
-//    LDS (Gr), and hands the rest to stage D - 1: each step's part runs as
-//    soon as L_s is out, so the window is current through q - 2 right after
-//    wave C's G_q-1,q-2 (measured, round 6: one wave for all LA steps took
-//    ~2.2 us a window, and wave C waited ~1 us a pivot);
-//  * wave C (the chain), step q: G_q,q-1 = L_{q-1}^-1 A_q,q-1, A_qq -= G G^T,
-//    b_q -= G y_{q-1}, the chain, P_q out; L_q^-1, y_q and G_q,q-1 to wave A;
-//  * wave B: the L_q fragment record for owner q (its import).
-// Nothing the owners need from here but P_q and that record: each owner forms
-// its own G_r of the last LA steps (w0_loop_pwg), so the owners' progress is
-// one hop behind the pivot records and never waits on this workgroup's G.
-// The operations and their order per tile are the owner-only layout's (the
-// same MFMA calls on the same operands), so the solve is bitwise the same.
-constexpr int GR = LA + 1;  // rows of G_j,j-d (d = 1..LA) kept for wave A
-constexpr int PR = 8;  // L_q^-1 / y_q kept for the stages (read up to window q + LA)
-// the window of row q between the stages: stage D (2 < D <= LA) hands the
-// D tiles A_q,q-D+1 .. A_qq (and b_q) to stage D - 1; offsets of those
-// double-buffered links in PSm.Lk
-__host__ __device__ constexpr int lk_off(int D) {  // doubles before the link into stage D - 1
-    int o = 0;
-    for (int d = 3; d < D; ++d) o += 2 * (d * 256 + 16);
-    return o;
-}
-struct PSm {
-    double Wm[2][4][64], Wd[2][4][64], Wb[2][16];  // stage 2 -> C (A_q,q-1, A_qq, b_q through step q - 2)
-    double Lk[lk_off(LA + 1)];                      // stage D -> D - 1, D = 3 .. LA
-    double Pl[PR][4][64], Py[PR][16];               // L_q^-1 fragment, y_q
-    double Gr[GR][LA][4][64];                       // Gr[j % GR][d - 1] = G_j,j-d
-    double Lrow[2][TL][TL + 1];                     // the L_q rows for wave B (its fragment for owner q)
-    int win_ready, win_done, pl_ready, gc_ready, lf_ready, b_done;
-    int wm_ready, wd_ready;  // the window's A_q,q-1 (look-ahead wave 3) and A_qq, b_q (wave 0) for wave C
-    int lk_ready[LA + 1], lk_done[LA + 1], grdy[LA + 1];  // link into stage d - 1; G_q,q-d of stage d ready
-};
-static_assert(sizeof(PSm) <= DYN_LDS, "pivot workgroup LDS");
-static_assert(LA >= 2 && LA <= PR && GR >= LA + 1 && 3 + LA <= NW, "stage waves, ring depths");
-
-__device__ __forceinline__ d4 lds4(const double (&t)[4][64], int lane) {
-    return d4{t[0][lane], t[1][lane], t[2][lane], t[3][lane]};
-}
-__device__ __forceinline__ void sto4(double (&t)[4][64], int lane, const d4 &v) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) t[e][lane] = v[e];
-}
-
-__device__ __forceinline__ bool pw_chain(const Args &a, const Rs &rs, Smem &S, PSm &P, int lane) {
-    const int nT = a.nT, li = lane & 15;
-    d4 lvp = zero4();
-    double yp = 0.0;
-    for (int q = 0; q < nT; ++q) {
-        const int s2 = q & 1;
-        if (!lds_wait(&P.wm_ready, q + 1, S) || !lds_wait(&P.wd_ready, q + 1, S)) return false;
-        stamp(a, q, PW_WIN);
-        d4 Tm = lds4(P.Wm[s2], lane), Td = lds4(P.Wd[s2], lane);
-        double b = P.Wb[s2][li];
-        lds_release();
-        lds_set(&P.win_done, q + 1);
-        if (q > 0) {
-            const d4 g = mfma4(zero4(), lvp, Tm);
-            sto4(P.Gr[q % GR][0], lane, g);  // the previous content was read by windows up to q - 2
-            lds_release();
-            lds_set(&P.gc_ready, q + 1);
-            stamp(a, q, PW_GPUB);
-            Td = mfma4(Td, -g, g);
-            b -= gy(g, yp, lane);
-        }
-        double rw[16], yr;
-        d4 lv;
-        pivot_core(a, S, q, lane, Td, b, rw, lv, yr, PW_CH0, PW_CH1);
-        put4(rs.P, q * PBYTES, a.tag, lv, lane);
-        put_pair(rs.P, q * PBYTES, 4, a.tag, yr, lane);
-        stamp(a, q, PW_PPUB);
-        sto4(P.Pl[q % PR], lane, lv);  // L_{q-PR}^-1 was read by windows up to q - PR + LA < q
-        if (lane < 16) P.Py[q % PR][lane] = yr;
-        lds_release();
-        lds_set(&P.pl_ready, q + 1);
-        if (!lds_wait(&P.b_done, q - 1, S)) return false;  // wave B read the rows of q - 2
-        if (lane < 16)  // the rows only: wave B forms the fragment, off this wave's path
-#pragma unroll
-            for (int j = 0; j < 16; ++j) P.Lrow[s2][lane][j] = j <= lane ? rw[j] : 0.0;
-        lds_release();
-        lds_set(&P.lf_ready, q + 1);
-        lvp = lv;
-        yp = yr;
-    }
-    return true;
-}
-
-// a stage of the look-ahead: steps q - DHI .. q - DLO of row q's window
-// (2 <= DLO <= DHI <= LA).  The window comes in through step q - DHI - 1
-// (from owner q's record for DHI = LA, else from the stage before), each step
-// s = q - d forms G_q,s = L_s^-1 A_q,s (the G of the rows between from LDS,
-// Gr), and the rest goes to the next stage (or wave C for DLO = 2).  Two
-// stages, steps q - LA .. q - 3 and step q - 2: a window's early steps need
-// only pivots long out, and the last one waits for wave C's G_q-1,q-2 alone.
-// Measured (round 6): one wave for all LA steps took ~2.2 us a window at
-// LA = 3 and wave C waited ~1 us a pivot; one wave a step (LA = 4) paid the
-// hand-offs between the stages (a window ~4.9 us).
-template <int DHI, int DLO>
-__device__ __forceinline__ bool pw_stage(const Args &a, const Rs &rs, Smem &S, PSm &P, int lane, double lambda) {
-    const int nT = a.nT, li = lane & 15;
-    for (int q = 0; q < nT; ++q) {
-        const int s2 = q & 1, s0 = q - DHI;
-        d4 T[DHI + 1];  // A_q,q-DHI .. A_qq
-        double b;
-        if (DHI == LA) {
-            if (q <= LA) {  // untouched rows: straight from the payload, as their owner would load them
-#pragma unroll
-                for (int i = 0; i <= DHI; ++i) T[i] = s0 + i >= 0 ? load_tile(a, lambda, q, s0 + i, lane) : zero4();
-                b = assembled_b_src(a.src, a.payload, a.ns, TL * q + li);
-            } else {
-                const int soff[1] = {q * WBYTES};
-                const bool need[1] = {true};
-                u32x4 v[1][WPAIRS];
-                if (!sweep<1, WPAIRS>(rs.W, soff, need, a.tag, v, lane, S)) return false;
-#pragma unroll
-                for (int i = 0; i <= DHI; ++i)
-                    T[i] = d4{dec(v[0][4 * i]), dec(v[0][4 * i + 1]), dec(v[0][4 * i + 2]), dec(v[0][4 * i + 3])};
-                b = dec(v[0][4 * WT]);
-            }
-            stamp(a, q, PW_AWIN);
-        } else {
-            if (!lds_wait(&P.lk_ready[DHI + 1], q + 1, S)) return false;
-            const double *lk = P.Lk + lk_off(DHI + 1) + s2 * ((DHI + 1) * 256 + 16);
-#pragma unroll
-            for (int i = 0; i <= DHI; ++i) T[i] = d4{lk[i * 256 + lane], lk[i * 256 + 64 + lane], lk[i * 256 + 128 + lane],
-                                                    lk[i * 256 + 192 + lane]};
-            b = lk[(DHI + 1) * 256 + li];
-            lds_release();
-            lds_set(&P.lk_done[DHI + 1], q + 1);
-            stamp(a, q, PW_LIN);
-        }
-#pragma unroll
-        for (int d = DHI; d >= DLO; --d) {
-            const int s = q - d, t = DHI - d;  // step s; T[t] is A_q,s
-            if (s < 0) continue;
-            // every wait of the step first, then the LDS reads, then the MFMA
-            // chains: a wait is a loop the compiler cannot move work across,
-            // so waits between the tiles' updates had serialised their
-            // dependent MFMA chains (round 6 stamps: ~0.3 us an update)
-            if (!lds_wait(&P.pl_ready, s + 1, S)) return false;
-#pragma unroll
-            for (int i = 1; i < d; ++i)  // G_j,s of the rows between, j = s + i (distance i; wave C's for i = 1)
-                if (!lds_wait(i == 1 ? &P.gc_ready : &P.grdy[i], s + i + 1, S)) return false;
-            const d4 lv = lds4(P.Pl[s % PR], lane);
-            const double ys = P.Py[s % PR][li];
-            d4 gj[DHI];
-#pragma unroll
-            for (int i = 1; i < d; ++i) gj[i] = -lds4(P.Gr[(s + i) % GR][i - 1], lane);
-            const d4 g = mfma4(zero4(), lv, T[t]);
-            sto4(P.Gr[q % GR][d - 1], lane, g);
-            lds_release();
-            lds_set(&P.grdy[d], q + 1);
-#pragma unroll
-            for (int i = 1; i < d; ++i) T[t + i] = mfma4(T[t + i], gj[i], g);
-            T[DHI] = mfma4(T[DHI], -g, g);
-            b -= gy(g, ys, lane);
-            stamp(a, q, PW_STEP + d);  // step q - d done (slots 11 .. 10 + LA)
-        }
-        constexpr int t0 = DHI - DLO + 1;  // the tiles left: T[t0 .. DHI], DLO of them
-        if (DLO == 2) {
-            if (!lds_wait(&P.win_done, q - 1, S)) return false;  // wave C read window q - 2 (the slot)
-            sto4(P.Wm[s2], lane, T[t0]);
-            sto4(P.Wd[s2], lane, T[t0 + 1]);
-            if (lane < 16) P.Wb[s2][lane] = b;
-            lds_release();
-            lds_set(&P.win_ready, q + 1);
-            stamp(a, q, PW_AOUT);
-        } else {
-            if (!lds_wait(&P.lk_done[DLO], q - 1, S)) return false;  // the next stage read window q - 2 (the slot)
-            double *lk = P.Lk + lk_off(DLO) + s2 * (DLO * 256 + 16);
-#pragma unroll
-            for (int i = 0; i < DLO; ++i) {
-                lk[i * 256 + lane] = T[t0 + i][0];
-                lk[i * 256 + 64 + lane] = T[t0 + i][1];
-                lk[i * 256 + 128 + lane] = T[t0 + i][2];
-                lk[i * 256 + 192 + lane] = T[t0 + i][3];
-            }
-            if (lane < 16) lk[DLO * 256 + lane] = b;
-            lds_release();
-            lds_set(&P.lk_ready[DLO], q + 1);
-        }
-    }
-    return true;
-}
-
-// The look-ahead, tile-parallel (round 6): four waves share row q's window,
-// wave K holding tile A_q,q-LA+K (wave 0 also A_qq and b_q).  Step s = q - d
-// (d = LA .. 2) has its pivot tile t = LA - d: that tile's wave forms
-// G_q,s = L_s^-1 A_q,s into Gr, and every wave updates its later tiles with
-// it (A_q,j -= G_j,s G_q,s^T, G_j,s of row j from Gr or wave C), so a step's
-// MFMA work runs on four SIMDs and its critical path is the pivot tile's G,
-// one LDS hand-off and the next tile's update.  Measured and not kept (same
-// round): one wave for every step (a window ~2.2 us at LA = 3, ~4.3 us at
-// LA = 4 through two stage waves): wave C waited for the window each pivot.
-template <int K>
-__device__ __forceinline__ bool pw_look(const Args &a, const Rs &rs, Smem &S, PSm &P, int lane, double lambda) {
-    static_assert(LA == 4, "tile i of the window on look-ahead wave i % 4");
-    const int nT = a.nT, li = lane & 15;
-    for (int q = 0; q < nT; ++q) {
-        const int s2 = q & 1, lo = q - LA;
-        d4 Ta = zero4(), Tb = zero4();  // tile K; wave 0: tile LA (A_qq) too
-        double b = 0.0;
-        if (lo <= 0) {  // untouched rows: straight from the payload, as their owner would load them
-            if (lo + K >= 0) Ta = load_tile(a, lambda, q, lo + K, lane);
-            if (K == 0) {
-                Tb = load_tile(a, lambda, q, q, lane);
-                b = assembled_b_src(a.src, a.payload, a.ns, TL * q + li);
-            }
-        } else {
-            {
-                const int soff[1] = {q * WBYTES + 4 * K * 1024};
-                const bool need[1] = {true};
-                u32x4 v[1][4];
-                if (!sweep<1, 4>(rs.W, soff, need, a.tag, v, lane, S)) return false;
-                Ta = dec4(v[0]);
-            }
-            if (K == 0) {
-                const int soff[1] = {q * WBYTES + 4 * LA * 1024};
-                const bool need[1] = {true};
-                u32x4 v[1][5];
-                if (!sweep<1, 5>(rs.W, soff, need, a.tag, v, lane, S)) return false;
-                Tb = d4{dec(v[0][0]), dec(v[0][1]), dec(v[0][2]), dec(v[0][3])};
-                b = dec(v[0][4]);
-            }
-        }
-        if (K == 0) stamp(a, q, PW_AWIN);
-#pragma unroll
-        for (int d = LA; d >= 2; --d) {
-            const int s = q - d, t = LA - d;  // step s, pivot tile t
-            if (s < 0) continue;
-            d4 g;
-            if (t == K) {  // this wave's tile is the step's pivot tile
-                if (!lds_wait(&P.pl_ready, s + 1, S)) return false;
-                g = mfma4(zero4(), lds4(P.Pl[s % PR], lane), Ta);
-                sto4(P.Gr[q % GR][d - 1], lane, g);
-                lds_release();
-                lds_set(&P.grdy[d], q + 1);
-            }
-            const bool upA = K > t, upB = K == 0;
-            if (!upA && !upB) continue;
-            if (t != K) {  // the pivot tile's G (another wave's)
-                if (!lds_wait(&P.grdy[d], q + 1, S)) return false;
-                g = lds4(P.Gr[q % GR][d - 1], lane);
-            }
-            if (upA) {  // A_q,j, j = s + (K - t): G_j,s of row j (distance K - t; wave C's for 1)
-                const int e = K - t, j = s + e;
-                if (!lds_wait(e == 1 ? &P.gc_ready : &P.grdy[e], j + 1, S)) return false;
-                Ta = mfma4(Ta, -lds4(P.Gr[j % GR][e - 1], lane), g);
-            }
-            if (upB) {  // A_qq and b_q
-                if (!lds_wait(&P.pl_ready, s + 1, S)) return false;
-                const double ys = P.Py[s % PR][li];
-                Tb = mfma4(Tb, -g, g);
-                b -= gy(g, ys, lane);
-            }
-            if (K == 0) stamp(a, q, PW_STEP + d);
-        }
-        if (K == LA - 1 || K == 0) {  // the window through step q - 2 for wave C
-            if (!lds_wait(&P.win_done, q - 1, S)) return false;  // wave C read window q - 2 (the slot)
-            if (K == LA - 1) {
-                sto4(P.Wm[s2], lane, Ta);
-                lds_release();
-                lds_set(&P.wm_ready, q + 1);
-            } else {
-                sto4(P.Wd[s2], lane, Tb);
-                if (lane < 16) P.Wb[s2][lane] = b;
-                lds_release();
-                lds_set(&P.wd_ready, q + 1);
-                stamp(a, q, PW_AOUT);
-            }
-        }
-    }
-    return true;
-}
-
-__device__ __forceinline__ bool pw_pub(const Args &a, const Rs &rs, Smem &S, PSm &P, int lane) {
-    const int nT = a.nT;
-    for (int q = 0; q < nT; ++q) {
-        if (!lds_wait(&P.lf_ready, q + 1, S)) return false;
-        d4 lf;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) lf[e] = P.Lrow[q & 1][lane & 15][4 * e + (lane >> 4)];  // L_q(l & 15, 4e + (l >> 4))
-        lds_release();
-        lds_set(&P.b_done, q + 1);
-        put4(rs.Lr, q * LBYTES, a.tag, lf, lane);
-        stamp(a, q, PW_BPUB);
-    }
-    return true;
-}
-
-template <int TR, int TLS, bool PWG>
+template <int TR, int TLS>
 __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
     if (a.gate && !*a.gate) return;  // device-side LM control: iteration gated off
     __shared__ Smem S;
@@ -1325,43 +725,20 @@ __global__ void __launch_bounds__(THREADS) k_gjr_solve(Args a) {
     stamp(a, a.nT, DBG_START);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = row_of(blockIdx.x, a.nT);
     const double lambda = *a.lam;
-    const bool pwg = PWG && (int)blockIdx.x == a.nT;  // the pivot workgroup
-    PSm &PS = *reinterpret_cast<PSm *>(dyn);
-    if (threadIdx.x < RING)
-        S.pready[threadIdx.x] = S.pdone[threadIdx.x] = S.gready[threadIdx.x] = S.gdone[threadIdx.x] = S.hgready[threadIdx.x] = 0;
+    if (threadIdx.x < RING) S.pready[threadIdx.x] = S.pdone[threadIdx.x] = S.gready[threadIdx.x] = S.gdone[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
-        S.lready = S.abort_ = S.last = S.w0done = 0;
+        S.lready = S.abort_ = S.last = 0;
         S.err = a.err;
         S.bad = a.bad;
-        if (pwg) PS.win_ready = PS.win_done = PS.pl_ready = PS.gc_ready = PS.lf_ready = PS.b_done = PS.wm_ready =
-            PS.wd_ready = 0;
-    }
-    if (pwg && threadIdx.x <= LA) {
-        PS.lk_ready[threadIdx.x] = PS.lk_done[threadIdx.x] = PS.grdy[threadIdx.x] = 0;
     }
     Rs rs;
     rs.P = Buf{a.P, 2 * a.nT * PBYTES};
     rs.G = Buf{a.G, a.nT * a.nT * GBYTES};
     rs.Gd = Buf{a.Gd, a.nT * a.nT * GDBYTES};
-    rs.W = Buf{a.W, a.nT * WBYTES};
-    rs.Lr = Buf{a.Lr, a.nT * LBYTES};
     __syncthreads();
     const int wu = __builtin_amdgcn_readfirstlane(wave);  // provably uniform: scalar record offsets
-    if (pwg) {  // no arrival: the owners' x is the result
-        if (wu == 0) pw_chain(a, rs, S, PS, lane);
-        else if (wu == 1) pw_pub(a, rs, S, PS, lane);
-        else if (wu == 2) pw_look<0>(a, rs, S, PS, lane, lambda);
-        else if (wu == 3) pw_look<1>(a, rs, S, PS, lane, lambda);
-        else if (wu == 4) pw_look<2>(a, rs, S, PS, lane, lambda);
-        else if (wu == 5) pw_look<3>(a, rs, S, PS, lane, lambda);
-        return;
-    }
-    if (wu == 0) {
-        if (PWG) w0_loop_pwg(a, rs, S, r, lane, lambda);
-        else w0_loop(a, rs, S, r, lane, lambda);
-    } else {
-        u_loop<TR, TLS, PWG>(a, rs, S, r, wu - 1, lane, lambda, dyn + (wu - 1) * TLS * 256);
-    }
+    if (wu == 0) w0_loop(a, rs, S, r, lane, lambda);
+    else u_loop<TR, TLS>(a, rs, S, r, wu - 1, lane, lambda, dyn + (wu - 1) * TLS * 256);
     // every owner arrives (an aborted one too, so the count stays whole); the
     // last one forms the trial cameras unless the solve failed
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // W0's x stores drained before the barrier

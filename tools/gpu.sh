@@ -6,8 +6,8 @@
 # gpurun_out/<out> (default: <what>).
 #   tests     the -m gpu suite, then smoke()
 #   bench     bench.py (N = 1, defaults)
-#   solve     the reduced solve: A/B of the pivot workgroup (gj_ab.py) and its
-#             per-pivot timeline at n = 1200 and 300 (gjp_timeline.py)
+#   solve     the reduced solve's per-pivot timeline (gjr_timeline.py, n = 1200
+#             and 300) and the BA kernel split with it and the Cholesky (gj_ab.py)
 #   e2e       the drop-in perform_bundle_adjustment at cfg4 and cfg5, with
 #             sfm_ba_create's host phases (SFM_CREATE_TIMING=1)
 #   profile   tools/profile_round.sh (bench, rocprofv3 kernel stats, PMC passes)
@@ -24,9 +24,9 @@ bench)
   timeout -k 10 900 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 1
   tail -c 600 $OUT/bench.json ;;
 solve)
-  timeout -k 10 300 python -u tools/gj_ab.py SFM_GJR_PWG 0,1 3 > $OUT/ab.txt 2>&1 || exit 1
-  timeout -k 10 120 python -u tools/gjp_timeline.py 1200 3 ${3:-10,40,70} > $OUT/tl1200.txt 2>&1 || exit 1
-  timeout -k 10 60 python -u tools/gjp_timeline.py 300 > $OUT/tl300.txt 2>&1 || exit 1
+  timeout -k 10 300 python -u tools/gj_ab.py SFM_SOLVE gj,chol 3 > $OUT/ab.txt 2>&1 || exit 1
+  timeout -k 10 120 python -u tools/gjr_timeline.py 1200 > $OUT/tl1200.txt 2>&1 || exit 1
+  timeout -k 10 60 python -u tools/gjr_timeline.py 300 > $OUT/tl300.txt 2>&1 || exit 1
   tail -4 $OUT/ab.txt ;;
 e2e)
   for C in cfg4 cfg5; do
