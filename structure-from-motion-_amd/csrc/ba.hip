@@ -1062,7 +1062,6 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
         return;
     }
     if (gate && !*gate) return;  // device-side LM control: iteration gated off
-    if (dbg & 8) return;         // timing probe: the launch without the sweep
     uint32_t *ldsw = reinterpret_cast<uint32_t *>(sw_lds);
     // the work item: a whole (spec, range), or a chunk sub-range of a split one
     int w, r, q0, q1;
@@ -1112,7 +1111,7 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     const bool diag = grp.flags & 1, second = grp.flags & 2;
     const int bw = L.words();
     double *scam = reinterpret_cast<double *>(ldsw + 2 * bw);  // the spec's cameras (rows 0 and 1)
-    // chunk hand-off counters (dbg bit 16 clear): filled[b] += 1 per producer
+    // chunk hand-off counters: filled[b] += 1 per producer
     // wave (two stagers, nload loaders) once its part of a chunk is in buffer
     // b; freed[b] += 1 per pair wave once it is done with the chunk in b.
     // Instead of a workgroup barrier per chunk, a pair wave waits only for
@@ -1120,7 +1119,6 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     // freed, so the per-chunk spread between the lane groups (Poisson pair
     // counts) averages out over the chunks instead of adding up chunk by chunk
     int *cnt = reinterpret_cast<int *>(scam + 24);  // filled[2] | freed[2] | abort
-    const bool csync = !(dbg & 16);
     if (t < 5) cnt[t] = 0;
     if (t < 24) {
         const int c = spec_cam[2 * w + t / 12];
@@ -1157,7 +1155,7 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
             // word 0: the (chunk, spec)'s slot count; the entries follow
             // (padded to list_cap > buf_slots: every load is in bounds)
             const uint32_t *lst = list + ((int64_t)qs * nspec + w) * L.list_cap;
-            n = (dbg & 4) ? 0 : (int)lst[0];
+            n = (int)lst[0];
 #pragma unroll
             for (int u = 0; u < SB; ++u) {
                 const int sl = tst + u * SSTEP;
@@ -1209,7 +1207,7 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
         load_pts(e1);
         __syncthreads();  // the cameras are in LDS
         if (q0 < q1) commit(e1, n1, ldsw);
-        if (csync) sw_signal(&cnt[0]);
+        sw_signal(&cnt[0]);
         auto advance = [&]() {  // chunk q+2's points and chunk q+3's list in flight
             load_pts(e2);
 #pragma unroll
@@ -1219,14 +1217,13 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
         advance();
         load_list(q0 + 2, e2, n2);
         stamp(1);
-        if (!csync) lds_barrier();
         for (int q = q0; q < q1; ++q) {
             if (q + 1 < q1) {
                 const int b1 = ((q - q0) & 1) ^ 1;
                 // buffer b1 held chunk q - 1: every pair wave done with it
-                if (!csync || sw_wait(&cnt[2 + b1], ((q + 1 - q0) >> 1) * SW_PAIR_WAVES, &cnt[4], sw_err)) {
+                if (sw_wait(&cnt[2 + b1], ((q + 1 - q0) >> 1) * SW_PAIR_WAVES, &cnt[4], sw_err)) {
                     commit(e1, n1, ldsw + b1 * bw);
-                    if (csync) sw_signal(&cnt[b1]);
+                    sw_signal(&cnt[b1]);
                 }
             }
             if (q + 2 < q1) {
@@ -1234,9 +1231,8 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
                 load_list(q + 3, e2, n2);
             }
             stamp(2 + q - q0);
-            if (!csync) lds_barrier();
         }
-        if (csync) lds_barrier();  // every pair wave is done with the buffers sweep_reduce reuses
+        lds_barrier();  // every pair wave is done with the buffers sweep_reduce reuses
         const double none[NACC] = {};  // no accumulators: output tasks only
         sweep_reduce<LPP>(none, false, t, ng, groups + spec_goff[w], slab_out, reinterpret_cast<double *>(sw_lds),
                           sub);
@@ -1253,30 +1249,26 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     __syncthreads();  // the cameras are in LDS
     stamp(1);
     const int nprod = SW_STAGE_WAVES + nload;  // producer waves of a chunk
-    if (csync) {
-        if (loader && q0 < q1) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA of chunk q0's pairs and header
-            sw_signal(&cnt[0]);
-        }
-    } else {
-        __syncthreads();  // chunk q0's slots are staged
+    if (loader && q0 < q1) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA of chunk q0's pairs and header
+        sw_signal(&cnt[0]);
     }
     for (int q = q0; q < q1; ++q) {
         const int cur = (q - q0) & 1;
         const uint32_t *bufw = ldsw + cur * bw;
         if (loader && q + 1 < q1) {
             // buffer cur ^ 1 held chunk q - 1: every pair wave done with it
-            if (!csync || sw_wait(&cnt[2 + (cur ^ 1)], ((q + 1 - q0) >> 1) * SW_PAIR_WAVES, &cnt[4], sw_err))
+            if (sw_wait(&cnt[2 + (cur ^ 1)], ((q + 1 - q0) >> 1) * SW_PAIR_WAVES, &cnt[4], sw_err))
                 sweep_fetch(t, nload, (int64_t)(q + 1) * nspec + w, L, pairs, hdr, ldsw + (cur ^ 1) * bw);
         }
-        const bool have = !csync || sw_wait(&cnt[cur], (((q - q0) >> 1) + 1) * nprod, &cnt[4], sw_err);
+        const bool have = sw_wait(&cnt[cur], (((q - q0) >> 1) + 1) * nprod, &cnt[4], sw_err);
         if (gi >= 0 && have) {
             const double2 *buf = reinterpret_cast<const double2 *>(bufw);
             const uint32_t *pl = bufw + L.buf_slots * 2 * SLOT_D;
             const int32_t *hd = reinterpret_cast<const int32_t *>(pl + L.pair_cap / 2);
             const int n0 = hd[ng + 1], n1 = hd[ng + 2];
             if (diag) {  // S_ii: the camera's own observations, b = a; plus sum Z_a q_p
-                const int a0 = second ? n0 : 0, a1 = (dbg & 2) ? a0 : second ? n0 + n1 : n0;
+                const int a0 = second ? n0 : 0, a1 = second ? n0 + n1 : n0;
                 for (int a = a0 + slot; a < a1; a += nslot) {
                     const double2 *sl = buf + a * (SLOT_D / 2);
                     double pa[3], Fa[3][3], x[3], pm[3], Aa[2][3], ara[2][3];
@@ -1289,7 +1281,7 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
                     diag_gq<LPP>(h, pa, gq, acc);
                 }
             } else {
-                const int k0 = hd[gi], k1 = (dbg & 1) ? k0 : hd[gi + 1];
+                const int k0 = hd[gi], k1 = hd[gi + 1];
                 const uint16_t *pl16 = reinterpret_cast<const uint16_t *>(pl);
                 for (int k = k0 + slot; k < k1; k += nslot) {
                     const double2 *sl = buf + (int)pl16[k] * (SLOT_D / 2);
@@ -1301,19 +1293,16 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
                 }
             }
         }
-        if (csync) {
-            if (loader && q + 1 < q1) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk q + 1's DMA, overlapped with chunk q
-                sw_signal(&cnt[cur ^ 1]);
-            }
-            sw_signal(&cnt[2 + cur]);
+        if (loader && q + 1 < q1) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk q + 1's DMA, overlapped with chunk q
+            sw_signal(&cnt[cur ^ 1]);
         }
+        sw_signal(&cnt[2 + cur]);
         stamp(2 + q - q0);
-        if (!csync) __syncthreads();  // chunk q's buffer is free; chunk q+1's slots, pairs and header have landed
     }
     // reduce the groups' slots in slot order through LDS (the staging
     // buffers are free now)
-    if (csync) lds_barrier();
+    lds_barrier();
     sweep_reduce<LPP>(acc, gi >= 0, t, ng, groups + spec_goff[w], slab_out, reinterpret_cast<double *>(sw_lds), sub);
     stamp(SW_STAMP_EV - 1);
 }
@@ -2117,11 +2106,11 @@ __global__ void k_lm_step(const LMState *__restrict__ lm_in, LMState *__restrict
 
 // Lanes per point for the grouped per-point kernels (1, 2, 4 or 8; an
 // environment override is read once, for tuning).
-static int lanes_per_point(const char *env, int dflt) {
-    const char *v = std::getenv(env);
-    const int g = v ? std::atoi(v) : dflt;
-    return (g == 1 || g == 2 || g == 4 || g == 8) ? g : dflt;
-}
+// lanes per point of the point kernels (the measured choices; the round-2..5
+// switches SFM_*_LANES, SFM_BACKSUB_THREADS / _BLOCKS are retired)
+constexpr int LIN_CL_LANES = 2;  // k_linearize_cl (cameras in LDS)
+constexpr int LIN_LANES = 4;     // k_linearize (global cameras: more nc than the LDS stage holds)
+constexpr int BS_LANES = 2;      // k_backsub_trial
 
 // Factor + forward solve (nT launches of k_chol_col) and backward solve of
 // the padded reduced camera system with tiles of tb (16 or 32) columns; A, b
@@ -2152,17 +2141,11 @@ static int launch_cholesky(const double *payload, int32_t ns, const double *lam,
                     : launch_cholesky_t<16>(payload, ns, lam, A, nsp, b, D, bad, s, gate, ct, src, dpp);
 }
 
-// Cholesky tile width (env SFM_CHOL_TILE = 32 for experiments).  Measured
-// on MI355X at ns = 300: 16 -> 0.167 ms, 32 -> 0.267 ms; each launch is bound
-// by its column's serial factor + TRSM chain, which grows as tb^2, not by the
-// launch count.
-static int chol_tile(int64_t) {
-    if (const char *e = std::getenv("SFM_CHOL_TILE")) {
-        const int v = std::atoi(e);
-        if (v == 16 || v == 32) return v;
-    }
-    return 16;
-}
+// Cholesky tile width 16.  Measured on MI355X at ns = 300: 16 -> 0.167 ms,
+// 32 -> 0.267 ms (round 2; the 32 variant and its switch are retired): each
+// launch is bound by its column's serial factor + TRSM chain, which grows as
+// tb^2, not by the launch count.
+static int chol_tile(int64_t) { return 16; }
 
 // S + lambda diag(clamp(diag U)) x = b from the Schur payload (assembled by the
 // tiled Cholesky); x -> b.
@@ -2195,10 +2178,7 @@ static GjPlan gj_plan(int nT, int ncu) {
         if (std::strcmp(e, "chol") == 0) return g;
     if (nT > gj::NTMAX) return g;
     const int nseg = (nT + gj::SR - 1) / gj::SR;
-    const char *fe = std::getenv("SFM_GJ_CB");  // tuning / tests: force the column-block width
-    const int force = fe ? std::atoi(fe) : 0;
     for (int cb : {gj::SR, 2 * gj::SR}) {
-        if (force && cb != force) continue;
         const int ncb = (nT + cb - 1) / cb;
         if (ncb * nseg <= ncu) {
             g.cb = cb;
@@ -2636,7 +2616,8 @@ static int env_int(const char *name, int dflt) {
 // k_backsub_trial's grid when the cameras fit its LDS stage: the resident
 // workgroup count for that LDS size (every workgroup starts at once), at most
 // the partial-sum slots; 0 selects the global-camera kernel
-static int backsub_cl_blocks(int32_t nc, int ncu, int max_blocks, int nt) {
+static int backsub_cl_blocks(int32_t nc, int ncu, int max_blocks) {
+    constexpr int nt = 256;
     if (env_int("SFM_BACKSUB_CAM_LDS", 1) == 0) return 0;
     const size_t lds = (size_t)8 * BS_CAM * nc;
     if (nc < 1 || lds > (size_t)BS_CAM_LDS_MAX) return 0;
@@ -2647,23 +2628,7 @@ static int backsub_cl_blocks(int32_t nc, int ncu, int max_blocks, int nt) {
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, nt, lds) != hipSuccess)
             nb = 0;
     };
-    // the instantiation the launch picks
-    const int g = lanes_per_point("SFM_BACKSUB_LANES", 2);
-    if (nt == 256) {
-        switch (g) {
-        case 1: occ(k_backsub_trial<1, true, 256>); break;
-        case 2: occ(k_backsub_trial<2, true, 256>); break;
-        case 4: occ(k_backsub_trial<4, true, 256>); break;
-        default: occ(k_backsub_trial<8, true, 256>); break;
-        }
-    } else {
-        switch (g) {
-        case 1: occ(k_backsub_trial<1, true>); break;
-        case 2: occ(k_backsub_trial<2, true>); break;
-        case 4: occ(k_backsub_trial<4, true>); break;
-        default: occ(k_backsub_trial<8, true>); break;
-        }
-    }
+    occ(k_backsub_trial<BS_LANES, true, 256>);  // the instantiation the launch picks
     (void)hipGetLastError();
     if (nb < 1) return 0;
     return std::max(1, std::min(nb * ncu, max_blocks));
@@ -2682,12 +2647,7 @@ static int linearize_cl_blocks(int32_t nc, int ncu, int max_blocks) {
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, LIN_CL_THREADS, lds) != hipSuccess)
             nb = 0;
     };
-    switch (lanes_per_point("SFM_LINEARIZE_LANES", 2)) {
-    case 1: occ(k_linearize_cl<1>); break;
-    case 2: occ(k_linearize_cl<2>); break;
-    case 4: occ(k_linearize_cl<4>); break;
-    default: occ(k_linearize_cl<8>); break;
-    }
+    occ(k_linearize_cl<LIN_CL_LANES>);
     (void)hipGetLastError();
     if (nb < 1) return 0;
     return std::max(1, std::min(nb * ncu, max_blocks));
@@ -3096,13 +3056,19 @@ static inline int sweep_trips(int P, int s) { return (P + s - 1) / s; }
 static int64_t sweep_alloc(const std::vector<std::vector<uint16_t>> &P, const std::vector<int> &dtrip, int budget,
                            std::vector<int> &slots) {
     const int ng = (int)P.size(), nq = (int)dtrip.size();
+    // sum over chunks of the largest trip count; group-major, the division
+    // ceil(P / s) as a multiply by the 32-bit reciprocal (exact: (P + s - 1)
+    // s < 2^32 for 16-bit P and s <= SW_THREADS), so the chunk loop vectorises
+    std::vector<int> mx(nq);
     auto objective = [&](const std::vector<int> &sl) {
-        int64_t f = 0;
-        for (int q = 0; q < nq; ++q) {
-            int m = dtrip[q];
-            for (int g = 0; g < ng; ++g) m = std::max(m, sweep_trips(P[g][q], sl[g]));
-            f += m;
+        mx.assign(dtrip.begin(), dtrip.end());
+        for (int g = 0; g < ng; ++g) {
+            const uint64_t s = (uint64_t)sl[g], m = (((uint64_t)1 << 32) + s - 1) / s;
+            const uint16_t *pg = P[g].data();
+            for (int q = 0; q < nq; ++q) mx[q] = std::max(mx[q], (int)(((uint64_t)pg[q] + s - 1) * m >> 32));
         }
+        int64_t f = 0;
+        for (int v : mx) f += v;
         return f;
     };
     // proportional split (the round-2/3 planner): floor shares, then the
@@ -3131,20 +3097,44 @@ static int64_t sweep_alloc(const std::vector<std::vector<uint16_t>> &P, const st
         prop[best] += 1;
         sum += 1;
     }
-    // greedy on the soft max
+    // greedy on the soft max.  A group's gain depends on its per-chunk pair
+    // counts only through their histogram: the distinct counts (descending)
+    // with their multiplicities, so a gain costs the distinct counts above s
+    // instead of every chunk (cfg5: ~100 chunks, ~15 distinct counts; the
+    // greedy was 2 of the 9 ms of the cfg5 create)
     auto pw = [](int t) { const double x = t; return x * x * x * x * x * x; };
+    std::vector<std::vector<std::pair<int, int>>> hist(ng);
+    {
+        std::vector<int> c;  // a counting pass (a sort per group cost more than the greedy)
+        for (int g = 0; g < ng; ++g) {
+            int top = 0;
+            for (int q = 0; q < nq; ++q) top = std::max(top, (int)P[g][q]);
+            c.assign(top + 1, 0);
+            for (int q = 0; q < nq; ++q) c[P[g][q]]++;
+            for (int v = top; v > 1; --v)  // counts <= 1 never gain
+                if (c[v]) hist[g].push_back({v, c[v]});
+        }
+    }
     auto gain = [&](int g, int s) {
         double d = 0;
-        for (int q = 0; q < nq; ++q) d += pw(sweep_trips(P[g][q], s)) - pw(sweep_trips(P[g][q], s + 1));
+        for (const auto &hm : hist[g]) {
+            if (hm.first <= s) break;  // one trip at s and s + 1 from here down
+            d += hm.second * (pw(sweep_trips(hm.first, s)) - pw(sweep_trips(hm.first, s + 1)));
+        }
         return d;
     };
+    // a heap of (gain, -group): the largest gain, the lowest group on ties
+    // (max_element's choice); only the chosen group's gain changes
     std::vector<int> gr(ng, 1);
-    std::vector<double> gn(ng);
-    for (int g = 0; g < ng; ++g) gn[g] = gain(g, 1);
+    std::vector<std::pair<double, int>> heap(ng);
+    for (int g = 0; g < ng; ++g) heap[g] = {gain(g, 1), -g};
+    std::make_heap(heap.begin(), heap.end());
     for (int used = ng; used < budget; ++used) {
-        const int g = (int)(std::max_element(gn.begin(), gn.end()) - gn.begin());
+        std::pop_heap(heap.begin(), heap.end());
+        const int g = -heap.back().second;
         gr[g] += 1;
-        gn[g] = gain(g, gr[g]);
+        heap.back() = {gain(g, gr[g]), -g};
+        std::push_heap(heap.begin(), heap.end());
     }
     const int64_t fp = objective(prop), fg = ng <= budget ? objective(gr) : INT64_MAX;
     slots = fg < fp ? gr : prop;
@@ -3171,7 +3161,7 @@ struct PhaseTimer {
 // first) and is emptied for a device whose hipMalloc fails.  Every buffer a
 // kernel reads before writing is memset or uploaded in create, so a reused
 // block's old contents are never read: SFM_POOL_POISON=1 fills reused blocks
-// with 0xFF (the tests' check of that claim), SFM_POOL=0 turns the cache off.
+// with 0xFF (the tests' check of that claim).
 struct DevBlockCache {
     struct Blk {
         int dev;
@@ -3187,10 +3177,7 @@ static DevBlockCache &dev_cache() {
     static auto *c = new DevBlockCache();
     return *c;
 }
-static bool pool_on() {
-    static const bool v = env_int("SFM_POOL", 1) != 0;
-    return v;
-}
+static constexpr bool pool_on() { return true; }  // (the SFM_POOL=0 switch is retired, round 6)
 static void pool_trim(int dev) {  // every cached block of dev back to the driver
     DevBlockCache &c = dev_cache();
     std::lock_guard<std::mutex> lk(c.mu);
@@ -3398,7 +3385,7 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     // chunks as large as the LDS allows (every chunk boundary is a barrier
     // and an imbalance point): from the 16-bit cap down, scaled by the
     // overshoot until the largest (chunk, spec) fits
-    int chunk_obs = std::max(64, std::min(env_int("SFM_SWEEP_CHUNK", 65535), 65535));
+    int chunk_obs = 65535;
     std::vector<int64_t> cut;  // chunk first points
     int32_t *d_spec_of = nullptr, *d_scam = nullptr;  // device planner: the spec tables
     for (;;) {
@@ -3413,9 +3400,18 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
         for (int r = 0; r < P.nrange && ok; ++r) {
             const int64_t oend = no * (r + 1) / P.nrange;
             while (pcur < np_ && pstart[pcur] < oend) {  // one chunk
+                // the chunk's end: the first point at or after oend, or the
+                // first whose observations would overflow chunk_obs (the
+                // first point always goes in); pstart is monotone, so two
+                // binary searches instead of a walk over the points
                 const int32_t o0 = pstart[pcur];
-                int64_t pe = pcur;
-                while (pe < np_ && pstart[pe] < oend && (pe == pcur || pstart[pe + 1] - o0 <= chunk_obs)) ++pe;
+                const int32_t *ps = pstart.data();
+                const int64_t a = std::lower_bound(ps + pcur + 1, ps + np_, (int32_t)std::min<int64_t>(oend, INT32_MAX)) - ps;
+                const int64_t lim = (int64_t)o0 + chunk_obs;
+                const int64_t j = pcur + 2 <= np_ ? std::upper_bound(ps + pcur + 2, ps + np_ + 1,
+                                                                     (int32_t)std::min<int64_t>(lim, INT32_MAX)) - ps
+                                                  : np_ + 1;
+                const int64_t pe = std::min({a, j - 1, np_});
                 if (pstart[pe] - o0 > 65535) { ok = false; break; }
                 cut.push_back(pcur);
                 cend.push_back(pe);
@@ -3544,11 +3540,11 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     });
     pt_.tick("plan:counts");
     // slots per group, then lanes: diagonal groups first (the loader
-    // waves), then the off-diagonal groups by size.  SFM_SWEEP_ALLOC=0 keeps
-    // the proportional split, SFM_SWEEP_POW2=1 the power-of-two sizes.
+    // waves), then the off-diagonal groups by size.  The proportional split
+    // remains for a spec with more groups than slots (the greedy needs one
+    // slot per group); its power-of-two variant is retired (round 6).
     P.lanegrp.assign((size_t)P.nspec * SW_THREADS, (int16_t)-1);
     std::vector<std::vector<int>> gid_of(P.nspec);  // (row, j - j0) -> group index within spec
-    const bool pow2 = env_int("SFM_SWEEP_POW2", 0) != 0, exact = env_int("SFM_SWEEP_ALLOC", 1) != 0;
     int64_t f_plan = 0, f_ideal = 0;
     // the slot allocation of every spec (independent: host threads), then the
     // lane layout in spec order
@@ -3565,20 +3561,15 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
         for (size_t k = 0; k < g.size(); ++k)
             Pg[k].assign(bq.begin() + (size_t)g[k].blk * P.nchunk, bq.begin() + (size_t)(g[k].blk + 1) * P.nchunk);
         std::vector<int> &sl = sl_of[w];
-        if (exact && !pow2 && !g.empty() && (int)g.size() <= budget) {
+        if (!g.empty() && (int)g.size() <= budget) {
             fplan_w[w] = sweep_alloc(Pg, dtrip, budget, sl);
-        } else {  // proportional (power-of-two sizes with SFM_SWEEP_POW2)
+        } else {  // proportional
             double tot = 0;
             for (auto &x : g) tot += x.work;
             sl.assign(g.size(), 1);
             int sum = 0;
             for (size_t k = 0; k < g.size(); ++k) {
                 sl[k] = std::max(1, (int)(tot > 0 ? g[k].work / tot * budget : 1.0));
-                if (pow2) {
-                    int v = 1;
-                    while (v * 2 <= sl[k] && v < 32) v *= 2;
-                    sl[k] = v;
-                }
                 sum += sl[k];
             }
             while (sum > budget) {
@@ -3586,7 +3577,7 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
                 *it -= 1;
                 sum -= 1;
             }
-            while (!pow2 && sum < budget && !g.empty()) {
+            while (sum < budget && !g.empty()) {
                 size_t best = 0;
                 for (size_t k = 1; k < g.size(); ++k)
                     if (g[k].work * sl[best] > g[best].work * sl[k]) best = k;
@@ -3745,7 +3736,7 @@ struct sfm_ba_problem {
     int32_t cl_fused_wg = 0, cl_fused_items = 0;  // k_schur_sweep's camera workgroups / their items
     bool cl_fused = false;                         // this solve: camera blocks inside the sweep launch
     bool chol_dpp = true, fin_fused = true;        // this solve: DPP tile factor; finish folded into the solve
-    int sw_debug = 0;                              // SFM_SWEEP_DEBUG (read once per solve)
+    int sw_debug = 0;                              // k_schur_sweep dbg argument: 0 (the work-skipping probes are retired)
     // Schur sweep plan (k_schur_sweep): ranges, chunks, specs
     int32_t sw_nrange = 0, sw_nspec = 0, sw_nbd = 0, sw_nchunk = 0;
     SweepSplit sw_split = {};
@@ -3785,7 +3776,6 @@ struct sfm_ba_problem {
     int64_t payload_len = 0;
     int pt_blocks = 0;
     int bs_cl_blocks = 0;  // k_backsub_trial with the cameras in LDS: its grid (0: cameras from global)
-    int bs_threads = PT_THREADS;  // and its workgroup size
     int lin_cl_blocks = 0;        // k_linearize_cl's grid (0: k_linearize, cameras from global)
     hipEvent_t ev[2 * T_NT] = {};
     hipEvent_t ev_it[2 * T_NT * kEvSlots] = {};  // per-iteration timing slots of a batch
@@ -3899,7 +3889,8 @@ static int upload_state(sfm_ba_problem *p) {
         for (int i = 0; i < 3; ++i) Rt[12 * c + 9 + i] = p->cams0[6 * c + 3 + i];
     }
     SFM_HIP(hipMemcpyAsync(p->d_Rt, Rt.data(), Rt.size() * 8, hipMemcpyHostToDevice, p->stream));
-    SFM_HIP(hipMemcpyAsync(p->d_X, p->pts0.data(), p->pts0.size() * 8, hipMemcpyHostToDevice, p->stream));
+    if (!p->pts0.empty())  // a one-shot problem's points went up in create
+        SFM_HIP(hipMemcpyAsync(p->d_X, p->pts0.data(), p->pts0.size() * 8, hipMemcpyHostToDevice, p->stream));
     SFM_HIP(hipStreamSynchronize(p->stream));
     return 0;
 }
@@ -3971,6 +3962,9 @@ extern "C" int sfm_comm_destroy(sfm_comm *c) {
 namespace sfm {
 bool dense_obs_info(void *handle, int64_t *n, int64_t *n_rows, int32_t *n_cams);  // dense_obs.cpp
 void dense_obs_copy(void *handle, int32_t *cam, int32_t *pt, double *obs);
+int dense_obs_pieces(void *handle, std::vector<int64_t> &off);
+void dense_obs_copy_pieces(void *handle, const std::vector<int64_t> &off, int t0, int t1, int32_t *cam, int32_t *pt,
+                           double *obs);
 }  // namespace sfm
 
 // sfm_ba_create; with `dense` (a sfm_dense_obs_scan handle) the
@@ -3978,7 +3972,7 @@ void dense_obs_copy(void *handle, int32_t *cam, int32_t *pt, double *obs);
 // upload buffer (cam / pt / obs are then null): no COO arrays in between
 static int ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const int32_t *pt, const double *obs,
                      void *dense, const double *K, const double *cams, const double *pts, int device, sfm_comm *comm,
-                     sfm_ba_problem **out) {
+                     sfm_ba_problem **out, bool oneshot = false) {
     SFM_CHECK_ARG(out && K && cams && (pts || np_ == 0) && (no == 0 || dense || (cam && pt && obs)), "null pointer");
     SFM_CHECK_ARG(nc >= 1 && np_ >= 0 && no >= 0, "bad sizes");
     SFM_CHECK_ARG(no < ((int64_t)1 << 31), "problem too large for int32 indexing");
@@ -4017,7 +4011,12 @@ static int ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, co
     p->sw_pinhole = K[1] == 0.0 && K[3] == 0.0 && K[6] == 0.0 && K[7] == 0.0 && K[8] == 1.0 &&
                     env_int("SFM_SWEEP_PINHOLE", 1) != 0;
     p->cams0.assign(cams, cams + 6 * (size_t)nc);
-    p->pts0.assign(pts, pts + 3 * (size_t)np_);
+    // x0's points are kept for sfm_ba_reset; a one-shot problem (sfm_ba_lm*:
+    // created, solved and destroyed in one call) uploads them from the
+    // caller's array through the pinned stage instead (cfg5: the 12-MB copy
+    // and a pageable upload, ~1 ms of the call)
+    if (!oneshot) p->pts0.assign(pts, pts + 3 * (size_t)np_);
+    bool x_up = false;
     // SFM_CREATE_PLAN_ONLY=1 (measurement, tools/create_probe.py): the host
     // planner alone, without a device; returns 1 and no problem.
     // SFM_PLAN_HOST=1: the host's CSR, counts and planner passes (the device
@@ -4043,7 +4042,7 @@ static int ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, co
         ctick("stream");
         if ((rc = p->alloc(p->d_cam, no)) || (rc = p->alloc(p->d_pt, no)) || (rc = p->alloc(p->d_pstart, np_ + 1)) ||
             (rc = p->alloc(p->d_obs, no)) || (rc = p->alloc(p->d_cm_pt, no)) || (rc = p->alloc(p->d_cm_obs, no)) ||
-            (rc = p->alloc(p->d_cstart, nc + 1)))
+            (rc = p->alloc(p->d_cstart, nc + 1)) || (rc = p->alloc(p->d_X, 3 * np_)))
             return rc;
     }
     // the COO up through a pinned staging buffer kept across calls (host
@@ -4065,7 +4064,7 @@ static int ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, co
     if (!plan_only && no) {
         PinnedStage &st = pinned_stage();
         stage_lk = std::unique_lock<std::mutex>(st.mu, std::try_to_lock);
-        const size_t need = (size_t)no * 24;
+        const size_t xoff = (size_t)no * 24, need = xoff + (oneshot ? (size_t)np_ * 24 : 0);
         bool staged = false;
         if (stage_lk.owns_lock()) {
             if (st.bytes < need) {
@@ -4076,26 +4075,54 @@ static int ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, co
                 else (void)hipGetLastError();
             }
             if (st.bytes >= need) {
+                // in batches: the copy engine takes batch b while the host
+                // threads fill batch b + 1 (cfg5: 96 MB, the host copy ~1.1 ms
+                // and the transfer ~1.9 ms had run back to back)
                 char *h = static_cast<char *>(st.p);
+                int32_t *hc = reinterpret_cast<int32_t *>(h), *hp = reinterpret_cast<int32_t *>(h + (size_t)no * 4);
+                double *ho = reinterpret_cast<double *>(h + (size_t)no * 8);
+                auto dma = [&](int64_t o0, int64_t o1) -> int {
+                    if (o1 <= o0) return 0;
+                    SFM_HIP(hipMemcpyAsync(p->d_cam + o0, hc + o0, (o1 - o0) * 4, hipMemcpyHostToDevice, p->stream));
+                    SFM_HIP(hipMemcpyAsync(p->d_pt + o0, hp + o0, (o1 - o0) * 4, hipMemcpyHostToDevice, p->stream));
+                    SFM_HIP(hipMemcpyAsync(p->d_obs + o0, ho + 2 * o0, (o1 - o0) * 16, hipMemcpyHostToDevice, p->stream));
+                    return 0;
+                };
+                constexpr int NBATCH = 4;
                 if (dense) {
-                    dense_obs_copy(dense, reinterpret_cast<int32_t *>(h), reinterpret_cast<int32_t *>(h + (size_t)no * 4),
-                                   reinterpret_cast<double *>(h + (size_t)no * 8));
-                    cam = reinterpret_cast<const int32_t *>(h);
-                    pt = reinterpret_cast<const int32_t *>(h + (size_t)no * 4);
-                    obs = reinterpret_cast<const double *>(h + (size_t)no * 8);
+                    std::vector<int64_t> off;
+                    const int npc = dense_obs_pieces(dense, off);
+                    for (int b = 0; b < NBATCH; ++b) {
+                        const int t0 = npc * b / NBATCH, t1 = npc * (b + 1) / NBATCH;
+                        dense_obs_copy_pieces(dense, off, t0, t1, hc, hp, ho);
+                        if ((rc = dma(off[t0], off[t1]))) return rc;
+                    }
+                    cam = hc;
+                    pt = hp;
+                    obs = ho;
                 } else {
                     constexpr int NB = 16;
-                    par_for(3 * NB, [&](int64_t k) {
-                        const int a = (int)(k / NB), t = (int)(k % NB);
-                        const size_t w = a == 2 ? 16 : 4, n0 = no * t / NB, n1 = no * (t + 1) / NB;
-                        const char *src = a == 0 ? (const char *)cam : a == 1 ? (const char *)pt : (const char *)obs;
-                        char *dst = h + (a == 0 ? 0 : a == 1 ? (size_t)no * 4 : (size_t)no * 8);
-                        std::memcpy(dst + n0 * w, src + n0 * w, (n1 - n0) * w);
-                    });
+                    for (int b = 0; b < NBATCH; ++b) {
+                        const int64_t b0 = no * b / NBATCH, b1 = no * (b + 1) / NBATCH;
+                        par_for(3 * NB, [&](int64_t k) {
+                            const int a = (int)(k / NB), t = (int)(k % NB);
+                            const size_t w = a == 2 ? 16 : 4, n0 = b0 + (b1 - b0) * t / NB, n1 = b0 + (b1 - b0) * (t + 1) / NB;
+                            const char *src = a == 0 ? (const char *)cam : a == 1 ? (const char *)pt : (const char *)obs;
+                            char *dst = a == 0 ? (char *)hc : a == 1 ? (char *)hp : (char *)ho;
+                            std::memcpy(dst + n0 * w, src + n0 * w, (n1 - n0) * w);
+                        });
+                        if ((rc = dma(b0, b1))) return rc;
+                    }
                 }
-                SFM_HIP(hipMemcpyAsync(p->d_cam, h, no * 4, hipMemcpyHostToDevice, p->stream));
-                SFM_HIP(hipMemcpyAsync(p->d_pt, h + (size_t)no * 4, no * 4, hipMemcpyHostToDevice, p->stream));
-                SFM_HIP(hipMemcpyAsync(p->d_obs, h + (size_t)no * 8, no * 16, hipMemcpyHostToDevice, p->stream));
+                if (oneshot && np_) {
+                    constexpr int NB = 16;
+                    par_for(NB, [&](int64_t t) {
+                        const size_t n0 = 3 * (size_t)np_ * t / NB, n1 = 3 * (size_t)np_ * (t + 1) / NB;
+                        std::memcpy(h + xoff + n0 * 8, pts + n0, (n1 - n0) * 8);
+                    });
+                    SFM_HIP(hipMemcpyAsync(p->d_X, h + xoff, (size_t)np_ * 24, hipMemcpyHostToDevice, p->stream));
+                    x_up = true;
+                }
                 staged = true;
             }
         }
@@ -4115,6 +4142,10 @@ static int ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, co
             SFM_HIP(hipMemcpyAsync(p->d_obs, obs, no * 16, hipMemcpyHostToDevice, p->stream));
         }
         ctick("up:obs");
+    }
+    if (oneshot && !plan_only && !x_up && np_) {
+        SFM_HIP(hipMemcpyAsync(p->d_X, pts, (size_t)np_ * 24, hipMemcpyHostToDevice, p->stream));
+        SFM_HIP(hipStreamSynchronize(p->stream));  // pts is the caller's: copied before create returns
     }
     if (host_plan) {  // host threads
         constexpr int NBC = 16;
@@ -4286,14 +4317,14 @@ static int ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, co
     // camera-major list cut into equal contiguous ranges (one per workgroup:
     // as many as the CUs the sweep leaves idle), each cut again at camera
     // boundaries
-    const int cam_chunk = std::max(64, env_int("SFM_CAM_CHUNK", CAM_CHUNK));
+    const int cam_chunk = CAM_CHUNK;
     const int busy = sw.split_S ? NXCD * (sw.split_w0 + sw.split_n * sw.split_S) : sw.nspec * sw.nrange,
               idle = (256 - busy % 256) % 256;
     // the camera workgroups take the CUs the sweep's last round leaves idle;
     // when the dispatch tail is split there are none, and a full round of
     // them (256) beats a short one behind the split round
     p->cl_fused_wg = (int32_t)std::min<int64_t>(std::max<int64_t>(1, ceil_div(no, SW_THREADS)),
-                                                env_int("SFM_CAMLIN_WG", sw.split_S ? 256 : idle >= 32 ? idle : 64));
+                                                sw.split_S ? 256 : idle >= 32 ? idle : 64);
     CamPlan csa, cfu;
     {
         std::vector<int32_t> cuts;
@@ -4364,7 +4395,7 @@ static int ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, co
         (rc = p->alloc(p->d_camlin, (int64_t)CAMLIN * nc)) ||
         (rc = p->alloc(p->d_slab2, (int64_t)CAMLIN * std::max<int64_t>(1, std::max(p->ndiag_items, p->cl_fused_items)))) ||
         (rc = p->alloc(p->d_Rt, 12 * (int64_t)nc)) || (rc = p->alloc(p->d_Rt2, 12 * (int64_t)nc)) ||
-        (rc = p->alloc(p->d_X, 3 * np_)) || (rc = p->alloc(p->d_X2, 3 * np_)) ||
+        (rc = p->alloc(p->d_X2, 3 * np_)) ||
         (rc = p->alloc(p->d_Vg, 9 * np_)) || (rc = p->alloc(p->d_Lq, 9 * np_)) ||
         (rc = p->alloc(p->d_sw_scam, sw.spec_cam.size())) || (rc = p->alloc(p->d_payload, p->payload_len + 8)) ||
         (rc = p->alloc(p->d_A, (int64_t)p->nsp * p->nsp)) || (rc = p->alloc(p->d_b, p->nsp)) ||
@@ -4376,8 +4407,7 @@ static int ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, co
         return rc;
     p->gjrp = p->tb == 16 ? gjr_plan(p->nT, device_cus(device)) : GjrPlan{};
     p->gjp = p->tb == 16 && !p->gjrp.ok() ? gj_plan(p->nT, device_cus(device)) : GjPlan{};
-    p->bs_threads = env_int("SFM_BACKSUB_THREADS", 256) == 256 ? 256 : PT_THREADS;
-    p->bs_cl_blocks = backsub_cl_blocks(nc, device_cus(device), p->pt_blocks, p->bs_threads);
+    p->bs_cl_blocks = backsub_cl_blocks(nc, device_cus(device), p->pt_blocks);
     p->lin_cl_blocks = linearize_cl_blocks(nc, device_cus(device), p->pt_blocks);
     if (p->gjrp.ok()) {
         gjr::u64 *gw = nullptr;
@@ -4717,14 +4747,10 @@ static int run_linearize(sfm_ba_problem *p, int par, int want_cost) {
     const int *glin = &p->d_lm[par].run_lin;
 
     if (p->lin_cl_blocks > 0) {  // the cameras in LDS
-        const int gc = lanes_per_point("SFM_LINEARIZE_LANES", 2);
-        const int nb = std::max(1, std::min(ceil_div(p->np * gc, LIN_CL_THREADS), p->lin_cl_blocks));
-#define SFM_LINC(G)                                                                                               \
-    hipLaunchKernelGGL(k_linearize_cl<G>, dim3(nb), dim3(LIN_CL_THREADS), (size_t)8 * LIN_CAM * p->nc, s, p->np, p->nc,     \
-                       p->d_pstart, p->d_cam, p->d_obs, p->K, p->d_Rt, p->d_X, p->d_Vg, p->d_partial, p->d_count,  \
-                       p->d_scal + 8, want_cost, glin, p->gtol, p->d_nbig)
-        switch (gc) { case 1: SFM_LINC(1); break; case 2: SFM_LINC(2); break; case 4: SFM_LINC(4); break; default: SFM_LINC(8); }
-#undef SFM_LINC
+        const int nb = std::max(1, std::min(ceil_div(p->np * LIN_CL_LANES, LIN_CL_THREADS), p->lin_cl_blocks));
+        hipLaunchKernelGGL(k_linearize_cl<LIN_CL_LANES>, dim3(nb), dim3(LIN_CL_THREADS), (size_t)8 * LIN_CAM * p->nc, s,
+                           p->np, p->nc, p->d_pstart, p->d_cam, p->d_obs, p->K, p->d_Rt, p->d_X, p->d_Vg, p->d_partial,
+                           p->d_count, p->d_scal + 8, want_cost, glin, p->gtol, p->d_nbig);
         SFM_HIP(hipGetLastError());
         if (p->ndiag_items && !p->cl_fused) {
             const CamLinArgs cl = camlin_args(p, false, glin);
@@ -4733,14 +4759,10 @@ static int run_linearize(sfm_ba_problem *p, int par, int want_cost) {
         }
         return want_cost ? allreduce(p, p->d_scal + 8, 1) : 0;
     }
-    const int gl = lanes_per_point("SFM_LINEARIZE_LANES", 4);
-    const int nbl = std::max(1, ceil_div(p->np * gl, PT_THREADS));
-#define SFM_LIN(G)                                                                                                \
-    hipLaunchKernelGGL(k_linearize<G>, dim3(nbl), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam, p->d_obs, \
-                       p->K, p->d_Rt, p->d_X, p->d_Vg, p->d_partial, p->d_count, p->d_scal + 8, want_cost, glin, \
-                       p->gtol, p->d_nbig)
-    switch (gl) { case 1: SFM_LIN(1); break; case 2: SFM_LIN(2); break; case 4: SFM_LIN(4); break; default: SFM_LIN(8); }
-#undef SFM_LIN
+    const int nbl = std::max(1, ceil_div(p->np * LIN_LANES, PT_THREADS));
+    hipLaunchKernelGGL(k_linearize<LIN_LANES>, dim3(nbl), dim3(PT_THREADS), 0, s, p->np, p->d_pstart, p->d_cam,
+                       p->d_obs, p->K, p->d_Rt, p->d_X, p->d_Vg, p->d_partial, p->d_count, p->d_scal + 8, want_cost,
+                       glin, p->gtol, p->d_nbig);
     SFM_HIP(hipGetLastError());
     if (p->ndiag_items && !p->cl_fused) {
         const CamLinArgs cl = camlin_args(p, false, glin);
@@ -4821,22 +4843,18 @@ static int run_step(sfm_ba_problem *p, hipEvent_t *ev, int par) {
         return rc;
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_SOLVE + 1], s));
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_TRIAL], s));
-    const int gb = lanes_per_point("SFM_BACKSUB_LANES", 2);
     // grid-stride: 1024 workgroups (4 per CU); measured at cfg4 (1563 needed
     // without the stride): 512 -> 49 us, 896..1152 -> 43 us, 2048+ -> 51 us
     // with the cameras in LDS: as many workgroups as are resident at once
     // (a grid-stride kernel whose last workgroups start late ends late)
     const bool cl = p->bs_cl_blocks > 0;
-    const int nbb = std::max(1, std::min(ceil_div(p->np * gb, cl ? p->bs_threads : PT_THREADS),
-                                         env_int("SFM_BACKSUB_BLOCKS", cl ? p->bs_cl_blocks : 1024)));
+    const int bst = cl ? 256 : PT_THREADS;
+    const int nbb = std::max(1, std::min(ceil_div(p->np * BS_LANES, bst), cl ? p->bs_cl_blocks : 1024));
     const size_t cl_lds = cl ? (size_t)8 * BS_CAM * p->nc : 0;
-#define SFM_BS(G)                                                                                                  \
-    hipLaunchKernelGGL((!cl ? k_backsub_trial<G, false> : p->bs_threads == 256 ? k_backsub_trial<G, true, 256>      \
-                                                                              : k_backsub_trial<G, true>),        \
-                       dim3(nbb), dim3(cl ? p->bs_threads : PT_THREADS), cl_lds, s, p->np, p->nc, p->d_pstart, p->d_cam, p->d_obs, p->K, p->d_Vg, p->d_Lq, p->d_b,  \
-                       lam, p->d_Rt, p->d_Rt2, p->d_X, p->d_X2, p->d_partial, p->d_count + GS_WORDS, p->d_scal, gst)
-    switch (gb) { case 1: SFM_BS(1); break; case 2: SFM_BS(2); break; case 4: SFM_BS(4); break; default: SFM_BS(8); }
-#undef SFM_BS
+    hipLaunchKernelGGL((cl ? k_backsub_trial<BS_LANES, true, 256> : k_backsub_trial<BS_LANES, false>), dim3(nbb),
+                       dim3(bst), cl_lds, s, p->np, p->nc, p->d_pstart, p->d_cam, p->d_obs, p->K, p->d_Vg, p->d_Lq,
+                       p->d_b, lam, p->d_Rt, p->d_Rt2, p->d_X, p->d_X2, p->d_partial, p->d_count + GS_WORDS, p->d_scal,
+                       gst);
     SFM_HIP(hipGetLastError());
     if ((rc = allreduce(p, p->d_scal, 4))) return rc;
     if (timed) SFM_HIP(hipEventRecord(ev[2 * T_TRIAL + 1], s));
@@ -4884,7 +4902,6 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
     p->chol_dpp = env_int("SFM_CHOL_DPP", 1) != 0;
     p->fin_fused = env_int("SFM_FINISH_FUSED", 1) != 0;
     p->gjr_fold = env_int("SFM_GJR_FOLD", 0) != 0;
-    p->sw_debug = env_int("SFM_SWEEP_DEBUG", 0) | (env_int("SFM_SWEEP_SYNC", 1) ? 0 : 16);
     (void)hipGetLastError();
     const auto t0 = std::chrono::steady_clock::now();
     for (double &t : p->t_acc) t = 0;
@@ -4895,9 +4912,8 @@ extern "C" int sfm_ba_solve(sfm_ba_problem *p, const sfm_ba_opts *o, sfm_ba_repo
     // iteration it - depth (pinned ring, no stream sync), so at most depth
     // gated-off iterations follow the one that ends the solve, and the device
     // always has the next iteration queued.
-    int depth = 2;
-    if (const char *e = std::getenv("SFM_LM_DEPTH")) depth = std::atoi(e);
-    depth = std::min(std::max(depth, 1), kHostRing - 1);
+    constexpr int depth = 2;
+    static_assert(depth >= 1 && depth < kHostRing, "the host ring holds the iterations in flight");
     const bool timed = p->timing;
     for (int k = 0; k < kHostRing; ++k) __atomic_store_n(&p->h_ring[k].seq, 0, __ATOMIC_RELAXED);
     hipLaunchKernelGGL(k_lm_reset, dim3(1), dim3(1), 0, s, p->d_lm, o->initial_lambda, p->d_bad);
@@ -5137,7 +5153,7 @@ static int ba_lm(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, const 
     SFM_CHECK_ARG(o && cams, "null pointer");
     const auto t0 = std::chrono::steady_clock::now();
     sfm_ba_problem *p = nullptr;
-    int rc = ba_create(nc, np_, no, cam, pt, obs, dense, K, cams, pts, device, nullptr, &p);
+    int rc = ba_create(nc, np_, no, cam, pt, obs, dense, K, cams, pts, device, nullptr, &p, true);
     if (rc) return rc;
     const auto t1 = std::chrono::steady_clock::now();
     rc = sfm_ba_solve(p, o, rep);

@@ -187,18 +187,32 @@ bool dense_obs_info(void *handle, int64_t *n, int64_t *n_rows, int32_t *n_cams) 
     return true;
 }
 
-void dense_obs_copy(void *handle, int32_t *cam, int32_t *pt, double *obs) {
+int dense_obs_pieces(void *handle, std::vector<int64_t> &off) {
     auto *h = static_cast<DenseObs *>(handle);
     const size_t np = h->pieces.size();
-    std::vector<int64_t> off(np + 1, 0);
+    off.assign(np + 1, 0);
     for (size_t t = 0; t < np; ++t) off[t + 1] = off[t] + h->pieces[t].n;
-    par_for((int64_t)np, [&](int64_t t) {
+    return (int)np;
+}
+
+// pieces [t0, t1) to their places in the concatenated arrays (off: dense_obs_pieces)
+void dense_obs_copy_pieces(void *handle, const std::vector<int64_t> &off, int t0, int t1, int32_t *cam, int32_t *pt,
+                           double *obs) {
+    auto *h = static_cast<DenseObs *>(handle);
+    par_for((int64_t)(t1 - t0), [&](int64_t k) {
+        const int64_t t = t0 + k;
         const Piece &p = h->pieces[t];
         if (!p.n) return;
         std::memcpy(cam + off[t], p.cam.data(), p.n * sizeof(int32_t));
         std::memcpy(pt + off[t], p.pt.data(), p.n * sizeof(int32_t));
         std::memcpy(obs + 2 * off[t], p.xy.data(), 2 * p.n * sizeof(double));
     });
+}
+
+void dense_obs_copy(void *handle, int32_t *cam, int32_t *pt, double *obs) {
+    std::vector<int64_t> off;
+    const int np = dense_obs_pieces(handle, off);
+    dense_obs_copy_pieces(handle, off, 0, np, cam, pt, obs);
 }
 
 }  // namespace sfm

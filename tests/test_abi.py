@@ -204,3 +204,34 @@ def test_ransac_wrong_shape_contract(case):
     random.seed(11)
     F2, idx2 = get_inliers_ransac(a, b, index, 0.06, n_max)
     assert F2 is None and idx2.shape == (0,) and idx2.dtype == np.float64
+
+
+@pytest.mark.parametrize("cfg", ["cfg3", "cfg4"])
+def test_sweep_planner_plan_only_is_deterministic(cfg, monkeypatch, capfd):
+    """sfm_ba_create's host planner without a device (SFM_CREATE_PLAN_ONLY=1:
+    the CSR, block counts, chunk cuts, slot allocation and (chunk, spec)
+    lists on host threads; returns 1 and no problem): two runs give the same
+    plan digest (the device planner's is checked against it on the GPU,
+    test_ba_device_plan_equals_host_plan)."""
+    import ctypes
+    import _sfmcore
+    import sfm_synthetic as syn
+    p = syn.ba_problem_cfg(cfg, dense=False)
+    nc, npt = p["n_cams"], p["n_pts"]
+    ci = np.ascontiguousarray(p["cam_idx"], np.int32)
+    pi = np.ascontiguousarray(p["pt_idx"], np.int32)
+    obs, K = np.ascontiguousarray(p["obs"]), np.ascontiguousarray(syn.K_REF, dtype=np.float64)
+    cams, X = np.zeros((nc, 6)), np.ascontiguousarray(p["X0"])
+    monkeypatch.setenv("SFM_CREATE_PLAN_ONLY", "1")
+    monkeypatch.setenv("SFM_PLAN_DIGEST", "1")
+    P, I32 = _sfmcore._p, _sfmcore._i32
+    digests = []
+    for _ in range(2):
+        out = ctypes.c_void_p()
+        rc = _sfmcore._lib.sfm_ba_create(nc, npt, len(ci), P(ci, I32), P(pi, I32), P(obs), P(K), P(cams), P(X), 0,
+                                         None, ctypes.byref(out))
+        assert rc == 1 and not out.value
+        m = re.findall(r"plan digest ([0-9a-f]{16})", capfd.readouterr().err)
+        assert len(m) == 1
+        digests.append(m[0])
+    assert digests[0] == digests[1]
