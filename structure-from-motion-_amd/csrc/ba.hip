@@ -2792,6 +2792,29 @@ struct PinnedStage {
     std::mutex mu;
     void *p = nullptr;
     size_t bytes = 0;
+    // a second stream per device, used only under mu: the coordinates (and a
+    // one-shot problem's points) go up on it while the CSR, the camera sort
+    // and the planner run on the problem's stream, which waits on `ev` only
+    // before the first kernel that reads them
+    struct Aux {
+        hipStream_t s = nullptr;
+        hipEvent_t ev = nullptr;
+    } aux[64];
+    Aux *aux_for(int dev) {
+        if (dev < 0 || dev >= 64) return nullptr;
+        Aux &a = aux[dev];
+        if (!a.s && hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking) != hipSuccess) {
+            (void)hipGetLastError();
+            a.s = nullptr;
+            return nullptr;
+        }
+        if (!a.ev && hipEventCreateWithFlags(&a.ev, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            a.ev = nullptr;
+            return nullptr;
+        }
+        return &a;
+    }
 };
 static PinnedStage &pinned_stage() {
     static PinnedStage *st = new PinnedStage();
@@ -4050,6 +4073,13 @@ static int ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, co
     // hipMemcpy of the 96 MB at cfg5 ran ~10 GB/s); a concurrent create
     // finding it busy uploads from pageable memory
     std::unique_lock<std::mutex> stage_lk;
+    hipEvent_t aux_ev = nullptr;  // the aux stream's uploads (the stage's coordinates and points)
+    struct AuxSync {  // on every return: the aux uploads drained before the stage and the buffers go
+        hipStream_t s = nullptr;
+        ~AuxSync() {
+            if (s) (void)hipStreamSynchronize(s);
+        }
+    } aux_sync;
     std::vector<int32_t> dense_cam, dense_pt;
     std::vector<double> dense_xy;
     if (dense && (plan_only || !no)) {  // no upload: the host arrays alone
@@ -4075,53 +4105,66 @@ static int ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, co
                 else (void)hipGetLastError();
             }
             if (st.bytes >= need) {
-                // in batches: the copy engine takes batch b while the host
-                // threads fill batch b + 1 (cfg5: 96 MB, the host copy ~1.1 ms
-                // and the transfer ~1.9 ms had run back to back)
+                // the point / camera indices first, on the problem's stream
+                // (the CSR and the planner need only them), then the
+                // coordinates in batches on the aux stream: the copy engine
+                // takes batch b while the host threads fill batch b + 1, and
+                // the device CSR runs meanwhile (cfg5: 96 MB had gone up
+                // before the CSR could start)
                 char *h = static_cast<char *>(st.p);
                 int32_t *hc = reinterpret_cast<int32_t *>(h), *hp = reinterpret_cast<int32_t *>(h + (size_t)no * 4);
                 double *ho = reinterpret_cast<double *>(h + (size_t)no * 8);
-                auto dma = [&](int64_t o0, int64_t o1) -> int {
-                    if (o1 <= o0) return 0;
-                    SFM_HIP(hipMemcpyAsync(p->d_cam + o0, hc + o0, (o1 - o0) * 4, hipMemcpyHostToDevice, p->stream));
-                    SFM_HIP(hipMemcpyAsync(p->d_pt + o0, hp + o0, (o1 - o0) * 4, hipMemcpyHostToDevice, p->stream));
-                    SFM_HIP(hipMemcpyAsync(p->d_obs + o0, ho + 2 * o0, (o1 - o0) * 16, hipMemcpyHostToDevice, p->stream));
-                    return 0;
-                };
-                constexpr int NBATCH = 4;
+                PinnedStage::Aux *ax = st.aux_for(device);
+                const hipStream_t xs = ax ? ax->s : p->stream;
+                aux_sync.s = ax ? ax->s : nullptr;
+                constexpr int NBATCH = 4, NB = 16;
+                std::vector<int64_t> off;
+                const int npc = dense ? dense_obs_pieces(dense, off) : 0;
                 if (dense) {
-                    std::vector<int64_t> off;
-                    const int npc = dense_obs_pieces(dense, off);
-                    for (int b = 0; b < NBATCH; ++b) {
+                    dense_obs_copy_pieces(dense, off, 0, npc, hc, hp, nullptr);
+                } else {
+                    par_for(2 * NB, [&](int64_t k) {
+                        const int a = (int)(k / NB), t = (int)(k % NB);
+                        const size_t n0 = no * t / NB, n1 = no * (t + 1) / NB;
+                        std::memcpy((a ? hp : hc) + n0, (a ? pt : cam) + n0, (n1 - n0) * 4);
+                    });
+                }
+                SFM_HIP(hipMemcpyAsync(p->d_cam, hc, no * 4, hipMemcpyHostToDevice, p->stream));
+                SFM_HIP(hipMemcpyAsync(p->d_pt, hp, no * 4, hipMemcpyHostToDevice, p->stream));
+                for (int b = 0; b < NBATCH; ++b) {
+                    int64_t o0, o1;
+                    if (dense) {
                         const int t0 = npc * b / NBATCH, t1 = npc * (b + 1) / NBATCH;
-                        dense_obs_copy_pieces(dense, off, t0, t1, hc, hp, ho);
-                        if ((rc = dma(off[t0], off[t1]))) return rc;
+                        dense_obs_copy_pieces(dense, off, t0, t1, nullptr, nullptr, ho);
+                        o0 = off[t0];
+                        o1 = off[t1];
+                    } else {
+                        o0 = no * b / NBATCH;
+                        o1 = no * (b + 1) / NBATCH;
+                        par_for(NB, [&](int64_t t) {
+                            const size_t n0 = o0 + (o1 - o0) * t / NB, n1 = o0 + (o1 - o0) * (t + 1) / NB;
+                            std::memcpy(ho + 2 * n0, obs + 2 * n0, (n1 - n0) * 16);
+                        });
                     }
+                    if (o1 > o0)
+                        SFM_HIP(hipMemcpyAsync(p->d_obs + o0, ho + 2 * o0, (o1 - o0) * 16, hipMemcpyHostToDevice, xs));
+                }
+                if (dense) {
                     cam = hc;
                     pt = hp;
                     obs = ho;
-                } else {
-                    constexpr int NB = 16;
-                    for (int b = 0; b < NBATCH; ++b) {
-                        const int64_t b0 = no * b / NBATCH, b1 = no * (b + 1) / NBATCH;
-                        par_for(3 * NB, [&](int64_t k) {
-                            const int a = (int)(k / NB), t = (int)(k % NB);
-                            const size_t w = a == 2 ? 16 : 4, n0 = b0 + (b1 - b0) * t / NB, n1 = b0 + (b1 - b0) * (t + 1) / NB;
-                            const char *src = a == 0 ? (const char *)cam : a == 1 ? (const char *)pt : (const char *)obs;
-                            char *dst = a == 0 ? (char *)hc : a == 1 ? (char *)hp : (char *)ho;
-                            std::memcpy(dst + n0 * w, src + n0 * w, (n1 - n0) * w);
-                        });
-                        if ((rc = dma(b0, b1))) return rc;
-                    }
                 }
                 if (oneshot && np_) {
-                    constexpr int NB = 16;
                     par_for(NB, [&](int64_t t) {
                         const size_t n0 = 3 * (size_t)np_ * t / NB, n1 = 3 * (size_t)np_ * (t + 1) / NB;
                         std::memcpy(h + xoff + n0 * 8, pts + n0, (n1 - n0) * 8);
                     });
-                    SFM_HIP(hipMemcpyAsync(p->d_X, h + xoff, (size_t)np_ * 24, hipMemcpyHostToDevice, p->stream));
+                    SFM_HIP(hipMemcpyAsync(p->d_X, h + xoff, (size_t)np_ * 24, hipMemcpyHostToDevice, xs));
                     x_up = true;
+                }
+                if (ax) {
+                    SFM_HIP(hipEventRecord(ax->ev, xs));
+                    aux_ev = ax->ev;
                 }
                 staged = true;
             }
@@ -4263,14 +4306,13 @@ static int ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, co
         }
         ctick("csr+blockcounts (device)");
     }
-    // the staged copies are done once the stream has passed them (a dense
-    // scan's observations live in the buffer, and plan_sweep may read them on
-    // the host whichever planner runs: kept until it returns)
-    if (stage_lk.owns_lock() && !dense) {
-        SFM_HIP(hipStreamSynchronize(p->stream));
-        stage_lk.unlock();
-    }
+    // the staged copies are done once the streams have passed them (a
+    // dense scan's observations live in the buffer, and plan_sweep may read
+    // them on the host whichever planner runs: kept until it returns; the
+    // aux stream's uploads are awaited by the problem's stream below)
     p->npairs = tot;
+    // the first reader of the coordinates (and, later, of the points)
+    if (aux_ev) SFM_HIP(hipStreamWaitEvent(p->stream, aux_ev, 0));
     if (!plan_only && no) {  // the camera-major copies gathered on the device (cm_pt: permutation -> points)
         hipLaunchKernelGGL(k_gather_cam_major, dim3((unsigned)ceil_div(no, 256)), dim3(256), 0, p->stream, no,
                            p->d_pt, p->d_obs, p->d_cm_pt, p->d_cm_obs);

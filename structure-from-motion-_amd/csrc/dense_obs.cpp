@@ -195,7 +195,8 @@ int dense_obs_pieces(void *handle, std::vector<int64_t> &off) {
     return (int)np;
 }
 
-// pieces [t0, t1) to their places in the concatenated arrays (off: dense_obs_pieces)
+// pieces [t0, t1) to their places in the concatenated arrays (off:
+// dense_obs_pieces); a null destination is skipped
 void dense_obs_copy_pieces(void *handle, const std::vector<int64_t> &off, int t0, int t1, int32_t *cam, int32_t *pt,
                            double *obs) {
     auto *h = static_cast<DenseObs *>(handle);
@@ -203,9 +204,9 @@ void dense_obs_copy_pieces(void *handle, const std::vector<int64_t> &off, int t0
         const int64_t t = t0 + k;
         const Piece &p = h->pieces[t];
         if (!p.n) return;
-        std::memcpy(cam + off[t], p.cam.data(), p.n * sizeof(int32_t));
-        std::memcpy(pt + off[t], p.pt.data(), p.n * sizeof(int32_t));
-        std::memcpy(obs + 2 * off[t], p.xy.data(), 2 * p.n * sizeof(double));
+        if (cam) std::memcpy(cam + off[t], p.cam.data(), p.n * sizeof(int32_t));
+        if (pt) std::memcpy(pt + off[t], p.pt.data(), p.n * sizeof(int32_t));
+        if (obs) std::memcpy(obs + 2 * off[t], p.xy.data(), 2 * p.n * sizeof(double));
     });
 }
 
