@@ -253,6 +253,30 @@ def test_ransac_edge_cases(core):
     b, counts, _, _ = O.ransac(y1, x2, samples, 0.5)
     b2, _, _, counts2 = core.ransac_f8(y1, x2, samples, 0.5, want_counts=True)
     assert np.array_equal(counts, counts2) and b == b2
+    # points that are not (N, 2) (Phase 1/GetInliersRANSAC.py:49-50, each
+    # iteration's EstimateFundamentalMatrix raising at :80-81 inside the
+    # loop's try): n_max draws consumed, (np.array([]), index, None) back;
+    # N mismatched between the two sets: np.hstack raises before any draw.
+    # The device call after them continues the same stream (tests/test_abi.py
+    # covers the shapes without a device)
+    random.seed(9)
+    inl, outl, F = GetInliersRANSAC(np.hstack([x1, np.ones((200, 1))]), x2, idx, 0.06, 40)
+    assert F is None and inl.shape == (0,) and np.array_equal(outl, idx)
+    st_dev = random.getstate()
+    random.seed(9)
+    for _ in range(40):
+        random.sample(range(200), 8)
+    assert random.getstate() == st_dev
+    with pytest.raises(ValueError):
+        GetInliersRANSAC(x1, x2[:150], idx, 0.06, 40)
+    assert random.getstate() == st_dev
+    Fd, fd = get_inliers_ransac(x1, x2, idx, threshold=0.06, n_max=64)
+    st_after = random.getstate()
+    random.setstate(st_dev)
+    samples = np.array([random.sample(range(200), 8) for _ in range(64)], dtype=np.int32)
+    assert random.getstate() == st_after
+    b, counts, Fo, mo = O.ransac(x1, x2, samples, 0.06)
+    assert b >= 0 and rel(Fd, Fo) < 1e-9 and np.array_equal(np.asarray(fd, dtype=np.int64), idx[mo])
 
 
 def test_ransac_full_size_properties(core):
