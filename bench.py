@@ -79,7 +79,7 @@ def design_bytes(name, n_obs, n_pts, n_pairs, nblocks, ns):
     return None
 
 
-PMC_ROUND = "round5"
+PMC_ROUND = "round6"
 
 # VALU issue (MI355X_MICROARCH.md): a SIMD issues a wave64 VALU instruction
 # over 2 cycles (32 lanes a cycle); an FP64 op takes the slot twice (78.6 TF
@@ -97,12 +97,17 @@ def ransac_valu_slots():
     out, src = {}, []
     base = os.path.join(REPO, "profiles", PMC_ROUND)
     try:
-        vals = [float(r["Counter_Value"])
-                for r in csv.DictReader(open(os.path.join(base, "ransac_oneshot_pmc", "pmc_counter_collection.csv")))
-                if "k_epi_score" in r["Kernel_Name"] and r["Counter_Name"] == "SQ_INSTS_VALU"]
-        if vals:  # no FP64 split in that pass: one slot each (a lower bound of the slots)
-            out["oneshot"] = float(np.mean(vals))
-            src.append(f"profiles/{PMC_ROUND}/ransac_oneshot_pmc (SQ_INSTS_VALU of k_epi_score, one slot each)")
+        per = {}
+        for r in csv.DictReader(open(os.path.join(base, "ransac_oneshot_pmc", "pmc_counter_collection.csv"))):
+            if "k_epi_score" in r["Kernel_Name"]:
+                per.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+        if per.get("SQ_INSTS_VALU"):  # FP64 ops take 2 slots, FP64 transcendentals 4 (the pass has the splits
+            # since round 6; round 5's had SQ_INSTS_VALU alone, one slot each)
+            m = {k: float(np.mean(v)) for k, v in per.items()}
+            out["oneshot"] = (m["SQ_INSTS_VALU"] + sum(m.get(f"SQ_INSTS_VALU_{c}_F64", 0.0) for c in ("ADD", "FMA", "MUL"))
+                              + 3 * m.get("SQ_INSTS_VALU_TRANS_F64", 0.0))
+            src.append(f"profiles/{PMC_ROUND}/ransac_oneshot_pmc (k_epi_score: SQ_INSTS_VALU + the FP64 splits, "
+                       f"tools/ransac_oneshot.py)")
     except (OSError, ValueError, KeyError):
         pass
     try:
