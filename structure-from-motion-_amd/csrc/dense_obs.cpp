@@ -200,7 +200,7 @@ int dense_obs_pieces(void *handle, std::vector<int64_t> &off) {
 void dense_obs_copy_pieces(void *handle, const std::vector<int64_t> &off, int t0, int t1, int32_t *cam, int32_t *pt,
                            double *obs) {
     auto *h = static_cast<DenseObs *>(handle);
-    par_for((int64_t)(t1 - t0), [&](int64_t k) {
+    par_for_dynamic((int64_t)(t1 - t0), [&](int64_t k) {
         const int64_t t = t0 + k;
         const Piece &p = h->pieces[t];
         if (!p.n) return;
@@ -229,9 +229,11 @@ extern "C" int sfm_dense_obs_scan(const void *flags, int32_t dtype, int64_t flag
     for (int64_t i = 0; i < n_rows; ++i)
         SFM_CHECK_ARG(rows[i] >= 0 && rows[i] < n_matrix_rows, "row index out of bounds of the flag matrix");
     SFM_CHECK_ARG(dtype >= 0 && dtype <= 4, "flag dtype: 0 f64, 1 f32, 2 i64, 3 i32, 4 u8/bool");
-    // jobs of >= 4096 rows; the pool runs them on up to 16 threads
-    int nj = n_threads > 0 ? n_threads : 64;
-    nj = (int)std::max<int64_t>(1, std::min<int64_t>(nj, (n_rows + 4095) / 4096));
+    // jobs of >= 1024 rows, dealt dynamically to up to 16 threads (round 6:
+    // 64 jobs of 4096+ rows in contiguous blocks per thread had the scan time
+    // set by the slowest thread -- 7 to 16 ms at cfg5 on a shared host)
+    int nj = n_threads > 0 ? n_threads : 256;
+    nj = (int)std::max<int64_t>(1, std::min<int64_t>(nj, (n_rows + 1023) / 1024));
     DenseObs *h = nullptr;
     {
         std::lock_guard<std::mutex> lk(g_pool_mu);
@@ -249,7 +251,7 @@ extern "C" int sfm_dense_obs_scan(const void *flags, int32_t dtype, int64_t flag
     const char *x = reinterpret_cast<const char *>(fx), *y = reinterpret_cast<const char *>(fy);
     const bool avx = have_avx512();
     const int rc = sfm::abi_guard("sfm_dense_obs_scan", [&] {
-        sfm::par_for(nj, [&](int64_t t) {
+        sfm::par_for_dynamic(nj, [&](int64_t t) {
             const int64_t r0 = n_rows * t / nj, r1 = n_rows * (t + 1) / nj;
             Piece &p = h->pieces[t];
             if (avx) scan_dispatch<true>(dtype, f, flag_row_bytes, rows, r0, r1, n_cams, x, y, xy_row_bytes, p);
@@ -295,11 +297,11 @@ extern "C" int sfm_dense_obs_free(void *handle) {
 extern "C" int sfm_gather_rows3(const double *src, int64_t src_rows, const int64_t *rows, int64_t n, double *dst) {
     SFM_CHECK_ARG(n == 0 || (src && dst), "null pointer");
     SFM_CHECK_ARG(n >= 0 && src_rows >= 0, "bad sizes");
-    constexpr int NJ = 16;
-    const int nj = n >= 65536 ? NJ : 1;  // small gathers: one thread
+    constexpr int NJ = 64;
+    const int nj = n >= 65536 ? NJ : 1;  // small gathers: one thread; large ones dealt dynamically
     int bad[NJ] = {0};
     const int rc = sfm::abi_guard("sfm_gather_rows3", [&] {
-        sfm::par_for(nj, [&](int64_t t) {
+        sfm::par_for_dynamic(nj, [&](int64_t t) {
             for (int64_t i = n * t / nj; i < n * (t + 1) / nj; ++i) {
                 const int64_t r = rows ? rows[i] : i;
                 if (r < 0 || r >= src_rows) {

@@ -2,6 +2,7 @@
 // the dense observation scan): parked on a condition variable between jobs.
 #pragma once
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
@@ -134,6 +135,25 @@ inline void par_for(int64_t n, F &&f) {
     for (auto &x : th) x.join();
     for (auto &e : ex)
         if (e) std::rethrow_exception(e);
+}
+
+// f(i) for i in [0, n), the items dealt dynamically: each thread takes the
+// next item from a shared counter.  For memory-bound passes over many items
+// (the dense scan's row blocks): on a shared host a thread whose core is busy
+// with another tenant's work takes fewer items instead of setting the time
+// of the whole pass, as a contiguous block per thread would.
+template <class F>
+inline void par_for_dynamic(int64_t n, F &&f) {
+    std::atomic<int64_t> next{0};
+    static const int nt0 = [] {
+        const char *s = std::getenv("SFM_PLAN_THREADS");
+        const int e = s ? std::atoi(s) : 0;
+        return e > 0 ? e : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    }();
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt0, n));
+    par_for(nt, [&](int64_t) {
+        for (int64_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n;) f(i);
+    });
 }
 
 // The C-ABI never lets a C++ exception out: a host allocation that fails
