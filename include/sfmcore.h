@@ -177,6 +177,15 @@ int sfm_dense_obs_free(void *handle);
  * dst[i] = src[rows[i]] for 3-double rows (rows NULL: src[i]), on the host
  * thread pool; SFM_ERR_ARG for a row outside [0, src_rows). */
 int sfm_gather_rows3(const double *src, int64_t src_rows, const int64_t *rows, int64_t n, double *dst);
+/* The camera parameter conversions around the solve (BundleAdjustment.py:
+ * 183-193 and 220-228), scipy's Rotation with its bits (csrc/rotations.cpp):
+ * sfm_matrix_to_rotvec = from_matrix(R).as_rotvec() for n row-major 3 x 3
+ * matrices, returning how many are not orthogonal to within 1e-13 (scipy
+ * orthogonalises those first: nothing is written for them, the caller
+ * converts the batch with scipy), -1 for a null pointer / negative n;
+ * sfm_rotvec_to_matrix = from_rotvec(w).as_matrix(). */
+int64_t sfm_matrix_to_rotvec(const double *R, int64_t n, double *w);
+int sfm_rotvec_to_matrix(const double *w, int64_t n, double *R);
 
 /* ---------------------------------------------------------------------
  * LinearTriangulation (LinearTriangulation.py:3-92)

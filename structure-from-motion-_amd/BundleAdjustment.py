@@ -16,7 +16,6 @@ least-squares solution (tests/test_gpu_parity.py).
 import time
 
 import numpy as np
-from scipy.spatial.transform import Rotation
 
 import _sfmcore as _core
 
@@ -210,7 +209,7 @@ def _adjust(all_world_coords, valid_point_indices, src, R_set, C_set, K, max_ite
     Rs = np.array([np.array(R) for R in R_set], dtype=np.float64).reshape(n_cameras, 3, 3)
     Cs = np.array([np.array(C) for C in C_set], dtype=np.float64).reshape(n_cameras, 3)
     cams0 = np.empty((n_cameras, 6))
-    cams0[:, :3] = Rotation.from_matrix(Rs).as_rotvec()
+    cams0[:, :3] = _core.matrix_to_rotvec(Rs)  # scipy's Rotation, its bits (csrc/rotations.cpp)
     cams0[:, 3:] = (-Rs @ Cs[:, :, None])[:, :, 0]
     t1 = time.perf_counter()
     last_timings["cams0"] = (t1 - t0) * 1e3  # :183-193, the stacked rotvec / t conversion
@@ -239,7 +238,7 @@ def _adjust(all_world_coords, valid_point_indices, src, R_set, C_set, K, max_ite
                             ba_lm_loop=rep["t_loop_ms"], ba_lm_download=rep["t_download_ms"],
                             iterations=rep["iterations"])
         # :220-228 for all cameras at once (bitwise the per-camera loop)
-        R_all = Rotation.from_rotvec(cams[:, :3]).as_matrix()
+        R_all = _core.rotvec_to_matrix(cams[:, :3])  # Rotation.from_rotvec(...).as_matrix(), its bits
         C_all = (-np.transpose(R_all, (0, 2, 1)) @ cams[:, 3:, None])[:, :, 0]
         R_set_opt = [R_all[i] for i in range(n_cameras)]
         C_set_opt = [C_all[i] for i in range(n_cameras)]

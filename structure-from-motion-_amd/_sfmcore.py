@@ -91,6 +91,8 @@ SIGNATURES = [
     ("sfm_dense_obs_read", _c, [ctypes.c_void_p, _i32, _i32, _d]),
     ("sfm_dense_obs_free", _c, [ctypes.c_void_p]),
     ("sfm_gather_rows3", _c, [_d, _i, _i64, _i, _d]),
+    ("sfm_matrix_to_rotvec", ctypes.c_int64, [_d, _i, _d]),
+    ("sfm_rotvec_to_matrix", _c, [_d, _i, _d]),
     ("sfm_triangulate_dlt", _c, [_d, _d, _d, _d, _i, _d, _c]),
     ("sfm_triangulate_nonlinear", _c, [_d, _d, _d, _d, _d, _i, ctypes.c_int32, _d, _i32, _c]),
     ("sfm_project_points", _c, [_d, _d, _i, _d, _c]),
@@ -605,6 +607,32 @@ def gather_points(all_world_coords, rows):
     if _lib.sfm_gather_rows3(a.ctypes.data_as(_d), a.shape[0], _p(rows, _i64), len(rows), _p(out)) != 0:
         return a[rows]  # an index out of range: numpy's IndexError
     return out
+
+
+def matrix_to_rotvec(Rs):
+    """Rotation.from_matrix(Rs).as_rotvec() for an (n, 3, 3) stack, with
+    scipy's bits (csrc/rotations.cpp); scipy itself when a matrix is not
+    orthogonal to within 1e-13 (scipy orthogonalises it first) or the input
+    is not a C-ordered float64 stack."""
+    R = np.asarray(Rs)
+    if R.dtype == np.float64 and R.ndim == 3 and R.shape[1:] == (3, 3) and R.flags.c_contiguous:
+        w = np.empty((len(R), 3))
+        if _lib.sfm_matrix_to_rotvec(R.ctypes.data_as(_d), len(R), _p(w)) == 0:
+            return w
+    from scipy.spatial.transform import Rotation
+    return Rotation.from_matrix(Rs).as_rotvec()
+
+
+def rotvec_to_matrix(w):
+    """Rotation.from_rotvec(w).as_matrix() for an (n, 3) array, with scipy's
+    bits (csrc/rotations.cpp)."""
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    if w.ndim != 2 or w.shape[1] != 3:
+        from scipy.spatial.transform import Rotation
+        return Rotation.from_rotvec(w).as_matrix()
+    R = np.empty((len(w), 3, 3))
+    _check(_lib.sfm_rotvec_to_matrix(_p(w), len(w), _p(R)))
+    return R
 
 
 def triangulate(P1, P2, x1, x2):

@@ -235,3 +235,36 @@ def test_sweep_planner_plan_only_is_deterministic(cfg, monkeypatch, capfd):
         assert len(m) == 1
         digests.append(m[0])
     assert digests[0] == digests[1]
+
+
+def test_rotation_conversions_are_scipys_bits():
+    """The BA drop-in's camera conversions (BundleAdjustment.py:183-193,
+    220-228) in the library (csrc/rotations.cpp) against scipy itself, bit
+    for bit: random, small-angle (series branch), tiny, near-pi and zero
+    rotations; a matrix scipy would orthogonalise (off by 1e-10) or a
+    reflection is left to scipy, so the batch still has scipy's result."""
+    import _sfmcore as core
+    from scipy.spatial.transform import Rotation
+    rng = np.random.default_rng(0)
+    unit = rng.normal(size=(500, 3))
+    unit /= np.linalg.norm(unit, axis=1, keepdims=True)
+    sets = [rng.normal(0, 1.0, (5000, 3)), rng.normal(0, 1e-4, (2000, 3)), rng.normal(0, 1e-9, (500, 3)),
+            (np.pi - 1e-7) * unit, 0.999e-3 * unit, 1.001e-3 * unit, np.zeros((3, 3))]
+    for w in sets:
+        R = Rotation.from_rotvec(w).as_matrix()
+        assert np.array_equal(core.rotvec_to_matrix(w), R)
+        assert np.array_equal(core.matrix_to_rotvec(R), Rotation.from_matrix(R).as_rotvec())
+        out = np.empty((len(R), 3))
+        assert core._lib.sfm_matrix_to_rotvec(np.ascontiguousarray(R).ctypes.data_as(core._d), len(R),
+                                              core._p(out)) == 0  # the native path took every matrix
+    R = Rotation.from_rotvec(rng.normal(0, 0.2, (50, 3))).as_matrix()
+    Rn = R + rng.normal(0, 1e-10, R.shape)  # scipy orthogonalises these
+    Rf = R.copy()
+    Rf[7] = -Rf[7]  # a reflection
+    for M in (Rn, Rf):
+        out = np.empty((len(M), 3))
+        assert core._lib.sfm_matrix_to_rotvec(np.ascontiguousarray(M).ctypes.data_as(core._d), len(M),
+                                              core._p(out)) > 0
+    assert np.array_equal(core.matrix_to_rotvec(Rn), Rotation.from_matrix(Rn).as_rotvec())
+    with pytest.raises(ValueError, match="determinant"):  # scipy's own error for a reflection
+        core.matrix_to_rotvec(Rf)
