@@ -12,7 +12,8 @@ R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if len(sys.argv) > 1 and sys.argv[1] == "--child":
     cfg, pkg = sys.argv[2], sys.argv[3]
     sys.path.insert(0, pkg)
-    import _sfmcore  # noqa: F401  (this build, before bench puts its own package first)
+    import _sfmcore  # noqa: F401  (this build and its drop-in, before bench puts its own package first)
+    import BundleAdjustment  # noqa: F401
     sys.path.insert(0, R)
     import bench
     print(json.dumps(bench.end_to_end_ba(cfg)), flush=True)
