@@ -21,9 +21,13 @@
 // that is already mapped (first-touch page faults of the ~100 MB of pieces
 // had cost more than the scan).
 #include <immintrin.h>
+#include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -59,6 +63,54 @@ std::mutex g_pool_mu;
 DenseObs *g_pool = nullptr;
 
 constexpr int ROW_BLOCK = 32;  // rows scanned before their coordinates are gathered
+
+// NUMA placement (round 6).  The flag and coordinate matrices were written
+// by the caller's thread, so their pages sit on one node of a two-socket
+// host; scan threads on the other socket read them across the socket link.
+// data_node: the node holding most of 16 pages sampled over [p, p + bytes)
+// (move_pages in query mode), -1 if unknown or split.
+int data_node(const void *p, size_t bytes) {
+    const long pg = sysconf(_SC_PAGESIZE);
+    if (pg <= 0 || bytes == 0) return -1;
+    constexpr int NS = 16;
+    void *pages[NS];
+    int status[NS];
+    for (int i = 0; i < NS; ++i)
+        pages[i] = reinterpret_cast<void *>((reinterpret_cast<uintptr_t>(p) + bytes / NS * i) & ~(uintptr_t)(pg - 1));
+    if (syscall(SYS_move_pages, 0, (unsigned long)NS, pages, nullptr, status, 0) != 0) return -1;
+    int cnt[64] = {0}, best = -1;
+    for (int s : status)
+        if (s >= 0 && s < 64 && ++cnt[s] > NS / 2) best = s;
+    return best;
+}
+// the CPUs of node n this process may run on (false: none or unreadable)
+bool node_cpus(int n, cpu_set_t *set) {
+    char path[96];
+    std::snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", n);
+    FILE *fp = std::fopen(path, "r");
+    if (!fp) return false;
+    char buf[4096];
+    const size_t len = std::fread(buf, 1, sizeof buf - 1, fp);
+    std::fclose(fp);
+    buf[len] = 0;
+    cpu_set_t allowed;
+    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return false;
+    CPU_ZERO(set);
+    for (char *q = buf; *q;) {
+        char *e;
+        const long a = std::strtol(q, &e, 10);
+        if (e == q) break;
+        long b = a;
+        if (*e == '-') b = std::strtol(e + 1, &e, 10);
+        for (long c = a; c <= b && c < CPU_SETSIZE; ++c)
+            if (CPU_ISSET(c, &allowed)) CPU_SET(c, set);
+        q = *e ? e + 1 : e;
+    }
+    return CPU_COUNT(set) > 0;
+}
+// the pool workers pinned to one node: each pins itself once per node (a
+// thread_local record); the caller's thread is never pinned
+thread_local int t_pinned = -1;
 
 inline bool have_avx512() {
     static const bool v = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
@@ -250,8 +302,17 @@ extern "C" int sfm_dense_obs_scan(const void *flags, int32_t dtype, int64_t flag
     const char *f = static_cast<const char *>(flags);
     const char *x = reinterpret_cast<const char *>(fx), *y = reinterpret_cast<const char *>(fy);
     const bool avx = have_avx512();
+    // SFM_SCAN_PIN=0: no pinning (the A/B of tools/e2e_ab.py)
+    static const bool pin_on = !std::getenv("SFM_SCAN_PIN") || std::atoi(std::getenv("SFM_SCAN_PIN")) != 0;
+    cpu_set_t node_set;
+    const int node = pin_on && n_rows ? data_node(f + rows[0] * flag_row_bytes, (size_t)flag_row_bytes * n_rows) : -1;
+    const bool pin = node >= 0 && node_cpus(node, &node_set);
+    const std::thread::id caller = std::this_thread::get_id();
     const int rc = sfm::abi_guard("sfm_dense_obs_scan", [&] {
         sfm::par_for_dynamic(nj, [&](int64_t t) {
+            if (pin && t_pinned != node && std::this_thread::get_id() != caller) {
+                t_pinned = sched_setaffinity(0, sizeof node_set, &node_set) == 0 ? node : -2;
+            }
             const int64_t r0 = n_rows * t / nj, r1 = n_rows * (t + 1) / nj;
             Piece &p = h->pieces[t];
             if (avx) scan_dispatch<true>(dtype, f, flag_row_bytes, rows, r0, r1, n_cams, x, y, xy_row_bytes, p);

@@ -2,6 +2,7 @@
 two builds of the library on one box, alternated over rounds, each run in a
 child process (one libsfmcore per process).  The build is the package
 directory whose _sfmcore / libsfmcore.so the child imports first.
+A build may carry environment settings: pkgdir:VAR=value[,VAR=value].
 Usage: e2e_ab.py cfg5 rounds pkgdir_a pkgdir_b"""
 import json
 import os
@@ -22,8 +23,10 @@ cfg, rounds, pkgs = sys.argv[1], int(sys.argv[2]), sys.argv[3:]
 res = {p: [] for p in pkgs}
 for r in range(rounds):
     for p in pkgs:
-        out = subprocess.run([sys.executable, "-u", __file__, "--child", cfg, p], capture_output=True, text=True,
-                             timeout=600, env=dict(os.environ, SFM_CREATE_TIMING="1"))
+        d, _, kv = p.partition(":")
+        env = dict(os.environ, SFM_CREATE_TIMING="1", **dict(a.split("=", 1) for a in kv.split(",") if a))
+        out = subprocess.run([sys.executable, "-u", __file__, "--child", cfg, d], capture_output=True, text=True,
+                             timeout=600, env=env)
         if out.returncode != 0:
             print(out.stderr[-2000:], flush=True)
             sys.exit(out.returncode)
