@@ -3442,6 +3442,32 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
             }
             P.rchunk.push_back((int32_t)cut.size());
         }
+        // a lower bound of the trial's overshoot from the cut alone (round 6):
+        // a spec's staged slots in its busiest chunk are at least its
+        // observations over the chunk count, and its pair list at least the
+        // 128-entry minimum.  When even that bound needs the largest shrink
+        // (0.5: overshoot >= 1.96), the exact statistics would give the same
+        // next size, so their pass (a device round trip) is skipped: cfg4's
+        // 65,535 and 32,767 trials (overshoot 5.4 and 2.8); the plan is the
+        // same (the digest tests)
+        if (ok && !cut.empty() && chunk_obs > 64) {
+            int64_t lb = 0;
+            for (auto &sp : specs) {
+                int64_t ow = 0;
+                for (auto &R : sp) ow += cnt[(size_t)R.c * nc + R.c];
+                lb = std::max<int64_t>(lb, ceil_div(ow, (int64_t)cut.size()));
+            }
+            const int bs0 = P.buf_slots, pc0 = P.pair_cap;
+            P.buf_slots = std::max(8, (int)((lb + 7) / 8 * 8));
+            P.pair_cap = 128;
+            const double over_lb = std::max((double)lb / SW_MAX_STAGED, (double)P.lds_bytes() / (160 * 1024));
+            P.buf_slots = bs0;
+            P.pair_cap = pc0;
+            if (0.98 / over_lb <= 0.5) {
+                chunk_obs = std::max(64, (int)(chunk_obs * 0.5));
+                continue;
+            }
+        }
         std::vector<int> cstaged(cut.size(), 0), cpmax(cut.size(), 0);
         if (ok && dev && !cut.empty()) {  // the same statistics from k_plan_chunkmax
             const size_t nk = cut.size();
