@@ -3126,21 +3126,27 @@ static int64_t sweep_alloc(const std::vector<std::vector<uint16_t>> &P, const st
     // instead of every chunk (cfg5: ~100 chunks, ~15 distinct counts; the
     // greedy was 2 of the 9 ms of the cfg5 create)
     auto pw = [](int t) { const double x = t; return x * x * x * x * x * x; };
-    std::vector<std::vector<std::pair<int, int>>> hist(ng);
+    // flat: group g's (count, multiplicity) pairs at hist[hoff[g], hoff[g + 1])
+    std::vector<std::pair<int, int>> hist;
+    std::vector<int> hoff(ng + 1, 0);
+    hist.reserve((size_t)ng * 16);
     {
         std::vector<int> c;  // a counting pass (a sort per group cost more than the greedy)
         for (int g = 0; g < ng; ++g) {
+            const uint16_t *pg = P[g].data();
             int top = 0;
-            for (int q = 0; q < nq; ++q) top = std::max(top, (int)P[g][q]);
+            for (int q = 0; q < nq; ++q) top = std::max(top, (int)pg[q]);
             c.assign(top + 1, 0);
-            for (int q = 0; q < nq; ++q) c[P[g][q]]++;
+            for (int q = 0; q < nq; ++q) c[pg[q]]++;
             for (int v = top; v > 1; --v)  // counts <= 1 never gain
-                if (c[v]) hist[g].push_back({v, c[v]});
+                if (c[v]) hist.push_back({v, c[v]});
+            hoff[g + 1] = (int)hist.size();
         }
     }
     auto gain = [&](int g, int s) {
         double d = 0;
-        for (const auto &hm : hist[g]) {
+        for (int k = hoff[g]; k < hoff[g + 1]; ++k) {
+            const auto &hm = hist[k];
             if (hm.first <= s) break;  // one trip at s and s + 1 from here down
             d += hm.second * (pw(sweep_trips(hm.first, s)) - pw(sweep_trips(hm.first, s + 1)));
         }
@@ -3599,7 +3605,7 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
     // lane layout in spec order
     std::vector<std::vector<int>> sl_of(P.nspec);
     std::vector<int64_t> fplan_w(P.nspec, 0), fideal_w(P.nspec, 0);
-    par_for(P.nspec, [&](int64_t w) {
+    par_for_dynamic(P.nspec, [&](int64_t w) {
         const auto &gd = sgd[w], &g = sg[w];
         const int Gd = sGd[w], budget = sbudget[w];
         std::vector<int> dtrip(P.nchunk, 0);
