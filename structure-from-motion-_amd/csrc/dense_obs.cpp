@@ -30,6 +30,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <new>
 #include <thread>
 #include <vector>
 
@@ -308,8 +309,13 @@ extern "C" int sfm_dense_obs_scan(const void *flags, int32_t dtype, int64_t flag
     const int node = pin_on && n_rows ? data_node(f + rows[0] * flag_row_bytes, (size_t)flag_row_bytes * n_rows) : -1;
     const bool pin = node >= 0 && node_cpus(node, &node_set);
     const std::thread::id caller = std::this_thread::get_id();
+    // SFM_TEST_SCAN_THROW=k (tests): job k throws std::bad_alloc, as a failed
+    // piece allocation would (the exception contract of csrc/host_pool.hpp)
+    const char *thr = std::getenv("SFM_TEST_SCAN_THROW");
+    const int64_t throw_job = thr ? std::atoll(thr) : -1;
     const int rc = sfm::abi_guard("sfm_dense_obs_scan", [&] {
         sfm::par_for_dynamic(nj, [&](int64_t t) {
+            if (t == throw_job) throw std::bad_alloc();
             if (pin && t_pinned != node && std::this_thread::get_id() != caller) {
                 t_pinned = sched_setaffinity(0, sizeof node_set, &node_set) == 0 ? node : -2;
             }

@@ -100,3 +100,24 @@ def test_gather_points_equals_numpy_fancy_index():
     assert np.array_equal(core.gather_points(np.asfortranarray(a), np.array([3, 9])), a[[3, 9]])
     with pytest.raises(IndexError):
         core.gather_points(a, np.array([len(a)], np.int64))
+
+
+@pytest.mark.parametrize("job", [0, 5, 97])
+def test_scan_exception_becomes_error_code(job, monkeypatch):
+    """A host allocation failure inside a scan job (the caller's thread or a
+    pool worker: jobs are dealt dynamically) comes back through the C-ABI as
+    SFM_ERR_NOMEM with its reason, after every worker has left the job; the
+    next scan runs normally (csrc/host_pool.hpp's exception contract)."""
+    import _sfmcore as core
+    rng = np.random.default_rng(4)
+    n, c = 98 * 1024, 24
+    flags = (rng.random((n, c)) < 0.3).astype(np.int64)
+    fx, fy = rng.random((n, c)), rng.random((n, c))
+    rows = np.arange(n, dtype=np.int64)
+    monkeypatch.setenv("SFM_TEST_SCAN_THROW", str(job))
+    with pytest.raises(core.SfmCoreError, match="host memory allocation failed"):
+        core.dense_observations(flags, fx, fy, rows, c)
+    monkeypatch.delenv("SFM_TEST_SCAN_THROW")
+    cam, pt, obs = core.dense_observations(flags, fx, fy, rows, c)
+    pi, ci = np.nonzero(flags == 1)
+    assert np.array_equal(cam, ci) and np.array_equal(pt, pi) and np.array_equal(obs[:, 0], fx[pi, ci])
