@@ -586,6 +586,7 @@ def ba_leg(workload, args, world, rank, local_rank, comm, barrier, allmax):
     ba = core.BAProblem(cams0, X0, ci, pi, ob, K, comm=comm, device=local_rank)
     ba.reset()
     conv = ba.solve(max_iterations=100)
+    conv_c, conv_x = ba.download() if world > 1 else (None, None)
     ba.reset()
     ba.solve(max_iterations=args.warmup, fixed_iterations=True)
     ba.reset()
@@ -602,8 +603,36 @@ def ba_leg(workload, args, world, rank, local_rank, comm, barrier, allmax):
     ktimes = ba.kernel_times()
     ba.set_timing(False)
     ba.close()
+    check = None
+    if world > 1:
+        # multi-GPU correctness on the driver's node (after the timed region):
+        # every rank must hold the same converged cost, and rank 0 re-solves
+        # the whole problem alone on its GPU -- the sharded solve must take
+        # the same LM path (iterations, accepted steps) to the same cost, its
+        # shard's points and the cameras as close as the multi-rank tests ask
+        spread = allmax(conv["cost"]) + allmax(-conv["cost"])
+        if rank == 0:
+            one = core.BAProblem(cams0, prob["X0"], prob["cam_idx"], prob["pt_idx"], prob["obs"], K,
+                                 device=local_rank)
+            srep = one.solve(max_iterations=100)
+            s_c, s_x = one.download()
+            one.close()
+            dx = float(np.abs(conv_x - s_x[lo:hi]).max()) if hi > lo else 0.0
+            dc = float(np.abs(conv_c - s_c).max())
+            check = {"ranks": world, "cost_spread_over_ranks": spread,
+                     "sharded": {"iterations": conv["iterations"], "accepted": conv["accepted"], "cost": conv["cost"]},
+                     "single_rank": {"iterations": srep["iterations"], "accepted": srep["accepted"],
+                                     "cost": srep["cost"]},
+                     "max_abs_diff_points_rank0_shard": dx, "max_abs_diff_cameras": dc,
+                     "ok": bool(spread == 0.0 and conv["iterations"] == srep["iterations"]
+                                and conv["accepted"] == srep["accepted"]
+                                and abs(conv["cost"] - srep["cost"]) <= 1e-9 * abs(srep["cost"])
+                                and dx < 1e-6 and dc < 1e-8),
+                     "tolerance": "same iterations and accepted steps, cost within 1e-9 relative, points 1e-6 and "
+                                  "cameras 1e-8 absolute (the in-process multi-rank tests' bounds)"}
+        barrier()
     return dict(workload=workload, prob=prob, cams0=cams0, dt=dt, rep=rep, conv=conv, ktimes=ktimes,
-                hi=hi, n_obs_local=len(ci), n_pts_local=len(X0))
+                hi=hi, n_obs_local=len(ci), n_pts_local=len(X0), check=check)
 
 
 def ba_record(leg, args, world):
@@ -662,6 +691,7 @@ def ba_record(leg, args, world):
                                          "loop_ms": round(conv["t_loop_ms"], 3),
                                          "ms_per_iteration": round(conv["t_loop_ms"] / max(1, conv["iterations"]), 4)}},
         "converged_LM_it_per_s": round(conv["iterations"] / (conv["t_loop_ms"] * 1e-3), 2) if conv["t_loop_ms"] else None,
+        **({"multi_rank_check": leg["check"]} if leg.get("check") else {}),
         "rmse": {f"{workload}_initial": round(syn.rmse_from_cost(conv["cost0"], n_obs_total), 6),
                  f"{workload}_gpu": round(syn.rmse_from_cost(conv["cost"], n_obs_total), 6),
                  "lm_iterations": conv["iterations"]},
@@ -758,6 +788,7 @@ def main():
         "pmc_bytes_per_iter": head["pmc_bytes_per_iter"],
         "step_mix": head["step_mix"],
         "converged_LM_it_per_s": head["converged_LM_it_per_s"],
+        **({"multi_rank_check": head["multi_rank_check"]} if "multi_rank_check" in head else {}),
         "rmse": head["rmse"],
         "ransac": ransac,
     }

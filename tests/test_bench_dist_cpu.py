@@ -44,6 +44,7 @@ class _FakeCore:
     def __init__(self, real):
         self.real = real
         self.iter_allreduces = 0
+        self.single_solves = 0
 
     def require_device(self):
         pass
@@ -69,12 +70,17 @@ class _FakeCore:
                 self.n_obs = len(cam_idx)
 
             def solve(self, max_iterations=100, fixed_iterations=False, **_):
-                for _ in range(max_iterations):  # one all-reduce of the reduced system per iteration
+                for _ in range(max_iterations if comm is not None else 0):  # one all-reduce per iteration
                     t = torch.full((self.payload,), float(self.n_obs), dtype=torch.float64)
                     dist.all_reduce(t)
                     core.iter_allreduces += 1
+                if comm is None:  # rank 0's single-rank re-solve (bench's multi_rank_check)
+                    core.single_solves += 1
                 return {"iterations": max_iterations, "accepted": min(5, max_iterations), "cost0": 2.0e5,
                         "cost": 1.0e5, "t_loop_ms": 0.5 * max_iterations, "status": 0}
+
+            def download(self):  # the points of this problem, unchanged (the stand-in does not move them)
+                return np.array(cams, dtype=np.float64), np.array(pts, dtype=np.float64)
 
             def reset(self):
                 pass
@@ -135,9 +141,9 @@ def _rank_main(rank, world, port, q):
     try:
         with contextlib.redirect_stdout(out):
             bench.main()
-        q.put((rank, out.getvalue(), fake.iter_allreduces, None))
+        q.put((rank, out.getvalue(), fake.iter_allreduces, None, fake.single_solves))
     except Exception as e:  # reported to the parent, which fails the test
-        q.put((rank, out.getvalue(), fake.iter_allreduces, repr(e)))
+        q.put((rank, out.getvalue(), fake.iter_allreduces, repr(e), fake.single_solves))
 
 
 def test_bench_two_rank_control_flow_gloo():
@@ -149,8 +155,8 @@ def test_bench_two_rank_control_flow_gloo():
         p.start()
     res = {}
     for _ in range(world):
-        rank, text, n_ar, err = q.get(timeout=600)
-        res[rank] = (text, n_ar, err)
+        rank, text, n_ar, err, n_single = q.get(timeout=600)
+        res[rank] = (text, n_ar, err, n_single)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -167,3 +173,7 @@ def test_bench_two_rank_control_flow_gloo():
     assert ra["hypotheses"] == HYPS and "of 2" in ra["sharding"] and ra["hyps_per_s_end_to_end"] > 0
     # the converged solve (100), warmup, timed and timing runs each all-reduced once per iteration, on both ranks
     assert res[0][1] == res[1][1] == 100 + WARMUP + 2 * STEPS
+    # the multi-rank check: rank 0 alone re-solves the whole problem once
+    mc = line["multi_rank_check"]
+    assert res[0][3] == 1 and res[1][3] == 0 and mc["ranks"] == world and mc["cost_spread_over_ranks"] == 0.0
+    assert mc["sharded"]["iterations"] == mc["single_rank"]["iterations"] and mc["ok"] is True
