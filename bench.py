@@ -530,6 +530,16 @@ def ransac_leg(args, world, rank, local_rank, comm):
             torch.distributed.all_reduce(t_t, op=torch.distributed.ReduceOp.MAX)
             t_e2e = float(t_t.item())
         out["sharding"] = f"hypotheses [{h0}, {h1}) on rank {rank} of {world}; packed-key max all-reduce (RCCL)"
+        if rank == 0:  # the sharded result against the unsharded call on this GPU (same stream state)
+            random.seed(0)
+            b1, F1, m1 = core.ransac_f8_pyrandom(x1, x2, H, 0.06, device=local_rank)[:3]
+            out["multi_rank_check"] = {
+                "best_iter": [int(best), int(b1)], "F_equal": bool(F is not None and F1 is not None
+                                                                     and np.array_equal(np.asarray(F), F1)),
+                "mask_equal": bool(np.array_equal(np.asarray(mask, dtype=bool), np.asarray(m1, dtype=bool))),
+                "ok": bool(int(best) == int(b1) and F is not None and F1 is not None
+                           and np.array_equal(np.asarray(F), F1)
+                           and np.array_equal(np.asarray(mask, dtype=bool), np.asarray(m1, dtype=bool)))}
     kt = []
     for _ in range(reps):
         core.ransac_f8(x1, x2, samples, 0.06, device=local_rank)

@@ -115,6 +115,12 @@ class _FakeCore:
         b, counts, F, _ = O.ransac(x1, x2, table[h0:h1], thr)
         return (sfm_dist.shard_key(counts[b], h0 + b) if b >= 0 else 0), F, None
 
+    def ransac_f8_pyrandom(self, x1, x2, H, thr, want_counts=False, want_samples=False, device=None):
+        import oracle as O
+        table = self.real.sample_table(len(x1), 8, H)  # the global stream, as the device call draws it
+        b, counts, F, m = O.ransac(x1, x2, table, thr)
+        return b, (F if b >= 0 else None), m, None, None
+
     def ransac_combine(self, comm, key, M):
         import sfm_dist
         return sfm_dist.combine_keys_torch(key, M)
@@ -171,6 +177,7 @@ def test_bench_two_rank_control_flow_gloo():
     assert "end_to_end" not in line and "shard_local" not in line and "cpu_baseline" not in line  # N = 1 only
     ra = line["ransac"]
     assert ra["hypotheses"] == HYPS and "of 2" in ra["sharding"] and ra["hyps_per_s_end_to_end"] > 0
+    assert ra["multi_rank_check"]["ok"] is True  # the sharded winner, F and mask are the unsharded call's
     # the converged solve (100), warmup, timed and timing runs each all-reduced once per iteration, on both ranks
     assert res[0][1] == res[1][1] == 100 + WARMUP + 2 * STEPS
     # the multi-rank check: rank 0 alone re-solves the whole problem once
