@@ -915,6 +915,37 @@ def test_ba_reused_device_blocks_poisoned(core, monkeypatch, capsys):
     assert capsys.readouterr().out.count("Bundle adjustment completed") == 2 * len(probs)
 
 
+def test_ba_concurrent_calls_equal_sequential(core):
+    """sfm_ba_lm from several host threads at once (ctypes drops the GIL):
+    the calls contend for the pinned upload stage, so some take the busy
+    path (the COO and x0 from pageable memory, no second stream) while one
+    holds the stage (indices first, coordinates and points on the stage's
+    second stream).  Every concurrent result is bitwise the sequential one."""
+    import threading
+    probs = [syn.ba_problem(12, 20000, 6, seed=s, dense=False) for s in (11, 12, 13, 14)]
+    args = [(np.column_stack([p["rotvec0"], np.einsum("nij,nj->ni", -p["R0"], p["C0"])]), p["X0"], p["cam_idx"],
+             p["pt_idx"], p["obs"], K) for p in probs]
+    seq = [core.ba_lm(*a, max_iterations=15) for a in args]
+    for _ in range(2):
+        out, errs = [None] * len(args), []
+
+        def run(i):
+            try:
+                out[i] = core.ba_lm(*args[i], max_iterations=15)
+            except Exception as e:  # reported below
+                errs.append(repr(e))
+
+        th = [threading.Thread(target=run, args=(i,)) for i in range(len(args))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        assert not errs, errs
+        for (c0, x0, r0), (c1, x1, r1) in zip(seq, out):
+            assert r1["iterations"] == r0["iterations"] and r1["cost"] == r0["cost"]
+            assert np.array_equal(c1, c0) and np.array_equal(x1, x0)
+
+
 def test_ba_failure_contract(core, capsys):
     from BundleAdjustment import perform_bundle_adjustment
     p = syn.ba_problem(3, 30, 2, seed=2)  # 2*60 residuals < 18 + 90 params? no: 120 >= 108
