@@ -1131,6 +1131,14 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
     // a scalar branch: the two roles run different barrier sequences, and a
     // barrier inside an exec-masked (divergent) region would still execute
     if (__builtin_amdgcn_readfirstlane(t >> 6) >= SW_THREADS / 64 - SW_STAGE_WAVES) {
+        // the next chunk's staging was the chunk hand-off's critical path
+        // (round 6 stamps at cfg5: the pair waves waited 1.01 us a chunk for
+        // it, the stagers 0.24 us for them): the staging waves issue first on
+        // the SIMDs they share with pair waves (waits 0.01 / 1.79 us; the
+        // sweep 0.296-0.301 -> 0.293-0.296 ms at cfg5, 0.0805 -> 0.0784 at
+        // cfg4).  Ranking the pair waves by their trips in the chunk the same
+        // way measured slower (cfg5 0.322-0.327 ms), not kept.
+        __builtin_amdgcn_s_setprio(2);
         // staging waves (no lane group): chunk q + 1's slots into the other
         // buffer while the groups work on chunk q; SW_STAGE_BATCH slots a
         // lane per round, their list entries, then their points' X and Lq,
@@ -1262,6 +1270,18 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
                 sweep_fetch(t, nload, (int64_t)(q + 1) * nspec + w, L, pairs, hdr, ldsw + (cur ^ 1) * bw);
         }
         const bool have = sw_wait(&cnt[cur], (((q - q0) >> 1) + 1) * nprod, &cnt[4], sw_err);
+        if (gi >= 0 && have) {
+                const uint32_t *pl = bufw + L.buf_slots * 2 * SLOT_D;
+                const int32_t *hd = reinterpret_cast<const int32_t *>(pl + L.pair_cap / 2);
+                const int c = diag ? (second ? hd[ng + 2] : hd[ng + 1]) : hd[gi + 1] - hd[gi];
+                my = c > slot ? (c - slot + nslot - 1) / nslot : 0;
+            }
+            for (int o = 32; o > 0; o >>= 1) my = max(my, __shfl_xor(my, o));
+            const int lvl = __builtin_amdgcn_readfirstlane(my >= 6 ? 2 : my >= 4 ? 1 : 0);
+            if (lvl == 2) __builtin_amdgcn_s_setprio(2);
+            else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         if (gi >= 0 && have) {
             const double2 *buf = reinterpret_cast<const double2 *>(bufw);
             const uint32_t *pl = bufw + L.buf_slots * 2 * SLOT_D;
