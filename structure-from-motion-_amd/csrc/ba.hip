@@ -1271,18 +1271,6 @@ __global__ void __launch_bounds__(SW_THREADS) k_schur_sweep(
         }
         const bool have = sw_wait(&cnt[cur], (((q - q0) >> 1) + 1) * nprod, &cnt[4], sw_err);
         if (gi >= 0 && have) {
-                const uint32_t *pl = bufw + L.buf_slots * 2 * SLOT_D;
-                const int32_t *hd = reinterpret_cast<const int32_t *>(pl + L.pair_cap / 2);
-                const int c = diag ? (second ? hd[ng + 2] : hd[ng + 1]) : hd[gi + 1] - hd[gi];
-                my = c > slot ? (c - slot + nslot - 1) / nslot : 0;
-            }
-            for (int o = 32; o > 0; o >>= 1) my = max(my, __shfl_xor(my, o));
-            const int lvl = __builtin_amdgcn_readfirstlane(my >= 6 ? 2 : my >= 4 ? 1 : 0);
-            if (lvl == 2) __builtin_amdgcn_s_setprio(2);
-            else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        }
-        if (gi >= 0 && have) {
             const double2 *buf = reinterpret_cast<const double2 *>(bufw);
             const uint32_t *pl = bufw + L.buf_slots * 2 * SLOT_D;
             const int32_t *hd = reinterpret_cast<const int32_t *>(pl + L.pair_cap / 2);
