@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <exception>
 #include <new>
+#include <sched.h>
 #include <stdexcept>
 #include <functional>
 #include <mutex>
@@ -103,15 +104,27 @@ class HostPool {
     int njob_ = 0, remaining_ = 0;
 };
 
+// threads for the host passes: SFM_PLAN_THREADS, else the CPUs this process
+// may run on (its affinity mask, not the machine's count: under taskset or a
+// cpuset more threads than CPUs would only time-slice), at most 16
+inline int host_threads() {
+    static const int n = [] {
+        const char *s = std::getenv("SFM_PLAN_THREADS");
+        const int e = s ? std::atoi(s) : 0;
+        if (e > 0) return e;
+        cpu_set_t cs;
+        const int c = sched_getaffinity(0, sizeof cs, &cs) == 0 ? CPU_COUNT(&cs)
+                                                               : (int)std::thread::hardware_concurrency();
+        return std::min(16, std::max(1, c));
+    }();
+    return n;
+}
+
 // the planner's independent loops (per chunk, per spec) on host threads:
 // f(i) for i in [0, n), contiguous blocks, up to 16 threads (SFM_PLAN_THREADS)
 template <class F>
 inline void par_for(int64_t n, F &&f) {
-    static const int nt0 = [] {
-        const char *s = std::getenv("SFM_PLAN_THREADS");
-        const int e = s ? std::atoi(s) : 0;
-        return e > 0 ? e : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-    }();
+    static const int nt0 = host_threads();
     const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt0, n));
     if (nt == 1) {
         for (int64_t i = 0; i < n; ++i) f(i);
@@ -145,11 +158,7 @@ inline void par_for(int64_t n, F &&f) {
 template <class F>
 inline void par_for_dynamic(int64_t n, F &&f) {
     std::atomic<int64_t> next{0};
-    static const int nt0 = [] {
-        const char *s = std::getenv("SFM_PLAN_THREADS");
-        const int e = s ? std::atoi(s) : 0;
-        return e > 0 ? e : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-    }();
+    static const int nt0 = host_threads();
     const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt0, n));
     par_for(nt, [&](int64_t) {
         for (int64_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n;) f(i);

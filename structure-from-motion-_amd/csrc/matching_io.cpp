@@ -25,6 +25,7 @@
 #include <thread>
 #include <vector>
 
+#include "host_pool.hpp"
 #include "sfm_common.hpp"
 
 namespace {
@@ -137,8 +138,7 @@ extern "C" int sfm_matching_parse(const char *data_path, int32_t no_of_images, i
     SFM_CHECK_ARG(no_of_images >= 1, "no_of_images must be >= 1");
     *handle = nullptr;
     auto st = new Store();
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const int nt = n_threads > 0 ? n_threads : (int)std::min(hw, 16u);
+    const int nt = n_threads > 0 ? n_threads : host_threads();
     for (int n = 1; n < no_of_images; ++n) {
         const std::string path = std::string(data_path) + "/matching" + std::to_string(n) + ".txt";
         FILE *f = std::fopen(path.c_str(), "rb");

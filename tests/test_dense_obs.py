@@ -121,3 +121,36 @@ def test_scan_exception_becomes_error_code(job, monkeypatch):
     cam, pt, obs = core.dense_observations(flags, fx, fy, rows, c)
     pi, ci = np.nonzero(flags == 1)
     assert np.array_equal(cam, ci) and np.array_equal(pt, pi) and np.array_equal(obs[:, 0], fx[pi, ci])
+
+
+def test_scan_on_one_allowed_cpu_is_serial_and_equal():
+    """the host passes size their threads from the process's
+    affinity mask (csrc/host_pool.hpp host_threads), not the machine's CPU
+    count.  A child pinned to one CPU runs the dense scan (256 jobs) on that
+    one thread and gets numpy's observations."""
+    import os
+    import subprocess
+    import sys
+    if not hasattr(os, "sched_setaffinity"):
+        pytest.skip("no affinity API")
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = (
+        "import os, sys, numpy as np\n"
+        "os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})\n"
+        f"sys.path.insert(0, {os.path.join(os.path.dirname(here), 'structure-from-motion-_amd')!r})\n"
+        "import _sfmcore as core\n"
+        "rng = np.random.default_rng(9)\n"
+        "n, c = 98 * 1024, 24\n"
+        "flags = (rng.random((n, c)) < 0.3).astype(np.int64)\n"
+        "fx, fy = rng.random((n, c)), rng.random((n, c))\n"
+        "before = len(os.listdir('/proc/self/task'))\n"
+        "cam, pt, obs = core.dense_observations(flags, fx, fy, np.arange(n, dtype=np.int64), c)\n"
+        "pi, ci = np.nonzero(flags == 1)\n"
+        "assert np.array_equal(cam, ci) and np.array_equal(pt, pi) and np.array_equal(obs[:, 1], fy[pi, ci])\n"
+        "tasks = len(os.listdir('/proc/self/task'))\n"
+        "assert tasks == before, (before, tasks)  # no pool workers were spawned for one CPU\n"
+    )
+    env = dict(os.environ)
+    env.pop("SFM_PLAN_THREADS", None)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
