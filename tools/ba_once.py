@@ -3,7 +3,7 @@ timed region) fixed LM iterations from x0, for rocprofv3 kernel-trace / PMC
 runs (tools/profile_round.sh; per-iteration traffic = totals / iterations)."""
 import os, sys
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, R + '/structure-from-motion-_amd')
+sys.path.insert(0, os.environ.get("SFM_PKG") or R + '/structure-from-motion-_amd')  # SFM_PKG: an A/B build's directory
 import numpy as np, _sfmcore as c, sfm_synthetic as syn
 p = syn.ba_problem_cfg(sys.argv[1] if len(sys.argv) > 1 else "cfg4", dense=False)
 n_it = int(sys.argv[2]) if len(sys.argv) > 2 else 20
