@@ -2767,28 +2767,38 @@ __global__ void __launch_bounds__(256) k_csr_cnt(int64_t no, int32_t nc, const i
 // land on those few addresses (cfg4: 5.5 M atomics on 1,275 counters, 1.0 ms;
 // cfg5 1.06 ms).  A bounded grid (CSR_CNT_WGS) keeps the flush small.
 constexpr int CSR_CNT_WGS = 128;
-__global__ void __launch_bounds__(256) k_csr_cnt_lds(int64_t no, int32_t nc, const int32_t *__restrict__ pstart,
+constexpr int CNT_THREADS = 1024;  // the counting kernels: 16 waves a CU hide their dependent loads (256: 4)
+__global__ void __launch_bounds__(CNT_THREADS) k_csr_cnt_lds(int64_t no, int32_t nc, const int32_t *__restrict__ pstart,
                                                      const int32_t *__restrict__ pt, const int32_t *__restrict__ cam,
                                                      uint32_t *__restrict__ cnt, uint32_t *__restrict__ dup) {
     extern __shared__ uint32_t csr_hist[];
     const int ntri = nc * (nc + 1) / 2;
-    for (int i = threadIdx.x; i < ntri; i += 256) csr_hist[i] = 0;
+    for (int i = threadIdx.x; i < ntri; i += CNT_THREADS) csr_hist[i] = 0;
     __syncthreads();
     bool twice = false;
-    for (int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x; a < no; a += (int64_t)gridDim.x * 256) {
+    for (int64_t a = (int64_t)blockIdx.x * CNT_THREADS + threadIdx.x; a < no; a += (int64_t)gridDim.x * CNT_THREADS) {
         const int ca = cam[a];
         const int32_t e = pstart[pt[a] + 1];
         atomicAdd(&csr_hist[dense_blk_d(nc, ca, ca)], 1u);
-        for (int32_t b = (int32_t)a + 1; b < e; ++b) {
-            const int cb = cam[b];
-            twice |= cb == ca;
-            atomicAdd(&csr_hist[ca < cb ? dense_blk_d(nc, ca, cb) : dense_blk_d(nc, cb, ca)], 1u);
+        // the point's later cameras four loads at a time (one wait per four,
+        // not one per camera: the loop is load-latency bound)
+        for (int32_t b0 = (int32_t)a + 1; b0 < e; b0 += 4) {
+            int cbv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) cbv[u] = b0 + u < e ? cam[b0 + u] : -1;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int cb = cbv[u];
+                if (cb < 0) continue;
+                twice |= cb == ca;
+                atomicAdd(&csr_hist[ca < cb ? dense_blk_d(nc, ca, cb) : dense_blk_d(nc, cb, ca)], 1u);
+            }
         }
     }
     if (twice) atomicOr(dup, 1u);
     __syncthreads();
     for (int r = 0; r < nc; ++r)
-        for (int c = r + (int)threadIdx.x; c < nc; c += 256) {
+        for (int c = r + (int)threadIdx.x; c < nc; c += CNT_THREADS) {
             const uint32_t v = csr_hist[dense_blk_d(nc, r, c)];
             if (v) atomicAdd(&cnt[(size_t)r * nc + c], v);
         }
@@ -2846,9 +2856,16 @@ __global__ void __launch_bounds__(256) k_plan_chunkmax(int32_t nc, int32_t nspec
     for (int32_t a = o0 + (int32_t)threadIdx.x; a < o1; a += blockDim.x) {
         const int ca = cam[a], pnt = pt[a];
         atomicAdd(&cc[ca], 1);
-        for (int32_t b = pstart[pnt]; b < pstart[pnt + 1]; ++b) {
-            const int cb = cam[b];
-            if (cb > ca) atomicAdd(&cp[spec_of[ca * nc + cb]], 1);
+        const int32_t e = pstart[pnt + 1];
+        for (int32_t b0 = pstart[pnt]; b0 < e; b0 += 8) {  // eight loads, then one wait (k_plan_counts_lds)
+            int cbv[8], spv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) cbv[u] = b0 + u < e ? cam[b0 + u] : -1;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) spv[u] = cbv[u] > ca ? spec_of[ca * nc + cbv[u]] : -1;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (spv[u] >= 0) atomicAdd(&cp[spv[u]], 1);
         }
     }
     __syncthreads();
@@ -2881,9 +2898,16 @@ __global__ void __launch_bounds__(256) k_plan_chunkcnt(int32_t nc, int32_t nspec
     for (int32_t a = a0 + (int32_t)threadIdx.x; a < a1; a += blockDim.x) {
         const int ca = cam[a], pnt = pt[a];
         atomicAdd(&cc[ca], 1);
-        for (int32_t b = pstart[pnt]; b < pstart[pnt + 1]; ++b) {
-            const int cb = cam[b];
-            if (cb > ca) atomicAdd(&cp[spec_of[ca * nc + cb]], 1);
+        const int32_t e = pstart[pnt + 1];
+        for (int32_t b0 = pstart[pnt]; b0 < e; b0 += 8) {  // eight loads, then one wait (k_plan_counts_lds)
+            int cbv[8], spv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) cbv[u] = b0 + u < e ? cam[b0 + u] : -1;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) spv[u] = cbv[u] > ca ? spec_of[ca * nc + cbv[u]] : -1;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (spv[u] >= 0) atomicAdd(&cp[spv[u]], 1);
         }
     }
     __syncthreads();
@@ -2929,29 +2953,34 @@ __global__ void __launch_bounds__(256) k_plan_counts(int64_t no, int32_t nc, int
 // into bq / cq once per nonzero counter and workgroup.  The global form's
 // atomics of a chunk land on its nbd block counters (cfg4: 1,275 of them,
 // 0.35 ms; cfg5 0.80 ms).
-__global__ void __launch_bounds__(256) k_plan_counts_lds(int32_t nc, int32_t nchunk, const int32_t *__restrict__ pstart,
+__global__ void __launch_bounds__(CNT_THREADS) k_plan_counts_lds(int32_t nc, int32_t nchunk, const int32_t *__restrict__ pstart,
                                                          const int32_t *__restrict__ pt, const int32_t *__restrict__ cam,
                                                          const int32_t *__restrict__ cut, uint32_t *__restrict__ bq,
                                                          uint32_t *__restrict__ cq) {
     extern __shared__ uint32_t pc_hist[];
     const int nbd = nc * (nc + 1) / 2;
     uint32_t *hb = pc_hist, *hc = pc_hist + nbd;
-    for (int i = threadIdx.x; i < nbd + nc; i += 256) pc_hist[i] = 0;
+    for (int i = threadIdx.x; i < nbd + nc; i += CNT_THREADS) pc_hist[i] = 0;
     __syncthreads();
     const int q = blockIdx.x;
     const int32_t o0 = pstart[cut[q]], o1 = pstart[cut[q + 1]], len = o1 - o0;
     const int32_t a0 = o0 + (int32_t)((int64_t)len * blockIdx.y / gridDim.y);
     const int32_t a1 = o0 + (int32_t)((int64_t)len * (blockIdx.y + 1) / gridDim.y);
-    for (int32_t a = a0 + (int32_t)threadIdx.x; a < a1; a += 256) {
+    for (int32_t a = a0 + (int32_t)threadIdx.x; a < a1; a += CNT_THREADS) {
         const int32_t pnt = pt[a], ca = cam[a];
         atomicAdd(&hc[ca], 1u);
-        for (int32_t b = pstart[pnt]; b < pstart[pnt + 1]; ++b) {
-            const int cb = cam[b];
-            if (cb > ca) atomicAdd(&hb[dense_blk_d(nc, ca, cb)], 1u);
+        const int32_t e = pstart[pnt + 1];
+        for (int32_t b0 = pstart[pnt]; b0 < e; b0 += 8) {  // eight loads, then one wait
+            int cbv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) cbv[u] = b0 + u < e ? cam[b0 + u] : -1;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (cbv[u] > ca) atomicAdd(&hb[dense_blk_d(nc, ca, cbv[u])], 1u);
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < nbd + nc; i += 256) {
+    for (int i = threadIdx.x; i < nbd + nc; i += CNT_THREADS) {
         const uint32_t v = pc_hist[i];
         if (v) atomicAdd(i < nbd ? &bq[(size_t)i * nchunk + q] : &cq[(size_t)(i - nbd) * nchunk + q], v);
     }
@@ -3015,10 +3044,17 @@ __global__ void __launch_bounds__(PLAN_THREADS) k_plan_lists(
         const int32_t pnt = cm_pt[lo[rr] + (rr ? s - n0 : s)];
         uint32_t *m = mask + (size_t)s * mw;
         for (int k = 0; k < mw; ++k) m[k] = 0u;
-        for (int32_t b = pstart[pnt]; b < pstart[pnt + 1]; ++b) {
-            const int cj = cam[b];
-            if (cj <= c || cj < j0 || cj >= j1) continue;
-            m[(cj - j0) >> 5] |= 1u << ((cj - j0) & 31);
+        const int32_t e = pstart[pnt + 1];
+        for (int32_t b0 = pstart[pnt]; b0 < e; b0 += 8) {  // eight loads, then one wait
+            int cjv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) cjv[u] = b0 + u < e ? cam[b0 + u] : -1;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int cj = cjv[u];
+                if (cj <= c || cj < j0 || cj >= j1) continue;
+                m[(cj - j0) >> 5] |= 1u << ((cj - j0) & 31);
+            }
         }
     }
     // the group offsets: one wave, 64 groups a step (inclusive scan by shuffles)
@@ -3576,7 +3612,7 @@ static void plan_sweep(int nc, int64_t np_, int64_t no, const int32_t *cam, cons
             const double pairs = (double)std::accumulate(cnt.begin(), cnt.end(), int64_t(0)) - (double)no;
             const int split = std::max(1, std::min(16, (int)(pairs / P.nchunk / (4.0 * (P.nbd + nc)))));
             if (hist <= (big_lds ? 160 * 1024 : 64 * 1024) && !env_int("SFM_PLAN_COUNTS_GLOBAL", 0))
-                hipLaunchKernelGGL(k_plan_counts_lds, dim3((unsigned)P.nchunk, (unsigned)split), dim3(256), hist,
+                hipLaunchKernelGGL(k_plan_counts_lds, dim3((unsigned)P.nchunk, (unsigned)split), dim3(CNT_THREADS), hist,
                                    dev->s, nc, P.nchunk, dev->pstart, dev->pt, dev->cam, dev->d_cut, b32, b32 + nb);
             else
                 hipLaunchKernelGGL(k_plan_counts, dim3((unsigned)ceil_div(no, 256)), dim3(256), 0, dev->s, no, nc,
@@ -4322,8 +4358,8 @@ static int ba_create(int32_t nc, int64_t np_, int64_t no, const int32_t *cam, co
                 hipFuncSetAttribute(reinterpret_cast<const void *>(&k_csr_cnt_lds),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
             if (hist <= (big_lds ? 160 * 1024 : 64 * 1024) && !env_int("SFM_CSR_CNT_GLOBAL", 0))
-                hipLaunchKernelGGL(k_csr_cnt_lds, dim3((unsigned)std::min<int64_t>(CSR_CNT_WGS, ceil_div(no, 256))),
-                                   dim3(256), hist, s, no, nc, p->d_pstart, p->d_pt, p->d_cam, cnt32,
+                hipLaunchKernelGGL(k_csr_cnt_lds, dim3((unsigned)std::min<int64_t>(CSR_CNT_WGS, ceil_div(no, CNT_THREADS))),
+                                   dim3(CNT_THREADS), hist, s, no, nc, p->d_pstart, p->d_pt, p->d_cam, cnt32,
                                    cnt32 + (size_t)nc * nc);
             else
                 hipLaunchKernelGGL(k_csr_cnt, dim3((unsigned)ceil_div(no, 256)), dim3(256), 0, s, no, nc,

@@ -4,7 +4,7 @@ loads; the later ones are what a drop-in call in a running pipeline pays).
 Usage: create_once.py [cfg4|cfg5] [host]  (host: SFM_PLAN_HOST=1)"""
 import os, sys, time
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, R + "/structure-from-motion-_amd")
+sys.path.insert(0, os.environ.get("SFM_PKG") or R + "/structure-from-motion-_amd")  # SFM_PKG: an A/B build's directory
 os.environ["SFM_CREATE_TIMING"] = "1"
 if len(sys.argv) > 2 and sys.argv[2] == "host":
     os.environ["SFM_PLAN_HOST"] = "1"
